@@ -1,0 +1,123 @@
+/*
+ * orbmi — MI355X-native ORB front-end + local BA for ORB-SLAM2 (C ABI).
+ *
+ * Drop-in boundary for the hot path of AHzZ123/orb_slam2_with_comment.
+ * Plain pointers and sizes only; every entry point cites the reference interface it replaces.
+ * Host buffers are owned by the caller (capacity based); each handle owns its device
+ * buffers, one HIP stream and the device-resident pyramid of its last extraction.
+ * Distinct handles may be used concurrently from different host threads (the reference runs
+ * the left and right ORBextractor on two std::threads, src/Frame.cc:78-81); one handle is not
+ * re-entrant.  All functions return ORBMI_OK (0) or a negative orbmi_status.
+ */
+#ifndef ORBMI_H
+#define ORBMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum orbmi_status {
+    ORBMI_OK = 0,
+    ORBMI_E_ARG = -1,         /* bad argument (null pointer, bad size)            */
+    ORBMI_E_HIP = -2,         /* HIP runtime / kernel launch failure              */
+    ORBMI_E_CAP = -3,         /* caller capacity too small; *n_out = needed count */
+    ORBMI_E_UNSUPPORTED = -4, /* geometry outside what the kernels are sized for  */
+    ORBMI_E_STATE = -5        /* call order violated (e.g. stereo before extract) */
+} orbmi_status;
+
+/* Field order of cv::KeyPoint (pt.x, pt.y, size, angle, response, octave, class_id). */
+typedef struct orbmi_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbmi_keypoint;
+
+typedef struct orbmi_extractor orbmi_extractor;
+
+/* ---- ORBextractor ------------------------------------------------------------------ */
+
+/* ORBextractor::ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ * int minThFAST)  include/ORBextractor.h:58-59, src/ORBextractor.cc:410-470.
+ * `device` is the HIP device ordinal the handle's buffers and stream live on. */
+int orbmi_extractor_create(int device, int nfeatures, float scale_factor, int nlevels,
+                           int ini_th_fast, int min_th_fast, orbmi_extractor** out);
+void orbmi_extractor_destroy(orbmi_extractor* h);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors)
+ * include/ORBextractor.h:64-66, src/ORBextractor.cc:1043-1105.  `image` is host u8 gray,
+ * rows x cols with row pitch `step` bytes.  Writes n keypoints (level-major, coordinates at
+ * level 0) and n x 32 descriptor bytes.  rows == 0 or cols == 0 -> *n_out = 0 (reference
+ * returns on an empty image).  capacity < n -> ORBMI_E_CAP with *n_out = n. */
+int orbmi_extract(orbmi_extractor* h, const uint8_t* image, int rows, int cols, size_t step,
+                  orbmi_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
+
+/* Batched, device-resident form (config 5 / throughput mode).  Image b is at
+ * d_images + b*image_stride (device memory).  Outputs stay on the device: keypoint i of
+ * image b at d_kps[b*capacity + i], its descriptor at d_desc + (b*capacity + i)*32, count at
+ * d_counts[b] (counts above `capacity` mean truncated output).  Asynchronous: enqueued on
+ * the handle's stream; call orbmi_extractor_synchronize() before reading. */
+int orbmi_extract_batch_device(orbmi_extractor* h, const uint8_t* d_images, int batch, int rows,
+                               int cols, size_t step, size_t image_stride, orbmi_keypoint* d_kps,
+                               uint8_t* d_desc, int* d_counts, int capacity);
+int orbmi_extractor_synchronize(orbmi_extractor* h);
+
+/* Getters  include/ORBextractor.h:68-90. `out` holds nlevels floats. */
+int orbmi_extractor_get_levels(const orbmi_extractor* h);
+float orbmi_extractor_get_scale_factor(const orbmi_extractor* h);
+int orbmi_extractor_get_scale_factors(const orbmi_extractor* h, float* out);
+int orbmi_extractor_get_inverse_scale_factors(const orbmi_extractor* h, float* out);
+int orbmi_extractor_get_scale_sigma_squares(const orbmi_extractor* h, float* out);
+int orbmi_extractor_get_inverse_scale_sigma_squares(const orbmi_extractor* h, float* out);
+int orbmi_extractor_get_features_per_level(const orbmi_extractor* h, int* out);
+
+/* ORBextractor::mvImagePyramid[level] (public, read by Frame::ComputeStereoMatches,
+ * src/Frame.cc:508,598,610) of batch item `item` of the last extraction.  padded = 0 copies
+ * the W_l x H_l interior, padded = 1 the (W_l+38) x (H_l+38) buffer with its 19-px
+ * reflect-101 border.  out_step = destination row pitch; *w, *h receive the copied size. */
+int orbmi_extractor_get_pyramid_level(orbmi_extractor* h, int item, int level, int padded,
+                                      uint8_t* out, size_t out_step, int* w, int* hgt);
+
+/* ---- Frame::ComputeStereoMatches ----------------------------------------------------- */
+
+/* Frame::ComputeStereoMatches()  src/Frame.cc:501-675 on the device-resident keypoints,
+ * descriptors and pyramids of the last extraction of (left, item_left) and
+ * (right, item_right); both handles must be on the same device.  bf = Camera.bf, fx =
+ * Camera.fx (mb = bf/fx).  Writes mvuRight / mvDepth (-1 = no match) for
+ * the n_left left keypoints, in left keypoint order. */
+int orbmi_compute_stereo_matches(orbmi_extractor* left, int item_left, orbmi_extractor* right,
+                                 int item_right, float bf, float fx, float* u_right,
+                                 float* depth, int n_left);
+
+/* Device-resident form: d_u_right / d_depth hold capacity floats per item of the last
+ * batch (item-major, same layout as orbmi_extract_batch_device outputs).  Stereo pairs are
+ * (left item 2p, right item 2p+1) of ONE handle for p < batch/2.  Asynchronous. */
+int orbmi_compute_stereo_matches_batch_device(orbmi_extractor* h, float bf, float fx,
+                                              float* d_u_right, float* d_depth);
+
+/* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
+
+/* Kernel stages of one handle; each is a single kernel launch (resize: one per level). */
+typedef enum orbmi_stage {
+    ORBMI_STAGE_PYR_LEVEL0 = 0,
+    ORBMI_STAGE_PYR_RESIZE = 1,
+    ORBMI_STAGE_FAST = 2,
+    ORBMI_STAGE_OCTREE = 3,
+    ORBMI_STAGE_DESCRIBE = 4,
+    ORBMI_STAGE_STEREO_ROWS = 5,
+    ORBMI_STAGE_STEREO_MATCH = 6,
+    ORBMI_STAGE_STEREO_FILTER = 7,
+    ORBMI_NUM_STAGES = 16
+} orbmi_stage;
+
+/* Bracket every launch of the stages in `stage_mask` (bit s = stage s) with HIP events. */
+int orbmi_set_profiling(orbmi_extractor* h, unsigned stage_mask);
+/* Synchronise, then add the elapsed device time (ms) and launch count of every bracketed
+ * launch since the last call into ms[s], launches[s] (ORBMI_NUM_STAGES entries each). */
+int orbmi_read_profile(orbmi_extractor* h, double* ms, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBMI_H */

@@ -1,0 +1,171 @@
+"""ORACLE loader — test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  It loads oracle/build/liborb_oracle.so (built by oracle/Makefile) and exposes numpy
+friendly wrappers of the C restatement of the reference's hot path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+
+
+class Keypoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float),
+                ("angle", C.c_float), ("response", C.c_float),
+                ("octave", C.c_int), ("class_id", C.c_int)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+def build(force: bool = False) -> str:
+    """make is incremental; a prebuilt .so is used as is when make is unavailable."""
+    try:
+        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []), check=True)
+    except (OSError, subprocess.CalledProcessError):
+        if not os.path.exists(LIB_PATH):
+            raise
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = C.CDLL(LIB_PATH)
+    return _lib
+
+
+def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> Params:
+    return Params(nfeatures, scale_factor, nlevels, ini_th, min_th)
+
+
+def _u8p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def tables(p: Params):
+    L = p.nlevels
+    out = [np.zeros(L, np.float32) for _ in range(4)] + [np.zeros(L, np.int32), np.zeros(16, np.int32)]
+    lib().orc_tables(C.byref(p), *[o.ctypes.data_as(C.c_void_p) for o in out])
+    keys = ("scale", "inv_scale", "sigma2", "inv_sigma2", "features_per_level", "umax")
+    return dict(zip(keys, out))
+
+
+def level_sizes(p: Params, rows: int, cols: int):
+    W = np.zeros(p.nlevels, np.int32)
+    H = np.zeros(p.nlevels, np.int32)
+    lib().orc_level_sizes(C.byref(p), rows, cols, W.ctypes.data_as(C.c_void_p), H.ctypes.data_as(C.c_void_p))
+    return W, H
+
+
+def pyramid(p: Params, img: np.ndarray):
+    """List of padded levels ((H+38) x (W+38) u8 arrays)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    W, H = level_sizes(p, *img.shape)
+    total = int(((W + 38) * (H + 38)).sum())
+    buf = np.zeros(total, np.uint8)
+    f = lib().orc_pyramid
+    f.restype = C.c_long
+    n = f(C.byref(p), _u8p(img), img.shape[0], img.shape[1], img.strides[0], _u8p(buf), C.c_long(total))
+    assert n == total, n
+    out, off = [], 0
+    for w, h in zip(W, H):
+        sz = int((w + 38) * (h + 38))
+        out.append(buf[off:off + sz].reshape(h + 38, w + 38))
+        off += sz
+    return out
+
+
+def fast_level(p: Params, img: np.ndarray, level: int, cap: int = 1 << 20):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    xyr = np.zeros((cap, 3), np.int32)
+    n = C.c_int()
+    rc = lib().orc_fast_level(C.byref(p), _u8p(img), img.shape[0], img.shape[1], img.strides[0],
+                              level, xyr.ctypes.data_as(C.c_void_p), cap, C.byref(n))
+    assert rc == 0, rc
+    return xyr[:n.value].copy()
+
+
+def octree_level(p: Params, img: np.ndarray, level: int, cap: int = 1 << 16):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    xyr = np.zeros((cap, 3), np.int32)
+    n = C.c_int()
+    rc = lib().orc_octree_level(C.byref(p), _u8p(img), img.shape[0], img.shape[1], img.strides[0],
+                                level, xyr.ctypes.data_as(C.c_void_p), cap, C.byref(n))
+    assert rc == 0, rc
+    return xyr[:n.value].copy()
+
+
+def blur_level(p: Params, img: np.ndarray, level: int):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    W, H = level_sizes(p, *img.shape)
+    out = np.zeros((H[level], W[level]), np.uint8)
+    lib().orc_blur_level(C.byref(p), _u8p(img), img.shape[0], img.shape[1], img.strides[0], level, _u8p(out))
+    return out
+
+
+def extract(p: Params, img: np.ndarray, cap: int | None = None):
+    """ORBextractor::operator() -> (keypoints structured array, descriptors n x 32 u8)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    cap = cap or (p.nfeatures + 64 * p.nlevels)
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int()
+    rc = lib().orc_extract(C.byref(p), _u8p(img), img.shape[0], img.shape[1], img.strides[0],
+                           kps.ctypes.data_as(C.c_void_p), _u8p(desc), cap, C.byref(n))
+    if rc == -3:
+        return extract(p, img, n.value)
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    f = lib().orc_fast_atan2
+    f.restype = C.c_float
+    f.argtypes = [C.c_float, C.c_float]
+    return f(y, x)
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_descriptor_distance(_u8p(a), _u8p(b))
+
+
+def stereo(p: Params, imL: np.ndarray, imR: np.ndarray, bf: float, fx: float,
+           kpsL: np.ndarray, descL: np.ndarray, kpsR: np.ndarray, descR: np.ndarray):
+    """Frame::ComputeStereoMatches restatement -> (uRight, depth) float32 arrays."""
+    imL = np.ascontiguousarray(imL, np.uint8)
+    imR = np.ascontiguousarray(imR, np.uint8)
+    kpsL = np.ascontiguousarray(kpsL, KP_DTYPE)
+    kpsR = np.ascontiguousarray(kpsR, KP_DTYPE)
+    descL = np.ascontiguousarray(descL, np.uint8).reshape(-1, 32)
+    descR = np.ascontiguousarray(descR, np.uint8).reshape(-1, 32)
+    N, Nr = len(kpsL), len(kpsR)
+    u = np.zeros(max(N, 1), np.float32)
+    d = np.zeros(max(N, 1), np.float32)
+    f = lib().orc_stereo
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                  C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    rc = f(C.byref(p), imL.ctypes.data, imR.ctypes.data, imL.shape[0], imL.shape[1], imL.strides[0], bf, fx,
+           kpsL.ctypes.data, descL.ctypes.data, N, kpsR.ctypes.data, descR.ctypes.data, Nr,
+           u.ctypes.data, d.ctypes.data)
+    assert rc == 0, rc
+    return u[:N], d[:N]

@@ -1,0 +1,110 @@
+"""ctypes binding of include/orbmi.h (liborbmi.so, built in-tree by build.py).
+
+There is no fallback: if the HIP library is missing or fails to load, importing the
+product classes raises.  Only the C-ABI is used; no torch types cross the boundary.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .build import LIB
+
+ORBMI_OK = 0
+ORBMI_E_ARG = -1
+ORBMI_E_HIP = -2
+ORBMI_E_CAP = -3
+ORBMI_E_UNSUPPORTED = -4
+ORBMI_E_STATE = -5
+STAGES = ["pyr_level0", "pyr_resize", "fast", "octree", "describe", "stereo_rows", "stereo_match",
+          "stereo_filter"]
+NUM_STAGES = 16
+_NAMES = {ORBMI_E_ARG: "ORBMI_E_ARG", ORBMI_E_HIP: "ORBMI_E_HIP", ORBMI_E_CAP: "ORBMI_E_CAP",
+          ORBMI_E_UNSUPPORTED: "ORBMI_E_UNSUPPORTED", ORBMI_E_STATE: "ORBMI_E_STATE"}
+
+
+class OrbmiError(RuntimeError):
+    def __init__(self, func: str, code: int):
+        super().__init__(f"{func} returned {_NAMES.get(code, code)}")
+        self.code = code
+
+
+class Keypoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == C.sizeof(Keypoint) == 28
+
+_vp, _i, _f, _sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+_PROTOS = {
+    "orbmi_extractor_create": (_i, [_i, _i, _f, _i, _i, _i, C.POINTER(_vp)]),
+    "orbmi_extractor_destroy": (None, [_vp]),
+    "orbmi_extract": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _i, C.POINTER(_i)]),
+    "orbmi_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp, _vp, _vp, _i]),
+    "orbmi_extractor_synchronize": (_i, [_vp]),
+    "orbmi_extractor_get_levels": (_i, [_vp]),
+    "orbmi_extractor_get_scale_factor": (_f, [_vp]),
+    "orbmi_extractor_get_scale_factors": (_i, [_vp, _vp]),
+    "orbmi_extractor_get_inverse_scale_factors": (_i, [_vp, _vp]),
+    "orbmi_extractor_get_scale_sigma_squares": (_i, [_vp, _vp]),
+    "orbmi_extractor_get_inverse_scale_sigma_squares": (_i, [_vp, _vp]),
+    "orbmi_extractor_get_features_per_level": (_i, [_vp, _vp]),
+    "orbmi_extractor_get_pyramid_level": (_i, [_vp, _i, _i, _i, _vp, _sz, C.POINTER(_i), C.POINTER(_i)]),
+    "orbmi_compute_stereo_matches": (_i, [_vp, _i, _vp, _i, _f, _f, _vp, _vp, _i]),
+    "orbmi_compute_stereo_matches_batch_device": (_i, [_vp, _f, _f, _vp, _vp]),
+    "orbmi_set_profiling": (_i, [_vp, C.c_uint]),
+    "orbmi_read_profile": (_i, [_vp, _vp, _vp]),
+    "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
+    "orbmi_debug_octree_level": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load liborbmi.so (raises if it is absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise ImportError(f"{LIB} not built: run `python -m orb_slam2_with_comment_amd.build`")
+        # torch bundles its own libamdhip64.so.7; loading it first lets liborbmi.so bind to that
+        # same runtime (same SONAME) so torch tensors/streams/RCCL and our kernels share one HIP
+        # runtime in the process.  Without torch, liborbmi.so uses /opt/rocm's runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(func: str, rc: int) -> None:
+    if rc != ORBMI_OK:
+        raise OrbmiError(func, rc)
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def declared_symbols(header: str | None = None):
+    """Function names declared in include/orbmi*.h (used by the symbol-export test)."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = []
+    for h in ([header] if header else sorted(glob.glob(os.path.join(root, "include", "orbmi*.h")))):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names += re.findall(r"^\s*(?:int|void|float|double|const char\s*\*)\s+(orbmi_\w+)\s*\(", text, flags=re.M)
+    return names

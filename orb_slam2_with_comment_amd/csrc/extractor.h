@@ -1,0 +1,121 @@
+// Host-side runtime of the device ORB extractor (shared by extractor.hip, stereo.hip, capi.cpp).
+#pragma once
+#include <vector>
+
+#include "orbmi_common.h"
+
+namespace orbmi {
+
+// Per pyramid level constants, resident in device memory (one copy per handle geometry).
+struct LevelGeom {
+    int W, H;            // interior size  (ComputePyramid :1111-1112)
+    int stride, ph;      // padded row pitch (>= W+38, 64-aligned) and padded height H+38
+    long long off;       // byte offset of the padded level inside one image's pyramid
+    int cell_begin, cell_end;   // FAST cell range (global cell index)
+    int nfeat;           // mnFeaturesPerLevel[level]
+    int out_base, out_cap;      // octree output slots (per image)
+    int key_base, key_cap;      // candidate scratch (per image)
+    int width, height;   // octree area maxBorderX-minBorderX, maxBorderY-minBorderY
+    int nIni;            // DistributeOctTree initial node count
+    float hX;            // (float)width / nIni
+    float scale;         // mvScaleFactor[level]
+    float size;          // (float)(int)(PATCH_SIZE * scale)
+    int blur_xv;         // first column of the GaussianBlur scalar tail (4*floor(W/4))
+    int resize_xv;       // first column of the resize vertical scalar tail
+    int xtab_off, ytab_off;     // offsets into the resize coefficient tables (level >= 1)
+};
+
+// One FAST cell of ComputeKeyPointsOctTree (src/ORBextractor.cc:789-829).
+struct CellGeom {
+    short x0, y0, w, h;  // ROI in interior coordinates; w == 0 -> skipped cell
+    short sx, sy;        // j*wCell, i*hCell shift added to ROI coordinates
+    int slot_base;       // first candidate slot (per image)
+    int level;
+};
+
+struct XTab { short sx0, sx1, a0, a1; };  // horizontal resize: source taps and 11-bit weights
+struct YTab { short y0, y1, b0, b1; };    // vertical resize
+
+constexpr int kOctNodeCap = 2048;  // live quadtree nodes per level held in LDS
+
+// Grow-only device buffer.
+template <class T>
+inline int ensure_buf(T** p, size_t* cap, size_t n) {
+    if (*p && *cap >= n) return ORBMI_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (n == 0) n = 1;
+    ORBMI_HIP(hipMalloc((void**)p, n * sizeof(T)));
+    *cap = n;
+    return ORBMI_OK;
+}
+
+struct Extractor {
+    int device = 0;
+    int nfeatures = 0, nlevels = 0, ini_th = 0, min_th = 0;
+    float scale_factor = 0.f;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nfeat, umax;
+
+    // geometry for the current image size
+    int rows = 0, cols = 0;
+    std::vector<LevelGeom> levels;
+    std::vector<CellGeom> cells;
+    long long pimg = 0;      // bytes of one padded pyramid
+    int nslots = 0, keys_cap = 0, out_cap = 0;
+
+    // device buffers (capacity for `bcap` images)
+    int bcap = 0;
+    hipStream_t stream = nullptr;
+    LevelGeom* d_levels = nullptr;
+    CellGeom* d_cells = nullptr;
+    XTab* d_xtab = nullptr;
+    YTab* d_ytab = nullptr;
+    uint8_t* d_pyr = nullptr;
+    int* d_cell_counts = nullptr;
+    uint32_t* d_slots = nullptr;
+    uint32_t* d_keys = nullptr;
+    uint16_t* d_node_of = nullptr;
+    uint2* d_oct = nullptr;        // {x | y << 16 (level coords), score}
+    int* d_oct_count = nullptr;    // [b][level]
+    // last outputs (host API and stereo input)
+    int out_capacity = 0;          // keypoints per image in d_kps / d_desc
+    orbmi_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_counts = nullptr;
+    uint8_t* d_image = nullptr;    // staging for host images
+    size_t image_bytes = 0;
+    int last_batch = 0;
+    // last batch output location (may be caller buffers for the device API)
+    orbmi_keypoint* last_kps = nullptr;
+    uint8_t* last_desc = nullptr;
+    int* last_counts = nullptr;
+    int last_capacity = 0;
+    // stereo scratch
+    float* d_scale_tab = nullptr;  // [scale | inv_scale], 2*nlevels floats
+    int* d_row_start = nullptr;
+    int* d_row_list = nullptr;
+    int* d_sad = nullptr;
+    size_t row_cap = 0, row_list_cap = 0, sad_cap = 0, stereo_cap = 0;
+    float* d_stereo_u = nullptr;
+    float* d_stereo_d = nullptr;
+
+    // per-stage HIP-event profiling (orbmi_set_profiling / orbmi_read_profile)
+    unsigned prof_mask = 0;
+    struct ProfPair { int stage; hipEvent_t a, b; };
+    std::vector<ProfPair> prof_pending;
+    std::vector<hipEvent_t> prof_pool;
+    hipEvent_t prof_event();
+    hipEvent_t prof_begin(int stage);
+    void prof_end(int stage, hipEvent_t a);
+
+    int init(int dev, int nf, float sf, int nl, int ini, int mn);
+    int set_geometry(int rows, int cols);
+    int reserve(int batch, int capacity);
+    int run(const uint8_t* d_images, int batch, size_t step, size_t image_stride,
+            orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity);
+    void release();
+};
+
+}  // namespace orbmi
