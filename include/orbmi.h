@@ -96,6 +96,110 @@ int orbmi_compute_stereo_matches(orbmi_extractor* left, int item_left, orbmi_ext
 int orbmi_compute_stereo_matches_batch_device(orbmi_extractor* h, float bf, float fx,
                                               float* d_u_right, float* d_depth);
 
+/* ---- ORBmatcher ----------------------------------------------------------------------- */
+
+/* Read-only view of the Frame members the matchers use (include/Frame.h).  Pointers may be
+ * host or device memory of the matcher's device (detected per call).  keys_un = mvKeysUn,
+ * u_right = mvuRight (NULL for monocular), desc = mDescriptors (n x 32), tcw = mTcw (4x4
+ * row-major float, needed by SearchByProjection(CF,LF) only). */
+typedef struct orbmi_frame_view {
+    int n;
+    const orbmi_keypoint* keys_un;
+    const float* u_right;
+    const uint8_t* desc;
+    const float* tcw;
+    float fx, fy, cx, cy;          /* Frame::fx, fy, cx, cy                         */
+    float bf, mb;                  /* mbf, mb                                       */
+    float min_x, max_x, min_y, max_y;      /* mnMinX, mnMaxX, mnMinY, mnMaxY        */
+    float grid_w_inv, grid_h_inv;  /* mfGridElementWidthInv, mfGridElementHeightInv */
+    int nlevels;
+    const float* scale_factors;    /* mvScaleFactors (host or device, nlevels)      */
+    float log_scale_factor;        /* mfLogScaleFactor                              */
+} orbmi_frame_view;
+
+/* MapPoint state read by Frame::isInFrustum (src/Frame.cc:274-342). flags: */
+#define ORBMI_MP_BAD 1u            /* isBad()                                       */
+#define ORBMI_MP_SEEN 2u           /* mnLastFrameSeen == current frame (already matched) */
+#define ORBMI_MP_HAS_OBS 4u        /* Observations() > 0                            */
+typedef struct orbmi_mappoint {
+    float pos[3];                  /* GetWorldPos()                                 */
+    float normal[3];               /* GetNormal()                                   */
+    float max_distance;            /* mfMaxDistance (invariance = 1.2 x)            */
+    float min_distance;            /* mfMinDistance (invariance = 0.8 x)            */
+    uint32_t flags;
+    uint8_t desc[32];              /* GetDescriptor()                               */
+} orbmi_mappoint;
+
+/* Output of isInFrustum: mbTrackInView, mTrackProjX/XR/Y, mnTrackScaleLevel, mTrackViewCos. */
+typedef struct orbmi_mappoint_track {
+    int32_t in_view;
+    float proj_x, proj_xr, proj_y;
+    int32_t level;
+    float view_cos;
+} orbmi_mappoint_track;
+
+typedef struct orbmi_matcher orbmi_matcher;
+
+/* ORBmatcher(float nnratio, bool checkOri) is stateless in the reference (include/ORBmatcher.h:
+ * 40); the handle holds a device, a stream and scratch buffers. */
+int orbmi_matcher_create(int device, orbmi_matcher** out);
+void orbmi_matcher_destroy(orbmi_matcher* m);
+
+/* Frame::isInFrustum(pMP, viewingCosLimit) for n_mp points (src/Frame.cc:274-342) with
+ * MapPoint::PredictScale (src/MapPoint.cc:421-436).  Points flagged BAD or SEEN are skipped
+ * (in_view = 0) as in Tracking::SearchLocalPoints (src/Tracking.cc:1375-1379).  track: n_mp. */
+int orbmi_is_in_frustum(orbmi_matcher* m, const orbmi_frame_view* F, const orbmi_mappoint* mps, int n_mp,
+                        float viewing_cos_limit, orbmi_mappoint_track* track);
+
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th)
+ * (src/ORBmatcher.cc:59-155), greedy in point order.  occupied[i] = F.mvpMapPoints[i] &&
+ * Observations() > 0 on entry.  match_mp[i] (n entries) = index of the point newly assigned
+ * to keypoint i, -1 otherwise.  Returns the count in *nmatches. */
+int orbmi_search_by_projection_local(orbmi_matcher* m, const orbmi_frame_view* F, const uint8_t* occupied,
+                                     const orbmi_mappoint* mps, const orbmi_mappoint_track* track, int n_mp,
+                                     float th, float nnratio, int32_t* match_mp, int* nmatches);
+
+/* Tracking::SearchLocalPoints (src/Tracking.cc:1345-1403) fused: isInFrustum(0.5) on every
+ * point, then SearchByProjection(F, points, th) with nnratio 0.8.  *n_to_match = nToMatch. */
+int orbmi_search_local_points(orbmi_matcher* m, const orbmi_frame_view* F, const uint8_t* occupied,
+                              const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp,
+                              int* nmatches, int* n_to_match);
+
+/* Last-frame map point view for SearchByProjection(CF, LF): one entry per LF keypoint. */
+#define ORBMI_LF_HAS_MP 1u         /* LastFrame.mvpMapPoints[i] != NULL             */
+#define ORBMI_LF_OUTLIER 2u        /* LastFrame.mvbOutlier[i]                       */
+typedef struct orbmi_lastframe_point {
+    float pos[3];                  /* pMP->GetWorldPos()                            */
+    uint32_t flags;                /* ORBMI_LF_* | ORBMI_MP_HAS_OBS                 */
+    uint8_t desc[32];              /* pMP->GetDescriptor()                          */
+} orbmi_lastframe_point;
+
+/* ORBmatcher::SearchByProjection(Frame& CF, const Frame& LF, float th, bool bMono)
+ * (src/ORBmatcher.cc:1540-1695) incl. the rotation-consistency histogram when check_ori.
+ * LF provides keys_un (octave = mvKeys[i].octave, angle = mvKeysUn[i].angle) and tcw.
+ * match_lf[i] (CF.n entries) = LF keypoint index newly assigned to CF keypoint i, else -1. */
+int orbmi_search_by_projection_last_frame(orbmi_matcher* m, const orbmi_frame_view* CF, const uint8_t* occupied,
+                                          const orbmi_frame_view* LF, const orbmi_lastframe_point* lf_points,
+                                          float th, int mono, int check_ori, int32_t* match_lf, int* nmatches);
+
+/* DBoW2::FeatureVector as CSR: node ids ascending, feature indices of node k at
+ * feat[off[k] .. off[k+1]) in insertion order (Thirdparty/DBoW2/DBoW2/FeatureVector.h:21-22). */
+typedef struct orbmi_feature_vector {
+    int nnodes;
+    const uint32_t* node_id;
+    const int32_t* off;            /* nnodes + 1 */
+    const int32_t* feat;
+} orbmi_feature_vector;
+
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& matches)
+ * (src/ORBmatcher.cc:211-344).  kf_mp_ok[j] = pKF->GetMapPointMatches()[j] && !isBad().
+ * KF keys_un supply angles (mvKeysUn), F keys_un supply angles of F.mvKeys.  match_kf[i]
+ * (F.n entries) = KF keypoint index whose map point is assigned to F keypoint i, else -1. */
+int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint8_t* kf_mp_ok,
+                        const orbmi_feature_vector* kf_fv, const orbmi_frame_view* F,
+                        const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
+                        int* nmatches);
+
 /* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
 
 /* Kernel stages of one handle; each is a single kernel launch (resize: one per level). */

@@ -169,3 +169,56 @@ def stereo(p: Params, imL: np.ndarray, imR: np.ndarray, bf: float, fx: float,
            u.ctypes.data, d.ctypes.data)
     assert rc == 0, rc
     return u[:N], d[:N]
+
+
+# ---- matchers (ORBmatcher restatement) -------------------------------------------------
+def _match_lib():
+    L = lib()
+    vp, i, f = C.c_void_p, C.c_int, C.c_float
+    L.orc_is_in_frustum.argtypes = [vp, vp, i, f, vp]
+    L.orc_search_by_projection_local.argtypes = [vp, vp, vp, vp, i, f, f, vp, C.POINTER(i)]
+    L.orc_search_by_projection_last_frame.argtypes = [vp, vp, vp, vp, f, i, i, vp, C.POINTER(i)]
+    L.orc_search_by_bow.argtypes = [vp, vp, vp, vp, vp, f, i, vp, C.POINTER(i)]
+    return L
+
+
+def is_in_frustum(frame, mps, viewing_cos_limit=0.5):
+    from orb_slam2_with_comment_amd.types import TRACK_DTYPE
+    mps = np.ascontiguousarray(mps)
+    tr = np.zeros(max(len(mps), 1), TRACK_DTYPE)
+    v = frame.view()
+    _match_lib().orc_is_in_frustum(C.addressof(v), mps.ctypes.data, len(mps), viewing_cos_limit, tr.ctypes.data)
+    return tr[:len(mps)]
+
+
+def search_by_projection_local(frame, occupied, mps, track, th=1.0, nnratio=0.8):
+    occ = np.ascontiguousarray(occupied, np.uint8)
+    mps = np.ascontiguousarray(mps)
+    track = np.ascontiguousarray(track)
+    out = np.zeros(max(len(frame.keys), 1), np.int32)
+    n = C.c_int()
+    v = frame.view()
+    _match_lib().orc_search_by_projection_local(C.addressof(v), occ.ctypes.data, mps.ctypes.data, track.ctypes.data,
+                                                len(mps), th, nnratio, out.ctypes.data, C.byref(n))
+    return out[:len(frame.keys)], n.value
+
+
+def search_by_projection_last_frame(cf, occupied, lf, lf_points, th, mono=False, check_ori=True):
+    occ = np.ascontiguousarray(occupied, np.uint8)
+    lfp = np.ascontiguousarray(lf_points)
+    out = np.zeros(max(len(cf.keys), 1), np.int32)
+    n = C.c_int()
+    vc, vl = cf.view(), lf.view()
+    _match_lib().orc_search_by_projection_last_frame(C.addressof(vc), occ.ctypes.data, C.addressof(vl), lfp.ctypes.data,
+                                                     th, int(mono), int(check_ori), out.ctypes.data, C.byref(n))
+    return out[:len(cf.keys)], n.value
+
+
+def search_by_bow(kf, kf_mp_ok, kf_fv, f, f_fv, nnratio=0.7, check_ori=True):
+    ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+    out = np.zeros(max(len(f.keys), 1), np.int32)
+    n = C.c_int()
+    vk, vf, fk, ff = kf.view(), f.view(), kf_fv.view(), f_fv.view()
+    _match_lib().orc_search_by_bow(C.addressof(vk), ok.ctypes.data, C.addressof(fk), C.addressof(vf), C.addressof(ff),
+                                   nnratio, int(check_ori), out.ctypes.data, C.byref(n))
+    return out[:len(f.keys)], n.value

@@ -5,6 +5,7 @@ for gfx950 behind a C ABI (include/orbmi.h, liborbmi.so).  This package holds th
 (csrc/), their build (build.py), the ctypes binding (_capi.py) and a Python mirror of the
 reference interface (orb.py) used by tests and bench.py.
 """
+from .matcher import ORBmatcher  # noqa: F401
 from .orb import ORBextractor, compute_stereo_matches  # noqa: F401
 
-__all__ = ["ORBextractor", "compute_stereo_matches"]
+__all__ = ["ORBextractor", "ORBmatcher", "compute_stereo_matches"]

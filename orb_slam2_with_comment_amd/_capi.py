@@ -57,6 +57,13 @@ _PROTOS = {
     "orbmi_extractor_get_pyramid_level": (_i, [_vp, _i, _i, _i, _vp, _sz, C.POINTER(_i), C.POINTER(_i)]),
     "orbmi_compute_stereo_matches": (_i, [_vp, _i, _vp, _i, _f, _f, _vp, _vp, _i]),
     "orbmi_compute_stereo_matches_batch_device": (_i, [_vp, _f, _f, _vp, _vp]),
+    "orbmi_matcher_create": (_i, [_i, C.POINTER(_vp)]),
+    "orbmi_matcher_destroy": (None, [_vp]),
+    "orbmi_is_in_frustum": (_i, [_vp, _vp, _vp, _i, _f, _vp]),
+    "orbmi_search_by_projection_local": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _f, _f, _vp, C.POINTER(_i)]),
+    "orbmi_search_local_points": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, C.POINTER(_i), C.POINTER(_i)]),
+    "orbmi_search_by_projection_last_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, C.POINTER(_i)]),
+    "orbmi_search_by_bow": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, C.POINTER(_i)]),
     "orbmi_set_profiling": (_i, [_vp, C.c_uint]),
     "orbmi_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),

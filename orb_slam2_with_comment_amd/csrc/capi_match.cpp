@@ -1,0 +1,297 @@
+// C ABI of the matchers (include/orbmi.h, "ORBmatcher" section).  Inputs may live in host
+// or device memory; host arrays are staged through a per-handle device arena.
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "matcher.h"
+
+using orbmi::DevFrame;
+using orbmi::DevFV;
+using orbmi::Matcher;
+
+struct orbmi_matcher {
+    Matcher m;
+};
+
+namespace orbmi {
+
+void* Matcher::stage(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    for (Block& b : arena)
+        if (b.size - b.used >= bytes) { void* p = b.p + b.used; b.used += bytes; return p; }
+    Block b{nullptr, std::max(bytes, (size_t)(4 << 20)), 0};
+    if (hipMalloc((void**)&b.p, b.size) != hipSuccess) return nullptr;
+    b.used = bytes;
+    arena.push_back(b);
+    return b.p;
+}
+
+void Matcher::arena_reset() {
+    for (Block& b : arena) b.used = 0;
+}
+
+void Matcher::release() {
+    (void)hipSetDevice(device);
+    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_res, d_bin_of, d_hist, d_scalars};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (Block& b : arena) (void)hipFree(b.p);
+    arena.clear();
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+}
+
+}  // namespace orbmi
+
+namespace {
+
+bool on_device(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+// Device view of an input array (copied into the arena when it is host memory).
+template <class T>
+const T* dev_in(Matcher& m, const T* p, size_t n, int* rc) {
+    if (!p || n == 0) return p;
+    if (on_device(p)) return p;
+    T* d = (T*)m.stage(n * sizeof(T));
+    if (!d || hipMemcpyAsync(d, p, n * sizeof(T), hipMemcpyHostToDevice, m.stream) != hipSuccess) {
+        *rc = ORBMI_E_HIP;
+        return nullptr;
+    }
+    return d;
+}
+
+struct OutBuf {
+    void* user = nullptr;
+    void* dev = nullptr;
+    size_t bytes = 0;
+};
+
+template <class T>
+T* dev_out(Matcher& m, T* p, size_t n, std::vector<OutBuf>& outs) {
+    if (on_device(p)) return p;
+    T* d = (T*)m.stage(std::max(n, (size_t)1) * sizeof(T));
+    outs.push_back(OutBuf{p, d, n * sizeof(T)});
+    return d;
+}
+
+int finish(Matcher& m, std::vector<OutBuf>& outs, int* nmatches_dev, int* nmatches, int* extra_dev = nullptr,
+           int* extra = nullptr) {
+    for (OutBuf& o : outs)
+        if (o.bytes) ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream));
+    int tmp[2] = {0, 0};
+    if (nmatches_dev) ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream));
+    if (extra_dev) ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream));
+    ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (nmatches) *nmatches = tmp[0];
+    if (extra) *extra = tmp[1];
+    return ORBMI_OK;
+}
+
+int read_small(const float* p, int n, float* out) {
+    if (on_device(p)) {
+        ORBMI_HIP(hipMemcpy(out, p, n * sizeof(float), hipMemcpyDeviceToHost));
+    } else {
+        memcpy(out, p, n * sizeof(float));
+    }
+    return ORBMI_OK;
+}
+
+int make_frame(Matcher& m, const orbmi_frame_view* v, DevFrame* F, bool need_pose) {
+    if (!v || v->n < 0 || (v->n > 0 && (!v->keys_un || !v->desc))) return ORBMI_E_ARG;
+    if (v->nlevels < 1 || v->nlevels > orbmi::kMaxLevels || !v->scale_factors) return ORBMI_E_ARG;
+    int rc = 0;
+    memset(F, 0, sizeof(*F));
+    F->n = v->n;
+    F->keys = dev_in(m, v->keys_un, (size_t)v->n, &rc);
+    F->u_right = dev_in(m, v->u_right, v->u_right ? (size_t)v->n : 0, &rc);
+    F->desc = dev_in(m, v->desc, (size_t)v->n * 32, &rc);
+    if (rc) return rc;
+    if (need_pose) {
+        if (!v->tcw) return ORBMI_E_ARG;
+        if ((rc = read_small(v->tcw, 16, F->tcw))) return rc;
+    }
+    if ((rc = read_small(v->scale_factors, v->nlevels, F->scale))) return rc;
+    F->fx = v->fx; F->fy = v->fy; F->cx = v->cx; F->cy = v->cy; F->bf = v->bf; F->mb = v->mb;
+    F->min_x = v->min_x; F->max_x = v->max_x; F->min_y = v->min_y; F->max_y = v->max_y;
+    F->grid_w_inv = v->grid_w_inv; F->grid_h_inv = v->grid_h_inv;
+    F->nlevels = v->nlevels;
+    F->log_scale_factor = v->log_scale_factor;
+    return ORBMI_OK;
+}
+
+int make_fv(Matcher& m, const orbmi_feature_vector* v, DevFV* d) {
+    if (!v || v->nnodes < 0) return ORBMI_E_ARG;
+    int rc = 0;
+    d->nnodes = v->nnodes;
+    if (v->nnodes == 0) { d->node_id = nullptr; d->off = nullptr; d->feat = nullptr; return ORBMI_OK; }
+    // total features = off[nnodes]
+    int total = 0;
+    if (on_device(v->off)) {
+        ORBMI_HIP(hipMemcpy(&total, v->off + v->nnodes, sizeof(int), hipMemcpyDeviceToHost));
+    } else {
+        total = v->off[v->nnodes];
+    }
+    d->node_id = dev_in(m, v->node_id, (size_t)v->nnodes, &rc);
+    d->off = dev_in(m, v->off, (size_t)v->nnodes + 1, &rc);
+    d->feat = dev_in(m, v->feat, (size_t)total, &rc);
+    return rc;
+}
+
+int scalars(Matcher& m) {
+    int rc = orbmi::ensure_buf(&m.d_scalars, &m.cap_scalars, 4);
+    if (rc) return rc;
+    ORBMI_HIP(hipMemsetAsync(m.d_scalars, 0, 4 * sizeof(int), m.stream));
+    return ORBMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbmi_matcher_create(int device, orbmi_matcher** out) {
+    if (!out) return ORBMI_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBMI_E_HIP;
+    orbmi_matcher* h = new (std::nothrow) orbmi_matcher();
+    if (!h) return ORBMI_E_ARG;
+    h->m.device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->m.stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return ORBMI_E_HIP;
+    }
+    *out = h;
+    return ORBMI_OK;
+}
+
+void orbmi_matcher_destroy(orbmi_matcher* h) {
+    if (!h) return;
+    h->m.release();
+    delete h;
+}
+
+int orbmi_is_in_frustum(orbmi_matcher* h, const orbmi_frame_view* v, const orbmi_mappoint* mps, int n_mp,
+                        float viewing_cos_limit, orbmi_mappoint_track* track) {
+    if (!h || n_mp < 0 || (n_mp > 0 && (!mps || !track))) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, true))) return rc;
+    const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
+    if (rc) return rc;
+    std::vector<OutBuf> outs;
+    orbmi_mappoint_track* d_tr = dev_out(m, track, (size_t)n_mp, outs);
+    if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, viewing_cos_limit, d_tr, nullptr))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, nullptr, nullptr);
+}
+
+int orbmi_search_by_projection_local(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
+                                     const orbmi_mappoint* mps, const orbmi_mappoint_track* track, int n_mp,
+                                     float th, float nnratio, int32_t* match_mp, int* nmatches) {
+    if (!h || !occupied || !match_mp || !nmatches || n_mp < 0 || (n_mp > 0 && (!mps || !track))) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, false))) return rc;
+    const uint8_t* d_occ = dev_in(m, occupied, (size_t)std::max(F.n, 1), &rc);
+    const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
+    const orbmi_mappoint_track* d_tr = dev_in(m, track, (size_t)n_mp, &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match_mp, (size_t)F.n, outs);
+    if ((rc = orbmi::launch_local_search(m, F, d_occ, d_mps, d_tr, n_mp, th, nnratio, d_out, m.d_scalars))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, m.d_scalars, nmatches);
+}
+
+int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
+                              const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp, int* nmatches,
+                              int* n_to_match) {
+    if (!h || !occupied || !match_mp || !nmatches || n_mp < 0 || (n_mp > 0 && !mps)) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, true))) return rc;
+    const uint8_t* d_occ = dev_in(m, occupied, (size_t)std::max(F.n, 1), &rc);
+    const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    orbmi_mappoint_track* d_tr = (orbmi_mappoint_track*)m.stage((size_t)std::max(n_mp, 1) * sizeof(orbmi_mappoint_track));
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match_mp, (size_t)F.n, outs);
+    // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5); ORBmatcher matcher(0.8)
+    if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, 0.5f, d_tr, m.d_scalars + 1))) return rc;
+    if ((rc = orbmi::launch_local_search(m, F, d_occ, d_mps, d_tr, n_mp, th, 0.8f, d_out, m.d_scalars))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    int ntm = 0;
+    rc = finish(m, outs, m.d_scalars, nmatches, m.d_scalars + 1, &ntm);
+    if (n_to_match) *n_to_match = ntm;
+    return rc;
+}
+
+int orbmi_search_by_projection_last_frame(orbmi_matcher* h, const orbmi_frame_view* cf, const uint8_t* occupied,
+                                          const orbmi_frame_view* lf, const orbmi_lastframe_point* lf_points,
+                                          float th, int mono, int check_ori, int32_t* match_lf, int* nmatches) {
+    if (!h || !occupied || !match_lf || !nmatches || !lf || (lf->n > 0 && !lf_points)) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame CF, LF;
+    int rc;
+    if ((rc = make_frame(m, cf, &CF, true))) return rc;
+    if ((rc = make_frame(m, lf, &LF, true))) return rc;
+    const uint8_t* d_occ = dev_in(m, occupied, (size_t)std::max(CF.n, 1), &rc);
+    const orbmi_lastframe_point* d_lfp = dev_in(m, lf_points, (size_t)LF.n, &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match_lf, (size_t)CF.n, outs);
+    if ((rc = orbmi::launch_lastframe_search(m, CF, d_occ, LF, d_lfp, th, mono, check_ori, d_out, m.d_scalars)))
+        return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, m.d_scalars, nmatches);
+}
+
+int orbmi_search_by_bow(orbmi_matcher* h, const orbmi_frame_view* kf, const uint8_t* kf_mp_ok,
+                        const orbmi_feature_vector* kf_fv, const orbmi_frame_view* f,
+                        const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
+                        int* nmatches) {
+    if (!h || !kf_mp_ok || !match_kf || !nmatches) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame KF, F;
+    DevFV kfv, fv;
+    int rc;
+    if ((rc = make_frame(m, kf, &KF, false))) return rc;
+    if ((rc = make_frame(m, f, &F, false))) return rc;
+    if ((rc = make_fv(m, kf_fv, &kfv))) return rc;
+    if ((rc = make_fv(m, f_fv, &fv))) return rc;
+    const uint8_t* d_ok = dev_in(m, kf_mp_ok, (size_t)std::max(KF.n, 1), &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match_kf, (size_t)F.n, outs);
+    if ((rc = orbmi::launch_bow(m, KF, d_ok, kfv, F, fv, nnratio, check_ori, d_out, m.d_scalars))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, m.d_scalars, nmatches);
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// Host-side state of the device matchers (matcher.hip, capi_match.cpp).
+#pragma once
+#include <vector>
+
+#include "extractor.h"
+
+namespace orbmi {
+
+// Frame view resolved to device pointers; pose and scale tables travel by value.
+struct DevFrame {
+    int n;
+    const orbmi_keypoint* keys;
+    const float* u_right;
+    const uint8_t* desc;
+    float tcw[16];
+    float fx, fy, cx, cy, bf, mb;
+    float min_x, max_x, min_y, max_y, grid_w_inv, grid_h_inv;
+    int nlevels;
+    float scale[kMaxLevels];
+    float log_scale_factor;
+};
+
+struct DevFV {
+    int nnodes;
+    const uint32_t* node_id;
+    const int32_t* off;
+    const int32_t* feat;
+};
+
+struct Matcher {
+    static constexpr int kCandCap = 96;  // candidates kept per query; overflow re-enumerates
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // grid
+    int* d_cell_start = nullptr; size_t cap_cell_start = 0;
+    int* d_cell_list = nullptr; size_t cap_cell_list = 0;
+    int* d_kp_cell = nullptr; size_t cap_kp_cell = 0;
+    // candidates / greedy
+    unsigned long long* d_cand = nullptr; size_t cap_cand = 0;
+    int* d_ncand = nullptr; size_t cap_ncand = 0;
+    int* d_res = nullptr; size_t cap_res = 0;
+    int* d_bin_of = nullptr; size_t cap_bin_of = 0;
+    int* d_hist = nullptr; size_t cap_hist = 0;
+    int* d_scalars = nullptr; size_t cap_scalars = 0;   // small per-call outputs
+    // staging arena for host inputs/outputs (reset per call)
+    struct Block { uint8_t* p; size_t size, used; };
+    std::vector<Block> arena;
+    void* stage(size_t bytes);
+    void arena_reset();
+    void release();
+};
+
+int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int n, float cosl,
+                   orbmi_mappoint_track* tr, int* n_in_view);
+int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, const orbmi_mappoint* mps,
+                        const orbmi_mappoint_track* tr, int n, float th, float nnratio, int* out, int* nmatches);
+int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0, const DevFrame& LF,
+                            const orbmi_lastframe_point* lfp, float th, int mono, int check_ori, int* out,
+                            int* nmatches);
+int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
+               const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
+
+}  // namespace orbmi

@@ -1,0 +1,592 @@
+// ORBmatcher on MI355X (src/ORBmatcher.cc):
+//   k_grid_build        Frame::AssignFeaturesToGrid (src/Frame.cc:232-247)        one workgroup
+//   k_frustum           Frame::isInFrustum + MapPoint::PredictScale               thread / point
+//   k_local_candidates  SearchByProjection(F, MPs): window + static filters + Hamming  thread / point
+//   k_lf_candidates     SearchByProjection(CF, LF): projection + window + Hamming     thread / LF kp
+//   k_greedy            exact greedy replay of the order-dependent exclusion           one workgroup
+//   k_bow_*             SearchByBoW: node merge-join + per-node greedy (one wave / node)
+//
+// Candidate order.  GetFeaturesInArea visits cells ix-major, iy-minor, keypoints in index
+// order inside a cell, so the reference's candidate order is the lexicographic order of
+// (cell ix*48+iy, keypoint index).  Entries are packed as dist<<40 | cellorder<<20 | idx and
+// "first minimum in visit order" becomes a plain u64 minimum, independent of how the grid
+// lists were filled.  The second best (bestDist2/bestLevel2 of :124-137) is the minimum entry
+// once the best entry is excluded.
+//
+// Greedy exclusion.  Query q may not take a keypoint already matched by an earlier query whose
+// map point has observations (:108-110, :1627-1629).  k_greedy iterates r_q = f(q, occ0 U
+// {r_p : p < q}) to a fixpoint inside one workgroup: after round k every query whose
+// dependency chain is <= k is final, and a fixpoint equals the sequential result by
+// induction on q.  A bounded round count falls back to the sequential replay.
+#include <algorithm>
+
+#include "matcher.h"
+
+namespace orbmi {
+
+constexpr int kGridCols = 64, kGridRows = 48, kGridCells = kGridCols * kGridRows;
+constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+
+__device__ inline int popc_desc(const uint8_t* a, const uint8_t* b) {
+    const uint4* x = reinterpret_cast<const uint4*>(a);
+    const uint4* y = reinterpret_cast<const uint4*>(b);
+    return popc256(x[0], x[1], y[0], y[1]);
+}
+
+// -------------------------------------------------------------------------- grid
+__global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict__ cell_start,
+                                                     int* __restrict__ cell_list, int* __restrict__ kp_cell) {
+    __shared__ int cnt[kGridCells + 1];
+    __shared__ int scratch[20];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kGridCells; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < F.n; i += blockDim.x) {
+        const orbmi_keypoint kp = F.keys[i];
+        const int px = (int)roundf((kp.x - F.min_x) * F.grid_w_inv);
+        const int py = (int)roundf((kp.y - F.min_y) * F.grid_h_inv);
+        int c = -1;
+        if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows)) { c = px * kGridRows + py; atomicAdd(&cnt[c], 1); }
+        kp_cell[i] = c;
+    }
+    __syncthreads();
+    int v[3], s = 0;
+    for (int k = 0; k < 3; k++) { v[k] = cnt[tid * 3 + k]; s += v[k]; }  // 1024*3 == kGridCells
+    int total;
+    int e = block_excl_scan(s, scratch, &total);
+    for (int k = 0; k < 3; k++) { cell_start[tid * 3 + k] = e; cnt[tid * 3 + k] = e; e += v[k]; }
+    if (tid == 0) cell_start[kGridCells] = total;
+    __syncthreads();
+    for (int i = tid; i < F.n; i += blockDim.x) {
+        const int c = kp_cell[i];
+        if (c >= 0) cell_list[atomicAdd(&cnt[c], 1)] = i;
+    }
+}
+
+// Frame::GetFeaturesInArea (src/Frame.cc:353-410): calls fn(idx) for every keypoint in the
+// window passing the level filter, in arbitrary order.
+template <class Fn>
+__device__ inline void for_features_in_area(const DevFrame& F, const int* cell_start, const int* cell_list,
+                                            float x, float y, float r, int minLevel, int maxLevel, Fn fn) {
+    const int nMinCellX = max(0, (int)floorf((x - F.min_x - r) * F.grid_w_inv));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - F.min_x + r) * F.grid_w_inv));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - F.min_y - r) * F.grid_h_inv));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - F.min_y + r) * F.grid_h_inv));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * kGridRows + iy;
+            for (int j = cell_start[c]; j < cell_start[c + 1]; j++) {
+                const int idx = cell_list[j];
+                const orbmi_keypoint kp = F.keys[idx];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                const float distx = kp.x - x, disty = kp.y - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) fn(idx, c);
+            }
+        }
+}
+
+__device__ inline unsigned long long cand_entry(int dist, int cell, int idx) {
+    return ((unsigned long long)dist << 40) | ((unsigned long long)cell << 20) | (unsigned)idx;
+}
+
+// R*p + t, float, left to right (pinned P10: cv::gemm small-matrix path)
+__device__ inline void transform(const float* T, const float* p, float* o) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) o[r] = ((T[4 * r] * p[0] + T[4 * r + 1] * p[1]) + T[4 * r + 2] * p[2]) + T[4 * r + 3];
+}
+__device__ inline void camera_center(const float* T, float* o) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) o[c] = -((T[c] * T[3] + T[4 + c] * T[7]) + T[8 + c] * T[11]);
+}
+
+// -------------------------------------------------------------------------- frustum
+__global__ __launch_bounds__(256) void k_frustum(DevFrame F, const orbmi_mappoint* __restrict__ mps, int n,
+                                                 float viewingCosLimit, orbmi_mappoint_track* __restrict__ tr,
+                                                 int* __restrict__ n_in_view) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    orbmi_mappoint_track t = {0, 0.f, 0.f, 0.f, 0, 0.f};
+    const orbmi_mappoint mp = mps[i];
+    bool ok = !(mp.flags & (ORBMI_MP_BAD | ORBMI_MP_SEEN));
+    float Pc[3], Ow[3], u = 0, v = 0, invz = 0, dist = 0, viewCos = 0;
+    if (ok) {
+        transform(F.tcw, mp.pos, Pc);
+        ok = !(Pc[2] < 0.0f);
+    }
+    if (ok) {
+        invz = 1.0f / Pc[2];
+        u = F.fx * Pc[0] * invz + F.cx;
+        v = F.fy * Pc[1] * invz + F.cy;
+        ok = !(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y);
+    }
+    if (ok) {
+        camera_center(F.tcw, Ow);
+        const float maxDistance = 1.2f * mp.max_distance, minDistance = 0.8f * mp.min_distance;
+        const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
+        dist = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        ok = !(dist < minDistance || dist > maxDistance);
+        if (ok) {
+            const double dot = (double)PO[0] * mp.normal[0] + (double)PO[1] * mp.normal[1] + (double)PO[2] * mp.normal[2];
+            viewCos = (float)(dot / (double)dist);
+            ok = !(viewCos < viewingCosLimit);
+        }
+    }
+    if (ok) {
+        const float ratio = mp.max_distance / dist;
+        int nScale = (int)ceilf((float)log((double)ratio) / F.log_scale_factor);
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= F.nlevels) nScale = F.nlevels - 1;
+        t.in_view = 1;
+        t.proj_x = u;
+        t.proj_xr = u - F.bf * invz;
+        t.proj_y = v;
+        t.level = nScale;
+        t.view_cos = viewCos;
+        if (n_in_view) atomicAdd(n_in_view, 1);
+    }
+    tr[i] = t;
+}
+
+// -------------------------------------------------------------------------- candidates
+// SearchByProjection(F, vpMapPoints, th): static part of the per-point search (:66-123).
+__device__ inline bool local_query(const DevFrame& F, const orbmi_mappoint& mp, const orbmi_mappoint_track& t,
+                                   float th, float* x, float* y, float* rs, int* level) {
+    if (!t.in_view || (mp.flags & ORBMI_MP_BAD)) return false;
+    float r = t.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:157-163)
+    if (th != 1.0) r *= th;
+    *level = t.level;
+    *rs = r * F.scale[t.level];
+    *x = t.proj_x;
+    *y = t.proj_y;
+    return true;
+}
+
+template <class Fn>
+__device__ inline void local_candidates(const DevFrame& F, const int* cs, const int* cl, const orbmi_mappoint& mp,
+                                        const orbmi_mappoint_track& t, float th, Fn emit) {
+    float x, y, rs;
+    int level;
+    if (!local_query(F, mp, t, th, &x, &y, &rs, &level)) return;
+    const uint8_t* md = mp.desc;
+    for_features_in_area(F, cs, cl, x, y, rs, level - 1, level, [&](int idx, int cell) {
+        if (F.u_right && F.u_right[idx] > 0) {
+            const float er = fabsf(t.proj_xr - F.u_right[idx]);
+            if (er > rs) return;
+        }
+        emit(cand_entry(popc_desc(md, F.desc + 32 * (long long)idx), cell, idx));
+    });
+}
+
+__global__ __launch_bounds__(256) void k_local_candidates(DevFrame F, const int* __restrict__ cs,
+                                                          const int* __restrict__ cl,
+                                                          const orbmi_mappoint* __restrict__ mps,
+                                                          const orbmi_mappoint_track* __restrict__ tr, int n, float th,
+                                                          unsigned long long* __restrict__ cand,
+                                                          int* __restrict__ ncand, int cap) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const orbmi_mappoint mp = mps[i];
+    const orbmi_mappoint_track t = tr[i];
+    int c = 0;
+    unsigned long long* out = cand + (long long)i * cap;
+    local_candidates(F, cs, cl, mp, t, th, [&](unsigned long long e) {
+        if (c < cap) out[c] = e;
+        c++;
+    });
+    ncand[i] = c;
+}
+
+// SearchByProjection(CF, LF, th, bMono): projection + static part (:1566-1637)
+struct LfQuery {
+    float u, v, radius, ur;
+    int minL, maxL;
+};
+
+__device__ inline bool lf_query(const DevFrame& CF, const DevFrame& LF, const orbmi_lastframe_point& p, int i,
+                                float th, bool bForward, bool bBackward, LfQuery* q) {
+    if (!(p.flags & ORBMI_LF_HAS_MP) || (p.flags & ORBMI_LF_OUTLIER)) return false;
+    float x3Dc[3];
+    transform(CF.tcw, p.pos, x3Dc);
+    const float xc = x3Dc[0], yc = x3Dc[1];
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    if (invzc < 0) return false;
+    const float u = CF.fx * xc * invzc + CF.cx;
+    const float v = CF.fy * yc * invzc + CF.cy;
+    if (!(u >= CF.min_x && u <= CF.max_x)) return false;  // also rejects NaN (zc == 0)
+    if (!(v >= CF.min_y && v <= CF.max_y)) return false;
+    const int nLastOctave = LF.keys[i].octave;
+    q->u = u;
+    q->v = v;
+    q->radius = th * CF.scale[nLastOctave];
+    q->ur = u - CF.bf * invzc;
+    if (bForward) { q->minL = nLastOctave; q->maxL = -1; }
+    else if (bBackward) { q->minL = 0; q->maxL = nLastOctave; }
+    else { q->minL = nLastOctave - 1; q->maxL = nLastOctave + 1; }
+    return true;
+}
+
+template <class Fn>
+__device__ inline void lf_candidates(const DevFrame& CF, const DevFrame& LF, const int* cs, const int* cl,
+                                     const orbmi_lastframe_point& p, int i, float th, bool fw, bool bw, Fn emit) {
+    LfQuery q;
+    if (!lf_query(CF, LF, p, i, th, fw, bw, &q)) return;
+    for_features_in_area(CF, cs, cl, q.u, q.v, q.radius, q.minL, q.maxL, [&](int i2, int cell) {
+        if (CF.u_right && CF.u_right[i2] > 0) {
+            const float er = fabsf(q.ur - CF.u_right[i2]);
+            if (er > q.radius) return;
+        }
+        emit(cand_entry(popc_desc(p.desc, CF.desc + 32 * (long long)i2), cell, i2));
+    });
+}
+
+__device__ inline void motion_direction(const DevFrame& CF, const DevFrame& LF, int mono, bool* fw, bool* bw) {
+    float twc[3], tlc[3];
+    camera_center(CF.tcw, twc);
+    transform(LF.tcw, twc, tlc);
+    *fw = tlc[2] > CF.mb && !mono;
+    *bw = -tlc[2] > CF.mb && !mono;
+}
+
+__global__ __launch_bounds__(256) void k_lf_candidates(DevFrame CF, DevFrame LF, const int* __restrict__ cs,
+                                                       const int* __restrict__ cl,
+                                                       const orbmi_lastframe_point* __restrict__ lfp, float th,
+                                                       int mono, unsigned long long* __restrict__ cand,
+                                                       int* __restrict__ ncand, int cap) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= LF.n) return;
+    bool fw, bw;
+    motion_direction(CF, LF, mono, &fw, &bw);
+    const orbmi_lastframe_point p = lfp[i];
+    int c = 0;
+    unsigned long long* out = cand + (long long)i * cap;
+    lf_candidates(CF, LF, cs, cl, p, i, th, fw, bw, [&](unsigned long long e) {
+        if (c < cap) out[c] = e;
+        c++;
+    });
+    ncand[i] = c;
+}
+
+// -------------------------------------------------------------------------- greedy
+struct GreedyArgs {
+    int mode;             // 0 = local map (best + ratio test), 1 = last frame (best + rotation)
+    int nq;               // queries (map points / LF keypoints), processed in index order
+    const unsigned long long* cand;
+    const int* ncand;
+    int cap;
+    const uint8_t* occ0;  // initial occupancy (F.mvpMapPoints[i] && Observations() > 0)
+    DevFrame F;           // frame searched (CF)
+    DevFrame LF;          // last frame (mode 1)
+    const int* cs;
+    const int* cl;
+    const orbmi_mappoint* mps;              // mode 0
+    const orbmi_mappoint_track* tr;         // mode 0
+    const orbmi_lastframe_point* lfp;       // mode 1
+    float th, nnratio;
+    int mono, check_ori;
+    int* res;             // per query: chosen keypoint or -1
+    int* out;             // per keypoint result (see orbmi.h)
+    int* nmatches;
+};
+
+constexpr int kGreedyMaxKp = 16384;
+constexpr int kGreedyRounds = 48;
+
+// Result of query q under occupancy test occ(idx) (sequential semantics of one iteration).
+template <class Occ>
+__device__ inline int greedy_eval(const GreedyArgs& a, int q, bool fw, bool bw, Occ occ) {
+    unsigned long long b1 = ~0ull, b2 = ~0ull;
+    auto take = [&](unsigned long long e) {
+        if (occ((int)(e & 0xFFFFF))) return;
+        if (e < b1) { b2 = b1; b1 = e; }
+        else if (e < b2) b2 = e;
+    };
+    const int nc = a.ncand[q];
+    if (nc <= a.cap) {
+        const unsigned long long* c = a.cand + (long long)q * a.cap;
+        for (int k = 0; k < nc; k++) take(c[k]);
+    } else if (a.mode == 0) {  // overflowed list: enumerate again
+        local_candidates(a.F, a.cs, a.cl, a.mps[q], a.tr[q], a.th, take);
+    } else {
+        lf_candidates(a.F, a.LF, a.cs, a.cl, a.lfp[q], q, a.th, fw, bw, take);
+    }
+    if (b1 == ~0ull) return -1;
+    const int bestDist = (int)(b1 >> 40);
+    const int bestIdx = (int)(b1 & 0xFFFFF);
+    if (a.mode == 0) {
+        if (bestDist > TH_HIGH) return -1;
+        const int bestDist2 = b2 == ~0ull ? 256 : (int)(b2 >> 40);
+        const int bestLevel = a.F.keys[bestIdx].octave;
+        const int bestLevel2 = b2 == ~0ull ? -1 : a.F.keys[(int)(b2 & 0xFFFFF)].octave;
+        if (bestLevel == bestLevel2 && bestDist > a.nnratio * bestDist2) return -1;
+        return bestIdx;
+    }
+    return bestDist <= TH_HIGH ? bestIdx : -1;
+}
+
+__device__ inline bool query_has_obs(const GreedyArgs& a, int q) {
+    return a.mode == 0 ? (a.mps[q].flags & ORBMI_MP_HAS_OBS) != 0 : (a.lfp[q].flags & ORBMI_MP_HAS_OBS) != 0;
+}
+
+__device__ inline int rot_bin(float a0, float a1) {
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a0 - a1;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+__global__ __launch_bounds__(1024) void k_greedy(GreedyArgs a) {
+    __shared__ int claim[kGreedyMaxKp];   // min query index holding the keypoint (with obs)
+    __shared__ int last[kGreedyMaxKp];    // max query index assigned to the keypoint
+    __shared__ int hist[HISTO_LENGTH];
+    __shared__ int flag[4];
+    const int tid = threadIdx.x, n = a.F.n;
+    bool fw = false, bw = false;
+    if (a.mode == 1) motion_direction(a.F, a.LF, a.mono, &fw, &bw);
+    for (int q = tid; q < a.nq; q += blockDim.x) a.res[q] = -1;
+    bool converged = false;
+    for (int round = 0; round < kGreedyRounds && !converged; round++) {
+        for (int i = tid; i < n; i += blockDim.x) claim[i] = 0x7FFFFFFF;
+        if (tid == 0) flag[0] = 0;
+        __syncthreads();
+        for (int q = tid; q < a.nq; q += blockDim.x) {
+            const int r = a.res[q];
+            if (r >= 0 && query_has_obs(a, q)) atomicMin(&claim[r], q);
+        }
+        __syncthreads();
+        int changed = 0;
+        for (int q = tid; q < a.nq; q += blockDim.x) {
+            const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return a.occ0[idx] || claim[idx] < q; });
+            if (r != a.res[q]) { a.res[q] = r; changed = 1; }
+        }
+        if (changed) atomicOr(&flag[0], 1);
+        __syncthreads();
+        converged = flag[0] == 0;
+        __syncthreads();
+    }
+    if (!converged) {  // sequential replay (exact), bounded-rounds fallback
+        if (tid == 0) {
+            for (int i = 0; i < n; i++) claim[i] = a.occ0[i];
+            for (int q = 0; q < a.nq; q++) {
+                const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return claim[idx] != 0; });
+                a.res[q] = r;
+                if (r >= 0 && query_has_obs(a, q)) claim[r] = 1;
+            }
+        }
+        __syncthreads();
+    }
+    // outputs: last assignment per keypoint; rotation consistency (mode 1)
+    for (int i = tid; i < n; i += blockDim.x) { last[i] = -1; claim[i] = 0; }
+    if (tid < HISTO_LENGTH) hist[tid] = 0;
+    if (tid == 0) flag[1] = 0;
+    __syncthreads();
+    for (int q = tid; q < a.nq; q += blockDim.x) {
+        const int r = a.res[q];
+        if (r < 0) continue;
+        atomicMax(&last[r], q);
+        atomicAdd(&flag[1], 1);
+        if (a.mode == 1 && a.check_ori) atomicAdd(&hist[rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle)], 1);
+    }
+    __syncthreads();
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    if (a.mode == 1 && a.check_ori) {  // ComputeThreeMaxima (:1854-1895), same in every thread
+        int max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        for (int q = tid; q < a.nq; q += blockDim.x) {
+            const int r = a.res[q];
+            if (r < 0) continue;
+            const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
+            if (bin != ind1 && bin != ind2 && bin != ind3) { claim[r] = 1; atomicSub(&flag[1], 1); }
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += blockDim.x) a.out[i] = claim[i] ? -2 : last[i];
+    if (tid == 0) *a.nmatches = flag[1];
+}
+
+// -------------------------------------------------------------------------- SearchByBoW
+// Each node of the KF feature vector finds its partner node in F (merge-join of two sorted
+// id lists, :234-320); nodes are independent (a feature belongs to one node), the greedy
+// exclusion (:265-266) is sequential inside the node: one wave per node.
+__global__ __launch_bounds__(256) void k_bow_match(DevFrame KF, const uint8_t* __restrict__ kf_ok, DevFV kfv,
+                                                   DevFrame F, DevFV fv, float nnratio, int check_ori,
+                                                   int* __restrict__ match, int* __restrict__ bin_of,
+                                                   int* __restrict__ hist) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int a = blockIdx.x * 4 + wid;
+    if (a >= kfv.nnodes) return;
+    const unsigned id = kfv.node_id[a];
+    int lo = 0, hi = fv.nnodes;  // lower_bound
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv.node_id[mid] < id) lo = mid + 1; else hi = mid; }
+    if (lo >= fv.nnodes || fv.node_id[lo] != id) return;
+    const int f0 = fv.off[lo], nf = fv.off[lo + 1] - f0;
+    constexpr int kPer = 8;  // F features per lane kept in registers
+    bool matched[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) matched[k] = false;
+    for (int ia = kfv.off[a]; ia < kfv.off[a + 1]; ia++) {
+        const int realIdxKF = kfv.feat[ia];
+        if (!kf_ok[realIdxKF]) continue;
+        const uint8_t* dKF = KF.desc + 32 * (long long)realIdxKF;
+        unsigned long long b1 = ~0ull, b2 = ~0ull;
+        for (int base = 0; base < nf; base += 64 * kPer) {
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                const int pos = base + k * 64 + lane;
+                if (pos >= nf) continue;
+                const int realIdxF = fv.feat[f0 + pos];
+                const bool done = base == 0 ? matched[k] : match[realIdxF] >= 0;
+                if (done) continue;
+                const unsigned long long e = ((unsigned long long)popc_desc(dKF, F.desc + 32 * (long long)realIdxF) << 32) | (unsigned)pos;
+                if (e < b1) { b2 = b1; b1 = e; } else if (e < b2) b2 = e;
+            }
+        }
+        // wave-wide best / second best of the (dist, position) keys
+        const unsigned long long m1 = wave_min_u64(b1);
+        const unsigned long long c2 = b1 == m1 ? b2 : b1;
+        const unsigned long long m2 = wave_min_u64(c2);
+        const int bestDist1 = m1 == ~0ull ? 256 : (int)(m1 >> 32);
+        const int bestDist2 = m2 == ~0ull ? 256 : (int)(m2 >> 32);
+        if (bestDist1 <= TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {
+            const int pos = (int)(m1 & 0xFFFFFFFFu);
+            const int realIdxF = fv.feat[f0 + pos];
+            if (pos < 64 * kPer && lane == (pos & 63)) {
+#pragma unroll
+                for (int k = 0; k < kPer; k++)
+                    if (k == (pos >> 6)) matched[k] = true;
+            }
+            if (lane == 0) {
+                match[realIdxF] = realIdxKF;
+                if (check_ori) {
+                    const int bin = rot_bin(KF.keys[realIdxKF].angle, F.keys[realIdxF].angle);
+                    bin_of[realIdxF] = bin;
+                    atomicAdd(&hist[bin], 1);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_bow_finalize(int n, int check_ori, const int* __restrict__ hist,
+                                                       const int* __restrict__ bin_of, int* __restrict__ match,
+                                                       int* __restrict__ nmatches) {
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    if (check_ori) {
+        int max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+    }
+    int local = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (match[i] < 0) continue;
+        if (check_ori) {
+            const int b = bin_of[i];
+            if (b != ind1 && b != ind2 && b != ind3) { match[i] = -1; continue; }
+        }
+        local++;
+    }
+    atomicAdd(&cnt, local);
+    __syncthreads();
+    if (threadIdx.x == 0) *nmatches = cnt;
+}
+
+// -------------------------------------------------------------------------- host launchers
+static int grid_for(Matcher& m, const DevFrame& F) {
+    if (F.n > kGreedyMaxKp) return ORBMI_E_UNSUPPORTED;
+    int rc;
+    if ((rc = ensure_buf(&m.d_cell_start, &m.cap_cell_start, (size_t)kGridCells + 1))) return rc;
+    if ((rc = ensure_buf(&m.d_cell_list, &m.cap_cell_list, (size_t)std::max(F.n, 1)))) return rc;
+    if ((rc = ensure_buf(&m.d_kp_cell, &m.cap_kp_cell, (size_t)std::max(F.n, 1)))) return rc;
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.stream, F, m.d_cell_start, m.d_cell_list, m.d_kp_cell);
+    return ORBMI_OK;
+}
+
+int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int n, float cosl,
+                   orbmi_mappoint_track* tr, int* n_in_view) {
+    if (n <= 0) return ORBMI_OK;
+    hipLaunchKernelGGL(k_frustum, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, mps, n, cosl, tr, n_in_view);
+    return ORBMI_OK;
+}
+
+int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, const orbmi_mappoint* mps,
+                        const orbmi_mappoint_track* tr, int n, float th, float nnratio, int* out, int* nmatches) {
+    int rc;
+    if ((rc = grid_for(m, F))) return rc;
+    const int cap = Matcher::kCandCap;
+    if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
+    if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
+    if ((rc = ensure_buf(&m.d_res, &m.cap_res, (size_t)std::max(n, 1)))) return rc;
+    if (n > 0)
+        hipLaunchKernelGGL(k_local_candidates, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start,
+                           m.d_cell_list, mps, tr, n, th, m.d_cand, m.d_ncand, cap);
+    GreedyArgs a{};
+    a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.cap = cap; a.occ0 = occ0; a.F = F;
+    a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
+    a.res = m.d_res; a.out = out; a.nmatches = nmatches;
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
+    return ORBMI_OK;
+}
+
+int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0, const DevFrame& LF,
+                            const orbmi_lastframe_point* lfp, float th, int mono, int check_ori, int* out,
+                            int* nmatches) {
+    int rc;
+    if ((rc = grid_for(m, CF))) return rc;
+    const int n = LF.n, cap = Matcher::kCandCap;
+    if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
+    if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
+    if ((rc = ensure_buf(&m.d_res, &m.cap_res, (size_t)std::max(n, 1)))) return rc;
+    if (n > 0)
+        hipLaunchKernelGGL(k_lf_candidates, dim3((n + 255) / 256), dim3(256), 0, m.stream, CF, LF, m.d_cell_start,
+                           m.d_cell_list, lfp, th, mono, m.d_cand, m.d_ncand, cap);
+    GreedyArgs a{};
+    a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.cap = cap; a.occ0 = occ0; a.F = CF; a.LF = LF;
+    a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
+    a.res = m.d_res; a.out = out; a.nmatches = nmatches;
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
+    return ORBMI_OK;
+}
+
+int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
+               const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches) {
+    int rc;
+    if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, (size_t)std::max(F.n, 1)))) return rc;
+    if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH))) return rc;
+    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, HISTO_LENGTH * sizeof(int), m.stream));
+    ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)std::max(F.n, 1) * sizeof(int), m.stream));
+    if (kfv.nnodes > 0)
+        hipLaunchKernelGGL(k_bow_match, dim3((kfv.nnodes + 3) / 4), dim3(256), 0, m.stream, KF, kf_ok, kfv, F, fv,
+                           nnratio, check_ori, match, m.d_bin_of, m.d_hist);
+    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, F.n, check_ori, m.d_hist, m.d_bin_of, match,
+                       nmatches);
+    return ORBMI_OK;
+}
+
+}  // namespace orbmi

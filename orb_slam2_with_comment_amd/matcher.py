@@ -1,0 +1,95 @@
+"""Python mirror of ORB_SLAM2::ORBmatcher (include/ORBmatcher.h:37-102) over the C ABI.
+
+The map/frame state crosses the boundary as flat arrays (types.py): keypoints, descriptors,
+mvuRight and the pose of a Frame; MapPoint state as orbmi_mappoint records.  Results are the
+reference's side effects as index arrays (see include/orbmi.h for the codes)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._capi import check, lib
+from .types import TRACK_DTYPE
+
+
+class ORBmatcher:
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30  # src/ORBmatcher.cc:37-39
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        h = C.c_void_p()
+        check("orbmi_matcher_create", lib().orbmi_matcher_create(device, C.byref(h)))
+        self._h = h
+        self.mfNNratio = nnratio
+        self.mbCheckOrientation = checkOri
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbmi_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def IsInFrustum(self, frame, mps, viewing_cos_limit=0.5):
+        """Frame::isInFrustum over all points (src/Frame.cc:274-342)."""
+        mps = np.ascontiguousarray(mps)
+        tr = np.zeros(max(len(mps), 1), TRACK_DTYPE)
+        v = frame.view()
+        check("orbmi_is_in_frustum", lib().orbmi_is_in_frustum(self._h, C.addressof(v), mps.ctypes.data, len(mps),
+                                                               viewing_cos_limit, tr.ctypes.data))
+        return tr[:len(mps)]
+
+    def SearchByProjection(self, frame, occupied, mps, track, th=3.0):
+        """SearchByProjection(Frame&, vector<MapPoint*>, th) (src/ORBmatcher.cc:59-155)."""
+        occ = np.ascontiguousarray(occupied, np.uint8)
+        mps = np.ascontiguousarray(mps)
+        track = np.ascontiguousarray(track)
+        out = np.zeros(max(len(frame.keys), 1), np.int32)
+        n = C.c_int()
+        v = frame.view()
+        check("orbmi_search_by_projection_local",
+              lib().orbmi_search_by_projection_local(self._h, C.addressof(v), occ.ctypes.data, mps.ctypes.data,
+                                                     track.ctypes.data, len(mps), th, self.mfNNratio,
+                                                     out.ctypes.data, C.byref(n)))
+        return out[:len(frame.keys)], n.value
+
+    def SearchLocalPoints(self, frame, occupied, mps, th=1.0):
+        """Tracking::SearchLocalPoints (src/Tracking.cc:1345-1403) fused on the GPU."""
+        occ = np.ascontiguousarray(occupied, np.uint8)
+        mps = np.ascontiguousarray(mps)
+        out = np.zeros(max(len(frame.keys), 1), np.int32)
+        n, ntm = C.c_int(), C.c_int()
+        v = frame.view()
+        check("orbmi_search_local_points",
+              lib().orbmi_search_local_points(self._h, C.addressof(v), occ.ctypes.data, mps.ctypes.data, len(mps), th,
+                                              out.ctypes.data, C.byref(n), C.byref(ntm)))
+        return out[:len(frame.keys)], n.value, ntm.value
+
+    def SearchByProjectionLastFrame(self, cf, occupied, lf, lf_points, th, bMono=False):
+        """SearchByProjection(Frame& CF, const Frame& LF, th, bMono) (src/ORBmatcher.cc:1540-1695)."""
+        occ = np.ascontiguousarray(occupied, np.uint8)
+        lfp = np.ascontiguousarray(lf_points)
+        out = np.zeros(max(len(cf.keys), 1), np.int32)
+        n = C.c_int()
+        vc, vl = cf.view(), lf.view()
+        check("orbmi_search_by_projection_last_frame",
+              lib().orbmi_search_by_projection_last_frame(self._h, C.addressof(vc), occ.ctypes.data, C.addressof(vl),
+                                                          lfp.ctypes.data, th, int(bMono),
+                                                          int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)))
+        return out[:len(cf.keys)], n.value
+
+    def SearchByBoW(self, kf, kf_mp_ok, kf_fv, f, f_fv):
+        """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:211-344)."""
+        ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+        out = np.zeros(max(len(f.keys), 1), np.int32)
+        n = C.c_int()
+        vk, vf, fk, ff = kf.view(), f.view(), kf_fv.view(), f_fv.view()
+        check("orbmi_search_by_bow",
+              lib().orbmi_search_by_bow(self._h, C.addressof(vk), ok.ctypes.data, C.addressof(fk), C.addressof(vf),
+                                        C.addressof(ff), self.mfNNratio, int(self.mbCheckOrientation),
+                                        out.ctypes.data, C.byref(n)))
+        return out[:len(f.keys)], n.value

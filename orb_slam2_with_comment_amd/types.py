@@ -1,0 +1,100 @@
+"""numpy / ctypes mirrors of the C-ABI boundary structs (include/orbmi.h)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+# orbmi_mappoint
+MAPPOINT_DTYPE = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("max_distance", "<f4"),
+                           ("min_distance", "<f4"), ("flags", "<u4"), ("desc", "u1", 32)])
+# orbmi_mappoint_track
+TRACK_DTYPE = np.dtype([("in_view", "<i4"), ("proj_x", "<f4"), ("proj_xr", "<f4"), ("proj_y", "<f4"),
+                        ("level", "<i4"), ("view_cos", "<f4")])
+# orbmi_lastframe_point
+LFPOINT_DTYPE = np.dtype([("pos", "<f4", 3), ("flags", "<u4"), ("desc", "u1", 32)])
+
+assert MAPPOINT_DTYPE.itemsize == 68 and TRACK_DTYPE.itemsize == 24 and LFPOINT_DTYPE.itemsize == 48
+
+MP_BAD, MP_SEEN, MP_HAS_OBS = 1, 2, 4
+LF_HAS_MP, LF_OUTLIER = 1, 2
+FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48
+
+
+class FrameView(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p),
+                ("tcw", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float),
+                ("cy", C.c_float), ("bf", C.c_float), ("mb", C.c_float), ("min_x", C.c_float),
+                ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
+                ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float)]
+
+
+class FeatureVectorView(C.Structure):
+    _fields_ = [("nnodes", C.c_int), ("node_id", C.c_void_p), ("off", C.c_void_p), ("feat", C.c_void_p)]
+
+
+class Frame:
+    """Host-side Frame data the matchers read (include/Frame.h), kept alive for the views."""
+
+    def __init__(self, keys, desc, u_right=None, tcw=None, cam=None, scale_factors=None, width=None,
+                 height=None):
+        self.keys = np.ascontiguousarray(keys, KP_DTYPE)
+        self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        self.u_right = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+        self.tcw = np.ascontiguousarray(np.eye(4) if tcw is None else tcw, np.float32)
+        self.cam = cam
+        sf = np.float32(1.2)
+        if scale_factors is None:
+            s, scale_factors = np.float32(1), []
+            for _ in range(8):
+                scale_factors.append(s)
+                s = np.float32(np.float64(s) * np.float64(sf))
+        self.scale_factors = np.ascontiguousarray(scale_factors, np.float32)
+        self.width = width if width is not None else cam.width
+        self.height = height if height is not None else cam.height
+
+    def view(self) -> FrameView:
+        v = FrameView()
+        v.n = len(self.keys)
+        v.keys_un = self.keys.ctypes.data
+        v.u_right = self.u_right.ctypes.data if self.u_right is not None else None
+        v.desc = self.desc.ctypes.data
+        v.tcw = self.tcw.ctypes.data
+        c = self.cam
+        v.fx, v.fy, v.cx, v.cy, v.bf = c.fx, c.fy, c.cx, c.cy, c.bf
+        v.mb = np.float32(np.float32(c.bf) / np.float32(c.fx))
+        # ComputeImageBounds without distortion (src/Frame.cc:481-498)
+        v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(self.width), 0.0, float(self.height)
+        v.grid_w_inv = np.float32(np.float32(FRAME_GRID_COLS) / np.float32(self.width))
+        v.grid_h_inv = np.float32(np.float32(FRAME_GRID_ROWS) / np.float32(self.height))
+        v.nlevels = len(self.scale_factors)
+        v.scale_factors = self.scale_factors.ctypes.data
+        v.log_scale_factor = np.float32(np.log(np.float32(self.scale_factors[1]))) if len(self.scale_factors) > 1 else 0.0
+        self._view = v
+        return v
+
+
+class FeatureVector:
+    """DBoW2::FeatureVector as CSR (node ids ascending, features in insertion order)."""
+
+    def __init__(self, node_of_feature: np.ndarray):
+        node_of_feature = np.asarray(node_of_feature, np.int64)
+        nodes = np.unique(node_of_feature)
+        order = np.argsort(node_of_feature, kind="stable")
+        counts = np.array([np.sum(node_of_feature == n) for n in nodes], np.int32)
+        self.node_id = nodes.astype(np.uint32)
+        self.off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        self.feat = order.astype(np.int32)
+
+    def view(self) -> FeatureVectorView:
+        v = FeatureVectorView()
+        v.nnodes = len(self.node_id)
+        v.node_id = self.node_id.ctypes.data
+        v.off = self.off.ctypes.data
+        v.feat = self.feat.ctypes.data
+        self._view = v
+        return v
