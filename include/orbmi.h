@@ -200,6 +200,61 @@ int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches);
 
+/* ---- Optimizer::LocalBundleAdjustment ------------------------------------------------ */
+
+/* The local-BA graph exactly as src/Optimizer.cc:483-683 builds it: local keyframes
+ * (optimised unless id == 0), fixed observer keyframes, local map points (marginalised), one
+ * edge per (point, keyframe) observation in the reference's insertion order (points in
+ * lLocalMapPoints order, observations in map order).  Poses cross as float Tcw (cv::Mat
+ * CV_32F), converted to double inside (src/Converter.cc:37-47). */
+typedef struct orbmi_ba_keyframe {
+    float tcw[16];                 /* KeyFrame::GetPose(), row-major 4x4                */
+    uint32_t id;                   /* KeyFrame::mnId (vertex id)                         */
+    int32_t fixed;                 /* fixed camera or mnId == 0                          */
+    float fx, fy, cx, cy, bf;      /* KeyFrame::fx, fy, cx, cy, mbf                     */
+} orbmi_ba_keyframe;
+
+typedef struct orbmi_ba_point {
+    float pos[3];                  /* MapPoint::GetWorldPos()                            */
+    uint32_t id;                   /* MapPoint::mnId (vertex id = id + maxKFid + 1)       */
+    int32_t bad;                   /* isBad() when the outlier loops run (:705, :747)     */
+} orbmi_ba_point;
+
+typedef struct orbmi_ba_edge {
+    int32_t point, kf;             /* indices into the point / keyframe arrays           */
+    float u, v;                    /* mvKeysUn[idx].pt                                   */
+    float ur;                      /* mvuRight[idx]; < 0 -> EdgeSE3ProjectXYZ (mono)     */
+    float inv_sigma2;              /* mvInvLevelSigma2[octave]                            */
+} orbmi_ba_edge;
+
+typedef struct orbmi_ba_problem {
+    int nkf, npt, nedge;
+    const orbmi_ba_keyframe* kfs;
+    const orbmi_ba_point* pts;
+    const orbmi_ba_edge* edges;
+} orbmi_ba_problem;
+
+typedef struct orbmi_ba_result {
+    float* tcw;                    /* nkf x 16: optimised poses (fixed ones unchanged)    */
+    float* pos;                    /* npt x 3                                            */
+    uint8_t* erase;                /* nedge: 1 -> (KF, MP) pair goes to vToErase (:741-773) */
+    int iterations[2];             /* optimize(5) / optimize(10) iterations run          */
+    double chi2[2];                /* final activeRobustChi2 of both optimisations       */
+    int aborted;                   /* stop flag seen before the first optimisation: no write-back */
+} orbmi_ba_result;
+
+typedef struct orbmi_ba orbmi_ba;
+int orbmi_ba_create(int device, orbmi_ba** out);
+void orbmi_ba_destroy(orbmi_ba* h);
+
+/* Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (include/Optimizer.h:62,
+ * src/Optimizer.cc:483-808) on the assembled graph: LM (g2o OptimizationAlgorithmLevenberg,
+ * BlockSolver_6_3 Schur complement, Huber sqrt(5.991)/sqrt(7.815)) 5 iterations, outlier
+ * levels, 10 iterations without kernels, erase list.  All arithmetic fp64 on the GPU.
+ * `stop` (may be NULL) is polled like pbStopFlag / mbAbortBA. */
+int orbmi_local_bundle_adjustment(orbmi_ba* h, const orbmi_ba_problem* problem, orbmi_ba_result* result,
+                                  const volatile int* stop);
+
 /* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
 
 /* Kernel stages of one handle; each is a single kernel launch (resize: one per level). */

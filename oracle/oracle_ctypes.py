@@ -222,3 +222,17 @@ def search_by_bow(kf, kf_mp_ok, kf_fv, f, f_fv, nnratio=0.7, check_ori=True):
     _match_lib().orc_search_by_bow(C.addressof(vk), ok.ctypes.data, C.addressof(fk), C.addressof(vf), C.addressof(ff),
                                    nnratio, int(check_ori), out.ctypes.data, C.byref(n))
     return out[:len(f.keys)], n.value
+
+
+def local_ba(problem, stop=False):
+    """Optimizer::LocalBundleAdjustment restatement -> dict(tcw, pos, erase, iterations, chi2, aborted)."""
+    L = lib()
+    L.orc_local_ba.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    r, tcw, pos, erase = problem.result_buffers()
+    v = problem.view()
+    flag = C.c_int(1 if stop else 0)
+    rc = L.orc_local_ba(C.addressof(v), C.addressof(r), C.addressof(flag))
+    assert rc == 0, rc
+    n = len(problem.kfs), len(problem.pts), len(problem.edges)
+    return {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
+            "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}

@@ -64,6 +64,9 @@ _PROTOS = {
     "orbmi_search_local_points": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, C.POINTER(_i), C.POINTER(_i)]),
     "orbmi_search_by_projection_last_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, C.POINTER(_i)]),
     "orbmi_search_by_bow": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, C.POINTER(_i)]),
+    "orbmi_ba_create": (_i, [_i, C.POINTER(_vp)]),
+    "orbmi_ba_destroy": (None, [_vp]),
+    "orbmi_local_bundle_adjustment": (_i, [_vp, _vp, _vp, _vp]),
     "orbmi_set_profiling": (_i, [_vp, C.c_uint]),
     "orbmi_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),

@@ -1,0 +1,107 @@
+"""Python mirror of Optimizer::LocalBundleAdjustment (include/Optimizer.h:62) over the C ABI.
+
+`gather_local_ba` restates the graph assembly of src/Optimizer.cc:486-683 (local keyframes =
+pKF + covisible, local points, fixed observer keyframes, one edge per observation) over a
+minimal map model; `LocalBA.run` optimises the assembled graph on the GPU."""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from ._capi import check, lib
+from .types import BA_EDGE_DTYPE, BA_KF_DTYPE, BA_PT_DTYPE, BAProblem
+
+
+class LocalBA:
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check("orbmi_ba_create", lib().orbmi_ba_create(device, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbmi_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, problem: BAProblem, stop: C.c_int | None = None):
+        r, tcw, pos, erase = problem.result_buffers()
+        v = problem.view()
+        check("orbmi_local_bundle_adjustment",
+              lib().orbmi_local_bundle_adjustment(self._h, C.addressof(v), C.addressof(r),
+                                                  C.addressof(stop) if stop is not None else None))
+        n = len(problem.kfs), len(problem.pts), len(problem.edges)
+        return {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
+                "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+
+
+# ---- minimal map model for the graph assembly (src/Optimizer.cc:486-534) ------------------
+@dataclasses.dataclass(eq=False)
+class KeyFrame:
+    id: int
+    tcw: np.ndarray                     # 4x4 float32
+    keys_un: np.ndarray                 # KP_DTYPE
+    u_right: np.ndarray                 # float32 (-1 = mono)
+    inv_level_sigma2: np.ndarray        # mvInvLevelSigma2
+    cam: object
+    map_points: list = dataclasses.field(default_factory=list)   # MapPoint or None per keypoint
+    covisible: list = dataclasses.field(default_factory=list)    # GetVectorCovisibleKeyFrames order
+    bad: bool = False
+
+
+@dataclasses.dataclass(eq=False)
+class MapPoint:
+    id: int
+    pos: np.ndarray
+    observations: dict = dataclasses.field(default_factory=dict)  # KeyFrame -> keypoint index
+    bad: bool = False
+
+
+def gather_local_ba(pKF: KeyFrame):
+    """Assemble the LocalBundleAdjustment graph around pKF exactly like the reference
+    (local KFs, local MPs in first-seen order, fixed cameras, edges per observation in KF-id
+    order -- the build's deterministic replacement of std::map<KeyFrame*> pointer order)."""
+    local_kfs = [pKF] + [k for k in pKF.covisible if not k.bad]
+    local_set = {id(k) for k in [pKF] + pKF.covisible}
+    local_mps, seen = [], set()
+    for kf in local_kfs:
+        for mp in kf.map_points:
+            if mp is not None and not mp.bad and id(mp) not in seen:
+                seen.add(id(mp))
+                local_mps.append(mp)
+    fixed, fixed_set = [], set()
+    for mp in local_mps:
+        for kf in sorted(mp.observations, key=lambda k: k.id):
+            if id(kf) not in local_set and id(kf) not in fixed_set:
+                fixed_set.add(id(kf))
+                if not kf.bad:
+                    fixed.append(kf)
+    kfs = local_kfs + fixed
+    kidx = {id(k): i for i, k in enumerate(kfs)}
+    K = np.zeros(len(kfs), BA_KF_DTYPE)
+    for i, k in enumerate(kfs):
+        K[i]["tcw"] = np.asarray(k.tcw, np.float32).reshape(-1)
+        K[i]["id"] = k.id
+        K[i]["fixed"] = 1 if (i >= len(local_kfs) or k.id == 0) else 0
+        K[i]["fx"], K[i]["fy"], K[i]["cx"], K[i]["cy"], K[i]["bf"] = k.cam.fx, k.cam.fy, k.cam.cx, k.cam.cy, k.cam.bf
+    P = np.zeros(len(local_mps), BA_PT_DTYPE)
+    edges = []
+    for pi, mp in enumerate(local_mps):
+        P[pi]["pos"] = mp.pos
+        P[pi]["id"] = mp.id
+        P[pi]["bad"] = int(mp.bad)
+        for kf in sorted(mp.observations, key=lambda k: k.id):
+            if kf.bad or id(kf) not in kidx:
+                continue
+            j = mp.observations[kf]
+            kp = kf.keys_un[j]
+            edges.append((pi, kidx[id(kf)], kp["x"], kp["y"], kf.u_right[j], kf.inv_level_sigma2[kp["octave"]]))
+    E = np.array(edges, dtype=BA_EDGE_DTYPE) if edges else np.zeros(0, BA_EDGE_DTYPE)
+    return BAProblem(K, P, E), kfs, local_mps

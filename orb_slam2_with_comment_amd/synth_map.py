@@ -78,3 +78,81 @@ def bow_nodes(desc: np.ndarray, bits=_NODE_BITS) -> np.ndarray:
     for k, bit in enumerate(bits):
         node |= b[:, bit].astype(np.int64) << k
     return node
+
+
+def local_ba_problem(seed=42, n_free=20, n_fixed=4, n_points=3000, stereo_frac=0.8, outlier_frac=0.05,
+                     obs_min=3, obs_max=8, cam=None, pose_noise=(0.02, 0.1), point_noise=0.2, first_id=10):
+    """Config 3 of BASELINE.json / SURVEY.md §8(d): 20 free KFs (1 m spacing, yaw +-0.2 deg) +
+    4 fixed observer KFs, 3000 points in x[-10,10] y[-2,2] z[5,40] m ahead, 3-8 observations per
+    point (~15k edges), octave from distance (PredictScale), sigma = 1 px x scale, 80 % stereo,
+    5 % outliers (+-20 px), initial perturbation +-0.02 rad / +-0.1 m, +-0.2 m on points.
+    Returns (BAProblem, ground truth dict)."""
+    from . import synth
+    from .types import BA_EDGE_DTYPE, BA_KF_DTYPE, BA_PT_DTYPE, BAProblem
+    cam = cam or synth.KITTI
+    rng = np.random.default_rng(seed)
+    sf = np.array([1.2 ** i for i in range(8)], np.float64)
+    n_kf = n_free + n_fixed
+    Twc = []
+    for k in range(n_kf):
+        z = float(k - n_fixed)  # fixed observers sit behind the local window
+        yaw = np.deg2rad(rng.uniform(-0.2, 0.2) * (k - n_fixed))
+        T = np.eye(4)
+        T[:3, :3] = [[np.cos(yaw), 0, np.sin(yaw)], [0, 1, 0], [-np.sin(yaw), 0, np.cos(yaw)]]
+        T[:3, 3] = [rng.uniform(-0.2, 0.2), rng.uniform(-0.05, 0.05), z]
+        Twc.append(T)
+    P = np.stack([rng.uniform(-10, 10, n_points), rng.uniform(-2, 2, n_points),
+                  rng.uniform(5, 40, n_points) + n_free * 0.5], -1)
+    edges, kept_pts = [], []
+    for p in range(n_points):
+        vis = []
+        for k in range(n_kf):
+            Tcw = np.linalg.inv(Twc[k])
+            pc = Tcw[:3, :3] @ P[p] + Tcw[:3, 3]
+            if pc[2] <= 0.5:
+                continue
+            u = cam.fx * pc[0] / pc[2] + cam.cx
+            v = cam.fy * pc[1] / pc[2] + cam.cy
+            if 0 <= u < cam.width and 0 <= v < cam.height:
+                vis.append((k, u, v, pc[2]))
+        if len(vis) < 2:
+            continue
+        m = min(len(vis), int(rng.integers(obs_min, obs_max + 1)))
+        sel = sorted(rng.choice(len(vis), m, replace=False))
+        pi = len(kept_pts)
+        kept_pts.append(p)
+        for s in sel:  # observation map order: by keyframe id
+            k, u, v, z = vis[s]
+            dist = z
+            octave = int(np.clip(np.floor(np.log(max(dist / 8.0, 1.0)) / np.log(1.2)), 0, 7))
+            sigma = sf[octave]
+            uu = u + rng.normal(0, sigma)
+            vv = v + rng.normal(0, sigma)
+            ur = -1.0
+            if rng.random() < stereo_frac:
+                ur = u - cam.bf / z + rng.normal(0, sigma)
+            if rng.random() < outlier_frac:
+                uu += rng.choice([-20, 20])
+                vv += rng.choice([-20, 20])
+            edges.append((pi, k, uu, vv, ur, 1.0 / (sigma * sigma)))
+    kfs = np.zeros(n_kf, BA_KF_DTYPE)
+    for k in range(n_kf):
+        T = Twc[k].copy()
+        if k >= n_fixed:
+            a = rng.uniform(-pose_noise[0], pose_noise[0], 3)
+            th = np.linalg.norm(a)
+            K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]]) / max(th, 1e-12)
+            dR = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+            T[:3, :3] = dR @ T[:3, :3]
+            T[:3, 3] += rng.uniform(-pose_noise[1], pose_noise[1], 3)
+        kfs[k]["tcw"] = tcw_from_twc(T).reshape(-1)
+        kfs[k]["id"] = first_id - n_fixed + k
+        kfs[k]["fixed"] = 1 if k < n_fixed else 0
+        kfs[k]["fx"], kfs[k]["fy"], kfs[k]["cx"], kfs[k]["cy"], kfs[k]["bf"] = cam.fx, cam.fy, cam.cx, cam.cy, cam.bf
+    pts = np.zeros(len(kept_pts), BA_PT_DTYPE)
+    pts["pos"] = (P[kept_pts] + rng.uniform(-point_noise, point_noise, (len(kept_pts), 3))).astype(np.float32)
+    pts["id"] = 1000 + np.arange(len(kept_pts))
+    e = np.array(edges, dtype=[("point", "<i4"), ("kf", "<i4"), ("u", "<f8"), ("v", "<f8"), ("ur", "<f8"),
+                               ("inv_sigma2", "<f8")]).astype(BA_EDGE_DTYPE)
+    gt = {"Twc": np.stack(Twc), "points": P[kept_pts]}
+    return BAProblem(kfs, pts, e), gt

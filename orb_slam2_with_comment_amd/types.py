@@ -98,3 +98,44 @@ class FeatureVector:
         v.feat = self.feat.ctypes.data
         self._view = v
         return v
+
+
+# Optimizer::LocalBundleAdjustment boundary (orbmi_ba_* in include/orbmi.h)
+BA_KF_DTYPE = np.dtype([("tcw", "<f4", 16), ("id", "<u4"), ("fixed", "<i4"), ("fx", "<f4"), ("fy", "<f4"),
+                        ("cx", "<f4"), ("cy", "<f4"), ("bf", "<f4")])
+BA_PT_DTYPE = np.dtype([("pos", "<f4", 3), ("id", "<u4"), ("bad", "<i4")])
+BA_EDGE_DTYPE = np.dtype([("point", "<i4"), ("kf", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                          ("inv_sigma2", "<f4")])
+assert BA_KF_DTYPE.itemsize == 92 and BA_PT_DTYPE.itemsize == 20 and BA_EDGE_DTYPE.itemsize == 24
+
+
+class BAProblemView(C.Structure):
+    _fields_ = [("nkf", C.c_int), ("npt", C.c_int), ("nedge", C.c_int), ("kfs", C.c_void_p), ("pts", C.c_void_p),
+                ("edges", C.c_void_p)]
+
+
+class BAResultView(C.Structure):
+    _fields_ = [("tcw", C.c_void_p), ("pos", C.c_void_p), ("erase", C.c_void_p), ("iterations", C.c_int * 2),
+                ("chi2", C.c_double * 2), ("aborted", C.c_int)]
+
+
+class BAProblem:
+    """Local-BA graph as the C ABI takes it; keeps arrays alive for the views."""
+
+    def __init__(self, kfs, pts, edges):
+        self.kfs = np.ascontiguousarray(kfs, BA_KF_DTYPE)
+        self.pts = np.ascontiguousarray(pts, BA_PT_DTYPE)
+        self.edges = np.ascontiguousarray(edges, BA_EDGE_DTYPE)
+
+    def view(self):
+        v = BAProblemView(len(self.kfs), len(self.pts), len(self.edges), self.kfs.ctypes.data, self.pts.ctypes.data,
+                          self.edges.ctypes.data)
+        self._v = v
+        return v
+
+    def result_buffers(self):
+        tcw = np.zeros((max(len(self.kfs), 1), 16), np.float32)
+        pos = np.zeros((max(len(self.pts), 1), 3), np.float32)
+        erase = np.zeros(max(len(self.edges), 1), np.uint8)
+        r = BAResultView(tcw.ctypes.data, pos.ctypes.data, erase.ctypes.data)
+        return r, tcw, pos, erase
