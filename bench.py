@@ -1,16 +1,24 @@
 #!/usr/bin/env python
-"""bench.py — MI355X ORB front-end throughput (BASELINE.json metric, config 2 workload).
+"""bench.py — MI355X Track+LocalMap throughput (BASELINE.json metric).
 
-One step = one KITTI-shaped 1241x376 stereo frame through the GPU hot path:
-ORBextractor on the left and right images (2000 features, 8 levels; one batched launch
-sequence) + Frame::ComputeStereoMatches.  Frames are synthetic (ray-cast KITTI-shaped
-sequence, orb_slam2_with_comment_amd/synth.py) and resident in HBM before timing.
+Default workload (`--mode track`, SURVEY.md §8(d) config 2 + amortised config 3): one step =
+one KITTI-shaped 1241x376 stereo frame through the GPU hot path, in Tracking's order:
+ORBextractor(left) + ORBextractor(right) (2000 features, 1.2, 8 levels, FAST 20/7; one batched
+launch sequence) + Frame::ComputeStereoMatches + SearchByProjection(CF, LF, th=7) against the
+previous frame's stereo points + SearchLocalPoints (isInFrustum + SearchByProjection, th=1)
+against ~3000 local map points; every 4th frame is a keyframe whose LocalBundleAdjustment
+(config 3: 20 free + 4 fixed KFs, 3000 points, ~15k edges) runs concurrently on the
+LocalMapping thread, as in the reference.  All LocalBAs started inside the timed region finish
+inside it.  Inputs (images, last-frame points, local map) are resident in HBM before timing.
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling:
-        every rank runs its own stereo stream; no data-path collective)
+N > 1 (torchrun, one rank per GPU, config 4): every rank tracks its own stereo stream (weak
+scaling) and each step all-gathers the streams' left descriptors + keypoints over RCCL and
+matches its descriptors against the other streams' (build-defined cross-stream matching).
 
-Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §Measurement).
+Other modes: `--mode extract` (extraction + stereo only), `--mode lba` (config 3 alone),
+`--mode batch` (config 5: EuRoC-shaped 752x480 mono, 5000 features, 64 frames per launch).
+
+Prints ONE JSON line on rank 0 (contract: task statement; fields documented in DESIGN.md).
 """
 from __future__ import annotations
 
@@ -29,7 +37,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (loaded before liborbmi.so: one HIP runtime in the process)
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6    # MI355X FP64 vector
+KF_EVERY = 4            # harness keyframe policy (SURVEY.md §8(d) "CPU baseline timing")
+_vp = C.c_void_p
 
 
 def parse():
@@ -37,16 +48,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--mode", choices=["track", "extract", "lba", "batch"], default="track")
     ap.add_argument("--frames", type=int, default=8, help="distinct stereo frames resident per rank")
     ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--cpu-sample-s", type=float, default=12.0)
+    ap.add_argument("--batch", type=int, default=64, help="frames per launch in --mode batch")
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="per-stage PMC HBM bytes (written by tools/pmc_traffic.py)")
+                    help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def level_geometry(orb_mod, rows, cols, nlevels=8, sf=1.2):
+def level_geometry(rows, cols, nlevels=8, sf=1.2):
     """Pyramid sizes exactly as ComputePyramid (cvRound((float)cols * invScale))."""
     s = np.float32(1.0)
     W, H = [], []
@@ -56,6 +69,574 @@ def level_geometry(orb_mod, rows, cols, nlevels=8, sf=1.2):
         H.append(int(np.rint(np.float32(rows) * inv)))
         s = np.float32(np.float64(s) * np.float64(np.float32(sf)))
     return W, H
+
+
+def read_traffic(path, name):
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("per_launch_bytes", {}).get(name)
+    except Exception:
+        return None
+
+
+# --------------------------------------------------------------------------------- track
+def setup_track(a, rank, local):
+    """Resident inputs for `frames` tracked steps: frames 2..F+1 of the rank's sequence."""
+    from orb_slam2_with_comment_amd import synth, synth_map as SM
+    from orb_slam2_with_comment_amd.orb import compute_stereo_matches
+    from orb_slam2_with_comment_amd.pipeline import StereoTracker, frame_view
+    cam = synth.KITTI
+    F = a.frames
+    seq = [synth.stereo_pair(cam, f, seed_base=1000 * (rank + 1)) for f in range(F + 2)]
+    tr = StereoTracker(cam, a.nfeatures, device=local)
+    sf = tr.scale_factors
+    # per-frame features through the host API (bit-exact with the oracle, tests/); stereo needs
+    # both pyramids resident, so the right images go through a second extractor
+    from orb_slam2_with_comment_amd.orb import ORBextractor
+    right = ORBextractor(a.nfeatures, 1.2, 8, 20, 7, device=local)
+    feats2 = []
+    for L, R, T in seq:
+        kl, dl = tr.extractor(L)
+        right(R)
+        u, d = compute_stereo_matches(tr.extractor, right, cam.bf, cam.fx, len(kl))
+        feats2.append((L, R, T, kl, dl, u, d))
+    right.close()
+    rng = np.random.default_rng(7 + rank)
+    cap = tr.cap
+    dev = torch.device("cuda", local)
+    nF = F + 2
+    lf_keys = torch.zeros((nF, cap, 7), dtype=torch.int32, device=dev)
+    lf_desc = torch.zeros((nF, cap, 32), dtype=torch.uint8, device=dev)
+    lf_u = torch.full((nF, cap), -1.0, dtype=torch.float32, device=dev)
+    from orb_slam2_with_comment_amd.types import LFPOINT_DTYPE, MAPPOINT_DTYPE
+    lf_pts = torch.zeros((nF, cap * LFPOINT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    n_lf, tcws = [], []
+    for f, (L, R, T, kl, dl, u, d) in enumerate(feats2):
+        n = len(kl)
+        n_lf.append(n)
+        lf_keys[f, :n] = torch.from_numpy(np.ascontiguousarray(kl).view(np.int32).reshape(n, 7)).to(dev)
+        lf_desc[f, :n] = torch.from_numpy(dl).to(dev)
+        lf_u[f, :n] = torch.from_numpy(u).to(dev)
+        lfp = SM.lastframe_points(kl, dl, d, cam, T, rng, outlier_frac=0.05)
+        lf_pts[f, :n * LFPOINT_DTYPE.itemsize] = torch.from_numpy(lfp.view(np.uint8)).to(dev)
+        Tn = T.copy()
+        Tn[:3, 3] += rng.normal(0, 0.02, 3)  # motion-model pose estimate, a few cm off
+        tcws.append(SM.tcw_from_twc(Tn))
+    lf_tcw = [SM.tcw_from_twc(x[2]) for x in feats2]
+    lf_views = [frame_view(n_lf[f], lf_keys[f].data_ptr(), lf_u[f].data_ptr(), lf_desc[f].data_ptr(), lf_tcw[f], cam,
+                           sf, cam.width, cam.height) for f in range(nF)]
+    # local map of frame f: points created from frames f-1 and f-2 (~3000)
+    mps, n_mp = [], []
+    for f in range(nF):
+        if f < 2:
+            mps.append(None)
+            n_mp.append(0)
+            continue
+        parts = []
+        for g in (f - 1, f - 2):
+            _, _, T, kl, dl, u, d = feats2[g]
+            mp, _ = SM.mappoints_from_frame(kl, dl, d, cam, T, sf, rng, bad_frac=0.02, noobs_frac=0.02)
+            parts.append(mp)
+        m = np.concatenate(parts)
+        mps.append(torch.from_numpy(m.view(np.uint8).copy()).to(dev))
+        n_mp.append(len(m))
+    imgs = torch.from_numpy(np.stack([np.stack([x[0], x[1]]) for x in feats2])).to(dev)  # nF x 2 x H x W
+    torch.cuda.synchronize()
+    return dict(cam=cam, tr=tr, imgs=imgs, tcws=tcws, lf_views=lf_views, lf_pts=lf_pts, n_lf=n_lf, mps=mps,
+                n_mp=n_mp, feats=feats2, keep=(lf_keys, lf_desc, lf_u, lf_tcw, sf), nF=nF)
+
+
+def run_track(a, rank, world, local, dist):
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd.pipeline import LocalMapper, gather_stream_features, match_cross_stream
+    S = setup_track(a, rank, local)
+    cam, tr = S["cam"], S["tr"]
+    rows, cols = cam.height, cam.width
+    img_bytes = rows * cols
+    F = a.frames
+    problem, _ = SM.local_ba_problem(seed=42)
+    mapper = LocalMapper(local)
+    xmatch = torch.full((tr.cap,), -1, dtype=torch.int32, device=tr.kps.device)
+    ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)
+
+    def step(i):
+        f = 2 + i % F
+        tr.track(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols, S["tcws"][f], S["lf_views"][f - 1],
+                 S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
+        if dist is not None:  # config 4: exchange left features, match against the other streams
+            cur = torch.cuda.current_stream()
+            cur.wait_stream(ext)
+            g_desc, g_kps, g_cnt = gather_stream_features(dist, tr.desc[0], tr.kps[0], tr.counts[:1])
+            ext.wait_stream(cur)
+            match_cross_stream(tr.matcher._h, tr.desc.data_ptr(), tr.cap, tr.counts.data_ptr(), g_desc,
+                               g_cnt.view(-1), rank, xmatch)
+            S["_g"] = (g_desc, g_kps, g_cnt)  # keep alive until the stream has consumed them
+        if i % KF_EVERY == 0:
+            mapper.insert_keyframe(problem)
+
+    def sync():
+        tr.synchronize()
+        mapper.wait()
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    sync()
+    # one LocalBA alone: its latency on an otherwise idle GPU
+    t0 = time.perf_counter()
+    mapper.insert_keyframe(problem)
+    mapper.wait()
+    lba_ms = (time.perf_counter() - t0) * 1e3
+    lba_info = mapper.last
+
+    # per-stage profile (untimed): extractor stages via the library's event brackets
+    stage = profile_stages(tr.extractor.handle, lambda i: (tr.extract_stereo(
+        S["imgs"].data_ptr() + (2 + i % F) * 2 * img_bytes, rows, cols), tr.synchronize()), max(F, 16))
+    # phase profile (untimed): HIP events on the tracking stream around each phase
+    n_tr = max(F, 32)
+    phases = {"extract_stereo": 0.0, "search_last_frame": 0.0, "search_local_points": 0.0}
+    tr.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_tr):
+        f = 2 + i % F
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(ext)
+        tr.extract_stereo(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols)
+        ev[1].record(ext)
+        tr.search_last_frame(S["tcws"][f], S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr())
+        ev[2].record(ext)
+        tr.search_local_points(S["tcws"][f], S["mps"][f].data_ptr(), S["n_mp"][f])
+        ev[3].record(ext)
+        tr.synchronize()
+        for k, name in enumerate(phases):
+            phases[name] += ev[k].elapsed_time(ev[k + 1]) / n_tr
+    track_only_ms = (time.perf_counter() - t0) / n_tr * 1e3  # includes a host sync per frame
+    nm_lf = int((tr.match_lf[:int(tr.counts[0])] >= 0).sum())
+    nm_mp = int((tr.match_mp[:int(tr.counts[0])] >= 0).sum())
+    kp_per_frame = float(stage["kp_per_step"])
+
+    # ---- timed region
+    dom = stage["dominant"]
+    lib = __import__("orb_slam2_with_comment_amd._capi", fromlist=["lib"]).lib()
+    lib.orbmi_set_profiling(tr.extractor.handle, 1 << stage["dominant_id"])
+    reset_profile(tr.extractor.handle)
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ms, nl = read_profile(tr.extractor.handle)
+    lib.orbmi_set_profiling(tr.extractor.handle, 0)
+    dt = max_over_ranks(dt, dist)
+    n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
+    value = a.steps * world / dt
+    roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic)
+    out = None
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline_track(S, problem, a)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: ray-cast KITTI-shaped 1241x376 stereo sequence + back-projected local map + "
+                    "config-3 LocalBA graph, resident in HBM",
+            "config": {
+                "workload": "Track+LocalMap per stereo frame: ORBextractor(L,R) [2000 feat, 1.2, 8 lv, FAST 20/7] "
+                            "+ ComputeStereoMatches + SearchByProjection(CF,LF,th=7) + SearchLocalPoints(th=1, "
+                            f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs) + LocalBundleAdjustment(config 3) "
+                            f"every {KF_EVERY}th frame on the concurrent LocalMapping thread"
+                            + ("; + RCCL all-gather of left desc/kps and cross-stream matching (config 4)"
+                               if world > 1 else ""),
+                "frames_resident": F, "parallelism": f"one stereo stream per GPU x{world}",
+                "not_on_gpu_path": "PoseOptimization (SURVEY.md §8(f) rank 1) — excluded on both sides",
+            },
+            "kpts_desc_per_s": round(value * kp_per_frame, 1),
+            "keypoints_per_frame": round(kp_per_frame, 1),
+            "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp},
+            "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},
+            "track_only_ms_per_frame_synced": round(track_only_ms, 4),
+            "local_ba": {"ms_per_call_idle_gpu": round(lba_ms, 3), "calls_in_timed_region": n_lba,
+                         "iterations": list(lba_info["iterations"]) if lba_info else None,
+                         "edges": int(len(problem.edges)), "points": int(len(problem.pts)),
+                         "keyframes": int(len(problem.kfs))},
+            "stage_ms_per_step": stage["stage_ms"],
+            "roofline": roof,
+            "pipeline_roofline": pipeline_roofline(stage, rows, cols),
+            "cpu_baseline": cpu,
+            "host": host_info(),
+        }
+    mapper.close()
+    tr.close()
+    return out
+
+
+# --------------------------------------------------------------------------------- helpers
+def profile_stages(handle, run_step, n):
+    """Per-stage GPU time of the extractor/stereo kernels (library event brackets) and the
+    algorithmic bytes of each stage's launch."""
+    from orb_slam2_with_comment_amd import _capi
+    lib = _capi.lib()
+    NS = _capi.NUM_STAGES
+    lib.orbmi_set_profiling(handle, 0xFF)
+    reset_profile(handle)
+    kp = 0
+    cand = 0
+    W, H = level_geometry(376, 1241)
+    for i in range(n):
+        run_step(i)
+    ms, nl = read_profile(handle)
+    lib.orbmi_set_profiling(handle, 0)
+    # keypoints and FAST candidates of the last step (debug views)
+    cnt = np.zeros(2, np.int32)
+    for item in range(2):
+        buf = np.zeros((1 << 16, 3), np.int32)
+        for l in range(8):
+            c = C.c_int()
+            lib.orbmi_debug_fast_candidates(handle, item, l, _capi.ptr(buf), 1 << 16, C.byref(c))
+            cand += c.value
+    lvl = np.zeros((1 << 14, 3), np.int32)
+    for item in range(2):
+        for l in range(8):
+            c = C.c_int()
+            lib.orbmi_debug_octree_level(handle, item, l, _capi.ptr(lvl), 1 << 14, C.byref(c))
+            kp += c.value
+    stage_ms = {_capi.STAGES[s]: round(ms[s] / n, 5) for s in range(NS) if nl[s] and s < len(_capi.STAGES)}
+    dom = int(np.argmax(ms))
+    P = sum(w * h for w, h in zip(W, H))
+    padded = [(w + 38) * (h + 38) for w, h in zip(W, H)]
+    cand_img, kp_img = cand / 2, kp / 2
+    alg = {
+        "pyr_level0": 2 * (W[0] * H[0] + padded[0]),
+        "pyr_resize": 2 * sum(W[l - 1] * H[l - 1] + padded[l] for l in range(1, 8)) / 7,
+        "fast": 2 * (P + 4 * cand_img),
+        "octree": 2 * (4 * cand_img + 8 * kp_img),
+        "describe": 2 * kp_img * (43 * 43 + 60),
+        "stereo_rows": kp_img * 28 * 2,
+        "stereo_match": kp_img * (28 + 32 + 8) + kp_img * 1452,
+        "stereo_filter": kp_img * 16,
+    }
+    return {"stage_ms": stage_ms, "dominant_id": dom, "dominant": _capi.STAGES[dom], "alg": alg, "P": P,
+            "kp_per_step": kp, "launch_counts": {_capi.STAGES[s]: int(nl[s]) / n for s in range(NS)
+                                                 if nl[s] and s < len(_capi.STAGES)}}
+
+
+def reset_profile(handle):
+    read_profile(handle)
+
+
+def read_profile(handle):
+    from orb_slam2_with_comment_amd import _capi
+    NS = _capi.NUM_STAGES
+    ms = np.zeros(NS)
+    nl = np.zeros(NS, np.int64)
+    _capi.check("orbmi_read_profile", _capi.lib().orbmi_read_profile(handle, _capi.ptr(ms), _capi.ptr(nl)))
+    return ms, nl
+
+
+def roofline_entry(name, stage, ms_total, launches, traffic_path):
+    avg_s = ms_total / max(int(launches), 1) / 1e3
+    alg = float(stage["alg"].get(name, 0.0))
+    achieved = alg / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": read_traffic(traffic_path, name),
+            "alg_bytes_per_launch": round(alg), "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches)}
+
+
+def pipeline_roofline(stage, rows, cols):
+    kp_img = stage["kp_per_step"] / 2
+    B = 7 * stage["P"] + 60 * kp_img  # SURVEY.md §8(d): B = 7P + 60N per image
+    ext_ms = sum(v for k, v in stage["stage_ms"].items() if k in ("pyr_level0", "pyr_resize", "fast", "octree",
+                                                                   "describe"))
+    out = {"alg_bytes_per_image": round(B), "extract_ms_per_step": round(ext_ms, 5)}
+    if ext_ms > 0:
+        gbs = 2 * B / (ext_ms / 1e3) / 1e9
+        out["achieved_GBs"] = round(gbs, 3)
+        out["frac"] = round(gbs / HBM_PEAK_GBS, 6)
+    return out
+
+
+def max_over_ranks(dt, dist):
+    if not dist:
+        return dt
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def host_info():
+    return {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count(), "hip": torch.version.hip}
+
+
+def cpu_baseline_track(S, problem, a):
+    """The oracle (C++ restatement of the reference path) on host cores with the reference's
+    threading: L/R extraction on two threads (src/Frame.cc:78-81), stereo + both searches
+    serial, LocalBundleAdjustment on a third thread (LocalMapping) every 4th frame."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle_ctypes as O
+    from orb_slam2_with_comment_amd.types import Frame, LFPOINT_DTYPE, MAPPOINT_DTYPE
+    cam = S["cam"]
+    p = O.params(a.nfeatures)
+    pool = ThreadPoolExecutor(2)
+    lm = ThreadPoolExecutor(1)
+    F = a.frames
+    lf_frames = {}
+    for f in range(S["nF"]):
+        L, R, T, kl, dl, u, d = S["feats"][f]
+        lf_frames[f] = Frame(kl, dl, u, S["keep"][3][f], cam)
+    lf_points = [S["lf_pts"][f][:S["n_lf"][f] * LFPOINT_DTYPE.itemsize].cpu().numpy().view(LFPOINT_DTYPE)
+                 for f in range(S["nF"])]
+    mps = [None if m is None else m.cpu().numpy().view(MAPPOINT_DTYPE) for m in S["mps"]]
+    futs = []
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        f = 2 + n % F
+        L, R, T, _, _, _, _ = S["feats"][f]
+        fl = pool.submit(O.extract, p, L)
+        fr = pool.submit(O.extract, p, R)
+        (kl, dl), (kr, dr) = fl.result(), fr.result()
+        u, d = O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
+        cf = Frame(kl, dl, u, S["tcws"][f], cam)
+        occ = np.zeros(len(kl), np.uint8)
+        O.search_by_projection_last_frame(cf, occ, lf_frames[f - 1], lf_points[f - 1], 7.0)
+        trk = O.is_in_frustum(cf, mps[f], 0.5)
+        O.search_by_projection_local(cf, occ, mps[f], trk, 1.0, 0.8)
+        if n % KF_EVERY == 0:
+            futs.append(lm.submit(O.local_ba, problem))
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= a.cpu_sample_s and n >= KF_EVERY) or n >= 10000:
+            break
+    for fu in futs:
+        fu.result()
+    el = time.perf_counter() - t0
+    pool.shutdown()
+    lm.shutdown()
+    return {"value": round(n / el, 4), "unit": "frames/s", "cores": 3, "kind": "port",
+            "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle extract L||R "
+                      f"(2 threads) + stereo + SearchByProjection(LF) + SearchLocalPoints serial, "
+                      f"{len(futs)} LocalBA on a 3rd thread; {el:.1f} s"}
+
+
+# --------------------------------------------------------------------------------- extract
+def run_extract(a, rank, world, local, dist):
+    from orb_slam2_with_comment_amd import synth
+    from orb_slam2_with_comment_amd.pipeline import StereoTracker
+    cam = synth.KITTI
+    rows, cols = cam.height, cam.width
+    frames = [synth.stereo_pair(cam, f, seed_base=1000 * (rank + 1))[:2] for f in range(a.frames)]
+    imgs = torch.from_numpy(np.stack([np.stack(p) for p in frames])).cuda()
+    tr = StereoTracker(cam, a.nfeatures, device=local)
+    img_bytes = rows * cols
+
+    def step(i):
+        tr.extract_stereo(imgs.data_ptr() + (i % a.frames) * 2 * img_bytes, rows, cols)
+
+    for i in range(a.warmup):
+        step(i)
+    tr.synchronize()
+    stage = profile_stages(tr.extractor.handle, lambda i: (step(i), tr.synchronize()), max(a.frames, 16))
+    from orb_slam2_with_comment_amd import _capi
+    lib = _capi.lib()
+    lib.orbmi_set_profiling(tr.extractor.handle, 1 << stage["dominant_id"])
+    reset_profile(tr.extractor.handle)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
+    ms, nl = read_profile(tr.extractor.handle)
+    lib.orbmi_set_profiling(tr.extractor.handle, 0)
+    value = a.steps * world / dt
+    out = None
+    if rank == 0:
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline_extract(frames, cam, a)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: ray-cast KITTI-shaped 1241x376 stereo sequence, resident in HBM",
+            "config": {"workload": "extraction only: ORBextractor(L,R) [2000 feat] + ComputeStereoMatches",
+                       "frames_resident": a.frames, "parallelism": f"one stereo stream per GPU x{world}"},
+            "kpts_desc_per_s": round(value * stage["kp_per_step"], 1),
+            "keypoints_per_frame": stage["kp_per_step"],
+            "stage_ms_per_step": stage["stage_ms"],
+            "roofline": roofline_entry(stage["dominant"], stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]],
+                                       a.traffic),
+            "pipeline_roofline": pipeline_roofline(stage, rows, cols),
+            "cpu_baseline": cpu, "host": host_info(),
+        }
+    tr.close()
+    return out
+
+
+def cpu_baseline_extract(frames, cam, a):
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle_ctypes as O
+    p = O.params(a.nfeatures)
+    pool = ThreadPoolExecutor(2)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        L, R = frames[n % len(frames)]
+        fl, fr = pool.submit(O.extract, p, L), pool.submit(O.extract, p, R)
+        (kl, dl), (kr, dr) = fl.result(), fr.result()
+        O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= a.cpu_sample_s and n >= 3) or n >= 10000:
+            break
+    pool.shutdown()
+    return {"value": round(n / el, 4), "unit": "frames/s", "cores": 2, "kind": "port",
+            "sample": f"{n} stereo frames, oracle extract L||R (2 threads) + stereo, {el:.1f} s"}
+
+
+# --------------------------------------------------------------------------------- lba
+def run_lba(a, rank, world, local, dist):
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd.optimizer import LocalBA
+    problem, _ = SM.local_ba_problem(seed=42 + rank)
+    ba = LocalBA(local)
+    for _ in range(max(a.warmup // 10, 1)):
+        res = ba.run(problem)
+    steps = max(a.steps // 10, 3)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = ba.run(problem)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
+    out = None
+    if rank == 0:
+        from oracle import oracle_ctypes as O
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            n, t0 = 0, time.perf_counter()
+            while True:
+                O.local_ba(problem)
+                n += 1
+                if time.perf_counter() - t0 > min(a.cpu_sample_s, 10) and n >= 3:
+                    break
+            el = time.perf_counter() - t0
+            cpu = {"value": round(n / el, 4), "unit": "LocalBA/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} config-3 LocalBAs on the oracle (g2o restatement, 1 thread), {el:.1f} s"}
+        it = res["iterations"]
+        E, M, K = len(problem.edges), len(problem.pts), int((problem.kfs["fixed"] == 0).sum())
+        # SURVEY.md §8(d): flops per LM iteration ~ E*600 + Schur + (6K)^3/3
+        obs = np.bincount(problem.edges["point"], minlength=M)
+        flops_it = E * 600 + 2 * np.sum(72 * obs + 108 * obs * (obs + 1) / 2) + (6 * K) ** 3 / 3
+        per_call_s = dt / steps
+        achieved = flops_it * (it[0] + it[1]) / per_call_s / 1e12
+        out = {
+            "metric": "LocalBundleAdjustment/s (config 3)", "value": round(steps * world / dt, 3), "unit": "LocalBA/s",
+            "n_gpus": world, "steps": steps, "warmup": a.warmup, "ms_per_step": round(per_call_s * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic config-3 graph (seed 42): 20 free + 4 fixed KFs, 3000 points",
+            "config": {"workload": "config3: Optimizer::LocalBundleAdjustment, 5+10 LM iterations, Huber",
+                       "edges": E, "points": M, "free_keyframes": K},
+            "iterations": list(it), "chi2": list(res["chi2"]),
+            "roofline": {"kernel": "k_local_ba", "bound": "latency (single persistent workgroup)",
+                         "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP64_PEAK_TFS, 8), "traffic": None},
+            "cpu_baseline": cpu, "host": host_info(),
+        }
+    ba.close()
+    return out
+
+
+# --------------------------------------------------------------------------------- batch
+def run_batch(a, rank, world, local, dist):
+    """Config 5: EuRoC-shaped 752x480 mono, 8 levels, 5000 features, batch frames per launch."""
+    from orb_slam2_with_comment_amd import _capi, synth
+    from orb_slam2_with_comment_amd.orb import ORBextractor
+    cam = synth.EUROC
+    rows, cols = cam.height, cam.width
+    nb = a.batch
+    distinct = min(nb, 16)
+    base = [synth.mono(cam, f, seed_base=5000 + 1000 * rank) for f in range(distinct)]
+    imgs = torch.from_numpy(np.stack([base[i % distinct] for i in range(nb)])).cuda()
+    ex = ORBextractor(5000, 1.2, 8, 20, 7, device=local)
+    cap = 5000 + 64
+    kps = torch.zeros((nb, cap, 7), dtype=torch.int32, device="cuda")
+    desc = torch.zeros((nb, cap, 32), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    lib = _capi.lib()
+
+    def step(i):
+        _capi.check("extract", lib.orbmi_extract_batch_device(
+            ex.handle, _vp(imgs.data_ptr()), nb, rows, cols, cols, rows * cols, _vp(kps.data_ptr()),
+            _vp(desc.data_ptr()), _vp(cnt.data_ptr()), cap))
+
+    def sync():
+        lib.orbmi_extractor_synchronize(ex.handle)
+        torch.cuda.synchronize()
+
+    for i in range(max(a.warmup // 4, 2)):
+        step(i)
+    sync()
+    steps = max(a.steps // 10, 5)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if dist:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
+    kp = float(cnt.float().mean().item())
+    W, H = level_geometry(rows, cols)
+    P = sum(w * h for w, h in zip(W, H))
+    B = (7 * P + 60 * kp) * nb
+    out = None
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            from oracle import oracle_ctypes as O
+            p = O.params(5000)
+            n, t0 = 0, time.perf_counter()
+            while True:
+                O.extract(p, base[n % distinct])
+                n += 1
+                if time.perf_counter() - t0 > min(a.cpu_sample_s, 10) and n >= 3:
+                    break
+            el = time.perf_counter() - t0
+            cpu = {"value": round(n / el, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} EuRoC-shaped frames on the oracle extractor (1 thread), {el:.1f} s"}
+        gbs = B / (dt / steps) / 1e9
+        out = {
+            "metric": "frames/s (config 5 batched mono extraction)", "value": round(steps * nb * world / dt, 3),
+            "unit": "frames/s", "n_gpus": world, "steps": steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic EuRoC-shaped 752x480 mono frames, resident in HBM",
+            "config": {"workload": f"config5: ORBextractor 5000 feat, 8 levels, {nb} frames per launch"},
+            "kpts_desc_per_s": round(steps * nb * world * kp / dt, 1), "keypoints_per_frame": round(kp, 1),
+            "roofline": {"kernel": "pipeline", "bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                         "alg_bytes_per_launch": round(B)},
+            "cpu_baseline": cpu, "host": host_info(),
+        }
+    ex.close()
+    return out
 
 
 def main():
@@ -68,210 +649,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from orb_slam2_with_comment_amd import _capi, synth
-    from orb_slam2_with_comment_amd.orb import ORBextractor
-
-    lib = _capi.lib()
-    cam = synth.KITTI
-    rows, cols = cam.height, cam.width
-    # every rank owns one stereo stream (weak scaling); frames resident in HBM
-    frames = [synth.stereo_pair(cam, f, seed_base=1000 * (rank + 1))[:2] for f in range(a.frames)]
-    host = np.stack([np.stack(p) for p in frames])  # F x 2 x H x W
-    d_img = torch.from_numpy(host).cuda()
-    ex = ORBextractor(a.nfeatures, 1.2, 8, 20, 7, device=local)
-    cap = a.nfeatures + 64
-    d_kps = torch.zeros((2, cap, 7), dtype=torch.int32, device="cuda")
-    d_desc = torch.zeros((2, cap, 32), dtype=torch.uint8, device="cuda")
-    d_cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
-    d_u = torch.zeros((2, cap), dtype=torch.float32, device="cuda")
-    d_d = torch.zeros((2, cap), dtype=torch.float32, device="cuda")
-    torch.cuda.synchronize()
-    img_bytes = rows * cols
-    vp = C.c_void_p
-
-    def step(i):
-        f = i % a.frames
-        _capi.check("extract", lib.orbmi_extract_batch_device(
-            ex.handle, vp(d_img.data_ptr() + f * 2 * img_bytes), 2, rows, cols, cols, img_bytes,
-            vp(d_kps.data_ptr()), vp(d_desc.data_ptr()), vp(d_cnt.data_ptr()), cap))
-        _capi.check("stereo", lib.orbmi_compute_stereo_matches_batch_device(
-            ex.handle, cam.bf, cam.fx, vp(d_u.data_ptr()), vp(d_d.data_ptr())))
-
-    def sync():
-        _capi.check("sync", lib.orbmi_extractor_synchronize(ex.handle))
-        torch.cuda.synchronize()
-
-    for i in range(a.warmup):
-        step(i)
-    sync()
-
-    # ---- per-stage profile pass (untimed): all stages, one cycle over the frame set
-    NS = _capi.NUM_STAGES
-    ms = np.zeros(NS)
-    nl = np.zeros(NS, np.int64)
-    lib.orbmi_set_profiling(ex.handle, 0xFF)
-    kp_total = 0
-    n_prof = max(a.frames, 16)
-    for i in range(n_prof):
-        step(i)
-        sync()
-        kp_total += int(d_cnt.sum().item())
-    _capi.check("prof", lib.orbmi_read_profile(ex.handle, _capi.ptr(ms), _capi.ptr(nl)))
-    lib.orbmi_set_profiling(ex.handle, 0)
-    stage_ms_per_step = {(_capi.STAGES[s] if s < len(_capi.STAGES) else str(s)): round(ms[s] / n_prof, 5)
-                         for s in range(NS) if nl[s]}
-    dom = int(np.argmax(ms))
-    kp_per_frame = kp_total / n_prof
-
-    # algorithmic bytes per launch of each stage
-    W, H = level_geometry(None, rows, cols)
-    P = sum(w * h for w, h in zip(W, H))
-    padded = [(w + 38) * (h + 38) for w, h in zip(W, H)]
-    n_img = 2
-    cand = 0
-    for f in range(a.frames):  # FAST candidates (reads the debug view of the last run per frame)
-        step(f)
-        sync()
-        for item in range(2):
-            for l in range(8):
-                buf = np.zeros((1 << 16, 3), np.int32)
-                n = C.c_int()
-                lib.orbmi_debug_fast_candidates(ex.handle, item, l, _capi.ptr(buf), 1 << 16, C.byref(n))
-                cand += n.value
-    cand_per_img = cand / (2 * a.frames)
-    kp_per_img = kp_per_frame / 2
-    alg = {
-        0: n_img * (W[0] * H[0] + padded[0]),                                   # pyr level 0
-        1: n_img * sum(W[l - 1] * H[l - 1] + padded[l] for l in range(1, 8)) / 7,  # per resize launch
-        2: n_img * (P + 4 * cand_per_img),                                      # FAST: pixels + candidates
-        3: n_img * (4 * cand_per_img + 8 * kp_per_img),                         # octree: candidates in, keys out
-        4: n_img * kp_per_img * (43 * 43 + 60),                                 # describe: window + kp+desc
-    }
-    dom_name = _capi.STAGES[dom]
-
-    # ---- timed region: K steps, events bracket the dominant kernel's launches
-    lib.orbmi_set_profiling(ex.handle, 1 << dom)
-    ms[:] = 0
-    nl[:] = 0
-    _capi.check("prof", lib.orbmi_read_profile(ex.handle, _capi.ptr(ms), _capi.ptr(nl)))
-    ms[:] = 0
-    nl[:] = 0
-    sync()
+    run = {"track": run_track, "extract": run_extract, "lba": run_lba, "batch": run_batch}[a.mode]
+    out = run(a, rank, world, local, dist)
+    if rank == 0 and out is not None:
+        print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    sync()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
-    _capi.check("prof", lib.orbmi_read_profile(ex.handle, _capi.ptr(ms), _capi.ptr(nl)))
-    lib.orbmi_set_profiling(ex.handle, 0)
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    frames_total = a.steps * world
-    value = frames_total / dt
-    avg_launch_s = ms[dom] / max(nl[dom], 1) / 1e3
-    achieved = alg.get(dom, 0.0) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = None
-    if os.path.exists(a.traffic):
-        try:
-            tj = json.load(open(a.traffic))
-            traffic = tj.get("per_launch_bytes", {}).get(dom_name)
-        except Exception:
-            traffic = None
-
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
-
-    cpu = None
-    if not a.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(frames, cam, a)
-
-    out = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "frames/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(dt / a.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic: ray-cast KITTI-shaped 1241x376 stereo sequence, resident in HBM",
-        "config": {
-            "workload": "config2: per step one stereo frame -> ORBextractor(left,right) [2000 feat, 1.2, 8 levels, "
-                        "FAST 20/7] + Frame::ComputeStereoMatches; batch=1 frame",
-            "frames_resident": a.frames,
-            "parallelism": f"replica-per-gpu x{world} (independent stereo streams)",
-        },
-        "kpts_desc_per_s": round(value * kp_per_frame, 1),
-        "keypoints_per_frame": round(kp_per_frame, 1),
-        "stage_ms_per_step": stage_ms_per_step,
-        "roofline": {
-            "kernel": dom_name,
-            "bound": "hbm",
-            "achieved": round(achieved, 3),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6),
-            "traffic": traffic,
-            "alg_bytes_per_launch": round(alg.get(dom, 0.0)),
-            "avg_launch_us": round(avg_launch_s * 1e6, 3),
-            "launches": int(nl[dom]),
-        },
-        "pipeline_roofline": {
-            "alg_bytes_per_image": 7 * P + 60 * kp_per_img,  # B = 7P + 60N
-            "extract_ms_per_step": round(sum(ms_ for k, ms_ in stage_ms_per_step.items()
-                                             if k in ("pyr_level0", "pyr_resize", "fast", "octree", "describe")), 5),
-        },
-        "cpu_baseline": cpu,
-        "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count(),
-                 "hip": torch.version.hip},
-    }
-    pr = out["pipeline_roofline"]
-    if pr["extract_ms_per_step"] > 0:
-        gbs = 2 * pr["alg_bytes_per_image"] / (pr["extract_ms_per_step"] / 1e3) / 1e9
-        pr["achieved_GBs"] = round(gbs, 3)
-        pr["frac"] = round(gbs / HBM_PEAK_GBS, 6)
-    print(json.dumps(out), flush=True)
-    if dist:
         dist.destroy_process_group()
-
-
-def cpu_baseline(frames, cam, a):
-    """Oracle (C++ restatement of the reference path) on host cores: L/R extraction on two
-    threads (src/Frame.cc:78-81) + ComputeStereoMatches, over a bounded frame sample."""
-    from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle_ctypes as O
-    p = O.params(a.nfeatures)
-    pool = ThreadPoolExecutor(2)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        L, R = frames[n % len(frames)]
-        fl = pool.submit(O.extract, p, L)
-        fr = pool.submit(O.extract, p, R)
-        (kl, dl), (kr, dr) = fl.result(), fr.result()
-        O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= a.cpu_sample_s and n >= 3) or n >= 10000:
-            break
-    pool.shutdown()
-    return {"value": round(n / el, 4), "unit": "frames/s", "cores": 2, "kind": "port",
-            "sample": f"{n} KITTI-shaped stereo frames (same synthetic frames), oracle extract L||R "
-                      f"(2 threads) + stereo, {el:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -62,6 +62,8 @@ int orbmi_extract_batch_device(orbmi_extractor* h, const uint8_t* d_images, int 
                                int cols, size_t step, size_t image_stride, orbmi_keypoint* d_kps,
                                uint8_t* d_desc, int* d_counts, int capacity);
 int orbmi_extractor_synchronize(orbmi_extractor* h);
+/* The handle's HIP stream (hipStream_t), for callers that order their own work after it. */
+int orbmi_extractor_get_stream(orbmi_extractor* h, void** stream);
 
 /* Getters  include/ORBextractor.h:68-90. `out` holds nlevels floats. */
 int orbmi_extractor_get_levels(const orbmi_extractor* h);
@@ -115,6 +117,9 @@ typedef struct orbmi_frame_view {
     int nlevels;
     const float* scale_factors;    /* mvScaleFactors (host or device, nlevels)      */
     float log_scale_factor;        /* mfLogScaleFactor                              */
+    const int* n_device;           /* optional device count (e.g. the extractor's count
+                                      output): the frame then has min(*n_device, n) keypoints
+                                      and n is the capacity of keys_un/u_right/desc      */
 } orbmi_frame_view;
 
 /* MapPoint state read by Frame::isInFrustum (src/Frame.cc:274-342). flags: */
@@ -144,6 +149,10 @@ typedef struct orbmi_matcher orbmi_matcher;
  * 40); the handle holds a device, a stream and scratch buffers. */
 int orbmi_matcher_create(int device, orbmi_matcher** out);
 void orbmi_matcher_destroy(orbmi_matcher* m);
+/* Run the matcher on `ex`'s stream (the frame's keypoints/descriptors come from that
+ * extraction): calls are then ordered behind it without host synchronisation, and a call whose
+ * outputs are all device pointers with nmatches == NULL returns without waiting. */
+int orbmi_matcher_share_stream(orbmi_matcher* m, orbmi_extractor* ex);
 
 /* Frame::isInFrustum(pMP, viewingCosLimit) for n_mp points (src/Frame.cc:274-342) with
  * MapPoint::PredictScale (src/MapPoint.cc:421-436).  Points flagged BAD or SEEN are skipped
@@ -199,6 +208,19 @@ int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint
                         const orbmi_feature_vector* kf_fv, const orbmi_frame_view* F,
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches);
+
+/* Cross-stream matching of config 4 (build-defined; no reference counterpart, SURVEY.md §8(d)
+ * "Config 4"): brute-force Hamming nearest neighbour of each of the nq query descriptors over
+ * the nseg gathered train segments (segment s = rows [s*seg_capacity, s*seg_capacity +
+ * seg_counts[s]) of train_desc; segment skip_seg is ignored, -1 = none).  Accepted when
+ * best <= th and best < ratio * second best (second = 256 when absent); equal distances
+ * resolve to the lowest row.  match[q] = global train row or -1.  nq_device as in
+ * orbmi_frame_view.  Inputs host or device; asynchronous when all outputs are device memory and
+ * nmatches == NULL. */
+int orbmi_match_descriptors_segments(orbmi_matcher* m, const uint8_t* q_desc, int nq, const int* nq_device,
+                                     const uint8_t* train_desc, int nseg, int seg_capacity,
+                                     const int* seg_counts, int skip_seg, int th, float ratio,
+                                     int32_t* match, int* nmatches);
 
 /* ---- Optimizer::LocalBundleAdjustment ------------------------------------------------ */
 

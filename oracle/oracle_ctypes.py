@@ -236,3 +236,34 @@ def local_ba(problem, stop=False):
     n = len(problem.kfs), len(problem.pts), len(problem.edges)
     return {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
             "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+
+
+# ---- cross-stream matching (config 4; build-defined, no reference counterpart) -----------
+_POPC8 = np.array([bin(i).count("1") for i in range(256)], np.int32)
+
+
+def match_descriptors_segments(q_desc, train_desc, seg_counts, skip_seg=-1, th=50, ratio=0.6):
+    """Restatement of orbmi_match_descriptors_segments (include/orbmi.h): nearest train row
+    by Hamming distance over the valid rows of each segment (train_desc: nseg x cap x 32),
+    accepted when best <= th and best < ratio * second (second = 256 when absent); ties ->
+    lowest global row.  Returns match[q] (global row or -1)."""
+    q = np.asarray(q_desc, np.uint8).reshape(-1, 32)
+    t = np.asarray(train_desc, np.uint8)
+    nseg, cap = t.shape[0], t.shape[1]
+    valid = np.zeros(nseg * cap, bool)
+    for s in range(nseg):
+        if s != skip_seg:
+            valid[s * cap:s * cap + min(int(seg_counts[s]), cap)] = True
+    rows = np.nonzero(valid)[0]
+    tt = t.reshape(-1, 32)[rows]
+    out = np.full(len(q), -1, np.int32)
+    if len(rows) == 0:
+        return out
+    for i in range(len(q)):
+        d = _POPC8[np.bitwise_xor(tt, q[i])].sum(1)
+        o = np.lexsort((rows, d))
+        d1 = int(d[o[0]])
+        d2 = int(d[o[1]]) if len(o) > 1 else 256
+        if d1 <= th and float(d1) < np.float32(ratio) * np.float32(d2):
+            out[i] = rows[o[0]]
+    return out

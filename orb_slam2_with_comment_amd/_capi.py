@@ -59,6 +59,9 @@ _PROTOS = {
     "orbmi_compute_stereo_matches_batch_device": (_i, [_vp, _f, _f, _vp, _vp]),
     "orbmi_matcher_create": (_i, [_i, C.POINTER(_vp)]),
     "orbmi_matcher_destroy": (None, [_vp]),
+    "orbmi_matcher_share_stream": (_i, [_vp, _vp]),
+    "orbmi_match_descriptors_segments": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _i, _i, _f, _vp, _vp]),
+    "orbmi_extractor_get_stream": (_i, [_vp, C.POINTER(_vp)]),
     "orbmi_is_in_frustum": (_i, [_vp, _vp, _vp, _i, _f, _vp]),
     "orbmi_search_by_projection_local": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _f, _f, _vp, C.POINTER(_i)]),
     "orbmi_search_local_points": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, C.POINTER(_i), C.POINTER(_i)]),

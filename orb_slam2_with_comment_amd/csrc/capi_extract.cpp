@@ -16,7 +16,15 @@ int stereo_run(Extractor& L, int itemL, Extractor& R, int itemR, float bf, float
                float* d_depth, int n_left_cap);
 }
 
+hipStream_t orbmi_extractor_stream_(orbmi_extractor* ex) { return ex ? ex->ex.stream : nullptr; }
+
 extern "C" {
+
+int orbmi_extractor_get_stream(orbmi_extractor* h, void** stream) {
+    if (!h || !stream) return ORBMI_E_ARG;
+    *stream = (void*)h->ex.stream;
+    return ORBMI_OK;
+}
 
 int orbmi_extractor_create(int device, int nfeatures, float scale_factor, int nlevels,
                            int ini_th_fast, int min_th_fast, orbmi_extractor** out) {

@@ -14,6 +14,8 @@ struct orbmi_matcher {
     Matcher m;
 };
 
+hipStream_t orbmi_extractor_stream_(orbmi_extractor* ex);  // capi_extract.cpp
+
 namespace orbmi {
 
 void* Matcher::stage(size_t bytes) {
@@ -28,17 +30,22 @@ void* Matcher::stage(size_t bytes) {
 }
 
 void Matcher::arena_reset() {
+    // a previous asynchronous call may still read staged inputs: order behind it
+    bool used = false;
+    for (Block& b : arena) used |= b.used > 0;
+    if (used) (void)hipStreamSynchronize(stream);
     for (Block& b : arena) b.used = 0;
 }
 
 void Matcher::release() {
     (void)hipSetDevice(device);
-    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_res, d_bin_of, d_hist, d_scalars};
+    if (own_stream && stream) (void)hipStreamSynchronize(stream);
+    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_res, d_bin_of, d_hist, d_scalars, d_track};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (Block& b : arena) (void)hipFree(b.p);
     arena.clear();
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream && own_stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
 }
 
@@ -83,14 +90,17 @@ T* dev_out(Matcher& m, T* p, size_t n, std::vector<OutBuf>& outs) {
     return d;
 }
 
+// Copy host-bound outputs back and synchronise; fully device-resident calls (every output a
+// device pointer, counts not requested) return without waiting.
 int finish(Matcher& m, std::vector<OutBuf>& outs, int* nmatches_dev, int* nmatches, int* extra_dev = nullptr,
            int* extra = nullptr) {
+    bool wait = false;
     for (OutBuf& o : outs)
-        if (o.bytes) ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream));
+        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
     int tmp[2] = {0, 0};
-    if (nmatches_dev) ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream));
-    if (extra_dev) ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream));
-    ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (nmatches && nmatches_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
+    if (extra && extra_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
     if (nmatches) *nmatches = tmp[0];
     if (extra) *extra = tmp[1];
     return ORBMI_OK;
@@ -111,6 +121,8 @@ int make_frame(Matcher& m, const orbmi_frame_view* v, DevFrame* F, bool need_pos
     int rc = 0;
     memset(F, 0, sizeof(*F));
     F->n = v->n;
+    F->n_dev = v->n_device;
+    if (F->n_dev && !on_device(F->n_dev)) return ORBMI_E_ARG;
     F->keys = dev_in(m, v->keys_un, (size_t)v->n, &rc);
     F->u_right = dev_in(m, v->u_right, v->u_right ? (size_t)v->n : 0, &rc);
     F->desc = dev_in(m, v->desc, (size_t)v->n * 32, &rc);
@@ -173,6 +185,19 @@ int orbmi_matcher_create(int device, orbmi_matcher** out) {
     return ORBMI_OK;
 }
 
+int orbmi_matcher_share_stream(orbmi_matcher* h, orbmi_extractor* ex) {
+    if (!h || !ex) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    hipStream_t s = orbmi_extractor_stream_(ex);
+    if (!s) return ORBMI_E_STATE;
+    ORBMI_HIP(hipSetDevice(m.device));
+    ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (m.own_stream) ORBMI_HIP(hipStreamDestroy(m.stream));
+    m.stream = s;
+    m.own_stream = false;
+    return ORBMI_OK;
+}
+
 void orbmi_matcher_destroy(orbmi_matcher* h) {
     if (!h) return;
     h->m.release();
@@ -200,7 +225,7 @@ int orbmi_is_in_frustum(orbmi_matcher* h, const orbmi_frame_view* v, const orbmi
 int orbmi_search_by_projection_local(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
                                      const orbmi_mappoint* mps, const orbmi_mappoint_track* track, int n_mp,
                                      float th, float nnratio, int32_t* match_mp, int* nmatches) {
-    if (!h || !occupied || !match_mp || !nmatches || n_mp < 0 || (n_mp > 0 && (!mps || !track))) return ORBMI_E_ARG;
+    if (!h || !occupied || !match_mp || n_mp < 0 || (n_mp > 0 && (!mps || !track))) return ORBMI_E_ARG;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
@@ -222,7 +247,7 @@ int orbmi_search_by_projection_local(orbmi_matcher* h, const orbmi_frame_view* v
 int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
                               const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp, int* nmatches,
                               int* n_to_match) {
-    if (!h || !occupied || !match_mp || !nmatches || n_mp < 0 || (n_mp > 0 && !mps)) return ORBMI_E_ARG;
+    if (!h || !occupied || !match_mp || n_mp < 0 || (n_mp > 0 && !mps)) return ORBMI_E_ARG;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
@@ -233,7 +258,8 @@ int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const
     const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
     if (rc) return rc;
     if ((rc = scalars(m))) return rc;
-    orbmi_mappoint_track* d_tr = (orbmi_mappoint_track*)m.stage((size_t)std::max(n_mp, 1) * sizeof(orbmi_mappoint_track));
+    if ((rc = orbmi::ensure_buf(&m.d_track, &m.cap_track, (size_t)std::max(n_mp, 1)))) return rc;
+    orbmi_mappoint_track* d_tr = m.d_track;
     std::vector<OutBuf> outs;
     int* d_out = dev_out(m, match_mp, (size_t)F.n, outs);
     // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5); ORBmatcher matcher(0.8)
@@ -249,7 +275,7 @@ int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const
 int orbmi_search_by_projection_last_frame(orbmi_matcher* h, const orbmi_frame_view* cf, const uint8_t* occupied,
                                           const orbmi_frame_view* lf, const orbmi_lastframe_point* lf_points,
                                           float th, int mono, int check_ori, int32_t* match_lf, int* nmatches) {
-    if (!h || !occupied || !match_lf || !nmatches || !lf || (lf->n > 0 && !lf_points)) return ORBMI_E_ARG;
+    if (!h || !occupied || !match_lf || !lf || (lf->n > 0 && !lf_points)) return ORBMI_E_ARG;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
@@ -273,7 +299,7 @@ int orbmi_search_by_bow(orbmi_matcher* h, const orbmi_frame_view* kf, const uint
                         const orbmi_feature_vector* kf_fv, const orbmi_frame_view* f,
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches) {
-    if (!h || !kf_mp_ok || !match_kf || !nmatches) return ORBMI_E_ARG;
+    if (!h || !kf_mp_ok || !match_kf) return ORBMI_E_ARG;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
@@ -290,6 +316,32 @@ int orbmi_search_by_bow(orbmi_matcher* h, const orbmi_frame_view* kf, const uint
     std::vector<OutBuf> outs;
     int* d_out = dev_out(m, match_kf, (size_t)F.n, outs);
     if ((rc = orbmi::launch_bow(m, KF, d_ok, kfv, F, fv, nnratio, check_ori, d_out, m.d_scalars))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, m.d_scalars, nmatches);
+}
+
+int orbmi_match_descriptors_segments(orbmi_matcher* h, const uint8_t* q_desc, int nq, const int* nq_device,
+                                     const uint8_t* train_desc, int nseg, int seg_capacity, const int* seg_counts,
+                                     int skip_seg, int th, float ratio, int32_t* match, int* nmatches) {
+    if (!h || nq < 0 || nseg < 0 || seg_capacity < 0 || (nq > 0 && (!q_desc || !match))) return ORBMI_E_ARG;
+    if ((long long)nseg * seg_capacity > 0xFFFFFFFLL) return ORBMI_E_UNSUPPORTED;
+    if (nseg * seg_capacity > 0 && (!train_desc || !seg_counts)) return ORBMI_E_ARG;
+    if (nq_device && !on_device(nq_device)) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    int rc = 0;
+    const uint8_t* d_q = dev_in(m, q_desc, (size_t)nq * 32, &rc);
+    const uint8_t* d_t = dev_in(m, train_desc, (size_t)nseg * seg_capacity * 32, &rc);
+    const int* d_cnt = dev_in(m, seg_counts, (size_t)nseg, &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match, (size_t)nq, outs);
+    if (nseg * seg_capacity == 0 && nq > 0) ORBMI_HIP(hipMemsetAsync(d_out, 0xFF, (size_t)nq * sizeof(int), m.stream));
+    else if ((rc = orbmi::launch_xmatch(m, d_q, nq, nq_device, d_t, nseg, seg_capacity, d_cnt, skip_seg, th, ratio,
+                                        d_out, m.d_scalars)))
+        return rc;
     ORBMI_HIP(hipGetLastError());
     return finish(m, outs, m.d_scalars, nmatches);
 }

@@ -1,21 +1,28 @@
 // Optimizer::LocalBundleAdjustment (src/Optimizer.cc:483-808) on MI355X, fp64.
 //
-// One persistent workgroup (1024 threads) runs the whole g2o schedule -- optimize(5), outlier
-// levels, optimize(10), erase list -- with every Levenberg trial on the device and no host
-// round trip (g2o/core/optimization_algorithm_levenberg.cpp:61-164):
-//   errors        thread per edge   EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::computeError
-//   linearise     thread per point  Hll, bl, Hpl blocks (constructQuadraticForm, Huber weights)
-//                 wave per pose     Hpp, bp (wave reduction over the pose's observations)
-//   Schur         thread per point  D^-1, b_schur -= B D^-1 b_l, H_schur -= B_i D^-1 B_j^T
-//                                   accumulated with ds_add_f64 into a packed upper-triangular
-//                                   reduced camera system held in LDS
-//   solve         block             dense LDL^T of the 6K x 6K system in LDS (K <= 30 poses)
-//   update        thread per point/pose  x_l = D^-1 (b_l - B^T x_p); SE3 exp/oplus
+// The g2o schedule -- optimize(5), outlier levels, optimize(10), erase list -- runs as a chain
+// of chip-wide kernels on one stream; the Levenberg control (g2o/core/
+// optimization_algorithm_levenberg.cpp:61-164) stays on the host, which reads four scalars per
+// trial (chi2, scale, solve status) and launches the next trial.  Per LM iteration:
+//   k_ba_errors        thread / edge   computeActiveErrors + robust chi2 (per-block partials)
+//   k_ba_linearize     thread / edge   Jacobians (types_six_dof_expmap.cpp), Huber weights,
+//                                      per-edge Hpl block and its Hll / Hpp / b contributions
+//   k_ba_points        thread / point  Hll, b_l (sum over the point's edges, g2o order)
+//   k_ba_poses         block / pose    Hpp, b_p (fixed-order reduction over the pose's edges)
+// per trial (lambda):
+//   k_ba_point_schur   thread / edge   D = Hll + lambda I, D^-1, B D^-1 and B D^-1 b_l per edge
+//   k_ba_schur_blocks  block / (pose i <= pose j)  H_schur(i,j) = Hpp - sum_points B_i D^-1 B_j^T,
+//                                      b_schur(i) = b_p - sum B_i D^-1 b_l (pair lists built once)
+//   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system in LDS
+//   k_ba_update        thread / point, pose   back substitution, x + dx, exp(dx) * T, scale
+//   k_ba_errors        on the trial state, then k_ba_scalars reduces the partials
 // The g2o semantics kept: lambda init tau = 1e-5, rho test with computeScale + 1e-3, the
 // ORB-SLAM "3 bad iterations" stop, stale edge errors after a rejected trial, push/pop of
-// the estimates, Huber kernels removed for the second pass.  Parity with the oracle: 1e-4.
+// the estimates (pointer swap of current / trial buffers), Huber kernels removed for the
+// second pass.  Every reduction has a fixed order (deterministic).  Parity with the oracle: 1e-4.
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 #include <new>
 #include <vector>
 
@@ -23,45 +30,45 @@
 
 namespace orbmi {
 
-constexpr int kBaThreads = 1024;
 constexpr int kBaMaxPoses = 30;                        // 6*30 = 180 unknowns
 constexpr int kBaMaxN = 6 * kBaMaxPoses;
 constexpr int kBaPacked = kBaMaxN * (kBaMaxN + 1) / 2;  // 16290 doubles = 127 KiB
+constexpr int kBaMaxKf = 1024;
+constexpr int kBaBlock = 256;
+constexpr int kBaSolveThreads = 256;
 
-struct BaArgs {
-    int nkf, npt, nedge;
-    // inputs
+struct BaDev {
+    int nkf, npt, nedge, nblk;
     const orbmi_ba_keyframe* kfs;
     const orbmi_ba_point* pts;
     const orbmi_ba_edge* edges;
     const int* kf_order;       // keyframe indices sorted by id (vertex order)
-    const int* pt_start;       // edges of point p: [pt_start[p], pt_start[p+1])  (edges grouped by point)
+    const int* pt_start;       // edges of point p: [pt_start[p], pt_start[p+1])
     const int* kf_start;       // CSR by keyframe over edge indices
     const int* kf_edges;
-    const volatile int* stop;  // host-mapped abort flag or nullptr
-    // state
-    double* T;                 // nkf x 8 : qx qy qz qw tx ty tz -
-    double* Tt;                // trial
-    double* X;                 // npt x 4
-    double* Xt;
+    const int* blk_kf;         // nblk x 2: keyframes (a, b), id(a) <= id(b), both not fixed
+    const int* blk_start;      // nblk + 1
+    const int2* blk_pairs;     // (e_a, e_b): edges of one point into keyframes a and b
     double* err;               // nedge x 3 (stale semantics)
     unsigned char* eflag;      // bit0 level-1, bit1 no robust kernel, bit2 active
     int* pose_idx;             // nkf
     int* pose_kf;              // kBaMaxPoses
     double* Hpl;               // nedge x 18 (pose rows x point cols)
+    double* Hle;               // nedge x 9: edge's Hll upper (6) + b_l (3)
+    double* Hpe;               // nedge x 27: edge's Hpp upper (21) + b_p (6)
     double* Hll;               // npt x 9
     double* bl;                // npt x 3
     double* Dinv;              // npt x 9
+    double* BD;                // nedge x 18: B D^-1
+    double* Bdb;               // nedge x 6: B D^-1 b_l
     double* Hpp;               // kBaMaxPoses x 36
     double* bp;                // kBaMaxPoses x 6
+    double* S;                 // packed upper reduced system (kBaPacked)
+    double* bs;                // kBaMaxN
     double* xp;                // kBaMaxN
-    double* xl;                // npt x 3
-    // outputs
-    float* out_tcw;
-    float* out_pos;
-    unsigned char* out_erase;
-    int* out_stats;            // [0..1] iterations, [2] aborted, [3] error
-    double* out_chi2;          // [0..1]
+    double* part;              // per-block partial sums
+    double* scal;              // scalars read by the host
+    int* istat;                // [0] np, [1] nl, [2] too many poses, [3] solve ok
 };
 
 // ---------------------------------------------------------------- SE3Quat helpers (fp64)
@@ -164,7 +171,7 @@ __device__ inline void se3_oplus(const double* u, const double* Tin, double* Tou
 // ---------------------------------------------------------------- edges
 __device__ inline bool edge_stereo(const orbmi_ba_edge& e) { return !(e.ur < 0); }
 
-__device__ inline void edge_error(const BaArgs& a, int i, const double* T, const double* X, double* err) {
+__device__ inline void edge_error(const BaDev& a, int i, const double* T, const double* X, double* err) {
     const orbmi_ba_edge e = a.edges[i];
     const orbmi_ba_keyframe& kf = a.kfs[e.kf];
     double p[3];
@@ -185,7 +192,7 @@ __device__ inline void edge_error(const BaArgs& a, int i, const double* T, const
     }
 }
 
-__device__ inline double edge_chi2(const BaArgs& a, int i) {
+__device__ inline double edge_chi2(const BaDev& a, int i) {
     const double* r = a.err + 3 * i;
     const double info = (double)a.edges[i].inv_sigma2;
     return r[0] * (info * r[0]) + r[1] * (info * r[1]) + (edge_stereo(a.edges[i]) ? r[2] * (info * r[2]) : 0.0);
@@ -198,7 +205,7 @@ __device__ inline double huber_delta(const orbmi_ba_edge& e) {
 }
 
 // robustified chi2 and weight rho' (RobustKernelHuber::robustify)
-__device__ inline void edge_robust(const BaArgs& a, int i, double c, double* rho0, double* rho1) {
+__device__ inline void edge_robust(const BaDev& a, int i, double c, double* rho0, double* rho1) {
     if (a.eflag[i] & 2) { *rho0 = c; *rho1 = 1.0; return; }
     const double d = huber_delta(a.edges[i]), dsqr = d * d;
     if (c <= dsqr) { *rho0 = c; *rho1 = 1.0; }
@@ -206,7 +213,7 @@ __device__ inline void edge_robust(const BaArgs& a, int i, double c, double* rho
 }
 
 // Jacobians (types_six_dof_expmap.cpp:103-134, :188-234)
-__device__ inline void edge_jacobians(const BaArgs& a, int i, const double* T, const double* X, double Jl[3][3],
+__device__ inline void edge_jacobians(const BaDev& a, int i, const double* T, const double* X, double Jl[3][3],
                                       double Jp[3][6]) {
     const orbmi_ba_edge e = a.edges[i];
     const orbmi_ba_keyframe& kf = a.kfs[e.kf];
@@ -243,7 +250,7 @@ __device__ inline void edge_jacobians(const BaArgs& a, int i, const double* T, c
 }
 
 // weight W = rho' * info and omega_r = -info * e * rho' (constructQuadraticForm)
-__device__ inline void edge_weights(const BaArgs& a, int i, double* w, double om[3]) {
+__device__ inline void edge_weights(const BaDev& a, int i, double* w, double om[3]) {
     const double info = (double)a.edges[i].inv_sigma2;
     double r0, r1;
     edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
@@ -254,481 +261,627 @@ __device__ inline void edge_weights(const BaArgs& a, int i, double* w, double om
 }
 
 // ---------------------------------------------------------------- block helpers
-constexpr int kBaMaxKf = 1024;
-
-struct BaShared {
-    double H[kBaPacked];       // packed upper-triangular reduced camera system
-    double bs[kBaMaxN];
-    int kfact[kBaMaxKf];       // keyframe has an active edge
-    double red[kBaThreads / 64];
-    double dstate[8];          // lambda, ni, currentChi, tempChi, scale, rho, iniChi
-    int istate[16];
-};
-
-__device__ inline double block_sum(double v, BaShared& S) {
+template <int NT>
+__device__ inline double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) S.red[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = 0;
-    for (int w = 0; w < kBaThreads / 64; w++) t += S.red[w];
+    for (int w = 0; w < NT / 64; w++) t += red[w];
     __syncthreads();
     return t;
 }
 
-__device__ inline double block_max(double v, BaShared& S) {
+template <int NT>
+__device__ inline double block_max(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) S.red[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = 0;
-    for (int w = 0; w < kBaThreads / 64; w++) t = fmax(t, S.red[w]);
+    for (int w = 0; w < NT / 64; w++) t = fmax(t, red[w]);
     __syncthreads();
     return t;
 }
 
 __device__ inline int packed(int r, int c, int N) { return r * N - r * (r - 1) / 2 + (c - r); }  // r <= c
 
-__device__ inline bool stop_requested(const BaArgs& a) {
-    return a.stop && __hip_atomic_load((int*)a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+__device__ inline bool point_active(const BaDev& a, int p) {
+    for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++)
+        if (a.eflag[i] & 4) return true;
+    return false;
 }
 
-// ---------------------------------------------------------------- the optimiser
-struct Lba {
-    const BaArgs& a;
-    BaShared& S;
-    int np = 0, N = 0, nl = 0;
-
-    __device__ Lba(const BaArgs& aa, BaShared& ss) : a(aa), S(ss) {}
-
-    // SparseOptimizer::initializeOptimization(level 0) + buildIndexMapping
-    __device__ void initialize() {
-        const int tid = threadIdx.x;
-        for (int k = tid; k < a.nkf; k += kBaThreads) S.kfact[k] = 0;
-        if (tid == 0) S.istate[3] = 0;
-        __syncthreads();
-        for (int i = tid; i < a.nedge; i += kBaThreads) {
-            unsigned char f = a.eflag[i] & 3;
-            if (!(f & 1)) { f |= 4; S.kfact[a.edges[i].kf] = 1; }  // active at level 0
-            a.eflag[i] = f;
-        }
-        __syncthreads();
-        int nlp = 0;
-        for (int p = tid; p < a.npt; p += kBaThreads) nlp += point_active(p);
-        if (nlp) atomicAdd(&S.istate[3], nlp);
-        if (tid == 0) {
-            int n = 0;
-            for (int oi = 0; oi < a.nkf; oi++) {
-                const int k = a.kf_order[oi];
-                a.pose_idx[k] = -1;
-                if (a.kfs[k].fixed || !S.kfact[k]) continue;
-                if (n < kBaMaxPoses) a.pose_kf[n] = k;
-                a.pose_idx[k] = n < kBaMaxPoses ? n : -1;
-                n++;
-            }
-            S.istate[0] = n;
-            if (n > kBaMaxPoses) S.istate[1] = 1;  // unsupported size
-        }
-        __syncthreads();
-        np = min(S.istate[0], kBaMaxPoses);
-        N = 6 * np;
-        nl = S.istate[3];
-    }
-
-    __device__ bool point_active(int p) const {
-        for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++)
-            if (a.eflag[i] & 4) return true;
-        return false;
-    }
-
-    // computeActiveErrors on (T, X) + activeRobustChi2
-    __device__ double errors(const double* T, const double* X) {
-        double s = 0;
-        for (int i = threadIdx.x; i < a.nedge; i += kBaThreads) {
-            if (!(a.eflag[i] & 4)) continue;
-            edge_error(a, i, T, X, a.err + 3 * i);
-            double r0, r1;
-            edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
-            s += r0;
-        }
-        return block_sum(s, S);
-    }
-
-    __device__ double robust_chi2() {
-        double s = 0;
-        for (int i = threadIdx.x; i < a.nedge; i += kBaThreads) {
-            if (!(a.eflag[i] & 4)) continue;
-            double r0, r1;
-            edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
-            s += r0;
-        }
-        return block_sum(s, S);
-    }
-
-    // BlockSolver::buildSystem
-    __device__ void build_system() {
-        const int tid = threadIdx.x;
-        for (int p = tid; p < a.npt; p += kBaThreads) {
-            double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-            for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++) {
-                if (!(a.eflag[i] & 4)) continue;
-                double Jl[3][3], Jp[3][6], w, om[3];
-                edge_jacobians(a, i, a.T, a.X, Jl, Jp);
-                edge_weights(a, i, &w, om);
-                for (int r = 0; r < 3; r++) {
-                    b[r] += Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
-                    for (int c = 0; c < 3; c++) H[r * 3 + c] += Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
-                }
-                if (a.pose_idx[a.edges[i].kf] >= 0) {
-                    double* B = a.Hpl + 18 * (long long)i;
-                    for (int r = 0; r < 6; r++)
-                        for (int c = 0; c < 3; c++) B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
-                }
-            }
-            for (int k = 0; k < 9; k++) a.Hll[9 * p + k] = H[k];
-            for (int k = 0; k < 3; k++) a.bl[3 * p + k] = b[k];
-        }
-        // poses: one wave each, lanes stride over the pose's observations
-        const int wid = tid >> 6, lane = tid & 63;
-        for (int pi = wid; pi < np; pi += kBaThreads / 64) {
-            const int k = a.pose_kf[pi];
-            double H[21], b[6];
-            for (int q = 0; q < 21; q++) H[q] = 0;
-            for (int q = 0; q < 6; q++) b[q] = 0;
-            for (int j = a.kf_start[k] + lane; j < a.kf_start[k + 1]; j += 64) {
-                const int i = a.kf_edges[j];
-                if (!(a.eflag[i] & 4)) continue;
-                double Jl[3][3], Jp[3][6], w, om[3];
-                edge_jacobians(a, i, a.T, a.X, Jl, Jp);
-                edge_weights(a, i, &w, om);
-                int q = 0;
-                for (int r = 0; r < 6; r++) {
-                    b[r] += Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
-                    for (int c = r; c < 6; c++, q++) H[q] += Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
-                }
-            }
-            for (int q = 0; q < 21; q++)
-                for (int o = 32; o > 0; o >>= 1) H[q] += __shfl_xor(H[q], o, 64);
-            for (int q = 0; q < 6; q++)
-                for (int o = 32; o > 0; o >>= 1) b[q] += __shfl_xor(b[q], o, 64);
-            if (lane == 0) {
-                int q = 0;
-                for (int r = 0; r < 6; r++)
-                    for (int c = r; c < 6; c++, q++) { a.Hpp[36 * pi + r * 6 + c] = H[q]; a.Hpp[36 * pi + c * 6 + r] = H[q]; }
-                for (int r = 0; r < 6; r++) a.bp[6 * pi + r] = b[r];
-            }
-        }
-        __syncthreads();
-    }
-
-    __device__ double lambda_init() {
-        double m = 0;
-        for (int q = threadIdx.x; q < np * 6; q += kBaThreads) m = fmax(m, fabs(a.Hpp[36 * (q / 6) + (q % 6) * 7]));
-        for (int p = threadIdx.x; p < a.npt; p += kBaThreads)
-            if (point_active(p))
-                for (int j = 0; j < 3; j++) m = fmax(m, fabs(a.Hll[9 * p + 4 * j]));
-        return 1e-5 * block_max(m, S);
-    }
-
-    // BlockSolver::setLambda + solve (Schur complement, reduced system, back substitution)
-    __device__ bool solve(double lam) {
-        const int tid = threadIdx.x;
-        const int NP = N * (N + 1) / 2;
-        for (int q = tid; q < NP; q += kBaThreads) S.H[q] = 0;
-        __syncthreads();
-        for (int q = tid; q < np * 36; q += kBaThreads) {
-            const int pi = q / 36, r = (q % 36) / 6, c = q % 6;
-            if (c < r) continue;
-            S.H[packed(6 * pi + r, 6 * pi + c, N)] = a.Hpp[q] + (r == c ? lam : 0.0);
-        }
-        for (int q = tid; q < N; q += kBaThreads) S.bs[q] = a.bp[q];
-        __syncthreads();
-        for (int p = tid; p < a.npt; p += kBaThreads) {
-            if (!point_active(p)) continue;
-            double D[3][3];
-            for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 3; c++) D[r][c] = a.Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
-            const double c00 = D[1][1] * D[2][2] - D[1][2] * D[2][1];
-            const double c10 = D[1][2] * D[2][0] - D[1][0] * D[2][2];
-            const double c20 = D[1][0] * D[2][1] - D[1][1] * D[2][0];
-            const double det = D[0][0] * c00 + D[0][1] * c10 + D[0][2] * c20;
-            double Di[9];
-            Di[0] = c00 / det; Di[3] = c10 / det; Di[6] = c20 / det;
-            Di[1] = (D[0][2] * D[2][1] - D[0][1] * D[2][2]) / det;
-            Di[4] = (D[0][0] * D[2][2] - D[0][2] * D[2][0]) / det;
-            Di[7] = (D[0][1] * D[2][0] - D[0][0] * D[2][1]) / det;
-            Di[2] = (D[0][1] * D[1][2] - D[0][2] * D[1][1]) / det;
-            Di[5] = (D[0][2] * D[1][0] - D[0][0] * D[1][2]) / det;
-            Di[8] = (D[0][0] * D[1][1] - D[0][1] * D[1][0]) / det;
-            for (int k = 0; k < 9; k++) a.Dinv[9 * p + k] = Di[k];
-            const double* blp = a.bl + 3 * p;
-            double db[3];
-            for (int r = 0; r < 3; r++) db[r] = Di[r * 3] * blp[0] + Di[r * 3 + 1] * blp[1] + Di[r * 3 + 2] * blp[2];
-            for (int e1 = a.pt_start[p]; e1 < a.pt_start[p + 1]; e1++) {
-                if (!(a.eflag[e1] & 4)) continue;
-                const int i1 = a.pose_idx[a.edges[e1].kf];
-                if (i1 < 0) continue;
-                const double* B1 = a.Hpl + 18 * (long long)e1;
-                double BD[6][3];
-                for (int r = 0; r < 6; r++) {
-                    for (int c = 0; c < 3; c++) BD[r][c] = B1[r * 3] * Di[c] + B1[r * 3 + 1] * Di[3 + c] + B1[r * 3 + 2] * Di[6 + c];
-                    atomicAdd(&S.bs[6 * i1 + r], -(B1[r * 3] * db[0] + B1[r * 3 + 1] * db[1] + B1[r * 3 + 2] * db[2]));
-                }
-                for (int e2 = a.pt_start[p]; e2 < a.pt_start[p + 1]; e2++) {
-                    if (!(a.eflag[e2] & 4)) continue;
-                    const int i2 = a.pose_idx[a.edges[e2].kf];
-                    if (i2 < i1) continue;
-                    const double* B2 = a.Hpl + 18 * (long long)e2;
-                    for (int r = 0; r < 6; r++)
-                        for (int c = (i1 == i2 ? r : 0); c < 6; c++)
-                            atomicAdd(&S.H[packed(6 * i1 + r, 6 * i2 + c, N)],
-                                      -(BD[r][0] * B2[c * 3] + BD[r][1] * B2[c * 3 + 1] + BD[r][2] * B2[c * 3 + 2]));
-                }
-            }
-        }
-        __syncthreads();
-        // LDL^T = U^T D U on the packed upper triangle (right-looking)
-        bool ok = true;
-        for (int j = 0; j < N; j++) {
-            const double d = S.H[packed(j, j, N)];
-            if (!(fabs(d) > 0) || !isfinite(d)) { ok = false; break; }
-            // trailing update: wave per row, lanes across the row's upper part
-            for (int rr = j + 1 + (tid >> 6); rr < N; rr += kBaThreads / 64) {
-                const double ujr = S.H[packed(j, rr, N)];
-                for (int cc = rr + (tid & 63); cc < N; cc += 64)
-                    S.H[packed(rr, cc, N)] -= ujr * S.H[packed(j, cc, N)] / d;
-            }
-            __syncthreads();
-            for (int c = j + 1 + tid; c < N; c += kBaThreads) S.H[packed(j, c, N)] /= d;
-            __syncthreads();
-        }
-        if (!ok) return false;
-        // U^T z = b ; y = z / D ; U x = y
-        for (int k = 0; k < N; k++) {
-            const double zk = S.bs[k];
-            for (int jj = k + 1 + tid; jj < N; jj += kBaThreads) S.bs[jj] -= S.H[packed(k, jj, N)] * zk;
-            __syncthreads();
-        }
-        for (int k = tid; k < N; k += kBaThreads) S.bs[k] /= S.H[packed(k, k, N)];
-        __syncthreads();
-        for (int k = N - 1; k >= 0; k--) {
-            const double xk = S.bs[k];
-            for (int jj = tid; jj < k; jj += kBaThreads) S.bs[jj] -= S.H[packed(jj, k, N)] * xk;
-            __syncthreads();
-        }
-        for (int k = tid; k < N; k += kBaThreads) a.xp[k] = S.bs[k];
-        __syncthreads();
-        // landmarks: x_l = D^-1 (b_l - Hpl^T x_p)
-        for (int p = tid; p < a.npt; p += kBaThreads) {
-            double cl[3] = {a.bl[3 * p], a.bl[3 * p + 1], a.bl[3 * p + 2]};
-            const bool act = point_active(p);
-            if (act) {
-                for (int e1 = a.pt_start[p]; e1 < a.pt_start[p + 1]; e1++) {
-                    if (!(a.eflag[e1] & 4)) continue;
-                    const int i1 = a.pose_idx[a.edges[e1].kf];
-                    if (i1 < 0) continue;
-                    const double* B = a.Hpl + 18 * (long long)e1;
-                    for (int c = 0; c < 3; c++)
-                        for (int r = 0; r < 6; r++) cl[c] -= B[r * 3 + c] * a.xp[6 * i1 + r];
-                }
-            }
-            const double* Di = a.Dinv + 9 * p;
-            for (int r = 0; r < 3; r++)
-                a.xl[3 * p + r] = act ? Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1] + Di[r * 3 + 2] * cl[2] : 0.0;
-        }
-        __syncthreads();
-        return true;
-    }
-
-    // SparseOptimizer::update into the trial buffers; returns computeScale()
-    __device__ double update(double lam) {
-        const int tid = threadIdx.x;
-        double s = 0;
-        for (int p = tid; p < a.npt; p += kBaThreads) {
-            for (int r = 0; r < 3; r++) {
-                const double x = a.xl[3 * p + r];
-                a.Xt[4 * p + r] = a.X[4 * p + r] + x;
-                s += x * (lam * x + a.bl[3 * p + r]);
-            }
-        }
-        for (int k = tid; k < a.nkf; k += kBaThreads) {
-            const int pi = a.pose_idx[k];
-            if (pi >= 0) se3_oplus(a.xp + 6 * pi, a.T + 8 * k, a.Tt + 8 * k);
-            else for (int q = 0; q < 8; q++) a.Tt[8 * k + q] = a.T[8 * k + q];
-        }
-        for (int q = tid; q < N; q += kBaThreads) s += a.xp[q] * (lam * a.xp[q] + a.bp[q]);
-        return block_sum(s, S);
-    }
-
-    __device__ void accept() {
-        for (int p = threadIdx.x; p < a.npt; p += kBaThreads)
-            for (int r = 0; r < 3; r++) a.X[4 * p + r] = a.Xt[4 * p + r];
-        for (int q = threadIdx.x; q < 8 * a.nkf; q += kBaThreads) a.T[q] = a.Tt[q];
-        __syncthreads();
-    }
-
-    // OptimizationAlgorithmLevenberg::solve ; returns 0 = OK, 1 = Terminate
-    __device__ int lm_iteration(int iteration) {
-        double currentChi = errors(a.T, a.X);
-        const double iniChi = currentChi;
-        build_system();
-        if (iteration == 0) {
-            const double l0 = lambda_init();
-            if (threadIdx.x == 0) { S.dstate[0] = l0; S.dstate[1] = 2; S.istate[2] = 0; }
-            __syncthreads();
-        }
-        double rho = 0;
-        int qmax = 0;
-        do {
-            const double lam = S.dstate[0];
-            const bool ok2 = solve(lam);
-            double scale;
-            if (ok2) scale = update(lam);
-            else {
-                for (int q = threadIdx.x; q < 8 * a.nkf; q += kBaThreads) a.Tt[q] = a.T[q];
-                for (int q = threadIdx.x; q < 4 * a.npt; q += kBaThreads) a.Xt[q] = a.X[q];
-                __syncthreads();
-                scale = 0;
-            }
-            double tempChi = errors(a.Tt, a.Xt);
-            if (!ok2) tempChi = DBL_MAX;
-            rho = (currentChi - tempChi) / (scale + 1e-3);
-            const bool good = rho > 0 && isfinite(tempChi);
-            if (good) {
-                double alpha = 1. - pow((2 * rho - 1), 3);
-                alpha = fmin(alpha, 2. / 3.);
-                const double sf = fmax(1. / 3., alpha);
-                currentChi = tempChi;
-                __syncthreads();
-                if (threadIdx.x == 0) { S.dstate[0] = lam * sf; S.dstate[1] = 2; }
-                accept();
-            } else {
-                __syncthreads();
-                if (threadIdx.x == 0) { S.dstate[0] = lam * S.dstate[1]; S.dstate[1] *= 2; }
-                __syncthreads();
-            }
-            qmax++;
-        } while (rho < 0 && qmax < 10 && !stop_requested(a));
-        if (qmax == 10 || rho == 0) return 1;
-        int nBad = S.istate[2];
-        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-        else nBad = 0;
-        __syncthreads();
-        if (threadIdx.x == 0) S.istate[2] = nBad;
-        __syncthreads();
-        return nBad >= 3 ? 1 : 0;
-    }
-
-    __device__ int optimize(int iterations) {
-        if (np + nl == 0) return -1;  // SparseOptimizer::optimize with an empty index mapping
-        int it = 0;
-        for (int i = 0; i < iterations && !stop_requested(a); i++) {
-            const int r = lm_iteration(i);
-            ++it;
-            if (r != 0) break;
-        }
-        return it;
-    }
-};
-
-__global__ __launch_bounds__(kBaThreads) void k_local_ba(BaArgs a) {
-    __shared__ BaShared S;
-    const int tid = threadIdx.x;
-    if (tid < 16) S.istate[tid] = 0;
-    // vertices: SE3Quat from float Tcw (Converter::toSE3Quat), points to double
-    for (int k = tid; k < a.nkf; k += kBaThreads) {
-        const float* t = a.kfs[k].tcw;
+// ---------------------------------------------------------------- setup / activation
+// vertices: SE3Quat from float Tcw (Converter::toSE3Quat), points to double
+__global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restrict__ T, double* __restrict__ X,
+                                                       unsigned char* __restrict__ out_erase) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.nkf) {
+        const float* t = a.kfs[i].tcw;
         double R[3][3];
         for (int r = 0; r < 3; r++)
             for (int c = 0; c < 3; c++) R[r][c] = t[4 * r + c];
         Q q = q_from_matrix(R);
         q_normalize(q);
-        double* T = a.T + 8 * k;
-        T[0] = q.x; T[1] = q.y; T[2] = q.z; T[3] = q.w; T[4] = t[3]; T[5] = t[7]; T[6] = t[11]; T[7] = 0;
+        double* Ti = T + 8 * i;
+        Ti[0] = q.x; Ti[1] = q.y; Ti[2] = q.z; Ti[3] = q.w; Ti[4] = t[3]; Ti[5] = t[7]; Ti[6] = t[11]; Ti[7] = 0;
     }
-    for (int p = tid; p < a.npt; p += kBaThreads) {
-        for (int r = 0; r < 3; r++) a.X[4 * p + r] = a.pts[p].pos[r];
-        a.X[4 * p + 3] = 0;
+    if (i < a.npt) {
+        for (int r = 0; r < 3; r++) X[4 * i + r] = a.pts[i].pos[r];
+        X[4 * i + 3] = 0;
     }
-    for (int i = tid; i < a.nedge; i += kBaThreads) {
+    if (i < a.nedge) {
         a.eflag[i] = 0;
-        a.out_erase[i] = 0;
+        out_erase[i] = 0;
         a.err[3 * i] = a.err[3 * i + 1] = a.err[3 * i + 2] = 0;
-    }
-    __syncthreads();
-    Lba L(a, S);
-    L.initialize();
-    if (S.istate[1]) { if (tid == 0) a.out_stats[3] = ORBMI_E_UNSUPPORTED; return; }
-    int it0 = L.optimize(5);
-    const double chi0 = L.robust_chi2();
-    const bool more = !stop_requested(a);
-    int it1 = 0;
-    double chi1 = 0;
-    if (more) {
-        // outlier levels, kernels off (src/Optimizer.cc:701-732), stale errors
-        for (int i = tid; i < a.nedge; i += kBaThreads) {
-            const orbmi_ba_edge e = a.edges[i];
-            if (a.pts[e.point].bad) continue;
-            double p[3];
-            se3_map(a.T + 8 * e.kf, a.X + 4 * e.point, p);
-            const double th = edge_stereo(e) ? 7.815 : 5.991;
-            unsigned char f = a.eflag[i] & 3;
-            if (edge_chi2(a, i) > th || !(p[2] > 0.0)) f |= 1;
-            f |= 2;
-            a.eflag[i] = f;
-        }
-        __syncthreads();
-        L.initialize();
-        if (S.istate[1]) { if (tid == 0) a.out_stats[3] = ORBMI_E_UNSUPPORTED; return; }
-        it1 = L.optimize(10);
-        chi1 = L.robust_chi2();
-    }
-    // vToErase (src/Optimizer.cc:741-773)
-    for (int i = tid; i < a.nedge; i += kBaThreads) {
-        const orbmi_ba_edge e = a.edges[i];
-        if (a.pts[e.point].bad) continue;
-        double p[3];
-        se3_map(a.T + 8 * e.kf, a.X + 4 * e.point, p);
-        const double th = edge_stereo(e) ? 7.815 : 5.991;
-        a.out_erase[i] = (edge_chi2(a, i) > th || !(p[2] > 0.0)) ? 1 : 0;
-    }
-    // write back (Converter::toCvMat)
-    for (int k = tid; k < a.nkf; k += kBaThreads) {
-        const double* T = a.T + 8 * k;
-        double R[3][3];
-        q_to_matrix(load_q(T), R);
-        float* o = a.out_tcw + 16 * k;
-        for (int r = 0; r < 3; r++) {
-            for (int c = 0; c < 3; c++) o[4 * r + c] = (float)R[r][c];
-            o[4 * r + 3] = (float)T[4 + r];
-        }
-        o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
-    }
-    for (int p = tid; p < a.npt; p += kBaThreads)
-        for (int r = 0; r < 3; r++) a.out_pos[3 * p + r] = (float)a.X[4 * p + r];
-    if (tid == 0) {
-        a.out_stats[0] = it0;
-        a.out_stats[1] = it1;
-        a.out_chi2[0] = chi0;
-        a.out_chi2[1] = chi1;
     }
 }
 
+// outlier levels, kernels off before the second optimisation (src/Optimizer.cc:701-732);
+// chi2 from the stale errors, depth from the current estimate
+__global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a, const double* __restrict__ T,
+                                                        const double* __restrict__ X) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.nedge) return;
+    const orbmi_ba_edge e = a.edges[i];
+    if (a.pts[e.point].bad) return;
+    double p[3];
+    se3_map(T + 8 * e.kf, X + 4 * e.point, p);
+    const double th = edge_stereo(e) ? 7.815 : 5.991;
+    unsigned char f = a.eflag[i] & 3;
+    if (edge_chi2(a, i) > th || !(p[2] > 0.0)) f |= 1;
+    f |= 2;
+    a.eflag[i] = f;
+}
+
+// SparseOptimizer::initializeOptimization(level 0) + buildIndexMapping: active edges, pose
+// indices in vertex-id order (poses first), number of active points
+__global__ __launch_bounds__(1024) void k_ba_activate(BaDev a) {
+    __shared__ int kfact[kBaMaxKf];
+    __shared__ int nl;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < a.nkf; k += blockDim.x) kfact[k] = 0;
+    if (tid == 0) nl = 0;
+    __syncthreads();
+    for (int i = tid; i < a.nedge; i += blockDim.x) {
+        unsigned char f = a.eflag[i] & 3;
+        if (!(f & 1)) { f |= 4; kfact[a.edges[i].kf] = 1; }
+        a.eflag[i] = f;
+    }
+    __syncthreads();
+    int nlp = 0;
+    for (int p = tid; p < a.npt; p += blockDim.x) nlp += point_active(a, p);
+    if (nlp) atomicAdd(&nl, nlp);
+    __syncthreads();
+    if (tid == 0) {
+        int n = 0;
+        for (int oi = 0; oi < a.nkf; oi++) {
+            const int k = a.kf_order[oi];
+            a.pose_idx[k] = -1;
+            if (a.kfs[k].fixed || !kfact[k]) continue;
+            if (n < kBaMaxPoses) a.pose_kf[n] = k;
+            a.pose_idx[k] = n < kBaMaxPoses ? n : -1;
+            n++;
+        }
+        a.istat[0] = n;
+        a.istat[1] = nl;
+        a.istat[2] = n > kBaMaxPoses;
+    }
+}
+
+// ---------------------------------------------------------------- errors
+// computeActiveErrors (recompute = 1) + activeRobustChi2; per-block partial sums
+__global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a, const double* __restrict__ T,
+                                                        const double* __restrict__ X, int recompute,
+                                                        double* __restrict__ part) {
+    __shared__ double red[kBaBlock / 64];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0;
+    if (i < a.nedge && (a.eflag[i] & 4)) {
+        if (recompute) edge_error(a, i, T, X, a.err + 3 * i);
+        double r0, r1;
+        edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
+        s = r0;
+    }
+    s = block_sum<kBaBlock>(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------- linear system
+// BaseBinaryEdge::constructQuadraticForm per edge (base_binary_edge.hpp:55-120)
+__global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a, const double* __restrict__ T,
+                                                           const double* __restrict__ X) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.nedge || !(a.eflag[i] & 4)) return;
+    double Jl[3][3], Jp[3][6], w, om[3];
+    edge_jacobians(a, i, T, X, Jl, Jp);
+    edge_weights(a, i, &w, om);
+    double* He = a.Hle + 9 * (long long)i;
+    int q = 0;
+    for (int r = 0; r < 3; r++)
+        for (int c = r; c < 3; c++, q++)
+            He[q] = Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
+    for (int r = 0; r < 3; r++) He[6 + r] = Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
+    if (a.pose_idx[a.edges[i].kf] < 0) return;
+    double* B = a.Hpl + 18 * (long long)i;
+    for (int r = 0; r < 6; r++)
+        for (int c = 0; c < 3; c++) B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
+    double* Hp = a.Hpe + 27 * (long long)i;
+    q = 0;
+    for (int r = 0; r < 6; r++)
+        for (int c = r; c < 6; c++, q++)
+            Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
+    for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
+}
+
+// Hll, b_l: sum over the point's active edges in edge order
+__global__ __launch_bounds__(kBaBlock) void k_ba_points(BaDev a) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.npt) return;
+    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++) {
+        if (!(a.eflag[i] & 4)) continue;
+        const double* He = a.Hle + 9 * (long long)i;
+        for (int k = 0; k < 6; k++) h[k] += He[k];
+        for (int k = 0; k < 3; k++) b[k] += He[6 + k];
+    }
+    double* H = a.Hll + 9 * p;
+    H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+    H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+    H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+    for (int k = 0; k < 3; k++) a.bl[3 * p + k] = b[k];
+}
+
+// Hpp, b_p: one block per free pose; each half-wave sums one edge's 27 values per step
+// (lane = value), then a fixed-order sum over the half-waves
+constexpr int kBaPoseThreads = 512;
+__global__ __launch_bounds__(kBaPoseThreads) void k_ba_poses(BaDev a) {
+    __shared__ double red[2 * kBaPoseThreads / 64][27];
+    const int pi = blockIdx.x, k = a.pose_kf[pi];
+    const int lane = threadIdx.x & 63, hw = threadIdx.x >> 5, q = lane & 31;
+    const int nhw = kBaPoseThreads / 32;
+    double v = 0;
+    if (q < 27)
+        for (int j = a.kf_start[k] + hw; j < a.kf_start[k + 1]; j += nhw) {
+            const int i = a.kf_edges[j];
+            if (a.eflag[i] & 4) v += a.Hpe[27 * (long long)i + q];
+        }
+    if (q < 27) red[hw][q] = v;
+    __syncthreads();
+    if (threadIdx.x < 27) {
+        double t = 0;
+        for (int w = 0; w < nhw; w++) t += red[w][threadIdx.x];
+        const int qq = threadIdx.x;
+        if (qq < 21) {
+            int r = 0, c = qq;
+            while (c >= 6 - r) { c -= 6 - r; r++; }
+            c += r;
+            a.Hpp[36 * pi + r * 6 + c] = t;
+            a.Hpp[36 * pi + c * 6 + r] = t;
+        } else {
+            a.bp[6 * pi + qq - 21] = t;
+        }
+    }
+}
+
+// max diagonal of H (computeLambdaInit, optimization_algorithm_levenberg.cpp:166-180)
+__global__ __launch_bounds__(1024) void k_ba_maxdiag(BaDev a) {
+    __shared__ double red[16];
+    const int np = a.istat[0] < kBaMaxPoses ? a.istat[0] : kBaMaxPoses;
+    double m = 0;
+    for (int q = threadIdx.x; q < np * 6; q += blockDim.x) m = fmax(m, fabs(a.Hpp[36 * (q / 6) + (q % 6) * 7]));
+    for (int p = threadIdx.x; p < a.npt; p += blockDim.x)
+        if (point_active(a, p))
+            for (int j = 0; j < 3; j++) m = fmax(m, fabs(a.Hll[9 * p + 4 * j]));
+    m = block_max<1024>(m, red);
+    if (threadIdx.x == 0) a.scal[3] = m;
+}
+
+// ---------------------------------------------------------------- Schur complement
+// thread per edge: D = Hll + lambda I of the edge's point, D^-1 (cofactors; the point's first
+// edge stores it), B D^-1 and B D^-1 b_l for edges into free poses
+__global__ __launch_bounds__(kBaBlock) void k_ba_point_schur(BaDev a, double lam) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.nedge) return;
+    const orbmi_ba_edge ed = a.edges[e];
+    const int p = ed.point;
+    const bool first = e == a.pt_start[p];
+    const bool use = (a.eflag[e] & 4) && a.pose_idx[ed.kf] >= 0;
+    if ((!first && !use) || !point_active(a, p)) return;
+    double D[3][3];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) D[r][c] = a.Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
+    const double c00 = D[1][1] * D[2][2] - D[1][2] * D[2][1];
+    const double c10 = D[1][2] * D[2][0] - D[1][0] * D[2][2];
+    const double c20 = D[1][0] * D[2][1] - D[1][1] * D[2][0];
+    const double det = D[0][0] * c00 + D[0][1] * c10 + D[0][2] * c20;
+    double Di[9];
+    Di[0] = c00 / det; Di[3] = c10 / det; Di[6] = c20 / det;
+    Di[1] = (D[0][2] * D[2][1] - D[0][1] * D[2][2]) / det;
+    Di[4] = (D[0][0] * D[2][2] - D[0][2] * D[2][0]) / det;
+    Di[7] = (D[0][1] * D[2][0] - D[0][0] * D[2][1]) / det;
+    Di[2] = (D[0][1] * D[1][2] - D[0][2] * D[1][1]) / det;
+    Di[5] = (D[0][2] * D[1][0] - D[0][0] * D[1][2]) / det;
+    Di[8] = (D[0][0] * D[1][1] - D[0][1] * D[1][0]) / det;
+    if (first)
+        for (int k = 0; k < 9; k++) a.Dinv[9 * p + k] = Di[k];
+    if (!use) return;
+    const double* blp = a.bl + 3 * p;
+    double db[3];
+    for (int r = 0; r < 3; r++) db[r] = Di[r * 3] * blp[0] + Di[r * 3 + 1] * blp[1] + Di[r * 3 + 2] * blp[2];
+    const double* B = a.Hpl + 18 * (long long)e;
+    double* BD = a.BD + 18 * (long long)e;
+    for (int r = 0; r < 6; r++) {
+        for (int c = 0; c < 3; c++) BD[r * 3 + c] = B[r * 3] * Di[c] + B[r * 3 + 1] * Di[3 + c] + B[r * 3 + 2] * Di[6 + c];
+        a.Bdb[6 * (long long)e + r] = B[r * 3] * db[0] + B[r * 3 + 1] * db[1] + B[r * 3 + 2] * db[2];
+    }
+}
+
+// one block per pose pair (i <= j): H_schur(i,j) = [Hpp_i + lambda I] - sum B_i D^-1 B_j^T
+// over the points both observe; the diagonal block also writes b_schur(i)
+__global__ __launch_bounds__(kBaBlock) void k_ba_schur_blocks(BaDev a, double lam, int N) {
+    __shared__ double red[kBaBlock / 64][42];
+    const int b = blockIdx.x;
+    const int ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
+    const int i1 = a.pose_idx[ka], i2 = a.pose_idx[kb];
+    if (i1 < 0 || i2 < 0) return;
+    const bool diag = ka == kb;
+    double acc[36];
+#pragma unroll
+    for (int q = 0; q < 36; q++) acc[q] = 0;
+    for (int j = a.blk_start[b] + threadIdx.x; j < a.blk_start[b + 1]; j += blockDim.x) {
+        const int2 pr = a.blk_pairs[j];
+        if (!(a.eflag[pr.x] & 4) || !(a.eflag[pr.y] & 4)) continue;
+        const double* BD = a.BD + 18 * (long long)pr.x;
+        const double* B2 = a.Hpl + 18 * (long long)pr.y;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 6; c++)
+                acc[r * 6 + c] += BD[r * 3] * B2[c * 3] + BD[r * 3 + 1] * B2[c * 3 + 1] + BD[r * 3 + 2] * B2[c * 3 + 2];
+    }
+    double bacc[6] = {0, 0, 0, 0, 0, 0};
+    if (diag)
+        for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
+            const int e = a.kf_edges[j];
+            if (!(a.eflag[e] & 4)) continue;
+#pragma unroll
+            for (int r = 0; r < 6; r++) bacc[r] += a.Bdb[6 * (long long)e + r];
+        }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 42; q++) {
+        double x = q < 36 ? acc[q] : bacc[q - 36];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if (lane == 0) red[wid][q] = x;
+    }
+    __syncthreads();
+    const int q = threadIdx.x;
+    if (q < 42) {
+        double t = 0;
+        for (int w = 0; w < kBaBlock / 64; w++) t += red[w][q];
+        if (q < 36) {
+            const int r = q / 6, c = q % 6;
+            if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
+            else if (c >= r) a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (a.Hpp[36 * i1 + q] + (r == c ? lam : 0.0)) - t;
+        } else if (diag) {
+            a.bs[6 * i1 + q - 36] = a.bp[6 * i1 + q - 36] - t;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- reduced system solve
+// LDL^T = U^T D U of the packed upper reduced system in LDS, blocked by the 6x6 pose blocks
+// (right-looking): per block step the diagonal block is factored by one wave, the block row
+// is solved column-parallel (W = U_kk^-T A_kj, U_kj = D^-1 W), and the trailing upper
+// triangle takes the rank-6 update A_ij -= W_ki^T U_kj (wave per row, lanes over columns).
+// Then U^T z = b, y = z / D, U x = y by one wave (LinearSolverEigen / SimplicialLDLT
+// equivalent up to rounding order).
+__device__ inline void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int N) {
+    __shared__ double H[kBaPacked];
+    __shared__ double W[6 * kBaMaxN];
+    __shared__ double bs[kBaMaxN];
+    __shared__ int rb[kBaMaxN];   // packed(r, c) = rb[r] + c
+    __shared__ int fail;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+    const int NP = N * (N + 1) / 2;
+    for (int q = tid; q < NP; q += blockDim.x) H[q] = a.S[q];
+    for (int q = tid; q < N; q += blockDim.x) { bs[q] = a.bs[q]; rb[q] = q * N - q * (q - 1) / 2 - q; }
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    for (int k0 = 0; k0 < N; k0 += 6) {
+        // (1) diagonal block, wave 0: lanes own (r, c) of the 6x6 upper block
+        if (wid == 0) {
+            const int r = lane / 6, c = lane % 6;
+            const bool own = lane < 36 && c >= r;
+            for (int j = 0; j < 6; j++) {
+                const double d = H[rb[k0 + j] + k0 + j];
+                if (!(fabs(d) > 0) || !isfinite(d)) { if (lane == 0) fail = 1; break; }
+                double upd = 0;
+                if (own && r > j) upd = H[rb[k0 + j] + k0 + r] * H[rb[k0 + j] + k0 + c] / d;
+                wave_sync_lds();
+                if (own && r > j) H[rb[k0 + r] + k0 + c] -= upd;
+                if (own && r == j && c > j) H[rb[k0 + j] + k0 + c] /= d;
+                wave_sync_lds();
+            }
+        }
+        __syncthreads();
+        if (fail) break;
+        const int c0 = k0 + 6;
+        if (c0 >= N) break;
+        // (2) block row: one thread per column
+        for (int c = c0 + tid; c < N; c += blockDim.x) {
+            double w[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                double v = H[rb[k0 + t] + c];
+#pragma unroll
+                for (int s2 = 0; s2 < t; s2++) v -= H[rb[k0 + s2] + k0 + t] * w[s2];
+                w[t] = v;
+            }
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                W[t * kBaMaxN + c] = w[t];
+                H[rb[k0 + t] + c] = w[t] / H[rb[k0 + t] + k0 + t];
+            }
+        }
+        __syncthreads();
+        // (3) trailing rank-6 update, wave per row
+        for (int r = c0 + wid; r < N; r += nw) {
+            double wr[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) wr[t] = W[t * kBaMaxN + r];
+            const int base = rb[r];
+            for (int c = r + lane; c < N; c += 64) {
+                double s2 = 0;
+#pragma unroll
+                for (int t = 0; t < 6; t++) s2 += wr[t] * H[rb[k0 + t] + c];
+                H[base + c] -= s2;
+            }
+        }
+        __syncthreads();
+    }
+    if (fail) {
+        if (tid == 0) a.istat[3] = 0;
+        return;
+    }
+    if (wid != 0) return;
+    // one wave: U^T z = b ; y = z / D ; U x = y
+    for (int k = 0; k < N; k++) {
+        const double zk = bs[k];
+        for (int jj = k + 1 + lane; jj < N; jj += 64) bs[jj] -= H[rb[k] + jj] * zk;
+        wave_sync_lds();
+    }
+    for (int k = lane; k < N; k += 64) bs[k] /= H[rb[k] + k];
+    wave_sync_lds();
+    for (int k = N - 1; k >= 0; k--) {
+        const double xk = bs[k];
+        for (int jj = lane; jj < k; jj += 64) bs[jj] -= H[rb[jj] + k] * xk;
+        wave_sync_lds();
+    }
+    for (int k = lane; k < N; k += 64) a.xp[k] = bs[k];
+    if (lane == 0) a.istat[3] = 1;
+}
+
+// ---------------------------------------------------------------- update
+// x_l = D^-1 (b_l - Hpl^T x_p); trial estimates (push/pop by buffer swap); computeScale
+__global__ __launch_bounds__(kBaBlock) void k_ba_update(BaDev a, double lam, int N, const double* __restrict__ T,
+                                                        const double* __restrict__ X, double* __restrict__ Tt,
+                                                        double* __restrict__ Xt, double* __restrict__ part) {
+    __shared__ double red[kBaBlock / 64];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = a.istat[3] != 0;
+    double s = 0;
+    if (i < a.npt) {
+        double xl[3] = {0, 0, 0};
+        if (ok && point_active(a, i)) {
+            double cl[3] = {a.bl[3 * i], a.bl[3 * i + 1], a.bl[3 * i + 2]};
+            for (int e = a.pt_start[i]; e < a.pt_start[i + 1]; e++) {
+                if (!(a.eflag[e] & 4)) continue;
+                const int i1 = a.pose_idx[a.edges[e].kf];
+                if (i1 < 0) continue;
+                const double* B = a.Hpl + 18 * (long long)e;
+                for (int c = 0; c < 3; c++)
+                    for (int r = 0; r < 6; r++) cl[c] -= B[r * 3 + c] * a.xp[6 * i1 + r];
+            }
+            const double* Di = a.Dinv + 9 * i;
+            for (int r = 0; r < 3; r++) xl[r] = Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1] + Di[r * 3 + 2] * cl[2];
+        }
+        for (int r = 0; r < 3; r++) {
+            Xt[4 * i + r] = X[4 * i + r] + xl[r];
+            if (ok) s += xl[r] * (lam * xl[r] + a.bl[3 * i + r]);
+        }
+    }
+    if (i < a.nkf) {
+        const int pi = a.pose_idx[i];
+        if (ok && pi >= 0) se3_oplus(a.xp + 6 * pi, T + 8 * i, Tt + 8 * i);
+        else for (int q = 0; q < 8; q++) Tt[8 * i + q] = T[8 * i + q];
+    }
+    if (ok && i < N) s += a.xp[i] * (lam * a.xp[i] + a.bp[i]);
+    s = block_sum<kBaBlock>(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// fixed-order sums of the partials -> scal[slot], solve status -> scal[2]
+__global__ __launch_bounds__(1024) void k_ba_scalars(BaDev a, const double* __restrict__ p0, int n0,
+                                                     const double* __restrict__ p1, int n1) {
+    __shared__ double red[16];
+    double s = 0;
+    for (int k = threadIdx.x; k < n0; k += blockDim.x) s += p0[k];
+    s = block_sum<1024>(s, red);
+    double t = 0;
+    for (int k = threadIdx.x; k < n1; k += blockDim.x) t += p1[k];
+    t = block_sum<1024>(t, red);
+    if (threadIdx.x == 0) {
+        a.scal[0] = s;
+        a.scal[1] = t;
+        a.scal[2] = a.istat[3];
+    }
+}
+
+// vToErase (src/Optimizer.cc:741-773) + write back (Converter::toCvMat)
+__global__ __launch_bounds__(kBaBlock) void k_ba_finish(BaDev a, const double* __restrict__ T,
+                                                        const double* __restrict__ X, float* __restrict__ out_tcw,
+                                                        float* __restrict__ out_pos,
+                                                        unsigned char* __restrict__ out_erase) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.nedge) {
+        const orbmi_ba_edge e = a.edges[i];
+        if (!a.pts[e.point].bad) {
+            double p[3];
+            se3_map(T + 8 * e.kf, X + 4 * e.point, p);
+            const double th = edge_stereo(e) ? 7.815 : 5.991;
+            out_erase[i] = (edge_chi2(a, i) > th || !(p[2] > 0.0)) ? 1 : 0;
+        }
+    }
+    if (i < a.nkf) {
+        const double* Ti = T + 8 * i;
+        double R[3][3];
+        q_to_matrix(load_q(Ti), R);
+        float* o = out_tcw + 16 * i;
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) o[4 * r + c] = (float)R[r][c];
+            o[4 * r + 3] = (float)Ti[4 + r];
+        }
+        o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
+    }
+    if (i < a.npt)
+        for (int r = 0; r < 3; r++) out_pos[3 * i + r] = (float)X[4 * i + r];
+}
+
+}  // namespace orbmi
+
 // ---------------------------------------------------------------- host
-struct BaHandle {
+struct orbmi_ba {
     int device = 0;
     hipStream_t stream = nullptr;
     uint8_t* d_buf = nullptr;
     size_t cap = 0;
-    int* h_stop = nullptr;  // pinned, device-mapped
-    int* d_stop = nullptr;
+    double* h_scal = nullptr;  // pinned readback of the per-trial scalars
+    int* h_istat = nullptr;
 };
 
-}  // namespace orbmi
+namespace {
 
-struct orbmi_ba {
-    orbmi::BaHandle h;
+using namespace orbmi;
+
+struct Runner {
+    orbmi_ba& h;
+    BaDev a;
+    double *T, *Tt, *X, *Xt;
+    double *part_e, *part_u;
+    int nb_e, nb_u, nb_p, nb_n;
+    const volatile int* stop;
+    int np = 0, nl = 0;
+
+    bool stopped() const { return stop && *stop; }
+    int grid(int n) const { return std::max(1, (n + kBaBlock - 1) / kBaBlock); }
+
+    int read_scalars() {
+        ORBMI_HIP(hipMemcpyAsync(h.h_scal, a.scal, 8 * sizeof(double), hipMemcpyDeviceToHost, h.stream));
+        ORBMI_HIP(hipStreamSynchronize(h.stream));
+        return ORBMI_OK;
+    }
+
+    int activate() {
+        hipLaunchKernelGGL(k_ba_activate, dim3(1), dim3(1024), 0, h.stream, a);
+        ORBMI_HIP(hipMemcpyAsync(h.h_istat, a.istat, 4 * sizeof(int), hipMemcpyDeviceToHost, h.stream));
+        ORBMI_HIP(hipStreamSynchronize(h.stream));
+        if (h.h_istat[2]) return ORBMI_E_UNSUPPORTED;
+        np = h.h_istat[0];
+        nl = h.h_istat[1];
+        return ORBMI_OK;
+    }
+
+    // activeRobustChi2 on the (stale) stored errors
+    int robust_chi2(double* out) {
+        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 0, part_e);
+        hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_e, 0);
+        int rc = read_scalars();
+        *out = h.h_scal[0];
+        return rc;
+    }
+
+    // OptimizationAlgorithmLevenberg::solve (levenberg.cpp:61-164); *terminate = 1 on stop
+    int lm_iteration(int iteration, double* lambda, double* ni, int* nbad, int* terminate) {
+        const int N = 6 * np;
+        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 1, part_e);
+        hipLaunchKernelGGL(k_ba_linearize, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X);
+        hipLaunchKernelGGL(k_ba_points, dim3(nb_p), dim3(kBaBlock), 0, h.stream, a);
+        if (np > 0) hipLaunchKernelGGL(k_ba_poses, dim3(np), dim3(kBaPoseThreads), 0, h.stream, a);
+        if (iteration == 0) hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(1024), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_e, 0);
+        int rc;
+        if ((rc = read_scalars())) return rc;
+        double currentChi = h.h_scal[0];
+        const double iniChi = currentChi;
+        if (iteration == 0) {  // computeLambdaInit, tau = 1e-5
+            *lambda = 1e-5 * h.h_scal[3];
+            *ni = 2;
+            *nbad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            const double lam = *lambda;
+            hipLaunchKernelGGL(k_ba_point_schur, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, lam);
+            if (a.nblk > 0)
+                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(a.nblk), dim3(kBaBlock), 0, h.stream, a, lam, N);
+            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, N);
+            hipLaunchKernelGGL(k_ba_update, dim3(nb_u), dim3(kBaBlock), 0, h.stream, a, lam, N, T, X, Tt, Xt, part_u);
+            hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, Tt, Xt, 1, part_e);
+            hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_u, nb_u);
+            if ((rc = read_scalars())) return rc;
+            const bool ok2 = h.h_scal[2] != 0;
+            double tempChi = ok2 ? h.h_scal[0] : DBL_MAX;
+            const double scale = ok2 ? h.h_scal[1] : 0.0;
+            rho = (currentChi - tempChi) / (scale + 1e-3);
+            if (rho > 0 && std::isfinite(tempChi)) {  // accept: the trial buffers become current
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double sf = std::max(1. / 3., alpha);
+                *lambda *= sf;
+                *ni = 2;
+                currentChi = tempChi;
+                std::swap(T, Tt);
+                std::swap(X, Xt);
+            } else {  // reject: pop (the trial buffers are simply not adopted)
+                *lambda *= *ni;
+                *ni *= 2;
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10 && !stopped());
+        if (qmax == 10 || rho == 0) { *terminate = 1; return ORBMI_OK; }
+        // ORB-SLAM2's modified g2o: 3 consecutive iterations without a 1e-3 relative decrease
+        if ((iniChi - currentChi) * 1e3 < iniChi) (*nbad)++;
+        else *nbad = 0;
+        *terminate = *nbad >= 3;
+        return ORBMI_OK;
+    }
+
+    // SparseOptimizer::optimize(iterations); -1 with an empty index mapping
+    int optimize(int iterations, int* it) {
+        *it = 0;
+        if (np + nl == 0) { *it = -1; return ORBMI_OK; }
+        double lambda = 0, ni = 2;
+        int nbad = 0;
+        for (int i = 0; i < iterations && !stopped(); i++) {
+            int term = 0, rc;
+            if ((rc = lm_iteration(i, &lambda, &ni, &nbad, &term))) return rc;
+            ++*it;
+            if (term) break;
+        }
+        return ORBMI_OK;
+    }
 };
+
+}  // namespace
 
 extern "C" {
 
@@ -739,34 +892,34 @@ int orbmi_ba_create(int device, orbmi_ba** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBMI_E_HIP;
     orbmi_ba* b = new (std::nothrow) orbmi_ba();
     if (!b) return ORBMI_E_ARG;
-    b->h.device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->h.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&b->h.h_stop, sizeof(int), hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&b->h.d_stop, b->h.h_stop, 0) != hipSuccess) {
-        delete b;
+    b->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&b->h_scal, 8 * sizeof(double)) != hipSuccess ||
+        hipHostMalloc((void**)&b->h_istat, 4 * sizeof(int)) != hipSuccess) {
+        orbmi_ba_destroy(b);
         return ORBMI_E_HIP;
     }
-    *b->h.h_stop = 0;
     *out = b;
     return ORBMI_OK;
 }
 
 void orbmi_ba_destroy(orbmi_ba* b) {
     if (!b) return;
-    (void)hipSetDevice(b->h.device);
-    if (b->h.d_buf) (void)hipFree(b->h.d_buf);
-    if (b->h.h_stop) (void)hipHostFree(b->h.h_stop);
-    if (b->h.stream) (void)hipStreamDestroy(b->h.stream);
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    if (b->d_buf) (void)hipFree(b->d_buf);
+    if (b->h_scal) (void)hipHostFree(b->h_scal);
+    if (b->h_istat) (void)hipHostFree(b->h_istat);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
 
 int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_ba_result* R,
                                   const volatile int* stop) {
-    using namespace orbmi;
     if (!b || !P || !R || P->nkf < 0 || P->npt < 0 || P->nedge < 0) return ORBMI_E_ARG;
     if ((P->nkf && (!P->kfs || !R->tcw)) || (P->npt && (!P->pts || !R->pos)) || (P->nedge && (!P->edges || !R->erase)))
         return ORBMI_E_ARG;
-    BaHandle& h = b->h;
+    orbmi_ba& h = *b;
     ORBMI_HIP(hipSetDevice(h.device));
     R->aborted = 0;
     R->iterations[0] = R->iterations[1] = 0;
@@ -795,19 +948,63 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     }
     for (int k = 0; k < nkf; k++) order[k] = k;
     std::stable_sort(order.begin(), order.begin() + nkf, [&](int x, int y) { return P->kfs[x].id < P->kfs[y].id; });
+    // Schur pair lists: blocks = pairs of non-fixed keyframes (a, b) with rank(a) <= rank(b)
+    // in id order; pairs (e_a, e_b) = two observations of one point (both orders inside a
+    // keyframe).  Pose indices follow the same order, so block (a, b) is (i <= j).
+    std::vector<int> rank(std::max(nkf, 1), -1), free_kf;
+    for (int oi = 0; oi < nkf; oi++)
+        if (!P->kfs[order[oi]].fixed) { rank[order[oi]] = (int)free_kf.size(); free_kf.push_back(order[oi]); }
+    const int nf = (int)free_kf.size();
+    const long long nblk_ll = (long long)nf * (nf + 1) / 2;
+    if (nblk_ll > (1 << 20)) return ORBMI_E_UNSUPPORTED;
+    const int nblk = (int)nblk_ll;
+    auto blk_of = [nf](int ra, int rb) { return ra * nf - ra * (ra - 1) / 2 + (rb - ra); };
+    std::vector<int> blk_kf(2 * std::max(nblk, 1)), blk_start(nblk + 1, 0);
+    for (int ra = 0; ra < nf; ra++)
+        for (int rb = ra; rb < nf; rb++) { blk_kf[2 * blk_of(ra, rb)] = free_kf[ra]; blk_kf[2 * blk_of(ra, rb) + 1] = free_kf[rb]; }
+    std::vector<int2> pairs;
+    for (int p = 0; p < npt; p++)
+        for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
+            const int r1 = rank[P->edges[e1].kf];
+            if (r1 < 0) continue;
+            for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
+                const int r2 = rank[P->edges[e2].kf];
+                if (r2 >= r1) blk_start[blk_of(r1, r2) + 1]++;
+            }
+        }
+    for (int k = 0; k < nblk; k++) blk_start[k + 1] += blk_start[k];
+    pairs.resize(std::max(blk_start[nblk], 1));
+    {
+        std::vector<int> fill(blk_start.begin(), blk_start.end() - 1);
+        for (int p = 0; p < npt; p++)
+            for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
+                const int r1 = rank[P->edges[e1].kf];
+                if (r1 < 0) continue;
+                for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
+                    const int r2 = rank[P->edges[e2].kf];
+                    if (r2 >= r1) pairs[fill[blk_of(r1, r2)]++] = make_int2(e1, e2);
+                }
+            }
+    }
+    const int npair = blk_start[nblk];
     // one device arena
+    const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
+    const int nb_u = std::max(1, (std::max(std::max(npt, nkf), kBaMaxN) + kBaBlock - 1) / kBaBlock);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off = 0;
-    auto take = [&](size_t bytes) { size_t o = off; off += al(bytes); return o; };
+    auto take = [&](size_t bytes) { size_t o = off; off += al(std::max(bytes, (size_t)8)); return o; };
     const size_t o_kfs = take(sizeof(orbmi_ba_keyframe) * nkf), o_pts = take(sizeof(orbmi_ba_point) * npt),
                  o_edges = take(sizeof(orbmi_ba_edge) * ne), o_order = take(4 * nkf), o_pts_start = take(4 * (npt + 1)),
-                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * std::max(ne, 1)), o_T = take(64 * nkf),
-                 o_Tt = take(64 * nkf), o_X = take(32 * npt), o_Xt = take(32 * npt), o_err = take(24 * ne),
-                 o_eflag = take(ne), o_pidx = take(4 * nkf), o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(144 * (size_t)ne),
-                 o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Dinv = take(72 * npt), o_Hpp = take(288 * kBaMaxPoses),
-                 o_bp = take(48 * kBaMaxPoses), o_xp = take(8 * kBaMaxN), o_xl = take(24 * npt),
-                 o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(std::max(ne, 1)), o_stats = take(16),
-                 o_chi2 = take(16);
+                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
+                 o_blk_start = take(4 * ((size_t)nblk + 1)), o_pairs = take(8 * (size_t)npair),
+                 o_T = take(64 * nkf), o_Tt = take(64 * nkf), o_X = take(32 * npt), o_Xt = take(32 * npt),
+                 o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_pkf = take(4 * kBaMaxPoses),
+                 o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne), o_Hpe = take(216 * (size_t)ne),
+                 o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Dinv = take(72 * npt), o_BD = take(144 * (size_t)ne),
+                 o_Bdb = take(48 * (size_t)ne), o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses),
+                 o_S = take(8 * (size_t)kBaPacked), o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN),
+                 o_part_e = take(8 * (size_t)nb_e), o_part_u = take(8 * (size_t)nb_u), o_scal = take(64),
+                 o_istat = take(16), o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
     if (off > h.cap) {
         if (h.d_buf) (void)hipFree(h.d_buf);
         h.d_buf = nullptr;
@@ -817,16 +1014,22 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     }
     uint8_t* B = h.d_buf;
     hipStream_t s = h.stream;
-    ORBMI_HIP(hipMemcpyAsync(B + o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf, hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_pts, P->pts, sizeof(orbmi_ba_point) * npt, hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_edges, P->edges, sizeof(orbmi_ba_edge) * ne, hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_order, order.data(), 4 * nkf, hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_pts_start, pt_start.data(), 4 * (npt + 1), hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_kfs_start, kf_start.data(), 4 * (nkf + 1), hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemcpyAsync(B + o_kf_edges, kf_edges.data(), 4 * std::max(ne, 1), hipMemcpyHostToDevice, s));
-    ORBMI_HIP(hipMemsetAsync(B + o_stats, 0, 16, s));
-    BaArgs a;
-    a.nkf = nkf; a.npt = npt; a.nedge = ne;
+    auto up = [&](size_t o, const void* src, size_t bytes) {
+        return bytes ? hipMemcpyAsync(B + o, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    ORBMI_HIP(up(o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf));
+    ORBMI_HIP(up(o_pts, P->pts, sizeof(orbmi_ba_point) * npt));
+    ORBMI_HIP(up(o_edges, P->edges, sizeof(orbmi_ba_edge) * ne));
+    ORBMI_HIP(up(o_order, order.data(), 4 * nkf));
+    ORBMI_HIP(up(o_pts_start, pt_start.data(), 4 * (npt + 1)));
+    ORBMI_HIP(up(o_kfs_start, kf_start.data(), 4 * (nkf + 1)));
+    ORBMI_HIP(up(o_kf_edges, kf_edges.data(), 4 * (size_t)ne));
+    ORBMI_HIP(up(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk));
+    ORBMI_HIP(up(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1)));
+    ORBMI_HIP(up(o_pairs, pairs.data(), 8 * (size_t)npair));
+    ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 16, s));
+    BaDev a;
+    a.nkf = nkf; a.npt = npt; a.nedge = ne; a.nblk = nblk;
     a.kfs = (const orbmi_ba_keyframe*)(B + o_kfs);
     a.pts = (const orbmi_ba_point*)(B + o_pts);
     a.edges = (const orbmi_ba_edge*)(B + o_edges);
@@ -834,35 +1037,46 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.pt_start = (const int*)(B + o_pts_start);
     a.kf_start = (const int*)(B + o_kfs_start);
     a.kf_edges = (const int*)(B + o_kf_edges);
-    *h.h_stop = 0;
-    a.stop = stop ? (const volatile int*)h.d_stop : nullptr;
-    a.T = (double*)(B + o_T); a.Tt = (double*)(B + o_Tt);
-    a.X = (double*)(B + o_X); a.Xt = (double*)(B + o_Xt);
+    a.blk_kf = (const int*)(B + o_blk_kf);
+    a.blk_start = (const int*)(B + o_blk_start);
+    a.blk_pairs = (const int2*)(B + o_pairs);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
     a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf);
-    a.Hpl = (double*)(B + o_Hpl); a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl);
-    a.Dinv = (double*)(B + o_Dinv); a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
-    a.xp = (double*)(B + o_xp); a.xl = (double*)(B + o_xl);
-    a.out_tcw = (float*)(B + o_otcw); a.out_pos = (float*)(B + o_opos); a.out_erase = B + o_oerase;
-    a.out_stats = (int*)(B + o_stats); a.out_chi2 = (double*)(B + o_chi2);
-    hipLaunchKernelGGL(k_local_ba, dim3(1), dim3(kBaThreads), 0, s, a);
+    a.Hpl = (double*)(B + o_Hpl); a.Hle = (double*)(B + o_Hle); a.Hpe = (double*)(B + o_Hpe);
+    a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl); a.Dinv = (double*)(B + o_Dinv);
+    a.BD = (double*)(B + o_BD); a.Bdb = (double*)(B + o_Bdb);
+    a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
+    a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
+    a.part = (double*)(B + o_part_e); a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
+    Runner r{h, a, (double*)(B + o_T), (double*)(B + o_Tt), (double*)(B + o_X), (double*)(B + o_Xt),
+             (double*)(B + o_part_e), (double*)(B + o_part_u), nb_e, nb_u, nb_p, 0, stop};
+    unsigned char* out_erase = B + o_oerase;
+    hipLaunchKernelGGL(k_ba_setup, dim3(std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock)),
+                       dim3(kBaBlock), 0, s, a, r.T, r.X, out_erase);
     ORBMI_HIP(hipGetLastError());
-    // mirror the caller's abort flag (mbAbortBA) into device-visible memory while it runs
-    while (true) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) ORBMI_HIP(q);
-        if (stop && *stop) __atomic_store_n(h.h_stop, 1, __ATOMIC_RELAXED);
+    int rc;
+    if ((rc = r.activate())) return rc;
+    int it0 = 0, it1 = 0;
+    double chi0 = 0, chi1 = 0;
+    if ((rc = r.optimize(5, &it0))) return rc;
+    if ((rc = r.robust_chi2(&chi0))) return rc;
+    if (!r.stopped()) {  // src/Optimizer.cc:694-737
+        hipLaunchKernelGGL(k_ba_levels, dim3(nb_e), dim3(kBaBlock), 0, s, a, r.T, r.X);
+        if ((rc = r.activate())) return rc;
+        if ((rc = r.optimize(10, &it1))) return rc;
+        if ((rc = r.robust_chi2(&chi1))) return rc;
     }
-    int stats[4];
-    ORBMI_HIP(hipMemcpy(stats, a.out_stats, 16, hipMemcpyDeviceToHost));
-    if (stats[3]) return stats[3];
-    ORBMI_HIP(hipMemcpy(R->chi2, a.out_chi2, 16, hipMemcpyDeviceToHost));
-    if (nkf) ORBMI_HIP(hipMemcpy(R->tcw, a.out_tcw, 64 * nkf, hipMemcpyDeviceToHost));
-    if (npt) ORBMI_HIP(hipMemcpy(R->pos, a.out_pos, 12 * npt, hipMemcpyDeviceToHost));
-    if (ne) ORBMI_HIP(hipMemcpy(R->erase, a.out_erase, ne, hipMemcpyDeviceToHost));
-    R->iterations[0] = stats[0];
-    R->iterations[1] = stats[1];
+    hipLaunchKernelGGL(k_ba_finish, dim3(std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock)),
+                       dim3(kBaBlock), 0, s, a, r.T, r.X, (float*)(B + o_otcw), (float*)(B + o_opos), out_erase);
+    ORBMI_HIP(hipGetLastError());
+    if (nkf) ORBMI_HIP(hipMemcpyAsync(R->tcw, B + o_otcw, 64 * nkf, hipMemcpyDeviceToHost, s));
+    if (npt) ORBMI_HIP(hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s));
+    if (ne) ORBMI_HIP(hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s));
+    ORBMI_HIP(hipStreamSynchronize(s));
+    R->iterations[0] = it0;
+    R->iterations[1] = it1;
+    R->chi2[0] = chi0;
+    R->chi2[1] = chi1;
     return ORBMI_OK;
 }
 

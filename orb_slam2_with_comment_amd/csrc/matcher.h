@@ -8,7 +8,8 @@ namespace orbmi {
 
 // Frame view resolved to device pointers; pose and scale tables travel by value.
 struct DevFrame {
-    int n;
+    int n;                 // capacity when n_dev is set
+    const int* n_dev;      // device-resident count (optional)
     const orbmi_keypoint* keys;
     const float* u_right;
     const uint8_t* desc;
@@ -19,6 +20,8 @@ struct DevFrame {
     float scale[kMaxLevels];
     float log_scale_factor;
 };
+
+__device__ inline int frame_n(const DevFrame& F) { return F.n_dev ? min(*F.n_dev, F.n) : F.n; }
 
 struct DevFV {
     int nnodes;
@@ -31,6 +34,7 @@ struct Matcher {
     static constexpr int kCandCap = 96;  // candidates kept per query; overflow re-enumerates
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;
     // grid
     int* d_cell_start = nullptr; size_t cap_cell_start = 0;
     int* d_cell_list = nullptr; size_t cap_cell_list = 0;
@@ -42,6 +46,7 @@ struct Matcher {
     int* d_bin_of = nullptr; size_t cap_bin_of = 0;
     int* d_hist = nullptr; size_t cap_hist = 0;
     int* d_scalars = nullptr; size_t cap_scalars = 0;   // small per-call outputs
+    orbmi_mappoint_track* d_track = nullptr; size_t cap_track = 0;  // fused frustum output
     // staging arena for host inputs/outputs (reset per call)
     struct Block { uint8_t* p; size_t size, used; };
     std::vector<Block> arena;
@@ -59,5 +64,7 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
                             int* nmatches);
 int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
                const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
+int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
+                  int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches);
 
 }  // namespace orbmi

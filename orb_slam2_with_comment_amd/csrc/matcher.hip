@@ -5,6 +5,7 @@
 //   k_lf_candidates     SearchByProjection(CF, LF): projection + window + Hamming     thread / LF kp
 //   k_greedy            exact greedy replay of the order-dependent exclusion           one workgroup
 //   k_bow_*             SearchByBoW: node merge-join + per-node greedy (one wave / node)
+//   k_xmatch_*          cross-stream brute-force matching of config 4 (build-defined)
 //
 // Candidate order.  GetFeaturesInArea visits cells ix-major, iy-minor, keypoints in index
 // order inside a cell, so the reference's candidate order is the lexicographic order of
@@ -41,7 +42,8 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict
     const int tid = threadIdx.x;
     for (int i = tid; i < kGridCells; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
-    for (int i = tid; i < F.n; i += blockDim.x) {
+    const int n = frame_n(F);
+    for (int i = tid; i < n; i += blockDim.x) {
         const orbmi_keypoint kp = F.keys[i];
         const int px = (int)roundf((kp.x - F.min_x) * F.grid_w_inv);
         const int py = (int)roundf((kp.y - F.min_y) * F.grid_h_inv);
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict
     for (int k = 0; k < 3; k++) { cell_start[tid * 3 + k] = e; cnt[tid * 3 + k] = e; e += v[k]; }
     if (tid == 0) cell_start[kGridCells] = total;
     __syncthreads();
-    for (int i = tid; i < F.n; i += blockDim.x) {
+    for (int i = tid; i < n; i += blockDim.x) {
         const int c = kp_cell[i];
         if (c >= 0) cell_list[atomicAdd(&cnt[c], 1)] = i;
     }
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) void k_lf_candidates(DevFrame CF, DevFrame LF,
                                                        int mono, unsigned long long* __restrict__ cand,
                                                        int* __restrict__ ncand, int cap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= LF.n) return;
+    if (i >= frame_n(LF)) return;
     bool fw, bw;
     motion_direction(CF, LF, mono, &fw, &bw);
     const orbmi_lastframe_point p = lfp[i];
@@ -349,7 +351,8 @@ __global__ __launch_bounds__(1024) void k_greedy(GreedyArgs a) {
     __shared__ int last[kGreedyMaxKp];    // max query index assigned to the keypoint
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int flag[4];
-    const int tid = threadIdx.x, n = a.F.n;
+    const int tid = threadIdx.x, n = frame_n(a.F);
+    if (a.mode == 1) a.nq = frame_n(a.LF);
     bool fw = false, bw = false;
     if (a.mode == 1) motion_direction(a.F, a.LF, a.mono, &fw, &bw);
     for (int q = tid; q < a.nq; q += blockDim.x) a.res[q] = -1;
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(256) void k_bow_match(DevFrame KF, const uint8_t* _
     }
 }
 
-__global__ __launch_bounds__(1024) void k_bow_finalize(int n, int check_ori, const int* __restrict__ hist,
+__global__ __launch_bounds__(1024) void k_bow_finalize(DevFrame F, int check_ori, const int* __restrict__ hist,
                                                        const int* __restrict__ bin_of, int* __restrict__ match,
                                                        int* __restrict__ nmatches) {
     __shared__ int cnt;
@@ -503,6 +506,7 @@ __global__ __launch_bounds__(1024) void k_bow_finalize(int n, int check_ori, con
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
     }
+    const int n = frame_n(F);
     int local = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         if (match[i] < 0) continue;
@@ -515,6 +519,99 @@ __global__ __launch_bounds__(1024) void k_bow_finalize(int n, int check_ori, con
     atomicAdd(&cnt, local);
     __syncthreads();
     if (threadIdx.x == 0) *nmatches = cnt;
+}
+
+
+// -------------------------------------------------------------------------- cross-stream
+// Config 4 (build-defined): every query descriptor against every valid train
+// row of the gathered segments.  Workgroup = 64 queries x one train chunk staged in LDS; the
+// four waves split the chunk and merge (best, second) through LDS.  Entries are dist<<32 | row
+// so ties resolve to the lowest global row.
+constexpr int kXQ = 64, kXChunk = 512;
+
+__global__ __launch_bounds__(256) void k_xmatch_partial(const uint8_t* __restrict__ qd, int nq_cap,
+                                                        const int* __restrict__ nq_dev,
+                                                        const uint8_t* __restrict__ td, int nseg, int seg_cap,
+                                                        const int* __restrict__ seg_counts, int skip_seg,
+                                                        int chunk, unsigned long long* __restrict__ part) {
+    __shared__ uint4 tile[kXChunk * 2];
+    __shared__ unsigned long long red[4][kXQ][2];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nq = nq_dev ? min(*nq_dev, nq_cap) : nq_cap;
+    const int q = blockIdx.x * kXQ + lane;
+    const int t0 = blockIdx.y * chunk, t1 = min(t0 + chunk, nseg * seg_cap);
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (q < nq) {
+        const uint4* p = reinterpret_cast<const uint4*>(qd + 32 * (long long)q);
+        a0 = p[0]; a1 = p[1];
+    }
+    unsigned long long b1 = ~0ull, b2 = ~0ull;
+    for (int base = t0; base < t1; base += kXChunk) {
+        const int nt = min(kXChunk, t1 - base);
+        __syncthreads();
+        for (int k = threadIdx.x; k < nt * 2; k += blockDim.x)
+            tile[k] = reinterpret_cast<const uint4*>(td + 32 * (long long)base)[k];
+        __syncthreads();
+        for (int k = w; k < nt; k += 4) {
+            const int row = base + k, seg = row / seg_cap;
+            if (seg == skip_seg || row - seg * seg_cap >= seg_counts[seg]) continue;
+            const unsigned long long e = ((unsigned long long)popc256(a0, a1, tile[2 * k], tile[2 * k + 1]) << 32) |
+                                         (unsigned)row;
+            if (e < b1) { b2 = b1; b1 = e; } else if (e < b2) b2 = e;
+        }
+    }
+    red[w][lane][0] = b1;
+    red[w][lane][1] = b2;
+    __syncthreads();
+    if (w == 0 && q < nq) {
+        for (int o = 1; o < 4; o++)
+            for (int j = 0; j < 2; j++) {
+                const unsigned long long e = red[o][lane][j];
+                if (e < b1) { b2 = b1; b1 = e; } else if (e < b2) b2 = e;
+            }
+        part[((long long)blockIdx.y * nq_cap + q) * 2] = b1;
+        part[((long long)blockIdx.y * nq_cap + q) * 2 + 1] = b2;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_xmatch_final(int nq_cap, const int* __restrict__ nq_dev, int nsplit,
+                                                      const unsigned long long* __restrict__ part, int th,
+                                                      float ratio, int* __restrict__ match,
+                                                      int* __restrict__ nmatches) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nq = nq_dev ? min(*nq_dev, nq_cap) : nq_cap;
+    if (q >= nq) return;
+    unsigned long long b1 = ~0ull, b2 = ~0ull;
+    for (int s = 0; s < nsplit; s++)
+        for (int j = 0; j < 2; j++) {
+            const unsigned long long e = part[((long long)s * nq_cap + q) * 2 + j];
+            if (e < b1) { b2 = b1; b1 = e; } else if (e < b2) b2 = e;
+        }
+    int r = -1;
+    if (b1 != ~0ull) {
+        const int d1 = (int)(b1 >> 32), d2 = b2 == ~0ull ? 256 : (int)(b2 >> 32);
+        if (d1 <= th && (float)d1 < ratio * (float)d2) r = (int)(b1 & 0xFFFFFFFFu);
+    }
+    match[q] = r;
+    if (r >= 0) atomicAdd(nmatches, 1);
+}
+
+int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
+                  int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches) {
+    if (nq_cap <= 0) return ORBMI_OK;
+    const long long ntrain = (long long)nseg * seg_cap;
+    // enough workgroups to cover the chip: 64-query blocks x train splits
+    const int qblocks = (nq_cap + kXQ - 1) / kXQ;
+    int nsplit = (int)std::max(1LL, std::min<long long>((ntrain + 255) / 256, (1024 + qblocks - 1) / qblocks));
+    const int chunk = (int)((ntrain + nsplit - 1) / nsplit);
+    nsplit = (int)std::max(1LL, (ntrain + chunk - 1) / chunk);
+    int rc;
+    if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)nsplit * nq_cap * 2))) return rc;
+    hipLaunchKernelGGL(k_xmatch_partial, dim3(qblocks, nsplit), dim3(256), 0, m.stream, qd, nq_cap, nq_dev, td, nseg,
+                       seg_cap, seg_counts, skip_seg, chunk, m.d_cand);
+    hipLaunchKernelGGL(k_xmatch_final, dim3((nq_cap + 255) / 256), dim3(256), 0, m.stream, nq_cap, nq_dev, nsplit,
+                       m.d_cand, th, ratio, match, nmatches);
+    return ORBMI_OK;
 }
 
 // -------------------------------------------------------------------------- host launchers
@@ -584,7 +681,7 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
     if (kfv.nnodes > 0)
         hipLaunchKernelGGL(k_bow_match, dim3((kfv.nnodes + 3) / 4), dim3(256), 0, m.stream, KF, kf_ok, kfv, F, fv,
                            nnratio, check_ori, match, m.d_bin_of, m.d_hist);
-    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, F.n, check_ori, m.d_hist, m.d_bin_of, match,
+    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, F, check_ori, m.d_hist, m.d_bin_of, match,
                        nmatches);
     return ORBMI_OK;
 }

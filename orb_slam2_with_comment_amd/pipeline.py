@@ -1,0 +1,198 @@
+"""Device-resident Track + LocalMap pipeline over the C ABI.
+
+One tracked stereo frame, in the order Tracking runs it (src/Tracking.cc:287-581):
+
+  Frame ctor          ORBextractor(left) || ORBextractor(right)   src/Frame.cc:78-81
+                      Frame::ComputeStereoMatches                 src/Frame.cc:92
+  TrackWithMotionModel ORBmatcher(0.9).SearchByProjection(CF, LF, th=7)  src/Tracking.cc:999-1028
+  TrackLocalMap       Tracking::SearchLocalPoints -> isInFrustum(0.5) +
+                      ORBmatcher(0.8).SearchByProjection(F, localMPs, th=1)  src/Tracking.cc:1362-1402
+  LocalMapping thread Optimizer::LocalBundleAdjustment on every new keyframe
+                      (src/LocalMapping.cc:89-90), concurrently with tracking
+
+All four tracking stages run on ONE HIP stream (the extractor's; the matcher shares it), with
+inputs and outputs in HBM and keypoint counts read on the device (orbmi_frame_view.n_device),
+so a frame is enqueued without a host round trip.  Local BA runs on its own stream from a
+worker thread (the LocalMapping thread), overlapping tracking as in the reference.
+
+PoseOptimization (src/Optimizer.cc:257-481) is not on this path yet;
+the local-map search therefore starts from the motion-model occupancy supplied by the caller.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import queue
+import threading
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+from .types import FRAME_GRID_COLS, FRAME_GRID_ROWS, FrameView
+
+_vp = C.c_void_p
+
+
+def frame_view(n, keys, u_right, desc, tcw, cam, scale_factors, width, height, n_device=None):
+    """orbmi_frame_view over (device or host) addresses; tcw / scale_factors are numpy arrays
+    that must outlive the view."""
+    v = FrameView()
+    v.n = int(n)
+    v.keys_un, v.u_right, v.desc = keys, u_right, desc
+    v.tcw = tcw.ctypes.data if tcw is not None else None
+    v.fx, v.fy, v.cx, v.cy, v.bf = cam.fx, cam.fy, cam.cx, cam.cy, cam.bf
+    v.mb = np.float32(np.float32(cam.bf) / np.float32(cam.fx))
+    v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(width), 0.0, float(height)
+    v.grid_w_inv = np.float32(np.float32(FRAME_GRID_COLS) / np.float32(width))
+    v.grid_h_inv = np.float32(np.float32(FRAME_GRID_ROWS) / np.float32(height))
+    v.nlevels = len(scale_factors)
+    v.scale_factors = scale_factors.ctypes.data
+    v.log_scale_factor = np.float32(np.log(np.float32(scale_factors[1]))) if len(scale_factors) > 1 else 0.0
+    v.n_device = n_device
+    return v
+
+
+class StereoTracker:
+    """Tracking-thread GPU work for one stereo stream (one GPU)."""
+
+    def __init__(self, cam, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, device=0):
+        import torch
+        from .matcher import ORBmatcher
+        from .orb import ORBextractor
+        self.cam, self.device = cam, device
+        self.extractor = ORBextractor(nfeatures, scale_factor, nlevels, ini_th, min_th, device=device)
+        self.matcher = ORBmatcher(device=device)
+        check("orbmi_matcher_share_stream", lib().orbmi_matcher_share_stream(self.matcher._h, self.extractor.handle))
+        s = _vp()
+        check("orbmi_extractor_get_stream", lib().orbmi_extractor_get_stream(self.extractor.handle, C.byref(s)))
+        self.stream_handle = s.value
+        self.scale_factors = self.extractor.GetScaleFactors()
+        self.cap = cap = nfeatures + 64
+        dev = torch.device("cuda", device)
+        # outputs of the current frame (item 0 = left, 1 = right)
+        self.kps = torch.zeros((2, cap, 7), dtype=torch.int32, device=dev)
+        self.desc = torch.zeros((2, cap, 32), dtype=torch.uint8, device=dev)
+        self.counts = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.u_right = torch.zeros((2, cap), dtype=torch.float32, device=dev)
+        self.depth = torch.zeros((2, cap), dtype=torch.float32, device=dev)
+        self.occupied = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        self.match_lf = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        self.match_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        self._views = {}
+
+    def current_view(self, tcw: np.ndarray):
+        """Frame view of the frame being tracked (device arrays, device count)."""
+        key = tcw.ctypes.data
+        v = self._views.get(key)
+        if v is None:
+            v = frame_view(self.cap, self.kps.data_ptr(), self.u_right.data_ptr(), self.desc.data_ptr(), tcw,
+                           self.cam, self.scale_factors, self.cam.width, self.cam.height,
+                           n_device=self.counts.data_ptr())
+            self._views[key] = v
+        return v
+
+    def extract_stereo(self, d_left_right: int, rows: int, cols: int):
+        """ORBextractor(left) + ORBextractor(right) as one batch + ComputeStereoMatches;
+        d_left_right = device address of the 2 x rows x cols u8 image pair."""
+        L = lib()
+        check("orbmi_extract_batch_device", L.orbmi_extract_batch_device(
+            self.extractor.handle, _vp(d_left_right), 2, rows, cols, cols, rows * cols, _vp(self.kps.data_ptr()),
+            _vp(self.desc.data_ptr()), _vp(self.counts.data_ptr()), self.cap))
+        check("orbmi_compute_stereo_matches_batch_device", L.orbmi_compute_stereo_matches_batch_device(
+            self.extractor.handle, self.cam.bf, self.cam.fx, _vp(self.u_right.data_ptr()), _vp(self.depth.data_ptr())))
+
+    def search_last_frame(self, tcw, last_view, last_points, th=7.0):
+        """ORBmatcher(0.9, true).SearchByProjection(mCurrentFrame, mLastFrame, th, !stereo)
+        (src/Tracking.cc:1016) -> self.match_lf (device)."""
+        cv = self.current_view(tcw)
+        check("orbmi_search_by_projection_last_frame", lib().orbmi_search_by_projection_last_frame(
+            self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), C.addressof(last_view),
+            _vp(last_points), th, 0, 1, _vp(self.match_lf.data_ptr()), None))
+
+    def search_local_points(self, tcw, local_mps, n_mp, th=1.0):
+        """Tracking::SearchLocalPoints (src/Tracking.cc:1362-1402) -> self.match_mp (device)."""
+        cv = self.current_view(tcw)
+        check("orbmi_search_local_points", lib().orbmi_search_local_points(
+            self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), _vp(local_mps), int(n_mp), th,
+            _vp(self.match_mp.data_ptr()), None, None))
+
+    def track(self, d_left_right, rows, cols, tcw, last_view, last_points, local_mps, n_mp, th_lf=7.0, th_local=1.0):
+        """Enqueue one tracked frame; results stay in self.match_lf / self.match_mp (device)."""
+        self.extract_stereo(d_left_right, rows, cols)
+        self.search_last_frame(tcw, last_view, last_points, th_lf)
+        self.search_local_points(tcw, local_mps, n_mp, th_local)
+
+    def synchronize(self):
+        check("orbmi_extractor_synchronize", lib().orbmi_extractor_synchronize(self.extractor.handle))
+
+    def close(self):
+        self.matcher.close()
+        self.extractor.close()
+
+
+class LocalMapper:
+    """LocalMapping thread: runs queued LocalBundleAdjustment problems on the GPU (own stream)
+    concurrently with tracking (src/LocalMapping.cc:47-128)."""
+
+    def __init__(self, device=0):
+        from .optimizer import LocalBA
+        self.ba = LocalBA(device)
+        self.q: queue.Queue = queue.Queue()
+        self.done = 0
+        self.last = None
+        self.error = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job = self.q.get()
+            if job is None:
+                self.q.task_done()
+                return
+            try:
+                self.last = self.ba.run(job)
+                self.done += 1
+            except Exception as e:  # surfaced by wait()
+                self.error = e
+            self.q.task_done()
+
+    def insert_keyframe(self, problem):
+        self.q.put(problem)
+
+    def wait(self):
+        self.q.join()
+        if self.error is not None:
+            raise self.error
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+        self.ba.close()
+
+
+def gather_stream_features(dist, desc, kps, count):
+    """Config 4 exchange: all-gather every stream's left descriptors (cap x 32 u8), keypoints
+    (cap x 7 x i32, cv::KeyPoint layout) and count over the process group (RCCL over xGMI on
+    the GPU, gloo on the CPU).  Returns (desc[W,cap,32], kps[W,cap,7], counts[W])."""
+    import torch
+    world = dist.get_world_size()
+
+    def gather(t):
+        t = t.contiguous()
+        out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t)  # rank-major concatenation along dim 0
+        return out.view((world,) + tuple(t.shape))
+
+    g_desc, g_kps, g_cnt = gather(desc), gather(kps), gather(count)
+    return g_desc, g_kps, g_cnt
+
+
+def match_cross_stream(matcher_handle, q_desc, nq, nq_device, g_desc, seg_counts, skip_seg, out, th=50, ratio=0.6,
+                       nmatches=None):
+    """orbmi_match_descriptors_segments over the gathered segments (device tensors)."""
+    world, cap = int(g_desc.shape[0]), int(g_desc.shape[1])
+    check("orbmi_match_descriptors_segments", lib().orbmi_match_descriptors_segments(
+        matcher_handle, _vp(q_desc), int(nq), _vp(nq_device) if nq_device else None, _vp(g_desc.data_ptr()), world, cap,
+        _vp(seg_counts.data_ptr()), int(skip_seg), int(th), float(ratio), _vp(out.data_ptr()),
+        C.byref(nmatches) if nmatches is not None else None))

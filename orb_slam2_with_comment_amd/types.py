@@ -30,7 +30,7 @@ class FrameView(C.Structure):
                 ("cy", C.c_float), ("bf", C.c_float), ("mb", C.c_float), ("min_x", C.c_float),
                 ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
                 ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float), ("nlevels", C.c_int),
-                ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float)]
+                ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float), ("n_device", C.c_void_p)]
 
 
 class FeatureVectorView(C.Structure):
