@@ -2,20 +2,21 @@
 //
 // The g2o schedule -- optimize(5), outlier levels, optimize(10), erase list -- runs as a chain
 // of chip-wide kernels on one stream; the Levenberg control (g2o/core/
-// optimization_algorithm_levenberg.cpp:61-164) stays on the host, which reads four scalars per
-// trial (chi2, scale, solve status) and launches the next trial.  Per LM iteration:
-//   k_ba_errors        thread / edge   computeActiveErrors + robust chi2 (per-block partials)
-//   k_ba_linearize     thread / edge   Jacobians (types_six_dof_expmap.cpp), Huber weights,
-//                                      per-edge Hpl block and its Hll / Hpp / b contributions
-//   k_ba_points        thread / point  Hll, b_l (sum over the point's edges, g2o order)
-//   k_ba_poses         block / pose    Hpp, b_p (fixed-order reduction over the pose's edges)
+// optimization_algorithm_levenberg.cpp:61-164) stays on the host, which reads one small block
+// of partial sums per trial and launches the next trial.  Per LM iteration:
+//   k_ba_linearize     thread / edge   computeActiveErrors + robust chi2, Jacobians
+//                                      (types_six_dof_expmap.cpp), Huber weights, the edge's
+//                                      Hpl block and its Hll / b_l, Hpp / b_p contributions
+//   k_ba_reduce        thread / point  Hll, b_l (sum over the point's edges, g2o order)
+//                      block / pose    Hpp, b_p (fixed-order sum over the keyframe's edges)
 // per trial (lambda):
-//   k_ba_point_schur   thread / edge   D = Hll + lambda I, D^-1, B D^-1 and B D^-1 b_l per edge
-//   k_ba_schur_blocks  block / (pose i <= pose j)  H_schur(i,j) = Hpp - sum_points B_i D^-1 B_j^T,
-//                                      b_schur(i) = b_p - sum B_i D^-1 b_l (pair lists built once)
-//   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system in LDS
-//   k_ba_update        thread / point, pose   back substitution, x + dx, exp(dx) * T, scale
-//   k_ba_errors        on the trial state, then k_ba_scalars reduces the partials
+//   k_ba_schur         block / (pose i <= pose j)  H_schur(i,j) = Hpp + lambda I - sum_points
+//                                      B_i D^-1 B_j^T over observation pairs (lists built once),
+//                                      b_schur = b_p - sum B D^-1 b_l; lambda init on iteration 0
+//   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system,
+//                                      triangular solves
+//   k_ba_pose_trial    thread / pose   trial poses exp(dx) * T, poses' part of computeScale
+//   k_ba_update_errors thread / point  back substitution x + dx, trial errors, computeScale
 // The g2o semantics kept: lambda init tau = 1e-5, rho test with computeScale + 1e-3, the
 // ORB-SLAM "3 bad iterations" stop, stale edge errors after a rejected trial, push/pop of
 // the estimates (pointer swap of current / trial buffers), Huber kernels removed for the
@@ -28,6 +29,10 @@
 
 #include "extractor.h"
 
+// fp64 solver with a 1e-4 parity tolerance: multiply-add contraction allowed here (the
+// bit-exact extractor / matcher sources keep -ffp-contract=off)
+#pragma clang fp contract(fast)
+
 namespace orbmi {
 
 constexpr int kBaMaxPoses = 30;                        // 6*30 = 180 unknowns
@@ -35,7 +40,6 @@ constexpr int kBaMaxN = 6 * kBaMaxPoses;
 constexpr int kBaPacked = kBaMaxN * (kBaMaxN + 1) / 2;  // 16290 doubles = 127 KiB
 constexpr int kBaMaxKf = 1024;
 constexpr int kBaBlock = 256;
-constexpr int kBaSolveThreads = 256;
 
 struct BaDev {
     int nkf, npt, nedge, nblk;
@@ -46,6 +50,8 @@ struct BaDev {
     const int* pt_start;       // edges of point p: [pt_start[p], pt_start[p+1])
     const int* kf_start;       // CSR by keyframe over edge indices
     const int* kf_edges;
+    const int* kf_pos;         // position of edge e in the keyframe CSR (kf_edges[kf_pos[e]] == e)
+    const int* kf_pt;          // point of the edge at keyframe-CSR position j
     const int* blk_kf;         // nblk x 2: keyframes (a, b), id(a) <= id(b), both not fixed
     const int* blk_start;      // nblk + 1
     const int2* blk_pairs;     // (e_a, e_b): edges of one point into keyframes a and b
@@ -53,21 +59,18 @@ struct BaDev {
     unsigned char* eflag;      // bit0 level-1, bit1 no robust kernel, bit2 active
     int* pose_idx;             // nkf
     int* pose_kf;              // kBaMaxPoses
+    int* e_pi;                 // nedge: pose index of the edge's keyframe (-1 fixed / inactive)
     double* Hpl;               // nedge x 18 (pose rows x point cols)
     double* Hle;               // nedge x 9: edge's Hll upper (6) + b_l (3)
-    double* Hpe;               // nedge x 27: edge's Hpp upper (21) + b_p (6)
+    double* Hpe;               // nedge x 27 in keyframe-CSR order: edge's Hpp upper (21) + b_p (6)
     double* Hll;               // npt x 9
     double* bl;                // npt x 3
-    double* Dinv;              // npt x 9
-    double* BD;                // nedge x 18: B D^-1
-    double* Bdb;               // nedge x 6: B D^-1 b_l
     double* Hpp;               // kBaMaxPoses x 36
     double* bp;                // kBaMaxPoses x 6
     double* S;                 // packed upper reduced system (kBaPacked)
     double* bs;                // kBaMaxN
     double* xp;                // kBaMaxN
-    double* part;              // per-block partial sums
-    double* scal;              // scalars read by the host
+    double* scal;              // [1] poses' computeScale part, [2] solve ok, [3] lambda used
     int* istat;                // [0] np, [1] nl, [2] too many poses, [3] solve ok
 };
 
@@ -146,7 +149,7 @@ __device__ inline void se3_oplus(const double* u, const double* Tin, double* Tou
             for (int j = 0; j < 3; j++) { R[i][j] = (i == j) + O[i][j] + O2[i][j]; V[i][j] = R[i][j]; }
     } else {
         const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / pow(theta, 3);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 R[i][j] = (i == j) + a * O[i][j] + b * O2[i][j];
@@ -171,11 +174,12 @@ __device__ inline void se3_oplus(const double* u, const double* Tin, double* Tou
 // ---------------------------------------------------------------- edges
 __device__ inline bool edge_stereo(const orbmi_ba_edge& e) { return !(e.ur < 0); }
 
-__device__ inline void edge_error(const BaDev& a, int i, const double* T, const double* X, double* err) {
+// error of edge i with the point's position at Xp (3 doubles)
+__device__ inline void edge_error_at(const BaDev& a, int i, const double* T, const double* Xp, double* err) {
     const orbmi_ba_edge e = a.edges[i];
     const orbmi_ba_keyframe& kf = a.kfs[e.kf];
     double p[3];
-    se3_map(T + 8 * e.kf, X + 4 * e.point, p);
+    se3_map(T + 8 * e.kf, Xp, p);
     if (!edge_stereo(e)) {
         const double px = p[0] / p[2], py = p[1] / p[2];
         err[0] = (double)e.u - (px * (double)kf.fx + (double)kf.cx);
@@ -190,6 +194,10 @@ __device__ inline void edge_error(const BaDev& a, int i, const double* T, const 
         err[1] = (double)e.v - r1;
         err[2] = (double)e.ur - r2;
     }
+}
+
+__device__ inline void edge_error(const BaDev& a, int i, const double* T, const double* X, double* err) {
+    edge_error_at(a, i, T, X + 4 * a.edges[i].point, err);
 }
 
 __device__ inline double edge_chi2(const BaDev& a, int i) {
@@ -367,6 +375,8 @@ __global__ __launch_bounds__(1024) void k_ba_activate(BaDev a) {
         a.istat[1] = nl;
         a.istat[2] = n > kBaMaxPoses;
     }
+    __syncthreads();
+    for (int i = tid; i < a.nedge; i += blockDim.x) a.e_pi[i] = a.pose_idx[a.edges[i].kf];
 }
 
 // ---------------------------------------------------------------- errors
@@ -388,69 +398,125 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a, const double* _
 }
 
 // ---------------------------------------------------------------- linear system
-// BaseBinaryEdge::constructQuadraticForm per edge (base_binary_edge.hpp:55-120)
-__global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a, const double* __restrict__ T,
-                                                           const double* __restrict__ X) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.nedge || !(a.eflag[i] & 4)) return;
-    double Jl[3][3], Jp[3][6], w, om[3];
-    edge_jacobians(a, i, T, X, Jl, Jp);
-    edge_weights(a, i, &w, om);
-    double* He = a.Hle + 9 * (long long)i;
-    int q = 0;
+// D^-1 of the point's damped 3x3 block, Hll + lambda I (cofactors)
+__device__ inline void point_dinv(const BaDev& a, int p, double lam, double Di[9]) {
+    double D[3][3];
     for (int r = 0; r < 3; r++)
-        for (int c = r; c < 3; c++, q++)
-            He[q] = Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
-    for (int r = 0; r < 3; r++) He[6 + r] = Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
-    if (a.pose_idx[a.edges[i].kf] < 0) return;
-    double* B = a.Hpl + 18 * (long long)i;
-    for (int r = 0; r < 6; r++)
-        for (int c = 0; c < 3; c++) B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
-    double* Hp = a.Hpe + 27 * (long long)i;
-    q = 0;
-    for (int r = 0; r < 6; r++)
-        for (int c = r; c < 6; c++, q++)
-            Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
-    for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
+        for (int c = 0; c < 3; c++) D[r][c] = a.Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
+    const double c00 = D[1][1] * D[2][2] - D[1][2] * D[2][1];
+    const double c10 = D[1][2] * D[2][0] - D[1][0] * D[2][2];
+    const double c20 = D[1][0] * D[2][1] - D[1][1] * D[2][0];
+    const double det = D[0][0] * c00 + D[0][1] * c10 + D[0][2] * c20;
+    const double id = 1.0 / det;
+    Di[0] = c00 * id; Di[3] = c10 * id; Di[6] = c20 * id;
+    Di[1] = (D[0][2] * D[2][1] - D[0][1] * D[2][2]) * id;
+    Di[4] = (D[0][0] * D[2][2] - D[0][2] * D[2][0]) * id;
+    Di[7] = (D[0][1] * D[2][0] - D[0][0] * D[2][1]) * id;
+    Di[2] = (D[0][1] * D[1][2] - D[0][2] * D[1][1]) * id;
+    Di[5] = (D[0][2] * D[1][0] - D[0][0] * D[1][2]) * id;
+    Di[8] = (D[0][0] * D[1][1] - D[0][1] * D[1][0]) * id;
 }
 
-// Hll, b_l: sum over the point's active edges in edge order
-__global__ __launch_bounds__(kBaBlock) void k_ba_points(BaDev a) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.npt) return;
-    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++) {
-        if (!(a.eflag[i] & 4)) continue;
-        const double* He = a.Hle + 9 * (long long)i;
-        for (int k = 0; k < 6; k++) h[k] += He[k];
-        for (int k = 0; k < 3; k++) b[k] += He[6 + k];
-    }
-    double* H = a.Hll + 9 * p;
-    H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
-    H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
-    H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
-    for (int k = 0; k < 3; k++) a.bl[3 * p + k] = b[k];
-}
-
-// Hpp, b_p: one block per free pose; each half-wave sums one edge's 27 values per step
-// (lane = value), then a fixed-order sum over the half-waves
-constexpr int kBaPoseThreads = 512;
-__global__ __launch_bounds__(kBaPoseThreads) void k_ba_poses(BaDev a) {
-    __shared__ double red[2 * kBaPoseThreads / 64][27];
-    const int pi = blockIdx.x, k = a.pose_kf[pi];
-    const int lane = threadIdx.x & 63, hw = threadIdx.x >> 5, q = lane & 31;
-    const int nhw = kBaPoseThreads / 32;
-    double v = 0;
-    if (q < 27)
-        for (int j = a.kf_start[k] + hw; j < a.kf_start[k + 1]; j += nhw) {
-            const int i = a.kf_edges[j];
-            if (a.eflag[i] & 4) v += a.Hpe[27 * (long long)i + q];
+// thread per edge: computeActiveErrors + robust chi2 (block partials), then
+// BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:55-120): Hpl block, the
+// edge's Hll / b_l and Hpp / b_p contributions.  Inactive edges into free poses write zeros,
+// so the reductions and the Schur products need no activity tests.
+__global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a, const double* __restrict__ T,
+                                                           const double* __restrict__ X, double* __restrict__ part) {
+    __shared__ double red[kBaBlock / 64];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double chi = 0;
+    if (i < a.nedge) {
+        const bool free_pose = a.e_pi[i] >= 0;
+        double* Hp = a.Hpe + 27 * (long long)a.kf_pos[i];
+        double* B = a.Hpl + 18 * (long long)i;
+        if (!(a.eflag[i] & 4)) {
+            if (free_pose) {
+                for (int q = 0; q < 27; q++) Hp[q] = 0;
+                for (int q = 0; q < 18; q++) B[q] = 0;
+            }
+        } else {
+            edge_error(a, i, T, X, a.err + 3 * i);
+            double r0, r1;
+            edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
+            chi = r0;
+            double Jl[3][3], Jp[3][6], w, om[3];
+            edge_jacobians(a, i, T, X, Jl, Jp);
+            edge_weights(a, i, &w, om);
+            double* He = a.Hle + 9 * (long long)i;
+            int q = 0;
+            for (int r = 0; r < 3; r++)
+                for (int c = r; c < 3; c++, q++)
+                    He[q] = Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
+            for (int r = 0; r < 3; r++) He[6 + r] = Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
+            if (free_pose) {
+                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 3; c++)
+                        B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
+                q = 0;
+                for (int r = 0; r < 6; r++)
+                    for (int c = r; c < 6; c++, q++)
+                        Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
+                for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
+            }
         }
-    if (q < 27) red[hw][q] = v;
+    }
+    chi = block_sum<kBaBlock>(chi, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = chi;
+}
+
+// blocks [0, nb_p): thread per point, Hll / b_l summed over its active edges in edge order;
+// blocks [nb_p, nb_p + np): one per free pose, Hpp / b_p over its contiguous keyframe-CSR
+// rows (thread = value x edge lane, fixed-order sum).  part_max = max |diag| per block
+// (computeLambdaInit, optimization_algorithm_levenberg.cpp:166-180).
+constexpr int kBaPoseLanes = kBaBlock / 27;  // 9
+__global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a, int nb_p, double* __restrict__ part_max) {
+    __shared__ double red[kBaPoseLanes][27];
+    __shared__ double redm[kBaBlock / 64];
+    if ((int)blockIdx.x < nb_p) {
+        const int p = blockIdx.x * blockDim.x + threadIdx.x;
+        double m = 0;
+        if (p < a.npt) {
+            double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+            for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++) {
+                if (!(a.eflag[i] & 4)) continue;
+                const double* He = a.Hle + 9 * (long long)i;
+                for (int k = 0; k < 6; k++) h[k] += He[k];
+                for (int k = 0; k < 3; k++) b[k] += He[6 + k];
+            }
+            double* H = a.Hll + 9 * p;
+            H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+            H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+            H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+            for (int k = 0; k < 3; k++) a.bl[3 * p + k] = b[k];
+            m = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
+        }
+        m = block_max<kBaBlock>(m, redm);
+        if (threadIdx.x == 0) part_max[blockIdx.x] = m;
+        return;
+    }
+    const int pi = blockIdx.x - nb_p, k = a.pose_kf[pi];
+    const int q = threadIdx.x % 27, el = threadIdx.x / 27;
+    if (el < kBaPoseLanes) {
+        double v = 0;
+        const double* base = a.Hpe + 27 * (long long)a.kf_start[k] + q;
+        const int n = a.kf_start[k + 1] - a.kf_start[k];
+        double v1 = 0, v2 = 0, v3 = 0;  // four loads in flight per lane
+        int m = el;
+        for (; m + 3 * kBaPoseLanes < n; m += 4 * kBaPoseLanes) {
+            v += base[27 * (long long)m];
+            v1 += base[27 * (long long)(m + kBaPoseLanes)];
+            v2 += base[27 * (long long)(m + 2 * kBaPoseLanes)];
+            v3 += base[27 * (long long)(m + 3 * kBaPoseLanes)];
+        }
+        for (; m < n; m += kBaPoseLanes) v += base[27 * (long long)m];
+        red[el][q] = (v + v1) + (v2 + v3);
+    }
     __syncthreads();
     if (threadIdx.x < 27) {
         double t = 0;
-        for (int w = 0; w < nhw; w++) t += red[w][threadIdx.x];
+        for (int w = 0; w < kBaPoseLanes; w++) t += red[w][threadIdx.x];
+        red[0][threadIdx.x] = t;  // row 0 is only re-read after the barrier below
         const int qq = threadIdx.x;
         if (qq < 21) {
             int r = 0, c = qq;
@@ -462,65 +528,34 @@ __global__ __launch_bounds__(kBaPoseThreads) void k_ba_poses(BaDev a) {
             a.bp[6 * pi + qq - 21] = t;
         }
     }
-}
-
-// max diagonal of H (computeLambdaInit, optimization_algorithm_levenberg.cpp:166-180)
-__global__ __launch_bounds__(1024) void k_ba_maxdiag(BaDev a) {
-    __shared__ double red[16];
-    const int np = a.istat[0] < kBaMaxPoses ? a.istat[0] : kBaMaxPoses;
-    double m = 0;
-    for (int q = threadIdx.x; q < np * 6; q += blockDim.x) m = fmax(m, fabs(a.Hpp[36 * (q / 6) + (q % 6) * 7]));
-    for (int p = threadIdx.x; p < a.npt; p += blockDim.x)
-        if (point_active(a, p))
-            for (int j = 0; j < 3; j++) m = fmax(m, fabs(a.Hll[9 * p + 4 * j]));
-    m = block_max<1024>(m, red);
-    if (threadIdx.x == 0) a.scal[3] = m;
-}
-
-// ---------------------------------------------------------------- Schur complement
-// thread per edge: D = Hll + lambda I of the edge's point, D^-1 (cofactors; the point's first
-// edge stores it), B D^-1 and B D^-1 b_l for edges into free poses
-__global__ __launch_bounds__(kBaBlock) void k_ba_point_schur(BaDev a, double lam) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.nedge) return;
-    const orbmi_ba_edge ed = a.edges[e];
-    const int p = ed.point;
-    const bool first = e == a.pt_start[p];
-    const bool use = (a.eflag[e] & 4) && a.pose_idx[ed.kf] >= 0;
-    if ((!first && !use) || !point_active(a, p)) return;
-    double D[3][3];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) D[r][c] = a.Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
-    const double c00 = D[1][1] * D[2][2] - D[1][2] * D[2][1];
-    const double c10 = D[1][2] * D[2][0] - D[1][0] * D[2][2];
-    const double c20 = D[1][0] * D[2][1] - D[1][1] * D[2][0];
-    const double det = D[0][0] * c00 + D[0][1] * c10 + D[0][2] * c20;
-    double Di[9];
-    Di[0] = c00 / det; Di[3] = c10 / det; Di[6] = c20 / det;
-    Di[1] = (D[0][2] * D[2][1] - D[0][1] * D[2][2]) / det;
-    Di[4] = (D[0][0] * D[2][2] - D[0][2] * D[2][0]) / det;
-    Di[7] = (D[0][1] * D[2][0] - D[0][0] * D[2][1]) / det;
-    Di[2] = (D[0][1] * D[1][2] - D[0][2] * D[1][1]) / det;
-    Di[5] = (D[0][2] * D[1][0] - D[0][0] * D[1][2]) / det;
-    Di[8] = (D[0][0] * D[1][1] - D[0][1] * D[1][0]) / det;
-    if (first)
-        for (int k = 0; k < 9; k++) a.Dinv[9 * p + k] = Di[k];
-    if (!use) return;
-    const double* blp = a.bl + 3 * p;
-    double db[3];
-    for (int r = 0; r < 3; r++) db[r] = Di[r * 3] * blp[0] + Di[r * 3 + 1] * blp[1] + Di[r * 3 + 2] * blp[2];
-    const double* B = a.Hpl + 18 * (long long)e;
-    double* BD = a.BD + 18 * (long long)e;
-    for (int r = 0; r < 6; r++) {
-        for (int c = 0; c < 3; c++) BD[r * 3 + c] = B[r * 3] * Di[c] + B[r * 3 + 1] * Di[3 + c] + B[r * 3 + 2] * Di[6 + c];
-        a.Bdb[6 * (long long)e + r] = B[r * 3] * db[0] + B[r * 3 + 1] * db[1] + B[r * 3 + 2] * db[2];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // diagonal of the packed upper 6x6: q = 0, 6, 11, 15, 18, 20
+        double m = 0;
+        const int dq[6] = {0, 6, 11, 15, 18, 20};
+        for (int j = 0; j < 6; j++) m = fmax(m, fabs(red[0][dq[j]]));
+        part_max[nb_p + pi] = m;
     }
 }
 
-// one block per pose pair (i <= j): H_schur(i,j) = [Hpp_i + lambda I] - sum B_i D^-1 B_j^T
-// over the points both observe; the diagonal block also writes b_schur(i)
-__global__ __launch_bounds__(kBaBlock) void k_ba_schur_blocks(BaDev a, double lam, int N) {
+// ---------------------------------------------------------------- Schur complement
+// one block per pose pair (i <= j): H_schur(i,j) = [Hpp_i + lambda I] - sum_points
+// B_i D^-1 B_j^T with D^-1 recomputed per observation pair; the diagonal block also writes
+// b_schur(i) = b_p - sum B D^-1 b_l.  lam < 0: lambda = 1e-5 max|diag H| (every block reduces
+// the same partials in the same order; block 0 publishes it in scal[3]).
+__global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int N, const double* __restrict__ part_max,
+                                                       int nmax) {
     __shared__ double red[kBaBlock / 64][42];
+    __shared__ double lam_s;
+    if (lam < 0) {
+        if (threadIdx.x == 0) {
+            double m = 0;
+            for (int k = 0; k < nmax; k++) m = fmax(m, part_max[k]);
+            lam_s = 1e-5 * m;
+        }
+        __syncthreads();
+        lam = lam_s;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
     const int b = blockIdx.x;
     const int ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
     const int i1 = a.pose_idx[ka], i2 = a.pose_idx[kb];
@@ -530,23 +565,38 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur_blocks(BaDev a, double la
 #pragma unroll
     for (int q = 0; q < 36; q++) acc[q] = 0;
     for (int j = a.blk_start[b] + threadIdx.x; j < a.blk_start[b + 1]; j += blockDim.x) {
-        const int2 pr = a.blk_pairs[j];
-        if (!(a.eflag[pr.x] & 4) || !(a.eflag[pr.y] & 4)) continue;
-        const double* BD = a.BD + 18 * (long long)pr.x;
+        const int2 pr = a.blk_pairs[j];  // inactive edges carry a zero Hpl block
+        double Di[9];
+        point_dinv(a, a.edges[pr.x].point, lam, Di);
+        const double* B1 = a.Hpl + 18 * (long long)pr.x;
         const double* B2 = a.Hpl + 18 * (long long)pr.y;
+        double BD[18];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) BD[r * 3 + c] = B1[r * 3] * Di[c] + B1[r * 3 + 1] * Di[3 + c] + B1[r * 3 + 2] * Di[6 + c];
+        double b2[18];
+#pragma unroll
+        for (int q = 0; q < 18; q++) b2[q] = B2[q];
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int c = 0; c < 6; c++)
-                acc[r * 6 + c] += BD[r * 3] * B2[c * 3] + BD[r * 3 + 1] * B2[c * 3 + 1] + BD[r * 3 + 2] * B2[c * 3 + 2];
+                acc[r * 6 + c] += BD[r * 3] * b2[c * 3] + BD[r * 3 + 1] * b2[c * 3 + 1] + BD[r * 3 + 2] * b2[c * 3 + 2];
     }
     double bacc[6] = {0, 0, 0, 0, 0, 0};
     if (diag)
         for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
             const int e = a.kf_edges[j];
-            if (!(a.eflag[e] & 4)) continue;
+            const int p = a.kf_pt[j];
+            double Di[9];
+            point_dinv(a, p, lam, Di);
+            const double* blp = a.bl + 3 * p;
+            double db[3];
+            for (int r = 0; r < 3; r++) db[r] = Di[r * 3] * blp[0] + Di[r * 3 + 1] * blp[1] + Di[r * 3 + 2] * blp[2];
+            const double* B = a.Hpl + 18 * (long long)e;
 #pragma unroll
-            for (int r = 0; r < 6; r++) bacc[r] += a.Bdb[6 * (long long)e + r];
+            for (int r = 0; r < 6; r++) bacc[r] += B[r * 3] * db[0] + B[r * 3 + 1] * db[1] + B[r * 3 + 2] * db[2];
         }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -571,157 +621,273 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur_blocks(BaDev a, double la
 }
 
 // ---------------------------------------------------------------- reduced system solve
-// LDL^T = U^T D U of the packed upper reduced system in LDS, blocked by the 6x6 pose blocks
-// (right-looking): per block step the diagonal block is factored by one wave, the block row
-// is solved column-parallel (W = U_kk^-T A_kj, U_kj = D^-1 W), and the trailing upper
-// triangle takes the rank-6 update A_ij -= W_ki^T U_kj (wave per row, lanes over columns).
-// Then U^T z = b, y = z / D, U x = y by one wave (LinearSolverEigen / SimplicialLDLT
-// equivalent up to rounding order).
+// LDL^T = U^T D U of the reduced camera system, blocked by the 6x6 pose blocks and held in
+// registers: thread t owns block (i, j), i <= j, of the upper triangle (36 doubles).  Block
+// step k (right-looking, two barriers): the owner of (k, k) factors it in registers and
+// publishes U_kk, D_k through LDS; owners of (k, j) solve W = U_kk^-T A_kj, U_kj = D_k^-1 W
+// and publish W, U; owners of (i, j), i > k apply A_ij -= W_ki^T U_kj.  The factor then goes
+// to LDS and one wave runs the blocked U^T z = b, y = z / D, U x = y.  Same factorisation as
+// LinearSolverEigen's SimplicialLDLT up to the rounding order.
+constexpr int kBaSolveThreads = 512;  // >= 465 blocks of 30 poses + 30 right-hand-side blocks
+#ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: phase timestamps of thread 0
+__device__ unsigned long long g_solve_trace[256];
+__device__ unsigned long long g_solve_clk[2];
+#define SOLVE_MARK(i)                                                                        \
+    do {                                                                                     \
+        if (threadIdx.x == 0) {                                                              \
+            g_solve_trace[i] = __builtin_amdgcn_s_memrealtime();                             \
+            if ((i) == 255) g_solve_clk[0] = __builtin_amdgcn_s_memtime();                   \
+            if ((i) == 201) g_solve_clk[1] = __builtin_amdgcn_s_memtime();                   \
+        }                                                                                    \
+    } while (0)
+#else
+#define SOLVE_MARK(i) do {} while (0)
+#endif
+
 __device__ inline void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int N) {
+__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
+    SOLVE_MARK(255);
+    constexpr int kSlot = 37;  // odd stride in doubles: conflict-free LDS rows
     __shared__ double H[kBaPacked];
-    __shared__ double W[6 * kBaMaxN];
+    __shared__ double Wp[(kBaMaxPoses + 1) * kSlot], Up[(kBaMaxPoses + 1) * kSlot];
+    __shared__ double Ud[36], Dinv6[6];
     __shared__ double bs[kBaMaxN];
-    __shared__ int rb[kBaMaxN];   // packed(r, c) = rb[r] + c
+    __shared__ int rb[kBaMaxN];  // packed(r, c) = rb[r] + c
     __shared__ int fail;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
-    const int NP = N * (N + 1) / 2;
-    for (int q = tid; q < NP; q += blockDim.x) H[q] = a.S[q];
-    for (int q = tid; q < N; q += blockDim.x) { bs[q] = a.bs[q]; rb[q] = q * N - q * (q - 1) / 2 - q; }
+    const int N = 6 * np, nblk = np * (np + 1) / 2;
+    const int tid = threadIdx.x;
+    // thread -> block (bi, bj) of the upper triangle, or (bi, np) = block bi of the right-hand
+    // side carried through the factorisation (the forward substitution U^T z = b, D y = z)
+    const bool own = tid < nblk + np;
+    const bool rhs = own && tid >= nblk;
+    int bi = 0, bj = 0;
+    if (rhs) {
+        bi = tid - nblk;
+        bj = np;
+    } else if (own) {
+        int t = tid;
+        while (t >= np - bi) { t -= np - bi; bi++; }
+        bj = bi + t;
+    }
+    const bool dg = !rhs && bi == bj;
+    for (int q = tid; q < N; q += blockDim.x) rb[q] = q * N - q * (q - 1) / 2 - q;
+    double A[36];
+#pragma unroll
+    for (int q = 0; q < 36; q++) {
+        const int r = q / 6, c = q % 6;
+        A[q] = 0.0;
+        if (rhs) { if (c == 0) A[q] = a.bs[6 * bi + r]; }
+        else if (own && (!dg || c >= r)) A[q] = a.S[packed(6 * bi + r, 6 * bj + c, N)];
+    }
     if (tid == 0) fail = 0;
     __syncthreads();
-    for (int k0 = 0; k0 < N; k0 += 6) {
-        // (1) diagonal block, wave 0: lanes own (r, c) of the 6x6 upper block
-        if (wid == 0) {
-            const int r = lane / 6, c = lane % 6;
-            const bool own = lane < 36 && c >= r;
+    SOLVE_MARK(0);
+    for (int k = 0; k < np; k++) {
+        if (own && bi == k && bj == k) {  // (1) diagonal block, column-by-column LDL^T
+            bool bad = false;
+#pragma unroll
             for (int j = 0; j < 6; j++) {
-                const double d = H[rb[k0 + j] + k0 + j];
-                if (!(fabs(d) > 0) || !isfinite(d)) { if (lane == 0) fail = 1; break; }
-                double upd = 0;
-                if (own && r > j) upd = H[rb[k0 + j] + k0 + r] * H[rb[k0 + j] + k0 + c] / d;
-                wave_sync_lds();
-                if (own && r > j) H[rb[k0 + r] + k0 + c] -= upd;
-                if (own && r == j && c > j) H[rb[k0 + j] + k0 + c] /= d;
-                wave_sync_lds();
+                const double d = A[j * 7];
+                bad |= !(fabs(d) > 0) || !isfinite(d);
+                const double inv = 1.0 / d;
+                Dinv6[j] = inv;
+#pragma unroll
+                for (int c = j + 1; c < 6; c++) {
+                    const double u = A[j * 6 + c] * inv;  // u_jc
+#pragma unroll
+                    for (int r = j + 1; r <= c; r++) A[r * 6 + c] -= A[j * 6 + r] * u;
+                }
+#pragma unroll
+                for (int c = j + 1; c < 6; c++) A[j * 6 + c] *= inv;
             }
+#pragma unroll
+            for (int q = 0; q < 36; q++) Ud[q] = A[q];
+            if (bad) fail = 1;
         }
         __syncthreads();
+        SOLVE_MARK(1 + 3 * k);
         if (fail) break;
-        const int c0 = k0 + 6;
-        if (c0 >= N) break;
-        // (2) block row: one thread per column
-        for (int c = c0 + tid; c < N; c += blockDim.x) {
-            double w[6];
+        if (own && bi == k && bj > k) {  // (2) block row: W = U_kk^-T A_kj, U_kj = D^-1 W
+            double ud[15], di[6];
 #pragma unroll
-            for (int t = 0; t < 6; t++) {
-                double v = H[rb[k0 + t] + c];
+            for (int t = 0; t < 6; t++) di[t] = Dinv6[t];
+            {
+                int q = 0;
 #pragma unroll
-                for (int s2 = 0; s2 < t; s2++) v -= H[rb[k0 + s2] + k0 + t] * w[s2];
-                w[t] = v;
+                for (int t = 1; t < 6; t++)
+#pragma unroll
+                    for (int s2 = 0; s2 < t; s2++, q++) ud[q] = Ud[s2 * 6 + t];
             }
 #pragma unroll
-            for (int t = 0; t < 6; t++) {
-                W[t * kBaMaxN + c] = w[t];
-                H[rb[k0 + t] + c] = w[t] / H[rb[k0 + t] + k0 + t];
+            for (int c = 0; c < 6; c++) {
+                int q = 0;
+#pragma unroll
+                for (int t = 1; t < 6; t++)
+#pragma unroll
+                    for (int s2 = 0; s2 < t; s2++, q++) A[t * 6 + c] -= ud[q] * A[s2 * 6 + c];
             }
-        }
-        __syncthreads();
-        // (3) trailing rank-6 update, wave per row
-        for (int r = c0 + wid; r < N; r += nw) {
-            double wr[6];
 #pragma unroll
-            for (int t = 0; t < 6; t++) wr[t] = W[t * kBaMaxN + r];
-            const int base = rb[r];
-            for (int c = r + lane; c < N; c += 64) {
-                double s2 = 0;
-#pragma unroll
-                for (int t = 0; t < 6; t++) s2 += wr[t] * H[rb[k0 + t] + c];
-                H[base + c] -= s2;
+            for (int q = 0; q < 36; q++) {
+                Wp[bj * kSlot + q] = A[q];
+                A[q] *= di[q / 6];
+                Up[bj * kSlot + q] = A[q];
             }
         }
         __syncthreads();
+        SOLVE_MARK(2 + 3 * k);
+        if (own && bi > k) {  // (3) trailing update of the owned block
+            double w[36];
+#pragma unroll
+            for (int q = 0; q < 36; q++) w[q] = Wp[bi * kSlot + q];
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                if (rhs && c > 0) continue;
+                double u[6];
+#pragma unroll
+                for (int t = 0; t < 6; t++) u[t] = Up[bj * kSlot + t * 6 + c];
+#pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    if (dg && c < r) continue;
+                    double s2 = 0;
+#pragma unroll
+                    for (int t = 0; t < 6; t++) s2 += w[t * 6 + r] * u[t];
+                    A[r * 6 + c] -= s2;
+                }
+            }
+        }
+#ifdef ORBMI_SOLVE_TRACE
+        __syncthreads();
+        SOLVE_MARK(3 + 3 * k);
+#endif
     }
     if (fail) {
         if (tid == 0) a.istat[3] = 0;
         return;
     }
-    if (wid != 0) return;
-    // one wave: U^T z = b ; y = z / D ; U x = y
-    for (int k = 0; k < N; k++) {
-        const double zk = bs[k];
-        for (int jj = k + 1 + lane; jj < N; jj += 64) bs[jj] -= H[rb[k] + jj] * zk;
+    // factor to LDS (packed upper, U above the diagonal) and y to bs
+    if (own && !rhs) {
+#pragma unroll
+        for (int q = 0; q < 36; q++) {
+            const int r = q / 6, c = q % 6;
+            if (!dg || c >= r) H[rb[6 * bi + r] + 6 * bj + c] = A[q];
+        }
+    }
+    if (rhs)
+#pragma unroll
+        for (int r = 0; r < 6; r++) bs[6 * bi + r] = A[r * 6];
+    __syncthreads();
+    SOLVE_MARK(200);
+    if (tid >= 64) return;
+    const int lane = tid;
+    SOLVE_MARK(202);
+    // U x = y, blocked from the last block up (one wave)
+    for (int k = np - 1; k >= 0; k--) {
+        const int k0 = 6 * k;
+        double x[6];
+#pragma unroll
+        for (int t = 5; t >= 0; t--) {
+            double v = bs[k0 + t];
+#pragma unroll
+            for (int s2 = t + 1; s2 < 6; s2++) v -= H[rb[k0 + t] + k0 + s2] * x[s2];
+            x[t] = v;
+        }
+        for (int jj = lane; jj < k0; jj += 64) {
+            const int base = rb[jj] + k0;
+            double v = bs[jj];
+#pragma unroll
+            for (int t = 0; t < 6; t++) v -= H[base + t] * x[t];
+            bs[jj] = v;
+        }
+        if (lane < 6) {
+#pragma unroll
+            for (int t = 0; t < 6; t++)
+                if (t == lane) a.xp[k0 + t] = x[t];
+        }
         wave_sync_lds();
     }
-    for (int k = lane; k < N; k += 64) bs[k] /= H[rb[k] + k];
-    wave_sync_lds();
-    for (int k = N - 1; k >= 0; k--) {
-        const double xk = bs[k];
-        for (int jj = lane; jj < k; jj += 64) bs[jj] -= H[rb[jj] + k] * xk;
-        wave_sync_lds();
-    }
-    for (int k = lane; k < N; k += 64) a.xp[k] = bs[k];
-    if (lane == 0) a.istat[3] = 1;
+    SOLVE_MARK(201);
+    if (tid == 0) a.istat[3] = 1;
 }
 
-// ---------------------------------------------------------------- update
-// x_l = D^-1 (b_l - Hpl^T x_p); trial estimates (push/pop by buffer swap); computeScale
-__global__ __launch_bounds__(kBaBlock) void k_ba_update(BaDev a, double lam, int N, const double* __restrict__ T,
-                                                        const double* __restrict__ X, double* __restrict__ Tt,
-                                                        double* __restrict__ Xt, double* __restrict__ part) {
-    __shared__ double red[kBaBlock / 64];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
+// computeScale, sum x_p (lambda x_p + b_p) in index order; copies T when the solve failed
+__global__ __launch_bounds__(kBaBlock) void k_ba_pose_trial(BaDev a, int np, double lam, const double* __restrict__ T,
+                                                            double* __restrict__ Tt) {
     const bool ok = a.istat[3] != 0;
-    double s = 0;
-    if (i < a.npt) {
+    if (lam < 0) lam = a.scal[3];
+    for (int k = threadIdx.x; k < a.nkf; k += blockDim.x) {
+        const int pi = a.pose_idx[k];
+        if (ok && pi >= 0) se3_oplus(a.xp + 6 * pi, T + 8 * k, Tt + 8 * k);
+        else
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+    }
+    if (threadIdx.x == 0) {
+        double sc = 0;
+        if (ok)
+            for (int q = 0; q < 6 * np; q++) sc += a.xp[q] * (lam * a.xp[q] + a.bp[q]);
+        a.scal[1] = sc;
+        a.scal[2] = ok ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------- update + trial errors
+// block = 32 points.  Threads 0..31: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
+// part); then every thread takes edges of the block's points: computeActiveErrors on the trial
+// state (T_t from k_ba_pose_trial).  Block partials: robust chi2 and scale.
+constexpr int kBaUpdPts = 32;
+__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a, double lam, const double* __restrict__ X,
+                                                               const double* __restrict__ Tt, double* __restrict__ Xt,
+                                                               double* __restrict__ part_chi,
+                                                               double* __restrict__ part_scale) {
+    __shared__ double red[kBaBlock / 64];
+    __shared__ double xs[kBaUpdPts][4];
+    if (lam < 0) lam = a.scal[3];
+    const bool ok = a.istat[3] != 0;
+    const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
+    double sc = 0, chi = 0;
+    if (threadIdx.x < kBaUpdPts && p0 + (int)threadIdx.x < p1) {
+        const int p = p0 + threadIdx.x;
         double xl[3] = {0, 0, 0};
-        if (ok && point_active(a, i)) {
-            double cl[3] = {a.bl[3 * i], a.bl[3 * i + 1], a.bl[3 * i + 2]};
-            for (int e = a.pt_start[i]; e < a.pt_start[i + 1]; e++) {
-                if (!(a.eflag[e] & 4)) continue;
-                const int i1 = a.pose_idx[a.edges[e].kf];
-                if (i1 < 0) continue;
+        if (ok && point_active(a, p)) {
+            double cl[3] = {a.bl[3 * p], a.bl[3 * p + 1], a.bl[3 * p + 2]};
+            for (int e = a.pt_start[p]; e < a.pt_start[p + 1]; e++) {
+                const int i1 = a.e_pi[e];
+                if (i1 < 0) continue;  // inactive edges into free poses carry a zero block
                 const double* B = a.Hpl + 18 * (long long)e;
                 for (int c = 0; c < 3; c++)
                     for (int r = 0; r < 6; r++) cl[c] -= B[r * 3 + c] * a.xp[6 * i1 + r];
             }
-            const double* Di = a.Dinv + 9 * i;
+            double Di[9];
+            point_dinv(a, p, lam, Di);
             for (int r = 0; r < 3; r++) xl[r] = Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1] + Di[r * 3 + 2] * cl[2];
         }
         for (int r = 0; r < 3; r++) {
-            Xt[4 * i + r] = X[4 * i + r] + xl[r];
-            if (ok) s += xl[r] * (lam * xl[r] + a.bl[3 * i + r]);
+            const double x = X[4 * p + r] + xl[r];
+            Xt[4 * p + r] = x;
+            xs[threadIdx.x][r] = x;
+            if (ok) sc += xl[r] * (lam * xl[r] + a.bl[3 * p + r]);
         }
     }
-    if (i < a.nkf) {
-        const int pi = a.pose_idx[i];
-        if (ok && pi >= 0) se3_oplus(a.xp + 6 * pi, T + 8 * i, Tt + 8 * i);
-        else for (int q = 0; q < 8; q++) Tt[8 * i + q] = T[8 * i + q];
-    }
-    if (ok && i < N) s += a.xp[i] * (lam * a.xp[i] + a.bp[i]);
-    s = block_sum<kBaBlock>(s, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
-}
-
-// fixed-order sums of the partials -> scal[slot], solve status -> scal[2]
-__global__ __launch_bounds__(1024) void k_ba_scalars(BaDev a, const double* __restrict__ p0, int n0,
-                                                     const double* __restrict__ p1, int n1) {
-    __shared__ double red[16];
-    double s = 0;
-    for (int k = threadIdx.x; k < n0; k += blockDim.x) s += p0[k];
-    s = block_sum<1024>(s, red);
-    double t = 0;
-    for (int k = threadIdx.x; k < n1; k += blockDim.x) t += p1[k];
-    t = block_sum<1024>(t, red);
+    __syncthreads();
+    if (p0 < p1)
+        for (int e = a.pt_start[p0] + threadIdx.x; e < a.pt_start[p1]; e += blockDim.x) {
+            if (!(a.eflag[e] & 4)) continue;
+            const orbmi_ba_edge ed = a.edges[e];
+            edge_error_at(a, e, Tt, &xs[ed.point - p0][0], a.err + 3 * e);
+            double r0, r1;
+            edge_robust(a, e, edge_chi2(a, e), &r0, &r1);
+            chi += r0;
+        }
+    chi = block_sum<kBaBlock>(chi, red);
+    sc = block_sum<kBaBlock>(sc, red);
     if (threadIdx.x == 0) {
-        a.scal[0] = s;
-        a.scal[1] = t;
-        a.scal[2] = a.istat[3];
+        part_chi[blockIdx.x] = chi;
+        part_scale[blockIdx.x] = sc;
     }
 }
 
@@ -763,7 +929,8 @@ struct orbmi_ba {
     hipStream_t stream = nullptr;
     uint8_t* d_buf = nullptr;
     size_t cap = 0;
-    double* h_scal = nullptr;  // pinned readback of the per-trial scalars
+    double* h_rb = nullptr;    // pinned readback of the per-trial scalars and partial sums
+    size_t cap_rb = 0;
     int* h_istat = nullptr;
 };
 
@@ -775,16 +942,25 @@ struct Runner {
     orbmi_ba& h;
     BaDev a;
     double *T, *Tt, *X, *Xt;
-    double *part_e, *part_u;
-    int nb_e, nb_u, nb_p, nb_n;
+    double* rb;        // device readback region: scal[8] | linearize chi2 | trial chi2 | trial scale
+    double* part_max;  // nb_p + np partial maxima of |diag H|
+    int nb_e, nb_p, nb_q;  // blocks: edges, points (256 / block), points (32 / block)
     const volatile int* stop;
     int np = 0, nl = 0;
 
     bool stopped() const { return stop && *stop; }
-    int grid(int n) const { return std::max(1, (n + kBaBlock - 1) / kBaBlock); }
+    double* lin() const { return rb + 8; }
+    double* tchi() const { return rb + 8 + nb_e; }
+    double* tscale() const { return rb + 8 + nb_e + nb_q; }
+    static double sum(const double* p, int n) {  // fixed order
+        double s = 0;
+        for (int k = 0; k < n; k++) s += p[k];
+        return s;
+    }
 
-    int read_scalars() {
-        ORBMI_HIP(hipMemcpyAsync(h.h_scal, a.scal, 8 * sizeof(double), hipMemcpyDeviceToHost, h.stream));
+    int readback() {
+        ORBMI_HIP(hipMemcpyAsync(h.h_rb, rb, (8 + nb_e + 2 * (size_t)nb_q) * sizeof(double), hipMemcpyDeviceToHost,
+                                 h.stream));
         ORBMI_HIP(hipStreamSynchronize(h.stream));
         return ORBMI_OK;
     }
@@ -801,46 +977,38 @@ struct Runner {
 
     // activeRobustChi2 on the (stale) stored errors
     int robust_chi2(double* out) {
-        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 0, part_e);
-        hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_e, 0);
-        int rc = read_scalars();
-        *out = h.h_scal[0];
+        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 0, lin());
+        int rc = readback();
+        *out = sum(h.h_rb + 8, nb_e);
         return rc;
     }
 
-    // OptimizationAlgorithmLevenberg::solve (levenberg.cpp:61-164); *terminate = 1 on stop
+    // OptimizationAlgorithmLevenberg::solve (levenberg.cpp:61-164); *terminate = 1 on stop.
+    // Per trial: k_ba_schur, k_ba_solve, k_ba_update_errors and one readback of the partials.
     int lm_iteration(int iteration, double* lambda, double* ni, int* nbad, int* terminate) {
         const int N = 6 * np;
-        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 1, part_e);
-        hipLaunchKernelGGL(k_ba_linearize, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X);
-        hipLaunchKernelGGL(k_ba_points, dim3(nb_p), dim3(kBaBlock), 0, h.stream, a);
-        if (np > 0) hipLaunchKernelGGL(k_ba_poses, dim3(np), dim3(kBaPoseThreads), 0, h.stream, a);
-        if (iteration == 0) hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(1024), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_e, 0);
-        int rc;
-        if ((rc = read_scalars())) return rc;
-        double currentChi = h.h_scal[0];
-        const double iniChi = currentChi;
-        if (iteration == 0) {  // computeLambdaInit, tau = 1e-5
-            *lambda = 1e-5 * h.h_scal[3];
-            *ni = 2;
-            *nbad = 0;
-        }
-        double rho = 0;
-        int qmax = 0;
+        hipLaunchKernelGGL(k_ba_linearize, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, lin());
+        hipLaunchKernelGGL(k_ba_reduce, dim3(nb_p + np), dim3(kBaBlock), 0, h.stream, a, nb_p, part_max);
+        double lam_arg = iteration == 0 ? -1.0 : *lambda;  // -1: computeLambdaInit on the device
+        if (iteration == 0) { *ni = 2; *nbad = 0; }
+        double currentChi = 0, iniChi = 0, rho = 0;
+        int qmax = 0, rc;
         do {
-            const double lam = *lambda;
-            hipLaunchKernelGGL(k_ba_point_schur, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, lam);
             if (a.nblk > 0)
-                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(a.nblk), dim3(kBaBlock), 0, h.stream, a, lam, N);
-            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, N);
-            hipLaunchKernelGGL(k_ba_update, dim3(nb_u), dim3(kBaBlock), 0, h.stream, a, lam, N, T, X, Tt, Xt, part_u);
-            hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, Tt, Xt, 1, part_e);
-            hipLaunchKernelGGL(k_ba_scalars, dim3(1), dim3(1024), 0, h.stream, a, part_e, nb_e, part_u, nb_u);
-            if ((rc = read_scalars())) return rc;
-            const bool ok2 = h.h_scal[2] != 0;
-            double tempChi = ok2 ? h.h_scal[0] : DBL_MAX;
-            const double scale = ok2 ? h.h_scal[1] : 0.0;
+                hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk), dim3(kBaBlock), 0, h.stream, a, lam_arg, N, part_max,
+                                   nb_p + np);
+            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np);
+            hipLaunchKernelGGL(k_ba_pose_trial, dim3(1), dim3(kBaBlock), 0, h.stream, a, np, lam_arg, T, Tt);
+            hipLaunchKernelGGL(k_ba_update_errors, dim3(nb_q), dim3(kBaBlock), 0, h.stream, a, lam_arg, X, Tt, Xt,
+                               tchi(), tscale());
+            ORBMI_HIP(hipGetLastError());
+            if ((rc = readback())) return rc;
+            const double* hb = h.h_rb;
+            if (qmax == 0) iniChi = currentChi = sum(hb + 8, nb_e);  // computeActiveErrors at entry
+            if (lam_arg < 0) *lambda = hb[3];                       // lambda chosen on the device
+            const bool ok2 = hb[2] != 0;
+            const double tempChi = ok2 ? sum(hb + 8 + nb_e, nb_q) : DBL_MAX;
+            const double scale = ok2 ? sum(hb + 8 + nb_e + nb_q, nb_q) + hb[1] : 0.0;
             rho = (currentChi - tempChi) / (scale + 1e-3);
             if (rho > 0 && std::isfinite(tempChi)) {  // accept: the trial buffers become current
                 double alpha = 1. - std::pow((2 * rho - 1), 3);
@@ -855,6 +1023,7 @@ struct Runner {
                 *lambda *= *ni;
                 *ni *= 2;
             }
+            lam_arg = *lambda;
             qmax++;
         } while (rho < 0 && qmax < 10 && !stopped());
         if (qmax == 10 || rho == 0) { *terminate = 1; return ORBMI_OK; }
@@ -894,7 +1063,7 @@ int orbmi_ba_create(int device, orbmi_ba** out) {
     if (!b) return ORBMI_E_ARG;
     b->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&b->h_scal, 8 * sizeof(double)) != hipSuccess ||
+
         hipHostMalloc((void**)&b->h_istat, 4 * sizeof(int)) != hipSuccess) {
         orbmi_ba_destroy(b);
         return ORBMI_E_HIP;
@@ -908,7 +1077,7 @@ void orbmi_ba_destroy(orbmi_ba* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     if (b->d_buf) (void)hipFree(b->d_buf);
-    if (b->h_scal) (void)hipHostFree(b->h_scal);
+    if (b->h_rb) (void)hipHostFree(b->h_rb);
     if (b->h_istat) (void)hipHostFree(b->h_istat);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
@@ -942,9 +1111,15 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     for (int i = 0; i < ne; i++) { pt_start[P->edges[i].point + 1]++; kf_start[P->edges[i].kf + 1]++; }
     for (int p = 0; p < npt; p++) pt_start[p + 1] += pt_start[p];
     for (int k = 0; k < nkf; k++) kf_start[k + 1] += kf_start[k];
+    std::vector<int> kf_pos(std::max(ne, 1)), kf_pt(std::max(ne, 1));
     {
         std::vector<int> fill(kf_start.begin(), kf_start.end() - 1);
-        for (int i = 0; i < ne; i++) kf_edges[fill[P->edges[i].kf]++] = i;
+        for (int i = 0; i < ne; i++) {
+            const int j = fill[P->edges[i].kf]++;
+            kf_pos[i] = j;
+            kf_edges[j] = i;
+            kf_pt[j] = P->edges[i].point;
+        }
     }
     for (int k = 0; k < nkf; k++) order[k] = k;
     std::stable_sort(order.begin(), order.begin() + nkf, [&](int x, int y) { return P->kfs[x].id < P->kfs[y].id; });
@@ -989,21 +1164,20 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const int npair = blk_start[nblk];
     // one device arena
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
-    const int nb_u = std::max(1, (std::max(std::max(npt, nkf), kBaMaxN) + kBaBlock - 1) / kBaBlock);
+    const int nb_q = std::max(1, (npt + kBaUpdPts - 1) / kBaUpdPts);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += al(std::max(bytes, (size_t)8)); return o; };
     const size_t o_kfs = take(sizeof(orbmi_ba_keyframe) * nkf), o_pts = take(sizeof(orbmi_ba_point) * npt),
                  o_edges = take(sizeof(orbmi_ba_edge) * ne), o_order = take(4 * nkf), o_pts_start = take(4 * (npt + 1)),
-                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
+                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne), o_kf_pt = take(4 * (size_t)ne), o_e_pi = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
                  o_blk_start = take(4 * ((size_t)nblk + 1)), o_pairs = take(8 * (size_t)npair),
                  o_T = take(64 * nkf), o_Tt = take(64 * nkf), o_X = take(32 * npt), o_Xt = take(32 * npt),
                  o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_pkf = take(4 * kBaMaxPoses),
                  o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne), o_Hpe = take(216 * (size_t)ne),
-                 o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Dinv = take(72 * npt), o_BD = take(144 * (size_t)ne),
-                 o_Bdb = take(48 * (size_t)ne), o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses),
+                 o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses),
                  o_S = take(8 * (size_t)kBaPacked), o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN),
-                 o_part_e = take(8 * (size_t)nb_e), o_part_u = take(8 * (size_t)nb_u), o_scal = take(64),
+                 o_rb = take(8 * (8 + (size_t)nb_e + 2 * (size_t)nb_q)), o_pmax = take(8 * ((size_t)nb_p + kBaMaxPoses)),
                  o_istat = take(16), o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
     if (off > h.cap) {
         if (h.d_buf) (void)hipFree(h.d_buf);
@@ -1024,6 +1198,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     ORBMI_HIP(up(o_pts_start, pt_start.data(), 4 * (npt + 1)));
     ORBMI_HIP(up(o_kfs_start, kf_start.data(), 4 * (nkf + 1)));
     ORBMI_HIP(up(o_kf_edges, kf_edges.data(), 4 * (size_t)ne));
+    ORBMI_HIP(up(o_kf_pos, kf_pos.data(), 4 * (size_t)ne));
+    ORBMI_HIP(up(o_kf_pt, kf_pt.data(), 4 * (size_t)ne));
     ORBMI_HIP(up(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk));
     ORBMI_HIP(up(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1)));
     ORBMI_HIP(up(o_pairs, pairs.data(), 8 * (size_t)npair));
@@ -1037,19 +1213,29 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.pt_start = (const int*)(B + o_pts_start);
     a.kf_start = (const int*)(B + o_kfs_start);
     a.kf_edges = (const int*)(B + o_kf_edges);
+    a.kf_pos = (const int*)(B + o_kf_pos);
+    a.kf_pt = (const int*)(B + o_kf_pt);
+    a.e_pi = (int*)(B + o_e_pi);
     a.blk_kf = (const int*)(B + o_blk_kf);
     a.blk_start = (const int*)(B + o_blk_start);
     a.blk_pairs = (const int2*)(B + o_pairs);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
     a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf);
     a.Hpl = (double*)(B + o_Hpl); a.Hle = (double*)(B + o_Hle); a.Hpe = (double*)(B + o_Hpe);
-    a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl); a.Dinv = (double*)(B + o_Dinv);
-    a.BD = (double*)(B + o_BD); a.Bdb = (double*)(B + o_Bdb);
+    a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl);
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
-    a.part = (double*)(B + o_part_e); a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
+    a.scal = (double*)(B + o_rb); a.istat = (int*)(B + o_istat);
+    const size_t rb_bytes = 8 * (8 + (size_t)nb_e + 2 * (size_t)nb_q);
+    if (rb_bytes > h.cap_rb) {
+        if (h.h_rb) (void)hipHostFree(h.h_rb);
+        h.h_rb = nullptr;
+        h.cap_rb = 0;
+        ORBMI_HIP(hipHostMalloc((void**)&h.h_rb, rb_bytes));
+        h.cap_rb = rb_bytes;
+    }
     Runner r{h, a, (double*)(B + o_T), (double*)(B + o_Tt), (double*)(B + o_X), (double*)(B + o_Xt),
-             (double*)(B + o_part_e), (double*)(B + o_part_u), nb_e, nb_u, nb_p, 0, stop};
+             (double*)(B + o_rb), (double*)(B + o_pmax), nb_e, nb_p, nb_q, stop};
     unsigned char* out_erase = B + o_oerase;
     hipLaunchKernelGGL(k_ba_setup, dim3(std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock)),
                        dim3(kBaBlock), 0, s, a, r.T, r.X, out_erase);
