@@ -40,7 +40,7 @@ void Matcher::arena_reset() {
 void Matcher::release() {
     (void)hipSetDevice(device);
     if (own_stream && stream) (void)hipStreamSynchronize(stream);
-    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_res, d_bin_of, d_hist, d_scalars, d_track};
+    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_top, d_res, d_bin_of, d_hist, d_scalars, d_track};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (Block& b : arena) (void)hipFree(b.p);

@@ -13,9 +13,9 @@
 //   k_ba_schur         block / (pose i <= pose j)  H_schur(i,j) = Hpp + lambda I - sum_points
 //                                      B_i D^-1 B_j^T over observation pairs (lists built once),
 //                                      b_schur = b_p - sum B D^-1 b_l; lambda init on iteration 0
-//   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system,
-//                                      triangular solves
-//   k_ba_pose_trial    thread / pose   trial poses exp(dx) * T, poses' part of computeScale
+//   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system with the
+//                                      right-hand side carried through, back substitution,
+//                                      trial poses exp(dx) * T, poses' part of computeScale
 //   k_ba_update_errors thread / point  back substitution x + dx, trial errors, computeScale
 // The g2o semantics kept: lambda init tau = 1e-5, rho test with computeScale + 1e-3, the
 // ORB-SLAM "3 bad iterations" stop, stale edge errors after a rejected trial, push/pop of
@@ -42,7 +42,7 @@ constexpr int kBaMaxKf = 1024;
 constexpr int kBaBlock = 256;
 
 struct BaDev {
-    int nkf, npt, nedge, nblk;
+    int nkf, npt, nedge, nblk, nf;  // nf = non-fixed keyframes (nblk = nf (nf + 1) / 2)
     const orbmi_ba_keyframe* kfs;
     const orbmi_ba_point* pts;
     const orbmi_ba_edge* edges;
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a, int nb_p, doubl
 // the same partials in the same order; block 0 publishes it in scal[3]).
 __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int N, const double* __restrict__ part_max,
                                                        int nmax) {
-    __shared__ double red[kBaBlock / 64][42];
+    __shared__ double red[kBaBlock / 64][36];
     __shared__ double lam_s;
     if (lam < 0) {
         if (threadIdx.x == 0) {
@@ -556,6 +556,39 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int 
         lam = lam_s;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if ((int)blockIdx.x >= a.nblk) {  // blocks nblk + r: b_schur of the r-th free keyframe
+        const int r = blockIdx.x - a.nblk;
+        const int ka = a.blk_kf[2 * (r * a.nf - r * (r - 1) / 2)];
+        const int i1 = a.pose_idx[ka];
+        if (i1 < 0) return;
+        double bacc[6] = {0, 0, 0, 0, 0, 0};
+        for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
+            const int e = a.kf_edges[j];
+            const int p = a.kf_pt[j];
+            double Di[9];
+            point_dinv(a, p, lam, Di);
+            const double* blp = a.bl + 3 * p;
+            double db[3];
+            for (int rr = 0; rr < 3; rr++) db[rr] = Di[rr * 3] * blp[0] + Di[rr * 3 + 1] * blp[1] + Di[rr * 3 + 2] * blp[2];
+            const double* B = a.Hpl + 18 * (long long)e;
+#pragma unroll
+            for (int rr = 0; rr < 6; rr++) bacc[rr] += B[rr * 3] * db[0] + B[rr * 3 + 1] * db[1] + B[rr * 3 + 2] * db[2];
+        }
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            double x = bacc[q];
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if (lane == 0) red[wid][q] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            double t = 0;
+            for (int w = 0; w < kBaBlock / 64; w++) t += red[w][threadIdx.x];
+            a.bs[6 * i1 + threadIdx.x] = a.bp[6 * i1 + threadIdx.x] - t;
+        }
+        return;
+    }
     const int b = blockIdx.x;
     const int ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
     const int i1 = a.pose_idx[ka], i2 = a.pose_idx[kb];
@@ -584,39 +617,20 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int 
             for (int c = 0; c < 6; c++)
                 acc[r * 6 + c] += BD[r * 3] * b2[c * 3] + BD[r * 3 + 1] * b2[c * 3 + 1] + BD[r * 3 + 2] * b2[c * 3 + 2];
     }
-    double bacc[6] = {0, 0, 0, 0, 0, 0};
-    if (diag)
-        for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
-            const int e = a.kf_edges[j];
-            const int p = a.kf_pt[j];
-            double Di[9];
-            point_dinv(a, p, lam, Di);
-            const double* blp = a.bl + 3 * p;
-            double db[3];
-            for (int r = 0; r < 3; r++) db[r] = Di[r * 3] * blp[0] + Di[r * 3 + 1] * blp[1] + Di[r * 3 + 2] * blp[2];
-            const double* B = a.Hpl + 18 * (long long)e;
 #pragma unroll
-            for (int r = 0; r < 6; r++) bacc[r] += B[r * 3] * db[0] + B[r * 3 + 1] * db[1] + B[r * 3 + 2] * db[2];
-        }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < 42; q++) {
-        double x = q < 36 ? acc[q] : bacc[q - 36];
+    for (int q = 0; q < 36; q++) {
+        double x = acc[q];
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
         if (lane == 0) red[wid][q] = x;
     }
     __syncthreads();
     const int q = threadIdx.x;
-    if (q < 42) {
+    if (q < 36) {
         double t = 0;
         for (int w = 0; w < kBaBlock / 64; w++) t += red[w][q];
-        if (q < 36) {
-            const int r = q / 6, c = q % 6;
-            if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
-            else if (c >= r) a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (a.Hpp[36 * i1 + q] + (r == c ? lam : 0.0)) - t;
-        } else if (diag) {
-            a.bs[6 * i1 + q - 36] = a.bp[6 * i1 + q - 36] - t;
-        }
+        const int r = q / 6, c = q % 6;
+        if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
+        else if (c >= r) a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (a.Hpp[36 * i1 + q] + (r == c ? lam : 0.0)) - t;
     }
 }
 
@@ -628,7 +642,8 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int 
 // and publish W, U; owners of (i, j), i > k apply A_ij -= W_ki^T U_kj.  The factor then goes
 // to LDS and one wave runs the blocked U^T z = b, y = z / D, U x = y.  Same factorisation as
 // LinearSolverEigen's SimplicialLDLT up to the rounding order.
-constexpr int kBaSolveThreads = 512;  // >= 465 blocks of 30 poses + 30 right-hand-side blocks
+constexpr int kBaSolveThreads = 512;  // >= TPT x tiles: 2 x (231 + 21) at np <= 21, 465 + 30 at np <= 30
+constexpr int kBaSolveTpt2MaxPoses = 21;
 #ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: phase timestamps of thread 0
 __device__ unsigned long long g_solve_trace[256];
 __device__ unsigned long long g_solve_clk[2];
@@ -650,7 +665,10 @@ __device__ inline void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
+template <int TPT>  // threads per tile: 2 (np <= 21) or 1 (np <= kBaMaxPoses)
+__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, double lam, const double* __restrict__ T,
+                                                              double* __restrict__ Tt) {
+    constexpr int CPT = 6 / TPT;  // tile columns per thread
     SOLVE_MARK(255);
     constexpr int kSlot = 37;  // odd stride in doubles: conflict-free LDS rows
     __shared__ double H[kBaPacked];
@@ -661,25 +679,27 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
     __shared__ int fail;
     const int N = 6 * np, nblk = np * (np + 1) / 2;
     const int tid = threadIdx.x;
-    // thread -> block (bi, bj) of the upper triangle, or (bi, np) = block bi of the right-hand
-    // side carried through the factorisation (the forward substitution U^T z = b, D y = z)
-    const bool own = tid < nblk + np;
-    const bool rhs = own && tid >= nblk;
+    // TPT adjacent threads -> tile (bi, bj) of the upper triangle, or (bi, np) = block bi of
+    // the right-hand side carried through the factorisation (the forward substitution
+    // U^T z = b, D y = z).  Thread h of the tile owns its columns CPT h .. CPT h + CPT - 1.
+    const int tile = tid / TPT, h = tid % TPT, c0 = CPT * h;
+    const bool own = tile < nblk + np;
+    const bool rhs = own && tile >= nblk;
     int bi = 0, bj = 0;
     if (rhs) {
-        bi = tid - nblk;
+        bi = tile - nblk;
         bj = np;
     } else if (own) {
-        int t = tid;
+        int t = tile;
         while (t >= np - bi) { t -= np - bi; bi++; }
         bj = bi + t;
     }
     const bool dg = !rhs && bi == bj;
     for (int q = tid; q < N; q += blockDim.x) rb[q] = q * N - q * (q - 1) / 2 - q;
-    double A[36];
+    double A[6 * CPT];  // A[r * CPT + cc] = element (r, c0 + cc) of the tile
 #pragma unroll
-    for (int q = 0; q < 36; q++) {
-        const int r = q / 6, c = q % 6;
+    for (int q = 0; q < 6 * CPT; q++) {
+        const int r = q / CPT, c = c0 + q % CPT;
         A[q] = 0.0;
         if (rhs) { if (c == 0) A[q] = a.bs[6 * bi + r]; }
         else if (own && (!dg || c >= r)) A[q] = a.S[packed(6 * bi + r, 6 * bj + c, N)];
@@ -688,34 +708,55 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
     __syncthreads();
     SOLVE_MARK(0);
     for (int k = 0; k < np; k++) {
-        if (own && bi == k && bj == k) {  // (1) diagonal block, column-by-column LDL^T
+        if (own && bi == k && bj == k) {  // (1) diagonal tile: both halves factor it redundantly
+            double F[36];
+            if constexpr (TPT == 2) {
+#pragma unroll
+                for (int q = 0; q < 18; q++) {
+                    const double o = __shfl_xor(A[q], 1, 64);
+                    const int r = q / 3, cc = q % 3;
+                    F[r * 6 + cc] = h == 0 ? A[q] : o;
+                    F[r * 6 + 3 + cc] = h == 0 ? o : A[q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 36; q++) F[q] = A[q];
+            }
             bool bad = false;
+            double inv6[6];
 #pragma unroll
             for (int j = 0; j < 6; j++) {
-                const double d = A[j * 7];
+                const double d = F[j * 7];
                 bad |= !(fabs(d) > 0) || !isfinite(d);
                 const double inv = 1.0 / d;
-                Dinv6[j] = inv;
+                inv6[j] = inv;
 #pragma unroll
                 for (int c = j + 1; c < 6; c++) {
-                    const double u = A[j * 6 + c] * inv;  // u_jc
+                    const double u = F[j * 6 + c] * inv;  // u_jc
 #pragma unroll
-                    for (int r = j + 1; r <= c; r++) A[r * 6 + c] -= A[j * 6 + r] * u;
+                    for (int r = j + 1; r <= c; r++) F[r * 6 + c] -= F[j * 6 + r] * u;
                 }
 #pragma unroll
-                for (int c = j + 1; c < 6; c++) A[j * 6 + c] *= inv;
+                for (int c = j + 1; c < 6; c++) F[j * 6 + c] *= inv;
             }
 #pragma unroll
-            for (int q = 0; q < 36; q++) Ud[q] = A[q];
-            if (bad) fail = 1;
+            for (int q = 0; q < 6 * CPT; q++) {
+                const int r = q / CPT, cc = q % CPT;
+                A[q] = (TPT == 1 || h == 0) ? F[r * 6 + cc] : F[r * 6 + CPT + cc];
+            }
+            if (h == 0) {
+#pragma unroll
+                for (int q = 0; q < 36; q++) Ud[q] = F[q];
+#pragma unroll
+                for (int j = 0; j < 6; j++) Dinv6[j] = inv6[j];
+                if (bad) fail = 1;
+            }
         }
         __syncthreads();
         SOLVE_MARK(1 + 3 * k);
         if (fail) break;
         if (own && bi == k && bj > k) {  // (2) block row: W = U_kk^-T A_kj, U_kj = D^-1 W
-            double ud[15], di[6];
-#pragma unroll
-            for (int t = 0; t < 6; t++) di[t] = Dinv6[t];
+            double ud[15];
             {
                 int q = 0;
 #pragma unroll
@@ -724,39 +765,40 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
                     for (int s2 = 0; s2 < t; s2++, q++) ud[q] = Ud[s2 * 6 + t];
             }
 #pragma unroll
-            for (int c = 0; c < 6; c++) {
+            for (int cc = 0; cc < CPT; cc++) {
                 int q = 0;
 #pragma unroll
                 for (int t = 1; t < 6; t++)
 #pragma unroll
-                    for (int s2 = 0; s2 < t; s2++, q++) A[t * 6 + c] -= ud[q] * A[s2 * 6 + c];
+                    for (int s2 = 0; s2 < t; s2++, q++) A[t * CPT + cc] -= ud[q] * A[s2 * CPT + cc];
             }
 #pragma unroll
-            for (int q = 0; q < 36; q++) {
-                Wp[bj * kSlot + q] = A[q];
-                A[q] *= di[q / 6];
-                Up[bj * kSlot + q] = A[q];
+            for (int q = 0; q < 6 * CPT; q++) {
+                const int r = q / CPT, c = c0 + q % CPT;
+                Wp[bj * kSlot + r * 6 + c] = A[q];
+                A[q] *= Dinv6[r];
+                Up[bj * kSlot + r * 6 + c] = A[q];
             }
         }
         __syncthreads();
         SOLVE_MARK(2 + 3 * k);
-        if (own && bi > k) {  // (3) trailing update of the owned block
-            double w[36];
+        if (own && bi > k && !(rhs && h > 0)) {  // (3) trailing update of the owned columns
+            double u[6 * CPT];
 #pragma unroll
-            for (int q = 0; q < 36; q++) w[q] = Wp[bi * kSlot + q];
+            for (int q = 0; q < 6 * CPT; q++) u[q] = Up[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
 #pragma unroll
-            for (int c = 0; c < 6; c++) {
-                if (rhs && c > 0) continue;
-                double u[6];
+            for (int r = 0; r < 6; r++) {
+                double w[6];
 #pragma unroll
-                for (int t = 0; t < 6; t++) u[t] = Up[bj * kSlot + t * 6 + c];
+                for (int t = 0; t < 6; t++) w[t] = Wp[bi * kSlot + t * 6 + r];
 #pragma unroll
-                for (int r = 0; r < 6; r++) {
-                    if (dg && c < r) continue;
+                for (int cc = 0; cc < CPT; cc++) {
+                    if (dg && c0 + cc < r) continue;
+                    if (rhs && cc > 0) continue;
                     double s2 = 0;
 #pragma unroll
-                    for (int t = 0; t < 6; t++) s2 += w[t * 6 + r] * u[t];
-                    A[r * 6 + c] -= s2;
+                    for (int t = 0; t < 6; t++) s2 += w[t] * u[t * CPT + cc];
+                    A[r * CPT + cc] -= s2;
                 }
             }
         }
@@ -765,21 +807,23 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
         SOLVE_MARK(3 + 3 * k);
 #endif
     }
-    if (fail) {
-        if (tid == 0) a.istat[3] = 0;
+    if (fail) {  // pop: trial poses = current ones, computeScale = 0
+        for (int k = tid; k < a.nkf; k += blockDim.x)
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
         return;
     }
     // factor to LDS (packed upper, U above the diagonal) and y to bs
     if (own && !rhs) {
 #pragma unroll
-        for (int q = 0; q < 36; q++) {
-            const int r = q / 6, c = q % 6;
+        for (int q = 0; q < 6 * CPT; q++) {
+            const int r = q / CPT, c = c0 + q % CPT;
             if (!dg || c >= r) H[rb[6 * bi + r] + 6 * bj + c] = A[q];
         }
     }
-    if (rhs)
+    if (rhs && h == 0)
 #pragma unroll
-        for (int r = 0; r < 6; r++) bs[6 * bi + r] = A[r * 6];
+        for (int r = 0; r < 6; r++) bs[6 * bi + r] = A[r * CPT];
     __syncthreads();
     SOLVE_MARK(200);
     if (tid >= 64) return;
@@ -806,32 +850,31 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np) {
         if (lane < 6) {
 #pragma unroll
             for (int t = 0; t < 6; t++)
-                if (t == lane) a.xp[k0 + t] = x[t];
+                if (t == lane) { a.xp[k0 + t] = x[t]; bs[k0 + t] = x[t]; }
         }
         wave_sync_lds();
     }
     SOLVE_MARK(201);
-    if (tid == 0) a.istat[3] = 1;
-}
-
-// trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
-// computeScale, sum x_p (lambda x_p + b_p) in index order; copies T when the solve failed
-__global__ __launch_bounds__(kBaBlock) void k_ba_pose_trial(BaDev a, int np, double lam, const double* __restrict__ T,
-                                                            double* __restrict__ Tt) {
-    const bool ok = a.istat[3] != 0;
+    // trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
+    // computeScale, sum x_p (lambda x_p + b_p) in index order
     if (lam < 0) lam = a.scal[3];
-    for (int k = threadIdx.x; k < a.nkf; k += blockDim.x) {
+    for (int k = lane; k < a.nkf; k += 64) {
         const int pi = a.pose_idx[k];
-        if (ok && pi >= 0) se3_oplus(a.xp + 6 * pi, T + 8 * k, Tt + 8 * k);
-        else
+        if (pi >= 0) {
+            double u[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) u[q] = bs[6 * pi + q];
+            se3_oplus(u, T + 8 * k, Tt + 8 * k);
+        } else {
             for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        }
     }
-    if (threadIdx.x == 0) {
+    if (lane == 0) {
         double sc = 0;
-        if (ok)
-            for (int q = 0; q < 6 * np; q++) sc += a.xp[q] * (lam * a.xp[q] + a.bp[q]);
+        for (int q = 0; q < N; q++) sc += bs[q] * (lam * bs[q] + a.bp[q]);
         a.scal[1] = sc;
-        a.scal[2] = ok ? 1 : 0;
+        a.scal[2] = 1;
+        a.istat[3] = 1;
     }
 }
 
@@ -995,10 +1038,12 @@ struct Runner {
         int qmax = 0, rc;
         do {
             if (a.nblk > 0)
-                hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk), dim3(kBaBlock), 0, h.stream, a, lam_arg, N, part_max,
+                hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kBaBlock), 0, h.stream, a, lam_arg, N, part_max,
                                    nb_p + np);
-            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np);
-            hipLaunchKernelGGL(k_ba_pose_trial, dim3(1), dim3(kBaBlock), 0, h.stream, a, np, lam_arg, T, Tt);
+            if (np <= kBaSolveTpt2MaxPoses)
+                hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np, lam_arg, T, Tt);
+            else
+                hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np, lam_arg, T, Tt);
             hipLaunchKernelGGL(k_ba_update_errors, dim3(nb_q), dim3(kBaBlock), 0, h.stream, a, lam_arg, X, Tt, Xt,
                                tchi(), tscale());
             ORBMI_HIP(hipGetLastError());
@@ -1178,7 +1223,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses),
                  o_S = take(8 * (size_t)kBaPacked), o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN),
                  o_rb = take(8 * (8 + (size_t)nb_e + 2 * (size_t)nb_q)), o_pmax = take(8 * ((size_t)nb_p + kBaMaxPoses)),
-                 o_istat = take(16), o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
+                 o_istat = take(32), o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
     if (off > h.cap) {
         if (h.d_buf) (void)hipFree(h.d_buf);
         h.d_buf = nullptr;
@@ -1203,9 +1248,9 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     ORBMI_HIP(up(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk));
     ORBMI_HIP(up(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1)));
     ORBMI_HIP(up(o_pairs, pairs.data(), 8 * (size_t)npair));
-    ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 16, s));
+    ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
     BaDev a;
-    a.nkf = nkf; a.npt = npt; a.nedge = ne; a.nblk = nblk;
+    a.nkf = nkf; a.npt = npt; a.nedge = ne; a.nblk = nblk; a.nf = nf;
     a.kfs = (const orbmi_ba_keyframe*)(B + o_kfs);
     a.pts = (const orbmi_ba_point*)(B + o_pts);
     a.edges = (const orbmi_ba_edge*)(B + o_edges);

@@ -42,6 +42,7 @@ struct Matcher {
     // candidates / greedy
     unsigned long long* d_cand = nullptr; size_t cap_cand = 0;
     int* d_ncand = nullptr; size_t cap_ncand = 0;
+    unsigned long long* d_top = nullptr; size_t cap_top = 0;
     int* d_res = nullptr; size_t cap_res = 0;
     int* d_bin_of = nullptr; size_t cap_bin_of = 0;
     int* d_hist = nullptr; size_t cap_hist = 0;

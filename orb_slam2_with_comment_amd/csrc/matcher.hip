@@ -1,8 +1,8 @@
 // ORBmatcher on MI355X (src/ORBmatcher.cc):
 //   k_grid_build        Frame::AssignFeaturesToGrid (src/Frame.cc:232-247)        one workgroup
 //   k_frustum           Frame::isInFrustum + MapPoint::PredictScale               thread / point
-//   k_local_candidates  SearchByProjection(F, MPs): window + static filters + Hamming  thread / point
-//   k_lf_candidates     SearchByProjection(CF, LF): projection + window + Hamming     thread / LF kp
+//   k_candidates<G>     SearchByProjection(F, MPs) / (CF, LF): window + static filters + Hamming,
+//                       G lanes per query (map point / LF keypoint), sorted top-8 prefix
 //   k_greedy            exact greedy replay of the order-dependent exclusion           one workgroup
 //   k_bow_*             SearchByBoW: node merge-join + per-node greedy (one wave / node)
 //   k_xmatch_*          cross-stream brute-force matching of config 4 (build-defined)
@@ -187,25 +187,6 @@ __device__ inline void local_candidates(const DevFrame& F, const int* cs, const 
     });
 }
 
-__global__ __launch_bounds__(256) void k_local_candidates(DevFrame F, const int* __restrict__ cs,
-                                                          const int* __restrict__ cl,
-                                                          const orbmi_mappoint* __restrict__ mps,
-                                                          const orbmi_mappoint_track* __restrict__ tr, int n, float th,
-                                                          unsigned long long* __restrict__ cand,
-                                                          int* __restrict__ ncand, int cap) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const orbmi_mappoint mp = mps[i];
-    const orbmi_mappoint_track t = tr[i];
-    int c = 0;
-    unsigned long long* out = cand + (long long)i * cap;
-    local_candidates(F, cs, cl, mp, t, th, [&](unsigned long long e) {
-        if (c < cap) out[c] = e;
-        c++;
-    });
-    ncand[i] = c;
-}
-
 // SearchByProjection(CF, LF, th, bMono): projection + static part (:1566-1637)
 struct LfQuery {
     float u, v, radius, ur;
@@ -257,23 +238,123 @@ __device__ inline void motion_direction(const DevFrame& CF, const DevFrame& LF, 
     *bw = -tlc[2] > CF.mb && !mono;
 }
 
-__global__ __launch_bounds__(256) void k_lf_candidates(DevFrame CF, DevFrame LF, const int* __restrict__ cs,
-                                                       const int* __restrict__ cl,
-                                                       const orbmi_lastframe_point* __restrict__ lfp, float th,
-                                                       int mono, unsigned long long* __restrict__ cand,
-                                                       int* __restrict__ ncand, int cap) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= frame_n(LF)) return;
+// -------------------------------------------------------------------------- group candidates
+// G lanes per query: lanes take the window's grid cells (ix-major order does not matter: the
+// entries carry their cell order), filter and score the cells' keypoints, append to an LDS
+// list, then select the kTopK smallest entries in order.  The greedy pass usually finds its
+// best and second best unclaimed entries in that prefix; the full list (or, past kCandCap,
+// a re-enumeration) is the fallback.
+constexpr int kTopK = 8;
+
+struct CandArgs {
+    int mode;  // 0 = local map (query = map point), 1 = last frame (query = LF keypoint)
+    int nq;    // mode 0: number of map points; mode 1: LF capacity (count read on the device)
+    DevFrame F, LF;
+    const int* cs;
+    const int* cl;
+    const orbmi_mappoint* mps;
+    const orbmi_mappoint_track* tr;
+    const orbmi_lastframe_point* lfp;
+    float th;
+    int mono;
+    unsigned long long* cand;
+    int* ncand;
+    unsigned long long* top;
+};
+
+struct Window {
+    float x, y, r, ur;
+    int minL, maxL;
+    const uint8_t* desc;
+};
+
+__device__ inline bool make_window(const CandArgs& a, int q, Window* w) {
+    if (a.mode == 0) {
+        const orbmi_mappoint& mp = a.mps[q];
+        const orbmi_mappoint_track t = a.tr[q];
+        int level;
+        if (!local_query(a.F, mp, t, a.th, &w->x, &w->y, &w->r, &level)) return false;
+        w->minL = level - 1;
+        w->maxL = level;
+        w->ur = t.proj_xr;
+        w->desc = mp.desc;
+        return true;
+    }
     bool fw, bw;
-    motion_direction(CF, LF, mono, &fw, &bw);
-    const orbmi_lastframe_point p = lfp[i];
-    int c = 0;
-    unsigned long long* out = cand + (long long)i * cap;
-    lf_candidates(CF, LF, cs, cl, p, i, th, fw, bw, [&](unsigned long long e) {
-        if (c < cap) out[c] = e;
-        c++;
-    });
-    ncand[i] = c;
+    motion_direction(a.F, a.LF, a.mono, &fw, &bw);
+    const orbmi_lastframe_point& p = a.lfp[q];
+    LfQuery lq;
+    if (!lf_query(a.F, a.LF, p, q, a.th, fw, bw, &lq)) return false;
+    w->x = lq.u; w->y = lq.v; w->r = lq.radius; w->ur = lq.ur; w->minL = lq.minL; w->maxL = lq.maxL;
+    w->desc = p.desc;
+    return true;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_candidates(CandArgs a) {
+    constexpr int NG = 256 / G, cap = Matcher::kCandCap;
+    __shared__ unsigned long long buf[NG][cap];
+    __shared__ int cnt[NG];
+    const int gl = threadIdx.x / G, lane = threadIdx.x % G;
+    const int q = blockIdx.x * NG + gl;
+    const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;
+    Window w;
+    const bool valid = q < nq && make_window(a, q, &w);
+    if (lane == 0) cnt[gl] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+        const DevFrame& F = a.F;
+        const int nMinCellX = max(0, (int)floorf((w.x - F.min_x - w.r) * F.grid_w_inv));
+        const int nMaxCellX = min(kGridCols - 1, (int)ceilf((w.x - F.min_x + w.r) * F.grid_w_inv));
+        const int nMinCellY = max(0, (int)floorf((w.y - F.min_y - w.r) * F.grid_h_inv));
+        const int nMaxCellY = min(kGridRows - 1, (int)ceilf((w.y - F.min_y + w.r) * F.grid_h_inv));
+        if (nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0) {
+            const int ny = nMaxCellY - nMinCellY + 1, ncell = (nMaxCellX - nMinCellX + 1) * ny;
+            const bool bCheckLevels = (w.minL > 0) || (w.maxL >= 0);
+            const uint4* md = reinterpret_cast<const uint4*>(w.desc);
+            const uint4 m0 = md[0], m1 = md[1];
+            for (int ci = lane; ci < ncell; ci += G) {
+                const int c = (nMinCellX + ci / ny) * kGridRows + nMinCellY + ci % ny;
+                for (int j = a.cs[c]; j < a.cs[c + 1]; j++) {
+                    const int idx = a.cl[j];
+                    const orbmi_keypoint kp = F.keys[idx];
+                    if (bCheckLevels) {
+                        if (kp.octave < w.minL) continue;
+                        if (w.maxL >= 0 && kp.octave > w.maxL) continue;
+                    }
+                    if (!(fabsf(kp.x - w.x) < w.r && fabsf(kp.y - w.y) < w.r)) continue;
+                    if (F.u_right && F.u_right[idx] > 0 && fabsf(w.ur - F.u_right[idx]) > w.r) continue;
+                    const uint4* fd = reinterpret_cast<const uint4*>(F.desc + 32 * (long long)idx);
+                    const int pos = atomicAdd(&cnt[gl], 1);
+                    if (pos < cap) buf[gl][pos] = cand_entry(popc256(m0, m1, fd[0], fd[1]), c, idx);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n = cnt[gl], nk = min(n, cap);
+    // kTopK smallest entries, ascending (entries are distinct: one per keypoint)
+    unsigned long long last = 0;
+    for (int k = 0; k < kTopK; k++) {
+        unsigned long long m = ~0ull;
+        for (int p = lane; p < nk; p += G) {
+            const unsigned long long e = buf[gl][p];
+            if ((k == 0 || e > last) && e < m) m = e;
+        }
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(m, o, G);
+            m = v < m ? v : m;
+        }
+        if (valid && lane == 0) a.top[(long long)q * kTopK + k] = m;
+        last = m;
+    }
+    if (valid && n > kTopK)
+        for (int p = lane; p < nk; p += G) a.cand[(long long)q * cap + p] = buf[gl][p];
+    if (q < nq && lane == 0) a.ncand[q] = valid ? n : 0;
 }
 
 // -------------------------------------------------------------------------- greedy
@@ -282,6 +363,7 @@ struct GreedyArgs {
     int nq;               // queries (map points / LF keypoints), processed in index order
     const unsigned long long* cand;
     const int* ncand;
+    const unsigned long long* top;  // kTopK smallest entries per query, ascending
     int cap;
     const uint8_t* occ0;  // initial occupancy (F.mvpMapPoints[i] && Observations() > 0)
     DevFrame F;           // frame searched (CF)
@@ -311,13 +393,20 @@ __device__ inline int greedy_eval(const GreedyArgs& a, int q, bool fw, bool bw, 
         else if (e < b2) b2 = e;
     };
     const int nc = a.ncand[q];
-    if (nc <= a.cap) {
-        const unsigned long long* c = a.cand + (long long)q * a.cap;
-        for (int k = 0; k < nc; k++) take(c[k]);
-    } else if (a.mode == 0) {  // overflowed list: enumerate again
-        local_candidates(a.F, a.cs, a.cl, a.mps[q], a.tr[q], a.th, take);
-    } else {
-        lf_candidates(a.F, a.LF, a.cs, a.cl, a.lfp[q], q, a.th, fw, bw, take);
+    // sorted prefix first: the two smallest unclaimed entries are usually there
+    const unsigned long long* t = a.top + (long long)q * kTopK;
+    const int kk = nc <= a.cap ? min(nc, kTopK) : 0;  // past kCandCap the prefix is partial
+    for (int k = 0; k < kk && b2 == ~0ull; k++) take(t[k]);
+    if (b2 == ~0ull && nc > kTopK) {
+        b1 = b2 = ~0ull;
+        if (nc <= a.cap) {
+            const unsigned long long* c = a.cand + (long long)q * a.cap;
+            for (int k = 0; k < nc; k++) take(c[k]);
+        } else if (a.mode == 0) {  // overflowed list: enumerate again
+            local_candidates(a.F, a.cs, a.cl, a.mps[q], a.tr[q], a.th, take);
+        } else {
+            lf_candidates(a.F, a.LF, a.cs, a.cl, a.lfp[q], q, a.th, fw, bw, take);
+        }
     }
     if (b1 == ~0ull) return -1;
     const int bestDist = (int)(b1 >> 40);
@@ -346,40 +435,135 @@ __device__ inline int rot_bin(float a0, float a1) {
     return bin;
 }
 
-__global__ __launch_bounds__(1024) void k_greedy(GreedyArgs a) {
-    __shared__ int claim[kGreedyMaxKp];   // min query index holding the keypoint (with obs)
-    __shared__ int last[kGreedyMaxKp];    // max query index assigned to the keypoint
+// query verdict from the two smallest unclaimed entries (dist, idx); idx2 < 0 = none
+__device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int d1, int i1, int d2, int i2) {
+    if (i1 < 0) return -1;
+    if (a.mode == 0) {
+        if (d1 > TH_HIGH) return -1;
+        const int bestDist2 = i2 < 0 ? 256 : d2;
+        const int bestLevel2 = i2 < 0 ? -1 : oct[i2];
+        if (oct[i1] == bestLevel2 && d1 > a.nnratio * bestDist2) return -1;
+        return i1;
+    }
+    return d1 <= TH_HIGH ? i1 : -1;
+}
+
+constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = 4;
+
+// Each thread keeps its queries (q = tid + k * 1024) in registers: current result, candidate
+// count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
+// octave and the initial occupancy live in LDS.  A round then touches LDS only, except for
+// queries whose prefix runs out of unclaimed entries (full list / re-enumeration).
+__global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
+    __shared__ int claim[kGreedyMaxKp];   // min query index holding the keypoint (with obs);
+                                          // afterwards the max query index assigned to it
+    __shared__ uint8_t occ0[kGreedyMaxKp], oct[kGreedyMaxKp];  // occ0: afterwards "rejected"
+    __shared__ int slowres[kGreedyQPer * kGreedyThreads];
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int flag[4];
     const int tid = threadIdx.x, n = frame_n(a.F);
-    if (a.mode == 1) a.nq = frame_n(a.LF);
+    const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;  // (the by-value argument stays unmodified)
     bool fw = false, bw = false;
     if (a.mode == 1) motion_direction(a.F, a.LF, a.mono, &fw, &bw);
-    for (int q = tid; q < a.nq; q += blockDim.x) a.res[q] = -1;
+    for (int i = tid; i < n; i += blockDim.x) { occ0[i] = a.occ0[i]; oct[i] = (uint8_t)a.F.keys[i].octave; }
+    const bool regs = nq <= kGreedyThreads * kGreedyQPer;
+    int res[kGreedyQPer], nc[kGreedyQPer];
+    unsigned pre[kGreedyQPer][kGreedyPre];
+    bool obs[kGreedyQPer];
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) {
+        const int q = tid + k * kGreedyThreads;
+        res[k] = -1;
+        nc[k] = 0;
+        obs[k] = false;
+#pragma unroll
+        for (int j = 0; j < kGreedyPre; j++) pre[k][j] = 0;
+        if (regs && q < nq) {
+            nc[k] = a.ncand[q];
+            obs[k] = query_has_obs(a, q);
+            const unsigned long long* t = a.top + (long long)q * kTopK;
+#pragma unroll
+            for (int j = 0; j < kGreedyPre; j++) {
+                const unsigned long long e = t[j];
+                pre[k][j] = ((unsigned)(e >> 40) << 16) | (unsigned)(e & 0xFFFF);
+            }
+        }
+    }
+    if (!regs)
+        for (int q = tid; q < nq; q += blockDim.x) a.res[q] = -1;
+    __syncthreads();
     bool converged = false;
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
         for (int i = tid; i < n; i += blockDim.x) claim[i] = 0x7FFFFFFF;
         if (tid == 0) flag[0] = 0;
         __syncthreads();
-        for (int q = tid; q < a.nq; q += blockDim.x) {
-            const int r = a.res[q];
-            if (r >= 0 && query_has_obs(a, q)) atomicMin(&claim[r], q);
+        if (regs) {
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++)
+                if (res[k] >= 0 && obs[k]) atomicMin(&claim[res[k]], tid + k * kGreedyThreads);
+        } else {
+            for (int q = tid; q < nq; q += blockDim.x) {
+                const int r = a.res[q];
+                if (r >= 0 && query_has_obs(a, q)) atomicMin(&claim[r], q);
+            }
         }
         __syncthreads();
         int changed = 0;
-        for (int q = tid; q < a.nq; q += blockDim.x) {
-            const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return a.occ0[idx] || claim[idx] < q; });
-            if (r != a.res[q]) { a.res[q] = r; changed = 1; }
+        if (regs) {
+            unsigned slow = 0;
+            int fast[kGreedyQPer];
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++) {
+                const int q = tid + k * kGreedyThreads;
+                fast[k] = res[k];
+                if (q >= nq) continue;
+                int d1 = 0, i1 = -1, d2 = 0, i2 = -1;
+                const int kk = nc[k] <= a.cap ? min(nc[k], kGreedyPre) : 0;
+#pragma unroll
+                for (int j = 0; j < kGreedyPre; j++) {
+                    if (j >= kk || i2 >= 0) continue;
+                    const int idx = (int)(pre[k][j] & 0xFFFF), d = (int)(pre[k][j] >> 16);
+                    if (occ0[idx] || claim[idx] < q) continue;
+                    if (i1 < 0) { d1 = d; i1 = idx; } else { d2 = d; i2 = idx; }
+                }
+                if (i2 < 0 && nc[k] > kGreedyPre) slow |= 1u << k;  // prefix exhausted
+                else fast[k] = greedy_decide(a, oct, d1, i1, d2, i2);
+            }
+            for (int k = 0; k < kGreedyQPer; k++)  // not unrolled: one copy of the slow path
+                if (slow >> k & 1) {
+                    const int q = tid + k * kGreedyThreads;
+                    slowres[k * kGreedyThreads + tid] =
+                        greedy_eval(a, q, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                }
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++) {
+                const int r = (slow >> k & 1) ? slowres[k * kGreedyThreads + tid] : fast[k];
+                if (r != res[k]) { res[k] = r; changed = 1; }
+            }
+        } else {
+            for (int q = tid; q < nq; q += blockDim.x) {
+                const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                if (r != a.res[q]) { a.res[q] = r; changed = 1; }
+            }
         }
         if (changed) atomicOr(&flag[0], 1);
         __syncthreads();
         converged = flag[0] == 0;
         __syncthreads();
     }
+    if (regs) {
+#pragma unroll
+        for (int k = 0; k < kGreedyQPer; k++) {
+            const int q = tid + k * kGreedyThreads;
+            if (q < nq) a.res[q] = res[k];
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
     if (!converged) {  // sequential replay (exact), bounded-rounds fallback
         if (tid == 0) {
-            for (int i = 0; i < n; i++) claim[i] = a.occ0[i];
-            for (int q = 0; q < a.nq; q++) {
+            for (int i = 0; i < n; i++) claim[i] = occ0[i];
+            for (int q = 0; q < nq; q++) {
                 const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return claim[idx] != 0; });
                 a.res[q] = r;
                 if (r >= 0 && query_has_obs(a, q)) claim[r] = 1;
@@ -387,12 +571,15 @@ __global__ __launch_bounds__(1024) void k_greedy(GreedyArgs a) {
         }
         __syncthreads();
     }
-    // outputs: last assignment per keypoint; rotation consistency (mode 1)
-    for (int i = tid; i < n; i += blockDim.x) { last[i] = -1; claim[i] = 0; }
+    // outputs: last assignment per keypoint (claim[] reused); rotation consistency (mode 1),
+    // rejected keypoints flagged in occ0[]
+    int* last = claim;
+    uint8_t* rejected = occ0;
+    for (int i = tid; i < n; i += blockDim.x) { last[i] = -1; rejected[i] = 0; }
     if (tid < HISTO_LENGTH) hist[tid] = 0;
     if (tid == 0) flag[1] = 0;
     __syncthreads();
-    for (int q = tid; q < a.nq; q += blockDim.x) {
+    for (int q = tid; q < nq; q += blockDim.x) {
         const int r = a.res[q];
         if (r < 0) continue;
         atomicMax(&last[r], q);
@@ -411,15 +598,15 @@ __global__ __launch_bounds__(1024) void k_greedy(GreedyArgs a) {
         }
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-        for (int q = tid; q < a.nq; q += blockDim.x) {
+        for (int q = tid; q < nq; q += blockDim.x) {
             const int r = a.res[q];
             if (r < 0) continue;
             const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
-            if (bin != ind1 && bin != ind2 && bin != ind3) { claim[r] = 1; atomicSub(&flag[1], 1); }
+            if (bin != ind1 && bin != ind2 && bin != ind3) { rejected[r] = 1; atomicSub(&flag[1], 1); }
         }
         __syncthreads();
     }
-    for (int i = tid; i < n; i += blockDim.x) a.out[i] = claim[i] ? -2 : last[i];
+    for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
     if (tid == 0) *a.nmatches = flag[1];
 }
 
@@ -640,11 +827,15 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
     if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
     if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_res, &m.cap_res, (size_t)std::max(n, 1)))) return rc;
-    if (n > 0)
-        hipLaunchKernelGGL(k_local_candidates, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start,
-                           m.d_cell_list, mps, tr, n, th, m.d_cand, m.d_ncand, cap);
+    if ((rc = ensure_buf(&m.d_top, &m.cap_top, (size_t)std::max(n, 1) * kTopK))) return rc;
+    if (n > 0) {
+        CandArgs ca{};
+        ca.mode = 0; ca.nq = n; ca.F = F; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.mps = mps; ca.tr = tr;
+        ca.th = th; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
+        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.stream, ca);
+    }
     GreedyArgs a{};
-    a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.cap = cap; a.occ0 = occ0; a.F = F;
+    a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = F;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches;
     hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
@@ -660,11 +851,16 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
     if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
     if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_res, &m.cap_res, (size_t)std::max(n, 1)))) return rc;
-    if (n > 0)
-        hipLaunchKernelGGL(k_lf_candidates, dim3((n + 255) / 256), dim3(256), 0, m.stream, CF, LF, m.d_cell_start,
-                           m.d_cell_list, lfp, th, mono, m.d_cand, m.d_ncand, cap);
+    if ((rc = ensure_buf(&m.d_top, &m.cap_top, (size_t)std::max(n, 1) * kTopK))) return rc;
+    if (n > 0) {
+        CandArgs ca{};
+        ca.mode = 1; ca.nq = n; ca.F = CF; ca.LF = LF; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.lfp = lfp;
+        ca.th = th; ca.mono = mono; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
+        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.stream, ca);
+    }
     GreedyArgs a{};
-    a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.cap = cap; a.occ0 = occ0; a.F = CF; a.LF = LF;
+    a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = CF;
+    a.LF = LF;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches;
     hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);

@@ -29,7 +29,8 @@ def _compare(r, ref, pt_tol=1e-3):
     np.testing.assert_allclose(r["chi2"], ref["chi2"], rtol=1e-6)
 
 
-@pytest.mark.parametrize("seed,free,fixed,npts", [(3, 6, 2, 300), (42, 20, 4, 3000), (7, 10, 0, 800)])
+@pytest.mark.parametrize("seed,free,fixed,npts", [(3, 6, 2, 300), (42, 20, 4, 3000), (7, 10, 0, 800),
+                                                 (11, 21, 3, 1500), (5, 27, 2, 2000)])
 def test_lba_parity(oracle, BA, seed, free, fixed, npts):
     prob, _ = SM.local_ba_problem(seed=seed, n_free=free, n_fixed=fixed, n_points=npts)
     ref = oracle.local_ba(prob)

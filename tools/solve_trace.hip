@@ -29,12 +29,21 @@ int main(int argc, char** argv) {
     hipMemcpy(dbs, b.data(), N * 8, hipMemcpyHostToDevice);
     BaDev a{};
     a.S = dS; a.bs = dbs; a.xp = dxp; a.istat = dist;
+    // no keyframes: the trial-pose tail only writes the scale
+    double *dT, *dTt, *dbp, *dscal;
+    hipMalloc(&dT, 64); hipMalloc(&dTt, 64); hipMalloc(&dbp, kBaMaxN * 8); hipMalloc(&dscal, 64);
+    hipMemset(dbp, 0, kBaMaxN * 8);
+    a.nkf = 0; a.bp = dbp; a.scal = dscal;
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
-    for (int it = 0; it < 3; it++) hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np);
+    auto launch = [&] {
+        if (np <= kBaSolveTpt2MaxPoses) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np, 1.0, dT, dTt);
+        else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np, 1.0, dT, dTt);
+    };
+    for (int it = 0; it < 3; it++) launch();
     hipEventRecord(e0);
     const int reps = 20;
-    for (int it = 0; it < reps; it++) hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np);
+    for (int it = 0; it < reps; it++) launch();
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
