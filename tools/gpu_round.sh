@@ -1,18 +1,36 @@
 #!/bin/bash
-# One GPU session: parity tests, bench, rocprofv3 kernel stats, PMC traffic passes.
-# Usage (via gpurun): bash tools/gpu_round.sh TAG
-set -o pipefail
-TAG=${1:-r1}
+# One GPU session of round evidence: parity tests, rocprofv3 kernel stats of the default bench,
+# two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, then the bench lines of every mode.
+# Usage (via gpurun): bash tools/gpu_round.sh TAG      -> gpurun_out/TAG/, profiles/TAG/
+# Stops at the first step that crashes or times out (exit status other than 0/1).
+TAG=${1:-r01}
 OUT=gpurun_out/$TAG
-mkdir -p $OUT profiles
+P=profiles/$TAG
+mkdir -p $OUT $P
 export TMPDIR=/tmp
+run() {  # name timeout cmd...
+    local name=$1 t=$2; shift 2
+    timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+    local rc=$?
+    echo "$name exit $rc" | tee -a $OUT/status.txt
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; tail -30 $OUT/$name.log; exit $rc; fi
+    return 0
+}
 python -c "import torch; print(torch.cuda.get_device_name(0))" > $OUT/device.txt 2>&1
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu.log 2>&1
-echo "pytest exit $?" >> $OUT/pytest_gpu.log
+run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
 tail -3 $OUT/pytest_gpu.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_stats -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || { echo "rocprof stats failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
-python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic_latest.json
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json
+cp $OUT/pytest_gpu.log $P/pytest_gpu.log
+run prof_stats 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_stats -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline
+run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline
+run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline
+python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic_latest.json && cp $OUT/traffic.json $P/traffic.json
+find $OUT/prof_stats -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats.csv \;
+cp $OUT/prof_stats.log $P/prof_stats_bench.log 2>/dev/null
+run bench 400 python bench.py
+tail -1 $OUT/bench.log > $P/bench.json; cat $P/bench.json
+run bench_lba 300 python bench.py --mode lba --steps 50 --warmup 10
+tail -1 $OUT/bench_lba.log > $P/bench_lba.json
+run bench_batch 300 python bench.py --mode batch --steps 50 --warmup 4
+tail -1 $OUT/bench_batch.log > $P/bench_batch.json
+run bench_extract 300 python bench.py --mode extract
+tail -1 $OUT/bench_extract.log > $P/bench_extract.json

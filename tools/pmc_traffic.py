@@ -21,10 +21,13 @@ STAGE_OF = [("k_pyr_level0", "pyr_level0"), ("k_pyr_resize", "pyr_resize"), ("k_
 
 
 def stage(name):
+    """Bench stage name for the extractor kernels, the kernel's own name (k_...) otherwise."""
+    import re
     for k, s in STAGE_OF:
         if k in name:
             return s
-    return None
+    m = re.search(r"(k_\w+)", name)
+    return m.group(1) if m else None
 
 
 def read(d, counter):
