@@ -12,7 +12,7 @@ run() {  # name timeout cmd...
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; tail -30 $OUT/$name.log; exit $rc; fi
     return 0
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -x
+run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf -x --timeout 120 --timeout-method thread
 tail -5 $OUT/pytest_gpu.log
 run bench_track 400 python bench.py --steps 60 --warmup 8 --cpu-sample-s 6
 tail -2 $OUT/bench_track.log

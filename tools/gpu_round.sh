@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
     return 0
 }
 python -c "import torch; print(torch.cuda.get_device_name(0))" > $OUT/device.txt 2>&1
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
 tail -3 $OUT/pytest_gpu.log
 cp $OUT/pytest_gpu.log $P/pytest_gpu.log
 run prof_stats 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_stats -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline
