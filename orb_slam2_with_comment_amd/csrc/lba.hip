@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 #include <new>
 #include <vector>
 
@@ -41,8 +42,35 @@ constexpr int kBaPacked = kBaMaxN * (kBaMaxN + 1) / 2;  // 16290 doubles = 127 K
 constexpr int kBaMaxKf = 1024;
 constexpr int kBaBlock = 256;
 
+// Levenberg state of one SparseOptimizer::optimize(n) call, kept on the device so that the
+// trials run back to back without a host round trip (optimization_algorithm_levenberg.cpp:61-164).
+struct BaCtl {
+    int cur;          // which of the two estimate buffers (Tb, Xb) holds the current state
+    int it, max_it;   // iterations finished / requested
+    int trial;        // qmax of the current iteration
+    int need_lin;     // the next step starts an iteration (computeActiveErrors + linearize)
+    int done;         // optimize() has returned (iterations exhausted, terminate, stop)
+    int nbad;         // ORB-SLAM2's consecutive iterations without a 1e-3 relative decrease
+    int np, nl;       // free poses / active points of the index mapping
+    int unsupported;  // more than kBaMaxPoses active poses
+    int steps;        // trial steps executed (diagnostics)
+    int pad;
+    double lambda, ni, currentChi, iniChi;
+    double chi_out[2];  // activeRobustChi2 after optimize(5) / optimize(10)
+    int it_out[2];      // iterations of optimize(5) / optimize(10); -1 with an empty mapping
+};
+
 struct BaDev {
     int nkf, npt, nedge, nblk, nf;  // nf = non-fixed keyframes (nblk = nf (nf + 1) / 2)
+    int nb_e, nb_p, nb_q;           // blocks: edges (256), points (256), points (32 per block)
+    BaCtl* ctl;
+    const volatile int* stop;  // host-mapped mirror of pbStopFlag (may be null)
+    double* Tb[2];             // poses: SE3Quat (x, y, z, w, tx, ty, tz, -), current / trial
+    double* Xb[2];             // points (x, y, z, -), current / trial
+    double* part_lin;          // nb_e: robust chi2 at linearisation
+    double* part_tchi;         // nb_q: trial robust chi2
+    double* part_tscale;       // nb_q: trial computeScale (points)
+    double* part_max;          // nb_p + kBaMaxPoses: max |diag H|
     const orbmi_ba_keyframe* kfs;
     const orbmi_ba_point* pts;
     const orbmi_ba_edge* edges;
@@ -327,9 +355,10 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restri
 
 // outlier levels, kernels off before the second optimisation (src/Optimizer.cc:701-732);
 // chi2 from the stale errors, depth from the current estimate
-__global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a, const double* __restrict__ T,
-                                                        const double* __restrict__ X) {
+__global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const double* T = a.Tb[a.ctl->cur];
+    const double* X = a.Xb[a.ctl->cur];
     if (i >= a.nedge) return;
     const orbmi_ba_edge e = a.edges[i];
     if (a.pts[e.point].bad) return;
@@ -344,7 +373,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a, const double* _
 
 // SparseOptimizer::initializeOptimization(level 0) + buildIndexMapping: active edges, pose
 // indices in vertex-id order (poses first), number of active points
-__global__ __launch_bounds__(1024) void k_ba_activate(BaDev a) {
+__global__ __launch_bounds__(1024) void k_ba_activate(BaDev a, int max_it) {
     __shared__ int kfact[kBaMaxKf];
     __shared__ int nl;
     const int tid = threadIdx.x;
@@ -374,6 +403,19 @@ __global__ __launch_bounds__(1024) void k_ba_activate(BaDev a) {
         a.istat[0] = n;
         a.istat[1] = nl;
         a.istat[2] = n > kBaMaxPoses;
+        // SparseOptimizer::optimize(max_it) begins: LM state of levenberg.cpp:61-70
+        BaCtl& c = *a.ctl;
+        c.np = min(n, kBaMaxPoses);
+        c.nl = nl;
+        c.unsupported |= n > kBaMaxPoses;
+        c.it = 0;
+        c.max_it = max_it;
+        c.trial = 0;
+        c.need_lin = 1;
+        c.nbad = 0;
+        c.lambda = 0;
+        c.ni = 2;
+        c.done = (n + nl == 0) || c.unsupported || max_it <= 0;
     }
     __syncthreads();
     for (int i = tid; i < a.nedge; i += blockDim.x) a.e_pi[i] = a.pose_idx[a.edges[i].kf];
@@ -381,14 +423,13 @@ __global__ __launch_bounds__(1024) void k_ba_activate(BaDev a) {
 
 // ---------------------------------------------------------------- errors
 // computeActiveErrors (recompute = 1) + activeRobustChi2; per-block partial sums
-__global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a, const double* __restrict__ T,
-                                                        const double* __restrict__ X, int recompute,
-                                                        double* __restrict__ part) {
+// activeRobustChi2 on the stored (possibly stale) errors; per-block partial sums
+__global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a) {
     __shared__ double red[kBaBlock / 64];
+    double* part = a.part_lin;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double s = 0;
     if (i < a.nedge && (a.eflag[i] & 4)) {
-        if (recompute) edge_error(a, i, T, X, a.err + 3 * i);
         double r0, r1;
         edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
         s = r0;
@@ -421,8 +462,12 @@ __device__ inline void point_dinv(const BaDev& a, int p, double lam, double Di[9
 // BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:55-120): Hpl block, the
 // edge's Hll / b_l and Hpp / b_p contributions.  Inactive edges into free poses write zeros,
 // so the reductions and the Schur products need no activity tests.
-__global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a, const double* __restrict__ T,
-                                                           const double* __restrict__ X, double* __restrict__ part) {
+__global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done || !ctl.need_lin) return;  // a retry trial keeps the linear system
+    const double* T = a.Tb[ctl.cur];
+    const double* X = a.Xb[ctl.cur];
+    double* part = a.part_lin;
     __shared__ double red[kBaBlock / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double chi = 0;
@@ -470,7 +515,11 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a, const double
 // rows (thread = value x edge lane, fixed-order sum).  part_max = max |diag| per block
 // (computeLambdaInit, optimization_algorithm_levenberg.cpp:166-180).
 constexpr int kBaPoseLanes = kBaBlock / 27;  // 9
-__global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a, int nb_p, double* __restrict__ part_max) {
+__global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done || !ctl.need_lin) return;
+    const int nb_p = a.nb_p;
+    double* part_max = a.part_max;
     __shared__ double red[kBaPoseLanes][27];
     __shared__ double redm[kBaBlock / 64];
     if ((int)blockIdx.x < nb_p) {
@@ -495,7 +544,9 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a, int nb_p, doubl
         if (threadIdx.x == 0) part_max[blockIdx.x] = m;
         return;
     }
-    const int pi = blockIdx.x - nb_p, k = a.pose_kf[pi];
+    const int pi = blockIdx.x - nb_p;
+    if (pi >= ctl.np) return;
+    const int k = a.pose_kf[pi];
     const int q = threadIdx.x % 27, el = threadIdx.x / 27;
     if (el < kBaPoseLanes) {
         double v = 0;
@@ -542,8 +593,13 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a, int nb_p, doubl
 // B_i D^-1 B_j^T with D^-1 recomputed per observation pair; the diagonal block also writes
 // b_schur(i) = b_p - sum B D^-1 b_l.  lam < 0: lambda = 1e-5 max|diag H| (every block reduces
 // the same partials in the same order; block 0 publishes it in scal[3]).
-__global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int N, const double* __restrict__ part_max,
-                                                       int nmax) {
+__global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done) return;
+    const int N = 6 * ctl.np, nmax = a.nb_p + ctl.np;
+    const double* part_max = a.part_max;
+    // lambda: computeLambdaInit on the first trial of iteration 0, the LM state otherwise
+    double lam = (ctl.it == 0 && ctl.trial == 0) ? -1.0 : ctl.lambda;
     __shared__ double red[kBaBlock / 64][36];
     __shared__ double lam_s;
     if (lam < 0) {
@@ -636,27 +692,34 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a, double lam, int 
 
 // ---------------------------------------------------------------- reduced system solve
 // LDL^T = U^T D U of the reduced camera system, blocked by the 6x6 pose blocks and held in
-// registers: thread t owns block (i, j), i <= j, of the upper triangle (36 doubles).  Block
-// step k (right-looking, two barriers): the owner of (k, k) factors it in registers and
-// publishes U_kk, D_k through LDS; owners of (k, j) solve W = U_kk^-T A_kj, U_kj = D_k^-1 W
-// and publish W, U; owners of (i, j), i > k apply A_ij -= W_ki^T U_kj.  The factor then goes
-// to LDS and one wave runs the blocked U^T z = b, y = z / D, U x = y.  Same factorisation as
-// LinearSolverEigen's SimplicialLDLT up to the rounding order.
+// registers: TPT threads own tile (i, j), i <= j, of the upper triangle, or block i of the
+// right-hand side carried through the factorisation as an extra tile column.  Block step k
+// has two phases and two barriers:
+//   B(k)  owners of (k, j > k) solve W = U_kk^-T A_kj, U_kj = D_k^-1 W and publish W, U (LDS);
+//         U_kj also goes to the packed factor H, the right-hand side tile gives y_k = D^-1 z_k.
+//         The owner of (k, k) stores U_kk^-1 (unit upper) for the back substitution.
+//   A(k)  owners of (i, j), i > k apply A_ij -= W_ki^T U_kj; the owner of (k+1, k+1) then
+//         factors its tile at once (lookahead), so no phase of its own is spent on it.
+// Back substitution U x = y: one wave, one block per step, x_k = U_kk^-1 (y_k - sum U_kj x_j).
+// Same factorisation as LinearSolverEigen's SimplicialLDLT up to the rounding order.
 constexpr int kBaSolveThreads = 512;  // >= TPT x tiles: 2 x (231 + 21) at np <= 21, 465 + 30 at np <= 30
 constexpr int kBaSolveTpt2MaxPoses = 21;
-#ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: phase timestamps of thread 0
+#ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: s_memtime stamps kept in LDS, copied out at the end
 __device__ unsigned long long g_solve_trace[256];
-__device__ unsigned long long g_solve_clk[2];
-#define SOLVE_MARK(i)                                                                        \
+#define SOLVE_STAMP_DECL __shared__ unsigned long long tstamp[256]
+#define SOLVE_STAMP(cond, i)                                                                 \
     do {                                                                                     \
-        if (threadIdx.x == 0) {                                                              \
-            g_solve_trace[i] = __builtin_amdgcn_s_memrealtime();                             \
-            if ((i) == 255) g_solve_clk[0] = __builtin_amdgcn_s_memtime();                   \
-            if ((i) == 201) g_solve_clk[1] = __builtin_amdgcn_s_memtime();                   \
-        }                                                                                    \
+        if (cond) tstamp[i] = __builtin_amdgcn_s_memtime();                                  \
+    } while (0)
+#define SOLVE_STAMP_FLUSH()                                                                  \
+    do {                                                                                     \
+        if (threadIdx.x == 0)                                                                \
+            for (int i_ = 0; i_ < 256; i_++) g_solve_trace[i_] = tstamp[i_];                 \
     } while (0)
 #else
-#define SOLVE_MARK(i) do {} while (0)
+#define SOLVE_STAMP_DECL
+#define SOLVE_STAMP(cond, i) do {} while (0)
+#define SOLVE_STAMP_FLUSH() do {} while (0)
 #endif
 
 __device__ inline void wave_sync_lds() {
@@ -665,13 +728,58 @@ __device__ inline void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// value of the neighbouring lane (lane ^ 1) through DPP quad_perm [1,0,3,2] (no LDS round trip)
+__device__ inline double dpp_xor1(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// 1 / d: v_rcp_f64 and two Newton steps (the pivots of the reduced system)
+__device__ inline double rcp_f64(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+// LDL^T of a 6x6 tile (full row-major, upper triangle used): on return F[j][c] = U_jc (c > j),
+// F[j][j] = d_j, inv6 = 1 / d.  False on a zero or non-finite pivot.
+__device__ inline bool ldl6(double F[36], double inv6[6]) {
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const double d = F[j * 7];
+        bad |= !(fabs(d) > 0) || !isfinite(d);
+        const double inv = rcp_f64(d);
+        inv6[j] = inv;
+#pragma unroll
+        for (int c = j + 1; c < 6; c++) {
+            const double u = F[j * 6 + c] * inv;  // u_jc
+#pragma unroll
+            for (int r = j + 1; r <= c; r++) F[r * 6 + c] -= F[j * 6 + r] * u;
+        }
+#pragma unroll
+        for (int c = j + 1; c < 6; c++) F[j * 6 + c] *= inv;
+    }
+    return !bad;
+}
+
 template <int TPT>  // threads per tile: 2 (np <= 21) or 1 (np <= kBaMaxPoses)
-__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, double lam, const double* __restrict__ T,
-                                                              double* __restrict__ Tt) {
+__global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done) return;
+    const int np = ctl.np;
+    double lam = a.scal[3];
+    const double* __restrict__ T = a.Tb[ctl.cur];
+    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
     constexpr int CPT = 6 / TPT;  // tile columns per thread
-    SOLVE_MARK(255);
+    SOLVE_STAMP_DECL;
+    SOLVE_STAMP(threadIdx.x == 0, 250);
     constexpr int kSlot = 37;  // odd stride in doubles: conflict-free LDS rows
-    __shared__ double H[kBaPacked];
+    __shared__ double H[kBaPacked];  // the factor: U_kj (k < j) at packed offsets
+    __shared__ double Ui[kBaMaxPoses * 15];  // U_kk^-1 (unit upper), strict upper row by row
     __shared__ double Wp[(kBaMaxPoses + 1) * kSlot], Up[(kBaMaxPoses + 1) * kSlot];
     __shared__ double Ud[36], Dinv6[6];
     __shared__ double bs[kBaMaxN];
@@ -680,8 +788,7 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
     const int N = 6 * np, nblk = np * (np + 1) / 2;
     const int tid = threadIdx.x;
     // TPT adjacent threads -> tile (bi, bj) of the upper triangle, or (bi, np) = block bi of
-    // the right-hand side carried through the factorisation (the forward substitution
-    // U^T z = b, D y = z).  Thread h of the tile owns its columns CPT h .. CPT h + CPT - 1.
+    // the right-hand side.  Thread h of the tile owns its columns CPT h .. CPT h + CPT - 1.
     const int tile = tid / TPT, h = tid % TPT, c0 = CPT * h;
     const bool own = tile < nblk + np;
     const bool rhs = own && tile >= nblk;
@@ -697,65 +804,57 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
     const bool dg = !rhs && bi == bj;
     for (int q = tid; q < N; q += blockDim.x) rb[q] = q * N - q * (q - 1) / 2 - q;
     double A[6 * CPT];  // A[r * CPT + cc] = element (r, c0 + cc) of the tile
+    // branch-free loads (clamped addresses, then a select) so that all of them are in flight
 #pragma unroll
     for (int q = 0; q < 6 * CPT; q++) {
         const int r = q / CPT, c = c0 + q % CPT;
-        A[q] = 0.0;
-        if (rhs) { if (c == 0) A[q] = a.bs[6 * bi + r]; }
-        else if (own && (!dg || c >= r)) A[q] = a.S[packed(6 * bi + r, 6 * bj + c, N)];
+        const bool mat = own && !rhs && (!dg || c >= r), vec = rhs && c == 0;
+        const double* src = vec ? a.bs + 6 * bi + r : a.S + (mat ? packed(6 * bi + r, 6 * bj + c, N) : 0);
+        const double v = *src;
+        A[q] = (mat || vec) ? v : 0.0;
     }
     if (tid == 0) fail = 0;
-    __syncthreads();
-    SOLVE_MARK(0);
-    for (int k = 0; k < np; k++) {
-        if (own && bi == k && bj == k) {  // (1) diagonal tile: both halves factor it redundantly
-            double F[36];
-            if constexpr (TPT == 2) {
+    // the owner of a diagonal tile factors it and publishes U_kk, 1 / D_k
+    auto factor_diag = [&]() {
+        double F[36];
+        if constexpr (TPT == 2) {
 #pragma unroll
-                for (int q = 0; q < 18; q++) {
-                    const double o = __shfl_xor(A[q], 1, 64);
-                    const int r = q / 3, cc = q % 3;
-                    F[r * 6 + cc] = h == 0 ? A[q] : o;
-                    F[r * 6 + 3 + cc] = h == 0 ? o : A[q];
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 36; q++) F[q] = A[q];
+            for (int q = 0; q < 18; q++) {
+                const double o = dpp_xor1(A[q]);
+                const int r = q / 3, cc = q % 3;
+                F[r * 6 + cc] = h == 0 ? A[q] : o;
+                F[r * 6 + 3 + cc] = h == 0 ? o : A[q];
             }
-            bool bad = false;
-            double inv6[6];
+        } else {
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const double d = F[j * 7];
-                bad |= !(fabs(d) > 0) || !isfinite(d);
-                const double inv = 1.0 / d;
-                inv6[j] = inv;
-#pragma unroll
-                for (int c = j + 1; c < 6; c++) {
-                    const double u = F[j * 6 + c] * inv;  // u_jc
-#pragma unroll
-                    for (int r = j + 1; r <= c; r++) F[r * 6 + c] -= F[j * 6 + r] * u;
-                }
-#pragma unroll
-                for (int c = j + 1; c < 6; c++) F[j * 6 + c] *= inv;
-            }
-#pragma unroll
-            for (int q = 0; q < 6 * CPT; q++) {
-                const int r = q / CPT, cc = q % CPT;
-                A[q] = (TPT == 1 || h == 0) ? F[r * 6 + cc] : F[r * 6 + CPT + cc];
-            }
-            if (h == 0) {
-#pragma unroll
-                for (int q = 0; q < 36; q++) Ud[q] = F[q];
-#pragma unroll
-                for (int j = 0; j < 6; j++) Dinv6[j] = inv6[j];
-                if (bad) fail = 1;
-            }
+            for (int q = 0; q < 36; q++) F[q] = A[q];
         }
-        __syncthreads();
-        SOLVE_MARK(1 + 3 * k);
+        double inv6[6];
+        const bool ok = ldl6(F, inv6);
+        if (h == 0) {
+#pragma unroll
+            for (int q = 0; q < 36; q++) Ud[q] = F[q];
+            int q = 0;
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = i + 1; j < 6; j++, q++) Ui[15 * bi + q] = F[i * 6 + j];
+#pragma unroll
+            for (int j = 0; j < 6; j++) Dinv6[j] = inv6[j];
+            if (!ok) fail = 1;
+        }
+    };
+    __syncthreads();
+    if (own && dg && bi == 0) factor_diag();
+    __syncthreads();
+    SOLVE_STAMP(tid == 0, 251);
+    for (int k = 0; k < np; k++) {
         if (fail) break;
-        if (own && bi == k && bj > k) {  // (2) block row: W = U_kk^-T A_kj, U_kj = D^-1 W
+        // ---- B(k): block row k
+        if (own && bi == k && bj > k) {
+            int hrow[6];
+#pragma unroll
+            for (int r = 0; r < 6; r++) hrow[r] = rb[6 * k + r];
             double ud[15];
             {
                 int q = 0;
@@ -779,33 +878,41 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
                 A[q] *= Dinv6[r];
                 Up[bj * kSlot + r * 6 + c] = A[q];
             }
+            if (!rhs) {
+#pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    const int o = hrow[r] + 6 * bj + c0;
+#pragma unroll
+                    for (int cc = 0; cc < CPT; cc++) H[o + cc] = A[r * CPT + cc];
+                }
+            } else if (h == 0) {
+#pragma unroll
+                for (int r = 0; r < 6; r++) bs[6 * k + r] = A[r * CPT];
+            }
+            SOLVE_STAMP(bj == k + 1 && h == 0, 4 * k);
         }
         __syncthreads();
-        SOLVE_MARK(2 + 3 * k);
-        if (own && bi > k && !(rhs && h > 0)) {  // (3) trailing update of the owned columns
-            double u[6 * CPT];
+        // ---- A(k): trailing update; the next diagonal tile is factored as soon as it is final
+        if (own && bi > k) {
+            // A -= W_ki^T U_kj with 6 CPT independent accumulation chains (the unused lower part
+            // of a diagonal tile and the zero columns of a right-hand-side tile stay harmless)
+            double u[6 * CPT], w[36];
 #pragma unroll
             for (int q = 0; q < 6 * CPT; q++) u[q] = Up[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
 #pragma unroll
-            for (int r = 0; r < 6; r++) {
-                double w[6];
+            for (int q = 0; q < 36; q++) w[q] = Wp[bi * kSlot + q];  // w[t * 6 + r] = W_ki(t, r)
 #pragma unroll
-                for (int t = 0; t < 6; t++) w[t] = Wp[bi * kSlot + t * 6 + r];
+            for (int t = 0; t < 6; t++)
 #pragma unroll
-                for (int cc = 0; cc < CPT; cc++) {
-                    if (dg && c0 + cc < r) continue;
-                    if (rhs && cc > 0) continue;
-                    double s2 = 0;
+                for (int r = 0; r < 6; r++)
 #pragma unroll
-                    for (int t = 0; t < 6; t++) s2 += w[t] * u[t * CPT + cc];
-                    A[r * CPT + cc] -= s2;
-                }
-            }
+                    for (int cc = 0; cc < CPT; cc++) A[r * CPT + cc] -= w[t * 6 + r] * u[t * CPT + cc];
+            SOLVE_STAMP(dg && bi == k + 1 && h == 0, 4 * k + 1);
+            if (dg && bi == k + 1) factor_diag();
+            SOLVE_STAMP(dg && bi == k + 1 && h == 0, 4 * k + 2);
         }
-#ifdef ORBMI_SOLVE_TRACE
         __syncthreads();
-        SOLVE_MARK(3 + 3 * k);
-#endif
+        SOLVE_STAMP(tid == 0, 4 * k + 3);
     }
     if (fail) {  // pop: trial poses = current ones, computeScale = 0
         for (int k = tid; k < a.nkf; k += blockDim.x)
@@ -813,39 +920,74 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
         if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
         return;
     }
-    // factor to LDS (packed upper, U above the diagonal) and y to bs
-    if (own && !rhs) {
+    // U_kk^-1 (unit upper) of every diagonal block in place, one thread per block:
+    // X(i, j) = -(U(i, j) + sum_{i < m < j} U(i, m) X(m, j))
+    if (tid < np) {
+        double U[36];
+        {
+            int q = 0;
 #pragma unroll
-        for (int q = 0; q < 6 * CPT; q++) {
-            const int r = q / CPT, c = c0 + q % CPT;
-            if (!dg || c >= r) H[rb[6 * bi + r] + 6 * bj + c] = A[q];
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = i + 1; j < 6; j++, q++) U[i * 6 + j] = Ui[15 * tid + q];
         }
-    }
-    if (rhs && h == 0)
+        double X[36];
 #pragma unroll
-        for (int r = 0; r < 6; r++) bs[6 * bi + r] = A[r * CPT];
+        for (int j = 1; j < 6; j++)
+#pragma unroll
+            for (int i = j - 1; i >= 0; i--) {
+                double s2 = U[i * 6 + j];
+#pragma unroll
+                for (int m = i + 1; m < j; m++) s2 += U[i * 6 + m] * X[m * 6 + j];
+                X[i * 6 + j] = -s2;
+            }
+        int q = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = i + 1; j < 6; j++, q++) Ui[15 * tid + q] = X[i * 6 + j];
+    }
     __syncthreads();
-    SOLVE_MARK(200);
     if (tid >= 64) return;
     const int lane = tid;
-    SOLVE_MARK(202);
-    // U x = y, blocked from the last block up (one wave)
+    // U x = y, blocked from the last block up (one wave): x_k = U_kk^-1 y_k, then y_j -= U_jk x_k.
+    // Every LDS read of a step is issued before the first use; rows jj = lane + 64 m.
+    constexpr int NM = kBaMaxN / 64 + 1;
+    int rbj[NM];
+#pragma unroll
+    for (int m = 0; m < NM; m++) rbj[m] = lane + 64 * m < N ? rb[lane + 64 * m] : 0;
     for (int k = np - 1; k >= 0; k--) {
         const int k0 = 6 * k;
-        double x[6];
+        double y[6], x[6], ui[15], hr[NM][6], bv[NM];
 #pragma unroll
-        for (int t = 5; t >= 0; t--) {
-            double v = bs[k0 + t];
+        for (int t = 0; t < 6; t++) y[t] = bs[k0 + t];
 #pragma unroll
-            for (int s2 = t + 1; s2 < 6; s2++) v -= H[rb[k0 + t] + k0 + s2] * x[s2];
-            x[t] = v;
+        for (int q = 0; q < 15; q++) ui[q] = Ui[15 * k + q];
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int jj = lane + 64 * m;
+            const bool v = jj < k0;
+            const int base = v ? rbj[m] + k0 : 0;
+#pragma unroll
+            for (int t = 0; t < 6; t++) hr[m][t] = H[base + t];
+            bv[m] = bs[v ? jj : 0];
         }
-        for (int jj = lane; jj < k0; jj += 64) {
-            const int base = rb[jj] + k0;
-            double v = bs[jj];
+        {
+            int q = 0;
 #pragma unroll
-            for (int t = 0; t < 6; t++) v -= H[base + t] * x[t];
-            bs[jj] = v;
+            for (int t = 0; t < 6; t++) {
+                double v = y[t];
+#pragma unroll
+                for (int s2 = t + 1; s2 < 6; s2++, q++) v += ui[q] * y[s2];
+                x[t] = v;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int jj = lane + 64 * m;
+            const double v0 = hr[m][0] * x[0] + hr[m][1] * x[1] + hr[m][2] * x[2];
+            const double v1 = hr[m][3] * x[3] + hr[m][4] * x[4] + hr[m][5] * x[5];
+            if (jj < k0) bs[jj] = bv[m] - (v0 + v1);
         }
         if (lane < 6) {
 #pragma unroll
@@ -854,10 +996,9 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
         }
         wave_sync_lds();
     }
-    SOLVE_MARK(201);
+    SOLVE_STAMP(lane == 0, 252);
     // trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
     // computeScale, sum x_p (lambda x_p + b_p) in index order
-    if (lam < 0) lam = a.scal[3];
     for (int k = lane; k < a.nkf; k += 64) {
         const int pi = a.pose_idx[k];
         if (pi >= 0) {
@@ -876,6 +1017,8 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
         a.scal[2] = 1;
         a.istat[3] = 1;
     }
+    SOLVE_STAMP(lane == 0, 253);
+    SOLVE_STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------- update + trial errors
@@ -883,13 +1026,17 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a, int np, d
 // part); then every thread takes edges of the block's points: computeActiveErrors on the trial
 // state (T_t from k_ba_pose_trial).  Block partials: robust chi2 and scale.
 constexpr int kBaUpdPts = 32;
-__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a, double lam, const double* __restrict__ X,
-                                                               const double* __restrict__ Tt, double* __restrict__ Xt,
-                                                               double* __restrict__ part_chi,
-                                                               double* __restrict__ part_scale) {
+__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done) return;
+    const double lam = a.scal[3];
+    const double* __restrict__ X = a.Xb[ctl.cur];
+    const double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    double* __restrict__ Xt = a.Xb[ctl.cur ^ 1];
+    double* __restrict__ part_chi = a.part_tchi;
+    double* __restrict__ part_scale = a.part_tscale;
     __shared__ double red[kBaBlock / 64];
     __shared__ double xs[kBaUpdPts][4];
-    if (lam < 0) lam = a.scal[3];
     const bool ok = a.istat[3] != 0;
     const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
     double sc = 0, chi = 0;
@@ -934,12 +1081,81 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a, double l
     }
 }
 
+// ---------------------------------------------------------------- Levenberg control
+// fixed-order sum of n partials by one wave (lane l: l, l + 64, ...; then a fixed xor tree,
+// lane 0's value broadcast): deterministic run to run
+__device__ inline double wave_sum_fixed(const double* p, int n) {
+    double s = 0;
+    for (int k = threadIdx.x; k < n; k += 64) s += p[k];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return __shfl(s, 0, 64);
+}
+
+// one wave, after each trial: OptimizationAlgorithmLevenberg::solve's decision
+// (levenberg.cpp:104-164) and SparseOptimizer::optimize's loop (sparse_optimizer.cpp:354-419)
+// with ORB-SLAM2's 3-bad-iterations stop; pbStopFlag is read through the host-mapped mirror
+__global__ __launch_bounds__(64) void k_ba_control(BaDev a) {
+    BaCtl& c = *a.ctl;
+    if (c.done) return;
+    const double lin = wave_sum_fixed(a.part_lin, a.nb_e);
+    const double tchi = wave_sum_fixed(a.part_tchi, a.nb_q);
+    const double tsc = wave_sum_fixed(a.part_tscale, a.nb_q);
+    if (threadIdx.x != 0) return;
+    if (c.trial == 0) c.iniChi = c.currentChi = lin;  // computeActiveErrors at iteration entry
+    if (c.it == 0 && c.trial == 0) c.lambda = a.scal[3];  // computeLambdaInit (k_ba_schur)
+    const bool ok2 = a.scal[2] != 0;
+    const double tempChi = ok2 ? tchi : DBL_MAX;
+    const double scale = ok2 ? tsc + a.scal[1] : 0.0;
+    const double rho = (c.currentChi - tempChi) / (scale + 1e-3);
+    if (rho > 0 && isfinite(tempChi)) {  // accept: the trial buffers become current
+        double alpha = 1. - pow(2 * rho - 1, 3);
+        alpha = fmin(alpha, 2. / 3.);
+        c.lambda *= fmax(1. / 3., alpha);
+        c.ni = 2;
+        c.currentChi = tempChi;
+        c.cur ^= 1;
+    } else {  // reject: pop (the trial buffers are not adopted)
+        c.lambda *= c.ni;
+        c.ni *= 2;
+    }
+    c.trial++;
+    c.steps++;
+    const bool stop = a.stop && *a.stop;
+    if (rho < 0 && c.trial < 10 && !stop) {  // next trial of the same iteration
+        c.need_lin = 0;
+        return;
+    }
+    c.it++;
+    bool term;
+    if (c.trial == 10 || rho == 0) {
+        term = true;
+    } else {
+        if ((c.iniChi - c.currentChi) * 1e3 < c.iniChi) c.nbad++;
+        else c.nbad = 0;
+        term = c.nbad >= 3;
+    }
+    c.trial = 0;
+    c.need_lin = 1;
+    if (term || c.it >= c.max_it || stop) c.done = 1;
+}
+
+// activeRobustChi2 after optimize() (k_ba_errors partials) and the iteration count
+__global__ __launch_bounds__(64) void k_ba_chi(BaDev a, int phase) {
+    const double chi = wave_sum_fixed(a.part_lin, a.nb_e);
+    if (threadIdx.x == 0) {
+        BaCtl& c = *a.ctl;
+        c.chi_out[phase] = chi;
+        c.it_out[phase] = (c.np + c.nl == 0) ? -1 : c.it;
+    }
+}
+
 // vToErase (src/Optimizer.cc:741-773) + write back (Converter::toCvMat)
-__global__ __launch_bounds__(kBaBlock) void k_ba_finish(BaDev a, const double* __restrict__ T,
-                                                        const double* __restrict__ X, float* __restrict__ out_tcw,
+__global__ __launch_bounds__(kBaBlock) void k_ba_finish(BaDev a, float* __restrict__ out_tcw,
                                                         float* __restrict__ out_pos,
                                                         unsigned char* __restrict__ out_erase) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const double* T = a.Tb[a.ctl->cur];
+    const double* X = a.Xb[a.ctl->cur];
     if (i < a.nedge) {
         const orbmi_ba_edge e = a.edges[i];
         if (!a.pts[e.point].bad) {
@@ -970,127 +1186,81 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_finish(BaDev a, const double* _
 struct orbmi_ba {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
     uint8_t* d_buf = nullptr;
     size_t cap = 0;
-    double* h_rb = nullptr;    // pinned readback of the per-trial scalars and partial sums
-    size_t cap_rb = 0;
-    int* h_istat = nullptr;
+    uint8_t* h_stage = nullptr;  // pinned staging of the uploaded graph (one H2D copy)
+    size_t cap_stage = 0;
+    orbmi::BaCtl* h_ctl = nullptr;  // pinned readback of the LM control block
+    int* h_stop = nullptr;          // host-mapped mirror of the caller's stop flag
+    int* d_stop = nullptr;          //   (its device address)
 };
 
 namespace {
 
 using namespace orbmi;
 
+// Trial steps enqueued beyond the iterations still to run: a rejected trial consumes one step
+// without finishing an iteration, so the first readback usually already sees optimize() done.
+constexpr int kBaStepSlack = 1;
+
 struct Runner {
     orbmi_ba& h;
     BaDev a;
-    double *T, *Tt, *X, *Xt;
-    double* rb;        // device readback region: scal[8] | linearize chi2 | trial chi2 | trial scale
-    double* part_max;  // nb_p + np partial maxima of |diag H|
-    int nb_e, nb_p, nb_q;  // blocks: edges, points (256 / block), points (32 / block)
     const volatile int* stop;
-    int np = 0, nl = 0;
+    int solve_tpt;  // 2: nf <= kBaSolveTpt2MaxPoses, else 1
 
     bool stopped() const { return stop && *stop; }
-    double* lin() const { return rb + 8; }
-    double* tchi() const { return rb + 8 + nb_e; }
-    double* tscale() const { return rb + 8 + nb_e + nb_q; }
-    static double sum(const double* p, int n) {  // fixed order
-        double s = 0;
-        for (int k = 0; k < n; k++) s += p[k];
-        return s;
-    }
 
-    int readback() {
-        ORBMI_HIP(hipMemcpyAsync(h.h_rb, rb, (8 + nb_e + 2 * (size_t)nb_q) * sizeof(double), hipMemcpyDeviceToHost,
-                                 h.stream));
-        ORBMI_HIP(hipStreamSynchronize(h.stream));
-        return ORBMI_OK;
-    }
-
-    int activate() {
-        hipLaunchKernelGGL(k_ba_activate, dim3(1), dim3(1024), 0, h.stream, a);
-        ORBMI_HIP(hipMemcpyAsync(h.h_istat, a.istat, 4 * sizeof(int), hipMemcpyDeviceToHost, h.stream));
-        ORBMI_HIP(hipStreamSynchronize(h.stream));
-        if (h.h_istat[2]) return ORBMI_E_UNSUPPORTED;
-        np = h.h_istat[0];
-        nl = h.h_istat[1];
-        return ORBMI_OK;
-    }
-
-    // activeRobustChi2 on the (stale) stored errors
-    int robust_chi2(double* out) {
-        hipLaunchKernelGGL(k_ba_errors, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, 0, lin());
-        int rc = readback();
-        *out = sum(h.h_rb + 8, nb_e);
-        return rc;
-    }
-
-    // OptimizationAlgorithmLevenberg::solve (levenberg.cpp:61-164); *terminate = 1 on stop.
-    // Per trial: k_ba_schur, k_ba_solve, k_ba_update_errors and one readback of the partials.
-    int lm_iteration(int iteration, double* lambda, double* ni, int* nbad, int* terminate) {
-        const int N = 6 * np;
-        hipLaunchKernelGGL(k_ba_linearize, dim3(nb_e), dim3(kBaBlock), 0, h.stream, a, T, X, lin());
-        hipLaunchKernelGGL(k_ba_reduce, dim3(nb_p + np), dim3(kBaBlock), 0, h.stream, a, nb_p, part_max);
-        double lam_arg = iteration == 0 ? -1.0 : *lambda;  // -1: computeLambdaInit on the device
-        if (iteration == 0) { *ni = 2; *nbad = 0; }
-        double currentChi = 0, iniChi = 0, rho = 0;
-        int qmax = 0, rc;
-        do {
-            if (a.nblk > 0)
-                hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kBaBlock), 0, h.stream, a, lam_arg, N, part_max,
-                                   nb_p + np);
-            if (np <= kBaSolveTpt2MaxPoses)
-                hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np, lam_arg, T, Tt);
-            else
-                hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a, np, lam_arg, T, Tt);
-            hipLaunchKernelGGL(k_ba_update_errors, dim3(nb_q), dim3(kBaBlock), 0, h.stream, a, lam_arg, X, Tt, Xt,
-                               tchi(), tscale());
-            ORBMI_HIP(hipGetLastError());
-            if ((rc = readback())) return rc;
-            const double* hb = h.h_rb;
-            if (qmax == 0) iniChi = currentChi = sum(hb + 8, nb_e);  // computeActiveErrors at entry
-            if (lam_arg < 0) *lambda = hb[3];                       // lambda chosen on the device
-            const bool ok2 = hb[2] != 0;
-            const double tempChi = ok2 ? sum(hb + 8 + nb_e, nb_q) : DBL_MAX;
-            const double scale = ok2 ? sum(hb + 8 + nb_e + nb_q, nb_q) + hb[1] : 0.0;
-            rho = (currentChi - tempChi) / (scale + 1e-3);
-            if (rho > 0 && std::isfinite(tempChi)) {  // accept: the trial buffers become current
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
-                alpha = std::min(alpha, 2. / 3.);
-                const double sf = std::max(1. / 3., alpha);
-                *lambda *= sf;
-                *ni = 2;
-                currentChi = tempChi;
-                std::swap(T, Tt);
-                std::swap(X, Xt);
-            } else {  // reject: pop (the trial buffers are simply not adopted)
-                *lambda *= *ni;
-                *ni *= 2;
-            }
-            lam_arg = *lambda;
-            qmax++;
-        } while (rho < 0 && qmax < 10 && !stopped());
-        if (qmax == 10 || rho == 0) { *terminate = 1; return ORBMI_OK; }
-        // ORB-SLAM2's modified g2o: 3 consecutive iterations without a 1e-3 relative decrease
-        if ((iniChi - currentChi) * 1e3 < iniChi) (*nbad)++;
-        else *nbad = 0;
-        *terminate = *nbad >= 3;
-        return ORBMI_OK;
-    }
-
-    // SparseOptimizer::optimize(iterations); -1 with an empty index mapping
-    int optimize(int iterations, int* it) {
-        *it = 0;
-        if (np + nl == 0) { *it = -1; return ORBMI_OK; }
-        double lambda = 0, ni = 2;
-        int nbad = 0;
-        for (int i = 0; i < iterations && !stopped(); i++) {
-            int term = 0, rc;
-            if ((rc = lm_iteration(i, &lambda, &ni, &nbad, &term))) return rc;
-            ++*it;
-            if (term) break;
+    // wait for the stream; meanwhile mirror the caller's stop flag to the device
+    int wait() {
+        ORBMI_HIP(hipEventRecord(h.done, h.stream));
+        if (!stop) {
+            ORBMI_HIP(hipEventSynchronize(h.done));
+            return ORBMI_OK;
         }
+        for (;;) {
+            *(volatile int*)h.h_stop = *stop ? 1 : 0;
+            const hipError_t e = hipEventQuery(h.done);
+            if (e == hipSuccess) return ORBMI_OK;
+            if (e != hipErrorNotReady) return ORBMI_E_HIP;
+        }
+    }
+
+    int read_ctl() {
+        ORBMI_HIP(hipMemcpyAsync(h.h_ctl, a.ctl, sizeof(BaCtl), hipMemcpyDeviceToHost, h.stream));
+        return wait();
+    }
+
+    // one LM trial: [linearize + reduce at an iteration start] + Schur + solve + update + control;
+    // every kernel returns at once when optimize() is done
+    void step() {
+        hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
+        if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kBaBlock), 0, h.stream, a);
+        if (solve_tpt == 2) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
+        else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaBlock), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(64), 0, h.stream, a);
+    }
+
+    // SparseOptimizer::optimize(iterations) as phase 0 / 1, then activeRobustChi2
+    int optimize(int iterations, int phase) {
+        hipLaunchKernelGGL(k_ba_activate, dim3(1), dim3(1024), 0, h.stream, a, stopped() ? 0 : iterations);
+        int todo = stopped() ? 0 : iterations + kBaStepSlack;
+        while (todo > 0) {
+            for (int k = 0; k < todo; k++) step();
+            ORBMI_HIP(hipGetLastError());
+            int rc;
+            if ((rc = read_ctl())) return rc;
+            const BaCtl& c = *h.h_ctl;
+            if (c.unsupported) return ORBMI_E_UNSUPPORTED;
+            if (c.done || stopped()) break;
+            todo = c.max_it - c.it;  // rejected trials used up the slack
+        }
+        hipLaunchKernelGGL(k_ba_errors, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_chi, dim3(1), dim3(64), 0, h.stream, a, phase);
+        ORBMI_HIP(hipGetLastError());
         return ORBMI_OK;
     }
 };
@@ -1108,11 +1278,14 @@ int orbmi_ba_create(int device, orbmi_ba** out) {
     if (!b) return ORBMI_E_ARG;
     b->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
-
-        hipHostMalloc((void**)&b->h_istat, 4 * sizeof(int)) != hipSuccess) {
+        hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&b->h_ctl, sizeof(BaCtl)) != hipSuccess ||
+        hipHostMalloc((void**)&b->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&b->d_stop, b->h_stop, 0) != hipSuccess) {
         orbmi_ba_destroy(b);
         return ORBMI_E_HIP;
     }
+    *b->h_stop = 0;
     *out = b;
     return ORBMI_OK;
 }
@@ -1122,8 +1295,10 @@ void orbmi_ba_destroy(orbmi_ba* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     if (b->d_buf) (void)hipFree(b->d_buf);
-    if (b->h_rb) (void)hipHostFree(b->h_rb);
-    if (b->h_istat) (void)hipHostFree(b->h_istat);
+    if (b->h_stage) (void)hipHostFree(b->h_stage);
+    if (b->h_ctl) (void)hipHostFree(b->h_ctl);
+    if (b->h_stop) (void)hipHostFree(b->h_stop);
+    if (b->done) (void)hipEventDestroy(b->done);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
@@ -1182,48 +1357,41 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     std::vector<int> blk_kf(2 * std::max(nblk, 1)), blk_start(nblk + 1, 0);
     for (int ra = 0; ra < nf; ra++)
         for (int rb = ra; rb < nf; rb++) { blk_kf[2 * blk_of(ra, rb)] = free_kf[ra]; blk_kf[2 * blk_of(ra, rb) + 1] = free_kf[rb]; }
-    std::vector<int2> pairs;
+    std::vector<int> erank(std::max(ne, 1));
+    for (int i = 0; i < ne; i++) erank[i] = rank[P->edges[i].kf];
     for (int p = 0; p < npt; p++)
         for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
-            const int r1 = rank[P->edges[e1].kf];
+            const int r1 = erank[e1];
             if (r1 < 0) continue;
             for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
-                const int r2 = rank[P->edges[e2].kf];
+                const int r2 = erank[e2];
                 if (r2 >= r1) blk_start[blk_of(r1, r2) + 1]++;
             }
         }
     for (int k = 0; k < nblk; k++) blk_start[k + 1] += blk_start[k];
-    pairs.resize(std::max(blk_start[nblk], 1));
-    {
-        std::vector<int> fill(blk_start.begin(), blk_start.end() - 1);
-        for (int p = 0; p < npt; p++)
-            for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
-                const int r1 = rank[P->edges[e1].kf];
-                if (r1 < 0) continue;
-                for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
-                    const int r2 = rank[P->edges[e2].kf];
-                    if (r2 >= r1) pairs[fill[blk_of(r1, r2)]++] = make_int2(e1, e2);
-                }
-            }
-    }
     const int npair = blk_start[nblk];
-    // one device arena
+    // ---- one device arena; the graph and its index arrays go up in one copy
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
     const int nb_q = std::max(1, (npt + kBaUpdPts - 1) / kBaUpdPts);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += al(std::max(bytes, (size_t)8)); return o; };
+    // uploaded region first (contiguous)
     const size_t o_kfs = take(sizeof(orbmi_ba_keyframe) * nkf), o_pts = take(sizeof(orbmi_ba_point) * npt),
                  o_edges = take(sizeof(orbmi_ba_edge) * ne), o_order = take(4 * nkf), o_pts_start = take(4 * (npt + 1)),
-                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne), o_kf_pt = take(4 * (size_t)ne), o_e_pi = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
-                 o_blk_start = take(4 * ((size_t)nblk + 1)), o_pairs = take(8 * (size_t)npair),
-                 o_T = take(64 * nkf), o_Tt = take(64 * nkf), o_X = take(32 * npt), o_Xt = take(32 * npt),
-                 o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_pkf = take(4 * kBaMaxPoses),
-                 o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne), o_Hpe = take(216 * (size_t)ne),
-                 o_Hll = take(72 * npt), o_bl = take(24 * npt), o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses),
-                 o_S = take(8 * (size_t)kBaPacked), o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN),
-                 o_rb = take(8 * (8 + (size_t)nb_e + 2 * (size_t)nb_q)), o_pmax = take(8 * ((size_t)nb_p + kBaMaxPoses)),
-                 o_istat = take(32), o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
+                 o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne),
+                 o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
+                 o_blk_start = take(4 * ((size_t)nblk + 1)), o_pairs = take(8 * (size_t)npair);
+    const size_t up_bytes = off;
+    const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
+                 o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf),
+                 o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne),
+                 o_Hpe = take(216 * (size_t)ne), o_Hll = take(72 * npt), o_bl = take(24 * npt),
+                 o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses), o_S = take(8 * (size_t)kBaPacked),
+                 o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN), o_scal = take(64), o_plin = take(8 * (size_t)nb_e),
+                 o_ptchi = take(8 * (size_t)nb_q), o_ptsc = take(8 * (size_t)nb_q),
+                 o_pmax = take(8 * ((size_t)nb_p + kBaMaxPoses)), o_istat = take(32), o_ctl = take(sizeof(BaCtl)),
+                 o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
     if (off > h.cap) {
         if (h.d_buf) (void)hipFree(h.d_buf);
         h.d_buf = nullptr;
@@ -1231,26 +1399,56 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         ORBMI_HIP(hipMalloc((void**)&h.d_buf, off));
         h.cap = off;
     }
+    if (up_bytes > h.cap_stage) {
+        if (h.h_stage) (void)hipHostFree(h.h_stage);
+        h.h_stage = nullptr;
+        h.cap_stage = 0;
+        ORBMI_HIP(hipHostMalloc((void**)&h.h_stage, up_bytes));
+        h.cap_stage = up_bytes;
+    }
     uint8_t* B = h.d_buf;
+    uint8_t* S = h.h_stage;
     hipStream_t s = h.stream;
-    auto up = [&](size_t o, const void* src, size_t bytes) {
-        return bytes ? hipMemcpyAsync(B + o, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
-    };
-    ORBMI_HIP(up(o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf));
-    ORBMI_HIP(up(o_pts, P->pts, sizeof(orbmi_ba_point) * npt));
-    ORBMI_HIP(up(o_edges, P->edges, sizeof(orbmi_ba_edge) * ne));
-    ORBMI_HIP(up(o_order, order.data(), 4 * nkf));
-    ORBMI_HIP(up(o_pts_start, pt_start.data(), 4 * (npt + 1)));
-    ORBMI_HIP(up(o_kfs_start, kf_start.data(), 4 * (nkf + 1)));
-    ORBMI_HIP(up(o_kf_edges, kf_edges.data(), 4 * (size_t)ne));
-    ORBMI_HIP(up(o_kf_pos, kf_pos.data(), 4 * (size_t)ne));
-    ORBMI_HIP(up(o_kf_pt, kf_pt.data(), 4 * (size_t)ne));
-    ORBMI_HIP(up(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk));
-    ORBMI_HIP(up(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1)));
-    ORBMI_HIP(up(o_pairs, pairs.data(), 8 * (size_t)npair));
+    // the previous call's upload may still be reading the staging buffer
+    ORBMI_HIP(hipStreamSynchronize(s));
+    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(S + o, src, bytes); };
+    put(o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf);
+    put(o_pts, P->pts, sizeof(orbmi_ba_point) * npt);
+    put(o_edges, P->edges, sizeof(orbmi_ba_edge) * ne);
+    put(o_order, order.data(), 4 * nkf);
+    put(o_pts_start, pt_start.data(), 4 * (npt + 1));
+    put(o_kfs_start, kf_start.data(), 4 * (nkf + 1));
+    put(o_kf_edges, kf_edges.data(), 4 * (size_t)ne);
+    put(o_kf_pos, kf_pos.data(), 4 * (size_t)ne);
+    put(o_kf_pt, kf_pt.data(), 4 * (size_t)ne);
+    put(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk);
+    put(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1));
+    {  // the pair lists, written straight into the staging buffer
+        int2* pairs = (int2*)(S + o_pairs);
+        std::vector<int> fill(blk_start.begin(), blk_start.end() - 1);
+        for (int p = 0; p < npt; p++)
+            for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
+                const int r1 = erank[e1];
+                if (r1 < 0) continue;
+                for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
+                    const int r2 = erank[e2];
+                    if (r2 >= r1) pairs[fill[blk_of(r1, r2)]++] = make_int2(e1, e2);
+                }
+            }
+    }
+    ORBMI_HIP(hipMemcpyAsync(B, S, up_bytes, hipMemcpyHostToDevice, s));
     ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
+    ORBMI_HIP(hipMemsetAsync(B + o_ctl, 0, sizeof(BaCtl), s));
     BaDev a;
     a.nkf = nkf; a.npt = npt; a.nedge = ne; a.nblk = nblk; a.nf = nf;
+    a.nb_e = nb_e; a.nb_p = nb_p; a.nb_q = nb_q;
+    a.ctl = (BaCtl*)(B + o_ctl);
+    a.stop = stop ? h.d_stop : nullptr;
+    *h.h_stop = 0;
+    a.Tb[0] = (double*)(B + o_T0); a.Tb[1] = (double*)(B + o_T1);
+    a.Xb[0] = (double*)(B + o_X0); a.Xb[1] = (double*)(B + o_X1);
+    a.part_lin = (double*)(B + o_plin); a.part_tchi = (double*)(B + o_ptchi); a.part_tscale = (double*)(B + o_ptsc);
+    a.part_max = (double*)(B + o_pmax);
     a.kfs = (const orbmi_ba_keyframe*)(B + o_kfs);
     a.pts = (const orbmi_ba_point*)(B + o_pts);
     a.edges = (const orbmi_ba_edge*)(B + o_edges);
@@ -1270,44 +1468,32 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl);
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
-    a.scal = (double*)(B + o_rb); a.istat = (int*)(B + o_istat);
-    const size_t rb_bytes = 8 * (8 + (size_t)nb_e + 2 * (size_t)nb_q);
-    if (rb_bytes > h.cap_rb) {
-        if (h.h_rb) (void)hipHostFree(h.h_rb);
-        h.h_rb = nullptr;
-        h.cap_rb = 0;
-        ORBMI_HIP(hipHostMalloc((void**)&h.h_rb, rb_bytes));
-        h.cap_rb = rb_bytes;
-    }
-    Runner r{h, a, (double*)(B + o_T), (double*)(B + o_Tt), (double*)(B + o_X), (double*)(B + o_Xt),
-             (double*)(B + o_rb), (double*)(B + o_pmax), nb_e, nb_p, nb_q, stop};
+    a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
+    Runner r{h, a, stop, nf <= kBaSolveTpt2MaxPoses ? 2 : 1};
     unsigned char* out_erase = B + o_oerase;
-    hipLaunchKernelGGL(k_ba_setup, dim3(std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock)),
-                       dim3(kBaBlock), 0, s, a, r.T, r.X, out_erase);
+    const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
+    hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);
     ORBMI_HIP(hipGetLastError());
     int rc;
-    if ((rc = r.activate())) return rc;
-    int it0 = 0, it1 = 0;
-    double chi0 = 0, chi1 = 0;
-    if ((rc = r.optimize(5, &it0))) return rc;
-    if ((rc = r.robust_chi2(&chi0))) return rc;
-    if (!r.stopped()) {  // src/Optimizer.cc:694-737
-        hipLaunchKernelGGL(k_ba_levels, dim3(nb_e), dim3(kBaBlock), 0, s, a, r.T, r.X);
-        if ((rc = r.activate())) return rc;
-        if ((rc = r.optimize(10, &it1))) return rc;
-        if ((rc = r.robust_chi2(&chi1))) return rc;
+    if ((rc = r.optimize(5, 0))) return rc;
+    const bool second = !r.stopped();
+    if (second) {  // src/Optimizer.cc:694-737
+        hipLaunchKernelGGL(k_ba_levels, dim3(nb_e), dim3(kBaBlock), 0, s, a);
+        if ((rc = r.optimize(10, 1))) return rc;
     }
-    hipLaunchKernelGGL(k_ba_finish, dim3(std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock)),
-                       dim3(kBaBlock), 0, s, a, r.T, r.X, (float*)(B + o_otcw), (float*)(B + o_opos), out_erase);
+    hipLaunchKernelGGL(k_ba_finish, dim3(nb_all), dim3(kBaBlock), 0, s, a, (float*)(B + o_otcw), (float*)(B + o_opos),
+                       out_erase);
     ORBMI_HIP(hipGetLastError());
     if (nkf) ORBMI_HIP(hipMemcpyAsync(R->tcw, B + o_otcw, 64 * nkf, hipMemcpyDeviceToHost, s));
     if (npt) ORBMI_HIP(hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s));
     if (ne) ORBMI_HIP(hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s));
-    ORBMI_HIP(hipStreamSynchronize(s));
-    R->iterations[0] = it0;
-    R->iterations[1] = it1;
-    R->chi2[0] = chi0;
-    R->chi2[1] = chi1;
+    if ((rc = r.read_ctl())) return rc;
+    const BaCtl& c = *h.h_ctl;
+    if (c.unsupported) return ORBMI_E_UNSUPPORTED;
+    R->iterations[0] = c.it_out[0];
+    R->iterations[1] = second ? c.it_out[1] : 0;
+    R->chi2[0] = c.chi_out[0];
+    R->chi2[1] = second ? c.chi_out[1] : 0;
     return ORBMI_OK;
 }
 

@@ -29,16 +29,23 @@ int main(int argc, char** argv) {
     hipMemcpy(dbs, b.data(), N * 8, hipMemcpyHostToDevice);
     BaDev a{};
     a.S = dS; a.bs = dbs; a.xp = dxp; a.istat = dist;
-    // no keyframes: the trial-pose tail only writes the scale
+    // no keyframes: the trial-pose tail only writes the scale; lambda = 1 in scal[3]
     double *dT, *dTt, *dbp, *dscal;
     hipMalloc(&dT, 64); hipMalloc(&dTt, 64); hipMalloc(&dbp, kBaMaxN * 8); hipMalloc(&dscal, 64);
     hipMemset(dbp, 0, kBaMaxN * 8);
-    a.nkf = 0; a.bp = dbp; a.scal = dscal;
+    const double hscal[8] = {0, 0, 0, 1.0, 0, 0, 0, 0};
+    hipMemcpy(dscal, hscal, sizeof(hscal), hipMemcpyHostToDevice);
+    BaCtl hctl{};
+    hctl.np = np;
+    BaCtl* dctl;
+    hipMalloc(&dctl, sizeof(BaCtl));
+    hipMemcpy(dctl, &hctl, sizeof(BaCtl), hipMemcpyHostToDevice);
+    a.nkf = 0; a.bp = dbp; a.scal = dscal; a.ctl = dctl; a.Tb[0] = dT; a.Tb[1] = dTt;
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     auto launch = [&] {
-        if (np <= kBaSolveTpt2MaxPoses) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np, 1.0, dT, dTt);
-        else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, 0, a, np, 1.0, dT, dTt);
+        if (np <= kBaSolveTpt2MaxPoses && !getenv("TPT1")) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
+        else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
     };
     for (int it = 0; it < 3; it++) launch();
     hipEventRecord(e0);
@@ -59,19 +66,20 @@ int main(int argc, char** argv) {
         res = std::max(res, std::fabs(s - b[i]));
     }
     printf("np=%d N=%d  avg kernel %.2f us  residual %.3e\n", np, N, ms * 1e3 / reps, res);
-    auto us = [&](int i, int j) { return (double)(tr[j] - tr[i]) * 0.01; };
-    printf("load %.2f us\n", us(255, 0));
-    double diag = 0, panel = 0, trail = 0;
-    for (int k = 0; k < np; k++) {
-        const int prev = k == 0 ? 0 : 3 + 3 * (k - 1);
-        const double d0 = us(prev, 1 + 3 * k), d1 = us(1 + 3 * k, 2 + 3 * k), d2 = us(2 + 3 * k, 3 + 3 * k);
-        if (k < 3 || k == np - 1) printf("step %2d: diag %.2f  panel %.2f  trailing %.2f\n", k, d0, d1, d2);
-        diag += d0; panel += d1; trail += d2;
+    // cycles (s_memtime) between stamps; per step k: panel(k, k+1) done, (k+1, k+1) updated,
+    // (k+1, k+1) factored, end of step (thread 0 after the barrier)
+    auto cy = [&](int i, int j) { return (long long)(tr[j] - tr[i]); };
+    printf("load+prologue %lld cycles\n", cy(250, 251));
+    long long sp = 0, su = 0, sf = 0, sb = 0;
+    for (int k = 0; k + 1 < np; k++) {
+        const int prev = k == 0 ? 251 : 4 * (k - 1) + 3;
+        const long long p = cy(prev, 4 * k), u = cy(4 * k, 4 * k + 1), f = cy(4 * k + 1, 4 * k + 2),
+                        e = cy(4 * k + 2, 4 * k + 3);
+        if (k < 3 || k == np - 2) printf("step %2d: start->panel %lld  panel->updated %lld  factor %lld  ->end %lld\n", k, p, u, f, e);
+        sp += p; su += u; sf += f; sb += e;
     }
-    unsigned long long clk[2];
-    hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_solve_clk), sizeof(clk));
-    printf("shader clock during the kernel: %.0f MHz\n", (double)(clk[1] - clk[0]) / us(255, 201));
-    printf("sum diag %.2f  panel %.2f  trailing %.2f  write-back %.2f  bwd %.2f  total %.2f\n", diag, panel, trail,
-           us(3 + 3 * (np - 1), 200), us(202, 201), us(255, 201));
+    printf("sums: start->panel %lld  panel->updated %lld  factor %lld  ->end %lld\n", sp, su, sf, sb);
+    printf("factor loop %lld  back substitution %lld  tail %lld  total %lld cycles\n", cy(251, 4 * (np - 1) + 3),
+           cy(4 * (np - 1) + 3, 252), cy(252, 253), cy(250, 253));
     return 0;
 }
