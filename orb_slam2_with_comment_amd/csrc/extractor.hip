@@ -181,6 +181,18 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, l
 // -- two prefix scans.  Keys never move: each key carries the index of its node, remapped
 // after every pass through the parent's (node, quadrant) -> child table.
 constexpr int kOctThreads = 1024;
+constexpr int kOctRegKeys = 16;  // candidates per thread held in registers (16,384 per level)
+#ifdef ORBMI_OCT_TRACE  // tools/octree_trace.hip: s_memtime stamps of (level 0, image 0)
+__device__ unsigned long long g_oct_trace[256];
+#define OCT_STAMP(i, v)                                                                      \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_oct_trace[i] = (v);    \
+    } while (0)
+#define OCT_SUB(it, j) do { if ((it) < 15) OCT_STAMP(100 + 10 * (it) + (j), __builtin_amdgcn_s_memtime()); } while (0)
+#else
+#define OCT_STAMP(i, v) do {} while (0)
+#define OCT_SUB(it, j) do {} while (0)
+#endif
 
 struct OctShared {
     short4 box[2][kOctNodeCap];          // x0, y0, x1, y1 (UL = (x0,y0), BR = (x1,y1))
@@ -256,23 +268,80 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
     uint32_t* K = keys + (long long)b * keys_cap + g.key_base;
     uint16_t* NO = node_of + (long long)b * keys_cap + g.key_base;
 
-    // ---- gather candidates in original order (cells row-major, FAST order inside a cell)
+    OCT_STAMP(0, __builtin_amdgcn_s_memtime());
+    // ---- gather candidates in original order (cells row-major, FAST order inside a cell):
+    // thread t holds keys t R .. t R + R - 1 in registers (R = kOctRegKeys, neighbours in the
+    // image, so a thread's increments mostly hit one counter); keys from kOctThreads R on
+    // spill to K / NO in global memory.  A key finds its cell by a binary search over
+    // the prefix of the cell counts, so every load of the gather is in flight at once.
+    uint32_t kreg[kOctRegKeys];
+    int nreg[kOctRegKeys];
+#pragma unroll
+    for (int r = 0; r < kOctRegKeys; r++) { kreg[r] = 0; nreg[r] = 0; }
     int nkeys = 0;
     for (int base = 0; base < nc; base += kOctNodeCap) {
         const int n = min(kOctNodeCap, nc - base);
-        for (int i = tid; i < n; i += blockDim.x) S.tmp[i] = cnts[base + i];
+        for (int i = tid; i < n; i += blockDim.x) {
+            S.tmp[i] = cnts[base + i];
+            S.newpos[i] = cells[c0 + base + i].slot_base;
+        }
         __syncthreads();
         const int tot = block_scan_array(S.tmp, n, S.scratch);
-        const int wid = tid >> 6, lane = tid & 63;
-        for (int i = wid; i < n; i += kOctThreads / 64) {
-            const int cnt = cnts[base + i];
-            const uint32_t* src = slots + (long long)b * nslots + cells[c0 + base + i].slot_base;
-            for (int j = lane; j < cnt; j += 64) K[nkeys + S.tmp[i] + j] = src[j];
+        auto cell_of = [&](int kk) {  // kk in [0, tot): upper_bound over the prefix, minus one
+            int lo = 0, hi = n;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (S.tmp[mid] <= kk) lo = mid;
+                else hi = mid;
+            }
+            return lo;
+        };
+        auto fetch = [&](int kk) -> uint32_t {
+            const int lo = cell_of(kk);
+            return slots[(long long)b * nslots + S.newpos[lo] + (kk - S.tmp[lo])];
+        };
+        {
+            // one search for the thread's first key, then walk the cells forward; all slot
+            // addresses first, then the loads
+            const int k0 = tid * kOctRegKeys;
+            const int kk0 = max(k0 - nkeys, 0);
+            int lo = kk0 < tot ? cell_of(kk0) : 0;
+            long long addr[kOctRegKeys];
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) {
+                const int kk = k0 + r - nkeys;
+                addr[r] = -1;
+                if (kk >= 0 && kk < tot) {
+                    while (lo + 1 < n && S.tmp[lo + 1] <= kk) lo++;
+                    addr[r] = (long long)b * nslots + S.newpos[lo] + (kk - S.tmp[lo]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++)
+                if (addr[r] >= 0) kreg[r] = slots[addr[r]];
         }
+        for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys + tot; k += kOctThreads)
+            if (k >= nkeys) K[k] = fetch(k - nkeys);
         nkeys += tot;
         __syncthreads();
     }
+    // f(k, key, node&) for every key, in increasing k per thread: the register-resident
+    // ones, then the global spill
+    auto for_keys = [&](auto&& f) {
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++) {
+            const int k = tid * kOctRegKeys + r;
+            if (k < nkeys) f(k, kreg[r], nreg[r]);
+        }
+        for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
+            int no = NO[k];
+            f(k, K[k], no);
+            NO[k] = (uint16_t)no;
+        }
+    };
 
+    OCT_STAMP(1, __builtin_amdgcn_s_memtime());
+    OCT_STAMP(62, nkeys);
     // ---- initial nodes (:543-579)
     const int nIni = g.nIni;
     int cur = 0;
@@ -282,12 +351,20 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         S.cnt[cur][i] = 0;
     }
     __syncthreads();
-    for (int k = tid; k < nkeys; k += blockDim.x) {
-        const uint32_t key = K[k];
-        int n = (int)((float)(key & 0xFFF) / g.hX);
-        n = min(n, nIni - 1);
-        NO[k] = (uint16_t)n;
-        atomicAdd(&S.cnt[cur][n], 1);
+    {
+        int run = -1, rc = 0;  // consecutive keys of a thread share a node: one atomic per run
+        for_keys([&](int, uint32_t key, int& no) {
+            int n = (int)((float)(key & 0xFFF) / g.hX);
+            n = min(n, nIni - 1);
+            no = n;
+            if (n != run) {
+                if (rc) atomicAdd(&S.cnt[cur][run], rc);
+                run = n;
+                rc = 0;
+            }
+            rc++;
+        });
+        if (rc) atomicAdd(&S.cnt[cur][run], rc);
     }
     __syncthreads();
     // drop empty initial nodes (:581-593)
@@ -304,22 +381,70 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
 
     const int N = g.nfeat;
     bool careful = false, finish = false;
+    OCT_STAMP(2, __builtin_amdgcn_s_memtime());
+    int iters = 0;
     for (int iter = 0; iter < 256 && !finish; iter++) {
+        iters++;
         const int prv = cur ^ 1;
         for (int i = tid; i < L; i += blockDim.x) {
             S.ccnt[i][0] = S.ccnt[i][1] = S.ccnt[i][2] = S.ccnt[i][3] = 0;
         }
         __syncthreads();
+        OCT_SUB(iter, 0);
         // keys: apply the previous pass's remap, then histogram children of nodes with >1 key
-        for (int k = tid; k < nkeys; k += blockDim.x) {
-            const uint32_t key = K[k];
-            const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
-            const int o = NO[k];
-            const int n = S.remap[o][quadrant(S.box[prv][o], x, y)];
-            NO[k] = (uint16_t)n;
-            if (S.cnt[cur][n] >= 2) atomicAdd(&S.ccnt[n][quadrant(S.box[cur][n], x, y)], 1);
+        {
+            // register keys: every LDS read of the pass first (independent across keys), then
+            // one atomic per run of equal (node, quadrant) -- atomics would serialise the reads
+            // branch-free (absent keys read node 0 and are masked), so the compiler can
+            // interleave the LDS round trips of all kOctRegKeys keys
+            // staged: all box reads, then all remap reads, then all child reads (absent keys
+            // carry key 0 / node 0 and are masked at the end)
+            int tgt[kOctRegKeys];
+            short4 bx[kOctRegKeys];
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) bx[r] = S.box[prv][nreg[r]];
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++)
+                tgt[r] = S.remap[nreg[r]][quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF)];
+            int cn[kOctRegKeys];
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) {
+                nreg[r] = max(tgt[r], 0);
+                bx[r] = S.box[cur][nreg[r]];
+                cn[r] = S.cnt[cur][nreg[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) {
+                const bool v = tid * kOctRegKeys + r < nkeys;
+                const int t = 4 * nreg[r] + quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF);
+                tgt[r] = (v && cn[r] >= 2) ? t : -1;
+            }
+            OCT_SUB(iter, 6);
+            int run = -1, rc = 0;
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) {
+                if (tgt[r] != run) {
+                    if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
+                    run = tgt[r];
+                    rc = 0;
+                }
+                rc++;
+            }
+            if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
+            OCT_SUB(iter, 7);
+            // spilled keys
+            for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
+                const uint32_t key = K[k];
+                const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
+                const int o = NO[k];
+                const int n = S.remap[o][quadrant(S.box[prv][o], x, y)];
+                NO[k] = (uint16_t)n;
+                if (S.cnt[cur][n] >= 2) atomicAdd(&S.ccnt[n][quadrant(S.box[cur][n], x, y)], 1);
+            }
+            OCT_SUB(iter, 8);
         }
         __syncthreads();
+        OCT_SUB(iter, 1);
         // which nodes divide, and in which push order
         int ncand = 0, kdiv = 0;
         if (!careful) {
@@ -333,20 +458,22 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
             for (int i = tid; i < L; i += blockDim.x) S.newpos[i] = S.tmp[i];
         } else {
             // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733)
-            int np2 = 2;
-            while (np2 < L) np2 <<= 1;
-            for (int i = tid; i < np2; i += blockDim.x) {
-                unsigned long long key = ~0ull;
-                if (i < L && S.cnt[cur][i] >= 2)
-                    key = ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
-                S.skey[i] = key;
+            {
+                int np2 = 2;
+                while (np2 < L) np2 <<= 1;
+                for (int i = tid; i < np2; i += blockDim.x) {
+                    unsigned long long key = ~0ull;
+                    if (i < L && S.cnt[cur][i] >= 2)
+                        key = ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
+                    S.skey[i] = key;
+                }
+                if (tid == 0) S.misc[0] = 0;
+                __syncthreads();
+                for (int i = tid; i < L; i += blockDim.x)
+                    if (S.cnt[cur][i] >= 2) atomicAdd(&S.misc[0], 1);
+                bitonic_sort(S.skey, np2);
+                ncand = S.misc[0];
             }
-            if (tid == 0) S.misc[0] = 0;
-            __syncthreads();
-            for (int i = tid; i < L; i += blockDim.x)
-                if (S.cnt[cur][i] >= 2) atomicAdd(&S.misc[0], 1);
-            bitonic_sort(S.skey, np2);
-            ncand = S.misc[0];
             for (int r = tid; r < ncand; r += blockDim.x) {
                 const int n = (int)(S.skey[r] & 0xFFFFFFFFu);
                 S.tmp[r] = (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0) - 1;
@@ -374,6 +501,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
             for (int r = tid; r < kdiv; r += blockDim.x) S.newpos[(int)(S.skey[r] & 0xFFFFFFFFu)] = S.tmp[r];
         }
         __syncthreads();
+        OCT_SUB(iter, 2);
         // P = total pushes; survivors ranked in list order
         int P = 0;
         {
@@ -385,6 +513,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         for (int i = tid; i < L; i += blockDim.x) S.tmp[i] = !S.dflag[i];
         __syncthreads();
         const int nsurv = block_scan_array(S.tmp, L, S.scratch);
+        OCT_SUB(iter, 3);
         int nexp_local = 0;
         for (int i = tid; i < L; i += blockDim.x) {
             if (S.dflag[i]) {
@@ -411,8 +540,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
                 S.remap[i][0] = S.remap[i][1] = S.remap[i][2] = S.remap[i][3] = (short)ni;
             }
         }
+        OCT_SUB(iter, 4);
         int nToExpand = 0;
         block_excl_scan(nexp_local, S.scratch, &nToExpand);
+        OCT_SUB(iter, 5);
         const int newL = min(P + nsurv, kOctNodeCap);
         // the remap just written refers to the boxes of list `cur`; keys apply it next pass
         cur = prv;
@@ -421,28 +552,54 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         L = newL;
         (void)ncand;
         (void)kdiv;
+        if (iter < 50) OCT_STAMP(3 + iter, __builtin_amdgcn_s_memtime() | ((unsigned long long)careful << 63));
     }
+    OCT_STAMP(61, iters);
+    OCT_STAMP(60, L);
 
-    // ---- keep the max-response key per node, first in original order on ties (:744-760)
+    // ---- keep the max-response key per node, first in original order on ties (:744-760):
+    // one 64-bit max per node over score << 56 | (2^20 - 1 - k) << 24 | (y << 12 | x)
     const int prv = cur ^ 1;
-    for (int i = tid; i < L; i += blockDim.x) S.ccnt[i][0] = 0;
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(&S.ccnt[0][0]);  // 2 per row
+    for (int i = tid; i < L; i += blockDim.x) best[2 * i] = 0;
     __syncthreads();
-    for (int k = tid; k < nkeys; k += blockDim.x) {
-        const uint32_t key = K[k];
-        const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
-        const int o = NO[k];
-        const int n = S.remap[o][quadrant(S.box[prv][o], x, y)];
-        atomicMax((unsigned*)&S.ccnt[n][0], ((key >> 24) << 20) | (0xFFFFFu - (unsigned)k));
+    {
+        int fn[kOctRegKeys];  // final node of each register key, all reads first
+        short4 bx[kOctRegKeys];
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++) bx[r] = S.box[prv][nreg[r]];
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++) {
+            const bool v = tid * kOctRegKeys + r < nkeys;
+            const int n = S.remap[nreg[r]][quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF)];
+            fn[r] = v ? n : -1;
+        }
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++) {
+            const int k = tid * kOctRegKeys + r;
+            const uint32_t key = kreg[r];
+            if (fn[r] >= 0)
+                atomicMax(&best[2 * fn[r]], ((unsigned long long)(key >> 24) << 56) |
+                                                ((unsigned long long)(0xFFFFFu - (unsigned)k) << 24) | (key & 0xFFFFFFu));
+        }
+        for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
+            const uint32_t key = K[k];
+            const int o = NO[k];
+            const int n = S.remap[o][quadrant(S.box[prv][o], key & 0xFFF, (key >> 12) & 0xFFF)];
+            atomicMax(&best[2 * n], ((unsigned long long)(key >> 24) << 56) |
+                                        ((unsigned long long)(0xFFFFFu - (unsigned)k) << 24) | (key & 0xFFFFFFu));
+        }
     }
     __syncthreads();
     const int minB = kEdge - 3;
     uint2* out = oct_out + (long long)b * out_cap + g.out_base;
     for (int i = tid; i < L && i < g.out_cap; i += blockDim.x) {
-        const unsigned v = (unsigned)S.ccnt[i][0];
-        const uint32_t key = K[0xFFFFFu - (v & 0xFFFFFu)];
-        out[i] = make_uint2(((key & 0xFFF) + minB) | ((((key >> 12) & 0xFFF) + minB) << 16), key >> 24);
+        const unsigned long long v = best[2 * i];
+        const uint32_t key = (uint32_t)(v & 0xFFFFFFu);
+        out[i] = make_uint2(((key & 0xFFF) + minB) | ((((key >> 12) & 0xFFF) + minB) << 16), (uint32_t)(v >> 56));
     }
     if (tid == 0) oct_count[b * nlevels + level] = min(L, g.out_cap);
+    OCT_STAMP(59, __builtin_amdgcn_s_memtime());
 }
 
 // ------------------------------------------------------------------------------ describe

@@ -81,16 +81,16 @@ __device__ inline int block_excl_scan(int v, int* scratch, int* total) {
     const int incl = wave_incl_scan(v);
     if (lane == 63) scratch[wid] = incl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int w = 0; w < nw; w++) { int t = scratch[w]; scratch[w] = acc; acc += t; }
-        scratch[nw] = acc;
+    // every thread adds up the wave totals itself (broadcast LDS reads, no serial pass)
+    int before = 0, all = 0;
+    for (int w = 0; w < nw; w++) {
+        const int t = scratch[w];
+        before += w < wid ? t : 0;
+        all += t;
     }
-    __syncthreads();
-    const int r = scratch[wid] + incl - v;
-    *total = scratch[nw];
-    __syncthreads();
-    return r;
+    *total = all;
+    __syncthreads();  // scratch may be rewritten by the next scan
+    return before + incl - v;
 }
 
 __device__ inline int popc256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
