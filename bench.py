@@ -286,7 +286,7 @@ def profile_stages(handle, run_step, n):
     from orb_slam2_with_comment_amd import _capi
     lib = _capi.lib()
     NS = _capi.NUM_STAGES
-    lib.orbmi_set_profiling(handle, 0xFF)
+    lib.orbmi_set_profiling(handle, 0x1FF)
     reset_profile(handle)
     kp = 0
     cand = 0
@@ -319,7 +319,8 @@ def profile_stages(handle, run_step, n):
         "pyr_resize": 2 * sum(W[l - 1] * H[l - 1] + padded[l] for l in range(1, 8)) / 7,
         "fast": 2 * (P + 4 * cand_img),
         "octree": 2 * (4 * cand_img + 8 * kp_img),
-        "describe": 2 * kp_img * (43 * 43 + 60),
+        "describe": 2 * kp_img * (37 * 37 + 31 * 31 + 60),
+        "blur": 2 * (2 * P),
         "stereo_rows": kp_img * 28 * 2,
         "stereo_match": kp_img * (28 + 32 + 8) + kp_img * 1452,
         "stereo_filter": kp_img * 16,
@@ -355,7 +356,7 @@ def pipeline_roofline(stage, rows, cols):
     kp_img = stage["kp_per_step"] / 2
     B = 7 * stage["P"] + 60 * kp_img  # B = 7P + 60N per image
     ext_ms = sum(v for k, v in stage["stage_ms"].items() if k in ("pyr_level0", "pyr_resize", "fast", "octree",
-                                                                   "describe"))
+                                                                   "blur", "describe"))
     out = {"alg_bytes_per_image": round(B), "extract_ms_per_step": round(ext_ms, 5)}
     if ext_ms > 0:
         gbs = 2 * B / (ext_ms / 1e3) / 1e9

@@ -289,6 +289,7 @@ typedef enum orbmi_stage {
     ORBMI_STAGE_STEREO_ROWS = 5,
     ORBMI_STAGE_STEREO_MATCH = 6,
     ORBMI_STAGE_STEREO_FILTER = 7,
+    ORBMI_STAGE_BLUR = 8,          /* GaussianBlur 7x7 of every level (ORBextractor.cc:1085-1086) */
     ORBMI_NUM_STAGES = 16
 } orbmi_stage;
 

@@ -19,7 +19,7 @@ ORBMI_E_CAP = -3
 ORBMI_E_UNSUPPORTED = -4
 ORBMI_E_STATE = -5
 STAGES = ["pyr_level0", "pyr_resize", "fast", "octree", "describe", "stereo_rows", "stereo_match",
-          "stereo_filter"]
+          "stereo_filter", "blur"]
 NUM_STAGES = 16
 _NAMES = {ORBMI_E_ARG: "ORBMI_E_ARG", ORBMI_E_HIP: "ORBMI_E_HIP", ORBMI_E_CAP: "ORBMI_E_CAP",
           ORBMI_E_UNSUPPORTED: "ORBMI_E_UNSUPPORTED", ORBMI_E_STATE: "ORBMI_E_STATE"}

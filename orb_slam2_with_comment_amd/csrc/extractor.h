@@ -23,6 +23,8 @@ struct LevelGeom {
     int blur_xv;         // first column of the GaussianBlur scalar tail (4*floor(W/4))
     int resize_xv;       // first column of the resize vertical scalar tail
     int xtab_off, ytab_off;     // offsets into the resize coefficient tables (level >= 1)
+    long long boff;      // byte offset of the blurred level (interior only) inside one image's blur
+    int bstride;         // blurred row pitch (W rounded up to 128)
 };
 
 // One FAST cell of ComputeKeyPointsOctTree (src/ORBextractor.cc:789-829).
@@ -37,6 +39,7 @@ struct XTab { short sx0, sx1, a0, a1; };  // horizontal resize: source taps and 
 struct YTab { short y0, y1, b0, b1; };    // vertical resize
 
 constexpr int kOctNodeCap = 2048;  // live quadtree nodes per level held in LDS
+constexpr int kBlurTW = 128, kBlurTH = 32;  // GaussianBlur output tile
 
 // Grow-only device buffer.
 template <class T>
@@ -62,7 +65,9 @@ struct Extractor {
     int rows = 0, cols = 0;
     std::vector<LevelGeom> levels;
     std::vector<CellGeom> cells;
+    std::vector<int2> btiles;
     long long pimg = 0;      // bytes of one padded pyramid
+    long long bimg = 0;      // bytes of one blurred pyramid
     int nslots = 0, keys_cap = 0, out_cap = 0;
 
     // device buffers (capacity for `bcap` images)
@@ -73,6 +78,9 @@ struct Extractor {
     XTab* d_xtab = nullptr;
     YTab* d_ytab = nullptr;
     uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;     // blurred levels: interior only, rows of bstride bytes
+    int2* d_btiles = nullptr;      // blur tiles: {level, x0 | y0 << 16}
+    int nbtiles = 0;
     int* d_cell_counts = nullptr;
     uint32_t* d_slots = nullptr;
     uint32_t* d_keys = nullptr;

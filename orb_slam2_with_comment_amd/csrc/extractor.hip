@@ -55,16 +55,24 @@ __global__ void k_pyr_resize(uint8_t* __restrict__ pyr, long long pimg, LevelGeo
 // ------------------------------------------------------------------------------ FAST
 constexpr int kTile = 64;  // max cell ROI edge (wCell+6, hCell+6)
 
-__device__ inline int fast_score16(const uint8_t* t, int x, int y, int th) {
+// LDS writes of this wave visible to its own later reads (wave-private LDS regions)
+__device__ inline void wave_sync_lds_ex() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline int fast_score16_p(const uint8_t* t, int pitch, int x, int y, int th) {
     // OpenCV offsets16: (dx,dy) of the radius-3 Bresenham circle.
     const int o[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
                           {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
-    const int v = t[y * kTile + x];
+    const int v = t[y * pitch + x];
     int p[16];
     unsigned bright = 0, dark = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        p[k] = t[(y + o[k][1]) * kTile + x + o[k][0]];
+        p[k] = t[(y + o[k][1]) * pitch + x + o[k][0]];
         bright |= (unsigned)(p[k] > v + th) << k;
         dark |= (unsigned)(p[k] < v - th) << k;
     }
@@ -118,59 +126,86 @@ __device__ inline bool nms_keep(const uint8_t* sc, int x, int y) {
            s > sc[(y + 1) * kTile + x - 1] && s > sc[(y + 1) * kTile + x] && s > sc[(y + 1) * kTile + x + 1];
 }
 
-// One workgroup per (image, cell).  Candidates are written row-major (FAST_t emission order)
-// as x | y << 12 | score << 24 with x, y relative to minBorder (:820-825).
-__global__ __launch_bounds__(256) void k_fast(const uint8_t* __restrict__ pyr, long long pimg,
-                                              const LevelGeom* __restrict__ levels,
-                                              const CellGeom* __restrict__ cells, int ncells,
-                                              uint32_t* __restrict__ slots, int nslots,
-                                              int* __restrict__ cell_counts, int ini_th, int min_th) {
-    __shared__ uint8_t tile[kTile * kTile];
-    __shared__ uint8_t sc[kTile * kTile];
-    __shared__ int scratch[8];
-    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+// One wave per (image, cell), four cells per workgroup, so every step syncs at wave level only.
+// The cell ROI (<= 64 x 64) is staged in the wave's LDS as aligned dwords (its first byte at a
+// per-cell offset 0..3); scores, strict 3x3 NMS, and a ballot compaction that emits the
+// survivors row-major (FAST_t emission order) as x | y << 12 | score << 24 with x, y relative to
+// minBorder (:820-825).  A cell retries with min_th when ini_th finds nothing (:804-817).
+constexpr int kFastCells = 4;           // waves (cells) per workgroup
+constexpr int kTileS = 68;              // LDS row pitch of a staged ROI row (17 dwords)
+__global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restrict__ pyr, long long pimg,
+                                                          const LevelGeom* __restrict__ levels,
+                                                          const CellGeom* __restrict__ cells, int ncells,
+                                                          uint32_t* __restrict__ slots, int nslots,
+                                                          int* __restrict__ cell_counts, int ini_th, int min_th) {
+    __shared__ unsigned tiles[kFastCells][kTile * kTileS / 4];
+    __shared__ uint8_t scores[kFastCells][kTile * kTile];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * kFastCells + wid, b = blockIdx.y;
+    if (c >= ncells) return;
     const CellGeom cg = cells[c];
     if (cg.w == 0) {
-        if (tid == 0) cell_counts[b * ncells + c] = 0;
+        if (lane == 0) cell_counts[b * ncells + c] = 0;
         return;
     }
     const LevelGeom lg = levels[cg.level];
-    const uint8_t* base = pyr + b * pimg + lg.off + (long long)(kEdge + cg.y0) * lg.stride + kEdge + cg.x0;
-    const int w = cg.w, h = cg.h;
-    for (int i = tid; i < w * h; i += blockDim.x) {
-        const int y = i / w, x = i - y * w;
-        tile[y * kTile + x] = base[(long long)y * lg.stride + x];
+    const long long a = b * pimg + lg.off + (long long)(kEdge + cg.y0) * lg.stride + kEdge + cg.x0;
+    const int o = (int)(a & 3);  // stride is a multiple of 64: the same offset on every row
+    const unsigned* src = reinterpret_cast<const unsigned*>(pyr + (a - o));
+    const int w = cg.w, h = cg.h, nd = (w + o + 3) >> 2, s4 = lg.stride >> 2;
+    unsigned* t4 = tiles[wid];
+    {
+        unsigned v[(kTile * 17 + 63) / 64];
+#pragma unroll
+        for (int k = 0; k < (kTile * 17 + 63) / 64; k++) {
+            const int i = lane + 64 * k, r = i / nd, d = i - r * nd;
+            v[k] = r < h ? src[(long long)r * s4 + d] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < (kTile * 17 + 63) / 64; k++) {
+            const int i = lane + 64 * k, r = i / nd, d = i - r * nd;
+            if (r < h) t4[r * (kTileS / 4) + d] = v[k];
+        }
     }
+    // fast_score16 / nms_keep address a kTile-pitched tile: re-pack the staged rows
+    uint8_t* sc = scores[wid];
+    wave_sync_lds_ex();
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * kTileS + x]
     const int dw = w - 6, dh = h - 6, npix = dw > 0 && dh > 0 ? dw * dh : 0;
-    const int chunk = (npix + blockDim.x - 1) / blockDim.x;
-    const int p0 = min(tid * chunk, npix), p1 = min(p0 + chunk, npix);
-    int total = 0, excl = 0;
+    int total = 0;
     for (int pass = 0; pass < 2; pass++) {
         int th = pass == 0 ? ini_th : min_th;
         th = min(max(th, 0), 255);
-        for (int i = tid; i < kTile * h; i += blockDim.x) sc[i] = 0;
-        __syncthreads();
-        for (int p = p0; p < p1; p++) {
+        for (int i = lane; i < kTile * h; i += 64) sc[i] = 0;
+        wave_sync_lds_ex();
+        for (int p = lane; p < npix; p += 64) {
             const int y = 3 + p / dw, x = 3 + p % dw;
-            sc[y * kTile + x] = (uint8_t)fast_score16(tile, x, y, th);
+            sc[y * kTile + x] = (uint8_t)fast_score16_p(tb, kTileS, x, y, th);
         }
-        __syncthreads();
-        int local = 0;
-        for (int p = p0; p < p1; p++) local += nms_keep(sc, 3 + p % dw, 3 + p / dw);
-        excl = block_excl_scan(local, scratch, &total);
+        wave_sync_lds_ex();
+        total = 0;
+        for (int p0 = 0; p0 < npix; p0 += 64) {
+            const int p = p0 + lane;
+            const bool k = p < npix && nms_keep(sc, 3 + p % dw, 3 + p / dw);
+            total += __popcll(__ballot(k));
+        }
         if (total > 0) break;
     }
     if (total > 0) {
         uint32_t* out = slots + (long long)b * nslots + cg.slot_base;
-        int r = excl;
-        for (int p = p0; p < p1; p++) {
+        int r = 0;
+        for (int p0 = 0; p0 < npix; p0 += 64) {
+            const int p = p0 + lane;
             const int y = 3 + p / dw, x = 3 + p % dw;
-            if (nms_keep(sc, x, y))
-                out[r++] = (uint32_t)(x + cg.sx) | ((uint32_t)(y + cg.sy) << 12) |
-                           ((uint32_t)sc[y * kTile + x] << 24);
+            const bool k = p < npix && nms_keep(sc, x, y);
+            const unsigned long long m = __ballot(k);
+            if (k)
+                out[r + __popcll(m & ((1ull << lane) - 1))] =
+                    (uint32_t)(x + cg.sx) | ((uint32_t)(y + cg.sy) << 12) | ((uint32_t)sc[y * kTile + x] << 24);
+            r += __popcll(m);
         }
     }
-    if (tid == 0) cell_counts[b * ncells + c] = total;
+    if (lane == 0) cell_counts[b * ncells + c] = total;
 }
 
 // ------------------------------------------------------------------------------ octree
@@ -555,6 +590,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         if (iter < 50) OCT_STAMP(3 + iter, __builtin_amdgcn_s_memtime() | ((unsigned long long)careful << 63));
     }
     OCT_STAMP(61, iters);
+    (void)iters;
     OCT_STAMP(60, L);
 
     // ---- keep the max-response key per node, first in original order on ties (:744-760):
@@ -602,10 +638,81 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
     OCT_STAMP(59, __builtin_amdgcn_s_memtime());
 }
 
+// ------------------------------------------------------------------------------ blur
+// GaussianBlur(7x7, sigma 2, REFLECT_101) of every level (src/ORBextractor.cc:1085-1086), pinned
+// as P3: separable integer taps {18,34,49,55,49,34,18}, float column pass for x < blur_xv,
+// integer tail.  The reflect-101 border of the padded pyramid supplies the taps outside the
+// image.  One 128x32 output tile per workgroup: 16-B loads of the padded rows (interior column
+// x0 - 3 sits at a 16-B boundary), row sums in LDS, 4x4 outputs per thread stored as dwords
+// into the interior-only blurred layout.
+constexpr int kBlurInH = kBlurTH + 6, kBlurChunks = (kBlurTW + 6 + 15) / 16;  // 38 rows x 9 x 16 B
+constexpr int kBlurInS = 16 * kBlurChunks;                                     // 144
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                              long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
+                                              const int2* __restrict__ tiles) {
+    __shared__ uint4 in4[kBlurInH * kBlurChunks];
+    __shared__ int rs[kBlurInH][kBlurTW];
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(in4);
+    const int2 t = tiles[blockIdx.x];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom g = levels[t.x];
+    const int x0 = t.y & 0xFFFF, y0 = t.y >> 16;
+    const uint8_t* lvl = pyr + b * pimg + g.off + kEdge - 3 + x0;  // column x0 - 3 of padded row 0
+    for (int i = tid; i < kBlurInH * kBlurChunks; i += 256) {
+        const int r = i / kBlurChunks, ch = i - r * kBlurChunks;
+        const int yy = min(y0 - 3 + r, g.H + 2);  // rows past H + 2 feed only discarded outputs
+        in4[i] = *reinterpret_cast<const uint4*>(lvl + (long long)(kEdge + yy) * g.stride + 16 * ch);
+    }
+    __syncthreads();
+    // row sums: one (row, 16 columns) run per task
+    for (int task = tid; task < kBlurInH * (kBlurTW / 16); task += 256) {
+        const int r = task / (kBlurTW / 16), c0 = 16 * (task - r * (kBlurTW / 16));
+        const uint8_t* q = in + r * kBlurInS + c0;  // q[k] = input column c0 + k - 3
+        int v[22];
+#pragma unroll
+        for (int k = 0; k < 22; k++) v[k] = q[k];
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            rs[r][c0 + c] = 55 * v[c + 3] + 49 * (v[c + 2] + v[c + 4]) + 34 * (v[c + 1] + v[c + 5]) +
+                            18 * (v[c] + v[c + 6]);
+    }
+    __syncthreads();
+    const int cq = 4 * (tid & 31), rb = 4 * (tid >> 5);  // 4 columns x 4 rows per thread
+    uint8_t* dst = blur + b * bimg + g.boff;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+        const int y = y0 + rb + rr;
+        if (y >= g.H) break;
+        unsigned packedv = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+            const int c = cq + cc, x = x0 + c, r = rb + rr;
+            const int c3 = rs[r + 3][c], p1 = rs[r + 2][c] + rs[r + 4][c], p2 = rs[r + 1][c] + rs[r + 5][c],
+                      p3 = rs[r][c] + rs[r + 6][c];
+            int v;
+            if (x < g.blur_xv) {  // SymmColumnVec_32s8u float path
+                float sacc = (float)c3 * (55.f / 65536.f) + 0.0f;
+                sacc = sacc + (float)p1 * (49.f / 65536.f);
+                sacc = sacc + (float)p2 * (34.f / 65536.f);
+                sacc = sacc + (float)p3 * (18.f / 65536.f);
+                v = (int)__builtin_rintf(sacc);
+            } else {
+                v = (c3 * 55 + p1 * 49 + p2 * 34 + p3 * 18 + (1 << 15)) >> 16;
+            }
+            packedv |= (unsigned)(v < 0 ? 0 : (v > 255 ? 255 : v)) << (8 * cc);
+        }
+        if (x0 + cq < g.bstride)
+            *reinterpret_cast<unsigned*>(dst + (long long)y * g.bstride + x0 + cq) = packedv;
+    }
+}
+
 // ------------------------------------------------------------------------------ describe
-constexpr int kWin = 43;       // 37x37 descriptor samples + 3-px blur halo
-constexpr int kWinStride = 44;
-constexpr int kWinR = 21;
+constexpr int kBR = 18;                 // rotated rBRIEF samples lie within 18 px (pattern radius 18.4)
+constexpr int kBW = 2 * kBR + 1;        // blurred window 37 x 37
+constexpr int kBD = (kBW + 3 + 3) / 4;  // dwords per window row (any start alignment): 10
+constexpr int kUR = 15;                 // IC_Angle patch radius (HALF_PATCH_SIZE)
+constexpr int kUW = 2 * kUR + 1;        // unblurred window 31 x 31
+constexpr int kUD = (kUW + 3 + 3) / 4;  // 9
 
 __device__ inline float fast_atan2_deg(float y, float x) {
     // cv::fastAtan2 (OpenCV 3.x mathfuncs): polynomial in degrees
@@ -629,36 +736,19 @@ __device__ inline float fast_atan2_deg(float y, float x) {
     return a;
 }
 
-// GaussianBlur(7x7, sigma 2, REFLECT_101) of the level at window position (wx, wy) (P3).
-__device__ inline int blurred_at(const uint8_t* win, int wx, int wy, bool simd) {
-    const int k[4] = {55, 49, 34, 18};
-    int rs[7];
-#pragma unroll
-    for (int r = 0; r < 7; r++) {
-        const uint8_t* row = win + (wy - 3 + r) * kWinStride + wx;
-        rs[r] = 55 * row[0] + 49 * (row[-1] + row[1]) + 34 * (row[-2] + row[2]) + 18 * (row[-3] + row[3]);
-    }
-    int v;
-    if (simd) {
-        float s = (float)rs[3] * (55.f / 65536.f) + 0.0f;
-        s = s + (float)(rs[2] + rs[4]) * (49.f / 65536.f);
-        s = s + (float)(rs[1] + rs[5]) * (34.f / 65536.f);
-        s = s + (float)(rs[0] + rs[6]) * (18.f / 65536.f);
-        v = (int)__builtin_rintf(s);
-    } else {
-        v = (rs[3] * k[0] + (rs[2] + rs[4]) * k[1] + (rs[1] + rs[5]) * k[2] + (rs[0] + rs[6]) * k[3] + (1 << 15)) >> 16;
-    }
-    return v < 0 ? 0 : (v > 255 ? 255 : v);
-}
-
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, long long pimg,
-                                                  const LevelGeom* __restrict__ levels, int nlevels,
+// One wave per keypoint: the 31x31 unblurred patch (IC_Angle) and the 37x37 blurred window
+// (k_blur output) go to the wave's LDS as aligned dwords covering each window row (the row's
+// first byte sits at a per-window offset 0..3), then 4 ballots give the 256 bits.
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                  long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
+                                                  int nlevels,
                                                   const uint2* __restrict__ oct_out, int oct_cap,
                                                   const int* __restrict__ oct_count,
                                                   orbmi_keypoint* __restrict__ kps,
                                                   uint8_t* __restrict__ desc, int* __restrict__ counts,
                                                   int capacity) {
-    __shared__ uint8_t wins[4][kWin * kWinStride];
+    __shared__ unsigned winb[4][kBW * kBD];
+    __shared__ unsigned winu[4][kUW * kUD];
     const int b = blockIdx.y, wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = blockIdx.x * 4 + wid;
     const int* lc = oct_count + b * nlevels;
@@ -670,7 +760,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     int level = -1;
     for (int l = 0; l < nlevels; l++)
         if (j >= levels[l].out_base && j < levels[l].out_base + levels[l].out_cap) level = l;
-    // every wave owns its own LDS window, so only wave-level ordering is needed below
+    // every wave owns its own LDS windows, so only wave-level ordering is needed below
     if (level < 0) return;
     const LevelGeom g = levels[level];
     const int idx = j - g.out_base;
@@ -679,12 +769,36 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     for (int l = 0; l < level; l++) off += lc[l];
     const uint2 o = oct_out[(long long)b * oct_cap + j];
     const int x = o.x & 0xFFFF, y = o.x >> 16;
-    uint8_t* win = wins[wid];
-    const uint8_t* lvl = pyr + b * pimg + g.off + (long long)(kEdge + y - kWinR) * g.stride + kEdge + x - kWinR;
-    for (int i = lane; i < kWin * kWin; i += 64) {
-        const int r = i / kWin, c = i - r * kWin;
-        win[r * kWinStride + c] = lvl[(long long)r * g.stride + c];
+    unsigned* wb = winb[wid];
+    unsigned* wu = winu[wid];
+    const long long base = b * pimg + g.off + (long long)(kEdge + y) * g.stride + kEdge + x;
+    const long long sb = b * bimg + g.boff + (long long)(y - kBR) * g.bstride + x - kBR;  // byte address
+    const long long su = base - (long long)kUR * g.stride - kUR;
+    const int ob = (int)(sb & 3), ou = (int)(su & 3);  // first window byte inside the first dword
+    {
+        const unsigned* b4 = reinterpret_cast<const unsigned*>(blur + (sb - ob));
+        const unsigned* u4 = reinterpret_cast<const unsigned*>(pyr + (su - ou));
+        const int bs4 = g.bstride >> 2, us4 = g.stride >> 2;
+        unsigned vb[(kBW * kBD + 63) / 64], vu[(kUW * kUD + 63) / 64];
+#pragma unroll
+        for (int k = 0; k < (kBW * kBD + 63) / 64; k++) {  // all loads first, then the LDS stores
+            const int i = lane + 64 * k, r = i / kBD, c = i - r * kBD;
+            vb[k] = i < kBW * kBD ? b4[(long long)r * bs4 + c] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < (kUW * kUD + 63) / 64; k++) {
+            const int i = lane + 64 * k, r = i / kUD, c = i - r * kUD;
+            vu[k] = i < kUW * kUD ? u4[(long long)r * us4 + c] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < (kBW * kBD + 63) / 64; k++)
+            if (lane + 64 * k < kBW * kBD) wb[lane + 64 * k] = vb[k];
+#pragma unroll
+        for (int k = 0; k < (kUW * kUD + 63) / 64; k++)
+            if (lane + 64 * k < kUW * kUD) wu[lane + 64 * k] = vu[k];
     }
+    const uint8_t* wbb = reinterpret_cast<const uint8_t*>(wb) + ob;  // wbb[r * 4 kBD + c] = window (r, c)
+    const uint8_t* wub = reinterpret_cast<const uint8_t*>(wu) + ou;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): window stores landed in LDS
     __builtin_amdgcn_wave_barrier();
@@ -693,7 +807,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     int m01 = 0, m10 = 0;
     for (int i = lane; i < c_ncircle; i += 64) {
         const int u = c_circle[i][0], v = c_circle[i][1];
-        const int val = win[(kWinR + v) * kWinStride + kWinR + u];
+        const int val = wub[(kUR + v) * 4 * kUD + kUR + u];
         m10 += u * val;
         m01 += v * val;
     }
@@ -711,8 +825,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
         const float px1 = c_pattern[t][2], py1 = c_pattern[t][3];
         const int c0 = cv_round_f(px0 * ca - py0 * sa), r0 = cv_round_f(px0 * sa + py0 * ca);
         const int c1 = cv_round_f(px1 * ca - py1 * sa), r1 = cv_round_f(px1 * sa + py1 * ca);
-        const int v0 = blurred_at(win, kWinR + c0, kWinR + r0, x + c0 < g.blur_xv);
-        const int v1 = blurred_at(win, kWinR + c1, kWinR + r1, x + c1 < g.blur_xv);
+        const int v0 = wbb[(kBR + r0) * 4 * kBD + kBR + c0];
+        const int v1 = wbb[(kBR + r1) * 4 * kBD + kBR + c1];
         masks[kk] = __ballot(v0 < v1);
     }
     if (off + idx < capacity) {
@@ -803,7 +917,7 @@ int Extractor::set_geometry(int r, int c) {
     cells.clear();
     std::vector<XTab> xt;
     std::vector<YTab> yt;
-    long long off = 0;
+    long long off = 0, boff = 0;
     int slot = 0, key = 0, outb = 0;
     for (int l = 0; l < nlevels; l++) {
         LevelGeom& g = levels[l];
@@ -815,6 +929,9 @@ int Extractor::set_geometry(int r, int c) {
         g.ph = g.H + 2 * kEdge;
         g.off = off;
         off += (long long)g.stride * g.ph;
+        g.bstride = (g.W + 127) & ~127;
+        g.boff = boff;
+        boff += (long long)g.bstride * g.H;
         g.scale = scale[l];
         g.size = (float)(int)(kPatch * scale[l]);
         g.blur_xv = (g.W / 4) * 4;
@@ -902,6 +1019,12 @@ int Extractor::set_geometry(int r, int c) {
         }
     }
     pimg = off;
+    bimg = boff;
+    btiles.clear();
+    for (int l = 0; l < nlevels; l++)
+        for (int y0 = 0; y0 < levels[l].H; y0 += kBlurTH)
+            for (int x0 = 0; x0 < levels[l].W; x0 += kBlurTW) btiles.push_back(make_int2(l, x0 | (y0 << 16)));
+    nbtiles = (int)btiles.size();
     nslots = slot;
     keys_cap = key;
     out_cap = outb;
@@ -909,6 +1032,8 @@ int Extractor::set_geometry(int r, int c) {
     int rc;
     if ((rc = dev_alloc(&d_levels, levels.size()))) return rc;
     if ((rc = dev_alloc(&d_cells, cells.size()))) return rc;
+    if ((rc = dev_alloc(&d_btiles, btiles.size()))) return rc;
+    ORBMI_HIP(hipMemcpy(d_btiles, btiles.data(), btiles.size() * sizeof(int2), hipMemcpyHostToDevice));
     if ((rc = dev_alloc(&d_xtab, xt.size()))) return rc;
     if ((rc = dev_alloc(&d_ytab, yt.size()))) return rc;
     ORBMI_HIP(hipMemcpy(d_levels, levels.data(), levels.size() * sizeof(LevelGeom), hipMemcpyHostToDevice));
@@ -923,6 +1048,7 @@ int Extractor::reserve(int batch, int capacity) {
     int rc;
     if (batch > bcap) {
         if ((rc = dev_alloc(&d_pyr, (size_t)batch * pimg))) return rc;
+        if ((rc = dev_alloc(&d_blur, (size_t)batch * bimg))) return rc;
         if ((rc = dev_alloc(&d_cell_counts, (size_t)batch * cells.size()))) return rc;
         if ((rc = dev_alloc(&d_slots, (size_t)batch * nslots))) return rc;
         if ((rc = dev_alloc(&d_keys, (size_t)batch * keys_cap))) return rc;
@@ -960,7 +1086,8 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         }
     }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
-    hipLaunchKernelGGL(k_fast, dim3(ncells, batch), dim3(256), 0, stream, d_pyr, pimg, d_levels, d_cells,
+    hipLaunchKernelGGL(k_fast, dim3((ncells + kFastCells - 1) / kFastCells, batch), dim3(64 * kFastCells), 0, stream,
+                       d_pyr, pimg, d_levels, d_cells,
                        ncells, d_slots, nslots, d_cell_counts, ini_th, min_th);
     prof_end(ORBMI_STAGE_FAST, ev);
     ev = prof_begin(ORBMI_STAGE_OCTREE);
@@ -968,9 +1095,13 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                        d_cell_counts, d_cells, d_slots, nslots, d_keys, d_node_of, keys_cap, d_oct, out_cap,
                        d_oct_count);
     prof_end(ORBMI_STAGE_OCTREE, ev);
+    ev = prof_begin(ORBMI_STAGE_BLUR);
+    hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg, d_levels,
+                       d_btiles);
+    prof_end(ORBMI_STAGE_BLUR, ev);
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
-    hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, pimg, d_levels,
-                       nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity);
+    hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
+                       d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity);
     prof_end(ORBMI_STAGE_DESCRIBE, ev);
     ORBMI_HIP(hipGetLastError());
     last_batch = batch;
@@ -1006,7 +1137,7 @@ void Extractor::release() {
     prof_pending.clear();
     prof_pool.clear();
     if (device >= 0) (void)hipSetDevice(device);
-    void* ptrs[] = {d_levels, d_cells, d_xtab, d_ytab, d_pyr, d_cell_counts, d_slots, d_keys, d_node_of,
+    void* ptrs[] = {d_levels, d_cells, d_btiles, d_blur, d_xtab, d_ytab, d_pyr, d_cell_counts, d_slots, d_keys, d_node_of,
                     d_oct, d_oct_count, d_kps, d_desc, d_counts, d_image, d_scale_tab, d_row_start,
                     d_row_list, d_sad, d_stereo_u, d_stereo_d};
     for (void* p : ptrs)
