@@ -277,6 +277,44 @@ void orbmi_ba_destroy(orbmi_ba* h);
 int orbmi_local_bundle_adjustment(orbmi_ba* h, const orbmi_ba_problem* problem, orbmi_ba_result* result,
                                   const volatile int* stop);
 
+/* ---- Optimizer::PoseOptimization ---------------------------------------------------- */
+
+/* One unary edge: a keypoint i of the Frame with a MapPoint (mvpMapPoints[i] != NULL),
+ * src/Optimizer.cc:296-375.  `index` is the caller's keypoint index (mvbOutlier slot). */
+typedef struct orbmi_pose_obs {
+    float Xw[3];                   /* MapPoint::GetWorldPos()                             */
+    float u, v;                    /* mvKeysUn[i].pt                                      */
+    float ur;                      /* mvuRight[i]; < 0 -> EdgeSE3ProjectXYZOnlyPose (mono)  */
+    float inv_sigma2;              /* mvInvLevelSigma2[mvKeysUn[i].octave]                 */
+    int32_t index;                 /* keypoint index i (returned untouched)               */
+} orbmi_pose_obs;
+
+/* One frame: its observations are obs[obs_begin, obs_begin + n_obs). */
+typedef struct orbmi_pose_frame {
+    float tcw[16];                 /* in: Frame::mTcw (row-major); out: optimised pose;
+                                      unchanged when fewer than 3 observations (:378-379)  */
+    float fx, fy, cx, cy, bf;      /* Frame::fx, fy, cx, cy, mbf                           */
+    int32_t obs_begin, n_obs;
+    int32_t inliers;               /* out: nInitialCorrespondences - nBad, the return value;
+                                      -1 when n_obs exceeds the kernel's 4096 (device path) */
+    int32_t iterations;            /* out: LM iterations run over the 4 rounds (diagnostic) */
+} orbmi_pose_frame;
+
+typedef struct orbmi_pose orbmi_pose;
+int orbmi_pose_create(int device, orbmi_pose** out);
+void orbmi_pose_destroy(orbmi_pose* h);
+
+/* Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:58, src/Optimizer.cc:257-481) on
+ * `nframes` independent frames in one launch (one workgroup per frame): 4 rounds of
+ * optimize(10) (g2o Levenberg, BlockSolver_6_3 + LinearSolverDense, Huber sqrt(5.991) /
+ * sqrt(7.815) for the first 3 rounds) from the frame's initial pose, outliers re-classified
+ * after each round (chi2 > 5.991 / 7.815, level 1).  outlier[k] receives mvbOutlier for obs k.
+ * fp64 on the GPU.  `frames`, `obs` and `outlier` may be host or device pointers; device
+ * pointers leave the work enqueued on the handle's stream (orbmi_pose_synchronize). */
+int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes, const orbmi_pose_obs* obs,
+                            int nobs, uint8_t* outlier);
+int orbmi_pose_synchronize(orbmi_pose* h);
+
 /* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
 
 /* Kernel stages of one handle; each is a single kernel launch (resize: one per level). */

@@ -238,6 +238,19 @@ def local_ba(problem, stop=False):
             "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
 
 
+def pose_optimization(frames, obs):
+    """Optimizer::PoseOptimization restatement over POSE_FRAME_DTYPE frames (updated in place:
+    tcw, inliers, iterations) and POSE_OBS_DTYPE observations -> outlier flags (bool, per obs)."""
+    L = lib()
+    L.orc_pose_optimization.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.orc_pose_optimization.restype = C.c_int
+    assert frames.flags.c_contiguous and obs.flags.c_contiguous
+    out = np.zeros(len(obs), np.uint8)
+    for f in range(len(frames)):
+        L.orc_pose_optimization(frames[f:f + 1].ctypes.data, obs.ctypes.data, out.ctypes.data)
+    return out.astype(bool)
+
+
 # ---- cross-stream matching (config 4; build-defined, no reference counterpart) -----------
 _POPC8 = np.array([bin(i).count("1") for i in range(256)], np.int32)
 

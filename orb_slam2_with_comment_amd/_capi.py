@@ -70,6 +70,10 @@ _PROTOS = {
     "orbmi_ba_create": (_i, [_i, C.POINTER(_vp)]),
     "orbmi_ba_destroy": (None, [_vp]),
     "orbmi_local_bundle_adjustment": (_i, [_vp, _vp, _vp, _vp]),
+    "orbmi_pose_create": (_i, [_i, C.POINTER(_vp)]),
+    "orbmi_pose_destroy": (None, [_vp]),
+    "orbmi_pose_optimization": (_i, [_vp, _vp, _i, _vp, _i, _vp]),
+    "orbmi_pose_synchronize": (_i, [_vp]),
     "orbmi_set_profiling": (_i, [_vp, C.c_uint]),
     "orbmi_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),

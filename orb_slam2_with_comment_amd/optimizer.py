@@ -42,6 +42,46 @@ class LocalBA:
                 "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
 
 
+class PoseOptimizer:
+    """Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:58) on the GPU, batched: one
+    workgroup per frame.  `run(frames, obs)` updates the POSE_FRAME_DTYPE records in place
+    (tcw, inliers = the reference's return value, iterations) and returns mvbOutlier per obs."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check("orbmi_pose_create", lib().orbmi_pose_create(device, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbmi_pose_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, frames: np.ndarray, obs: np.ndarray) -> np.ndarray:
+        from .types import POSE_FRAME_DTYPE, POSE_OBS_DTYPE
+        assert frames.dtype == POSE_FRAME_DTYPE and obs.dtype == POSE_OBS_DTYPE
+        assert frames.flags.c_contiguous and obs.flags.c_contiguous
+        out = np.zeros(len(obs), np.uint8)
+        check("orbmi_pose_optimization",
+              lib().orbmi_pose_optimization(self._h, frames.ctypes.data, len(frames), obs.ctypes.data, len(obs),
+                                            out.ctypes.data))
+        return out.astype(bool)
+
+    def run_device(self, frames_ptr: int, nframes: int, obs_ptr: int, nobs: int, outlier_ptr: int):
+        """Device-resident frames / observations / flags: enqueued on the handle's stream."""
+        check("orbmi_pose_optimization",
+              lib().orbmi_pose_optimization(self._h, frames_ptr, nframes, obs_ptr, nobs, outlier_ptr))
+
+    def synchronize(self):
+        check("orbmi_pose_synchronize", lib().orbmi_pose_synchronize(self._h))
+
+
 # ---- minimal map model for the graph assembly (src/Optimizer.cc:486-534) ------------------
 @dataclasses.dataclass(eq=False)
 class KeyFrame:

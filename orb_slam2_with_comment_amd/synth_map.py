@@ -156,3 +156,62 @@ def local_ba_problem(seed=42, n_free=20, n_fixed=4, n_points=3000, stereo_frac=0
                                ("inv_sigma2", "<f8")]).astype(BA_EDGE_DTYPE)
     gt = {"Twc": np.stack(Twc), "points": P[kept_pts]}
     return BAProblem(kfs, pts, e), gt
+
+
+def pose_problem(seed=0, n_obs=600, stereo_frac=0.7, outlier_frac=0.1, cam=None, pose_noise=(0.01, 0.08),
+                 nframes=1, point_noise=0.0005):
+    """Synthetic Frames for Optimizer::PoseOptimization (src/Optimizer.cc:257-481), the
+    TrackWithMotionModel / TrackLocalMap situation: `n_obs` matched map points per frame at
+    3-40 m, keypoint noise sigma = 1 px x scale (octave from distance, PredictScale rule), a
+    `stereo_frac` share with a right coordinate, `outlier_frac` gross outliers (10-30 px), map
+    points off by `point_noise` x depth, and an initial pose off by +-pose_noise (rad, m).
+    Returns (frames POSE_FRAME_DTYPE[nframes], obs POSE_OBS_DTYPE[nframes * n_obs], gt Tcw list)."""
+    from . import synth
+    from .types import POSE_FRAME_DTYPE, POSE_OBS_DTYPE
+    cam = cam or synth.KITTI
+    rng = np.random.default_rng(seed)
+    frames = np.zeros(nframes, POSE_FRAME_DTYPE)
+    obs = np.zeros(nframes * n_obs, POSE_OBS_DTYPE)
+    gts = []
+    for f in range(nframes):
+        yaw = rng.uniform(-0.3, 0.3)
+        Twc = np.eye(4)
+        Twc[:3, :3] = [[np.cos(yaw), 0, np.sin(yaw)], [0, 1, 0], [-np.sin(yaw), 0, np.cos(yaw)]]
+        Twc[:3, 3] = rng.uniform(-5, 5, 3)
+        Tcw = tcw_from_twc(Twc).astype(np.float64)
+        u = rng.uniform(20, cam.width - 20, n_obs)
+        v = rng.uniform(20, cam.height - 20, n_obs)
+        z = np.exp(rng.uniform(np.log(3.0), np.log(40.0), n_obs))
+        Xc = np.stack([(u - cam.cx) * z / cam.fx, (v - cam.cy) * z / cam.fy, z], -1)
+        Xw = Xc @ Twc[:3, :3].T + Twc[:3, 3]
+        Xw += rng.normal(0, 1, Xw.shape) * (point_noise * z)[:, None]
+        octave = np.clip(np.floor(np.log(np.maximum(z / 8.0, 1.0)) / np.log(1.2)), 0, 7).astype(int)
+        sigma = 1.2 ** octave
+        uu = u + rng.normal(0, 1, n_obs) * sigma
+        vv = v + rng.normal(0, 1, n_obs) * sigma
+        ur = np.where(rng.random(n_obs) < stereo_frac, u - cam.bf / z + rng.normal(0, 1, n_obs) * sigma, -1.0)
+        bad = rng.random(n_obs) < outlier_frac
+        du = rng.uniform(10, 30, n_obs) * rng.choice([-1, 1], n_obs)
+        dv = rng.uniform(10, 30, n_obs) * rng.choice([-1, 1], n_obs)
+        uu = np.where(bad, uu + du, uu)
+        vv = np.where(bad, vv + dv, vv)
+        ur = np.where(bad & (ur >= 0), ur + du, ur)
+        sl = slice(f * n_obs, (f + 1) * n_obs)
+        obs["Xw"][sl] = Xw.astype(np.float32)
+        obs["u"][sl], obs["v"][sl], obs["ur"][sl] = uu, vv, ur
+        obs["inv_sigma2"][sl] = (1.0 / (sigma * sigma)).astype(np.float32)
+        obs["index"][sl] = rng.permutation(4 * n_obs)[:n_obs]
+        # initial estimate: the motion model's guess, a few cm / mrad off
+        a = rng.uniform(-pose_noise[0], pose_noise[0], 3)
+        th = np.linalg.norm(a)
+        K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]]) / max(th, 1e-12)
+        dR = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        T0 = Tcw.copy()
+        T0[:3, :3] = dR @ Tcw[:3, :3]
+        T0[:3, 3] += rng.uniform(-pose_noise[1], pose_noise[1], 3)
+        frames[f]["tcw"] = T0.astype(np.float32).reshape(-1)
+        frames[f]["fx"], frames[f]["fy"], frames[f]["cx"], frames[f]["cy"], frames[f]["bf"] = (
+            cam.fx, cam.fy, cam.cx, cam.cy, cam.bf)
+        frames[f]["obs_begin"], frames[f]["n_obs"] = f * n_obs, n_obs
+        gts.append(Tcw)
+    return frames, obs, gts

@@ -109,6 +109,15 @@ BA_EDGE_DTYPE = np.dtype([("point", "<i4"), ("kf", "<i4"), ("u", "<f4"), ("v", "
 assert BA_KF_DTYPE.itemsize == 92 and BA_PT_DTYPE.itemsize == 20 and BA_EDGE_DTYPE.itemsize == 24
 
 
+# orbmi_pose_obs / orbmi_pose_frame (Optimizer::PoseOptimization)
+POSE_OBS_DTYPE = np.dtype([("Xw", "<f4", 3), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("inv_sigma2", "<f4"),
+                           ("index", "<i4")])
+POSE_FRAME_DTYPE = np.dtype([("tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                             ("bf", "<f4"), ("obs_begin", "<i4"), ("n_obs", "<i4"), ("inliers", "<i4"),
+                             ("iterations", "<i4")])
+assert POSE_OBS_DTYPE.itemsize == 32 and POSE_FRAME_DTYPE.itemsize == 100
+
+
 class BAProblemView(C.Structure):
     _fields_ = [("nkf", C.c_int), ("npt", C.c_int), ("nedge", C.c_int), ("kfs", C.c_void_p), ("pts", C.c_void_p),
                 ("edges", C.c_void_p)]
