@@ -4,9 +4,11 @@
 Default workload (`--mode track`, SURVEY.md §8(d) config 2 + amortised config 3): one step =
 one KITTI-shaped 1241x376 stereo frame through the GPU hot path, in Tracking's order:
 ORBextractor(left) + ORBextractor(right) (2000 features, 1.2, 8 levels, FAST 20/7; one batched
-launch sequence) + Frame::ComputeStereoMatches + SearchByProjection(CF, LF, th=7) against the
-previous frame's stereo points + SearchLocalPoints (isInFrustum + SearchByProjection, th=1)
-against ~3000 local map points; every 4th frame is a keyframe whose LocalBundleAdjustment
+launch sequence) + Frame::ComputeStereoMatches + TrackWithMotionModel (SearchByProjection(CF, LF,
+th=7) against the previous frame's stereo points, device-side retry test, PoseOptimization,
+outlier discard) + TrackLocalMap (SearchLocalPoints (isInFrustum + SearchByProjection, th=1)
+against ~2000 local map points at the optimised pose, PoseOptimization, inlier count); every 4th
+frame is a keyframe whose LocalBundleAdjustment
 (config 3: 20 free + 4 fixed KFs, 3000 points, ~15k edges) runs concurrently on the
 LocalMapping thread, as in the reference.  All LocalBAs started inside the timed region finish
 inside it.  Inputs (images, last-frame points, local map) are resident in HBM before timing.
@@ -195,7 +197,7 @@ def run_track(a, rank, world, local, dist):
         S["imgs"].data_ptr() + (2 + i % F) * 2 * img_bytes, rows, cols), tr.synchronize()), max(F, 16))
     # phase profile (untimed): HIP events on the tracking stream around each phase
     n_tr = max(F, 32)
-    phases = {"extract_stereo": 0.0, "search_last_frame": 0.0, "search_local_points": 0.0}
+    phases = {"extract_stereo": 0.0, "track_motion_model": 0.0, "track_local_map": 0.0}
     tr.synchronize()
     t0 = time.perf_counter()
     for i in range(n_tr):
@@ -204,14 +206,16 @@ def run_track(a, rank, world, local, dist):
         ev[0].record(ext)
         tr.extract_stereo(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols)
         ev[1].record(ext)
-        tr.search_last_frame(S["tcws"][f], S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr())
+        tr.track_with_motion_model(S["tcws"][f], S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr())
         ev[2].record(ext)
-        tr.search_local_points(S["tcws"][f], S["mps"][f].data_ptr(), S["n_mp"][f])
+        tr.track_local_map(S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(),
+                           S["n_mp"][f])
         ev[3].record(ext)
         tr.synchronize()
         for k, name in enumerate(phases):
             phases[name] += ev[k].elapsed_time(ev[k + 1]) / n_tr
     track_only_ms = (time.perf_counter() - t0) / n_tr * 1e3  # includes a host sync per frame
+    outcome = tr.results()
     nm_lf = int((tr.match_lf[:int(tr.counts[0])] >= 0).sum())
     nm_mp = int((tr.match_mp[:int(tr.counts[0])] >= 0).sum())
     kp_per_frame = float(stage["kp_per_step"])
@@ -251,17 +255,19 @@ def run_track(a, rank, world, local, dist):
                     "config-3 LocalBA graph, resident in HBM",
             "config": {
                 "workload": "Track+LocalMap per stereo frame: ORBextractor(L,R) [2000 feat, 1.2, 8 lv, FAST 20/7] "
-                            "+ ComputeStereoMatches + SearchByProjection(CF,LF,th=7) + SearchLocalPoints(th=1, "
-                            f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs) + LocalBundleAdjustment(config 3) "
+                            "+ ComputeStereoMatches + TrackWithMotionModel [SearchByProjection(CF,LF,th=7), "
+                            "PoseOptimization] + TrackLocalMap [SearchLocalPoints(th=1, "
+                            f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
+                            "+ LocalBundleAdjustment(config 3) "
                             f"every {KF_EVERY}th frame on the concurrent LocalMapping thread"
                             + ("; + RCCL all-gather of left desc/kps and cross-stream matching (config 4)"
                                if world > 1 else ""),
                 "frames_resident": F, "parallelism": f"one stereo stream per GPU x{world}",
-                "not_on_gpu_path": "PoseOptimization (SURVEY.md §8(f) rank 1) — excluded on both sides",
             },
             "kpts_desc_per_s": round(value * kp_per_frame, 1),
             "keypoints_per_frame": round(kp_per_frame, 1),
-            "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp},
+            "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp, "inliers": outcome["inliers"],
+                                  "tracking_ok": outcome["ok"]},
             "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},
             "track_only_ms_per_frame_synced": round(track_only_ms, 4),
             "local_ba": {"ms_per_call_idle_gpu": round(lba_ms, 3), "calls_in_timed_region": n_lba,
@@ -379,13 +385,14 @@ def host_info():
 
 def cpu_baseline_track(S, problem, a):
     """The oracle (C++ restatement of the reference path) on host cores with the reference's
-    threading: L/R extraction on two threads (src/Frame.cc:78-81), stereo + both searches
-    serial, LocalBundleAdjustment on a third thread (LocalMapping) every 4th frame."""
+    threading: L/R extraction on two threads (src/Frame.cc:78-81), stereo + TrackWithMotionModel +
+    TrackLocalMap serial, LocalBundleAdjustment on a third thread (LocalMapping) every 4th frame."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle_ctypes as O
     from orb_slam2_with_comment_amd.types import Frame, LFPOINT_DTYPE, MAPPOINT_DTYPE
     cam = S["cam"]
     p = O.params(a.nfeatures)
+    inv_sigma2 = O.tables(p)["inv_sigma2"]
     pool = ThreadPoolExecutor(2)
     lm = ThreadPoolExecutor(1)
     F = a.frames
@@ -407,10 +414,7 @@ def cpu_baseline_track(S, problem, a):
         (kl, dl), (kr, dr) = fl.result(), fr.result()
         u, d = O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
         cf = Frame(kl, dl, u, S["tcws"][f], cam)
-        occ = np.zeros(len(kl), np.uint8)
-        O.search_by_projection_last_frame(cf, occ, lf_frames[f - 1], lf_points[f - 1], 7.0)
-        trk = O.is_in_frustum(cf, mps[f], 0.5)
-        O.search_by_projection_local(cf, occ, mps[f], trk, 1.0, 0.8)
+        O.track_frame(cf, lf_frames[f - 1], lf_points[f - 1], mps[f], inv_sigma2, 7.0)
         if n % KF_EVERY == 0:
             futs.append(lm.submit(O.local_ba, problem))
         n += 1
@@ -424,7 +428,7 @@ def cpu_baseline_track(S, problem, a):
     lm.shutdown()
     return {"value": round(n / el, 4), "unit": "frames/s", "cores": 3, "kind": "port",
             "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle extract L||R "
-                      f"(2 threads) + stereo + SearchByProjection(LF) + SearchLocalPoints serial, "
+                      f"(2 threads) + stereo + TrackWithMotionModel + TrackLocalMap (both PoseOptimizations) serial, "
                       f"{len(futs)} LocalBA on a 3rd thread; {el:.1f} s"}
 
 

@@ -103,7 +103,9 @@ int orbmi_compute_stereo_matches_batch_device(orbmi_extractor* h, float bf, floa
 /* Read-only view of the Frame members the matchers use (include/Frame.h).  Pointers may be
  * host or device memory of the matcher's device (detected per call).  keys_un = mvKeysUn,
  * u_right = mvuRight (NULL for monocular), desc = mDescriptors (n x 32), tcw = mTcw (4x4
- * row-major float, needed by SearchByProjection(CF,LF) only). */
+ * row-major float, needed by the projection searches and isInFrustum).  A device tcw is read by
+ * the kernels when they run (stream order), so it may be the output of an enqueued
+ * orbmi_pose_optimization_frame (orbmi_pose_frame.tcw). */
 typedef struct orbmi_frame_view {
     int n;
     const orbmi_keypoint* keys_un;
@@ -314,6 +316,59 @@ void orbmi_pose_destroy(orbmi_pose* h);
 int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes, const orbmi_pose_obs* obs,
                             int nobs, uint8_t* outlier);
 int orbmi_pose_synchronize(orbmi_pose* h);
+/* Run the handle on `ex`'s stream (like orbmi_matcher_share_stream): a tracked frame's
+ * extraction, searches and pose optimisations are then ordered without host round trips. */
+int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex);
+
+/* Frame::mvpMapPoints of the frame being tracked, as the matchers left it: keypoint i holds
+ * local map point mps[match_mp[i]] when match_mp && match_mp[i] >= 0, otherwise last-frame
+ * point lf_points[match_lf[i]] when match_lf && match_lf[i] >= 0, otherwise NULL.  The match
+ * arrays are the outputs of orbmi_search_local_points / orbmi_search_by_projection_last_frame
+ * (CF.n entries; -1 and -2 both mean NULL). */
+typedef struct orbmi_frame_mappoints {
+    int32_t* match_lf;
+    const orbmi_lastframe_point* lf_points;
+    int n_lf_points;               /* entries of lf_points (last frame's N)                */
+    int32_t* match_mp;
+    const orbmi_mappoint* mps;
+    int n_mps;                     /* entries of mps                                       */
+} orbmi_frame_mappoints;
+
+/* Optimizer::PoseOptimization(Frame* pFrame) (include/Optimizer.h:58, src/Optimizer.cc:257-481)
+ * with its edge assembly (:296-375): one unary edge per keypoint holding a map point, in
+ * keypoint order, stereo when mvuRight[i] >= 0, information mvInvLevelSigma2[octave].  The
+ * initial pose is F->tcw (host or device).  rec receives the optimised tcw, fx..bf, n_obs =
+ * nInitialCorrespondences, inliers (the return value) and iterations; outlier[i] = mvbOutlier[i]
+ * (F->n entries; 0 for keypoints without a map point).  inv_level_sigma2: host, F->nlevels
+ * floats.  Every array may be host or device memory; with rec and outlier in device memory the
+ * call is asynchronous on the handle's stream (F->n_device is then honoured). */
+int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
+                                  const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier);
+
+/* ---- Tracking (TrackWithMotionModel / TrackLocalMap bookkeeping) -------------------- */
+
+/* The wider-window retry of Tracking::TrackWithMotionModel (src/Tracking.cc:1018-1023) with
+ * the count kept on the device: when *nmatches_dev < min_matches, SearchByProjection(CF, LF,
+ * th) runs as orbmi_search_by_projection_last_frame (match_lf rewritten, *nmatches_dev = its
+ * count); otherwise nothing changes.  nmatches_dev must be device memory; asynchronous. */
+int orbmi_search_by_projection_last_frame_if(orbmi_matcher* m, const orbmi_frame_view* CF,
+                                             const uint8_t* occupied, const orbmi_frame_view* LF,
+                                             const orbmi_lastframe_point* lf_points, float th, int mono,
+                                             int check_ori, int32_t* match_lf, int* nmatches_dev,
+                                             int min_matches);
+
+/* Tracking's pass over mvpMapPoints after a PoseOptimization, on the device:
+ * stage 0 = TrackWithMotionModel "Discard outliers" (src/Tracking.cc:1036-1058): outlier map
+ *   points become NULL (their match entry -1); counts[0] = outliers removed (the reference's
+ *   nmatches -= counts[0]), counts[1] = nmatchesMap (inliers whose point has Observations() > 0);
+ *   occupied_out[i] = 1 when keypoint i keeps a point with observations (the `occupied` input of
+ *   the local-map search).
+ * stage 1 = TrackLocalMap statistics (src/Tracking.cc:1085-1104): counts[0] = mnMatchesInliers
+ *   (non-outliers with Observations() > 0), counts[1] = outliers; with stereo (F->u_right set)
+ *   outliers become NULL.  occupied_out may be NULL.
+ * counts: 2 ints, host or device (device -> asynchronous). */
+int orbmi_track_update_matches(orbmi_matcher* m, const orbmi_frame_view* F, int stage, const uint8_t* outlier,
+                               const orbmi_frame_mappoints* mp, uint8_t* occupied_out, int* counts);
 
 /* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
 

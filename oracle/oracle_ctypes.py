@@ -251,6 +251,77 @@ def pose_optimization(frames, obs):
     return out.astype(bool)
 
 
+def pose_optimization_frame(frame, inv_level_sigma2, match_lf=None, lf_points=None, match_mp=None, mps=None):
+    """Optimizer::PoseOptimization(Frame*) with edge assembly (oracle/track_oracle.cpp) ->
+    (POSE_FRAME_DTYPE record, per-keypoint outlier flags)."""
+    from orb_slam2_with_comment_amd.types import POSE_FRAME_DTYPE
+    L = lib()
+    L.orc_pose_optimization_frame.argtypes = [C.c_void_p] * 5
+    mp, keep = _mappoints(match_lf, lf_points, match_mp, mps)
+    rec = np.zeros(1, POSE_FRAME_DTYPE)
+    out = np.zeros(max(len(frame.keys), 1), np.uint8)
+    sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+    v = frame.view()
+    L.orc_pose_optimization_frame(C.addressof(v), sig.ctypes.data, C.addressof(mp), rec.ctypes.data, out.ctypes.data)
+    return rec[0], out[:len(frame.keys)]
+
+
+def _mappoints(match_lf, lf_points, match_mp, mps):
+    from orb_slam2_with_comment_amd.types import FrameMapPoints
+    mp = FrameMapPoints()
+    keep = []
+    if match_lf is not None:
+        assert match_lf.dtype == np.int32 and match_lf.flags.c_contiguous
+        lf_points = np.ascontiguousarray(lf_points)
+        keep += [lf_points]
+        mp.match_lf, mp.lf_points, mp.n_lf_points = match_lf.ctypes.data, lf_points.ctypes.data, len(lf_points)
+    if match_mp is not None:
+        assert match_mp.dtype == np.int32 and match_mp.flags.c_contiguous
+        mps = np.ascontiguousarray(mps)
+        keep += [mps]
+        mp.match_mp, mp.mps, mp.n_mps = match_mp.ctypes.data, mps.ctypes.data, len(mps)
+    mp._keep = keep
+    return mp, keep
+
+
+def track_update_matches(frame, stage, outlier, match_lf=None, lf_points=None, match_mp=None, mps=None):
+    """Tracking's mvpMapPoints pass after PoseOptimization (stage 0 / 1): updates the match
+    arrays in place -> (occupied, counts[2])."""
+    L = lib()
+    L.orc_track_update_matches.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    mp, keep = _mappoints(match_lf, lf_points, match_mp, mps)
+    occ = np.zeros(max(len(frame.keys), 1), np.uint8)
+    cnt = np.zeros(2, np.int32)
+    o = np.ascontiguousarray(outlier, np.uint8)
+    v = frame.view()
+    L.orc_track_update_matches(C.addressof(v), stage, o.ctypes.data, C.addressof(mp), occ.ctypes.data, cnt.ctypes.data)
+    return occ[:len(frame.keys)], cnt
+
+
+def track_frame(cf, lf, lf_points, mps, inv_level_sigma2, th=7.0):
+    """Tracking::TrackWithMotionModel + TrackLocalMap (oracle/track_oracle.cpp) for the stereo
+    frame cf (cf.tcw = motion-model pose) -> dict(ok, match_lf, match_mp, outlier, tcw_mm, tcw,
+    stats = [search matches, nmatchesMap, mnMatchesInliers, nToMatch])."""
+    L = lib()
+    L.orc_track_frame.argtypes = [C.c_void_p] * 4 + [C.c_int, C.c_void_p, C.c_float] + [C.c_void_p] * 6
+    n = len(cf.keys)
+    lfp = np.ascontiguousarray(lf_points)
+    mps = np.ascontiguousarray(mps)
+    m_lf = np.zeros(max(n, 1), np.int32)
+    m_mp = np.zeros(max(n, 1), np.int32)
+    out = np.zeros(max(n, 1), np.uint8)
+    t_mm = np.zeros(16, np.float32)
+    t = np.zeros(16, np.float32)
+    st = np.zeros(4, np.int32)
+    sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+    vc, vl = cf.view(), lf.view()
+    ok = L.orc_track_frame(C.addressof(vc), C.addressof(vl), lfp.ctypes.data, mps.ctypes.data, len(mps),
+                           sig.ctypes.data, th, m_lf.ctypes.data, m_mp.ctypes.data, out.ctypes.data, t_mm.ctypes.data,
+                           t.ctypes.data, st.ctypes.data)
+    return {"ok": bool(ok), "match_lf": m_lf[:n], "match_mp": m_mp[:n], "outlier": out[:n].astype(bool),
+            "tcw_mm": t_mm.reshape(4, 4), "tcw": t.reshape(4, 4), "stats": st}
+
+
 # ---- cross-stream matching (config 4; build-defined, no reference counterpart) -----------
 _POPC8 = np.array([bin(i).count("1") for i in range(256)], np.int32)
 

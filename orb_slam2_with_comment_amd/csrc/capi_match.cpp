@@ -129,7 +129,8 @@ int make_frame(Matcher& m, const orbmi_frame_view* v, DevFrame* F, bool need_pos
     if (rc) return rc;
     if (need_pose) {
         if (!v->tcw) return ORBMI_E_ARG;
-        if ((rc = read_small(v->tcw, 16, F->tcw))) return rc;
+        if (on_device(v->tcw)) F->tcw_dev = v->tcw;  // read by the kernels in stream order
+        else memcpy(F->tcw, v->tcw, sizeof(F->tcw));
     }
     if ((rc = read_small(v->scale_factors, v->nlevels, F->scale))) return rc;
     F->fx = v->fx; F->fy = v->fy; F->cx = v->cx; F->cy = v->cy; F->bf = v->bf; F->mb = v->mb;
@@ -293,6 +294,66 @@ int orbmi_search_by_projection_last_frame(orbmi_matcher* h, const orbmi_frame_vi
         return rc;
     ORBMI_HIP(hipGetLastError());
     return finish(m, outs, m.d_scalars, nmatches);
+}
+
+int orbmi_search_by_projection_last_frame_if(orbmi_matcher* h, const orbmi_frame_view* cf, const uint8_t* occupied,
+                                             const orbmi_frame_view* lf, const orbmi_lastframe_point* lf_points,
+                                             float th, int mono, int check_ori, int32_t* match_lf, int* nmatches_dev,
+                                             int min_matches) {
+    if (!h || !occupied || !match_lf || !lf || (lf->n > 0 && !lf_points) || !on_device(nmatches_dev)) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame CF, LF;
+    int rc;
+    if ((rc = make_frame(m, cf, &CF, true))) return rc;
+    if ((rc = make_frame(m, lf, &LF, true))) return rc;
+    const uint8_t* d_occ = dev_in(m, occupied, (size_t)std::max(CF.n, 1), &rc);
+    const orbmi_lastframe_point* d_lfp = dev_in(m, lf_points, (size_t)LF.n, &rc);
+    if (rc) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match_lf, (size_t)CF.n, outs);
+    if ((rc = orbmi::launch_lastframe_search(m, CF, d_occ, LF, d_lfp, th, mono, check_ori, d_out, nmatches_dev,
+                                             nmatches_dev, min_matches)))
+        return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, nullptr, nullptr);
+}
+
+int orbmi_track_update_matches(orbmi_matcher* h, const orbmi_frame_view* f, int stage, const uint8_t* outlier,
+                               const orbmi_frame_mappoints* mp, uint8_t* occupied_out, int* counts) {
+    if (!h || !f || !outlier || !mp || !counts || (stage != 0 && stage != 1)) return ORBMI_E_ARG;
+    if ((mp->match_lf && (!mp->lf_points || mp->n_lf_points < 0)) || (mp->match_mp && (!mp->mps || mp->n_mps < 0)))
+        return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, f, &F, false))) return rc;
+    // the match arrays are updated in place: host arrays go through the arena and back
+    std::vector<OutBuf> outs;
+    const size_t n = (size_t)std::max(F.n, 1);
+    int* d_lf = nullptr;
+    int* d_mp = nullptr;
+    if (mp->match_lf) {
+        d_lf = const_cast<int*>(dev_in(m, (const int*)mp->match_lf, n, &rc));
+        if (!on_device(mp->match_lf)) outs.push_back(OutBuf{mp->match_lf, d_lf, n * sizeof(int)});
+    }
+    if (mp->match_mp) {
+        d_mp = const_cast<int*>(dev_in(m, (const int*)mp->match_mp, n, &rc));
+        if (!on_device(mp->match_mp)) outs.push_back(OutBuf{mp->match_mp, d_mp, n * sizeof(int)});
+    }
+    const uint8_t* d_outl = dev_in(m, outlier, n, &rc);
+    const orbmi_lastframe_point* d_lfp = mp->match_lf ? dev_in(m, mp->lf_points, (size_t)mp->n_lf_points, &rc) : nullptr;
+    const orbmi_mappoint* d_mps = mp->match_mp ? dev_in(m, mp->mps, (size_t)mp->n_mps, &rc) : nullptr;
+    if (rc) return rc;
+    uint8_t* d_occ = occupied_out ? dev_out(m, occupied_out, n, outs) : nullptr;
+    int* d_cnt = dev_out(m, counts, 2, outs);
+    if ((rc = orbmi::launch_track_update(m, F, stage, d_outl, d_lf, d_lfp, mp->n_lf_points, d_mp, d_mps,
+                                                mp->n_mps, d_occ, d_cnt))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, nullptr, nullptr);
 }
 
 int orbmi_search_by_bow(orbmi_matcher* h, const orbmi_frame_view* kf, const uint8_t* kf_mp_ok,

@@ -13,7 +13,8 @@ struct DevFrame {
     const orbmi_keypoint* keys;
     const float* u_right;
     const uint8_t* desc;
-    float tcw[16];
+    float tcw[16];         // host pose (by value) ...
+    const float* tcw_dev;  // ... or a device pose read when the kernel runs
     float fx, fy, cx, cy, bf, mb;
     float min_x, max_x, min_y, max_y, grid_w_inv, grid_h_inv;
     int nlevels;
@@ -22,6 +23,20 @@ struct DevFrame {
 };
 
 __device__ inline int frame_n(const DevFrame& F) { return F.n_dev ? min(*F.n_dev, F.n) : F.n; }
+
+// Rows 0-2 of Tcw (12 floats, constant indices: registers).
+struct Pose34 { float m[12]; };
+__device__ inline Pose34 frame_pose(const DevFrame& F) {
+    Pose34 T;
+    if (F.tcw_dev) {
+#pragma unroll
+        for (int k = 0; k < 12; k++) T.m[k] = F.tcw_dev[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; k++) T.m[k] = F.tcw[k];
+    }
+    return T;
+}
 
 struct DevFV {
     int nnodes;
@@ -62,7 +77,10 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
                         const orbmi_mappoint_track* tr, int n, float th, float nnratio, int* out, int* nmatches);
 int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0, const DevFrame& LF,
                             const orbmi_lastframe_point* lfp, float th, int mono, int check_ori, int* out,
-                            int* nmatches);
+                            int* nmatches, const int* gate = nullptr, int gate_min = 0);
+int launch_track_update(Matcher& m, const DevFrame& F, int stage, const uint8_t* outlier, int* match_lf,
+                        const orbmi_lastframe_point* lfp, int n_lf, int* match_mp, const orbmi_mappoint* mps,
+                        int n_mp, uint8_t* occ_out, int* counts);
 int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
                const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,

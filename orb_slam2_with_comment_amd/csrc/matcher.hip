@@ -36,7 +36,9 @@ __device__ inline int popc_desc(const uint8_t* a, const uint8_t* b) {
 
 // -------------------------------------------------------------------------- grid
 __global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict__ cell_start,
-                                                     int* __restrict__ cell_list, int* __restrict__ kp_cell) {
+                                                     int* __restrict__ cell_list, int* __restrict__ kp_cell,
+                                                     const int* gate, int gate_min) {
+    if (gate && *gate >= gate_min) return;
     __shared__ int cnt[kGridCells + 1];
     __shared__ int scratch[20];
     const int tid = threadIdx.x;
@@ -119,8 +121,9 @@ __global__ __launch_bounds__(256) void k_frustum(DevFrame F, const orbmi_mappoin
     const orbmi_mappoint mp = mps[i];
     bool ok = !(mp.flags & (ORBMI_MP_BAD | ORBMI_MP_SEEN));
     float Pc[3], Ow[3], u = 0, v = 0, invz = 0, dist = 0, viewCos = 0;
+    const Pose34 T = frame_pose(F);
     if (ok) {
-        transform(F.tcw, mp.pos, Pc);
+        transform(T.m, mp.pos, Pc);
         ok = !(Pc[2] < 0.0f);
     }
     if (ok) {
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void k_frustum(DevFrame F, const orbmi_mappoin
         ok = !(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y);
     }
     if (ok) {
-        camera_center(F.tcw, Ow);
+        camera_center(T.m, Ow);
         const float maxDistance = 1.2f * mp.max_distance, minDistance = 0.8f * mp.min_distance;
         const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
         dist = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
@@ -193,11 +196,11 @@ struct LfQuery {
     int minL, maxL;
 };
 
-__device__ inline bool lf_query(const DevFrame& CF, const DevFrame& LF, const orbmi_lastframe_point& p, int i,
+__device__ inline bool lf_query(const DevFrame& CF, const float* Tc, const DevFrame& LF, const orbmi_lastframe_point& p, int i,
                                 float th, bool bForward, bool bBackward, LfQuery* q) {
     if (!(p.flags & ORBMI_LF_HAS_MP) || (p.flags & ORBMI_LF_OUTLIER)) return false;
     float x3Dc[3];
-    transform(CF.tcw, p.pos, x3Dc);
+    transform(Tc, p.pos, x3Dc);
     const float xc = x3Dc[0], yc = x3Dc[1];
     const float invzc = (float)(1.0 / (double)x3Dc[2]);
     if (invzc < 0) return false;
@@ -217,10 +220,10 @@ __device__ inline bool lf_query(const DevFrame& CF, const DevFrame& LF, const or
 }
 
 template <class Fn>
-__device__ inline void lf_candidates(const DevFrame& CF, const DevFrame& LF, const int* cs, const int* cl,
+__device__ inline void lf_candidates(const DevFrame& CF, const float* Tc, const DevFrame& LF, const int* cs, const int* cl,
                                      const orbmi_lastframe_point& p, int i, float th, bool fw, bool bw, Fn emit) {
     LfQuery q;
-    if (!lf_query(CF, LF, p, i, th, fw, bw, &q)) return;
+    if (!lf_query(CF, Tc, LF, p, i, th, fw, bw, &q)) return;
     for_features_in_area(CF, cs, cl, q.u, q.v, q.radius, q.minL, q.maxL, [&](int i2, int cell) {
         if (CF.u_right && CF.u_right[i2] > 0) {
             const float er = fabsf(q.ur - CF.u_right[i2]);
@@ -230,10 +233,12 @@ __device__ inline void lf_candidates(const DevFrame& CF, const DevFrame& LF, con
     });
 }
 
-__device__ inline void motion_direction(const DevFrame& CF, const DevFrame& LF, int mono, bool* fw, bool* bw) {
+__device__ inline void motion_direction(const DevFrame& CF, const float* Tc, const DevFrame& LF, int mono, bool* fw,
+                                        bool* bw) {
     float twc[3], tlc[3];
-    camera_center(CF.tcw, twc);
-    transform(LF.tcw, twc, tlc);
+    const Pose34 Tl = frame_pose(LF);
+    camera_center(Tc, twc);
+    transform(Tl.m, twc, tlc);
     *fw = tlc[2] > CF.mb && !mono;
     *bw = -tlc[2] > CF.mb && !mono;
 }
@@ -260,6 +265,8 @@ struct CandArgs {
     unsigned long long* cand;
     int* ncand;
     unsigned long long* top;
+    const int* gate;  // optional: the launch does nothing when *gate >= gate_min
+    int gate_min;
 };
 
 struct Window {
@@ -268,7 +275,7 @@ struct Window {
     const uint8_t* desc;
 };
 
-__device__ inline bool make_window(const CandArgs& a, int q, Window* w) {
+__device__ inline bool make_window(const CandArgs& a, int q, const float* Tc, bool fw, bool bw, Window* w) {
     if (a.mode == 0) {
         const orbmi_mappoint& mp = a.mps[q];
         const orbmi_mappoint_track t = a.tr[q];
@@ -280,11 +287,9 @@ __device__ inline bool make_window(const CandArgs& a, int q, Window* w) {
         w->desc = mp.desc;
         return true;
     }
-    bool fw, bw;
-    motion_direction(a.F, a.LF, a.mono, &fw, &bw);
     const orbmi_lastframe_point& p = a.lfp[q];
     LfQuery lq;
-    if (!lf_query(a.F, a.LF, p, q, a.th, fw, bw, &lq)) return false;
+    if (!lf_query(a.F, Tc, a.LF, p, q, a.th, fw, bw, &lq)) return false;
     w->x = lq.u; w->y = lq.v; w->r = lq.radius; w->ur = lq.ur; w->minL = lq.minL; w->maxL = lq.maxL;
     w->desc = p.desc;
     return true;
@@ -297,9 +302,16 @@ __global__ __launch_bounds__(256) void k_candidates(CandArgs a) {
     __shared__ int cnt[NG];
     const int gl = threadIdx.x / G, lane = threadIdx.x % G;
     const int q = blockIdx.x * NG + gl;
+    if (a.gate && *a.gate >= a.gate_min) return;  // orbmi_search_by_projection_last_frame_if
     const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;
+    Pose34 Tc;
+    bool fw = false, bw = false;
+    if (a.mode == 1) {
+        Tc = frame_pose(a.F);
+        motion_direction(a.F, Tc.m, a.LF, a.mono, &fw, &bw);
+    }
     Window w;
-    const bool valid = q < nq && make_window(a, q, &w);
+    const bool valid = q < nq && make_window(a, q, Tc.m, fw, bw, &w);
     if (lane == 0) cnt[gl] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -378,6 +390,8 @@ struct GreedyArgs {
     int* res;             // per query: chosen keypoint or -1
     int* out;             // per keypoint result (see orbmi.h)
     int* nmatches;
+    const int* gate;      // optional: nothing happens when *gate >= gate_min (may alias nmatches:
+    int gate_min;         // read by every thread before the single write at the end)
 };
 
 constexpr int kGreedyMaxKp = 16384;
@@ -385,7 +399,7 @@ constexpr int kGreedyRounds = 48;
 
 // Result of query q under occupancy test occ(idx) (sequential semantics of one iteration).
 template <class Occ>
-__device__ inline int greedy_eval(const GreedyArgs& a, int q, bool fw, bool bw, Occ occ) {
+__device__ inline int greedy_eval(const GreedyArgs& a, int q, const float* Tc, bool fw, bool bw, Occ occ) {
     unsigned long long b1 = ~0ull, b2 = ~0ull;
     auto take = [&](unsigned long long e) {
         if (occ((int)(e & 0xFFFFF))) return;
@@ -405,7 +419,7 @@ __device__ inline int greedy_eval(const GreedyArgs& a, int q, bool fw, bool bw, 
         } else if (a.mode == 0) {  // overflowed list: enumerate again
             local_candidates(a.F, a.cs, a.cl, a.mps[q], a.tr[q], a.th, take);
         } else {
-            lf_candidates(a.F, a.LF, a.cs, a.cl, a.lfp[q], q, a.th, fw, bw, take);
+            lf_candidates(a.F, Tc, a.LF, a.cs, a.cl, a.lfp[q], q, a.th, fw, bw, take);
         }
     }
     if (b1 == ~0ull) return -1;
@@ -461,10 +475,15 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     __shared__ int slowres[kGreedyQPer * kGreedyThreads];
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int flag[4];
+    if (a.gate && *a.gate >= a.gate_min) return;  // uniform: every thread reads before any write
     const int tid = threadIdx.x, n = frame_n(a.F);
     const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;  // (the by-value argument stays unmodified)
     bool fw = false, bw = false;
-    if (a.mode == 1) motion_direction(a.F, a.LF, a.mono, &fw, &bw);
+    Pose34 Tc;
+    if (a.mode == 1) {
+        Tc = frame_pose(a.F);
+        motion_direction(a.F, Tc.m, a.LF, a.mono, &fw, &bw);
+    }
     for (int i = tid; i < n; i += blockDim.x) { occ0[i] = a.occ0[i]; oct[i] = (uint8_t)a.F.keys[i].octave; }
     const bool regs = nq <= kGreedyThreads * kGreedyQPer;
     int res[kGreedyQPer], nc[kGreedyQPer];
@@ -533,7 +552,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                 if (slow >> k & 1) {
                     const int q = tid + k * kGreedyThreads;
                     slowres[k * kGreedyThreads + tid] =
-                        greedy_eval(a, q, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                        greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
                 }
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++) {
@@ -542,7 +561,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             }
         } else {
             for (int q = tid; q < nq; q += blockDim.x) {
-                const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
                 if (r != a.res[q]) { a.res[q] = r; changed = 1; }
             }
         }
@@ -564,7 +583,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         if (tid == 0) {
             for (int i = 0; i < n; i++) claim[i] = occ0[i];
             for (int q = 0; q < nq; q++) {
-                const int r = greedy_eval(a, q, fw, bw, [&](int idx) { return claim[idx] != 0; });
+                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return claim[idx] != 0; });
                 a.res[q] = r;
                 if (r >= 0 && query_has_obs(a, q)) claim[r] = 1;
             }
@@ -608,6 +627,51 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     }
     for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
     if (tid == 0) *a.nmatches = flag[1];
+}
+
+// -------------------------------------------------------------------------- Tracking
+// Tracking's pass over mvpMapPoints after a PoseOptimization (orbmi_track_update_matches):
+// stage 0 = TrackWithMotionModel "Discard outliers" (src/Tracking.cc:1036-1058), stage 1 =
+// TrackLocalMap statistics (src/Tracking.cc:1085-1104).  Keypoint i's point is the local map
+// point when match_mp[i] >= 0, else the last-frame point when match_lf[i] >= 0.
+__global__ __launch_bounds__(1024) void k_track_update(DevFrame F, int stage, const uint8_t* __restrict__ outlier,
+                                                       int* __restrict__ match_lf,
+                                                       const orbmi_lastframe_point* __restrict__ lfp, int n_lf,
+                                                       int* __restrict__ match_mp,
+                                                       const orbmi_mappoint* __restrict__ mps, int n_mp,
+                                                       uint8_t* __restrict__ occ_out, int* __restrict__ counts) {
+    __shared__ int cnt[2];
+    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = frame_n(F);
+    int c0 = 0, c1 = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int* slot = nullptr;
+        bool obs = false;
+        if (match_mp && match_mp[i] >= 0 && match_mp[i] < n_mp) {  // (out-of-range indices read as NULL)
+            slot = &match_mp[i];
+            obs = (mps[*slot].flags & ORBMI_MP_HAS_OBS) != 0;
+        } else if (match_lf && match_lf[i] >= 0 && match_lf[i] < n_lf) {
+            slot = &match_lf[i];
+            obs = (lfp[*slot].flags & ORBMI_MP_HAS_OBS) != 0;
+        }
+        bool occ = false;
+        if (slot) {
+            const bool out = outlier[i] != 0;
+            if (stage == 0) {          // :1042-1055
+                if (out) { *slot = -1; c0++; }
+                else if (obs) { c1++; occ = true; }
+            } else {                   // :1087-1101
+                if (!out) c0 += obs;
+                else { c1++; if (F.u_right) *slot = -1; }
+            }
+        }
+        if (occ_out) occ_out[i] = occ;
+    }
+    if (c0) atomicAdd(&cnt[0], c0);
+    if (c1) atomicAdd(&cnt[1], c1);
+    __syncthreads();
+    if (threadIdx.x < 2) counts[threadIdx.x] = cnt[threadIdx.x];
 }
 
 // -------------------------------------------------------------------------- SearchByBoW
@@ -802,13 +866,14 @@ int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, 
 }
 
 // -------------------------------------------------------------------------- host launchers
-static int grid_for(Matcher& m, const DevFrame& F) {
+static int grid_for(Matcher& m, const DevFrame& F, const int* gate = nullptr, int gate_min = 0) {
     if (F.n > kGreedyMaxKp) return ORBMI_E_UNSUPPORTED;
     int rc;
     if ((rc = ensure_buf(&m.d_cell_start, &m.cap_cell_start, (size_t)kGridCells + 1))) return rc;
     if ((rc = ensure_buf(&m.d_cell_list, &m.cap_cell_list, (size_t)std::max(F.n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_kp_cell, &m.cap_kp_cell, (size_t)std::max(F.n, 1)))) return rc;
-    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.stream, F, m.d_cell_start, m.d_cell_list, m.d_kp_cell);
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.stream, F, m.d_cell_start, m.d_cell_list, m.d_kp_cell,
+                       gate, gate_min);
     return ORBMI_OK;
 }
 
@@ -844,9 +909,9 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
 
 int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0, const DevFrame& LF,
                             const orbmi_lastframe_point* lfp, float th, int mono, int check_ori, int* out,
-                            int* nmatches) {
+                            int* nmatches, const int* gate, int gate_min) {
     int rc;
-    if ((rc = grid_for(m, CF))) return rc;
+    if ((rc = grid_for(m, CF, gate, gate_min))) return rc;
     const int n = LF.n, cap = Matcher::kCandCap;
     if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
     if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
@@ -856,14 +921,23 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
         CandArgs ca{};
         ca.mode = 1; ca.nq = n; ca.F = CF; ca.LF = LF; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.lfp = lfp;
         ca.th = th; ca.mono = mono; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
+        ca.gate = gate; ca.gate_min = gate_min;
         hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.stream, ca);
     }
     GreedyArgs a{};
     a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = CF;
     a.LF = LF;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
-    a.res = m.d_res; a.out = out; a.nmatches = nmatches;
+    a.res = m.d_res; a.out = out; a.nmatches = nmatches; a.gate = gate; a.gate_min = gate_min;
     hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
+    return ORBMI_OK;
+}
+
+int launch_track_update(Matcher& m, const DevFrame& F, int stage, const uint8_t* outlier, int* match_lf,
+                        const orbmi_lastframe_point* lfp, int n_lf, int* match_mp, const orbmi_mappoint* mps,
+                        int n_mp, uint8_t* occ_out, int* counts) {
+    hipLaunchKernelGGL(k_track_update, dim3(1), dim3(1024), 0, m.stream, F, stage, outlier, match_lf, lfp, n_lf,
+                       match_mp, mps, n_mp, occ_out, counts);
     return ORBMI_OK;
 }
 

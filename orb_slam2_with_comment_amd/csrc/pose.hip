@@ -11,7 +11,9 @@
 // The edge errors of the last computeActiveErrors stay in LDS: the outlier classification after
 // each optimize(10) reads them as g2o does (stale after a rejected trial).  Parity: 1e-4 on the
 // pose, identical outlier flags and inlier count (tests/test_pose_gpu.py).
+#include <algorithm>
 #include <cfloat>
+#include <cstring>
 #include <cmath>
 #include <new>
 
@@ -140,7 +142,7 @@ __device__ inline bool pose_solve6(const double H[21], const double b[6], double
 
 __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __restrict__ frames,
                                                            const orbmi_pose_obs* __restrict__ obs,
-                                                           uint8_t* __restrict__ outlier_out) {
+                                                           uint8_t* __restrict__ outlier_out, int by_index) {
     __shared__ double err[kPoseMaxObs][3];
     __shared__ uint8_t outl[kPoseMaxObs];  // mvbOutlier; the edge's level is the same flag
     __shared__ double red[kPoseThreads / 64][28];
@@ -149,14 +151,18 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     orbmi_pose_frame& F = frames[blockIdx.x];
     const int n = F.n_obs;
     const orbmi_pose_obs* O = obs + F.obs_begin;
-    uint8_t* out_flags = outlier_out + F.obs_begin;
+    // mvbOutlier per observation (orbmi_pose_optimization) or per keypoint (by_index: obs.index)
+    auto put_flag = [&](int k, uint8_t v) {
+        if (by_index) outlier_out[O[k].index] = v;
+        else outlier_out[F.obs_begin + k] = v;
+    };
     if (n > kPoseMaxObs) {  // sized for kPoseMaxObs edges per frame (the host path checks first)
         if (tid == 0) { F.inliers = -1; F.iterations = 0; }
         return;
     }
     for (int k = tid; k < n; k += kPoseThreads) outl[k] = 0;
     if (n < 3) {  // src/Optimizer.cc:378-379: no optimisation, pose untouched
-        for (int k = tid; k < n; k += kPoseThreads) out_flags[k] = 0;
+        for (int k = tid; k < n; k += kPoseThreads) put_flag(k, 0);
         if (tid == 0) { F.inliers = 0; F.iterations = 0; }
         return;
     }
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         nBad = pose_reduce_int(bad, redi);
         if (n < 10) break;  // optimizer.edges().size() < 10
     }
-    for (int k = tid; k < n; k += kPoseThreads) out_flags[k] = outl[k];
+    for (int k = tid; k < n; k += kPoseThreads) put_flag(k, outl[k]);
     if (tid == 0) {  // Converter::toCvMat(SE3quat_recov)
         double R[3][3];
         q_to_matrix(load_q(T), R);
@@ -329,15 +335,103 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     }
 }
 
+// Edge assembly of PoseOptimization (src/Optimizer.cc:296-375): one edge per keypoint holding a
+// map point, compacted in keypoint order (workgroup scan), plus the frame record.  The map
+// point of keypoint i is mps[match_mp[i]] if match_mp[i] >= 0, else lfp[match_lf[i]] if
+// match_lf[i] >= 0 (orbmi_frame_mappoints); out-of-range indices read as NULL.
+struct PoseGatherArgs {
+    int n;                  // keypoint capacity
+    const int* n_dev;       // device count (optional)
+    const orbmi_keypoint* keys;
+    const float* u_right;   // NULL = monocular
+    const float* tcw_dev;   // initial pose on the device, else tcw
+    float tcw[16];
+    float fx, fy, cx, cy, bf;
+    float inv_sigma2[kMaxLevels];
+    int nlevels;
+    const int* match_lf;
+    const orbmi_lastframe_point* lfp;
+    int n_lf;
+    const int* match_mp;
+    const orbmi_mappoint* mps;
+    int n_mp;
+    orbmi_pose_frame* rec;
+    orbmi_pose_obs* obs;
+    uint8_t* outlier;       // per keypoint, zeroed here
+};
+
+constexpr int kGatherThreads = 1024;
+
+__global__ __launch_bounds__(kGatherThreads) void k_pose_gather(PoseGatherArgs a) {
+    __shared__ int wsum[kGatherThreads / 64];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n = a.n_dev ? min(*a.n_dev, a.n) : a.n;
+    if (tid == 0) base = 0;
+    for (int c0 = 0; c0 < n; c0 += kGatherThreads) {
+        const int i = c0 + tid;
+        const float* X = nullptr;
+        if (i < n) {
+            const int jm = a.match_mp ? a.match_mp[i] : -1;
+            const int jl = a.match_lf ? a.match_lf[i] : -1;
+            if (jm >= 0 && jm < a.n_mp) X = a.mps[jm].pos;
+            else if (jl >= 0 && jl < a.n_lf) X = a.lfp[jl].pos;
+            a.outlier[i] = 0;
+        }
+        const unsigned long long m = __ballot(X != nullptr);
+        const int before = __popcll(m & ((1ull << lane) - 1));
+        if (lane == 0) wsum[wid] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wid; w++) off += wsum[w];
+        if (X) {
+            const orbmi_keypoint kp = a.keys[i];
+            orbmi_pose_obs o;
+            o.Xw[0] = X[0]; o.Xw[1] = X[1]; o.Xw[2] = X[2];
+            o.u = kp.x;
+            o.v = kp.y;
+            o.ur = a.u_right ? a.u_right[i] : -1.0f;
+            const int oct = min(max(kp.octave, 0), a.nlevels - 1);
+            o.inv_sigma2 = a.inv_sigma2[oct];
+            o.index = i;
+            a.obs[off + before] = o;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int w = 0; w < kGatherThreads / 64; w++) t += wsum[w];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (tid < 16) a.rec->tcw[tid] = a.tcw_dev ? a.tcw_dev[tid] : a.tcw[tid];
+    if (tid == 0) {
+        orbmi_pose_frame& R = *a.rec;
+        R.fx = a.fx; R.fy = a.fy; R.cx = a.cx; R.cy = a.cy; R.bf = a.bf;
+        R.obs_begin = 0;
+        R.n_obs = base;
+        R.inliers = 0;
+        R.iterations = 0;
+    }
+}
+
 }  // namespace orbmi
 
 // ---------------------------------------------------------------- host
 struct orbmi_pose {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;
     uint8_t* d_buf = nullptr;  // staging of host frames / obs / flags
     size_t cap = 0;
+    // orbmi_pose_optimization_frame: edge buffer + staging of host inputs (reset per call)
+    orbmi_pose_obs* d_obs = nullptr;
+    size_t cap_obs = 0;
+    uint8_t* d_stage = nullptr;
+    size_t cap_stage = 0, used_stage = 0;
 };
+
+hipStream_t orbmi_extractor_stream_(orbmi_extractor* ex);  // capi_extract.cpp
 
 namespace {
 
@@ -376,8 +470,22 @@ void orbmi_pose_destroy(orbmi_pose* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->d_buf) (void)hipFree(h->d_buf);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->d_obs) (void)hipFree(h->d_obs);
+    if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
+}
+
+int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex) {
+    if (!h || !ex) return ORBMI_E_ARG;
+    hipStream_t s = orbmi_extractor_stream_(ex);
+    if (!s) return ORBMI_E_STATE;
+    ORBMI_HIP(hipSetDevice(h->device));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) ORBMI_HIP(hipStreamDestroy(h->stream));
+    h->stream = s;
+    h->own_stream = false;
+    return ORBMI_OK;
 }
 
 int orbmi_pose_synchronize(orbmi_pose* h) {
@@ -396,7 +504,7 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     if (dev != is_device_ptr(obs) && nobs) return ORBMI_E_ARG;
     if (nobs && dev != is_device_ptr(outlier)) return ORBMI_E_ARG;
     if (dev) {
-        hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier);
+        hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0);
         ORBMI_HIP(hipGetLastError());
         return ORBMI_OK;
     }
@@ -419,11 +527,96 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     uint8_t* dFl = h->d_buf + ((fb + 255) & ~(size_t)255) + ((ob + 255) & ~(size_t)255);
     ORBMI_HIP(hipMemcpyAsync(dF, frames, fb, hipMemcpyHostToDevice, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(dO, obs, ob, hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl);
+    hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl, 0);
     ORBMI_HIP(hipGetLastError());
     ORBMI_HIP(hipMemcpyAsync(frames, dF, fb, hipMemcpyDeviceToHost, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(outlier, dFl, nobs, hipMemcpyDeviceToHost, h->stream));
     ORBMI_HIP(hipStreamSynchronize(h->stream));
+    return ORBMI_OK;
+}
+
+int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
+                                  const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier) {
+    using namespace orbmi;
+    if (!h || !F || !inv_level_sigma2 || !mp || !rec || !outlier || F->n < 0 || !F->tcw) return ORBMI_E_ARG;
+    if (F->nlevels < 1 || F->nlevels > kMaxLevels || (F->n > 0 && !F->keys_un)) return ORBMI_E_ARG;
+    if ((mp->match_lf && (!mp->lf_points || mp->n_lf_points < 0)) || (mp->match_mp && (!mp->mps || mp->n_mps < 0)))
+        return ORBMI_E_ARG;
+    if (F->n_device && !is_device_ptr(F->n_device)) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(h->device));
+    const bool async = is_device_ptr(rec) && is_device_ptr(outlier);
+    const size_t n = (size_t)std::max(F->n, 1);
+    if (n > h->cap_obs) {
+        if (h->d_obs) { ORBMI_HIP(hipStreamSynchronize(h->stream)); (void)hipFree(h->d_obs); }
+        h->d_obs = nullptr;
+        h->cap_obs = 0;
+        ORBMI_HIP(hipMalloc((void**)&h->d_obs, n * sizeof(orbmi_pose_obs)));
+        h->cap_obs = n;
+    }
+    // staging of host inputs / outputs: one block, sized for this call
+    auto host_bytes = [&](const void* p, size_t b) { return (p && !is_device_ptr(p)) ? ((b + 255) & ~(size_t)255) : 0; };
+    const size_t need = host_bytes(F->keys_un, n * sizeof(orbmi_keypoint)) + host_bytes(F->u_right, n * 4) +
+                        host_bytes(mp->match_lf, n * 4) + host_bytes(mp->match_mp, n * 4) +
+                        (mp->match_lf ? host_bytes(mp->lf_points, mp->n_lf_points * sizeof(orbmi_lastframe_point)) : 0) +
+                        (mp->match_mp ? host_bytes(mp->mps, mp->n_mps * sizeof(orbmi_mappoint)) : 0) +
+                        host_bytes(rec, sizeof(orbmi_pose_frame)) + host_bytes(outlier, n) + 512;
+    if (h->used_stage) ORBMI_HIP(hipStreamSynchronize(h->stream));  // an earlier call may still read it
+    h->used_stage = 0;
+    if (need > h->cap_stage) {
+        if (h->d_stage) (void)hipFree(h->d_stage);
+        h->d_stage = nullptr;
+        h->cap_stage = 0;
+        ORBMI_HIP(hipMalloc((void**)&h->d_stage, need));
+        h->cap_stage = need;
+    }
+    int rc = ORBMI_OK;
+    auto dev_in = [&](const void* p, size_t b) -> const void* {
+        if (!p || is_device_ptr(p) || b == 0) return p;
+        uint8_t* d = h->d_stage + h->used_stage;
+        h->used_stage += (b + 255) & ~(size_t)255;
+        if (hipMemcpyAsync(d, p, b, hipMemcpyHostToDevice, h->stream) != hipSuccess) rc = ORBMI_E_HIP;
+        return d;
+    };
+    auto dev_out = [&](void* p, size_t b) -> void* {
+        if (is_device_ptr(p)) return p;
+        uint8_t* d = h->d_stage + h->used_stage;
+        h->used_stage += (b + 255) & ~(size_t)255;
+        return d;
+    };
+    PoseGatherArgs a{};
+    a.n = F->n;
+    a.n_dev = F->n_device;
+    a.keys = (const orbmi_keypoint*)dev_in(F->keys_un, n * sizeof(orbmi_keypoint));
+    a.u_right = (const float*)dev_in(F->u_right, n * 4);
+    if (is_device_ptr(F->tcw)) a.tcw_dev = F->tcw;
+    else memcpy(a.tcw, F->tcw, sizeof(a.tcw));
+    a.fx = F->fx; a.fy = F->fy; a.cx = F->cx; a.cy = F->cy; a.bf = F->bf;
+    for (int l = 0; l < F->nlevels; l++) a.inv_sigma2[l] = inv_level_sigma2[l];
+    a.nlevels = F->nlevels;
+    a.match_lf = (const int*)dev_in(mp->match_lf, n * 4);
+    a.lfp = mp->match_lf ? (const orbmi_lastframe_point*)dev_in(mp->lf_points, mp->n_lf_points * sizeof(orbmi_lastframe_point))
+                         : nullptr;
+    a.n_lf = mp->match_lf ? mp->n_lf_points : 0;
+    a.match_mp = (const int*)dev_in(mp->match_mp, n * 4);
+    a.mps = mp->match_mp ? (const orbmi_mappoint*)dev_in(mp->mps, mp->n_mps * sizeof(orbmi_mappoint)) : nullptr;
+    a.n_mp = mp->match_mp ? mp->n_mps : 0;
+    a.rec = (orbmi_pose_frame*)dev_out(rec, sizeof(orbmi_pose_frame));
+    a.obs = h->d_obs;
+    a.outlier = (uint8_t*)dev_out(outlier, n);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pose_gather, dim3(1), dim3(kGatherThreads), 0, h->stream, a);
+    ORBMI_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_pose_opt, dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec, (const orbmi_pose_obs*)h->d_obs,
+                       a.outlier, 1);
+    ORBMI_HIP(hipGetLastError());
+    if (async) return ORBMI_OK;
+    if (!is_device_ptr(rec))
+        ORBMI_HIP(hipMemcpyAsync(rec, a.rec, sizeof(orbmi_pose_frame), hipMemcpyDeviceToHost, h->stream));
+    if (!is_device_ptr(outlier))
+        ORBMI_HIP(hipMemcpyAsync(outlier, a.outlier, (size_t)std::max(F->n, 0), hipMemcpyDeviceToHost, h->stream));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    h->used_stage = 0;
+    if (rec->inliers < 0) return ORBMI_E_UNSUPPORTED;  // more than kPoseMaxObs edges
     return ORBMI_OK;
 }
 

@@ -81,6 +81,23 @@ class PoseOptimizer:
     def synchronize(self):
         check("orbmi_pose_synchronize", lib().orbmi_pose_synchronize(self._h))
 
+    def share_stream(self, extractor_handle):
+        check("orbmi_pose_share_stream", lib().orbmi_pose_share_stream(self._h, extractor_handle))
+
+    def PoseOptimization(self, view, inv_level_sigma2: np.ndarray, mappoints, rec, outlier):
+        """Optimizer::PoseOptimization(Frame*) with its edge assembly: `view` = FrameView
+        (initial tcw), `mappoints` = FrameMapPoints, rec = POSE_FRAME_DTYPE record (numpy, or a
+        device address), outlier = per-keypoint mvbOutlier (numpy u8, or a device address).
+        Returns the inlier count for host records, None when enqueued on the device."""
+        sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        host = isinstance(rec, np.ndarray)
+        rp = rec.ctypes.data if host else rec
+        op = outlier.ctypes.data if isinstance(outlier, np.ndarray) else outlier
+        check("orbmi_pose_optimization_frame",
+              lib().orbmi_pose_optimization_frame(self._h, C.addressof(view), sig.ctypes.data, C.addressof(mappoints),
+                                                  rp, op))
+        return int(rec["inliers"]) if host else None
+
 
 # ---- minimal map model for the graph assembly (src/Optimizer.cc:486-534) ------------------
 @dataclasses.dataclass(eq=False)

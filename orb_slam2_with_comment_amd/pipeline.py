@@ -4,19 +4,22 @@ One tracked stereo frame, in the order Tracking runs it (src/Tracking.cc:287-581
 
   Frame ctor          ORBextractor(left) || ORBextractor(right)   src/Frame.cc:78-81
                       Frame::ComputeStereoMatches                 src/Frame.cc:92
-  TrackWithMotionModel ORBmatcher(0.9).SearchByProjection(CF, LF, th=7)  src/Tracking.cc:999-1028
+  TrackWithMotionModel ORBmatcher(0.9).SearchByProjection(CF, LF, th=7) [+ retry at 14 when
+                      < 20 matches], Optimizer::PoseOptimization, discard outliers
+                                                                  src/Tracking.cc:997-1063
   TrackLocalMap       Tracking::SearchLocalPoints -> isInFrustum(0.5) +
-                      ORBmatcher(0.8).SearchByProjection(F, localMPs, th=1)  src/Tracking.cc:1362-1402
+                      ORBmatcher(0.8).SearchByProjection(F, localMPs, th=1) at the optimised
+                      pose, Optimizer::PoseOptimization, mnMatchesInliers
+                                                                  src/Tracking.cc:1065-1104
   LocalMapping thread Optimizer::LocalBundleAdjustment on every new keyframe
                       (src/LocalMapping.cc:89-90), concurrently with tracking
 
-All four tracking stages run on ONE HIP stream (the extractor's; the matcher shares it), with
-inputs and outputs in HBM and keypoint counts read on the device (orbmi_frame_view.n_device),
-so a frame is enqueued without a host round trip.  Local BA runs on its own stream from a
-worker thread (the LocalMapping thread), overlapping tracking as in the reference.
-
-PoseOptimization (src/Optimizer.cc:257-481) is not on this path yet (SURVEY.md §8(f) rank 1);
-the local-map search therefore starts from the motion-model occupancy supplied by the caller.
+All tracking stages run on ONE HIP stream (the extractor's; the matcher and the pose optimiser
+share it), with inputs and outputs in HBM, keypoint counts read on the device
+(orbmi_frame_view.n_device) and the optimised pose read by the next search from its device
+record (orbmi_frame_view.tcw in device memory), so a frame is enqueued without a host round
+trip.  Local BA runs on its own stream from a worker thread (the LocalMapping thread),
+overlapping tracking as in the reference.
 """
 from __future__ import annotations
 
@@ -39,7 +42,7 @@ def frame_view(n, keys, u_right, desc, tcw, cam, scale_factors, width, height, n
     v = FrameView()
     v.n = int(n)
     v.keys_un, v.u_right, v.desc = keys, u_right, desc
-    v.tcw = tcw.ctypes.data if tcw is not None else None
+    v.tcw = tcw.ctypes.data if isinstance(tcw, np.ndarray) else None
     v.fx, v.fy, v.cx, v.cy, v.bf = cam.fx, cam.fy, cam.cx, cam.cy, cam.bf
     v.mb = np.float32(np.float32(cam.bf) / np.float32(cam.fx))
     v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(width), 0.0, float(height)
@@ -49,6 +52,8 @@ def frame_view(n, keys, u_right, desc, tcw, cam, scale_factors, width, height, n
     v.scale_factors = scale_factors.ctypes.data
     v.log_scale_factor = np.float32(np.log(np.float32(scale_factors[1]))) if len(scale_factors) > 1 else 0.0
     v.n_device = n_device
+    if isinstance(tcw, int):  # device address (an orbmi_pose_frame record's tcw)
+        v.tcw = tcw
     return v
 
 
@@ -58,11 +63,16 @@ class StereoTracker:
     def __init__(self, cam, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, device=0):
         import torch
         from .matcher import ORBmatcher
+        from .optimizer import PoseOptimizer
         from .orb import ORBextractor
+        from .types import POSE_FRAME_DTYPE
         self.cam, self.device = cam, device
         self.extractor = ORBextractor(nfeatures, scale_factor, nlevels, ini_th, min_th, device=device)
         self.matcher = ORBmatcher(device=device)
         check("orbmi_matcher_share_stream", lib().orbmi_matcher_share_stream(self.matcher._h, self.extractor.handle))
+        self.pose = PoseOptimizer(device)
+        self.pose.share_stream(self.extractor.handle)
+        self.inv_sigma2 = np.ascontiguousarray(self.extractor.GetInverseScaleSigmaSquares(), np.float32)
         s = _vp()
         check("orbmi_extractor_get_stream", lib().orbmi_extractor_get_stream(self.extractor.handle, C.byref(s)))
         self.stream_handle = s.value
@@ -75,14 +85,26 @@ class StereoTracker:
         self.counts = torch.zeros(2, dtype=torch.int32, device=dev)
         self.u_right = torch.zeros((2, cap), dtype=torch.float32, device=dev)
         self.depth = torch.zeros((2, cap), dtype=torch.float32, device=dev)
-        self.occupied = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        self.occupied = torch.zeros(cap, dtype=torch.uint8, device=dev)   # after the motion-model stage
+        self.no_points = torch.zeros(cap, dtype=torch.uint8, device=dev)  # fill(mvpMapPoints, NULL)
         self.match_lf = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         self.match_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        self.outlier = torch.zeros(cap, dtype=torch.uint8, device=dev)    # mvbOutlier
+        # pose records: [0] after TrackWithMotionModel, [1] after TrackLocalMap (POSE_FRAME_DTYPE)
+        self.rec_bytes = POSE_FRAME_DTYPE.itemsize
+        self.recs = torch.zeros((2, self.rec_bytes), dtype=torch.uint8, device=dev)
+        # [0] SearchByProjection(CF, LF) matches, [1:3] stage-0 counts, [3:5] stage-1 counts
+        self.tcounts = torch.zeros(8, dtype=torch.int32, device=dev)
         self._views = {}
 
-    def current_view(self, tcw: np.ndarray):
-        """Frame view of the frame being tracked (device arrays, device count)."""
-        key = tcw.ctypes.data
+    def rec_tcw(self, k):
+        """Device address of pose record k's tcw (its first field)."""
+        return self.recs.data_ptr() + k * self.rec_bytes
+
+    def current_view(self, tcw):
+        """Frame view of the frame being tracked (device arrays, device count); tcw = host
+        numpy pose or the device address of a pose record."""
+        key = tcw if isinstance(tcw, int) else tcw.ctypes.data
         v = self._views.get(key)
         if v is None:
             v = frame_view(self.cap, self.kps.data_ptr(), self.u_right.data_ptr(), self.desc.data_ptr(), tcw,
@@ -106,7 +128,7 @@ class StereoTracker:
         (src/Tracking.cc:1016) -> self.match_lf (device)."""
         cv = self.current_view(tcw)
         check("orbmi_search_by_projection_last_frame", lib().orbmi_search_by_projection_last_frame(
-            self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), C.addressof(last_view),
+            self.matcher._h, C.addressof(cv), _vp(self.no_points.data_ptr()), C.addressof(last_view),
             _vp(last_points), th, 0, 1, _vp(self.match_lf.data_ptr()), None))
 
     def search_local_points(self, tcw, local_mps, n_mp, th=1.0):
@@ -116,16 +138,71 @@ class StereoTracker:
             self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), _vp(local_mps), int(n_mp), th,
             _vp(self.match_mp.data_ptr()), None, None))
 
+    def track_with_motion_model(self, tcw, last_view, last_points, th=7.0):
+        """Tracking::TrackWithMotionModel (src/Tracking.cc:997-1063) after the frame's
+        extraction: SearchByProjection(CF, LF, th) from the motion-model pose `tcw` (host), the
+        retry at 2*th when fewer than 20 matches (device-side test), PoseOptimization -> pose
+        record 0, outliers discarded -> self.occupied for the local-map search."""
+        L = lib()
+        cv = self.current_view(tcw)
+        mp = self.frame_mappoints(last_view, last_points, None, 0)
+        for t, gate in ((th, 0x7FFFFFFF), (2 * th, 20)):  # the first search always runs
+            check("orbmi_search_by_projection_last_frame_if", L.orbmi_search_by_projection_last_frame_if(
+                self.matcher._h, C.addressof(cv), _vp(self.no_points.data_ptr()), C.addressof(last_view),
+                _vp(last_points), t, 0, 1, _vp(self.match_lf.data_ptr()), _vp(self.tcounts.data_ptr()), gate))
+        self.pose.PoseOptimization(cv, self.inv_sigma2, mp, self.rec_tcw(0), self.outlier.data_ptr())
+        check("orbmi_track_update_matches", L.orbmi_track_update_matches(
+            self.matcher._h, C.addressof(cv), 0, _vp(self.outlier.data_ptr()), C.addressof(mp),
+            _vp(self.occupied.data_ptr()), _vp(self.tcounts.data_ptr() + 4)))
+
+    def track_local_map(self, last_view, last_points, local_mps, n_mp, th=1.0):
+        """Tracking::TrackLocalMap (src/Tracking.cc:1065-1104) at pose record 0: SearchLocalPoints,
+        PoseOptimization -> pose record 1, mnMatchesInliers (stereo outliers -> NULL)."""
+        L = lib()
+        cv = self.current_view(self.rec_tcw(0))
+        check("orbmi_search_local_points", L.orbmi_search_local_points(
+            self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), _vp(local_mps), int(n_mp), th,
+            _vp(self.match_mp.data_ptr()), None, None))
+        mp = self.frame_mappoints(last_view, last_points, local_mps, n_mp)
+        self.pose.PoseOptimization(cv, self.inv_sigma2, mp, self.rec_tcw(1), self.outlier.data_ptr())
+        check("orbmi_track_update_matches", L.orbmi_track_update_matches(
+            self.matcher._h, C.addressof(cv), 1, _vp(self.outlier.data_ptr()), C.addressof(mp), None,
+            _vp(self.tcounts.data_ptr() + 12)))
+
+    def frame_mappoints(self, last_view, last_points, local_mps, n_mp):
+        from .types import FrameMapPoints
+        mp = FrameMapPoints()
+        mp.match_lf, mp.lf_points, mp.n_lf_points = self.match_lf.data_ptr(), last_points, last_view.n
+        if local_mps is not None:
+            mp.match_mp, mp.mps, mp.n_mps = self.match_mp.data_ptr(), local_mps, int(n_mp)
+        return mp
+
     def track(self, d_left_right, rows, cols, tcw, last_view, last_points, local_mps, n_mp, th_lf=7.0, th_local=1.0):
-        """Enqueue one tracked frame; results stay in self.match_lf / self.match_mp (device)."""
+        """Enqueue one tracked stereo frame (Frame ctor + TrackWithMotionModel + TrackLocalMap);
+        results stay on the device: self.match_lf / match_mp (final mvpMapPoints), self.outlier,
+        pose records self.recs, counts self.tcounts (see results())."""
         self.extract_stereo(d_left_right, rows, cols)
-        self.search_last_frame(tcw, last_view, last_points, th_lf)
-        self.search_local_points(tcw, local_mps, n_mp, th_local)
+        self.track_with_motion_model(tcw, last_view, last_points, th_lf)
+        self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
+
+    def results(self):
+        """Synchronise and read the frame's tracking outcome: ok follows the reference's return
+        values (search >= 20, nmatchesMap >= 10, mnMatchesInliers >= 30); when a stage fails
+        the later outputs are unspecified (the reference stops there)."""
+        from .types import POSE_FRAME_DTYPE
+        self.synchronize()
+        c = self.tcounts.cpu().numpy()
+        recs = self.recs.cpu().numpy().copy().view(POSE_FRAME_DTYPE).reshape(2)
+        ok = c[0] >= 20 and c[2] >= 10 and c[3] >= 30
+        return {"ok": bool(ok), "search_matches": int(c[0]), "outliers_mm": int(c[1]), "nmatches_map": int(c[2]),
+                "inliers": int(c[3]), "outliers": int(c[4]), "tcw_mm": recs[0]["tcw"].reshape(4, 4).copy(),
+                "tcw": recs[1]["tcw"].reshape(4, 4).copy(), "recs": recs}
 
     def synchronize(self):
         check("orbmi_extractor_synchronize", lib().orbmi_extractor_synchronize(self.extractor.handle))
 
     def close(self):
+        self.pose.close()
         self.matcher.close()
         self.extractor.close()
 

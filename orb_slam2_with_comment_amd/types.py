@@ -118,6 +118,12 @@ POSE_FRAME_DTYPE = np.dtype([("tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"), (
 assert POSE_OBS_DTYPE.itemsize == 32 and POSE_FRAME_DTYPE.itemsize == 100
 
 
+class FrameMapPoints(C.Structure):
+    """orbmi_frame_mappoints: Frame::mvpMapPoints as match arrays (include/orbmi.h)."""
+    _fields_ = [("match_lf", C.c_void_p), ("lf_points", C.c_void_p), ("n_lf_points", C.c_int),
+                ("match_mp", C.c_void_p), ("mps", C.c_void_p), ("n_mps", C.c_int)]
+
+
 class BAProblemView(C.Structure):
     _fields_ = [("nkf", C.c_int), ("npt", C.c_int), ("nedge", C.c_int), ("kfs", C.c_void_p), ("pts", C.c_void_p),
                 ("edges", C.c_void_p)]

@@ -19,8 +19,10 @@ def _lf_view_host(f):
 
 
 def test_tracker_device_resident_matches_oracle(oracle):
-    """extract(L,R) -> stereo -> SearchByProjection(CF,LF) -> SearchLocalPoints, all enqueued on
-    one stream with device-side keypoint counts, equals the oracle on the same frames."""
+    """extract(L,R) -> stereo -> SearchByProjection(CF,LF) -> SearchLocalPoints (the searches
+    alone, at the same pose and with empty occupancy; the full chain with PoseOptimization is
+    tests/test_track_gpu.py), all enqueued on one stream with device-side keypoint counts,
+    equals the oracle on the same frames."""
     import torch
     from orb_slam2_with_comment_amd import synth, synth_map as SM
     from orb_slam2_with_comment_amd.pipeline import StereoTracker
@@ -42,7 +44,9 @@ def test_tracker_device_resident_matches_oracle(oracle):
     d_lfp = torch.from_numpy(lfp.view(np.uint8).copy()).cuda()
     d_mps = torch.from_numpy(mps.view(np.uint8).copy()).cuda()
     lv = lf.view()  # host arrays: exercises the mixed host/device path too
-    tr.track(imgs.data_ptr(), cam.height, cam.width, tcw, lv, d_lfp.data_ptr(), d_mps.data_ptr(), len(mps))
+    tr.extract_stereo(imgs.data_ptr(), cam.height, cam.width)
+    tr.search_last_frame(tcw, lv, d_lfp.data_ptr())
+    tr.search_local_points(tcw, d_mps.data_ptr(), len(mps))  # tr.occupied is still all zero
     tr.synchronize()
     n = int(tr.counts[0])
     kl, dl, u, d, _ = frame_data(f)
