@@ -82,6 +82,7 @@ _PROTOS = {
     "orbmi_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "orbmi_debug_octree_level": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
+    "orbmi_debug_pose_trace": (_i, [_vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

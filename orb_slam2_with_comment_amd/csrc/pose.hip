@@ -8,9 +8,11 @@
 //                                                              .cpp:266-364 (float invz, stereo)
 //   BaseUnaryEdge::constructQuadraticForm                      core/base_unary_edge.hpp:43-75
 //   OptimizationAlgorithmLevenberg::solve                      levenberg.cpp:61-189
-// The edge errors of the last computeActiveErrors stay in LDS: the outlier classification after
-// each optimize(10) reads them as g2o does (stale after a rejected trial).  Parity: 1e-4 on the
-// pose, identical outlier flags and inlier count (tests/test_pose_gpu.py).
+// The edges live in LDS for the whole kernel; the chi2 of each edge's last computeActiveErrors
+// stays there too: the outlier classification after each optimize(10) reads it as g2o does
+// (stale after a rejected trial).  Reductions are wave reduce-scatters on DPP / permlane swaps
+// plus one LDS slot per wave, in a fixed order.  Parity: 1e-4 on the pose, outlier flags and
+// inlier count equal up to chi2-on-threshold flips (tests/test_pose_gpu.py).
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
@@ -24,29 +26,38 @@
 
 namespace orbmi {
 
-constexpr int kPoseThreads = 256;
+constexpr int kPoseThreads = 512;  // 8 waves, 2 per SIMD: the per-edge passes hide fp64 latency
+constexpr int kPoseWaves = kPoseThreads / 64;
 constexpr int kPoseMaxObs = 4096;
+constexpr int kPoseTraceSeqs = 64;  // passes recorded by orbmi_debug_pose_trace
+constexpr int kPoseTraceWords = 16 + kPoseTraceSeqs * kPoseWaves * 8;
 
 struct PoseCam { double fx, fy, cx, cy, bf; };
 
-// obs - cam_project(T Xw) (EdgeSE3ProjectXYZOnlyPose::computeError / the stereo variant)
-__device__ inline void pose_error(const double* T, const PoseCam& c, const orbmi_pose_obs& o, double e[3]) {
+// Huber delta of the edge (src/Optimizer.cc:290-291, float sqrt)
+__device__ inline double pose_delta(const orbmi_pose_obs& o) {
+    return o.ur < 0 ? (double)sqrtf(5.991f) : (double)sqrtf(7.815f);
+}
+
+// camera-frame point and obs - cam_project(T Xw) (EdgeSE3ProjectXYZOnlyPose::computeError /
+// the stereo variant); invz = 1 / p.z (the stereo projection rounds it to float,
+// types_six_dof_expmap.cpp:309)
+__device__ inline void pose_error(const double* T, const PoseCam& c, const orbmi_pose_obs& o, double p[3],
+                                  double& invz, double e[3]) {
     const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
-    double p[3];
     se3_map(T, X, p);
+    invz = fast_rcp(p[2]);
     if (o.ur < 0) {
-        const double px = p[0] / p[2], py = p[1] / p[2];
-        e[0] = (double)o.u - (px * c.fx + c.cx);
-        e[1] = (double)o.v - (py * c.fy + c.cy);
+        e[0] = (double)o.u - (p[0] * invz * c.fx + c.cx);
+        e[1] = (double)o.v - (p[1] * invz * c.fy + c.cy);
         e[2] = 0;
     } else {
-        const float invz = (float)(1.0f / p[2]);  // types_six_dof_expmap.cpp:309
-        const double r0 = p[0] * invz * c.fx + c.cx;
-        const double r1 = p[1] * invz * c.fy + c.cy;
-        const double r2 = r0 - c.bf * invz;
+        const float fz = (float)invz;
+        const double r0 = p[0] * fz * c.fx + c.cx;
+        const double r1 = p[1] * fz * c.fy + c.cy;
         e[0] = (double)o.u - r0;
         e[1] = (double)o.v - r1;
-        e[2] = (double)o.ur - r2;
+        e[2] = (double)o.ur - (r0 - c.bf * fz);
     }
 }
 
@@ -55,69 +66,153 @@ __device__ inline double pose_chi2(const orbmi_pose_obs& o, const double e[3]) {
     return e[0] * (info * e[0]) + e[1] * (info * e[1]) + (o.ur < 0 ? 0.0 : e[2] * (info * e[2]));
 }
 
-// Huber delta of the edge (src/Optimizer.cc:290-291, float sqrt)
-__device__ inline double pose_delta(const orbmi_pose_obs& o) {
-    return o.ur < 0 ? (double)sqrtf(5.991f) : (double)sqrtf(7.815f);
+// ---------------------------------------------------------------- wave primitives (gfx950)
+// Cross-lane moves without LDS: DPP inside a row of 16 lanes, v_permlane16/32_swap across rows.
+template <int CTRL>
+__device__ inline double dpp_mov(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+constexpr int kDppXor1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7-i within 8 (pairs lane bit 2 clear/set)
+constexpr int kDppRor8 = 0x128;        // row_ror:8 = lane i <-> i^8 within 16
 
-// fixed-order workgroup sum of NV doubles: lane 0 of each wave publishes, every thread adds the
-// wave partials in wave order (uniform result, no broadcast step)
-template <int NV>
-__device__ inline void pose_reduce(double (&v)[NV], double (*red)[NV]) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < NV; q++) {
-        double x = v[q];
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if (lane == 0) red[wid][q] = x;
+// v_permlane{16,32}_swap on (a, b): lanes with the bit clear end with a_own + a_partner, lanes
+// with it set with b_partner + b_own (partner = lane ^ 16 or ^ 32)
+template <int W>
+__device__ inline double swap_combine(double a, double b) {
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+    const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+    unsigned xl = (unsigned)ua, xh = (unsigned)(ua >> 32), yl = (unsigned)ub, yh = (unsigned)(ub >> 32);
+    if constexpr (W == 32) {
+        auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+        auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+        xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
+    } else {
+        auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+        auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+        xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
     }
-    __syncthreads();
+    const double nx = __longlong_as_double((long long)(((unsigned long long)xh << 32) | xl));
+    const double ny = __longlong_as_double((long long)(((unsigned long long)yh << 32) | yl));
+    return nx + ny;
+}
+
+// one reduce-scatter step inside a row: lanes with `upper` keep b, the others a, each adding
+// the partner's copy of what it keeps
+template <int CTRL>
+__device__ inline double dpp_combine(double a, double b, bool upper) {
+    const double recv = dpp_mov<CTRL>(upper ? a : b);
+    return (upper ? b : a) + recv;
+}
+
+// Reduce-scatter of 32 per-lane values over the wave: afterwards lane l holds the wave sum of
+// value l >> 1 (32 exchanges instead of 6 per value)
+__device__ inline double wave_reduce_scatter32(double (&v)[32]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < NV; q++) {
-        double s = 0;
-        for (int w = 0; w < kPoseThreads / 64; w++) s += red[w][q];
-        v[q] = s;
+    for (int j = 0; j < 16; j++) v[j] = swap_combine<32>(v[j], v[16 + j]);
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = swap_combine<16>(v[j], v[8 + j]);
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = dpp_combine<kDppRor8>(v[j], v[4 + j], lane & 8);
+#pragma unroll
+    for (int j = 0; j < 2; j++) v[j] = dpp_combine<kDppHalfMirror>(v[j], v[2 + j], lane & 4);
+    v[0] = dpp_combine<kDppXor2>(v[0], v[1], lane & 2);
+    return v[0] + dpp_mov<kDppXor1>(v[0]);
+}
+
+// all-reduce of one value over the wave (every lane ends with the same sum)
+__device__ inline double wave_sum(double v) {
+    const int lane = threadIdx.x & 63;
+    v += dpp_mov<kDppXor1>(v);
+    v += dpp_mov<kDppXor2>(v);
+    v += dpp_mov<kDppHalfMirror>(v);
+    v += dpp_mov<kDppRor8>(v);
+    {
+        const double s = swap_combine<16>(v, v);  // own + partner on every lane
+        v = s;
     }
-    __syncthreads();
+    (void)lane;
+    return swap_combine<32>(v, v);
 }
 
-__device__ inline int pose_reduce_int(int v, int* redi) {
+__device__ inline double readlane_d(double v, int l) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// fixed-order workgroup sum of the 28 normal-equation terms into wave 0: every wave
+// reduce-scatters its lanes' terms (DPP / permlane swaps), writes one LDS slot per (wave, value);
+// after the barrier wave 0's lane q sums value q over the waves in wave order and readlane
+// broadcasts the totals to all of wave 0's lanes.  The other waves' acc is left unspecified.
+// ev (trace builds only): this wave's event slots of the current pass, see k_pose_opt
+__device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], unsigned long long* ev = nullptr) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) redi[wid] = v;
+    double v[32];
+#pragma unroll
+    for (int q = 0; q < 28; q++) v[q] = acc[q];
+    v[28] = v[29] = v[30] = v[31] = 0;
+    const double s = wave_reduce_scatter32(v);
+    if (!(lane & 1)) red[wid][lane >> 1] = s;
+    if (ev && lane == 0) ev[2] = __builtin_amdgcn_s_memtime();
     __syncthreads();
-    int s = 0;
-    for (int w = 0; w < kPoseThreads / 64; w++) s += redi[w];
-    __syncthreads();
-    return s;
+    if (ev && lane == 0) ev[3] = __builtin_amdgcn_s_memtime();
+    if (wid == 0) {
+        double t = 0;
+#pragma unroll
+        for (int w = 0; w < kPoseWaves; w++) t += red[w][lane & 31];
+#pragma unroll
+        for (int q = 0; q < 28; q++) acc[q] = readlane_d(t, q);
+        if (ev && lane == 0) ev[4] = __builtin_amdgcn_s_memtime();
+    }
 }
 
-// LDL^T solve of the damped 6x6 system (LinearSolverDense); false on a non-positive pivot
+__device__ inline double pose_reduce1(double v, double* red1) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red1[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0;
+#pragma unroll
+    for (int w = 0; w < kPoseWaves; w++) t += red1[w];
+    return t;
+}
+
+// LDL^T solve of the damped 6x6 system (LinearSolverDense); false on a non-positive pivot.
+// LD[i][k] = L[i][k] * D[k] is kept so every inner product is a chain of FMAs.
 __device__ inline bool pose_solve6(const double H[21], const double b[6], double lam, double x[6]) {
-    double A[6][6];
+    double A[6][6], LD[6][6];
     {
         int q = 0;
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = r; c < 6; c++, q++) { A[r][c] = H[q]; A[c][r] = H[q]; }
+            for (int c = r; c < 6; c++, q++) A[c][r] = H[q];  // lower triangle
     }
 #pragma unroll
     for (int j = 0; j < 6; j++) A[j][j] += lam;
     bool ok = true;
+    double inv[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) {
         double d = A[j][j];
 #pragma unroll
-        for (int k = 0; k < j; k++) d -= A[j][k] * A[j][k] * A[k][k];
+        for (int k = 0; k < j; k++) d -= A[j][k] * LD[j][k];
         ok &= (fabs(d) > 0) && isfinite(d);
         A[j][j] = d;
+        inv[j] = fast_rcp(d);
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
             double s = A[i][j];
 #pragma unroll
-            for (int k = 0; k < j; k++) s -= A[i][k] * A[j][k] * A[k][k];
-            A[i][j] = s / d;
+            for (int k = 0; k < j; k++) s -= A[i][k] * LD[j][k];
+            LD[i][j] = s;          // L[i][j] * D[j]
+            A[i][j] = s * inv[j];  // L[i][j]
         }
     }
     double y[6];
@@ -129,7 +224,7 @@ __device__ inline bool pose_solve6(const double H[21], const double b[6], double
         y[i] = s;
     }
 #pragma unroll
-    for (int i = 0; i < 6; i++) y[i] /= A[i][i];
+    for (int i = 0; i < 6; i++) y[i] *= inv[i];
 #pragma unroll
     for (int i = 5; i >= 0; i--) {
         double s = y[i];
@@ -140,13 +235,94 @@ __device__ inline bool pose_solve6(const double H[21], const double b[6], double
     return ok;
 }
 
+// computeActiveErrors + activeRobustChi2 + buildSystem at T for this thread's level-0 edges:
+// acc[0..20] = upper 6x6 of J^T W J, acc[21..26] = b, acc[27] = robust chi2; schi = (float) chi2
+// of each edge (the stale errors the outlier test reads).
+__device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbmi_pose_obs* sobs, const uint8_t* outl,
+                                 float* schi, int n, bool robust, double (&acc)[28]) {
+#pragma unroll
+    for (int q = 0; q < 28; q++) acc[q] = 0;
+    for (int k = threadIdx.x; k < n; k += kPoseThreads) {
+        if (outl[k]) continue;
+        const orbmi_pose_obs o = sobs[k];
+        double p[3], invz, e[3];
+        pose_error(T, cam, o, p, invz, e);
+        const double c2 = pose_chi2(o, e), info = (double)o.inv_sigma2;
+        schi[k] = (float)c2;
+        double rho0 = c2, rho1 = 1.0;
+        if (robust) {
+            const double d = pose_delta(o), dsqr = d * d;
+            if (c2 > dsqr) { const double r = fast_rsqrt(c2), sq = c2 * r; rho0 = 2 * sq * d - dsqr; rho1 = d * r; }
+        }
+        acc[27] += rho0;
+        // linearizeOplus (types_six_dof_expmap.cpp:266-290, :332-364); J[0][4] = J[1][3] =
+        // J[2][4] = 0 and the third row is zero for monocular edges: those products are skipped
+        const double x = p[0], y = p[1], invz_2 = invz * invz;
+        const double a0 = x * y * invz_2 * cam.fx, a1 = -(1 + (x * x * invz_2)) * cam.fx, a2 = y * invz * cam.fx;
+        const double a3 = -invz * cam.fx, a5 = x * invz_2 * cam.fx;
+        const double b0 = (1 + y * y * invz_2) * cam.fy, b1 = -x * y * invz_2 * cam.fy, b2 = -x * invz * cam.fy;
+        const double b4 = -invz * cam.fy, b5 = y * invz_2 * cam.fy;
+        const double w = rho1 * info;  // robustInformation
+        const double wa0 = w * a0, wa1 = w * a1, wa2 = w * a2, wa3 = w * a3, wa5 = w * a5;
+        const double wb0 = w * b0, wb1 = w * b1, wb2 = w * b2, wb4 = w * b4, wb5 = w * b5;
+        const double ea = rho1 * (info * e[0]), eb = rho1 * (info * e[1]);
+        // upper triangle, row-major: (0,0..5) (1,1..5) (2,2..5) (3,3..5) (4,4..5) (5,5)
+        acc[0] += a0 * wa0 + b0 * wb0;  acc[1] += a0 * wa1 + b0 * wb1;  acc[2] += a0 * wa2 + b0 * wb2;
+        acc[3] += a0 * wa3;             acc[4] += b0 * wb4;             acc[5] += a0 * wa5 + b0 * wb5;
+        acc[6] += a1 * wa1 + b1 * wb1;  acc[7] += a1 * wa2 + b1 * wb2;  acc[8] += a1 * wa3;
+        acc[9] += b1 * wb4;             acc[10] += a1 * wa5 + b1 * wb5;
+        acc[11] += a2 * wa2 + b2 * wb2; acc[12] += a2 * wa3;            acc[13] += b2 * wb4;
+        acc[14] += a2 * wa5 + b2 * wb5;
+        acc[15] += a3 * wa3;            acc[17] += a3 * wa5;            // acc[16] = H(3,4) = 0
+        acc[18] += b4 * wb4;            acc[19] += b4 * wb5;
+        acc[20] += a5 * wa5 + b5 * wb5;
+        acc[21] -= a0 * ea + b0 * eb;   acc[22] -= a1 * ea + b1 * eb;   acc[23] -= a2 * ea + b2 * eb;
+        acc[24] -= a3 * ea;             acc[25] -= b4 * eb;             acc[26] -= a5 * ea + b5 * eb;
+        if (!(o.ur < 0)) {  // stereo: third row
+            const double c0 = a0 - cam.bf * y * invz_2, c1 = a1 + cam.bf * x * invz_2, c2_ = a2, c3 = a3;
+            const double c5 = a5 - cam.bf * invz_2;
+            const double wc0 = w * c0, wc1 = w * c1, wc2 = w * c2_, wc3 = w * c3, wc5 = w * c5;
+            const double ec = rho1 * (info * e[2]);
+            acc[0] += c0 * wc0;  acc[1] += c0 * wc1;  acc[2] += c0 * wc2;  acc[3] += c0 * wc3;  acc[5] += c0 * wc5;
+            acc[6] += c1 * wc1;  acc[7] += c1 * wc2;  acc[8] += c1 * wc3;  acc[10] += c1 * wc5;
+            acc[11] += c2_ * wc2; acc[12] += c2_ * wc3; acc[14] += c2_ * wc5;
+            acc[15] += c3 * wc3; acc[17] += c3 * wc5;
+            acc[20] += c5 * wc5;
+            acc[21] -= c0 * ec;  acc[22] -= c1 * ec;  acc[23] -= c2_ * ec; acc[24] -= c3 * ec;  acc[26] -= c5 * ec;
+        }
+    }
+}
+
+// One workgroup per frame.  The Levenberg trial pass is fused with the next iteration's
+// buildSystem: g2o's next iteration starts with computeActiveErrors + buildSystem at the state
+// the accepted trial left (levenberg.cpp:67-85), so the trial pass accumulates J^T W J and b at
+// the trial pose too, and an accepted trial hands them on (a rejected one keeps H, b: g2o
+// re-solves the same system with a larger lambda).  One edge pass + one reduction per trial.
+// TR = event trace (orbmi_debug_pose_trace): lane 0 of every wave stamps s_memtime per edge
+// pass (seq) into trace[16 + (seq * kPoseWaves + wave) * 8 + e]: e = 0 pass start, 1 pass end,
+// 2 reduce-scatter written, 3 barrier B passed, 4 (wave 0) totals broadcast, 5 (wave 0) LM
+// update done, 6 (wave 0) next trial pose published; trace[0] = total cycles, [1] = total
+// s_memrealtime ticks, [2] = passes of thread 0's wave.
+template <bool TR>
 __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __restrict__ frames,
                                                            const orbmi_pose_obs* __restrict__ obs,
-                                                           uint8_t* __restrict__ outlier_out, int by_index) {
-    __shared__ double err[kPoseMaxObs][3];
+                                                           uint8_t* __restrict__ outlier_out, int by_index,
+                                                           unsigned long long* __restrict__ trace) {
+    __shared__ orbmi_pose_obs sobs[kPoseMaxObs];
+    __shared__ float schi[kPoseMaxObs];    // (float) chi2 of the last computeActiveErrors
     __shared__ uint8_t outl[kPoseMaxObs];  // mvbOutlier; the edge's level is the same flag
-    __shared__ double red[kPoseThreads / 64][28];
-    __shared__ int redi[kPoseThreads / 64];
+    __shared__ double red[2][kPoseWaves][32];
+    __shared__ double red1[2][kPoseWaves];
+    __shared__ double sTt[8];  // wave 0's trial (or final) pose, read after the next barrier
+    __shared__ int sCmd;
+    unsigned long long tstart = 0, rstart = 0;
+    if (TR && threadIdx.x == 0) { tstart = __builtin_amdgcn_s_memtime(); rstart = __builtin_amdgcn_s_memrealtime(); }
+    int seq = 0;  // passes run by this wave (trace builds)
+    auto evp = [&]() -> unsigned long long* {
+        return (TR && seq < kPoseTraceSeqs) ? trace + 16 + (seq * kPoseWaves + (threadIdx.x >> 6)) * 8 : nullptr;
+    };
+#define EV(e)                                                                                    \
+    if (TR && (threadIdx.x & 63) == 0 && seq < kPoseTraceSeqs) evp()[e] = __builtin_amdgcn_s_memtime();
     const int tid = threadIdx.x;
     orbmi_pose_frame& F = frames[blockIdx.x];
     const int n = F.n_obs;
@@ -160,12 +336,12 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         if (tid == 0) { F.inliers = -1; F.iterations = 0; }
         return;
     }
-    for (int k = tid; k < n; k += kPoseThreads) outl[k] = 0;
     if (n < 3) {  // src/Optimizer.cc:378-379: no optimisation, pose untouched
         for (int k = tid; k < n; k += kPoseThreads) put_flag(k, 0);
         if (tid == 0) { F.inliers = 0; F.iterations = 0; }
         return;
     }
+    for (int k = tid; k < n; k += kPoseThreads) { sobs[k] = O[k]; outl[k] = 0; }
     const PoseCam cam{F.fx, F.fy, F.cx, F.cy, F.bf};
     double T0[8];  // Converter::toSE3Quat(pFrame->mTcw)
     {
@@ -178,147 +354,134 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         T0[4] = F.tcw[3]; T0[5] = F.tcw[7]; T0[6] = F.tcw[11]; T0[7] = 0;
     }
     double T[8];
-    int nBad = 0, iters = 0;
+    int nBad = 0, iters = 0, rb = 0;  // rb: alternating reduction buffer
+    const int wid = tid >> 6;
     __syncthreads();
     for (int it = 0; it < 4; it++) {
         const bool robust = it < 3;  // setRobustKernel(0) after the third round (:463-464)
 #pragma unroll
         for (int q = 0; q < 8; q++) T[q] = T0[q];
-        int nact = 0;
+        double nact = 0;
         for (int k = tid; k < n; k += kPoseThreads) nact += !outl[k];
-        nact = pose_reduce_int(nact, redi);
-        // ---- optimize(10) on the level-0 edges
-        double lambda = 0, ni = 2;
-        int nbadIt = 0;
-        for (int i = 0; i < 10 && nact > 0; i++) {
-            // computeActiveErrors + activeRobustChi2 + buildSystem at T, one pass
+        nact = pose_reduce1(nact, red1[rb]);
+        rb ^= 1;
+        if (nact > 0) {
+            // ---- optimize(10) on the level-0 edges.  Every wave runs the edge passes; wave 0
+            // alone runs the Levenberg control, the damped solve and the exponential map, and
+            // hands each trial pose to the others through LDS (sCmd = 1: evaluate sTt; 0: done,
+            // sTt = the final estimate).
             double acc[28];
+            EV(0);
+            pose_pass(T, cam, sobs, outl, schi, n, robust, acc);  // computeActiveErrors + buildSystem
+            EV(1);
+            pose_reduce28_w0(acc, red[rb], evp());
+            rb ^= 1;
+            if (wid == 0) {
+                double currentChi = acc[27];
+                // computeLambdaInit, tau = 1e-5
+                double lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
+                                            fmax(fabs(acc[18]), fabs(acc[20])));
+                double ni = 2;
+                int nbadIt = 0;
+                for (int i = 0; i < 10; i++) {
+                    const double iniChi = currentChi;
+                    double rho = 0;
+                    int qmax = 0;
+                    do {
+                        double xv[6], Tt[8];
+                        const bool ok2 = pose_solve6(acc, acc + 21, lambda, xv);
+                        if (ok2) se3_oplus(xv, T, Tt);
+                        else {
 #pragma unroll
-            for (int q = 0; q < 28; q++) acc[q] = 0;
-            for (int k = tid; k < n; k += kPoseThreads) {
-                if (outl[k]) continue;
-                const orbmi_pose_obs o = O[k];
-                double e[3];
-                pose_error(T, cam, o, e);
-                err[k][0] = e[0]; err[k][1] = e[1]; err[k][2] = e[2];
-                const double c2 = pose_chi2(o, e), info = (double)o.inv_sigma2;
-                double rho0 = c2, rho1 = 1.0;
-                if (robust) {
-                    const double d = pose_delta(o), dsqr = d * d;
-                    if (c2 > dsqr) { const double sq = sqrt(c2); rho0 = 2 * sq * d - dsqr; rho1 = d / sq; }
+                            for (int q = 0; q < 8; q++) Tt[q] = T[q];
+#pragma unroll
+                            for (int q = 0; q < 6; q++) xv[q] = 0;
+                        }
+                        if (tid == 0) {
+#pragma unroll
+                            for (int q = 0; q < 8; q++) sTt[q] = Tt[q];
+                            sCmd = 1;
+                        }
+                        EV(6);
+                        seq++;
+                        __syncthreads();  // A: trial published
+                        EV(0);
+                        double tacc2[28];
+                        pose_pass(Tt, cam, sobs, outl, schi, n, robust, tacc2);
+                        EV(1);
+                        pose_reduce28_w0(tacc2, red[rb], evp());
+                        rb ^= 1;
+                        const double tempChi = ok2 ? tacc2[27] : DBL_MAX;
+                        double scale = 0;
+#pragma unroll
+                        for (int j = 0; j < 6; j++) scale += xv[j] * (lambda * xv[j] + acc[21 + j]);
+                        rho = (currentChi - tempChi) * fast_rcp(scale + 1e-3);
+                        if (rho > 0 && isfinite(tempChi)) {
+                            const double t = 2 * rho - 1;
+                            double alpha = 1. - t * t * t;
+                            alpha = fmin(alpha, 2. / 3.);
+                            lambda *= fmax(1. / 3., alpha);
+                            ni = 2;
+                            currentChi = tempChi;
+#pragma unroll
+                            for (int q = 0; q < 8; q++) T[q] = Tt[q];
+#pragma unroll
+                            for (int q = 0; q < 28; q++) acc[q] = tacc2[q];
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                        }
+                        qmax++;
+                        EV(5);
+                    } while (rho < 0 && qmax < 10);
+                    iters++;
+                    if (qmax == 10 || rho == 0) break;
+                    if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
+                    else nbadIt = 0;
+                    if (nbadIt >= 3) break;
                 }
-                acc[27] += rho0;
-                // linearizeOplus (types_six_dof_expmap.cpp:266-290, :332-364)
-                const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
-                double p[3];
-                se3_map(T, X, p);
-                const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
-                double J[3][6];
-                J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx; J[0][2] = y * invz * cam.fx;
-                J[0][3] = -invz * cam.fx; J[0][4] = 0; J[0][5] = x * invz_2 * cam.fx;
-                J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy; J[1][2] = -x * invz * cam.fy;
-                J[1][3] = 0; J[1][4] = -invz * cam.fy; J[1][5] = y * invz_2 * cam.fy;
-                const bool st = !(o.ur < 0);
-                J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
-                J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
-                J[2][2] = st ? J[0][2] : 0.0;
-                J[2][3] = st ? J[0][3] : 0.0;
-                J[2][4] = 0;
-                J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
-                const double w = rho1 * info;  // robustInformation
-                const double om[3] = {info * e[0], info * e[1], st ? info * e[2] : 0.0};
-                int q = 0;
+                if (tid == 0) {
 #pragma unroll
-                for (int r = 0; r < 6; r++)
+                    for (int q = 0; q < 8; q++) sTt[q] = T[q];
+                    sCmd = 0;
+                }
+                __syncthreads();  // A: done
+            } else {
+                for (;;) {
+                    seq++;
+                    __syncthreads();  // A
+                    if (sCmd == 0) break;
+                    EV(0);
+                    double Tt[8], tacc2[28];
 #pragma unroll
-                    for (int c = r; c < 6; c++, q++) acc[q] += J[0][r] * w * J[0][c] + J[1][r] * w * J[1][c] + J[2][r] * w * J[2][c];
+                    for (int q = 0; q < 8; q++) Tt[q] = sTt[q];
+                    pose_pass(Tt, cam, sobs, outl, schi, n, robust, tacc2);
+                    EV(1);
+                    pose_reduce28_w0(tacc2, red[rb], evp());
+                    rb ^= 1;
+                }
 #pragma unroll
-                for (int r = 0; r < 6; r++) acc[21 + r] -= rho1 * (J[0][r] * om[0] + J[1][r] * om[1] + J[2][r] * om[2]);
+                for (int q = 0; q < 8; q++) T[q] = sTt[q];
             }
-            pose_reduce<28>(acc, red);
-            const double* H = acc;        // upper 6x6, row by row
-            const double* bvec = acc + 21;
-            double currentChi = acc[27];
-            const double iniChi = currentChi;
-            if (i == 0) {  // computeLambdaInit, tau = 1e-5
-                const int dq[6] = {0, 6, 11, 15, 18, 20};
-                double m = 0;
-#pragma unroll
-                for (int j = 0; j < 6; j++) m = fmax(m, fabs(H[dq[j]]));
-                lambda = 1e-5 * m;
-                ni = 2;
-                nbadIt = 0;
-            }
-            double rho = 0;
-            int qmax = 0;
-            do {
-                double xv[6];
-                const bool ok2 = pose_solve6(H, bvec, lambda, xv);
-                double Tt[8];
-                if (ok2) se3_oplus(xv, T, Tt);
-                else {
-#pragma unroll
-                    for (int q = 0; q < 8; q++) Tt[q] = T[q];
-#pragma unroll
-                    for (int q = 0; q < 6; q++) xv[q] = 0;
-                }
-                double tc[1] = {0};
-                for (int k = tid; k < n; k += kPoseThreads) {
-                    if (outl[k]) continue;
-                    const orbmi_pose_obs o = O[k];
-                    double e[3];
-                    pose_error(Tt, cam, o, e);
-                    err[k][0] = e[0]; err[k][1] = e[1]; err[k][2] = e[2];
-                    const double c2 = pose_chi2(o, e);
-                    double rho0 = c2;
-                    if (robust) {
-                        const double d = pose_delta(o), dsqr = d * d;
-                        if (c2 > dsqr) rho0 = 2 * sqrt(c2) * d - dsqr;
-                    }
-                    tc[0] += rho0;
-                }
-                pose_reduce<1>(tc, reinterpret_cast<double(*)[1]>(&red[0][0]));
-                const double tempChi = ok2 ? tc[0] : DBL_MAX;
-                double scale = 0;
-#pragma unroll
-                for (int j = 0; j < 6; j++) scale += xv[j] * (lambda * xv[j] + bvec[j]);
-                rho = (currentChi - tempChi) / (scale + 1e-3);
-                if (rho > 0 && isfinite(tempChi)) {
-                    double alpha = 1. - pow(2 * rho - 1, 3);
-                    alpha = fmin(alpha, 2. / 3.);
-                    lambda *= fmax(1. / 3., alpha);
-                    ni = 2;
-                    currentChi = tempChi;
-#pragma unroll
-                    for (int q = 0; q < 8; q++) T[q] = Tt[q];
-                } else {
-                    lambda *= ni;
-                    ni *= 2;
-                }
-                qmax++;
-            } while (rho < 0 && qmax < 10);
-            iters++;
-            if (qmax == 10 || rho == 0) break;
-            if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
-            else nbadIt = 0;
-            if (nbadIt >= 3) break;
         }
         // ---- outlier classification (:418-466): stale errors of the inliers, fresh ones of the
         // outliers, chi2 compared in float
-        int bad = 0;
+        double bad = 0;
         for (int k = tid; k < n; k += kPoseThreads) {
-            const orbmi_pose_obs o = O[k];
-            double e[3] = {err[k][0], err[k][1], err[k][2]};
+            const orbmi_pose_obs o = sobs[k];
+            float c2 = schi[k];
             if (outl[k]) {
-                pose_error(T, cam, o, e);
-                err[k][0] = e[0]; err[k][1] = e[1]; err[k][2] = e[2];
+                double p[3], invz, e[3];
+                pose_error(T, cam, o, p, invz, e);
+                c2 = (float)pose_chi2(o, e);
+                schi[k] = c2;
             }
-            const float c2 = (float)pose_chi2(o, e);
             const bool out = c2 > (o.ur < 0 ? 5.991f : 7.815f);
             outl[k] = out;
             bad += out;
         }
-        nBad = pose_reduce_int(bad, redi);
+        nBad = (int)pose_reduce1(bad, red1[rb]);
+        rb ^= 1;
         if (n < 10) break;  // optimizer.edges().size() < 10
     }
     for (int k = tid; k < n; k += kPoseThreads) put_flag(k, outl[k]);
@@ -333,7 +496,14 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         F.inliers = n - nBad;
         F.iterations = iters;
     }
+    if (TR && tid == 0) {
+        trace[0] = __builtin_amdgcn_s_memtime() - tstart;
+        trace[1] = __builtin_amdgcn_s_memrealtime() - rstart;
+        trace[2] = seq;
+    }
+#undef EV
 }
+
 
 // Edge assembly of PoseOptimization (src/Optimizer.cc:296-375): one edge per keypoint holding a
 // map point, compacted in keypoint order (workgroup scan), plus the frame record.  The map
@@ -504,7 +674,8 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     if (dev != is_device_ptr(obs) && nobs) return ORBMI_E_ARG;
     if (nobs && dev != is_device_ptr(outlier)) return ORBMI_E_ARG;
     if (dev) {
-        hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0);
+        hipLaunchKernelGGL(k_pose_opt<false>, dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0,
+                           nullptr);
         ORBMI_HIP(hipGetLastError());
         return ORBMI_OK;
     }
@@ -527,7 +698,7 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     uint8_t* dFl = h->d_buf + ((fb + 255) & ~(size_t)255) + ((ob + 255) & ~(size_t)255);
     ORBMI_HIP(hipMemcpyAsync(dF, frames, fb, hipMemcpyHostToDevice, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(dO, obs, ob, hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(k_pose_opt, dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl, 0);
+    hipLaunchKernelGGL(k_pose_opt<false>, dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl, 0, nullptr);
     ORBMI_HIP(hipGetLastError());
     ORBMI_HIP(hipMemcpyAsync(frames, dF, fb, hipMemcpyDeviceToHost, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(outlier, dFl, nobs, hipMemcpyDeviceToHost, h->stream));
@@ -606,8 +777,8 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     if (rc) return rc;
     hipLaunchKernelGGL(k_pose_gather, dim3(1), dim3(kGatherThreads), 0, h->stream, a);
     ORBMI_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_pose_opt, dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec, (const orbmi_pose_obs*)h->d_obs,
-                       a.outlier, 1);
+    hipLaunchKernelGGL(k_pose_opt<false>, dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec,
+                       (const orbmi_pose_obs*)h->d_obs, a.outlier, 1, nullptr);
     ORBMI_HIP(hipGetLastError());
     if (async) return ORBMI_OK;
     if (!is_device_ptr(rec))
@@ -618,6 +789,25 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     h->used_stage = 0;
     if (rec->inliers < 0) return ORBMI_E_UNSUPPORTED;  // more than kPoseMaxObs edges
     return ORBMI_OK;
+}
+
+// debug: one traced launch of the pose kernel on device arrays (include/orbmi_debug.h)
+int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_pose_obs* obs, uint8_t* outlier,
+                           unsigned long long* trace) {
+    using namespace orbmi;
+    if (!h || !frames || !obs || !outlier || !trace) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(h->device));
+    unsigned long long* d_tr = nullptr;
+    ORBMI_HIP(hipMalloc((void**)&d_tr, kPoseTraceWords * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d_tr, 0, kPoseTraceWords * sizeof(unsigned long long), h->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_pose_opt<true>, dim3(1), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0, d_tr);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(trace, d_tr, kPoseTraceWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(d_tr);
+    return e == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 
 }  // extern "C"

@@ -6,13 +6,34 @@
 
 namespace orbmi {
 
+// ---------------------------------------------------------------- fp64 latency helpers
+// 1/x and 1/sqrt(x) from v_rcp_f64 / v_rsq_f64 with Newton steps: within an ulp or two of the
+// IEEE quotient / root at a third of their dependent latency (gfx950: div 76, sqrt 111, rcp 17
+// cycles; tools/ubench/lat.hip).  Used where the parity tolerance is 1e-4 (poses, BA).
+__device__ inline double fast_rcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
+__device__ inline double fast_rsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    double e = fma(-hx * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-hx * y, y, 0.5);
+    return fma(y, e, y);
+}
+
 // ---------------------------------------------------------------- SE3Quat helpers (fp64)
 struct Q { double x, y, z, w; };
 
 __device__ inline void q_normalize(Q& q) {
     if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
-    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-    q.x /= n; q.y /= n; q.z /= n; q.w /= n;
+    const double inv = fast_rsqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x *= inv; q.y *= inv; q.z *= inv; q.w *= inv;
 }
 
 // Eigen::Quaternion(const Matrix3&): the largest-diagonal branch spelled out per pivot so that
@@ -76,29 +97,50 @@ __device__ inline void se3_map(const double* T, const double* p, double o[3]) {
     o[0] += T[4]; o[1] += T[5]; o[2] += T[6];
 }
 
-// T <- exp(u) * T   (VertexSE3Expmap::oplusImpl, SE3Quat::exp / operator*)
+// sin and cos of a small angle (|x| <= 0.1): Taylor to x^11 / x^12, below 1e-22 truncation
+__device__ inline void sincos_small(double x, double& s, double& c) {
+    const double x2 = x * x;
+    s = x * (1.0 + x2 * (-1.0 / 6 + x2 * (1.0 / 120 + x2 * (-1.0 / 5040 + x2 * (1.0 / 362880 + x2 * (-1.0 / 39916800))))));
+    c = 1.0 + x2 * (-0.5 + x2 * (1.0 / 24 + x2 * (-1.0 / 720 + x2 * (1.0 / 40320 + x2 * (-1.0 / 3628800 + x2 * (1.0 / 479001600))))));
+}
+
+// T <- exp(u) * T   (VertexSE3Expmap::oplusImpl, SE3Quat::exp / operator*; se3quat.h:223-257).
+// For theta >= 1e-5 the exponential is formed in quaternion form: Quaterniond(R) of
+// R = I + sin(t)/t Omega + (1-cos t)/t^2 Omega^2 is (sin(t/2)/t * omega, cos(t/2)) exactly, and
+// V * upsilon = upsilon + b omega x upsilon + c omega x (omega x upsilon) with
+// b = (1-cos t)/t^2 = 2 sin^2(t/2)/t^2, c = (t - sin t)/t^3; equal to the matrix form up to
+// rounding.  Below 1e-5 the reference's non-orthonormal R = I + Omega + Omega^2 (V = R) is kept.
 __device__ inline void se3_oplus(const double* u, const double* Tin, double* Tout) {
     const double w0 = u[0], w1 = u[1], w2 = u[2];
-    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-    const double O[3][3] = {{0, -w2, w1}, {w2, 0, -w0}, {-w1, w0, 0}};
-    double O2[3][3], R[3][3], V[3][3];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
-    if (theta < 0.00001) {
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) { R[i][j] = (i == j) + O[i][j] + O2[i][j]; V[i][j] = R[i][j]; }
-    } else {
-        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / (theta * theta * theta);
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-                R[i][j] = (i == j) + a * O[i][j] + b * O2[i][j];
-                V[i][j] = (i == j) + b * O[i][j] + c * O2[i][j];
-            }
-    }
-    Q qe = q_from_matrix(R);
+    const double n2 = w0 * w0 + w1 * w1 + w2 * w2;
+    Q qe;
     double te[3];
-    for (int i = 0; i < 3; i++) te[i] = V[i][0] * u[3] + V[i][1] * u[4] + V[i][2] * u[5];
+    if (n2 < 1e-10) {  // theta < 0.00001
+        const double O[3][3] = {{0, -w2, w1}, {w2, 0, -w0}, {-w1, w0, 0}};
+        double R[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++)
+                R[i][j] = (i == j) + O[i][j] + (O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j]);
+        qe = q_from_matrix(R);
+        for (int i = 0; i < 3; i++) te[i] = R[i][0] * u[3] + R[i][1] * u[4] + R[i][2] * u[5];
+    } else {
+        const double it = fast_rsqrt(n2), theta = n2 * it, it2 = it * it;
+        double sh, ch;  // sin, cos of theta / 2
+        const double h = 0.5 * theta;
+        if (h <= 0.1) sincos_small(h, sh, ch);
+        else sincos(h, &sh, &ch);
+        const double k = sh * it;
+        qe = Q{k * w0, k * w1, k * w2, ch};
+        const double st = 2 * sh * ch;                  // sin(theta)
+        const double b = 2 * sh * sh * it2;             // (1 - cos theta) / theta^2
+        const double c = (theta - st) * (it2 * it);     // (theta - sin theta) / theta^3
+        const double v0 = u[3], v1 = u[4], v2 = u[5];
+        const double a0 = w1 * v2 - w2 * v1, a1 = w2 * v0 - w0 * v2, a2 = w0 * v1 - w1 * v0;  // omega x v
+        const double c0 = w1 * a2 - w2 * a1, c1 = w2 * a0 - w0 * a2, c2 = w0 * a1 - w1 * a0;  // omega x a
+        te[0] = v0 + b * a0 + c * c0;
+        te[1] = v1 + b * a1 + c * c1;
+        te[2] = v2 + b * a2 + c * c2;
+    }
     q_normalize(qe);
     const Q qb = load_q(Tin);
     const double tb[3] = {Tin[4], Tin[5], Tin[6]};

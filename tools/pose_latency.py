@@ -1,5 +1,6 @@
-"""Latency of one PoseOptimization launch (k_pose_gather + k_pose_opt via the device path) for
-the Track stages' edge counts; run under rocprofv3 --kernel-trace --stats for per-kernel time."""
+"""Latency of one PoseOptimization launch (k_pose_opt via the device path) for the Track stages'
+edge counts, plus the per-wave event timeline of the traced variant (orbmi_debug_pose_trace);
+run under rocprofv3 --kernel-trace --stats for per-kernel time."""
 import sys
 import time
 
@@ -8,7 +9,10 @@ import torch
 
 sys.path.insert(0, ".")
 from orb_slam2_with_comment_amd import synth_map as SM  # noqa: E402
+from orb_slam2_with_comment_amd._capi import lib  # noqa: E402
 from orb_slam2_with_comment_amd.optimizer import PoseOptimizer  # noqa: E402
+
+SEQS, WAVES = 64, 8
 
 po = PoseOptimizer(0)
 for n in (420, 680):
@@ -29,4 +33,35 @@ for n in (420, 680):
     res = d_fr.cpu().numpy().view(fr.dtype)
     print(f"n_obs={n}: {dt * 1e6:.1f} us per synchronous launch, iterations={res[0]['iterations']}, "
           f"inliers={res[0]['inliers']}", flush=True)
+    tr = np.zeros(16 + SEQS * WAVES * 8, np.uint64)
+    d_fr.copy_(d_fr0)
+    torch.cuda.synchronize()
+    rc = lib().orbmi_debug_pose_trace(po._h, d_fr.data_ptr(), d_ob.data_ptr(), d_out.data_ptr(), tr.ctypes.data)
+    assert rc == 0, rc
+    tot, real, nseq = int(tr[0]), int(tr[1]), int(tr[2])
+    print(f"  traced: {real / 100.0:.1f} us, {tot} cycles ({tot / (real / 100.0):.0f} MHz), {nseq} passes", flush=True)
+    ev = tr[16:].reshape(SEQS, WAVES, 8).astype(np.int64)
+    # per pass: duration of each wave's pass, barrier wait, wave-0 phases (cycles)
+    sums = {"pass(max wave)": [], "pass(wave0)": [], "rs(wave0)": [], "B wait(wave0)": [], "gather(wave0)": [],
+            "lm(wave0)": [], "solve+oplus(wave0)": [], "A wait(others)": []}
+    for s in range(min(nseq, SEQS) - 1):
+        e = ev[s]
+        act = [w for w in range(WAVES) if e[w, 0] and e[w, 1]]
+        if 0 not in act:
+            continue
+        sums["pass(max wave)"].append(max(e[w, 1] - e[w, 0] for w in act))
+        sums["pass(wave0)"].append(e[0, 1] - e[0, 0])
+        sums["rs(wave0)"].append(e[0, 2] - e[0, 1])
+        sums["B wait(wave0)"].append(e[0, 3] - e[0, 2])
+        sums["gather(wave0)"].append(e[0, 4] - e[0, 3])
+        if e[0, 5]:
+            sums["lm(wave0)"].append(e[0, 5] - e[0, 4])
+        if e[0, 6] and e[0, 5]:
+            sums["solve+oplus(wave0)"].append(e[0, 6] - e[0, 5])
+        nxt = ev[s + 1]
+        if nxt[1, 0] and e[1, 3]:
+            sums["A wait(others)"].append(nxt[1, 0] - e[1, 3])
+    for k, v in sums.items():
+        if v:
+            print(f"    {k:22s} mean {np.mean(v):8.0f} cycles  (n={len(v)})", flush=True)
 po.close()
