@@ -91,7 +91,7 @@ def setup_track(a, rank, local):
     cam = synth.KITTI
     F = a.frames
     seq = [synth.stereo_pair(cam, f, seed_base=1000 * (rank + 1)) for f in range(F + 2)]
-    tr = StereoTracker(cam, a.nfeatures, device=local)
+    tr = StereoTracker(cam, a.nfeatures, device=local, pipelined=True)
     sf = tr.scale_factors
     # per-frame features through the host API (bit-exact with the oracle, tests/); stereo needs
     # both pyramids resident, so the right images go through a second extractor
@@ -160,7 +160,8 @@ def run_track(a, rank, world, local, dist):
     problem, _ = SM.local_ba_problem(seed=42)
     mapper = LocalMapper(local)
     xmatch = torch.full((tr.cap,), -1, dtype=torch.int32, device=tr.kps.device)
-    ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)
+    ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)        # extraction (E)
+    trk = torch.cuda.ExternalStream(tr.track_stream_handle, device=tr.kps.device)  # tracking (T)
 
     def step(i):
         f = 2 + i % F
@@ -168,9 +169,9 @@ def run_track(a, rank, world, local, dist):
                  S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
         if dist is not None:  # config 4: exchange left features, match against the other streams
             cur = torch.cuda.current_stream()
-            cur.wait_stream(ext)
+            cur.wait_stream(trk)  # T already waits for this frame's extraction
             g_desc, g_kps, g_cnt = gather_stream_features(dist, tr.desc[0], tr.kps[0], tr.counts[:1])
-            ext.wait_stream(cur)
+            trk.wait_stream(cur)
             match_cross_stream(tr.matcher._h, tr.desc.data_ptr(), tr.cap, tr.counts.data_ptr(), g_desc,
                                g_cnt.view(-1), rank, xmatch)
             S["_g"] = (g_desc, g_kps, g_cnt)  # keep alive until the stream has consumed them
@@ -206,15 +207,26 @@ def run_track(a, rank, world, local, dist):
         ev[0].record(ext)
         tr.extract_stereo(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols)
         ev[1].record(ext)
+        trk.wait_event(ev[1])
         tr.track_with_motion_model(S["tcws"][f], S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr())
-        ev[2].record(ext)
+        ev[2].record(trk)
         tr.track_local_map(S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(),
                            S["n_mp"][f])
-        ev[3].record(ext)
+        ev[3].record(trk)
         tr.synchronize()
         for k, name in enumerate(phases):
             phases[name] += ev[k].elapsed_time(ev[k + 1]) / n_tr
     track_only_ms = (time.perf_counter() - t0) / n_tr * 1e3  # includes a host sync per frame
+    # tracking alone, back to back (no LocalBA): host enqueue time vs GPU-bound time per frame
+    tr.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_tr):
+        f = 2 + i % F
+        tr.track(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols, S["tcws"][f], S["lf_views"][f - 1],
+                 S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
+    enqueue_ms = (time.perf_counter() - t0) / n_tr * 1e3
+    tr.synchronize()
+    track_async_ms = (time.perf_counter() - t0) / n_tr * 1e3
     outcome = tr.results()
     nm_lf = int((tr.match_lf[:int(tr.counts[0])] >= 0).sum())
     nm_mp = int((tr.match_mp[:int(tr.counts[0])] >= 0).sum())
@@ -270,6 +282,8 @@ def run_track(a, rank, world, local, dist):
                                   "tracking_ok": outcome["ok"]},
             "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},
             "track_only_ms_per_frame_synced": round(track_only_ms, 4),
+            "track_only_ms_per_frame_back_to_back": round(track_async_ms, 4),
+            "host_enqueue_ms_per_frame": round(enqueue_ms, 4),
             "local_ba": {"ms_per_call_idle_gpu": round(lba_ms, 3), "calls_in_timed_region": n_lba,
                          "iterations": list(lba_info["iterations"]) if lba_info else None,
                          "edges": int(len(problem.edges)), "points": int(len(problem.pts)),
@@ -440,7 +454,7 @@ def run_extract(a, rank, world, local, dist):
     rows, cols = cam.height, cam.width
     frames = [synth.stereo_pair(cam, f, seed_base=1000 * (rank + 1))[:2] for f in range(a.frames)]
     imgs = torch.from_numpy(np.stack([np.stack(p) for p in frames])).cuda()
-    tr = StereoTracker(cam, a.nfeatures, device=local)
+    tr = StereoTracker(cam, a.nfeatures, device=local, pipelined=True)
     img_bytes = rows * cols
 
     def step(i):

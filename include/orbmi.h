@@ -155,6 +155,8 @@ void orbmi_matcher_destroy(orbmi_matcher* m);
  * extraction): calls are then ordered behind it without host synchronisation, and a call whose
  * outputs are all device pointers with nmatches == NULL returns without waiting. */
 int orbmi_matcher_share_stream(orbmi_matcher* m, orbmi_extractor* ex);
+/* The handle's HIP stream (hipStream_t): its own, or the extractor's after share_stream. */
+int orbmi_matcher_get_stream(orbmi_matcher* m, void** stream);
 
 /* Frame::isInFrustum(pMP, viewingCosLimit) for n_mp points (src/Frame.cc:274-342) with
  * MapPoint::PredictScale (src/MapPoint.cc:421-436).  Points flagged BAD or SEEN are skipped
@@ -319,6 +321,9 @@ int orbmi_pose_synchronize(orbmi_pose* h);
 /* Run the handle on `ex`'s stream (like orbmi_matcher_share_stream): a tracked frame's
  * extraction, searches and pose optimisations are then ordered without host round trips. */
 int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex);
+/* Run the handle on the matcher's stream instead: the tracking stages (searches, pose
+ * optimisations) then form one stream that can run beside the next frame's extraction. */
+int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m);
 
 /* Frame::mvpMapPoints of the frame being tracked, as the matchers left it: keypoint i holds
  * local map point mps[match_mp[i]] when match_mp && match_mp[i] >= 0, otherwise last-frame

@@ -60,6 +60,7 @@ _PROTOS = {
     "orbmi_matcher_create": (_i, [_i, C.POINTER(_vp)]),
     "orbmi_matcher_destroy": (None, [_vp]),
     "orbmi_matcher_share_stream": (_i, [_vp, _vp]),
+    "orbmi_matcher_get_stream": (_i, [_vp, C.POINTER(_vp)]),
     "orbmi_match_descriptors_segments": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _i, _i, _f, _vp, _vp]),
     "orbmi_extractor_get_stream": (_i, [_vp, C.POINTER(_vp)]),
     "orbmi_is_in_frustum": (_i, [_vp, _vp, _vp, _i, _f, _vp]),
@@ -75,6 +76,7 @@ _PROTOS = {
     "orbmi_pose_optimization": (_i, [_vp, _vp, _i, _vp, _i, _vp]),
     "orbmi_pose_synchronize": (_i, [_vp]),
     "orbmi_pose_share_stream": (_i, [_vp, _vp]),
+    "orbmi_pose_share_matcher_stream": (_i, [_vp, _vp]),
     "orbmi_pose_optimization_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_search_by_projection_last_frame_if": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _i]),
     "orbmi_track_update_matches": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp]),

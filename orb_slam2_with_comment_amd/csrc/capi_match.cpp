@@ -199,6 +199,12 @@ int orbmi_matcher_share_stream(orbmi_matcher* h, orbmi_extractor* ex) {
     return ORBMI_OK;
 }
 
+int orbmi_matcher_get_stream(orbmi_matcher* h, void** stream) {
+    if (!h || !stream) return ORBMI_E_ARG;
+    *stream = (void*)h->m.stream;
+    return ORBMI_OK;
+}
+
 void orbmi_matcher_destroy(orbmi_matcher* h) {
     if (!h) return;
     h->m.release();
@@ -267,8 +273,8 @@ int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const
     if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, 0.5f, d_tr, m.d_scalars + 1))) return rc;
     if ((rc = orbmi::launch_local_search(m, F, d_occ, d_mps, d_tr, n_mp, th, 0.8f, d_out, m.d_scalars))) return rc;
     ORBMI_HIP(hipGetLastError());
-    int ntm = 0;
-    rc = finish(m, outs, m.d_scalars, nmatches, m.d_scalars + 1, &ntm);
+    int ntm = 0;  // read back (and waited for) only when the caller asks for it
+    rc = finish(m, outs, m.d_scalars, nmatches, m.d_scalars + 1, n_to_match ? &ntm : nullptr);
     if (n_to_match) *n_to_match = ntm;
     return rc;
 }

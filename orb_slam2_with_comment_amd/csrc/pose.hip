@@ -658,6 +658,18 @@ int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex) {
     return ORBMI_OK;
 }
 
+int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m) {
+    if (!h || !m) return ORBMI_E_ARG;
+    void* sv = nullptr;
+    if (orbmi_matcher_get_stream(m, &sv) != ORBMI_OK || !sv) return ORBMI_E_STATE;
+    ORBMI_HIP(hipSetDevice(h->device));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) ORBMI_HIP(hipStreamDestroy(h->stream));
+    h->stream = (hipStream_t)sv;
+    h->own_stream = false;
+    return ORBMI_OK;
+}
+
 int orbmi_pose_synchronize(orbmi_pose* h) {
     if (!h) return ORBMI_E_ARG;
     ORBMI_HIP(hipStreamSynchronize(h->stream));

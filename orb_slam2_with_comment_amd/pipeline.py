@@ -14,11 +14,13 @@ One tracked stereo frame, in the order Tracking runs it (src/Tracking.cc:287-581
   LocalMapping thread Optimizer::LocalBundleAdjustment on every new keyframe
                       (src/LocalMapping.cc:89-90), concurrently with tracking
 
-All tracking stages run on ONE HIP stream (the extractor's; the matcher and the pose optimiser
-share it), with inputs and outputs in HBM, keypoint counts read on the device
-(orbmi_frame_view.n_device) and the optimised pose read by the next search from its device
-record (orbmi_frame_view.tcw in device memory), so a frame is enqueued without a host round
-trip.  Local BA runs on its own stream from a worker thread (the LocalMapping thread),
+The tracking stages run on one HIP stream (the matcher's; the pose optimiser shares it) and the
+Frame constructor's extraction on the extractor's stream, double-buffered, so that the next
+frame's extraction overlaps this frame's tracking (StereoTracker(pipelined=True); with
+pipelined=False everything shares the extractor's stream).  Inputs and outputs stay in HBM,
+keypoint counts are read on the device (orbmi_frame_view.n_device) and the optimised pose is
+read by the next search from its device record (orbmi_frame_view.tcw in device memory), so a
+frame is enqueued without a host round trip.  Local BA runs on its own stream from a worker thread (the LocalMapping thread),
 overlapping tracking as in the reference.
 """
 from __future__ import annotations
@@ -58,33 +60,58 @@ def frame_view(n, keys, u_right, desc, tcw, cam, scale_factors, width, height, n
 
 
 class StereoTracker:
-    """Tracking-thread GPU work for one stereo stream (one GPU)."""
+    """Tracking-thread GPU work for one stereo stream (one GPU).
 
-    def __init__(self, cam, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, device=0):
+    pipelined=False: extraction, searches and pose optimisations run on ONE stream (the
+    extractor's).  pipelined=True: the Frame constructor's work (extraction + stereo) runs on the
+    extractor's stream E and the tracking stages on the matcher's stream T, with the frame
+    buffers double-buffered in two slots, so frame k+1's extraction overlaps frame k's tracking
+    (it depends only on the image; the reference builds the Frame before Track() too,
+    src/Tracking.cc:168-205).  Frame k's tracking waits for its own extraction (event), and
+    frame k+2's extraction for frame k's tracking to release the slot."""
+
+    def __init__(self, cam, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, device=0,
+                 pipelined=False):
         import torch
         from .matcher import ORBmatcher
         from .optimizer import PoseOptimizer
         from .orb import ORBextractor
         from .types import POSE_FRAME_DTYPE
-        self.cam, self.device = cam, device
+        self.cam, self.device, self.pipelined = cam, device, pipelined
         self.extractor = ORBextractor(nfeatures, scale_factor, nlevels, ini_th, min_th, device=device)
         self.matcher = ORBmatcher(device=device)
-        check("orbmi_matcher_share_stream", lib().orbmi_matcher_share_stream(self.matcher._h, self.extractor.handle))
         self.pose = PoseOptimizer(device)
-        self.pose.share_stream(self.extractor.handle)
+        L = lib()
+        if pipelined:
+            check("orbmi_pose_share_matcher_stream", L.orbmi_pose_share_matcher_stream(self.pose._h, self.matcher._h))
+        else:
+            check("orbmi_matcher_share_stream", L.orbmi_matcher_share_stream(self.matcher._h, self.extractor.handle))
+            self.pose.share_stream(self.extractor.handle)
         self.inv_sigma2 = np.ascontiguousarray(self.extractor.GetInverseScaleSigmaSquares(), np.float32)
         s = _vp()
-        check("orbmi_extractor_get_stream", lib().orbmi_extractor_get_stream(self.extractor.handle, C.byref(s)))
-        self.stream_handle = s.value
+        check("orbmi_extractor_get_stream", L.orbmi_extractor_get_stream(self.extractor.handle, C.byref(s)))
+        self.stream_handle = s.value  # extraction stream E
+        t = _vp()
+        check("orbmi_matcher_get_stream", L.orbmi_matcher_get_stream(self.matcher._h, C.byref(t)))
+        self.track_stream_handle = t.value  # tracking stream T (== E unless pipelined)
         self.scale_factors = self.extractor.GetScaleFactors()
         self.cap = cap = nfeatures + 64
         dev = torch.device("cuda", device)
-        # outputs of the current frame (item 0 = left, 1 = right)
-        self.kps = torch.zeros((2, cap, 7), dtype=torch.int32, device=dev)
-        self.desc = torch.zeros((2, cap, 32), dtype=torch.uint8, device=dev)
-        self.counts = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.u_right = torch.zeros((2, cap), dtype=torch.float32, device=dev)
-        self.depth = torch.zeros((2, cap), dtype=torch.float32, device=dev)
+        nslots = 2 if pipelined else 1
+        # per slot: outputs of a frame's extraction (item 0 = left, 1 = right)
+        self.slots = [dict(kps=torch.zeros((2, cap, 7), dtype=torch.int32, device=dev),
+                           desc=torch.zeros((2, cap, 32), dtype=torch.uint8, device=dev),
+                           counts=torch.zeros(2, dtype=torch.int32, device=dev),
+                           u_right=torch.zeros((2, cap), dtype=torch.float32, device=dev),
+                           depth=torch.zeros((2, cap), dtype=torch.float32, device=dev)) for _ in range(nslots)]
+        self.slot = 0        # slot of the frame tracked last (the kps/desc/... properties)
+        self._next = 0       # slot of the next frame
+        if pipelined:
+            self._E = torch.cuda.ExternalStream(self.stream_handle, device=dev)
+            self._T = torch.cuda.ExternalStream(self.track_stream_handle, device=dev)
+            self._ev_extracted = [torch.cuda.Event() for _ in range(nslots)]
+            self._ev_tracked = [torch.cuda.Event() for _ in range(nslots)]
+            self._pending = [False] * nslots
         self.occupied = torch.zeros(cap, dtype=torch.uint8, device=dev)   # after the motion-model stage
         self.no_points = torch.zeros(cap, dtype=torch.uint8, device=dev)  # fill(mvpMapPoints, NULL)
         self.match_lf = torch.full((cap,), -1, dtype=torch.int32, device=dev)
@@ -97,31 +124,41 @@ class StereoTracker:
         self.tcounts = torch.zeros(8, dtype=torch.int32, device=dev)
         self._views = {}
 
+    # the frame tracked last (its slot's buffers)
+    kps = property(lambda self: self.slots[self.slot]["kps"])
+    desc = property(lambda self: self.slots[self.slot]["desc"])
+    counts = property(lambda self: self.slots[self.slot]["counts"])
+    u_right = property(lambda self: self.slots[self.slot]["u_right"])
+    depth = property(lambda self: self.slots[self.slot]["depth"])
+
     def rec_tcw(self, k):
         """Device address of pose record k's tcw (its first field)."""
         return self.recs.data_ptr() + k * self.rec_bytes
 
     def current_view(self, tcw):
-        """Frame view of the frame being tracked (device arrays, device count); tcw = host
-        numpy pose or the device address of a pose record."""
-        key = tcw if isinstance(tcw, int) else tcw.ctypes.data
+        """Frame view of the frame being tracked (its slot's device arrays, device count); tcw =
+        host numpy pose or the device address of a pose record."""
+        key = (self.slot, tcw if isinstance(tcw, int) else tcw.ctypes.data)
         v = self._views.get(key)
         if v is None:
-            v = frame_view(self.cap, self.kps.data_ptr(), self.u_right.data_ptr(), self.desc.data_ptr(), tcw,
+            sl = self.slots[self.slot]
+            v = frame_view(self.cap, sl["kps"].data_ptr(), sl["u_right"].data_ptr(), sl["desc"].data_ptr(), tcw,
                            self.cam, self.scale_factors, self.cam.width, self.cam.height,
-                           n_device=self.counts.data_ptr())
+                           n_device=sl["counts"].data_ptr())
             self._views[key] = v
         return v
 
-    def extract_stereo(self, d_left_right: int, rows: int, cols: int):
-        """ORBextractor(left) + ORBextractor(right) as one batch + ComputeStereoMatches;
-        d_left_right = device address of the 2 x rows x cols u8 image pair."""
+    def extract_stereo(self, d_left_right: int, rows: int, cols: int, slot=None):
+        """ORBextractor(left) + ORBextractor(right) as one batch + ComputeStereoMatches into
+        `slot` (default: the current one) on the extraction stream; d_left_right = device address
+        of the 2 x rows x cols u8 image pair."""
         L = lib()
+        sl = self.slots[self.slot if slot is None else slot]
         check("orbmi_extract_batch_device", L.orbmi_extract_batch_device(
-            self.extractor.handle, _vp(d_left_right), 2, rows, cols, cols, rows * cols, _vp(self.kps.data_ptr()),
-            _vp(self.desc.data_ptr()), _vp(self.counts.data_ptr()), self.cap))
+            self.extractor.handle, _vp(d_left_right), 2, rows, cols, cols, rows * cols, _vp(sl["kps"].data_ptr()),
+            _vp(sl["desc"].data_ptr()), _vp(sl["counts"].data_ptr()), self.cap))
         check("orbmi_compute_stereo_matches_batch_device", L.orbmi_compute_stereo_matches_batch_device(
-            self.extractor.handle, self.cam.bf, self.cam.fx, _vp(self.u_right.data_ptr()), _vp(self.depth.data_ptr())))
+            self.extractor.handle, self.cam.bf, self.cam.fx, _vp(sl["u_right"].data_ptr()), _vp(sl["depth"].data_ptr())))
 
     def search_last_frame(self, tcw, last_view, last_points, th=7.0):
         """ORBmatcher(0.9, true).SearchByProjection(mCurrentFrame, mLastFrame, th, !stereo)
@@ -181,9 +218,23 @@ class StereoTracker:
         """Enqueue one tracked stereo frame (Frame ctor + TrackWithMotionModel + TrackLocalMap);
         results stay on the device: self.match_lf / match_mp (final mvpMapPoints), self.outlier,
         pose records self.recs, counts self.tcounts (see results())."""
-        self.extract_stereo(d_left_right, rows, cols)
+        if not self.pipelined:
+            self.extract_stereo(d_left_right, rows, cols)
+            self.track_with_motion_model(tcw, last_view, last_points, th_lf)
+            self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
+            return
+        s = self._next
+        self._next ^= 1
+        if self._pending[s]:  # the slot's previous frame must be tracked before it is overwritten
+            self._E.wait_event(self._ev_tracked[s])
+        self.extract_stereo(d_left_right, rows, cols, slot=s)
+        self._ev_extracted[s].record(self._E)
+        self._T.wait_event(self._ev_extracted[s])
+        self.slot = s
         self.track_with_motion_model(tcw, last_view, last_points, th_lf)
         self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
+        self._ev_tracked[s].record(self._T)
+        self._pending[s] = True
 
     def results(self):
         """Synchronise and read the frame's tracking outcome: ok follows the reference's return
@@ -200,6 +251,8 @@ class StereoTracker:
 
     def synchronize(self):
         check("orbmi_extractor_synchronize", lib().orbmi_extractor_synchronize(self.extractor.handle))
+        if self.pipelined:
+            self._T.synchronize()
 
     def close(self):
         self.pose.close()
