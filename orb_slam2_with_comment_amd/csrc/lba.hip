@@ -30,6 +30,7 @@
 
 #include "extractor.h"
 #include "se3_device.h"
+#include "wave_ops.h"
 
 // fp64 solver with a 1e-4 parity tolerance: multiply-add contraction allowed here (the
 // bit-exact extractor / matcher sources keep -ffp-contract=off)
@@ -496,15 +497,20 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
 // one block per pose pair (i <= j): H_schur(i,j) = [Hpp_i + lambda I] - sum_points
 // B_i D^-1 B_j^T with D^-1 recomputed per observation pair; the diagonal block also writes
 // b_schur(i) = b_p - sum B D^-1 b_l.  lam < 0: lambda = 1e-5 max|diag H| (every block reduces
-// the same partials in the same order; block 0 publishes it in scal[3]).
-__global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a) {
+// the same partials in the same order; block 0 publishes it in scal[3]).  512 threads (two
+// waves per SIMD hide the dependent loads of a pair); the 36 block sums are reduced per wave
+// by DPP / permlane reduce-scatter (wave_ops.h) and across waves in wave order.
+constexpr int kSchurThreads = 512;
+constexpr int kSchurWaves = kSchurThreads / 64;
+
+__global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     const BaCtl& ctl = *a.ctl;
     if (ctl.done) return;
     const int N = 6 * ctl.np, nmax = a.nb_p + ctl.np;
     const double* part_max = a.part_max;
     // lambda: computeLambdaInit on the first trial of iteration 0, the LM state otherwise
     double lam = (ctl.it == 0 && ctl.trial == 0) ? -1.0 : ctl.lambda;
-    __shared__ double red[kBaBlock / 64][36];
+    __shared__ double red[kSchurWaves][36];
     __shared__ double lam_s;
     if (lam < 0) {
         if (threadIdx.x == 0) {
@@ -537,14 +543,13 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a) {
         }
 #pragma unroll
         for (int q = 0; q < 6; q++) {
-            double x = bacc[q];
-            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            const double x = wave_sum(bacc[q]);
             if (lane == 0) red[wid][q] = x;
         }
         __syncthreads();
         if (threadIdx.x < 6) {
             double t = 0;
-            for (int w = 0; w < kBaBlock / 64; w++) t += red[w][threadIdx.x];
+            for (int w = 0; w < kSchurWaves; w++) t += red[w][threadIdx.x];
             a.bs[6 * i1 + threadIdx.x] = a.bp[6 * i1 + threadIdx.x] - t;
         }
         return;
@@ -577,17 +582,23 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a) {
             for (int c = 0; c < 6; c++)
                 acc[r * 6 + c] += BD[r * 3] * b2[c * 3] + BD[r * 3 + 1] * b2[c * 3 + 1] + BD[r * 3 + 2] * b2[c * 3 + 2];
     }
+    {  // values 0..31: reduce-scatter (lane l holds value l >> 1); 32..35: all-reduce
+        double v[32];
 #pragma unroll
-    for (int q = 0; q < 36; q++) {
-        double x = acc[q];
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if (lane == 0) red[wid][q] = x;
+        for (int q = 0; q < 32; q++) v[q] = acc[q];
+        const double s = wave_reduce_scatter32(v);
+        if (!(lane & 1)) red[wid][lane >> 1] = s;
+#pragma unroll
+        for (int q = 32; q < 36; q++) {
+            const double x = wave_sum(acc[q]);
+            if (lane == 0) red[wid][q] = x;
+        }
     }
     __syncthreads();
     const int q = threadIdx.x;
     if (q < 36) {
         double t = 0;
-        for (int w = 0; w < kBaBlock / 64; w++) t += red[w][q];
+        for (int w = 0; w < kSchurWaves; w++) t += red[w][q];
         const int r = q / 6, c = q % 6;
         if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
         else if (c >= r) a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (a.Hpp[36 * i1 + q] + (r == c ? lam : 0.0)) - t;
@@ -595,17 +606,19 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_schur(BaDev a) {
 }
 
 // ---------------------------------------------------------------- reduced system solve
-// LDL^T = U^T D U of the reduced camera system, blocked by the 6x6 pose blocks and held in
-// registers: TPT threads own tile (i, j), i <= j, of the upper triangle, or block i of the
-// right-hand side carried through the factorisation as an extra tile column.  Block step k
-// has two phases and two barriers:
-//   B(k)  owners of (k, j > k) solve W = U_kk^-T A_kj, U_kj = D_k^-1 W and publish W, U (LDS);
-//         U_kj also goes to the packed factor H, the right-hand side tile gives y_k = D^-1 z_k.
-//         The owner of (k, k) stores U_kk^-1 (unit upper) for the back substitution.
-//   A(k)  owners of (i, j), i > k apply A_ij -= W_ki^T U_kj; the owner of (k+1, k+1) then
-//         factors its tile at once (lookahead), so no phase of its own is spent on it.
-// Back substitution U x = y: one wave, one block per step, x_k = U_kk^-1 (y_k - sum U_kj x_j).
-// Same factorisation as LinearSolverEigen's SimplicialLDLT up to the rounding order.
+// Block Gauss-Jordan on the LDL^T = U^T D U factorisation of the reduced camera system,
+// blocked by the 6x6 pose blocks and held in registers: TPT threads own tile (i, j), i <= j, of
+// the upper triangle, or block i of the right-hand side carried as an extra tile column.  Block
+// step k has two phases and two barriers:
+//   B(k)  owners of (k, j > k) form W = U_kk^-T A_kj, U_kj = D_k^-1 W and the normalised pivot
+//         row R_kj = U_kk^-1 U_kj (= A_kk^-1 A_kj) and publish W, U, R (LDS); the right-hand
+//         side tile gives y_k = D_k^-1 U_kk^-T z_k and r_k = U_kk^-1 y_k.  Owners of the
+//         column-k tiles above the pivot, (i < k, k), publish M_ik and drop the tile.
+//   A(k)  rows below the pivot (i > k): A_ij -= W_ki^T U_kj (the LDL^T trailing update; the
+//         owner of (k+1, k+1) then factors its tile at once, lookahead); rows above (i < k),
+//         already normalised: M_ij -= M_ik R_kj, right-hand side r_i -= M_ik r_k.
+// After the last step the right-hand side column holds x: no back substitution.  Same solution
+// as LinearSolverEigen's SimplicialLDLT up to the rounding order.
 constexpr int kBaSolveThreads = 512;  // >= TPT x tiles: 2 x (231 + 21) at np <= 21, 465 + 30 at np <= 30
 constexpr int kBaSolveTpt2MaxPoses = 21;
 #ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: s_memtime stamps kept in LDS, copied out at the end
@@ -682,12 +695,10 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
     SOLVE_STAMP_DECL;
     SOLVE_STAMP(threadIdx.x == 0, 250);
     constexpr int kSlot = 37;  // odd stride in doubles: conflict-free LDS rows
-    __shared__ double H[kBaPacked];  // the factor: U_kj (k < j) at packed offsets
-    __shared__ double Ui[kBaMaxPoses * 15];  // U_kk^-1 (unit upper), strict upper row by row
-    __shared__ double Wp[(kBaMaxPoses + 1) * kSlot], Up[(kBaMaxPoses + 1) * kSlot];
+    __shared__ double Wp[(kBaMaxPoses + 1) * kSlot], Up[(kBaMaxPoses + 1) * kSlot], Rp[(kBaMaxPoses + 1) * kSlot];
+    __shared__ double Mp[kBaMaxPoses * kSlot];
     __shared__ double Ud[36], Dinv6[6];
     __shared__ double bs[kBaMaxN];
-    __shared__ int rb[kBaMaxN];  // packed(r, c) = rb[r] + c
     __shared__ int fail;
     const int N = 6 * np, nblk = np * (np + 1) / 2;
     const int tid = threadIdx.x;
@@ -706,7 +717,6 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
         bj = bi + t;
     }
     const bool dg = !rhs && bi == bj;
-    for (int q = tid; q < N; q += blockDim.x) rb[q] = q * N - q * (q - 1) / 2 - q;
     double A[6 * CPT];  // A[r * CPT + cc] = element (r, c0 + cc) of the tile
     // branch-free loads (clamped addresses, then a select) so that all of them are in flight
 #pragma unroll
@@ -738,11 +748,6 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
         if (h == 0) {
 #pragma unroll
             for (int q = 0; q < 36; q++) Ud[q] = F[q];
-            int q = 0;
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int j = i + 1; j < 6; j++, q++) Ui[15 * bi + q] = F[i * 6 + j];
 #pragma unroll
             for (int j = 0; j < 6; j++) Dinv6[j] = inv6[j];
             if (!ok) fail = 1;
@@ -754,27 +759,19 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
     SOLVE_STAMP(tid == 0, 251);
     for (int k = 0; k < np; k++) {
         if (fail) break;
-        // ---- B(k): block row k
+        // ---- B(k): pivot row k; column k above the pivot
         if (own && bi == k && bj > k) {
-            int hrow[6];
+            double ud[6][6];  // strict upper of U_kk (static indices only)
 #pragma unroll
-            for (int r = 0; r < 6; r++) hrow[r] = rb[6 * k + r];
-            double ud[15];
-            {
-                int q = 0;
+            for (int t = 0; t < 6; t++)
 #pragma unroll
-                for (int t = 1; t < 6; t++)
+                for (int s2 = t + 1; s2 < 6; s2++) ud[t][s2] = Ud[t * 6 + s2];
 #pragma unroll
-                    for (int s2 = 0; s2 < t; s2++, q++) ud[q] = Ud[s2 * 6 + t];
-            }
-#pragma unroll
-            for (int cc = 0; cc < CPT; cc++) {
-                int q = 0;
+            for (int cc = 0; cc < CPT; cc++)  // W = U_kk^-T A (unit lower solve)
 #pragma unroll
                 for (int t = 1; t < 6; t++)
 #pragma unroll
-                    for (int s2 = 0; s2 < t; s2++, q++) A[t * CPT + cc] -= ud[q] * A[s2 * CPT + cc];
-            }
+                    for (int s2 = 0; s2 < t; s2++) A[t * CPT + cc] -= ud[s2][t] * A[s2 * CPT + cc];
 #pragma unroll
             for (int q = 0; q < 6 * CPT; q++) {
                 const int r = q / CPT, c = c0 + q % CPT;
@@ -782,29 +779,34 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
                 A[q] *= Dinv6[r];
                 Up[bj * kSlot + r * 6 + c] = A[q];
             }
-            if (!rhs) {
 #pragma unroll
-                for (int r = 0; r < 6; r++) {
-                    const int o = hrow[r] + 6 * bj + c0;
+            for (int cc = 0; cc < CPT; cc++)  // R = U_kk^-1 U (unit upper solve, bottom up)
 #pragma unroll
-                    for (int cc = 0; cc < CPT; cc++) H[o + cc] = A[r * CPT + cc];
-                }
-            } else if (h == 0) {
+                for (int t = 4; t >= 0; t--)
 #pragma unroll
-                for (int r = 0; r < 6; r++) bs[6 * k + r] = A[r * CPT];
-            }
+                    for (int s2 = t + 1; s2 < 6; s2++) A[t * CPT + cc] -= ud[t][s2] * A[s2 * CPT + cc];
+#pragma unroll
+            for (int q = 0; q < 6 * CPT; q++) Rp[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = A[q];
             SOLVE_STAMP(bj == k + 1 && h == 0, 4 * k);
         }
+        if (own && !rhs && bj == k && bi < k) {  // M_ik, stored transposed like W_ki
+#pragma unroll
+            for (int q = 0; q < 6 * CPT; q++) Mp[bi * kSlot + (c0 + q % CPT) * 6 + q / CPT] = A[q];
+        }
         __syncthreads();
-        // ---- A(k): trailing update; the next diagonal tile is factored as soon as it is final
-        if (own && bi > k) {
-            // A -= W_ki^T U_kj with 6 CPT independent accumulation chains (the unused lower part
-            // of a diagonal tile and the zero columns of a right-hand-side tile stay harmless)
+        // ---- A(k): eliminate column k from every other row
+        if (own && bj > k && bi != k) {
+            // A -= L^T P with L(t, r) = W_ki(t, r) below the pivot or M_ik(r, t) above it, and P =
+            // U_kj or R_kj: 6 CPT independent accumulation chains (the unused lower part of a
+            // diagonal tile and the zero columns of a right-hand-side tile stay harmless)
+            const bool below = bi > k;
+            const double* Pp = below ? Up : Rp;
+            const double* Lp = below ? Wp : Mp;
             double u[6 * CPT], w[36];
 #pragma unroll
-            for (int q = 0; q < 6 * CPT; q++) u[q] = Up[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
+            for (int q = 0; q < 6 * CPT; q++) u[q] = Pp[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
 #pragma unroll
-            for (int q = 0; q < 36; q++) w[q] = Wp[bi * kSlot + q];  // w[t * 6 + r] = W_ki(t, r)
+            for (int q = 0; q < 36; q++) w[q] = Lp[bi * kSlot + q];  // w[t * 6 + r] = L(t, r)
 #pragma unroll
             for (int t = 0; t < 6; t++)
 #pragma unroll
@@ -824,82 +826,16 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
         if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
         return;
     }
-    // U_kk^-1 (unit upper) of every diagonal block in place, one thread per block:
-    // X(i, j) = -(U(i, j) + sum_{i < m < j} U(i, m) X(m, j))
-    if (tid < np) {
-        double U[36];
-        {
-            int q = 0;
+    if (rhs && h == 0) {  // x = the right-hand side column
 #pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int j = i + 1; j < 6; j++, q++) U[i * 6 + j] = Ui[15 * tid + q];
+        for (int r = 0; r < 6; r++) {
+            bs[6 * bi + r] = A[r * CPT];
+            a.xp[6 * bi + r] = A[r * CPT];
         }
-        double X[36];
-#pragma unroll
-        for (int j = 1; j < 6; j++)
-#pragma unroll
-            for (int i = j - 1; i >= 0; i--) {
-                double s2 = U[i * 6 + j];
-#pragma unroll
-                for (int m = i + 1; m < j; m++) s2 += U[i * 6 + m] * X[m * 6 + j];
-                X[i * 6 + j] = -s2;
-            }
-        int q = 0;
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-            for (int j = i + 1; j < 6; j++, q++) Ui[15 * tid + q] = X[i * 6 + j];
     }
     __syncthreads();
     if (tid >= 64) return;
     const int lane = tid;
-    // U x = y, blocked from the last block up (one wave): x_k = U_kk^-1 y_k, then y_j -= U_jk x_k.
-    // Every LDS read of a step is issued before the first use; rows jj = lane + 64 m.
-    constexpr int NM = kBaMaxN / 64 + 1;
-    int rbj[NM];
-#pragma unroll
-    for (int m = 0; m < NM; m++) rbj[m] = lane + 64 * m < N ? rb[lane + 64 * m] : 0;
-    for (int k = np - 1; k >= 0; k--) {
-        const int k0 = 6 * k;
-        double y[6], x[6], ui[15], hr[NM][6], bv[NM];
-#pragma unroll
-        for (int t = 0; t < 6; t++) y[t] = bs[k0 + t];
-#pragma unroll
-        for (int q = 0; q < 15; q++) ui[q] = Ui[15 * k + q];
-#pragma unroll
-        for (int m = 0; m < NM; m++) {
-            const int jj = lane + 64 * m;
-            const bool v = jj < k0;
-            const int base = v ? rbj[m] + k0 : 0;
-#pragma unroll
-            for (int t = 0; t < 6; t++) hr[m][t] = H[base + t];
-            bv[m] = bs[v ? jj : 0];
-        }
-        {
-            int q = 0;
-#pragma unroll
-            for (int t = 0; t < 6; t++) {
-                double v = y[t];
-#pragma unroll
-                for (int s2 = t + 1; s2 < 6; s2++, q++) v += ui[q] * y[s2];
-                x[t] = v;
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < NM; m++) {
-            const int jj = lane + 64 * m;
-            const double v0 = hr[m][0] * x[0] + hr[m][1] * x[1] + hr[m][2] * x[2];
-            const double v1 = hr[m][3] * x[3] + hr[m][4] * x[4] + hr[m][5] * x[5];
-            if (jj < k0) bs[jj] = bv[m] - (v0 + v1);
-        }
-        if (lane < 6) {
-#pragma unroll
-            for (int t = 0; t < 6; t++)
-                if (t == lane) { a.xp[k0 + t] = x[t]; bs[k0 + t] = x[t]; }
-        }
-        wave_sync_lds();
-    }
     SOLVE_STAMP(lane == 0, 252);
     // trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
     // computeScale, sum x_p (lambda x_p + b_p) in index order
@@ -1141,7 +1077,7 @@ struct Runner {
     void step() {
         hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
-        if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kBaBlock), 0, h.stream, a);
+        if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
         if (solve_tpt == 2) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaBlock), 0, h.stream, a);
