@@ -237,6 +237,10 @@ def run_track(a, rank, world, local, dist):
     lib = __import__("orb_slam2_with_comment_amd._capi", fromlist=["lib"]).lib()
     lib.orbmi_set_profiling(tr.extractor.handle, 1 << stage["dominant_id"])
     reset_profile(tr.extractor.handle)
+    # the path's dominant kernel (rocprofv3, profiles/): PoseOptimization, bracketed with HIP
+    # events on the tracking stream it is launched on
+    lib.orbmi_pose_set_profiling(tr.pose._h, 1)
+    pose_prof = read_pose_profile(lib, tr.pose._h)
     sync()
     if dist:
         dist.barrier()
@@ -250,10 +254,13 @@ def run_track(a, rank, world, local, dist):
     dt = time.perf_counter() - t0
     ms, nl = read_profile(tr.extractor.handle)
     lib.orbmi_set_profiling(tr.extractor.handle, 0)
+    pose_prof = read_pose_profile(lib, tr.pose._h)
+    lib.orbmi_pose_set_profiling(tr.pose._h, 0)
     dt = max_over_ranks(dt, dist)
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
     value = a.steps * world / dt
-    roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic)
+    ext_roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic)
+    roof = pose_roofline(pose_prof, outcome["recs"], a.traffic)
     out = None
     if rank == 0:
         cpu = None
@@ -290,6 +297,7 @@ def run_track(a, rank, world, local, dist):
                          "keyframes": int(len(problem.kfs))},
             "stage_ms_per_step": stage["stage_ms"],
             "roofline": roof,
+            "extractor_roofline": ext_roof,
             "pipeline_roofline": pipeline_roofline(stage, rows, cols),
             "cpu_baseline": cpu,
             "host": host_info(),
@@ -370,6 +378,36 @@ def roofline_entry(name, stage, ms_total, launches, traffic_path):
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": read_traffic(traffic_path, name),
             "alg_bytes_per_launch": round(alg), "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches)}
+
+
+def read_pose_profile(lib, handle):
+    ms, nl = C.c_double(), C.c_longlong()
+    rc = lib.orbmi_pose_read_profile(handle, C.byref(ms), C.byref(nl))
+    if rc:
+        raise RuntimeError(f"orbmi_pose_read_profile returned {rc}")
+    return ms.value, nl.value
+
+
+# algorithmic fp64 flops of PoseOptimization: per edge and edge pass
+# (computeActiveErrors + linearizeOplus + J^T W J + b) and per Levenberg trial (damped 6x6 LDL^T
+# + exponential map + step control)
+POSE_FLOPS_PER_EDGE_PASS = 300
+POSE_FLOPS_PER_TRIAL = 600
+
+
+def pose_roofline(prof, recs, traffic_path):
+    """k_pose_opt against the FP64 peak: edge passes counted as (iterations + 4 rounds) x edges
+    of the frame's two PoseOptimizations (a lower bound: rejected trials add passes)."""
+    ms_total, launches = prof
+    avg_s = ms_total / max(int(launches), 1) / 1e3
+    flops = np.mean([int(r["n_obs"]) * POSE_FLOPS_PER_EDGE_PASS * (int(r["iterations"]) + 4)
+                     + int(r["iterations"]) * POSE_FLOPS_PER_TRIAL for r in recs])
+    achieved = flops / avg_s / 1e12 if avg_s > 0 else 0.0
+    return {"kernel": "k_pose_opt", "bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFS, 8),
+            "traffic": read_traffic(traffic_path, "k_pose_opt"), "alg_flops_per_launch": round(float(flops)),
+            "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches),
+            "note": "fp64 Levenberg on one workgroup per frame: serial-latency-bound (DESIGN.md)"}
 
 
 def pipeline_roofline(stage, rows, cols):

@@ -324,6 +324,11 @@ int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex);
 /* Run the handle on the matcher's stream instead: the tracking stages (searches, pose
  * optimisations) then form one stream that can run beside the next frame's extraction. */
 int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m);
+/* Bracket every PoseOptimization kernel launched by orbmi_pose_optimization_frame with HIP
+ * events on the handle's stream (on != 0); orbmi_pose_read_profile synchronises and returns
+ * the summed device time (ms) and launch count since the last read. */
+int orbmi_pose_set_profiling(orbmi_pose* h, int on);
+int orbmi_pose_read_profile(orbmi_pose* h, double* ms, long long* launches);
 
 /* Frame::mvpMapPoints of the frame being tracked, as the matchers left it: keypoint i holds
  * local map point mps[match_mp[i]] when match_mp && match_mp[i] >= 0, otherwise last-frame

@@ -18,6 +18,8 @@
 #include <cstring>
 #include <cmath>
 #include <new>
+#include <utility>
+#include <vector>
 
 #include "extractor.h"
 #include "se3_device.h"
@@ -519,6 +521,10 @@ struct orbmi_pose {
     size_t cap_obs = 0;
     uint8_t* d_stage = nullptr;
     size_t cap_stage = 0, used_stage = 0;
+    // orbmi_pose_set_profiling: HIP event pairs around every k_pose_opt launch
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    size_t used_events = 0;
 };
 
 hipStream_t orbmi_extractor_stream_(orbmi_extractor* ex);  // capi_extract.cpp
@@ -533,6 +539,17 @@ bool is_device_ptr(const void* p) {
         return false;
     }
     return a.type == hipMemoryTypeDevice;
+}
+
+// event pair for the next profiled launch (grown on demand, reused after each read)
+std::pair<hipEvent_t, hipEvent_t>* next_events(orbmi_pose* h) {
+    if (h->used_events == h->events.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess) return nullptr;
+        if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return nullptr; }
+        h->events.emplace_back(a, b);
+    }
+    return &h->events[h->used_events++];
 }
 
 }  // namespace
@@ -562,6 +579,7 @@ void orbmi_pose_destroy(orbmi_pose* h) {
     if (h->d_buf) (void)hipFree(h->d_buf);
     if (h->d_obs) (void)hipFree(h->d_obs);
     if (h->d_stage) (void)hipFree(h->d_stage);
+    for (auto& e : h->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -587,6 +605,28 @@ int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m) {
     if (h->own_stream) ORBMI_HIP(hipStreamDestroy(h->stream));
     h->stream = (hipStream_t)sv;
     h->own_stream = false;
+    return ORBMI_OK;
+}
+
+int orbmi_pose_set_profiling(orbmi_pose* h, int on) {
+    if (!h) return ORBMI_E_ARG;
+    h->profiling = on != 0;
+    return ORBMI_OK;
+}
+
+int orbmi_pose_read_profile(orbmi_pose* h, double* ms, long long* launches) {
+    if (!h || !ms || !launches) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(h->device));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    double t = 0;
+    for (size_t i = 0; i < h->used_events; i++) {
+        float e = 0;
+        ORBMI_HIP(hipEventElapsedTime(&e, h->events[i].first, h->events[i].second));
+        t += e;
+    }
+    *ms = t;
+    *launches = (long long)h->used_events;
+    h->used_events = 0;
     return ORBMI_OK;
 }
 
@@ -709,9 +749,12 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     if (rc) return rc;
     hipLaunchKernelGGL(k_pose_gather, dim3(1), dim3(kGatherThreads), 0, h->stream, a);
     ORBMI_HIP(hipGetLastError());
+    auto* ev = h->profiling ? next_events(h) : nullptr;
+    if (ev) ORBMI_HIP(hipEventRecord(ev->first, h->stream));
     hipLaunchKernelGGL(k_pose_opt<false>, dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec,
                        (const orbmi_pose_obs*)h->d_obs, a.outlier, 1, nullptr);
     ORBMI_HIP(hipGetLastError());
+    if (ev) ORBMI_HIP(hipEventRecord(ev->second, h->stream));
     if (async) return ORBMI_OK;
     if (!is_device_ptr(rec))
         ORBMI_HIP(hipMemcpyAsync(rec, a.rec, sizeof(orbmi_pose_frame), hipMemcpyDeviceToHost, h->stream));
