@@ -21,8 +21,8 @@ run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeo
 tail -3 $OUT/pytest_gpu.log
 cp $OUT/pytest_gpu.log $P/pytest_gpu.log
 run prof_stats 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_stats -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline
-run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline
-run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline
+run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline --cpu-sample-s 1
+run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline --cpu-sample-s 1
 python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic_latest.json && cp $OUT/traffic.json $P/traffic.json
 find $OUT/prof_stats -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats.csv \;
 cp $OUT/prof_stats.log $P/prof_stats_bench.log 2>/dev/null
