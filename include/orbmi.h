@@ -213,6 +213,45 @@ int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches);
 
+/* ---- DBoW2 vocabulary: Frame::ComputeBoW / KeyFrame::ComputeBoW ---- */
+
+/* DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (Thirdparty/DBoW2/DBoW2/
+ * TemplatedVocabulary.h) as flat arrays, nodes in id order (node 0 = root, as
+ * loadFromTextFile builds them, :1338-1424): 32-B descriptor, children as CSR in insertion
+ * order, word id (-1 for inner nodes) and weight (idf for TF_IDF) per node.  scoring and
+ * weighting are DBoW2::ScoringType / WeightingType (BowVector.h:36-53). */
+typedef struct orbmi_vocabulary_desc {
+    int k, L;                      /* m_k, m_L                                               */
+    int scoring, weighting;        /* L1_NORM .. DOT_PRODUCT; TF_IDF, TF, IDF, BINARY         */
+    int nnodes;
+    const uint8_t* desc;           /* nnodes x 32                                            */
+    const int32_t* child_off;      /* nnodes + 1                                             */
+    const int32_t* children;       /* child_off[nnodes] node ids                             */
+    const int32_t* word_id;        /* nnodes                                                 */
+    const double* weight;          /* nnodes                                                 */
+} orbmi_vocabulary_desc;
+
+typedef struct orbmi_vocabulary orbmi_vocabulary;
+/* Upload a vocabulary (host arrays) to `device`; the handle owns a stream. */
+int orbmi_vocabulary_create(int device, const orbmi_vocabulary_desc* d, orbmi_vocabulary** out);
+void orbmi_vocabulary_destroy(orbmi_vocabulary* v);
+int orbmi_vocabulary_synchronize(orbmi_vocabulary* v);
+
+/* TemplatedVocabulary::transform(features, BowVector& v, FeatureVector& fv, levelsup)
+ * (TemplatedVocabulary.h:1126-1194, per feature :1217-1259) as Frame::ComputeBoW calls it
+ * (levelsup = 4, src/Frame.cc:425-432): each of the n descriptors (n x 32 u8) descends the tree
+ * (FORB::distance, first child wins ties); features whose word weight is 0 are skipped.
+ * Outputs (capacity n each; fv_off n + 1): the BowVector as word ids ascending + values
+ * (addWeight for TF / TF_IDF, addIfNotExist for IDF / BINARY, 1/size for TF without
+ * normalisation, then normalize(L1 | L2) when the scoring asks for it, BowVector.cpp:34-86),
+ * the FeatureVector as CSR (orbmi_feature_vector: node ids at level L - levelsup ascending,
+ * feature indices ascending), counts[0] = words, counts[1] = nodes.  n_device (optional)
+ * overrides n with a device-resident count <= n.  Arrays host or device; asynchronous on the
+ * handle's stream when every output (counts included) is device memory.  n <= 8192. */
+int orbmi_transform(orbmi_vocabulary* v, const uint8_t* desc, int n, const int* n_device, int levelsup,
+                    uint32_t* bow_word, double* bow_value, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat,
+                    int* counts);
+
 /* Cross-stream matching of config 4 (build-defined; no reference counterpart, SURVEY.md §8(d)
  * "Config 4"): brute-force Hamming nearest neighbour of each of the nq query descriptors over
  * the nseg gathered train segments (segment s = rows [s*seg_capacity, s*seg_capacity +

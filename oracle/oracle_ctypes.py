@@ -351,3 +351,20 @@ def match_descriptors_segments(q_desc, train_desc, seg_counts, skip_seg=-1, th=5
         if d1 <= th and float(d1) < np.float32(ratio) * np.float32(d2):
             out[i] = rows[o[0]]
     return out
+
+
+def transform(vocab, desc, levelsup=4):
+    """TemplatedVocabulary::transform restatement -> (bow_word, bow_value, node_id, off, feat)."""
+    L = lib()
+    L.orc_transform.argtypes = [C.c_void_p] * 2 + [C.c_int, C.c_int] + [C.c_void_p] * 6
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(desc)
+    cap = max(n, 1)
+    word, value = np.zeros(cap, np.uint32), np.zeros(cap, np.float64)
+    node, off, feat = np.zeros(cap, np.uint32), np.zeros(cap + 1, np.int32), np.zeros(cap, np.int32)
+    counts = np.zeros(2, np.int32)
+    d = vocab.desc_struct()
+    L.orc_transform(C.addressof(d), desc.ctypes.data, n, levelsup, word.ctypes.data, value.ctypes.data,
+                    node.ctypes.data, off.ctypes.data, feat.ctypes.data, counts.ctypes.data)
+    nw, nn = int(counts[0]), int(counts[1])
+    return word[:nw], value[:nw], node[:nn], off[:nn + 1], feat[:int(off[nn])]

@@ -78,6 +78,10 @@ _PROTOS = {
     "orbmi_pose_share_stream": (_i, [_vp, _vp]),
     "orbmi_pose_share_matcher_stream": (_i, [_vp, _vp]),
     "orbmi_pose_set_profiling": (_i, [_vp, _i]),
+    "orbmi_vocabulary_create": (_i, [_i, _vp, C.POINTER(_vp)]),
+    "orbmi_vocabulary_destroy": (None, [_vp]),
+    "orbmi_vocabulary_synchronize": (_i, [_vp]),
+    "orbmi_transform": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_pose_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_pose_optimization_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_search_by_projection_last_frame_if": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _i]),

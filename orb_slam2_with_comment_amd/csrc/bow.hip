@@ -1,0 +1,362 @@
+// DBoW2 TemplatedVocabulary::transform on MI355X: Frame::ComputeBoW / KeyFrame::ComputeBoW
+// (src/Frame.cc:425-432, src/KeyFrame.cc:59), SURVEY.md §8(f) rank 2.
+//   TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)
+//                                               Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1126-1194
+//   per-feature descent                         :1217-1259 (FORB::distance, strict < : first child wins)
+//   BowVector::addWeight / addIfNotExist / normalize   Thirdparty/DBoW2/DBoW2/BowVector.cpp:34-86
+//   FeatureVector::addFeature                   Thirdparty/DBoW2/DBoW2/FeatureVector.cpp:31-45
+// Two kernels:
+//   k_bow_descend  thread per descriptor: the descriptor stays in registers (2 x uint4), every
+//                  level reads the children's 32-B descriptors (16-B loads) and keeps the first
+//                  minimum; outputs (word, weight, node at level L - levelsup).
+//   k_bow_build    one 1024-thread workgroup: bitonic sort in LDS of (word << 32 | feature) keys,
+//                  segment heads -> BowVector entries in word order with the per-word weight
+//                  accumulated sequentially in feature order (as addWeight does), the L1 / L2 norm
+//                  summed sequentially in word order (as normalize does); then the same sort on
+//                  (node << 32 | feature) -> FeatureVector CSR.  Every sum has the reference's
+//                  order, so the BowVector values are bit-exact, not merely close.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "orbmi_common.h"
+
+namespace orbmi {
+
+constexpr int kBowMaxFeatures = 8192;
+constexpr int kBowBuildThreads = 1024;
+constexpr unsigned long long kNoKey = ~0ull;
+
+struct VocDev {
+    int k, L, scoring, weighting, nnodes;
+    const uint4* desc;       // nnodes x 2
+    const int* child_off;
+    const int* children;
+    const int* word_id;
+    const double* weight;
+};
+
+// DBoW2 ScoringObject::mustNormalize (ScoringObject.h:60-92): L1 for L1 / chi-square / KL /
+// Bhattacharyya, L2 for L2, none for the dot product.  norm: 1 = L1, 2 = L2.
+__host__ __device__ inline bool must_normalize(int scoring, int* norm) {
+    if (scoring == 1) { *norm = 2; return true; }
+    *norm = 1;
+    return scoring != 5;
+}
+
+__global__ __launch_bounds__(256) void k_bow_descend(VocDev v, const uint4* __restrict__ feats, int n,
+                                                     const int* __restrict__ n_dev, int nid_level,
+                                                     unsigned long long* __restrict__ key_w,
+                                                     unsigned long long* __restrict__ key_n, double* __restrict__ wv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nn = n_dev ? min(*n_dev, n) : n;
+    if (i >= n) return;
+    if (i >= nn) { key_w[i] = kNoKey; key_n[i] = kNoKey; return; }
+    const uint4 a0 = feats[2 * i], a1 = feats[2 * i + 1];
+    int node = 0, level = 0, nid = 0;
+    for (;;) {
+        const int c0 = v.child_off[node], c1 = v.child_off[node + 1];
+        if (c0 == c1) break;  // leaf
+        level++;
+        int best = v.children[c0];
+        int bd = popc256(a0, a1, v.desc[2 * best], v.desc[2 * best + 1]);
+        for (int j = c0 + 1; j < c1; j++) {
+            const int id = v.children[j];
+            const int d = popc256(a0, a1, v.desc[2 * id], v.desc[2 * id + 1]);
+            if (d < bd) { bd = d; best = id; }
+        }
+        node = best;
+        if (level == nid_level) nid = node;
+    }
+    const double w = v.weight[node];
+    const int word = v.word_id[node];
+    const bool keep = w > 0;  // "not stopped"
+    key_w[i] = keep ? ((unsigned long long)(unsigned)word << 32 | (unsigned)i) : kNoKey;
+    key_n[i] = keep ? ((unsigned long long)(unsigned)nid << 32 | (unsigned)i) : kNoKey;
+    wv[i] = w;
+}
+
+// ascending bitonic sort of m (power of two) keys in LDS
+__device__ void bitonic_sort(unsigned long long* s, int m) {
+    for (int size = 2; size <= m; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < (m >> 1); t += blockDim.x) {
+                const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = s[lo], b = s[hi];
+                if ((a > b) == up) { s[lo] = b; s[hi] = a; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// heads[j] = 1 where sorted key j starts a new segment (same high 32 bits); returns the exclusive
+// prefix of heads per element in pos[] and the number of segments
+__device__ int segment_heads(const unsigned long long* s, int m, int* pos, int* scratch) {
+    constexpr int PER = kBowMaxFeatures / kBowBuildThreads;  // 8 keys per thread
+    const int base = threadIdx.x * PER;
+    int h[PER], cnt = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = base + q;
+        const bool valid = j < m && s[j] != kNoKey;
+        h[q] = valid && (j == 0 || (s[j] >> 32) != (s[j - 1] >> 32));
+        cnt += h[q];
+    }
+    int total;
+    int run = block_excl_scan(cnt, scratch, &total);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = base + q;
+        if (j < m) pos[j] = h[q] ? run : -1;
+        run += h[q];
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(
+    const unsigned long long* __restrict__ key_w, const unsigned long long* __restrict__ key_n,
+    const double* __restrict__ wv, int n, int weighting, int scoring, unsigned* __restrict__ bow_word,
+    double* __restrict__ bow_value, unsigned* __restrict__ fv_node, int* __restrict__ fv_off, int* __restrict__ fv_feat,
+    int* __restrict__ counts) {
+    __shared__ unsigned long long s[kBowMaxFeatures];
+    __shared__ int pos[kBowMaxFeatures];
+    __shared__ int scratch[kBowBuildThreads / 64 + 1];
+    __shared__ double norm_s;
+    int m = 64;
+    while (m < n) m <<= 1;
+    // ---- BowVector
+    for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_w[j] : kNoKey;
+    __syncthreads();
+    bitonic_sort(s, m);
+    const int nw = segment_heads(s, m, pos, scratch);
+    const bool tf = weighting == 0 || weighting == 1;  // TF_IDF, TF: addWeight; IDF, BINARY: addIfNotExist
+    int nrm = 1;
+    const bool must = must_normalize(scoring, &nrm);
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        const int k = pos[j];
+        if (k < 0) continue;
+        const unsigned word = (unsigned)(s[j] >> 32);
+        double val = wv[(unsigned)s[j]];
+        if (tf)
+            for (int q = j + 1; q < m && s[q] != kNoKey && (unsigned)(s[q] >> 32) == word; q++) val += wv[(unsigned)s[q]];
+        if (tf && !must) val /= (double)nw;  // "unnecessary when normalizing": divide by v.size()
+        bow_word[k] = word;
+        bow_value[k] = val;
+    }
+    __syncthreads();
+    if (must) {  // BowVector::normalize: sequential in word order
+        if (threadIdx.x == 0) {
+            double norm = 0.0;
+            if (nrm == 1) {
+                for (int k = 0; k < nw; k++) norm += fabs(bow_value[k]);
+            } else {
+                for (int k = 0; k < nw; k++) norm += bow_value[k] * bow_value[k];
+                norm = sqrt(norm);
+            }
+            norm_s = norm;
+        }
+        __syncthreads();
+        const double norm = norm_s;
+        if (norm > 0.0)
+            for (int k = threadIdx.x; k < nw; k += blockDim.x) bow_value[k] /= norm;
+    }
+    __syncthreads();
+    // ---- FeatureVector
+    for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_n[j] : kNoKey;
+    __syncthreads();
+    bitonic_sort(s, m);
+    const int nnod = segment_heads(s, m, pos, scratch);
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        if (s[j] == kNoKey) continue;
+        fv_feat[j] = (int)(unsigned)s[j];  // valid keys sort first: j is the CSR position
+        const int k = pos[j];
+        if (k >= 0) {
+            fv_node[k] = (unsigned)(s[j] >> 32);
+            fv_off[k] = j;
+        }
+        if (j + 1 == m || s[j + 1] == kNoKey) fv_off[nnod] = j + 1;
+    }
+    if (threadIdx.x == 0) {
+        if (nnod == 0) fv_off[0] = 0;
+        counts[0] = nw;
+        counts[1] = nnod;
+    }
+}
+
+}  // namespace orbmi
+
+// ---------------------------------------------------------------- host
+struct orbmi_vocabulary {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    orbmi::VocDev v{};
+    void* d_vocab = nullptr;          // one allocation for all vocabulary arrays
+    uint8_t* d_work = nullptr;        // keys, weights and staging of one transform
+    size_t cap_work = 0;
+};
+
+namespace {
+
+bool on_device(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+int orbmi_vocabulary_create(int device, const orbmi_vocabulary_desc* d, orbmi_vocabulary** out) {
+    if (!out || !d) return ORBMI_E_ARG;
+    *out = nullptr;
+    if (d->nnodes < 1 || !d->desc || !d->child_off || !d->word_id || !d->weight) return ORBMI_E_ARG;
+    const int nch = d->child_off[d->nnodes];
+    if (d->child_off[0] != 0 || nch < 0 || (nch > 0 && !d->children)) return ORBMI_E_ARG;
+    for (int i = 0; i < d->nnodes; i++)  // CSR sanity: children ids in range, offsets monotone
+        if (d->child_off[i + 1] < d->child_off[i]) return ORBMI_E_ARG;
+    for (int j = 0; j < nch; j++)
+        if (d->children[j] <= 0 || d->children[j] >= d->nnodes) return ORBMI_E_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBMI_E_HIP;
+    orbmi_vocabulary* h = new (std::nothrow) orbmi_vocabulary();
+    if (!h) return ORBMI_E_ARG;
+    h->device = device;
+    const size_t nn = (size_t)d->nnodes;
+    const size_t b_desc = align256(nn * 32), b_off = align256((nn + 1) * 4), b_ch = align256((size_t)std::max(nch, 1) * 4),
+                 b_word = align256(nn * 4), b_w = align256(nn * 8);
+    auto fail = [&](int rc) { orbmi_vocabulary_destroy(h); return rc; };
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(ORBMI_E_HIP);
+    if (hipMalloc(&h->d_vocab, b_desc + b_off + b_ch + b_word + b_w) != hipSuccess) return fail(ORBMI_E_HIP);
+    uint8_t* base = (uint8_t*)h->d_vocab;
+    uint8_t* p_desc = base;
+    int* p_off = (int*)(base + b_desc);
+    int* p_ch = (int*)(base + b_desc + b_off);
+    int* p_word = (int*)(base + b_desc + b_off + b_ch);
+    double* p_w = (double*)(base + b_desc + b_off + b_ch + b_word);
+    if (hipMemcpy(p_desc, d->desc, nn * 32, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p_off, d->child_off, (nn + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (nch > 0 && hipMemcpy(p_ch, d->children, (size_t)nch * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(p_word, d->word_id, nn * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p_w, d->weight, nn * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(ORBMI_E_HIP);
+    h->v = orbmi::VocDev{d->k, d->L, d->scoring, d->weighting, d->nnodes, (const uint4*)p_desc, p_off, p_ch, p_word, p_w};
+    *out = h;
+    return ORBMI_OK;
+}
+
+void orbmi_vocabulary_destroy(orbmi_vocabulary* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->d_vocab) (void)hipFree(h->d_vocab);
+    if (h->d_work) (void)hipFree(h->d_work);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int orbmi_vocabulary_synchronize(orbmi_vocabulary* h) {
+    if (!h) return ORBMI_E_ARG;
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    return ORBMI_OK;
+}
+
+int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* n_device, int levelsup,
+                    uint32_t* bow_word, double* bow_value, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat,
+                    int* counts) {
+    using namespace orbmi;
+    if (!h || n < 0 || (n > 0 && !desc) || !bow_word || !bow_value || !fv_node || !fv_off || !fv_feat || !counts)
+        return ORBMI_E_ARG;
+    if (n > kBowMaxFeatures) return ORBMI_E_UNSUPPORTED;
+    if (n_device && !on_device(n_device)) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(h->device));
+    const size_t nn = (size_t)std::max(n, 1);
+    // work: keys (2 x 8 n), weights (8 n), staged input (32 n), staged outputs
+    const size_t b_key = align256(nn * 8), b_w = align256(nn * 8), b_in = align256(nn * 32), b_u = align256(nn * 4),
+                 b_d = align256(nn * 8), b_off = align256((nn + 1) * 4), b_cnt = 256;
+    const size_t need = 2 * b_key + b_w + b_in + b_u + b_d + b_u + b_off + b_u + b_cnt;
+    if (need > h->cap_work) {
+        ORBMI_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_work) (void)hipFree(h->d_work);
+        h->d_work = nullptr;
+        h->cap_work = 0;
+        ORBMI_HIP(hipMalloc((void**)&h->d_work, need));
+        h->cap_work = need;
+    }
+    uint8_t* w = h->d_work;
+    unsigned long long* key_w = (unsigned long long*)w; w += b_key;
+    unsigned long long* key_n = (unsigned long long*)w; w += b_key;
+    double* wv = (double*)w; w += b_w;
+    uint8_t* in_stage = w; w += b_in;
+    uint32_t* s_word = (uint32_t*)w; w += b_u;
+    double* s_value = (double*)w; w += b_d;
+    uint32_t* s_node = (uint32_t*)w; w += b_u;
+    int32_t* s_off = (int32_t*)w; w += b_off;
+    int32_t* s_feat = (int32_t*)w; w += b_u;
+    int* s_cnt = (int*)w;
+    const uint8_t* d_in = desc;
+    if (n > 0 && !on_device(desc)) {
+        ORBMI_HIP(hipMemcpyAsync(in_stage, desc, (size_t)n * 32, hipMemcpyHostToDevice, h->stream));
+        d_in = in_stage;
+    }
+    bool host_out = false;
+    auto dev_out = [&](auto* p, auto* stage) {
+        if (on_device(p)) return p;
+        host_out = true;
+        return stage;
+    };
+    uint32_t* o_word = dev_out(bow_word, s_word);
+    double* o_value = dev_out(bow_value, s_value);
+    uint32_t* o_node = dev_out(fv_node, s_node);
+    int32_t* o_off = dev_out(fv_off, s_off);
+    int32_t* o_feat = dev_out(fv_feat, s_feat);
+    int* o_cnt = dev_out(counts, s_cnt);
+    const int nid_level = h->v.L - levelsup;  // <= 0: the root (node 0)
+    if (n > 0) {
+        hipLaunchKernelGGL(k_bow_descend, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->v, (const uint4*)d_in, n,
+                           n_device, nid_level, key_w, key_n, wv);
+        ORBMI_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_bow_build, dim3(1), dim3(kBowBuildThreads), 0, h->stream, key_w, key_n, wv, n,
+                       h->v.weighting, h->v.scoring, (unsigned*)o_word, o_value, (unsigned*)o_node, (int*)o_off,
+                       (int*)o_feat, o_cnt);
+    ORBMI_HIP(hipGetLastError());
+    if (!host_out) return ORBMI_OK;
+    int hc[2] = {0, 0};
+    ORBMI_HIP(hipMemcpyAsync(hc, o_cnt, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    const size_t nwd = (size_t)hc[0], nnd = (size_t)hc[1];
+    size_t nfeat = 0;
+    if (nnd > 0) {
+        int last = 0;
+        ORBMI_HIP(hipMemcpy(&last, o_off + nnd, sizeof(int), hipMemcpyDeviceToHost));
+        nfeat = (size_t)last;
+    }
+    auto back = [&](void* user, const void* dev, size_t bytes) -> int {
+        if (user != dev && bytes) ORBMI_HIP(hipMemcpyAsync(user, dev, bytes, hipMemcpyDeviceToHost, h->stream));
+        return ORBMI_OK;
+    };
+    int rc = ORBMI_OK;
+    rc |= back(bow_word, o_word, nwd * 4);
+    rc |= back(bow_value, o_value, nwd * 8);
+    rc |= back(fv_node, o_node, nnd * 4);
+    rc |= back(fv_off, o_off, (nnd + 1) * 4);
+    rc |= back(fv_feat, o_feat, nfeat * 4);
+    rc |= back(counts, o_cnt, 2 * sizeof(int));
+    if (rc) return ORBMI_E_HIP;
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    return ORBMI_OK;
+}
+
+}  // extern "C"

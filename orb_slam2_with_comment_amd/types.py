@@ -33,6 +33,13 @@ class FrameView(C.Structure):
                 ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float), ("n_device", C.c_void_p)]
 
 
+class VocabularyDesc(C.Structure):
+    """orbmi_vocabulary_desc (include/orbmi.h): DBoW2::TemplatedVocabulary as flat arrays."""
+    _fields_ = [("k", C.c_int), ("L", C.c_int), ("scoring", C.c_int), ("weighting", C.c_int), ("nnodes", C.c_int),
+                ("desc", C.c_void_p), ("child_off", C.c_void_p), ("children", C.c_void_p), ("word_id", C.c_void_p),
+                ("weight", C.c_void_p)]
+
+
 class FeatureVectorView(C.Structure):
     _fields_ = [("nnodes", C.c_int), ("node_id", C.c_void_p), ("off", C.c_void_p), ("feat", C.c_void_p)]
 
@@ -89,6 +96,15 @@ class FeatureVector:
         self.node_id = nodes.astype(np.uint32)
         self.off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
         self.feat = order.astype(np.int32)
+
+    @classmethod
+    def from_csr(cls, node_id, off, feat) -> "FeatureVector":
+        """From CSR arrays (the output of ORBVocabulary.transform / orbmi_transform)."""
+        fv = cls.__new__(cls)
+        fv.node_id = np.ascontiguousarray(node_id, np.uint32)
+        fv.off = np.ascontiguousarray(off, np.int32)
+        fv.feat = np.ascontiguousarray(feat, np.int32)
+        return fv
 
     def view(self) -> FeatureVectorView:
         v = FeatureVectorView()
