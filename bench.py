@@ -158,7 +158,14 @@ def run_track(a, rank, world, local, dist):
     img_bytes = rows * cols
     F = a.frames
     problem, _ = SM.local_ba_problem(seed=42)
-    mapper = LocalMapper(local)
+    # KeyFrame::ComputeBoW on the LocalMapping thread needs an ORB vocabulary: synthetic, of the
+    # ORB vocabulary's shape (k = 10, L = 6, 1.1 M nodes; the file is not available offline)
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary, Vocabulary
+    vocab = Vocabulary.synthetic(k=10, L=6, seed=7)
+    S["vocab"] = vocab
+    voc = ORBVocabulary(vocab, device=local)
+    mapper = LocalMapper(local, vocabulary=voc)
+    kf_desc = lambda f: (S["keep"][1][f].data_ptr(), S["n_lf"][f])  # noqa: E731  (the keyframe's descriptors)
     xmatch = torch.full((tr.cap,), -1, dtype=torch.int32, device=tr.kps.device)
     ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)        # extraction (E)
     trk = torch.cuda.ExternalStream(tr.track_stream_handle, device=tr.kps.device)  # tracking (T)
@@ -176,7 +183,7 @@ def run_track(a, rank, world, local, dist):
                                g_cnt.view(-1), rank, xmatch)
             S["_g"] = (g_desc, g_kps, g_cnt)  # keep alive until the stream has consumed them
         if i % KF_EVERY == 0:
-            mapper.insert_keyframe(problem)
+            mapper.insert_keyframe(problem, kf_desc(f))
 
     def sync():
         tr.synchronize()
@@ -186,12 +193,20 @@ def run_track(a, rank, world, local, dist):
     for i in range(a.warmup):
         step(i)
     sync()
-    # one LocalBA alone: its latency on an otherwise idle GPU
+    # one keyframe alone (ComputeBoW + LocalBA): its latency on an otherwise idle GPU
     t0 = time.perf_counter()
-    mapper.insert_keyframe(problem)
+    mapper.insert_keyframe(problem, kf_desc(2))
     mapper.wait()
     lba_ms = (time.perf_counter() - t0) * 1e3
     lba_info = mapper.last
+    t0 = time.perf_counter()
+    for _ in range(10):
+        b = mapper.bow
+        voc.transform_device(kf_desc(2)[0], kf_desc(2)[1], None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                             b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
+        voc.synchronize()
+    bow_us = (time.perf_counter() - t0) / 10 * 1e6
+    bow_words = int(mapper.bow["counts"][0])
 
     # per-stage profile (untimed): extractor stages via the library's event brackets
     stage = profile_stages(tr.extractor.handle, lambda i: (tr.extract_stereo(
@@ -277,7 +292,7 @@ def run_track(a, rank, world, local, dist):
                             "+ ComputeStereoMatches + TrackWithMotionModel [SearchByProjection(CF,LF,th=7), "
                             "PoseOptimization] + TrackLocalMap [SearchLocalPoints(th=1, "
                             f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
-                            "+ LocalBundleAdjustment(config 3) "
+                            "+ KeyFrame::ComputeBoW + LocalBundleAdjustment(config 3) "
                             f"every {KF_EVERY}th frame on the concurrent LocalMapping thread"
                             + ("; + RCCL all-gather of left desc/kps and cross-stream matching (config 4)"
                                if world > 1 else ""),
@@ -291,7 +306,9 @@ def run_track(a, rank, world, local, dist):
             "track_only_ms_per_frame_synced": round(track_only_ms, 4),
             "track_only_ms_per_frame_back_to_back": round(track_async_ms, 4),
             "host_enqueue_ms_per_frame": round(enqueue_ms, 4),
-            "local_ba": {"ms_per_call_idle_gpu": round(lba_ms, 3), "calls_in_timed_region": n_lba,
+            "compute_bow": {"us_per_keyframe_synced": round(bow_us, 1), "words": bow_words,
+                            "vocabulary": "synthetic k=10 L=6 (1,111,111 nodes), L1 / TF-IDF, levelsup 4"},
+            "local_ba": {"ms_per_keyframe_idle_gpu (ComputeBoW + LocalBA)": round(lba_ms, 3), "calls_in_timed_region": n_lba,
                          "iterations": list(lba_info["iterations"]) if lba_info else None,
                          "edges": int(len(problem.edges)), "points": int(len(problem.pts)),
                          "keyframes": int(len(problem.kfs))},
@@ -467,8 +484,8 @@ def cpu_baseline_track(S, problem, a):
         u, d = O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
         cf = Frame(kl, dl, u, S["tcws"][f], cam)
         O.track_frame(cf, lf_frames[f - 1], lf_points[f - 1], mps[f], inv_sigma2, 7.0)
-        if n % KF_EVERY == 0:
-            futs.append(lm.submit(O.local_ba, problem))
+        if n % KF_EVERY == 0:  # LocalMapping: KeyFrame::ComputeBoW, then LocalBundleAdjustment
+            futs.append(lm.submit(lambda dl_=dl: (O.transform(S["vocab"], dl_, 4), O.local_ba(problem))))
         n += 1
         el = time.perf_counter() - t0
         if (el >= a.cpu_sample_s and n >= KF_EVERY) or n >= 10000:
@@ -481,7 +498,7 @@ def cpu_baseline_track(S, problem, a):
     return {"value": round(n / el, 4), "unit": "frames/s", "cores": 3, "kind": "port",
             "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle extract L||R "
                       f"(2 threads) + stereo + TrackWithMotionModel + TrackLocalMap (both PoseOptimizations) serial, "
-                      f"{len(futs)} LocalBA on a 3rd thread; {el:.1f} s"}
+                      f"{len(futs)} ComputeBoW + LocalBA on a 3rd thread; {el:.1f} s"}
 
 
 # --------------------------------------------------------------------------------- extract

@@ -6,9 +6,11 @@
 //   BowVector::addWeight / addIfNotExist / normalize   Thirdparty/DBoW2/DBoW2/BowVector.cpp:34-86
 //   FeatureVector::addFeature                   Thirdparty/DBoW2/DBoW2/FeatureVector.cpp:31-45
 // Two kernels:
-//   k_bow_descend  thread per descriptor: the descriptor stays in registers (2 x uint4), every
-//                  level reads the children's 32-B descriptors (16-B loads) and keeps the first
-//                  minimum; outputs (word, weight, node at level L - levelsup).
+//   k_bow_descend16  16 lanes (one DPP row) per descriptor, lane j on child j: per level one load
+//                  of the children's 32-B descriptors, stored again in CSR order at upload (cdesc)
+//                  so a node's children are contiguous, and a DPP min; fan-out > 16 falls back to
+//                  k_bow_descend (thread per descriptor).  Outputs (word, weight, node at level
+//                  L - levelsup).
 //   k_bow_build    one 1024-thread workgroup: bitonic sort in LDS of (word << 32 | feature) keys,
 //                  segment heads -> BowVector entries in word order with the per-word weight
 //                  accumulated sequentially in feature order (as addWeight does), the L1 / L2 norm
@@ -19,6 +21,7 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "orbmi_common.h"
 
@@ -29,8 +32,9 @@ constexpr int kBowBuildThreads = 1024;
 constexpr unsigned long long kNoKey = ~0ull;
 
 struct VocDev {
-    int k, L, scoring, weighting, nnodes;
+    int k, L, scoring, weighting, nnodes, max_fanout;
     const uint4* desc;       // nnodes x 2
+    const uint4* cdesc;      // child_off[nnodes] x 2: descriptor of children[j] at j (CSR order)
     const int* child_off;
     const int* children;
     const int* word_id;
@@ -68,6 +72,51 @@ __global__ __launch_bounds__(256) void k_bow_descend(VocDev v, const uint4* __re
         }
         node = best;
         if (level == nid_level) nid = node;
+    }
+    const double w = v.weight[node];
+    const int word = v.word_id[node];
+    const bool keep = w > 0;  // "not stopped"
+    key_w[i] = keep ? ((unsigned long long)(unsigned)word << 32 | (unsigned)i) : kNoKey;
+    key_n[i] = keep ? ((unsigned long long)(unsigned)nid << 32 | (unsigned)i) : kNoKey;
+    wv[i] = w;
+}
+
+// 16 lanes per descriptor (one DPP row): lane j of the row takes child j of the current node
+// (fan-out <= 16), so a level costs one load of the children's descriptors (contiguous in CSR
+// order, cdesc) and a 4-step DPP min over (distance << 8 | child position) -- the lowest
+// position wins ties, as the reference's strict `d < best_d` scan does.
+__device__ inline unsigned row_min_u32(unsigned v) {
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));   // xor 1
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false));   // xor 2
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // mirror 8
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // ror 8
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_bow_descend16(VocDev v, const uint4* __restrict__ feats, int n,
+                                                       const int* __restrict__ n_dev, int nid_level,
+                                                       unsigned long long* __restrict__ key_w,
+                                                       unsigned long long* __restrict__ key_n, double* __restrict__ wv) {
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4, lane = threadIdx.x & 15;
+    const int nn = n_dev ? min(*n_dev, n) : n;
+    const bool valid = g < nn;
+    const int i = valid ? g : 0;  // lanes of invalid groups run along (uniform DPP rows), write nothing
+    const uint4 a0 = feats[2 * i], a1 = feats[2 * i + 1];
+    int node = 0, level = 0, nid = 0;
+    for (;;) {
+        const int c0 = v.child_off[node], c1 = v.child_off[node + 1];
+        if (c0 == c1) break;  // leaf (uniform in the row)
+        level++;
+        const int j = c0 + lane;
+        unsigned key = 0xFFFFFFFFu;
+        if (j < c1) key = (unsigned)popc256(a0, a1, v.cdesc[2 * j], v.cdesc[2 * j + 1]) << 8 | (unsigned)lane;
+        key = row_min_u32(key);
+        node = v.children[c0 + (int)(key & 0xFF)];
+        if (level == nid_level) nid = node;
+    }
+    if (!valid || lane != 0) {
+        if (lane == 0 && g < n) { key_w[g] = kNoKey; key_n[g] = kNoKey; }
+        return;
     }
     const double w = v.weight[node];
     const int word = v.word_id[node];
@@ -136,34 +185,42 @@ __global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(
     const bool tf = weighting == 0 || weighting == 1;  // TF_IDF, TF: addWeight; IDF, BINARY: addIfNotExist
     int nrm = 1;
     const bool must = must_normalize(scoring, &nrm);
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        const int k = pos[j];
-        if (k < 0) continue;
+    constexpr int PER = kBowMaxFeatures / kBowBuildThreads;
+    double val[PER];
+    int slot[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {  // segment heads: one BowVector entry each
+        const int j = threadIdx.x + q * kBowBuildThreads;
+        slot[q] = (j < m) ? pos[j] : -1;
+        val[q] = 0;
+        if (slot[q] < 0) continue;
         const unsigned word = (unsigned)(s[j] >> 32);
-        double val = wv[(unsigned)s[j]];
+        double x = wv[(unsigned)s[j]];
         if (tf)
-            for (int q = j + 1; q < m && s[q] != kNoKey && (unsigned)(s[q] >> 32) == word; q++) val += wv[(unsigned)s[q]];
-        if (tf && !must) val /= (double)nw;  // "unnecessary when normalizing": divide by v.size()
-        bow_word[k] = word;
-        bow_value[k] = val;
+            for (int r = j + 1; r < m && s[r] != kNoKey && (unsigned)(s[r] >> 32) == word; r++) x += wv[(unsigned)s[r]];
+        if (tf && !must) x /= (double)nw;  // "unnecessary when normalizing": divide by v.size()
+        bow_word[slot[q]] = word;
+        val[q] = x;
+    }
+    __syncthreads();  // the keys are dead: their LDS holds the values, in word order
+    double* vals = reinterpret_cast<double*>(s);
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+        if (slot[q] >= 0) vals[slot[q]] = val[q];
+    __syncthreads();
+    if (must && threadIdx.x == 0) {  // BowVector::normalize: sequential in word order
+        double norm = 0.0;
+        if (nrm == 1) {
+            for (int k = 0; k < nw; k++) norm += fabs(vals[k]);
+        } else {
+            for (int k = 0; k < nw; k++) norm += vals[k] * vals[k];
+            norm = sqrt(norm);
+        }
+        norm_s = norm;
     }
     __syncthreads();
-    if (must) {  // BowVector::normalize: sequential in word order
-        if (threadIdx.x == 0) {
-            double norm = 0.0;
-            if (nrm == 1) {
-                for (int k = 0; k < nw; k++) norm += fabs(bow_value[k]);
-            } else {
-                for (int k = 0; k < nw; k++) norm += bow_value[k] * bow_value[k];
-                norm = sqrt(norm);
-            }
-            norm_s = norm;
-        }
-        __syncthreads();
-        const double norm = norm_s;
-        if (norm > 0.0)
-            for (int k = threadIdx.x; k < nw; k += blockDim.x) bow_value[k] /= norm;
-    }
+    const double norm = must ? norm_s : 0.0;
+    for (int k = threadIdx.x; k < nw; k += blockDim.x) bow_value[k] = norm > 0.0 ? vals[k] / norm : vals[k];
     __syncthreads();
     // ---- FeatureVector
     for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_n[j] : kNoKey;
@@ -234,24 +291,31 @@ int orbmi_vocabulary_create(int device, const orbmi_vocabulary_desc* d, orbmi_vo
     h->device = device;
     const size_t nn = (size_t)d->nnodes;
     const size_t b_desc = align256(nn * 32), b_off = align256((nn + 1) * 4), b_ch = align256((size_t)std::max(nch, 1) * 4),
-                 b_word = align256(nn * 4), b_w = align256(nn * 8);
+                 b_word = align256(nn * 4), b_w = align256(nn * 8), b_cdesc = align256((size_t)std::max(nch, 1) * 32);
+    int max_fanout = 0;
+    for (int i = 0; i < d->nnodes; i++) max_fanout = std::max(max_fanout, d->child_off[i + 1] - d->child_off[i]);
+    std::vector<uint8_t> cdesc((size_t)std::max(nch, 1) * 32);
+    for (int j = 0; j < nch; j++) memcpy(&cdesc[(size_t)j * 32], d->desc + (size_t)d->children[j] * 32, 32);
     auto fail = [&](int rc) { orbmi_vocabulary_destroy(h); return rc; };
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(ORBMI_E_HIP);
-    if (hipMalloc(&h->d_vocab, b_desc + b_off + b_ch + b_word + b_w) != hipSuccess) return fail(ORBMI_E_HIP);
+    if (hipMalloc(&h->d_vocab, b_desc + b_off + b_ch + b_word + b_w + b_cdesc) != hipSuccess) return fail(ORBMI_E_HIP);
     uint8_t* base = (uint8_t*)h->d_vocab;
     uint8_t* p_desc = base;
     int* p_off = (int*)(base + b_desc);
     int* p_ch = (int*)(base + b_desc + b_off);
     int* p_word = (int*)(base + b_desc + b_off + b_ch);
     double* p_w = (double*)(base + b_desc + b_off + b_ch + b_word);
+    uint8_t* p_cdesc = base + b_desc + b_off + b_ch + b_word + b_w;
     if (hipMemcpy(p_desc, d->desc, nn * 32, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p_off, d->child_off, (nn + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
         (nch > 0 && hipMemcpy(p_ch, d->children, (size_t)nch * 4, hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(p_word, d->word_id, nn * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p_w, d->weight, nn * 8, hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(p_w, d->weight, nn * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        (nch > 0 && hipMemcpy(p_cdesc, cdesc.data(), (size_t)nch * 32, hipMemcpyHostToDevice) != hipSuccess))
         return fail(ORBMI_E_HIP);
-    h->v = orbmi::VocDev{d->k, d->L, d->scoring, d->weighting, d->nnodes, (const uint4*)p_desc, p_off, p_ch, p_word, p_w};
+    h->v = orbmi::VocDev{d->k, d->L, d->scoring, d->weighting, d->nnodes, max_fanout, (const uint4*)p_desc,
+                         (const uint4*)p_cdesc, p_off, p_ch, p_word, p_w};
     *out = h;
     return ORBMI_OK;
 }
@@ -324,8 +388,12 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
     int* o_cnt = dev_out(counts, s_cnt);
     const int nid_level = h->v.L - levelsup;  // <= 0: the root (node 0)
     if (n > 0) {
-        hipLaunchKernelGGL(k_bow_descend, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->v, (const uint4*)d_in, n,
-                           n_device, nid_level, key_w, key_n, wv);
+        if (h->v.max_fanout <= 16)  // one DPP row per descriptor
+            hipLaunchKernelGGL(k_bow_descend16, dim3((16 * n + 255) / 256), dim3(256), 0, h->stream, h->v,
+                               (const uint4*)d_in, n, n_device, nid_level, key_w, key_n, wv);
+        else
+            hipLaunchKernelGGL(k_bow_descend, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->v, (const uint4*)d_in,
+                               n, n_device, nid_level, key_w, key_n, wv);
         ORBMI_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_bow_build, dim3(1), dim3(kBowBuildThreads), 0, h->stream, key_w, key_n, wv, n,

@@ -11,8 +11,8 @@ One tracked stereo frame, in the order Tracking runs it (src/Tracking.cc:287-581
                       ORBmatcher(0.8).SearchByProjection(F, localMPs, th=1) at the optimised
                       pose, Optimizer::PoseOptimization, mnMatchesInliers
                                                                   src/Tracking.cc:1065-1104
-  LocalMapping thread Optimizer::LocalBundleAdjustment on every new keyframe
-                      (src/LocalMapping.cc:89-90), concurrently with tracking
+  LocalMapping thread KeyFrame::ComputeBoW + Optimizer::LocalBundleAdjustment on every new
+                      keyframe (src/LocalMapping.cc:89-90, :152-160), concurrently with tracking
 
 The tracking stages run on one HIP stream (the matcher's; the pose optimiser shares it) and the
 Frame constructor's extraction on the extractor's stream, double-buffered, so that the next
@@ -261,12 +261,25 @@ class StereoTracker:
 
 
 class LocalMapper:
-    """LocalMapping thread: runs queued LocalBundleAdjustment problems on the GPU (own stream)
-    concurrently with tracking (src/LocalMapping.cc:47-128)."""
+    """LocalMapping thread: for every queued keyframe, KeyFrame::ComputeBoW (ProcessNewKeyFrame,
+    src/LocalMapping.cc:152-160) when a vocabulary is given, then LocalBundleAdjustment
+    (src/LocalMapping.cc:89-90), on the GPU on the handles' own streams, concurrently with
+    tracking (src/LocalMapping.cc:47-128)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, vocabulary=None, max_features=8192):
+        import torch
         from .optimizer import LocalBA
         self.ba = LocalBA(device)
+        self.voc = vocabulary  # ORBVocabulary (device handle) or None
+        if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
+            dev = torch.device("cuda", device)
+            cap = max_features
+            self.bow = dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
+                            value=torch.zeros(cap, dtype=torch.float64, device=dev),
+                            node=torch.zeros(cap, dtype=torch.int32, device=dev),
+                            off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
+                            feat=torch.zeros(cap, dtype=torch.int32, device=dev),
+                            counts=torch.zeros(2, dtype=torch.int32, device=dev))
         self.q: queue.Queue = queue.Queue()
         self.done = 0
         self.last = None
@@ -281,14 +294,24 @@ class LocalMapper:
                 self.q.task_done()
                 return
             try:
-                self.last = self.ba.run(job)
+                problem, kf_desc = job
+                if self.voc is not None and kf_desc is not None:
+                    d_desc, n = kf_desc
+                    b = self.bow
+                    self.voc.transform_device(d_desc, n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                                              b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
+                                              b["counts"].data_ptr())
+                    self.voc.synchronize()
+                self.last = self.ba.run(problem)
                 self.done += 1
             except Exception as e:  # surfaced by wait()
                 self.error = e
             self.q.task_done()
 
-    def insert_keyframe(self, problem):
-        self.q.put(problem)
+    def insert_keyframe(self, problem, kf_desc=None):
+        """Queue a keyframe: its LocalBA problem and, for ComputeBoW, (device address of its
+        n x 32 descriptors, n)."""
+        self.q.put((problem, kf_desc))
 
     def wait(self):
         self.q.join()
