@@ -213,6 +213,18 @@ int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches);
 
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for np map points: the
+ * observation descriptors of point p are rows obs_off[p] .. obs_off[p + 1] - 1 of obs_desc
+ * (x 32 B), in mObservations order with bad keyframes left out by the caller (the reference
+ * iterates a map keyed by KeyFrame*; the build orders by keyframe id).
+ * best[p] = the row (within the point) of least median Hamming distance to the point's other
+ * descriptors (sorted row incl. the self-distance, element 0.5 (N - 1)), first row on ties; -1
+ * without observations.  desc_out[p] (32 B) = that descriptor (mDescriptor); left unchanged for
+ * points without observations.  Arrays host or device; asynchronous when best and desc_out are
+ * device memory. */
+int orbmi_compute_distinctive_descriptors(orbmi_matcher* m, const uint8_t* obs_desc, const int32_t* obs_off, int np,
+                                          int32_t* best, uint8_t* desc_out);
+
 /* ---- DBoW2 vocabulary: Frame::ComputeBoW / KeyFrame::ComputeBoW ---- */
 
 /* DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (Thirdparty/DBoW2/DBoW2/

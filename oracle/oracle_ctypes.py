@@ -368,3 +368,16 @@ def transform(vocab, desc, levelsup=4):
                     node.ctypes.data, off.ctypes.data, feat.ctypes.data, counts.ctypes.data)
     nw, nn = int(counts[0]), int(counts[1])
     return word[:nw], value[:nw], node[:nn], off[:nn + 1], feat[:int(off[nn])]
+
+
+def compute_distinctive_descriptors(obs_desc, obs_off):
+    """MapPoint::ComputeDistinctiveDescriptors restatement -> (best row per point, descriptors)."""
+    L = lib()
+    L.orc_compute_distinctive_descriptors.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    d = np.ascontiguousarray(obs_desc, np.uint8).reshape(-1, 32)
+    off = np.ascontiguousarray(obs_off, np.int32)
+    np_ = len(off) - 1
+    best = np.zeros(max(np_, 1), np.int32)
+    out = np.zeros((max(np_, 1), 32), np.uint8)
+    L.orc_compute_distinctive_descriptors(d.ctypes.data, off.ctypes.data, np_, best.ctypes.data, out.ctypes.data)
+    return best[:np_], out[:np_]

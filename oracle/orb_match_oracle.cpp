@@ -6,6 +6,7 @@
 // Pinned float semantics (P10): 3x3*3x1 + t products are float, left to right
 // ((r0*x + r1*y) + r2*z) + t (cv::gemm small-matrix path); -R^T t likewise; cv::norm and
 // Mat::dot accumulate in double; PredictScale uses (float)log((double)ratio).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -310,3 +311,38 @@ int orc_search_by_bow(const orbmi_frame_view* KF, const uint8_t* kf_mp_ok, const
 }
 
 }  // extern "C"
+
+// MapPoint::ComputeDistinctiveDescriptors  src/MapPoint.cc:247-316 (literal: float distance
+// matrix, std::sort of each row, vDists[0.5*(N-1)], strict < over the rows)
+extern "C" int orc_compute_distinctive_descriptors(const uint8_t* obs_desc, const int32_t* obs_off, int np,
+                                                   int32_t* best, uint8_t* desc_out) {
+    for (int p = 0; p < np; p++) {
+        const int b = obs_off[p];
+        const size_t N = (size_t)(obs_off[p + 1] - b);
+        if (N == 0) { best[p] = -1; continue; }
+        std::vector<float> Distances(N * N);
+        for (size_t i = 0; i < N; i++) {
+            Distances[i * N + i] = 0;
+            for (size_t j = i + 1; j < N; j++) {
+                int distij = 0;
+                for (int q = 0; q < 32; q++)
+                    distij += __builtin_popcount((unsigned)(obs_desc[32 * (b + i) + q] ^ obs_desc[32 * (b + j) + q]));
+                Distances[i * N + j] = (float)distij;
+                Distances[j * N + i] = (float)distij;
+            }
+        }
+        int BestMedian = 0x7FFFFFFF, BestIdx = 0;
+        for (size_t i = 0; i < N; i++) {
+            std::vector<int> vDists(Distances.begin() + i * N, Distances.begin() + (i + 1) * N);
+            std::sort(vDists.begin(), vDists.end());
+            const int median = vDists[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = (int)i;
+            }
+        }
+        best[p] = BestIdx;
+        memcpy(desc_out + 32 * (size_t)p, obs_desc + 32 * (size_t)(b + BestIdx), 32);
+    }
+    return 0;
+}

@@ -413,4 +413,27 @@ int orbmi_match_descriptors_segments(orbmi_matcher* h, const uint8_t* q_desc, in
     return finish(m, outs, m.d_scalars, nmatches);
 }
 
+int orbmi_compute_distinctive_descriptors(orbmi_matcher* h, const uint8_t* obs_desc, const int32_t* obs_off, int np,
+                                          int32_t* best, uint8_t* desc_out) {
+    if (!h || np < 0 || (np > 0 && (!obs_off || !best || !desc_out))) return ORBMI_E_ARG;
+    if (np == 0) return ORBMI_OK;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    int total = 0;
+    if (on_device(obs_off)) ORBMI_HIP(hipMemcpy(&total, obs_off + np, sizeof(int), hipMemcpyDeviceToHost));
+    else total = obs_off[np];
+    if (total < 0 || (total > 0 && !obs_desc)) return ORBMI_E_ARG;
+    int rc = 0;
+    const uint8_t* d_desc = dev_in(m, obs_desc, (size_t)total * 32, &rc);
+    const int* d_off = dev_in(m, obs_off, (size_t)np + 1, &rc);
+    if (rc) return rc;
+    std::vector<OutBuf> outs;
+    int* d_best = dev_out(m, best, (size_t)np, outs);
+    uint8_t* d_out = dev_out(m, desc_out, (size_t)np * 32, outs);
+    if (!on_device(desc_out)) ORBMI_HIP(hipMemcpyAsync(d_out, desc_out, (size_t)np * 32, hipMemcpyHostToDevice, m.stream));
+    if ((rc = orbmi::launch_distinctive(m, d_desc, d_off, np, d_best, d_out))) return rc;
+    return finish(m, outs, nullptr, nullptr);
+}
+
 }  // extern "C"

@@ -956,4 +956,52 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
     return ORBMI_OK;
 }
 
+// ---------------------------------------------------------------- MapPoint descriptor
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316): one wave per map point,
+// lane = row i of the N x N distance matrix (rows in chunks of 64).  The row's median
+// (vDists[0.5 (N - 1)] of the sorted row, self-distance 0 included) is found by a binary search
+// on the value: the smallest v with #{j : d_ij <= v} > (N - 1) / 2, 9 steps over [0, 256].  The
+// best row is the minimum of (median << 16 | i): least median, first index on ties, as the
+// reference's strict `median < BestMedian` scan.  The point's descriptors are read from L1/L2.
+__global__ __launch_bounds__(256) void k_distinctive(const uint4* __restrict__ desc, const int* __restrict__ off,
+                                                     int np, int* __restrict__ best, uint4* __restrict__ out) {
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (p >= np) return;  // whole waves
+    const int b = off[p], N = off[p + 1] - b;
+    if (N <= 0) {
+        if (lane == 0) best[p] = -1;
+        return;
+    }
+    const int k = (N - 1) / 2;  // (size_t)(0.5 * (N - 1))
+    unsigned long long bestkey = ~0ull;
+    for (int i0 = 0; i0 < N; i0 += 64) {
+        const int i = i0 + lane;
+        unsigned long long key = ~0ull;
+        if (i < N) {
+            const uint4 a0 = desc[2 * (b + i)], a1 = desc[2 * (b + i) + 1];
+            int lo = 0, hi = 256;  // answer in [lo, hi]
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                int c = 0;
+                for (int j = 0; j < N; j++) c += popc256(a0, a1, desc[2 * (b + j)], desc[2 * (b + j) + 1]) <= mid;
+                if (c > k) hi = mid;
+                else lo = mid + 1;
+            }
+            key = (unsigned long long)lo << 32 | (unsigned)i;
+        }
+        key = wave_min_u64(key);
+        bestkey = key < bestkey ? key : bestkey;
+    }
+    const int bi = (int)(unsigned)bestkey;
+    if (lane == 0) best[p] = bi;
+    if (lane < 2) out[2 * p + lane] = desc[2 * (b + bi) + lane];
+}
+
+int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out) {
+    if (np <= 0) return ORBMI_OK;
+    hipLaunchKernelGGL(k_distinctive, dim3((np + 3) / 4), dim3(256), 0, m.stream, (const uint4*)desc, off, np, best,
+                       (uint4*)out);
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+}
+
 }  // namespace orbmi

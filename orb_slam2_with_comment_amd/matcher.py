@@ -82,6 +82,19 @@ class ORBmatcher:
                                                           int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)))
         return out[:len(cf.keys)], n.value
 
+    def ComputeDistinctiveDescriptors(self, obs_desc: np.ndarray, obs_off: np.ndarray, desc_out=None):
+        """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for a batch of map
+        points: rows obs_off[p]..obs_off[p+1] of obs_desc are point p's observation descriptors.
+        Returns (best row per point, -1 without observations; np x 32 mDescriptor)."""
+        d = np.ascontiguousarray(obs_desc, np.uint8).reshape(-1, 32)
+        off = np.ascontiguousarray(obs_off, np.int32)
+        n = len(off) - 1
+        best = np.zeros(max(n, 1), np.int32)
+        out = np.zeros((max(n, 1), 32), np.uint8) if desc_out is None else np.ascontiguousarray(desc_out, np.uint8)
+        check("orbmi_compute_distinctive_descriptors", lib().orbmi_compute_distinctive_descriptors(
+            self._h, d.ctypes.data if len(d) else None, off.ctypes.data, n, best.ctypes.data, out.ctypes.data))
+        return best[:n], out[:n]
+
     def SearchByBoW(self, kf, kf_mp_ok, kf_fv, f, f_fv):
         """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:211-344)."""
         ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
