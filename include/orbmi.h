@@ -213,6 +213,20 @@ int orbmi_search_by_bow(orbmi_matcher* m, const orbmi_frame_view* KF, const uint
                         const orbmi_feature_vector* f_fv, float nnratio, int check_ori, int32_t* match_kf,
                         int* nmatches);
 
+/* ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+ * vector<pair<size_t,size_t>>& vMatchedPairs, bool bOnlyStereo) (src/ORBmatcher.cc:783-975)
+ * with CheckDistEpipolarLine (:173-196): KF1 / KF2 views need keys_un, u_right, desc, tcw, the
+ * intrinsics and scale factors (mvLevelSigma2 = scale^2); has_mp[i] = pKF->GetMapPoint(i) !=
+ * NULL; fv = the keyframes' mFeatVec; F12 = LocalMapping::ComputeF12 (3x3 row-major float, host
+ * or device).  match12[i1] (KF1.n entries) = the KF2 keypoint paired with KF1 keypoint i1, else
+ * -1 (vMatchedPairs = the pairs in i1 order); *nmatches = the return value.  The reference
+ * never marks KF2 keypoints as used (vbMatched2 stays false), so one KF2 keypoint may pair with
+ * several KF1 keypoints, as here. */
+int orbmi_search_for_triangulation(orbmi_matcher* m, const orbmi_frame_view* KF1, const uint8_t* has_mp1,
+                                   const orbmi_feature_vector* fv1, const orbmi_frame_view* KF2, const uint8_t* has_mp2,
+                                   const orbmi_feature_vector* fv2, const float* F12, int only_stereo, int check_ori,
+                                   int32_t* match12, int* nmatches);
+
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for np map points: the
  * observation descriptors of point p are rows obs_off[p] .. obs_off[p + 1] - 1 of obs_desc
  * (x 32 B), in mObservations order with bad keyframes left out by the caller (the reference

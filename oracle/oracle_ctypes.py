@@ -381,3 +381,19 @@ def compute_distinctive_descriptors(obs_desc, obs_off):
     out = np.zeros((max(np_, 1), 32), np.uint8)
     L.orc_compute_distinctive_descriptors(d.ctypes.data, off.ctypes.data, np_, best.ctypes.data, out.ctypes.data)
     return best[:np_], out[:np_]
+
+
+def search_for_triangulation(kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, only_stereo=False, check_ori=True):
+    """ORBmatcher::SearchForTriangulation restatement -> (match12, nmatches)."""
+    L = lib()
+    L.orc_search_for_triangulation.argtypes = [C.c_void_p] * 7 + [C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+    m1 = np.ascontiguousarray(has_mp1, np.uint8)
+    m2 = np.ascontiguousarray(has_mp2, np.uint8)
+    F = np.ascontiguousarray(F12, np.float32).reshape(3, 3)
+    out = np.zeros(max(len(kf1.keys), 1), np.int32)
+    n = C.c_int()
+    v1, v2, f1, f2 = kf1.view(), kf2.view(), fv1.view(), fv2.view()
+    L.orc_search_for_triangulation(C.addressof(v1), m1.ctypes.data, C.addressof(f1), C.addressof(v2), m2.ctypes.data,
+                                   C.addressof(f2), F.ctypes.data, int(only_stereo), int(check_ori), out.ctypes.data,
+                                   C.byref(n))
+    return out[:len(kf1.keys)], n.value

@@ -346,3 +346,93 @@ extern "C" int orc_compute_distinctive_descriptors(const uint8_t* obs_desc, cons
     }
     return 0;
 }
+
+// ORBmatcher::SearchForTriangulation  src/ORBmatcher.cc:783-975 with CheckDistEpipolarLine
+// (:173-196) and ComputeThreeMaxima.  Literal: FeatureVector merge-join, no exclusion of already
+// matched KF2 keypoints (vbMatched2 is never set in the reference), the last candidate of equal
+// distance that passes the epipolar test wins.  The epipole uses the camera centre
+// Ow1 = -R1w^T t1w and C2 = R2w Ow1 + t2w with the P10 float order.
+extern "C" int orc_search_for_triangulation(const orbmi_frame_view* KF1, const uint8_t* has_mp1,
+                                            const orbmi_feature_vector* fv1, const orbmi_frame_view* KF2,
+                                            const uint8_t* has_mp2, const orbmi_feature_vector* fv2,
+                                            const float* F12, int only_stereo, int check_ori, int32_t* match12,
+                                            int* nmatches_out) {
+    const float* T1 = KF1->tcw;
+    const float* T2 = KF2->tcw;
+    float Ow[3];
+    for (int i = 0; i < 3; i++) Ow[i] = -(((T1[0 * 4 + i] * T1[3]) + T1[1 * 4 + i] * T1[7]) + T1[2 * 4 + i] * T1[11]);
+    float C2[3];
+    for (int i = 0; i < 3; i++) C2[i] = (((T2[i * 4 + 0] * Ow[0]) + T2[i * 4 + 1] * Ow[1]) + T2[i * 4 + 2] * Ow[2]) + T2[i * 4 + 3];
+    const float invz = 1.0f / C2[2];
+    const float ex = KF2->fx * C2[0] * invz + KF2->cx;
+    const float ey = KF2->fy * C2[1] * invz + KF2->cy;
+    std::vector<float> sigma2(KF2->nlevels);
+    for (int l = 0; l < KF2->nlevels; l++) sigma2[l] = KF2->scale_factors[l] * KF2->scale_factors[l];
+    int nmatches = 0;
+    for (int i = 0; i < KF1->n; i++) match12[i] = -1;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    auto check_epi = [&](const orbmi_keypoint& kp1, const orbmi_keypoint& kp2) {
+        const float a = kp1.x * F12[0 * 3 + 0] + kp1.y * F12[1 * 3 + 0] + F12[2 * 3 + 0];
+        const float b = kp1.x * F12[0 * 3 + 1] + kp1.y * F12[1 * 3 + 1] + F12[2 * 3 + 1];
+        const float c = kp1.x * F12[0 * 3 + 2] + kp1.y * F12[1 * 3 + 2] + F12[2 * 3 + 2];
+        const float num = a * kp2.x + b * kp2.y + c;
+        const float den = a * a + b * b;
+        if (den == 0) return false;
+        const float dsqr = num * num / den;
+        return dsqr < 3.84 * sigma2[kp2.octave];
+    };
+    int a = 0, b = 0;
+    while (a < fv1->nnodes && b < fv2->nnodes) {
+        if (fv1->node_id[a] == fv2->node_id[b]) {
+            for (int i1 = fv1->off[a]; i1 < fv1->off[a + 1]; i1++) {
+                const int idx1 = fv1->feat[i1];
+                if (has_mp1[idx1]) continue;
+                const bool bStereo1 = KF1->u_right[idx1] >= 0;
+                if (only_stereo && !bStereo1) continue;
+                const orbmi_keypoint& kp1 = KF1->keys_un[idx1];
+                const uint8_t* d1 = KF1->desc + 32 * (size_t)idx1;
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int i2 = fv2->off[b]; i2 < fv2->off[b + 1]; i2++) {
+                    const int idx2 = fv2->feat[i2];
+                    if (has_mp2[idx2]) continue;
+                    const bool bStereo2 = KF2->u_right[idx2] >= 0;
+                    if (only_stereo && !bStereo2) continue;
+                    int dist = 0;
+                    for (int q = 0; q < 32; q++) dist += __builtin_popcount((unsigned)(d1[q] ^ KF2->desc[32 * (size_t)idx2 + q]));
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const orbmi_keypoint& kp2 = KF2->keys_un[idx2];
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ex - kp2.x;
+                        const float distey = ey - kp2.y;
+                        if (distex * distex + distey * distey < 100 * KF2->scale_factors[kp2.octave]) continue;
+                    }
+                    if (check_epi(kp1, kp2)) {
+                        bestIdx2 = idx2;
+                        bestDist = dist;
+                    }
+                }
+                if (bestIdx2 >= 0) {
+                    match12[idx1] = bestIdx2;
+                    nmatches++;
+                    if (check_ori) rotHist[rot_bin(kp1.angle, KF2->keys_un[bestIdx2].angle)].push_back(idx1);
+                }
+            }
+            a++;
+            b++;
+        } else if (fv1->node_id[a] < fv2->node_id[b]) {
+            while (a < fv1->nnodes && fv1->node_id[a] < fv2->node_id[b]) a++;
+        } else {
+            while (b < fv2->nnodes && fv2->node_id[b] < fv1->node_id[a]) b++;
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int idx1 : rotHist[i]) { match12[idx1] = -1; nmatches--; }
+        }
+    }
+    *nmatches_out = nmatches;
+    return 0;
+}

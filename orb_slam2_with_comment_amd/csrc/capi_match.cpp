@@ -436,4 +436,36 @@ int orbmi_compute_distinctive_descriptors(orbmi_matcher* h, const uint8_t* obs_d
     return finish(m, outs, nullptr, nullptr);
 }
 
+int orbmi_search_for_triangulation(orbmi_matcher* h, const orbmi_frame_view* kf1, const uint8_t* has_mp1,
+                                   const orbmi_feature_vector* fv1, const orbmi_frame_view* kf2, const uint8_t* has_mp2,
+                                   const orbmi_feature_vector* fv2, const float* F12, int only_stereo, int check_ori,
+                                   int32_t* match12, int* nmatches) {
+    if (!h || !has_mp1 || !has_mp2 || !F12 || !match12 || !kf1 || !kf2 || !kf1->u_right || !kf2->u_right)
+        return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame K1, K2;
+    DevFV f1, f2;
+    int rc;
+    if ((rc = make_frame(m, kf1, &K1, true))) return rc;
+    if ((rc = make_frame(m, kf2, &K2, true))) return rc;
+    if ((rc = make_fv(m, fv1, &f1))) return rc;
+    if ((rc = make_fv(m, fv2, &f2))) return rc;
+    const uint8_t* d_mp1 = dev_in(m, has_mp1, (size_t)std::max(K1.n, 1), &rc);
+    const uint8_t* d_mp2 = dev_in(m, has_mp2, (size_t)std::max(K2.n, 1), &rc);
+    if (rc) return rc;
+    float F[9];
+    if (on_device(F12)) ORBMI_HIP(hipMemcpy(F, F12, sizeof(F), hipMemcpyDeviceToHost));
+    else memcpy(F, F12, sizeof(F));
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_out = dev_out(m, match12, (size_t)K1.n, outs);
+    if ((rc = orbmi::launch_triangulation(m, K1, d_mp1, f1, K2, d_mp2, f2, F, only_stereo, check_ori, d_out,
+                                          m.d_scalars)))
+        return rc;
+    ORBMI_HIP(hipGetLastError());
+    return finish(m, outs, m.d_scalars, nmatches);
+}
+
 }  // extern "C"

@@ -83,6 +83,9 @@ int launch_track_update(Matcher& m, const DevFrame& F, int stage, const uint8_t*
                         int n_mp, uint8_t* occ_out, int* counts);
 int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
                const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
+int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1,
+                         const DevFrame& KF2, const uint8_t* has_mp2, const DevFV& fv2, const float* F12,
+                         int only_stereo, int check_ori, int* match, int* nmatches);
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
                   int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches);

@@ -28,6 +28,8 @@ namespace orbmi {
 constexpr int kGridCols = 64, kGridRows = 48, kGridCells = kGridCols * kGridRows;
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
 
+struct Mat3f { float m[9]; };  // row-major 3x3 (by value)
+
 __device__ inline int popc_desc(const uint8_t* a, const uint8_t* b) {
     const uint4* x = reinterpret_cast<const uint4*>(a);
     const uint4* y = reinterpret_cast<const uint4*>(b);
@@ -952,6 +954,104 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
         hipLaunchKernelGGL(k_bow_match, dim3((kfv.nnodes + 3) / 4), dim3(256), 0, m.stream, KF, kf_ok, kfv, F, fv,
                            nnratio, check_ori, match, m.d_bin_of, m.d_hist);
     hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, F, check_ori, m.d_hist, m.d_bin_of, match,
+                       nmatches);
+    return ORBMI_OK;
+}
+
+// ------------------------------------------------------------- SearchForTriangulation
+// ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:783-975): one wave per KF1 vocabulary
+// node (merge-join partner found by lower_bound), KF1 features of the node in order, KF2
+// features of the node across the lanes.  The reference keeps no exclusion state (vbMatched2
+// is never set), so features are independent; its scan `if (dist > bestDist) continue; ...
+// if (CheckDistEpipolarLine) {bestIdx2 = idx2; bestDist = dist;}` ends on the smallest distance
+// <= TH_LOW among the candidates that pass, the LAST one on ties: key (dist << 32 | ~pos), min.
+// CheckDistEpipolarLine (:173-196) compares in double (3.84 * sigma2); the epipole and the
+// keyframe-1 centre follow the P10 float order.  The rotation histogram is k_bow_finalize's.
+__global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* __restrict__ has_mp1, DevFV fv1,
+                                                   DevFrame KF2, const uint8_t* __restrict__ has_mp2, DevFV fv2,
+                                                   Mat3f F12, int only_stereo, int check_ori, int* __restrict__ match,
+                                                   int* __restrict__ bin_of, int* __restrict__ hist) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int a = blockIdx.x * 4 + wid;
+    if (a >= fv1.nnodes) return;
+    const unsigned id = fv1.node_id[a];
+    int lo = 0, hi = fv2.nnodes;  // lower_bound
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv2.node_id[mid] < id) lo = mid + 1; else hi = mid; }
+    if (lo >= fv2.nnodes || fv2.node_id[lo] != id) return;
+    const int f0 = fv2.off[lo], nf = fv2.off[lo + 1] - f0;
+    // epipole of KF1's centre in KF2
+    const Pose34 T1 = frame_pose(KF1), T2 = frame_pose(KF2);
+    float Ow[3], C2[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) Ow[i] = -(((T1.m[0 * 4 + i] * T1.m[3]) + T1.m[1 * 4 + i] * T1.m[7]) + T1.m[2 * 4 + i] * T1.m[11]);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        C2[i] = (((T2.m[i * 4 + 0] * Ow[0]) + T2.m[i * 4 + 1] * Ow[1]) + T2.m[i * 4 + 2] * Ow[2]) + T2.m[i * 4 + 3];
+    const float invz = 1.0f / C2[2];
+    const float ex = KF2.fx * C2[0] * invz + KF2.cx;
+    const float ey = KF2.fy * C2[1] * invz + KF2.cy;
+    for (int ia = fv1.off[a]; ia < fv1.off[a + 1]; ia++) {
+        const int idx1 = fv1.feat[ia];
+        if (has_mp1[idx1]) continue;
+        const bool st1 = KF1.u_right[idx1] >= 0;
+        if (only_stereo && !st1) continue;
+        const orbmi_keypoint kp1 = KF1.keys[idx1];
+        const uint8_t* d1 = KF1.desc + 32 * (long long)idx1;
+        // epipolar line of kp1 in KF2: l = x1' F12
+        const float la = kp1.x * F12.m[0] + kp1.y * F12.m[3] + F12.m[6];
+        const float lb = kp1.x * F12.m[1] + kp1.y * F12.m[4] + F12.m[7];
+        const float lc = kp1.x * F12.m[2] + kp1.y * F12.m[5] + F12.m[8];
+        unsigned long long key = ~0ull;
+        for (int pos = lane; pos < nf; pos += 64) {
+            const int idx2 = fv2.feat[f0 + pos];
+            if (has_mp2[idx2]) continue;
+            const bool st2 = KF2.u_right[idx2] >= 0;
+            if (only_stereo && !st2) continue;
+            const int dist = popc_desc(d1, KF2.desc + 32 * (long long)idx2);
+            if (dist > TH_LOW) continue;
+            const orbmi_keypoint kp2 = KF2.keys[idx2];
+            if (!st1 && !st2) {
+                const float distex = ex - kp2.x;
+                const float distey = ey - kp2.y;
+                if (distex * distex + distey * distey < 100 * KF2.scale[kp2.octave]) continue;
+            }
+            const float num = la * kp2.x + lb * kp2.y + lc;
+            const float den = la * la + lb * lb;
+            if (den == 0) continue;
+            const float dsqr = num * num / den;
+            const float sigma2 = KF2.scale[kp2.octave] * KF2.scale[kp2.octave];
+            if (!((double)dsqr < 3.84 * (double)sigma2)) continue;
+            const unsigned long long k = (unsigned long long)dist << 32 | (unsigned)(0xFFFFFFFFu - (unsigned)pos);
+            key = k < key ? k : key;
+        }
+        key = wave_min_u64(key);
+        if (key != ~0ull && lane == 0) {
+            const int pos = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFu));
+            const int idx2 = fv2.feat[f0 + pos];
+            match[idx1] = idx2;
+            if (check_ori) {
+                const int bin = rot_bin(kp1.angle, KF2.keys[idx2].angle);
+                bin_of[idx1] = bin;
+                atomicAdd(&hist[bin], 1);
+            }
+        }
+    }
+}
+
+int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1,
+                         const DevFrame& KF2, const uint8_t* has_mp2, const DevFV& fv2, const float* F12,
+                         int only_stereo, int check_ori, int* match, int* nmatches) {
+    int rc;
+    if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, (size_t)std::max(KF1.n, 1)))) return rc;
+    if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH))) return rc;
+    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, HISTO_LENGTH * sizeof(int), m.stream));
+    ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)std::max(KF1.n, 1) * sizeof(int), m.stream));
+    Mat3f F;
+    for (int q = 0; q < 9; q++) F.m[q] = F12[q];
+    if (fv1.nnodes > 0)
+        hipLaunchKernelGGL(k_tri_match, dim3((fv1.nnodes + 3) / 4), dim3(256), 0, m.stream, KF1, has_mp1, fv1, KF2, has_mp2,
+                           fv2, F, only_stereo, check_ori, match, m.d_bin_of, m.d_hist);
+    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, KF1, check_ori, m.d_hist, m.d_bin_of, match,
                        nmatches);
     return ORBMI_OK;
 }

@@ -82,6 +82,23 @@ class ORBmatcher:
                                                           int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)))
         return out[:len(cf.keys)], n.value
 
+    def SearchForTriangulation(self, kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, bOnlyStereo=False):
+        """SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12, vector<pair<size_t,size_t>>&,
+        bool) (src/ORBmatcher.cc:783-975): kf1 / kf2 are types.Frame (keys_un, u_right, desc, tcw),
+        has_mp = GetMapPoint(i) != NULL, fv = mFeatVec.  Returns (match12, nmatches); the matched
+        pairs are (i, match12[i]) for match12[i] >= 0."""
+        m1 = np.ascontiguousarray(has_mp1, np.uint8)
+        m2 = np.ascontiguousarray(has_mp2, np.uint8)
+        F = np.ascontiguousarray(F12, np.float32).reshape(3, 3)
+        out = np.zeros(max(len(kf1.keys), 1), np.int32)
+        n = C.c_int()
+        v1, v2, f1, f2 = kf1.view(), kf2.view(), fv1.view(), fv2.view()
+        check("orbmi_search_for_triangulation", lib().orbmi_search_for_triangulation(
+            self._h, C.addressof(v1), m1.ctypes.data, C.addressof(f1), C.addressof(v2), m2.ctypes.data,
+            C.addressof(f2), F.ctypes.data, int(bOnlyStereo), int(self.mbCheckOrientation), out.ctypes.data,
+            C.byref(n)))
+        return out[:len(kf1.keys)], n.value
+
     def ComputeDistinctiveDescriptors(self, obs_desc: np.ndarray, obs_off: np.ndarray, desc_out=None):
         """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for a batch of map
         points: rows obs_off[p]..obs_off[p+1] of obs_desc are point p's observation descriptors.
