@@ -227,6 +227,21 @@ int orbmi_search_for_triangulation(orbmi_matcher* m, const orbmi_frame_view* KF1
                                    const orbmi_feature_vector* fv2, const float* F12, int only_stereo, int check_ori,
                                    int32_t* match12, int* nmatches);
 
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th)
+ * (src/ORBmatcher.cc:977-1127), its search: for each of the n_mp candidate map points (in
+ * vpMapPoints order; NULL entries left out by the caller, isBad() as ORBMI_MP_BAD, in_kf[i] =
+ * IsInKeyFrame(pKF), in_kf may be NULL) the keyframe keypoint it fuses with: best_idx[i] (-1
+ * when the point is skipped or its best distance exceeds TH_LOW = 50) and best_dist[i] (256
+ * without a candidate).  The KF view needs keys_un, u_right (NULL = monocular), desc, tcw, the
+ * intrinsics, bounds (mnMinX.., IsInImage) and scale factors.  The map updates stay with the
+ * caller, replayed in list order as the reference does them: skip points that became bad or
+ * joined pKF meanwhile; pMPinKF = pKF->GetMapPoint(best_idx[i]): if present and not bad,
+ * Replace toward the point with more observations, otherwise AddObservation + AddMapPoint;
+ * count nFused.  *ncandidates = the points with best_idx >= 0 (= nFused when
+ * the replay skips none). */
+int orbmi_fuse_search(orbmi_matcher* m, const orbmi_frame_view* KF, const orbmi_mappoint* mps, const uint8_t* in_kf,
+                      int n_mp, float th, int32_t* best_idx, int32_t* best_dist, int* ncandidates);
+
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for np map points: the
  * observation descriptors of point p are rows obs_off[p] .. obs_off[p + 1] - 1 of obs_desc
  * (x 32 B), in mObservations order with bad keyframes left out by the caller (the reference

@@ -397,3 +397,18 @@ def search_for_triangulation(kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, only_ste
                                    C.addressof(f2), F.ctypes.data, int(only_stereo), int(check_ori), out.ctypes.data,
                                    C.byref(n))
     return out[:len(kf1.keys)], n.value
+
+
+def fuse_search(kf, mps, in_kf=None, th=3.0):
+    """ORBmatcher::Fuse search restatement -> (best_idx, best_dist, ncandidates)."""
+    L = lib()
+    L.orc_fuse_search.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+    mps = np.ascontiguousarray(mps)
+    n = len(mps)
+    ink = None if in_kf is None else np.ascontiguousarray(in_kf, np.uint8)
+    bi, bd = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.int32)
+    c = C.c_int()
+    v = kf.view()
+    L.orc_fuse_search(C.addressof(v), mps.ctypes.data, None if ink is None else ink.ctypes.data, n, th, bi.ctypes.data,
+                      bd.ctypes.data, C.byref(c))
+    return bi[:n], bd[:n], c.value

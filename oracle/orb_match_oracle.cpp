@@ -436,3 +436,74 @@ extern "C" int orc_search_for_triangulation(const orbmi_frame_view* KF1, const u
     *nmatches_out = nmatches;
     return 0;
 }
+
+// ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th)  src/ORBmatcher.cc:977-1127, the
+// search part in list order (the map updates are the caller's replay, include/orbmi.h).
+extern "C" int orc_fuse_search(const orbmi_frame_view* KF, const orbmi_mappoint* mps, const uint8_t* in_kf, int n_mp,
+                               float th, int32_t* best_idx, int32_t* best_dist, int* ncand) {
+    Grid g;
+    build_grid(*KF, g);
+    float Ow[3];
+    camera_center(KF->tcw, Ow);
+    std::vector<int> idxs;
+    int n = 0;
+    for (int i = 0; i < n_mp; i++) {
+        best_idx[i] = -1;
+        best_dist[i] = 256;
+        const orbmi_mappoint& mp = mps[i];
+        if ((mp.flags & ORBMI_MP_BAD) || (in_kf && in_kf[i])) continue;
+        float p3Dc[3];
+        transform(KF->tcw, mp.pos, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue;  // IsInImage
+        const float ur = u - KF->bf * invz;
+        const float maxDistance = 1.2f * mp.max_distance;
+        const float minDistance = 0.8f * mp.min_distance;
+        const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
+        const float dist3D = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const double dot = (double)PO[0] * mp.normal[0] + (double)PO[1] * mp.normal[1] + (double)PO[2] * mp.normal[2];
+        if (dot < 0.5 * dist3D) continue;
+        const float ratio = mp.max_distance / dist3D;
+        int nPredictedLevel = (int)ceilf((float)log((double)ratio) / KF->log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= KF->nlevels) nPredictedLevel = KF->nlevels - 1;
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        features_in_area(*KF, g, u, v, radius, -1, -1, idxs);
+        if (idxs.empty()) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (int idx : idxs) {
+            const orbmi_keypoint& kp = KF->keys_un[idx];
+            const int kpLevel = kp.octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const float sigma2 = KF->scale_factors[kpLevel] * KF->scale_factors[kpLevel];
+            const float inv = 1.0f / sigma2;  // mvInvLevelSigma2
+            if (KF->u_right && KF->u_right[idx] >= 0) {
+                const float ex = u - kp.x, ey = v - kp.y, er = ur - KF->u_right[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if (e2 * inv > 7.8) continue;
+            } else {
+                const float ex = u - kp.x, ey = v - kp.y;
+                const float e2 = ex * ex + ey * ey;
+                if (e2 * inv > 5.99) continue;
+            }
+            const int dist = hamming(mp.desc, KF->desc + 32 * idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        best_dist[i] = bestDist;
+        if (bestDist <= TH_LOW) {
+            best_idx[i] = bestIdx;
+            n++;
+        }
+    }
+    *ncand = n;
+    return 0;
+}

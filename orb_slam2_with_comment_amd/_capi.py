@@ -83,6 +83,7 @@ _PROTOS = {
     "orbmi_vocabulary_synchronize": (_i, [_vp]),
     "orbmi_transform": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
+    "orbmi_fuse_search": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, _vp, C.POINTER(_i)]),
     "orbmi_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, C.POINTER(_i)]),
     "orbmi_pose_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_pose_optimization_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

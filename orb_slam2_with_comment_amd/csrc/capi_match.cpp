@@ -468,4 +468,24 @@ int orbmi_search_for_triangulation(orbmi_matcher* h, const orbmi_frame_view* kf1
     return finish(m, outs, m.d_scalars, nmatches);
 }
 
+int orbmi_fuse_search(orbmi_matcher* h, const orbmi_frame_view* kf, const orbmi_mappoint* mps, const uint8_t* in_kf,
+                      int n_mp, float th, int32_t* best_idx, int32_t* best_dist, int* ncandidates) {
+    if (!h || !kf || n_mp < 0 || (n_mp > 0 && (!mps || !best_idx || !best_dist))) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, kf, &F, true))) return rc;
+    const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
+    const uint8_t* d_in = dev_in(m, in_kf, in_kf ? (size_t)std::max(n_mp, 1) : 0, &rc);
+    if (rc) return rc;
+    if ((rc = scalars(m))) return rc;
+    std::vector<OutBuf> outs;
+    int* d_bi = dev_out(m, best_idx, (size_t)n_mp, outs);
+    int* d_bd = dev_out(m, best_dist, (size_t)n_mp, outs);
+    if ((rc = orbmi::launch_fuse(m, F, d_mps, d_in, n_mp, th, d_bi, d_bd, m.d_scalars))) return rc;
+    return finish(m, outs, m.d_scalars, ncandidates);
+}
+
 }  // extern "C"

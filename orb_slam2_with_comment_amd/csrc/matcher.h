@@ -86,6 +86,8 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
 int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1,
                          const DevFrame& KF2, const uint8_t* has_mp2, const DevFV& fv2, const float* F12,
                          int only_stereo, int check_ori, int* match, int* nmatches);
+int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
+                int* best_idx, int* best_dist, int* ncand);
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
                   int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches);

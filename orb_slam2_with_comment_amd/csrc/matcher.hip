@@ -1056,6 +1056,96 @@ int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1
     return ORBMI_OK;
 }
 
+// -------------------------------------------------------------------------- Fuse
+// ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:977-1127), the
+// search: thread per candidate map point.  Projection (P10 order), KeyFrame::IsInImage, the
+// scale-invariance and 60-degree viewing tests, PredictScale, KeyFrame::GetFeaturesInArea
+// without level limits, the level window [pred - 1, pred], the chi2 gates on the reprojection
+// error (double compares against 7.8 / 5.99) and the descriptor distance; the first keypoint of
+// the reference's grid order wins ties (key dist << 40 | cell << 20 | idx).  The map updates
+// (Replace / AddObservation) are the caller's sequential replay of (best_idx, best_dist) in
+// list order (include/orbmi.h).
+__global__ __launch_bounds__(256) void k_fuse(DevFrame F, const int* __restrict__ cs, const int* __restrict__ cl,
+                                              const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf,
+                                              int n, float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
+                                              int* __restrict__ ncand) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int bi = -1, bd = 256;
+    const orbmi_mappoint mp = mps[i];
+    const Pose34 T = frame_pose(F);
+    float Pc[3];
+    bool ok = !(mp.flags & ORBMI_MP_BAD) && !(in_kf && in_kf[i]);
+    if (ok) {
+        transform(T.m, mp.pos, Pc);
+        ok = !(Pc[2] < 0.0f);
+    }
+    float u = 0, v = 0, invz = 0, dist3D = 0;
+    if (ok) {
+        invz = 1.0f / Pc[2];
+        const float x = Pc[0] * invz, y = Pc[1] * invz;
+        u = F.fx * x + F.cx;
+        v = F.fy * y + F.cy;
+        ok = u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y;  // KeyFrame::IsInImage
+    }
+    if (ok) {
+        float Ow[3];
+        camera_center(T.m, Ow);
+        const float maxDistance = 1.2f * mp.max_distance, minDistance = 0.8f * mp.min_distance;
+        const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
+        dist3D = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        ok = !(dist3D < minDistance || dist3D > maxDistance);
+        if (ok) {
+            const double dot = (double)PO[0] * mp.normal[0] + (double)PO[1] * mp.normal[1] + (double)PO[2] * mp.normal[2];
+            ok = !(dot < 0.5 * (double)dist3D);
+        }
+    }
+    if (ok) {
+        const float ratio = mp.max_distance / dist3D;  // MapPoint::PredictScale(dist, KeyFrame*)
+        int nPredictedLevel = (int)ceilf((float)log((double)ratio) / F.log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= F.nlevels) nPredictedLevel = F.nlevels - 1;
+        const float radius = th * F.scale[nPredictedLevel];
+        const float ur = u - F.bf * invz;
+        unsigned long long best = ~0ull;
+        for_features_in_area(F, cs, cl, u, v, radius, -1, -1, [&](int idx, int cell) {
+            const orbmi_keypoint kp = F.keys[idx];
+            const int kpLevel = kp.octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) return;
+            const float inv = 1.0f / (F.scale[kpLevel] * F.scale[kpLevel]);  // mvInvLevelSigma2
+            const float ex = u - kp.x, ey = v - kp.y;
+            if (F.u_right && F.u_right[idx] >= 0) {
+                const float er = ur - F.u_right[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if ((double)(e2 * inv) > 7.8) return;
+            } else {
+                const float e2 = ex * ex + ey * ey;
+                if ((double)(e2 * inv) > 5.99) return;
+            }
+            const unsigned long long e = cand_entry(popc_desc(mp.desc, F.desc + 32 * (long long)idx), cell, idx);
+            best = e < best ? e : best;
+        });
+        if (best != ~0ull) {
+            bd = (int)(best >> 40);
+            bi = (int)(best & 0xFFFFF);
+        }
+    }
+    const bool fused = bi >= 0 && bd <= TH_LOW;
+    best_idx[i] = fused ? bi : -1;
+    best_dist[i] = bi >= 0 ? bd : 256;
+    if (fused) atomicAdd(ncand, 1);
+}
+
+int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
+                int* best_idx, int* best_dist, int* ncand) {
+    int rc;
+    if ((rc = grid_for(m, F))) return rc;
+    if (n > 0)
+        hipLaunchKernelGGL(k_fuse, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start, m.d_cell_list,
+                           mps, in_kf, n, th, best_idx, best_dist, ncand);
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+}
+
 // ---------------------------------------------------------------- MapPoint descriptor
 // MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316): one wave per map point,
 // lane = row i of the N x N distance matrix (rows in chunks of 64).  The row's median

@@ -99,6 +99,21 @@ class ORBmatcher:
             C.byref(n)))
         return out[:len(kf1.keys)], n.value
 
+    def FuseSearch(self, kf, mps, in_kf=None, th=3.0):
+        """The search of Fuse(KeyFrame*, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:977-1127):
+        -> (best_idx, best_dist, ncandidates); the Replace / AddObservation replay in list order
+        is the caller's (include/orbmi.h)."""
+        mps = np.ascontiguousarray(mps)
+        n = len(mps)
+        ink = None if in_kf is None else np.ascontiguousarray(in_kf, np.uint8)
+        bi, bd = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.int32)
+        c = C.c_int()
+        v = kf.view()
+        check("orbmi_fuse_search", lib().orbmi_fuse_search(
+            self._h, C.addressof(v), mps.ctypes.data if n else None, None if ink is None else ink.ctypes.data, n,
+            th, bi.ctypes.data, bd.ctypes.data, C.byref(c)))
+        return bi[:n], bd[:n], c.value
+
     def ComputeDistinctiveDescriptors(self, obs_desc: np.ndarray, obs_off: np.ndarray, desc_out=None):
         """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for a batch of map
         points: rows obs_off[p]..obs_off[p+1] of obs_desc are point p's observation descriptors.
