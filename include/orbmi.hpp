@@ -199,12 +199,92 @@ public:
         return n;
     }
 
+    // SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12, vector<pair<size_t,size_t>>&,
+    // bool bOnlyStereo) (src/ORBmatcher.cc:783-975): the matched pairs in i1 order
+    int SearchForTriangulation(const orbmi_frame_view& KF1, const std::vector<uint8_t>& hasMapPoint1,
+                               const orbmi_feature_vector& fv1, const orbmi_frame_view& KF2,
+                               const std::vector<uint8_t>& hasMapPoint2, const orbmi_feature_vector& fv2,
+                               const float F12[9], std::vector<std::pair<size_t, size_t>>& vMatchedPairs,
+                               bool bOnlyStereo) {
+        std::vector<int32_t> m12(KF1.n > 0 ? KF1.n : 1, -1);
+        int n = 0;
+        check(orbmi_search_for_triangulation(h_, &KF1, hasMapPoint1.data(), &fv1, &KF2, hasMapPoint2.data(), &fv2, F12,
+                                             bOnlyStereo, mbCheckOrientation, m12.data(), &n),
+              "orbmi_search_for_triangulation");
+        vMatchedPairs.clear();
+        vMatchedPairs.reserve(n);
+        for (int i = 0; i < KF1.n; i++)
+            if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);
+        return n;
+    }
+
+    // The search of Fuse(KeyFrame*, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:977-1127):
+    // bestIdx[i] (-1 = no fusion), bestDist[i]; the caller replays the map updates in list order
+    int FuseSearch(const orbmi_frame_view& KF, const std::vector<orbmi_mappoint>& mps,
+                   const std::vector<uint8_t>& inKeyFrame, float th, std::vector<int32_t>& bestIdx,
+                   std::vector<int32_t>& bestDist) {
+        bestIdx.assign(mps.size(), -1);
+        bestDist.assign(mps.size(), 256);
+        int n = 0;
+        check(orbmi_fuse_search(h_, &KF, mps.data(), inKeyFrame.empty() ? nullptr : inKeyFrame.data(), (int)mps.size(),
+                                th, bestIdx.data(), bestDist.data(), &n),
+              "orbmi_fuse_search");
+        return n;
+    }
+
+    // MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for a batch of points
+    void ComputeDistinctiveDescriptors(const std::vector<uint8_t>& obsDesc, const std::vector<int32_t>& obsOff,
+                                       std::vector<int32_t>& best, std::vector<uint8_t>& descOut) {
+        const int np = obsOff.empty() ? 0 : (int)obsOff.size() - 1;
+        best.assign(np > 0 ? np : 1, -1);
+        descOut.resize((size_t)(np > 0 ? np : 1) * 32);
+        check(orbmi_compute_distinctive_descriptors(h_, obsDesc.data(), obsOff.data(), np, best.data(), descOut.data()),
+              "orbmi_compute_distinctive_descriptors");
+    }
+
     orbmi_matcher* handle() const { return h_; }
 
 private:
     orbmi_matcher* h_ = nullptr;
     float mfNNratio;
     bool mbCheckOrientation;
+};
+
+// ORB_SLAM2::ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
+// (include/ORBVocabulary.h) on the device; transform() = TemplatedVocabulary::transform(
+// features, BowVector&, FeatureVector&, levelsup), as Frame/KeyFrame::ComputeBoW call it.
+class ORBVocabulary {
+public:
+    ORBVocabulary(const orbmi_vocabulary_desc& d, int device = 0) {
+        check(orbmi_vocabulary_create(device, &d, &h_), "orbmi_vocabulary_create");
+    }
+    ~ORBVocabulary() { orbmi_vocabulary_destroy(h_); }
+    ORBVocabulary(const ORBVocabulary&) = delete;
+    ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+
+    struct BowVector { std::vector<uint32_t> word; std::vector<double> value; };
+    struct FeatureVector {
+        std::vector<uint32_t> node;
+        std::vector<int32_t> off, feat;
+        orbmi_feature_vector view() const {
+            return orbmi_feature_vector{(int)node.size(), node.data(), off.data(), feat.data()};
+        }
+    };
+
+    void transform(const uint8_t* desc, int n, BowVector& v, FeatureVector& fv, int levelsup) {
+        const size_t cap = n > 0 ? (size_t)n : 1;
+        v.word.resize(cap); v.value.resize(cap);
+        fv.node.resize(cap); fv.off.resize(cap + 1); fv.feat.resize(cap);
+        int counts[2] = {0, 0};
+        check(orbmi_transform(h_, desc, n, nullptr, levelsup, v.word.data(), v.value.data(), fv.node.data(),
+                              fv.off.data(), fv.feat.data(), counts),
+              "orbmi_transform");
+        v.word.resize(counts[0]); v.value.resize(counts[0]);
+        fv.node.resize(counts[1]); fv.off.resize(counts[1] + 1); fv.feat.resize(fv.off.back());
+    }
+
+private:
+    orbmi_vocabulary* h_ = nullptr;
 };
 
 // Optimizer::LocalBundleAdjustment (include/Optimizer.h:62) on the assembled local graph
