@@ -620,7 +620,6 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
 // After the last step the right-hand side column holds x: no back substitution.  Same solution
 // as LinearSolverEigen's SimplicialLDLT up to the rounding order.
 constexpr int kBaSolveThreads = 512;  // >= TPT x tiles: 2 x (231 + 21) at np <= 21, 465 + 30 at np <= 30
-constexpr int kBaSolveTpt2MaxPoses = 21;
 #ifdef ORBMI_SOLVE_TRACE  // tools/solve_trace.hip: s_memtime stamps kept in LDS, copied out at the end
 __device__ unsigned long long g_solve_trace[256];
 #define SOLVE_STAMP_DECL __shared__ unsigned long long tstamp[256]
@@ -861,6 +860,187 @@ __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
     SOLVE_STAMP_FLUSH();
 }
 
+// The same elimination with the tiles laid out by row pairs, 3 threads per tile (2 tile columns
+// each) and 1 thread per right-hand-side block: wave 0 owns tile row 0, wave w >= 1 rows w and
+// np - w (3 np + 2 <= 64 lanes), so a pivot row, its diagonal tile and its right-hand side sit in
+// one wave.  The pivot row publishes its tiles as they are (A_kj) and normalised (R_kj =
+// A_kk^-1 A_kj, through the LDL^T of A_kk); since W_ki^T U_kj = A_ki^T A_kk^-1 A_kj, every other
+// row then applies the same update A_ij -= L^T R_kj with L = A_ki below the pivot and M_ik above.
+// Step k is one phase and one barrier: every tile applies pivot k; the wave of row k + 1 then
+// publishes its updated diagonal tile, every lane of that wave factors it redundantly (no
+// broadcast of the factor) and the row forms pivot row k + 1, synchronised within the wave only,
+// at raised issue priority; the owners of column k + 1 above the pivot publish M.  The pivot-row
+// and M buffers alternate by parity of k (the readers of step k and the writers for step k + 1
+// overlap).  np <= kBaSolveRowsMaxPoses; larger systems use k_ba_solve<1>.
+constexpr int kBaSolveRowsMaxPoses = 20;
+constexpr int kBaSolveRowsThreads = 64 * (1 + kBaSolveRowsMaxPoses / 2);
+static_assert(3 * kBaSolveRowsMaxPoses + 2 <= 64, "a row pair must fit one wave");
+__device__ inline int solve_rows_wave(int row, int np) { return row <= np - row ? row : np - row; }
+__global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done) return;
+    const int np = ctl.np;
+    double lam = a.scal[3];
+    const double* __restrict__ T = a.Tb[ctl.cur];
+    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    constexpr int CPT = 2;
+    constexpr int kSlot = 38;  // doubles; 16-B aligned rows for b128 access
+    constexpr int kRowSlots = kBaSolveRowsMaxPoses + 1;
+    SOLVE_STAMP_DECL;
+    SOLVE_STAMP(threadIdx.x == 0, 250);
+    __shared__ __attribute__((aligned(16))) double Ap[2][kRowSlots * kSlot], Rp[2][kRowSlots * kSlot];
+    __shared__ __attribute__((aligned(16))) double Mp[2][kBaSolveRowsMaxPoses * kSlot];
+    __shared__ __attribute__((aligned(16))) double Dg[2][36];
+    __shared__ double bs[6 * kBaSolveRowsMaxPoses];
+    __shared__ int fail;
+    const int N = 6 * np;
+    const int tid = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // lane -> (bi, bj, h); bj = np is the right-hand side (h = 0 only)
+    const int ra = wv, rb = np - wv;  // rows of this wave (rb only for wv >= 1, rb > ra)
+    const int na = 3 * (np - ra) + 1;
+    int bi = -1, bj = 0, h = 0;
+    if (ra < np && (wv == 0 || ra <= rb)) {
+        int l = lane, r = ra;
+        if (l >= na && wv > 0 && rb > ra) { l -= na; r = rb; }
+        if (l < 3 * (np - r) + 1) {
+            bi = r;
+            bj = l < 3 * (np - r) ? r + l / 3 : np;
+            h = l < 3 * (np - r) ? l % 3 : 0;
+        }
+    }
+    const int c0 = CPT * h;
+    const bool own = bi >= 0;
+    const bool rhs = own && bj == np;
+    const bool dg = own && !rhs && bi == bj;
+    double A[6 * CPT];  // A[r * CPT + cc] = element (r, c0 + cc) of the tile
+#pragma unroll
+    for (int q = 0; q < 6 * CPT; q++) {
+        const int r = q / CPT, c = c0 + q % CPT;
+        const bool mat = own && !rhs && (!dg || c >= r), vec = rhs && c == 0;
+        const double* src = vec ? a.bs + 6 * bi + r : a.S + (mat ? packed(6 * bi + r, 6 * bj + c, N) : 0);
+        const double v = *src;
+        A[q] = (mat || vec) ? v : 0.0;
+    }
+    if (tid == 0) fail = 0;
+    // pivot row k: the diagonal tile's owners publish it, every lane of the wave factors it, then
+    // tiles (k, j > k) and the right-hand side publish A_kj and R_kj into buffer k & 1
+    auto pivot_row = [&](int k) {
+        double* __restrict__ D = Dg[k & 1];
+        if (dg && bi == k) {
+#pragma unroll
+            for (int q = 0; q < 6 * CPT; q++) D[(q / CPT) * 6 + c0 + q % CPT] = A[q];
+        }
+        wave_sync_lds();
+        double F[36], inv6[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = r; c < 6; c++) F[r * 6 + c] = D[r * 6 + c];
+        const bool ok = ldl6(F, inv6);
+        if (dg && bi == k && h == 0 && !ok) fail = 1;
+        if (!(own && bi == k && bj > k)) return;
+        double* __restrict__ Ao = Ap[k & 1];
+        double* __restrict__ R = Rp[k & 1];
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) Ao[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = A[q];
+#pragma unroll
+        for (int cc = 0; cc < CPT; cc++)  // U_kk^-T A (unit lower solve)
+#pragma unroll
+            for (int t = 1; t < 6; t++)
+#pragma unroll
+                for (int s2 = 0; s2 < t; s2++) A[t * CPT + cc] -= F[s2 * 6 + t] * A[s2 * CPT + cc];
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) A[q] *= inv6[q / CPT];  // D^-1
+#pragma unroll
+        for (int cc = 0; cc < CPT; cc++)  // R = U_kk^-1 (unit upper solve, bottom up)
+#pragma unroll
+            for (int t = 4; t >= 0; t--)
+#pragma unroll
+                for (int s2 = t + 1; s2 < 6; s2++) A[t * CPT + cc] -= F[t * 6 + s2] * A[s2 * CPT + cc];
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) R[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = A[q];
+    };
+    __syncthreads();
+    if (wv == 0) pivot_row(0);  // prologue: pivot row 0
+    __syncthreads();
+    SOLVE_STAMP(tid == 0, 251);
+    for (int k = 0; k < np; k++) {
+        if (fail) break;
+        const bool crit = k + 1 < np && wv == solve_rows_wave(k + 1, np);  // wave-uniform
+        if (crit) __builtin_amdgcn_s_setprio(3);
+        // ---- A(k): eliminate column k from every other row
+        if (own && bj > k && bi != k) {
+            const double* Lp = bi > k ? Ap[k & 1] : Mp[k & 1];
+            double u[6 * CPT], w[36];
+#pragma unroll
+            for (int q = 0; q < 6 * CPT; q++) u[q] = Rp[k & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
+#pragma unroll
+            for (int q = 0; q < 36; q++) w[q] = Lp[bi * kSlot + q];  // w[t * 6 + r] = L(t, r)
+#pragma unroll
+            for (int t = 0; t < 6; t++)
+#pragma unroll
+                for (int r = 0; r < 6; r++)
+#pragma unroll
+                    for (int cc = 0; cc < CPT; cc++) A[r * CPT + cc] -= w[t * 6 + r] * u[t * CPT + cc];
+        }
+        if (k + 1 < np) {
+            // M_i,k+1 (column k + 1 above its pivot, final after A(k)), stored transposed
+            if (own && !rhs && bj == k + 1 && bi <= k) {
+#pragma unroll
+                for (int q = 0; q < 6 * CPT; q++) Mp[(k + 1) & 1][bi * kSlot + (c0 + q % CPT) * 6 + q / CPT] = A[q];
+            }
+            if (crit) {
+                SOLVE_STAMP(dg && bi == k + 1 && h == 0, 4 * k);
+                pivot_row(k + 1);
+                SOLVE_STAMP(own && bi == k + 1 && rhs, 4 * k + 2);
+                __builtin_amdgcn_s_setprio(0);
+            }
+        }
+        __syncthreads();
+        SOLVE_STAMP(tid == 0, 4 * k + 3);
+    }
+    if (fail) {  // pop: trial poses = current ones, computeScale = 0
+        for (int k = tid; k < a.nkf; k += blockDim.x)
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
+        return;
+    }
+    if (rhs) {  // x = the right-hand side column
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            bs[6 * bi + r] = A[r * CPT];
+            a.xp[6 * bi + r] = A[r * CPT];
+        }
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    SOLVE_STAMP(lane == 0, 252);
+    // trial poses T_t = exp(x_p) * T (VertexSE3Expmap::oplusImpl) and the poses' part of
+    // computeScale, sum x_p (lambda x_p + b_p) in index order
+    for (int k = lane; k < a.nkf; k += 64) {
+        const int pi = a.pose_idx[k];
+        if (pi >= 0) {
+            double u[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) u[q] = bs[6 * pi + q];
+            se3_oplus(u, T + 8 * k, Tt + 8 * k);
+        } else {
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        }
+    }
+    double sc = 0;  // lane partials in index order, then a fixed-order wave sum
+    for (int q = lane; q < N; q += 64) sc += bs[q] * (lam * bs[q] + a.bp[q]);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+        a.scal[1] = sc;
+        a.scal[2] = 1;
+        a.istat[3] = 1;
+    }
+    SOLVE_STAMP(lane == 0, 253);
+    SOLVE_STAMP_FLUSH();
+}
+
 // ---------------------------------------------------------------- update + trial errors
 // block = 32 points.  Threads 0..31: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
 // part); then every thread takes edges of the block's points: computeActiveErrors on the trial
@@ -1048,7 +1228,7 @@ struct Runner {
     orbmi_ba& h;
     BaDev a;
     const volatile int* stop;
-    int solve_tpt;  // 2: nf <= kBaSolveTpt2MaxPoses, else 1
+    bool solve_rows;  // nf <= kBaSolveRowsMaxPoses: k_ba_solve_rows, else k_ba_solve<1>
 
     bool stopped() const { return stop && *stop; }
 
@@ -1078,7 +1258,7 @@ struct Runner {
         hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
         if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
-        if (solve_tpt == 2) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
+        if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaBlock), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(64), 0, h.stream, a);
@@ -1309,7 +1489,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
     a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
-    Runner r{h, a, stop, nf <= kBaSolveTpt2MaxPoses ? 2 : 1};
+    Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses};
     unsigned char* out_erase = B + o_oerase;
     const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
     hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);

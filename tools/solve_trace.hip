@@ -1,5 +1,5 @@
 // Phase timing of k_ba_solve (LocalBA reduced-system LDL^T) on a random SPD 6K x 6K system.
-// Build: hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -DORBMI_SOLVE_TRACE \
+// Build: hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -DORBMI_SOLVE_TRACE -Wno-unused-value \
 //        -I include -I orb_slam2_with_comment_amd/csrc tools/solve_trace.hip -o /tmp/solve_trace
 #include "lba.hip"
 
@@ -44,7 +44,10 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     auto launch = [&] {
-        if (np <= kBaSolveTpt2MaxPoses && !getenv("TPT1")) hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
+        if (np <= kBaSolveRowsMaxPoses && !getenv("TPT1") && !getenv("OLD"))
+            hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, 0, a);
+        else if (np <= 21 && !getenv("TPT1"))  // the previous tile layout, TPT 2
+            hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
     };
     for (int it = 0; it < 3; it++) launch();
@@ -66,19 +69,27 @@ int main(int argc, char** argv) {
         res = std::max(res, std::fabs(s - b[i]));
     }
     printf("np=%d N=%d  avg kernel %.2f us  residual %.3e\n", np, N, ms * 1e3 / reps, res);
-    // cycles (s_memtime) between stamps; per step k: panel(k, k+1) done, (k+1, k+1) updated,
-    // (k+1, k+1) factored, end of step (thread 0 after the barrier)
+    // cycles (s_memtime) between stamps.  k_ba_solve<TPT>, per step k: panel(k, k+1) done,
+    // (k+1, k+1) updated, (k+1, k+1) factored, end of step (thread 0 after the barrier).
+    // k_ba_solve_rows: (k+1, k+1) updated, factored, pivot row k+1 done, end of step.
     auto cy = [&](int i, int j) { return (long long)(tr[j] - tr[i]); };
     printf("load+prologue %lld cycles\n", cy(250, 251));
+    const bool rows = np <= kBaSolveRowsMaxPoses && !getenv("TPT1") && !getenv("OLD");
     long long sp = 0, su = 0, sf = 0, sb = 0;
     for (int k = 0; k + 1 < np; k++) {
         const int prev = k == 0 ? 251 : 4 * (k - 1) + 3;
+        if (rows) {  // stamps 4k (diagonal k+1 updated), 4k+2 (pivot row k+1 done), 4k+3
+            const long long p = cy(prev, 4 * k), f = cy(4 * k, 4 * k + 2), e = cy(4 * k + 2, 4 * k + 3);
+            if (k < 3 || k == np - 2) printf("step %2d: start->updated %lld  pivot row %lld  ->end %lld\n", k, p, f, e);
+            sp += p; sf += f; sb += e;
+            continue;
+        }
         const long long p = cy(prev, 4 * k), u = cy(4 * k, 4 * k + 1), f = cy(4 * k + 1, 4 * k + 2),
                         e = cy(4 * k + 2, 4 * k + 3);
         if (k < 3 || k == np - 2) printf("step %2d: start->panel %lld  panel->updated %lld  factor %lld  ->end %lld\n", k, p, u, f, e);
         sp += p; su += u; sf += f; sb += e;
     }
-    printf("sums: start->panel %lld  panel->updated %lld  factor %lld  ->end %lld\n", sp, su, sf, sb);
+    printf("sums: %lld  %lld  %lld  %lld\n", sp, su, sf, sb);
     printf("factor loop %lld  back substitution %lld  tail %lld  total %lld cycles\n", cy(251, 4 * (np - 1) + 3),
            cy(4 * (np - 1) + 3, 252), cy(252, 253), cy(250, 253));
     return 0;
