@@ -83,8 +83,9 @@ struct BaDev {
     const int* kf_pos;         // position of edge e in the keyframe CSR (kf_edges[kf_pos[e]] == e)
     const int* kf_pt;          // point of the edge at keyframe-CSR position j
     const int* blk_kf;         // nblk x 2: keyframes (a, b), id(a) <= id(b), both not fixed
-    const int* blk_start;      // nblk + 1
-    const int2* blk_pairs;     // (e_a, e_b): edges of one point into keyframes a and b
+    int* blk_cnt;              // nblk: pairs per block (k_ba_pairs_count)
+    int* blk_start;            // nblk + 1 (k_ba_pairs_fill)
+    int2* blk_pairs;           // (e_a, e_b): edges of one point into keyframes a and b
     double* err;               // nedge x 3 (stale semantics)
     unsigned char* eflag;      // bit0 level-1, bit1 no robust kernel, bit2 active
     int* pose_idx;             // nkf
@@ -324,6 +325,85 @@ __global__ __launch_bounds__(1024) void k_ba_activate(BaDev a, int max_it) {
     }
     __syncthreads();
     for (int i = tid; i < a.nedge; i += blockDim.x) a.e_pi[i] = a.pose_idx[a.edges[i].kf];
+}
+
+// ---------------------------------------------------------------- Schur pair lists
+// Block (a, b) of the reduced system sums over the points keyframes a and b both observe: the
+// pairs (e_a, e_b) of their edges, ordered by point, then edge (the order the points' edges
+// are inserted).  A keyframe's CSR lists its edges in edge order, hence by point: each edge of
+// a looks its point up in b's list by binary search (staged in LDS when it fits).
+constexpr int kPairThreads = 256;
+constexpr int kPairLdsPts = 4096;
+
+// [lo, hi) of point p in the sorted list l[0..n)
+__device__ inline int2 pair_range(const int* __restrict__ l, int n, int p) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (l[m] < p) lo = m + 1; else hi = m;
+    }
+    int e = lo;
+    hi = n;
+    while (e < hi) {
+        const int m = (e + hi) >> 1;
+        if (l[m] <= p) e = m + 1; else hi = m;
+    }
+    return make_int2(lo, e);
+}
+
+// stages b's point list; returns the list to search (LDS or global)
+__device__ inline const int* pair_list_b(const BaDev& a, int kb, int* lds, int* nb) {
+    const int b0 = a.kf_start[kb];
+    *nb = a.kf_start[kb + 1] - b0;
+    if (*nb > kPairLdsPts) return a.kf_pt + b0;
+    for (int j = threadIdx.x; j < *nb; j += blockDim.x) lds[j] = a.kf_pt[b0 + j];
+    __syncthreads();
+    return lds;
+}
+
+__global__ __launch_bounds__(kPairThreads) void k_ba_pairs_count(BaDev a) {
+    __shared__ int lb[kPairLdsPts];
+    __shared__ int scratch[kPairThreads / 64];
+    const int b = blockIdx.x, ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
+    int nb;
+    const int* L = pair_list_b(a, kb, lb, &nb);
+    int cnt = 0;
+    for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
+        const int2 r = pair_range(L, nb, a.kf_pt[j]);
+        cnt += r.y - r.x;
+    }
+    int total;
+    block_excl_scan(cnt, scratch, &total);
+    if (threadIdx.x == 0) a.blk_cnt[b] = total;
+}
+
+__global__ __launch_bounds__(kPairThreads) void k_ba_pairs_fill(BaDev a) {
+    __shared__ int lb[kPairLdsPts];
+    __shared__ int scratch[kPairThreads / 64];
+    const int b = blockIdx.x, ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
+    int before = 0;  // pairs of the blocks before b
+    for (int q = threadIdx.x; q < b; q += blockDim.x) before += a.blk_cnt[q];
+    int off;
+    block_excl_scan(before, scratch, &off);
+    if (threadIdx.x == 0) {
+        a.blk_start[b] = off;
+        if (b == a.nblk - 1) a.blk_start[a.nblk] = off + a.blk_cnt[b];
+    }
+    int nb;
+    const int* L = pair_list_b(a, kb, lb, &nb);
+    const int b0 = a.kf_start[kb], a0 = a.kf_start[ka], a1 = a.kf_start[ka + 1];
+    for (int c = a0; c < a1; c += blockDim.x) {  // chunks of a's list, in order
+        const int j = c + threadIdx.x;
+        int2 r = make_int2(0, 0);
+        if (j < a1) r = pair_range(L, nb, a.kf_pt[j]);
+        int total;
+        const int o = off + block_excl_scan(r.y - r.x, scratch, &total);
+        if (j < a1) {
+            const int ea = a.kf_edges[j];
+            for (int t = r.x; t < r.y; t++) a.blk_pairs[o + t - r.x] = make_int2(ea, a.kf_edges[b0 + t]);
+        }
+        off += total;
+    }
 }
 
 // ---------------------------------------------------------------- errors
@@ -1374,22 +1454,18 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     if (nblk_ll > (1 << 20)) return ORBMI_E_UNSUPPORTED;
     const int nblk = (int)nblk_ll;
     auto blk_of = [nf](int ra, int rb) { return ra * nf - ra * (ra - 1) / 2 + (rb - ra); };
-    std::vector<int> blk_kf(2 * std::max(nblk, 1)), blk_start(nblk + 1, 0);
+    std::vector<int> blk_kf(2 * std::max(nblk, 1));
     for (int ra = 0; ra < nf; ra++)
         for (int rb = ra; rb < nf; rb++) { blk_kf[2 * blk_of(ra, rb)] = free_kf[ra]; blk_kf[2 * blk_of(ra, rb) + 1] = free_kf[rb]; }
-    std::vector<int> erank(std::max(ne, 1));
-    for (int i = 0; i < ne; i++) erank[i] = rank[P->edges[i].kf];
-    for (int p = 0; p < npt; p++)
-        for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
-            const int r1 = erank[e1];
-            if (r1 < 0) continue;
-            for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
-                const int r2 = erank[e2];
-                if (r2 >= r1) blk_start[blk_of(r1, r2) + 1]++;
-            }
-        }
-    for (int k = 0; k < nblk; k++) blk_start[k + 1] += blk_start[k];
-    const int npair = blk_start[nblk];
+    // capacity of the pair lists (built on the device): sum over points of (free edges)^2
+    long long npair_cap = 0;
+    for (int p = 0; p < npt; p++) {
+        long long m = 0;
+        for (int e = pt_start[p]; e < pt_start[p + 1]; e++) m += rank[P->edges[e].kf] >= 0;
+        npair_cap += m * m;
+    }
+    if (npair_cap > (1LL << 28)) return ORBMI_E_UNSUPPORTED;
+    const int npair = (int)npair_cap;
     // ---- one device arena; the graph and its index arrays go up in one copy
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
     const int nb_q = std::max(1, (npt + kBaUpdPts - 1) / kBaUpdPts);
@@ -1400,9 +1476,10 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const size_t o_kfs = take(sizeof(orbmi_ba_keyframe) * nkf), o_pts = take(sizeof(orbmi_ba_point) * npt),
                  o_edges = take(sizeof(orbmi_ba_edge) * ne), o_order = take(4 * nkf), o_pts_start = take(4 * (npt + 1)),
                  o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne),
-                 o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk),
-                 o_blk_start = take(4 * ((size_t)nblk + 1)), o_pairs = take(8 * (size_t)npair);
+                 o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk);
     const size_t up_bytes = off;
+    const size_t o_blk_cnt = take(4 * (size_t)nblk), o_blk_start = take(4 * ((size_t)nblk + 1)),
+                 o_pairs = take(8 * (size_t)npair);
     const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
                  o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf),
                  o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne),
@@ -1442,20 +1519,6 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     put(o_kf_pos, kf_pos.data(), 4 * (size_t)ne);
     put(o_kf_pt, kf_pt.data(), 4 * (size_t)ne);
     put(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk);
-    put(o_blk_start, blk_start.data(), 4 * ((size_t)nblk + 1));
-    {  // the pair lists, written straight into the staging buffer
-        int2* pairs = (int2*)(S + o_pairs);
-        std::vector<int> fill(blk_start.begin(), blk_start.end() - 1);
-        for (int p = 0; p < npt; p++)
-            for (int e1 = pt_start[p]; e1 < pt_start[p + 1]; e1++) {
-                const int r1 = erank[e1];
-                if (r1 < 0) continue;
-                for (int e2 = pt_start[p]; e2 < pt_start[p + 1]; e2++) {
-                    const int r2 = erank[e2];
-                    if (r2 >= r1) pairs[fill[blk_of(r1, r2)]++] = make_int2(e1, e2);
-                }
-            }
-    }
     ORBMI_HIP(hipMemcpyAsync(B, S, up_bytes, hipMemcpyHostToDevice, s));
     ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
     ORBMI_HIP(hipMemsetAsync(B + o_ctl, 0, sizeof(BaCtl), s));
@@ -1480,8 +1543,9 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.kf_pt = (const int*)(B + o_kf_pt);
     a.e_pi = (int*)(B + o_e_pi);
     a.blk_kf = (const int*)(B + o_blk_kf);
-    a.blk_start = (const int*)(B + o_blk_start);
-    a.blk_pairs = (const int2*)(B + o_pairs);
+    a.blk_cnt = (int*)(B + o_blk_cnt);
+    a.blk_start = (int*)(B + o_blk_start);
+    a.blk_pairs = (int2*)(B + o_pairs);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
     a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf);
     a.Hpl = (double*)(B + o_Hpl); a.Hle = (double*)(B + o_Hle); a.Hpe = (double*)(B + o_Hpe);
@@ -1493,6 +1557,10 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     unsigned char* out_erase = B + o_oerase;
     const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
     hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);
+    if (nblk > 0) {
+        hipLaunchKernelGGL(k_ba_pairs_count, dim3(nblk), dim3(kPairThreads), 0, s, a);
+        hipLaunchKernelGGL(k_ba_pairs_fill, dim3(nblk), dim3(kPairThreads), 0, s, a);
+    }
     ORBMI_HIP(hipGetLastError());
     int rc;
     if ((rc = r.optimize(5, 0))) return rc;
