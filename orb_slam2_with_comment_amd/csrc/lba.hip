@@ -91,6 +91,7 @@ struct BaDev {
     int* pose_idx;             // nkf
     int* pose_kf;              // kBaMaxPoses
     int* e_pi;                 // nedge: pose index of the edge's keyframe (-1 fixed / inactive)
+    int* kf_act;               // nkf: activation generation that saw an active edge of the keyframe
     double* Hpl;               // nedge x 18 (pose rows x point cols)
     double* Hle;               // nedge x 9: edge's Hll upper (6) + b_l (3)
     double* Hpe;               // nedge x 27 in keyframe-CSR order: edge's Hpp upper (21) + b_p (6)
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restri
         q_normalize(q);
         double* Ti = T + 8 * i;
         Ti[0] = q.x; Ti[1] = q.y; Ti[2] = q.z; Ti[3] = q.w; Ti[4] = t[3]; Ti[5] = t[7]; Ti[6] = t[11]; Ti[7] = 0;
+        a.kf_act[i] = 0;
     }
     if (i < a.npt) {
         for (int r = 0; r < 3; r++) X[4 * i + r] = a.pts[i].pos[r];
@@ -277,54 +279,73 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a) {
     a.eflag[i] = f;
 }
 
-// SparseOptimizer::initializeOptimization(level 0) + buildIndexMapping: active edges, pose
-// indices in vertex-id order (poses first), number of active points
-__global__ __launch_bounds__(1024) void k_ba_activate(BaDev a, int max_it) {
-    __shared__ int kfact[kBaMaxKf];
-    __shared__ int nl;
-    const int tid = threadIdx.x;
-    for (int k = tid; k < a.nkf; k += blockDim.x) kfact[k] = 0;
-    if (tid == 0) nl = 0;
-    __syncthreads();
-    for (int i = tid; i < a.nedge; i += blockDim.x) {
+// SparseOptimizer::initializeOptimization(level 0) + buildIndexMapping, in two launches.
+// Grid part: edges of level 0 become active (bit 2), their keyframes are marked (kf_act = gen)
+// and each block counts the points whose first active edge it holds (partials in part_lin,
+// which the next linearisation overwrites).  Bit 0 is never rewritten, so reading it from the
+// point's other edges while they are updated is safe.
+__global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int gen) {
+    __shared__ double red[kBaBlock / 64];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int first = 0;
+    if (i < a.nedge) {
         unsigned char f = a.eflag[i] & 3;
-        if (!(f & 1)) { f |= 4; kfact[a.edges[i].kf] = 1; }
+        if (!(f & 1)) {
+            f |= 4;
+            const orbmi_ba_edge e = a.edges[i];
+            a.kf_act[e.kf] = gen;
+            first = 1;
+            for (int j = a.pt_start[e.point]; j < i; j++)
+                if (!(a.eflag[j] & 1)) { first = 0; break; }
+        }
         a.eflag[i] = f;
     }
-    __syncthreads();
-    int nlp = 0;
-    for (int p = tid; p < a.npt; p += blockDim.x) nlp += point_active(a, p);
-    if (nlp) atomicAdd(&nl, nlp);
-    __syncthreads();
-    if (tid == 0) {
-        int n = 0;
-        for (int oi = 0; oi < a.nkf; oi++) {
-            const int k = a.kf_order[oi];
-            a.pose_idx[k] = -1;
-            if (a.kfs[k].fixed || !kfact[k]) continue;
-            if (n < kBaMaxPoses) a.pose_kf[n] = k;
-            a.pose_idx[k] = n < kBaMaxPoses ? n : -1;
-            n++;
+    const double n = block_sum<kBaBlock>((double)first, red);
+    if (threadIdx.x == 0) a.part_lin[blockIdx.x] = n;
+}
+
+// One wave: the number of active points, pose indices in vertex-id order (poses first) by a
+// ballot scan over the id-ordered keyframes, and the LM state of levenberg.cpp:61-70.  The
+// edges' pose indices (e_pi) are written by the next k_ba_linearize.
+__global__ __launch_bounds__(64) void k_ba_activate_ctl(BaDev a, int max_it, int gen) {
+    const int lane = threadIdx.x;
+    double c = 0;
+    for (int b = lane; b < a.nb_e; b += 64) c += a.part_lin[b];
+    const int nl = (int)wave_sum(c);
+    int n = 0;
+    for (int o0 = 0; o0 < a.nkf; o0 += 64) {
+        const int oi = o0 + lane;
+        int k = -1;
+        bool take = false;
+        if (oi < a.nkf) {
+            k = a.kf_order[oi];
+            take = !a.kfs[k].fixed && a.kf_act[k] == gen;
         }
+        const unsigned long long m = __ballot(take);
+        const int idx = n + __popcll(m & ((1ull << lane) - 1));
+        if (k >= 0) {
+            a.pose_idx[k] = take && idx < kBaMaxPoses ? idx : -1;
+            if (take && idx < kBaMaxPoses) a.pose_kf[idx] = k;
+        }
+        n += __popcll(m);
+    }
+    if (lane == 0) {
         a.istat[0] = n;
         a.istat[1] = nl;
         a.istat[2] = n > kBaMaxPoses;
-        // SparseOptimizer::optimize(max_it) begins: LM state of levenberg.cpp:61-70
-        BaCtl& c = *a.ctl;
-        c.np = min(n, kBaMaxPoses);
-        c.nl = nl;
-        c.unsupported |= n > kBaMaxPoses;
-        c.it = 0;
-        c.max_it = max_it;
-        c.trial = 0;
-        c.need_lin = 1;
-        c.nbad = 0;
-        c.lambda = 0;
-        c.ni = 2;
-        c.done = (n + nl == 0) || c.unsupported || max_it <= 0;
+        BaCtl& c2 = *a.ctl;
+        c2.np = min(n, kBaMaxPoses);
+        c2.nl = nl;
+        c2.unsupported |= n > kBaMaxPoses;
+        c2.it = 0;
+        c2.max_it = max_it;
+        c2.trial = 0;
+        c2.need_lin = 1;
+        c2.nbad = 0;
+        c2.lambda = 0;
+        c2.ni = 2;
+        c2.done = (n + nl == 0) || c2.unsupported || max_it <= 0;
     }
-    __syncthreads();
-    for (int i = tid; i < a.nedge; i += blockDim.x) a.e_pi[i] = a.pose_idx[a.edges[i].kf];
 }
 
 // ---------------------------------------------------------------- Schur pair lists
@@ -457,7 +478,9 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double chi = 0;
     if (i < a.nedge) {
-        const bool free_pose = a.e_pi[i] >= 0;
+        const int pi = a.pose_idx[a.edges[i].kf];
+        a.e_pi[i] = pi;  // for k_ba_update_errors (set by the first linearisation of optimize())
+        const bool free_pose = pi >= 0;
         double* Hp = a.Hpe + 27 * (long long)a.kf_pos[i];
         double* B = a.Hpl + 18 * (long long)i;
         if (!(a.eflag[i] & 4)) {
@@ -1346,7 +1369,8 @@ struct Runner {
 
     // SparseOptimizer::optimize(iterations) as phase 0 / 1, then activeRobustChi2
     int optimize(int iterations, int phase) {
-        hipLaunchKernelGGL(k_ba_activate, dim3(1), dim3(1024), 0, h.stream, a, stopped() ? 0 : iterations);
+        hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, phase + 1);
+        hipLaunchKernelGGL(k_ba_activate_ctl, dim3(1), dim3(64), 0, h.stream, a, stopped() ? 0 : iterations, phase + 1);
         int todo = stopped() ? 0 : iterations + kBaStepSlack;
         while (todo > 0) {
             for (int k = 0; k < todo; k++) step();
@@ -1481,7 +1505,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const size_t o_blk_cnt = take(4 * (size_t)nblk), o_blk_start = take(4 * ((size_t)nblk + 1)),
                  o_pairs = take(8 * (size_t)npair);
     const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
-                 o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf),
+                 o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_kfact = take(4 * nkf),
                  o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne),
                  o_Hpe = take(216 * (size_t)ne), o_Hll = take(72 * npt), o_bl = take(24 * npt),
                  o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses), o_S = take(8 * (size_t)kBaPacked),
@@ -1547,7 +1571,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.blk_start = (int*)(B + o_blk_start);
     a.blk_pairs = (int2*)(B + o_pairs);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
-    a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf);
+    a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf); a.kf_act = (int*)(B + o_kfact);
     a.Hpl = (double*)(B + o_Hpl); a.Hle = (double*)(B + o_Hle); a.Hpe = (double*)(B + o_Hpe);
     a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl);
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
