@@ -103,8 +103,9 @@ def lib() -> C.CDLL:
     """Load liborbmi.so (raises if it is absent: there is no CPU fallback)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            raise ImportError(f"{LIB} not built: run `python -m orb_slam2_with_comment_amd.build`")
+        path = os.environ.get("ORBMI_LIB", LIB)  # an alternative build (A/B timing)
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built: run `python -m orb_slam2_with_comment_amd.build`")
         # torch bundles its own libamdhip64.so.7; loading it first lets liborbmi.so bind to that
         # same runtime (same SONAME) so torch tensors/streams/RCCL and our kernels share one HIP
         # runtime in the process.  Without torch, liborbmi.so uses /opt/rocm's runtime.
@@ -112,7 +113,7 @@ def lib() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-        L = C.CDLL(LIB)
+        L = C.CDLL(path)
         for name, (res, args) in _PROTOS.items():
             fn = getattr(L, name)
             fn.restype = res
