@@ -28,9 +28,12 @@ __device__ inline double fast_rsqrt(double x) {
 }
 
 // ---------------------------------------------------------------- SE3Quat helpers (fp64)
+// The helpers below contract multiply-adds (fp contract fast): the optimisers that use them
+// carry a 1e-4 parity tolerance.
 struct Q { double x, y, z, w; };
 
 __device__ inline void q_normalize(Q& q) {
+#pragma clang fp contract(fast)
     if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
     const double inv = fast_rsqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
     q.x *= inv; q.y *= inv; q.z *= inv; q.w *= inv;
@@ -72,6 +75,7 @@ __device__ inline Q q_from_matrix(const double m[3][3]) {
 }
 
 __device__ inline void q_to_matrix(const Q& q, double R[3][3]) {
+#pragma clang fp contract(fast)
     const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
     const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
     const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
@@ -82,6 +86,7 @@ __device__ inline void q_to_matrix(const Q& q, double R[3][3]) {
 }
 
 __device__ inline void q_rotate(const Q& q, const double v[3], double o[3]) {
+#pragma clang fp contract(fast)
     double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
     uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
     o[0] = v[0] + q.w * uv[0] + (q.y * uv[2] - q.z * uv[1]);
@@ -111,18 +116,23 @@ __device__ inline void sincos_small(double x, double& s, double& c) {
 // b = (1-cos t)/t^2 = 2 sin^2(t/2)/t^2, c = (t - sin t)/t^3; equal to the matrix form up to
 // rounding.  Below 1e-5 the reference's non-orthonormal R = I + Omega + Omega^2 (V = R) is kept.
 __device__ inline void se3_oplus(const double* u, const double* Tin, double* Tout) {
+#pragma clang fp contract(fast)
     const double w0 = u[0], w1 = u[1], w2 = u[2];
     const double n2 = w0 * w0 + w1 * w1 + w2 * w2;
     Q qe;
     double te[3];
     if (n2 < 1e-10) {  // theta < 0.00001
-        const double O[3][3] = {{0, -w2, w1}, {w2, 0, -w0}, {-w1, w0, 0}};
-        double R[3][3];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++)
-                R[i][j] = (i == j) + O[i][j] + (O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j]);
-        qe = q_from_matrix(R);
-        for (int i = 0; i < 3; i++) te[i] = R[i][0] * u[3] + R[i][1] * u[4] + R[i][2] * u[5];
+        // R = I + Omega + Omega^2 (Omega^2 = w w^T - |w|^2 I, symmetric: R_kj - R_jk = 2 w_i
+        // exactly), trace 3 - 2 |w|^2 > 0: Eigen's Quaternion(R) takes its trace branch,
+        // q = ((R_kj - R_jk) / (2 t), ..., t / 2) with t = sqrt(trace + 1)
+        const double R00 = 1 - (w1 * w1 + w2 * w2), R11 = 1 - (w0 * w0 + w2 * w2), R22 = 1 - (w0 * w0 + w1 * w1);
+        const double R01 = w0 * w1 - w2, R02 = w0 * w2 + w1, R10 = w0 * w1 + w2;
+        const double R12 = w1 * w2 - w0, R20 = w0 * w2 - w1, R21 = w1 * w2 + w0;
+        const double x = R00 + R11 + R22 + 1.0, r = fast_rsqrt(x), hs = 0.5 * r;
+        qe = Q{(R21 - R12) * hs, (R02 - R20) * hs, (R10 - R01) * hs, 0.5 * (x * r)};
+        te[0] = R00 * u[3] + R01 * u[4] + R02 * u[5];
+        te[1] = R10 * u[3] + R11 * u[4] + R12 * u[5];
+        te[2] = R20 * u[3] + R21 * u[4] + R22 * u[5];
     } else {
         const double it = fast_rsqrt(n2), theta = n2 * it, it2 = it * it;
         double sh, ch;  // sin, cos of theta / 2
