@@ -1,0 +1,871 @@
+"""Stereo SLAM host integration: System::TrackStereo, the stereo
+Tracking state machine and a synchronous LocalMapping, driving the MI355X operators.
+
+This module is the host code around the GPU path, in the reference's own structure:
+
+  System::TrackStereo        -> StereoSLAM.TrackStereo              src/System.cc:110-159
+  Tracking::Track (stereo)   -> StereoSLAM._track                   src/Tracking.cc:287-581
+  StereoInitialization       -> StereoSLAM._stereo_initialization   src/Tracking.cc:584-636
+  TrackReferenceKeyFrame     -> StereoSLAM._track_reference_kf      src/Tracking.cc:871-917
+  TrackWithMotionModel       -> StereoSLAM._track_motion_model      src/Tracking.cc:997-1063
+  TrackLocalMap              -> StereoSLAM._track_local_map         src/Tracking.cc:1075-1104
+  UpdateLocalKeyFrames/Points, SearchLocalPoints                    src/Tracking.cc:1345-1580
+  NeedNewKeyFrame / CreateNewKeyFrame                               src/Tracking.cc:1140-1330
+  LocalMapping::ProcessNewKeyFrame + LocalBundleAdjustment          src/LocalMapping.cc:152-200, :89-90
+  KeyFrame::UpdateConnections / MapPoint bookkeeping                src/KeyFrame.cc, src/MapPoint.cc
+  System::SaveTrajectoryKITTI / SaveTrajectoryTUM / SaveKeyFrameTrajectoryTUM
+                                                                    src/System.cc:334-486
+
+Every per-keypoint operation (ORBextractor, ComputeStereoMatches, ComputeBoW, the three
+SearchBy* matchers, PoseOptimization, ComputeDistinctiveDescriptors, LocalBundleAdjustment)
+goes through a *backend*; the product backend is `GpuBackend` (liborbmi.so on MI355X, no CPU
+fallback: a missing library raises).  The host logic here only keeps the map and the
+reference's bookkeeping.  Tests drive the same host logic with an oracle-backed backend
+(tests/slam_backends.py) to prove that the GPU run yields the oracle's trajectory.
+
+Deterministic replacements of the reference's unordered behaviour (documented in DESIGN.md §9):
+  * LocalMapping runs synchronously after each new keyframe (the reference runs it on its own
+    thread; with LocalMapping always idle NeedNewKeyFrame's c1b holds, as on a fast machine).
+  * std::map<KeyFrame*, ...> iteration (pointer order) is keyframe-id order; covisibility ties
+    sort by id like ascending heap addresses do.
+  * LocalMapping's MapPointCulling, CreateNewMapPoints, SearchInNeighbors and KeyFrameCulling,
+    relocalisation and loop closing are not part of this path (out of scope).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from .types import (LF_HAS_MP, LF_OUTLIER, LFPOINT_DTYPE, MAPPOINT_DTYPE, MP_BAD, MP_HAS_OBS, MP_SEEN,
+                    FeatureVector, Frame)
+
+NO_IMAGES_YET, NOT_INITIALIZED, OK, LOST = 0, 1, 2, 3   # Tracking::eTrackingState (include/Tracking.h)
+
+
+# ---- float32 pose algebra (cv::Mat CV_32F products accumulate in double, src/Converter.cc) --
+def _mul(*ms) -> np.ndarray:
+    out = np.asarray(ms[0], np.float32)
+    for m in ms[1:]:
+        out = (out.astype(np.float64) @ np.asarray(m, np.float32).astype(np.float64)).astype(np.float32)
+    return out
+
+
+def pose_inverse(T: np.ndarray) -> np.ndarray:
+    """Twc from Tcw as Frame::UpdatePoseMatrices does: Rwc = Rcw^T, Ow = -Rcw^T tcw."""
+    T = np.asarray(T, np.float32)
+    Rwc = T[:3, :3].T.copy()
+    out = np.eye(4, dtype=np.float32)
+    out[:3, :3] = Rwc
+    out[:3, 3] = -_mul(Rwc, T[:3, 3:4])[:, 0]
+    return out
+
+
+def quaternion_xyzw(R) -> np.ndarray:
+    """Converter::toQuaternion (src/Converter.cc:137-149): Eigen::Quaterniond(Matrix3d) of a
+    float rotation, returned as float [x, y, z, w]."""
+    m = np.asarray(R, np.float32).astype(np.float64)
+    q = np.zeros(4)  # x y z w
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0:
+        t = np.sqrt(t + 1.0)
+        q[3] = 0.5 * t
+        t = 0.5 / t
+        q[0], q[1], q[2] = (m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t
+    else:
+        i = 1 if m[1, 1] > m[0, 0] else 0
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        q[3] = (m[k, j] - m[j, k]) * t
+        q[j] = (m[j, i] + m[i, j]) * t
+        q[k] = (m[k, i] + m[i, k]) * t
+    return q.astype(np.float32)
+
+
+# ---- map model (src/KeyFrame.cc, src/MapPoint.cc) ------------------------------------------
+@dataclasses.dataclass(eq=False)
+class KeyFrame:
+    """The fields of ORB_SLAM2::KeyFrame this path reads; also the graph node type of
+    optimizer.gather_local_ba (id, tcw, keys_un, u_right, inv_level_sigma2, cam, map_points,
+    covisible, bad)."""
+    id: int
+    frame_id: int
+    timestamp: float
+    tcw: np.ndarray
+    keys_un: np.ndarray
+    desc: np.ndarray
+    u_right: np.ndarray
+    depth: np.ndarray
+    inv_level_sigma2: np.ndarray
+    scale_factors: np.ndarray
+    cam: object
+    map_points: list
+    feat_vec: object = None
+    covisible: list = dataclasses.field(default_factory=list)  # mvpOrderedConnectedKeyFrames
+    conn: dict = dataclasses.field(default_factory=dict)       # mConnectedKeyFrameWeights
+    parent: object = None
+    children: list = dataclasses.field(default_factory=list)
+    first_connection: bool = True
+    bad: bool = False
+
+    @property
+    def Ow(self) -> np.ndarray:
+        return pose_inverse(self.tcw)[:3, 3]
+
+    def tracked_map_points(self, min_obs: int) -> int:
+        """KeyFrame::TrackedMapPoints (src/KeyFrame.cc:166-193)."""
+        n = 0
+        for mp in self.map_points:
+            if mp is not None and not mp.bad and (min_obs <= 0 or mp.nobs >= min_obs):
+                n += 1
+        return n
+
+    def add_connection(self, kf, weight):
+        """KeyFrame::AddConnection + UpdateBestCovisibles (src/KeyFrame.cc:97-135): the ordered
+        list holds every connection, heaviest first."""
+        self.conn[kf] = weight
+        self.covisible = [k for w, _, k in sorted(((w, k.id, k) for k, w in self.conn.items()),
+                                                 key=lambda p: (p[0], p[1]), reverse=True)]
+
+    def best_covisibility(self, n: int) -> list:
+        return self.covisible[:n]
+
+    def update_connections(self):
+        """KeyFrame::UpdateConnections (src/KeyFrame.cc:285-371)."""
+        counter: dict = {}
+        for mp in self.map_points:
+            if mp is None or mp.bad:
+                continue
+            for kf in mp.observations:
+                if kf is not self:
+                    counter[kf] = counter.get(kf, 0) + 1
+        if not counter:
+            return
+        th = 15
+        nmax, kfmax = 0, None
+        pairs = []
+        for kf in sorted(counter, key=lambda k: k.id):
+            w = counter[kf]
+            if w > nmax:
+                nmax, kfmax = w, kf
+            if w >= th:
+                pairs.append((w, kf.id, kf))
+                kf.add_connection(self, w)
+        if not pairs:
+            pairs.append((nmax, kfmax.id, kfmax))
+            kfmax.add_connection(self, nmax)
+        pairs.sort(key=lambda p: (p[0], p[1]), reverse=True)
+        self.conn = counter
+        self.covisible = [p[2] for p in pairs]
+        if self.first_connection and self.id != 0:
+            self.parent = self.covisible[0]
+            self.parent.children.append(self)
+            self.first_connection = False
+
+
+@dataclasses.dataclass(eq=False)
+class MapPoint:
+    id: int
+    pos: np.ndarray                 # float32[3]
+    ref_kf: KeyFrame
+    desc: np.ndarray = None         # distinctive descriptor (32 B)
+    normal: np.ndarray = None
+    max_distance: np.float32 = np.float32(0)
+    min_distance: np.float32 = np.float32(0)
+    observations: dict = dataclasses.field(default_factory=dict)   # KeyFrame -> keypoint index
+    nobs: int = 0
+    bad: bool = False
+
+    def add_observation(self, kf: KeyFrame, idx: int):
+        """MapPoint::AddObservation (src/MapPoint.cc:90-105): stereo observations count 2."""
+        if kf in self.observations:
+            return
+        self.observations[kf] = idx
+        self.nobs += 2 if kf.u_right[idx] >= 0 else 1
+
+    def erase_observation(self, kf: KeyFrame):
+        """MapPoint::EraseObservation (src/MapPoint.cc:111-137)."""
+        if kf not in self.observations:
+            return
+        idx = self.observations.pop(kf)
+        self.nobs -= 2 if kf.u_right[idx] >= 0 else 1
+        if self.ref_kf is kf and self.observations:
+            self.ref_kf = min(self.observations, key=lambda k: k.id)
+        if self.nobs <= 2:
+            self.set_bad()
+
+    def set_bad(self):
+        """MapPoint::SetBadFlag (src/MapPoint.cc:151-170)."""
+        self.bad = True
+        for kf, idx in self.observations.items():
+            if kf.map_points[idx] is self:
+                kf.map_points[idx] = None
+        self.observations = {}
+
+    def update_normal_and_depth(self):
+        """MapPoint::UpdateNormalAndDepth (src/MapPoint.cc:339-390) in float32."""
+        if self.bad or not self.observations:
+            return
+        normal = np.zeros(3, np.float32)
+        for kf in sorted(self.observations, key=lambda k: k.id):
+            v = (self.pos - kf.Ow).astype(np.float32)   # normali / cv::norm(normali): alpha in double
+            normal = (normal + (v.astype(np.float64) * (1.0 / np.linalg.norm(v.astype(np.float64)))).astype(np.float32))
+        PC = (self.pos - self.ref_kf.Ow).astype(np.float32)
+        dist = np.float32(np.linalg.norm(PC.astype(np.float64)))
+        level = int(self.ref_kf.keys_un[self.observations[self.ref_kf]]["octave"])
+        sf = self.ref_kf.scale_factors
+        self.max_distance = np.float32(dist * sf[level])
+        self.min_distance = np.float32(self.max_distance / sf[len(sf) - 1])
+        self.normal = (normal.astype(np.float64) * (1.0 / len(self.observations))).astype(np.float32)
+
+
+# ---- the per-frame state Tracking keeps (include/Frame.h) ----------------------------------
+@dataclasses.dataclass(eq=False)
+class TrackedFrame:
+    id: int
+    timestamp: float
+    keys: np.ndarray
+    desc: np.ndarray
+    u_right: np.ndarray
+    depth: np.ndarray
+    tcw: np.ndarray = None
+    map_points: list = None          # mvpMapPoints
+    outlier: np.ndarray = None       # mvbOutlier
+    ref_kf: KeyFrame = None
+    feat_vec: object = None
+
+    @property
+    def n(self):
+        return len(self.keys)
+
+
+class GpuBackend:
+    """The MI355X operators behind the reference's interfaces (liborbmi.so; raises when the
+    library or the GPU is missing -- there is no CPU path)."""
+
+    def __init__(self, settings, device: int = 0, vocabulary=None):
+        from .matcher import ORBmatcher
+        from .optimizer import LocalBA, PoseOptimizer
+        from .orb import ORBextractor
+        s = settings
+        self.left = ORBextractor(s.n_features, float(s.scale_factor), s.n_levels, s.ini_th_fast, s.min_th_fast,
+                                 device=device)
+        self.right = ORBextractor(s.n_features, float(s.scale_factor), s.n_levels, s.ini_th_fast, s.min_th_fast,
+                                  device=device)
+        self.scale_factors = np.ascontiguousarray(self.left.GetScaleFactors(), np.float32)
+        self.inv_level_sigma2 = np.ascontiguousarray(self.left.GetInverseScaleSigmaSquares(), np.float32)
+        self.m_lf = ORBmatcher(0.9, True, device=device)     # src/Tracking.cc:1002
+        self.m_local = ORBmatcher(0.8, True, device=device)  # src/Tracking.cc:1391
+        self.m_bow = ORBmatcher(0.7, True, device=device)    # src/Tracking.cc:878
+        self.m_util = ORBmatcher(device=device)
+        self.pose = PoseOptimizer(device)
+        self.ba = LocalBA(device)
+        self.vocab = None
+        if vocabulary is not None:
+            from .vocabulary import ORBVocabulary
+            self.vocab = ORBVocabulary(vocabulary, device)
+
+    def extract_stereo(self, imL, imR):
+        """Frame::Frame (stereo) (src/Frame.cc:58-100): ORBextractor on both images and
+        ComputeStereoMatches -> keys, desc, mvuRight, mvDepth."""
+        from .orb import compute_stereo_matches
+        kl, dl = self.left(imL)
+        kr, dr = self.right(imR)
+        n = len(kl)
+        if dl is None:
+            dl = np.zeros((0, 32), np.uint8)
+        u, d = compute_stereo_matches(self.left, self.right, self.cam_bf, self.cam_fx, n)
+        return kl, dl, u, d
+
+    def bind_camera(self, cam):
+        self.cam_bf, self.cam_fx = float(cam.bf), float(cam.fx)
+
+    def compute_bow(self, desc):
+        if self.vocab is None:
+            raise RuntimeError("TrackReferenceKeyFrame needs a vocabulary (StereoSLAM(vocabulary=...))")
+        return self.vocab.ComputeBoW(desc)[2]
+
+    def search_by_bow(self, kf, kf_mp_ok, kf_fv, f, f_fv):
+        return self.m_bow.SearchByBoW(kf, kf_mp_ok, kf_fv, f, f_fv)
+
+    def search_last_frame(self, cf, occupied, lf, lfp, th):
+        return self.m_lf.SearchByProjectionLastFrame(cf, occupied, lf, lfp, th, False)
+
+    def search_local_points(self, cf, occupied, mps, th):
+        m, n, _ = self.m_local.SearchLocalPoints(cf, occupied, mps, th)
+        return m, n
+
+    def pose_optimization(self, cf, match_lf=None, lf_points=None, match_mp=None, mps=None):
+        from .types import POSE_FRAME_DTYPE
+        mp, keep = frame_mappoints(match_lf, lf_points, match_mp, mps)
+        rec = np.zeros(1, POSE_FRAME_DTYPE)
+        out = np.zeros(max(len(cf.keys), 1), np.uint8)
+        v = cf.view()
+        self.pose.PoseOptimization(v, self.inv_level_sigma2, mp, rec, out)
+        del keep
+        return rec[0]["tcw"].reshape(4, 4).copy(), out[:len(cf.keys)].copy()
+
+    def distinctive(self, obs_desc, obs_off):
+        return self.m_util.ComputeDistinctiveDescriptors(obs_desc, obs_off)[1]
+
+    def local_ba(self, problem, stop=None):
+        return self.ba.run(problem, stop)
+
+    def close(self):
+        for h in (self.ba, self.pose, self.m_util, self.m_bow, self.m_local, self.m_lf, self.right, self.left):
+            h.close()
+        if self.vocab is not None:
+            self.vocab.close()
+
+
+def frame_mappoints(match_lf, lf_points, match_mp, mps):
+    """orbmi_frame_mappoints over host arrays -> (struct, arrays to keep alive)."""
+    from .types import FrameMapPoints
+    mp = FrameMapPoints()
+    keep = []
+    if match_lf is not None:
+        match_lf = np.ascontiguousarray(match_lf, np.int32)
+        lf_points = np.ascontiguousarray(lf_points)
+        keep += [match_lf, lf_points]
+        mp.match_lf, mp.lf_points, mp.n_lf_points = match_lf.ctypes.data, lf_points.ctypes.data, len(lf_points)
+    if match_mp is not None:
+        match_mp = np.ascontiguousarray(match_mp, np.int32)
+        mps = np.ascontiguousarray(mps)
+        keep += [match_mp, mps]
+        mp.match_mp, mp.mps, mp.n_mps = match_mp.ctypes.data, mps.ctypes.data, len(mps)
+    return mp, keep
+
+
+class StereoSLAM:
+    """System(strSettingsFile, STEREO) + Tracking + a synchronous LocalMapping over a backend.
+
+    TrackStereo(imLeft, imRight, timestamp) -> Tcw (4x4 float32, or None while not
+    initialised / lost), as System::TrackStereo returns mCurrentFrame.mTcw."""
+
+    def __init__(self, settings, backend=None, device: int = 0, vocabulary=None, local_ba: bool = True):
+        from .settings import Settings, load_settings
+        self.settings = settings if isinstance(settings, Settings) else load_settings(settings)
+        s = self.settings
+        if s.width <= 0 or s.height <= 0:
+            raise ValueError("settings need Camera.width / Camera.height")
+        self.cam = s.camera
+        self.backend = backend if backend is not None else GpuBackend(s, device, vocabulary)
+        if hasattr(self.backend, "bind_camera"):
+            self.backend.bind_camera(self.cam)
+        self.use_local_ba = local_ba
+        self.state = NO_IMAGES_YET
+        self.keyframes: list[KeyFrame] = []
+        self.mappoints: list[MapPoint] = []
+        self.frame_count = 0
+        self.last_frame: TrackedFrame | None = None
+        self.velocity = None
+        self.ref_kf: KeyFrame | None = None
+        self.last_kf_frame_id = 0
+        self.last_reloc_frame_id = 0
+        self.local_kfs: list[KeyFrame] = []
+        self.local_mps: list[MapPoint] = []
+        self.matches_inliers = 0
+        # mlRelativeFramePoses, mlpReferences, mlFrameTimes, mlbLost (src/Tracking.cc:557-580)
+        self.rel_poses, self.references, self.frame_times, self.lost = [], [], [], []
+        self.stats = []   # per frame: dict of the Tracking counters
+        self.ba_log = []  # per LocalBundleAdjustment: graph size and erased observations
+
+    # ---- System::TrackStereo ----------------------------------------------------------------
+    def TrackStereo(self, imLeft, imRight, timestamp: float):
+        keys, desc, u_right, depth = self.backend.extract_stereo(imLeft, imRight)
+        n = len(keys)
+        cf = TrackedFrame(self.frame_count, float(timestamp), keys, desc.reshape(-1, 32), u_right, depth,
+                          map_points=[None] * n, outlier=np.zeros(n, bool))
+        self.frame_count += 1
+        self._track(cf)
+        return None if cf.tcw is None else cf.tcw.copy()
+
+    def _frame(self, f: TrackedFrame, tcw=None) -> Frame:
+        return Frame(f.keys, f.desc, f.u_right, f.tcw if tcw is None else tcw, self.cam, self.backend.scale_factors,
+                     self.cam.width, self.cam.height)
+
+    def _track(self, cf: TrackedFrame):
+        """Tracking::Track for a stereo sensor in SLAM mode (src/Tracking.cc:287-581)."""
+        if self.state == NO_IMAGES_YET:
+            self.state = NOT_INITIALIZED
+        st = {"frame": cf.id, "n": cf.n}
+        if self.state == NOT_INITIALIZED:
+            self._stereo_initialization(cf)
+            st["init"] = self.state == OK
+            if self.state != OK:
+                self.stats.append(st)
+                return
+            ok = True
+        else:
+            if self.state == OK:
+                if self.velocity is None or cf.id < self.last_reloc_frame_id + 2:
+                    ok = self._track_reference_kf(cf, st)
+                else:
+                    ok = self._track_motion_model(cf, st)
+                    if not ok:
+                        ok = self._track_reference_kf(cf, st)
+            else:
+                ok = False   # Relocalization is out of scope
+            cf.ref_kf = self.ref_kf
+            if ok:
+                ok = self._track_local_map(cf, st)
+            self.state = OK if ok else LOST
+            if ok:
+                if self.last_frame.tcw is not None:
+                    self.velocity = _mul(cf.tcw, pose_inverse(self.last_frame.tcw))
+                else:
+                    self.velocity = None
+                for i, mp in enumerate(cf.map_points):   # clean VO matches (:504-513)
+                    if mp is not None and mp.nobs < 1:
+                        cf.outlier[i] = False
+                        cf.map_points[i] = None
+                if self._need_new_keyframe(cf, st):
+                    self._create_new_keyframe(cf)
+                for i, mp in enumerate(cf.map_points):   # (:535-539)
+                    if mp is not None and cf.outlier[i]:
+                        cf.map_points[i] = None
+            if cf.ref_kf is None:
+                cf.ref_kf = self.ref_kf
+        self.last_frame = cf
+        if cf.tcw is not None:
+            self.rel_poses.append(_mul(cf.tcw, pose_inverse(cf.ref_kf.tcw)))
+            self.references.append(self.ref_kf)
+            self.frame_times.append(cf.timestamp)
+            self.lost.append(self.state == LOST)
+        elif self.rel_poses:
+            self.rel_poses.append(self.rel_poses[-1])
+            self.references.append(self.references[-1])
+            self.frame_times.append(self.frame_times[-1])
+            self.lost.append(self.state == LOST)
+        st["state"] = self.state
+        st["keyframes"] = len(self.keyframes)
+        st["mappoints"] = sum(1 for m in self.mappoints if not m.bad)
+        self.stats.append(st)
+
+    # ---- initialisation and keyframes ---------------------------------------------------------
+    def _new_keyframe(self, cf: TrackedFrame) -> KeyFrame:
+        kf = KeyFrame(len(self.keyframes), cf.id, cf.timestamp, cf.tcw.copy(), cf.keys, cf.desc, cf.u_right,
+                      cf.depth, self.backend.inv_level_sigma2, self.backend.scale_factors, self.cam,
+                      list(cf.map_points), feat_vec=cf.feat_vec)
+        return kf
+
+    def _unproject(self, f: TrackedFrame, idx: np.ndarray) -> np.ndarray:
+        """Frame::UnprojectStereo (src/Frame.cc:701-715) in float32."""
+        c = self.cam
+        z = f.depth[idx].astype(np.float32)
+        invfx, invfy = np.float32(1.0) / np.float32(c.fx), np.float32(1.0) / np.float32(c.fy)
+        x = ((f.keys["x"][idx] - np.float32(c.cx)) * z * invfx).astype(np.float32)
+        y = ((f.keys["y"][idx] - np.float32(c.cy)) * z * invfy).astype(np.float32)
+        Twc = pose_inverse(f.tcw)
+        pc = np.stack([x, y, z], 0).astype(np.float64)
+        return ((Twc[:3, :3].astype(np.float64) @ pc).astype(np.float32) + Twc[:3, 3:4]).T.astype(np.float32)
+
+    def _create_points(self, kf: KeyFrame, cf: TrackedFrame, idx: list):
+        """new MapPoint(x3D, pKF, pMap) + AddObservation + AddMapPoint + ComputeDistinctive +
+        UpdateNormalAndDepth for the keypoints `idx` (src/Tracking.cc:602-616, :1308-1320)."""
+        if not idx:
+            return
+        X = self._unproject(cf, np.asarray(idx))
+        for j, i in enumerate(idx):
+            mp = MapPoint(len(self.mappoints), X[j].copy(), kf)
+            mp.add_observation(kf, i)
+            kf.map_points[i] = mp
+            mp.desc = cf.desc[i].copy()   # ComputeDistinctiveDescriptors of one observation
+            mp.update_normal_and_depth()
+            self.mappoints.append(mp)
+            cf.map_points[i] = mp
+
+    def _stereo_initialization(self, cf: TrackedFrame):
+        """Tracking::StereoInitialization (src/Tracking.cc:584-636)."""
+        if cf.n <= 500:
+            return
+        cf.tcw = np.eye(4, dtype=np.float32)
+        kf = self._new_keyframe(cf)
+        self.keyframes.append(kf)
+        self._create_points(kf, cf, [i for i in range(cf.n) if cf.depth[i] > 0])
+        self._local_mapping(kf)
+        self.last_kf_frame_id = cf.id
+        self.local_kfs = [kf]
+        self.local_mps = [m for m in self.mappoints if not m.bad]
+        self.ref_kf = kf
+        cf.ref_kf = kf
+        self.last_frame = cf
+        self.state = OK
+
+    def _need_new_keyframe(self, cf: TrackedFrame, st) -> bool:
+        """Tracking::NeedNewKeyFrame (src/Tracking.cc:1140-1249) with LocalMapping idle."""
+        s = self.settings
+        nkfs = len(self.keyframes)
+        if cf.id < self.last_reloc_frame_id + s.max_frames and nkfs > s.max_frames:
+            return False
+        min_obs = 2 if nkfs <= 2 else 3
+        n_ref = self.ref_kf.tracked_map_points(min_obs)
+        close = (cf.depth > 0) & (cf.depth < s.th_depth)
+        tracked = np.array([mp is not None for mp in cf.map_points], bool) & ~cf.outlier
+        n_tracked_close = int(np.sum(close & tracked))
+        n_non_tracked_close = int(np.sum(close & ~tracked))
+        need_close = n_tracked_close < 100 and n_non_tracked_close > 70
+        th_ref = 0.4 if nkfs < 2 else 0.75
+        c1a = cf.id >= self.last_kf_frame_id + s.max_frames
+        c1b = cf.id >= self.last_kf_frame_id + s.min_frames   # LocalMapping idle (synchronous)
+        c1c = self.matches_inliers < n_ref * 0.25 or need_close
+        c2 = (self.matches_inliers < n_ref * np.float32(th_ref) or need_close) and self.matches_inliers > 15
+        st["need_kf"] = bool((c1a or c1b or c1c) and c2)
+        return st["need_kf"]
+
+    def _create_new_keyframe(self, cf: TrackedFrame):
+        """Tracking::CreateNewKeyFrame for stereo (src/Tracking.cc:1251-1330)."""
+        kf = self._new_keyframe(cf)
+        self.keyframes.append(kf)
+        self.ref_kf = kf
+        cf.ref_kf = kf
+        order = sorted(((float(cf.depth[i]), i) for i in range(cf.n) if cf.depth[i] > 0))
+        new, npts = [], 0
+        for z, i in order:
+            mp = cf.map_points[i]
+            create = mp is None or mp.nobs < 1
+            if create and mp is not None:
+                cf.map_points[i] = None
+                kf.map_points[i] = None
+            if create:
+                new.append(i)
+            npts += 1
+            if z > self.settings.th_depth and npts > 100:
+                break
+        self._create_points(kf, cf, new)
+        self._local_mapping(kf)
+        self.last_kf_frame_id = cf.id
+
+    # ---- LocalMapping (synchronous) ---------------------------------------------------------
+    def _distinctive(self, mps: list):
+        """MapPoint::ComputeDistinctiveDescriptors for a batch of points (src/MapPoint.cc:247-316)
+        on the backend: descriptors of the non-bad observing keyframes, keyframe-id order."""
+        rows, off = [], [0]
+        for mp in mps:
+            for kf in sorted(mp.observations, key=lambda k: k.id):
+                if not kf.bad:
+                    rows.append(kf.desc[mp.observations[kf]])
+            off.append(len(rows))
+        if not rows:
+            return
+        d = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32))
+        for j, mp in enumerate(mps):
+            if off[j + 1] > off[j]:
+                mp.desc = np.asarray(d[j], np.uint8).copy()
+
+    def _local_mapping(self, kf: KeyFrame):
+        """LocalMapping::Run for one keyframe: ProcessNewKeyFrame (src/LocalMapping.cc:152-200)
+        and Optimizer::LocalBundleAdjustment when the map holds more than 2 keyframes (:89-90)."""
+        if self.backend_has_bow():
+            kf.feat_vec = kf.feat_vec or self.backend.compute_bow(kf.desc)
+        updated = []
+        for i, mp in enumerate(kf.map_points):
+            if mp is None or mp.bad:
+                continue
+            if kf not in mp.observations:
+                mp.add_observation(kf, i)
+                mp.update_normal_and_depth()
+                updated.append(mp)
+        self._distinctive(updated)
+        kf.update_connections()
+        if self.use_local_ba and len(self.keyframes) > 2:
+            self._local_bundle_adjustment(kf)
+
+    def backend_has_bow(self) -> bool:
+        return getattr(self.backend, "vocab", None) is not None
+
+    def _local_bundle_adjustment(self, kf: KeyFrame):
+        """Optimizer::LocalBundleAdjustment (src/Optimizer.cc:483-808): graph assembly on the host
+        (optimizer.gather_local_ba), optimisation on the backend, write-back under the map lock."""
+        from .optimizer import gather_local_ba
+        problem, kfs, mps = gather_local_ba(kf)
+        if len(problem.edges) == 0:
+            return
+        res = self.backend.local_ba(problem)
+        erase = np.asarray(res["erase"], bool)
+        self.ba_log.append({"keyframe": kf.id, "keyframes": len(kfs), "points": len(mps),
+                            "edges": len(problem.edges), "erased": int(erase.sum())})
+        for e in np.nonzero(erase)[0]:
+            ed = problem.edges[e]
+            mp, k = mps[int(ed["point"])], kfs[int(ed["kf"])]
+            if k in mp.observations and k.map_points[mp.observations[k]] is mp:
+                k.map_points[mp.observations[k]] = None    # KeyFrame::EraseMapPointMatch
+            mp.erase_observation(k)
+        n_local = 1 + sum(1 for k in kf.covisible if not k.bad)
+        for i in range(n_local):
+            kfs[i].tcw = np.asarray(res["tcw"][i], np.float32).reshape(4, 4).copy()
+        for j, mp in enumerate(mps):
+            mp.pos = np.asarray(res["pos"][j], np.float32).copy()
+            mp.update_normal_and_depth()
+
+    # ---- tracking stages --------------------------------------------------------------------
+    def _mp_records(self, mps: list, seen: set) -> np.ndarray:
+        """orbmi_mappoint records of local map points (include/orbmi.h)."""
+        rec = np.zeros(len(mps), MAPPOINT_DTYPE)
+        for j, mp in enumerate(mps):
+            rec[j]["pos"] = mp.pos
+            rec[j]["normal"] = mp.normal
+            rec[j]["max_distance"] = mp.max_distance
+            rec[j]["min_distance"] = mp.min_distance
+            rec[j]["desc"] = mp.desc
+            fl = (MP_BAD if mp.bad else 0) | (MP_SEEN if id(mp) in seen else 0) | (MP_HAS_OBS if mp.nobs > 0 else 0)
+            rec[j]["flags"] = fl
+        return rec
+
+    def _lf_records(self, lf_mps: list, outlier) -> np.ndarray:
+        """orbmi_lastframe_point records of a frame's mvpMapPoints (include/orbmi.h)."""
+        rec = np.zeros(len(lf_mps), LFPOINT_DTYPE)
+        for i, mp in enumerate(lf_mps):
+            if mp is None:
+                continue
+            rec[i]["pos"] = mp.pos
+            rec[i]["desc"] = mp.desc
+            rec[i]["flags"] = LF_HAS_MP | (LF_OUTLIER if outlier is not None and outlier[i] else 0) | \
+                (MP_HAS_OBS if mp.nobs > 0 else 0)
+        return rec
+
+    def _discard_outliers(self, cf: TrackedFrame, outlier, seen: set) -> int:
+        """The pass after PoseOptimization in TrackReferenceKeyFrame / TrackWithMotionModel
+        (src/Tracking.cc:904-917, :1036-1058) -> nmatchesMap."""
+        nmap = 0
+        for i, mp in enumerate(cf.map_points):
+            if mp is None:
+                continue
+            if outlier[i]:
+                cf.map_points[i] = None
+                cf.outlier[i] = False
+                seen.add(id(mp))   # pMP->mnLastFrameSeen = mCurrentFrame.mnId
+            elif mp.nobs > 0:
+                nmap += 1
+        return nmap
+
+    def _update_last_frame(self):
+        """Tracking::UpdateLastFrame (src/Tracking.cc:919-995) in SLAM mode: only the pose."""
+        lf = self.last_frame
+        lf.tcw = _mul(self.rel_poses[-1], lf.ref_kf.tcw)
+
+    def _track_reference_kf(self, cf: TrackedFrame, st) -> bool:
+        """Tracking::TrackReferenceKeyFrame (src/Tracking.cc:871-917)."""
+        cf.feat_vec = self.backend.compute_bow(cf.desc)
+        kf = self.ref_kf
+        if kf.feat_vec is None:
+            kf.feat_vec = self.backend.compute_bow(kf.desc)
+        ok_mp = np.array([mp is not None and not mp.bad for mp in kf.map_points], np.uint8)
+        kfv = Frame(kf.keys_un, kf.desc, kf.u_right, kf.tcw, self.cam, self.backend.scale_factors,
+                    self.cam.width, self.cam.height)
+        m, n = self.backend.search_by_bow(kfv, ok_mp, kf.feat_vec, self._frame(cf, np.eye(4)), cf.feat_vec)
+        st["bow_matches"] = n
+        st["track"] = "reference_kf"
+        if n < 15:
+            return False
+        cf.map_points = [kf.map_points[j] if j >= 0 else None for j in m]
+        cf.tcw = self.last_frame.tcw.copy()
+        lfp = self._lf_records(kf.map_points, None)
+        tcw, out = self.backend.pose_optimization(self._frame(cf), np.asarray(m, np.int32), lfp)
+        cf.tcw = tcw
+        cf.outlier = out.astype(bool)
+        self._seen = set()
+        nmap = self._discard_outliers(cf, cf.outlier.copy(), self._seen)
+        st["nmatches_map"] = nmap
+        return nmap >= 10
+
+    def _track_motion_model(self, cf: TrackedFrame, st) -> bool:
+        """Tracking::TrackWithMotionModel (src/Tracking.cc:997-1063)."""
+        self._update_last_frame()
+        lf = self.last_frame
+        cf.tcw = _mul(self.velocity, lf.tcw)
+        lfp = self._lf_records(lf.map_points, lf.outlier)
+        occ = np.zeros(cf.n, np.uint8)
+        lfv = self._frame(lf)
+        th = 7.0   # stereo (src/Tracking.cc:1011-1014)
+        m, n = self.backend.search_last_frame(self._frame(cf), occ, lfv, lfp, th)
+        if n < 20:
+            m, n = self.backend.search_last_frame(self._frame(cf), occ, lfv, lfp, 2 * th)
+        st["track"] = "motion_model"
+        st["lf_matches"] = n
+        if n < 20:
+            return False
+        cf.map_points = [lf.map_points[j] if j >= 0 else None for j in m]
+        tcw, out = self.backend.pose_optimization(self._frame(cf), np.asarray(m, np.int32), lfp)
+        cf.tcw = tcw
+        cf.outlier = out.astype(bool)
+        self._seen = set()
+        nmap = self._discard_outliers(cf, cf.outlier.copy(), self._seen)
+        st["nmatches_map"] = nmap
+        return nmap >= 10
+
+    def _update_local_keyframes(self, cf: TrackedFrame):
+        """Tracking::UpdateLocalKeyFrames (src/Tracking.cc:1452-1580), including its early exit
+        of the outer loop after a parent is added."""
+        counter: dict = {}
+        for i, mp in enumerate(cf.map_points):
+            if mp is None:
+                continue
+            if mp.bad:
+                cf.map_points[i] = None
+                continue
+            for kf in mp.observations:
+                counter[kf] = counter.get(kf, 0) + 1
+        if not counter:
+            return
+        best, kfmax = 0, None
+        local, mark = [], set()
+        for kf in sorted(counter, key=lambda k: k.id):
+            if kf.bad:
+                continue
+            if counter[kf] > best:
+                best, kfmax = counter[kf], kf
+            local.append(kf)
+            mark.add(id(kf))
+        i = 0
+        while i < len(local):
+            if len(local) > 80:
+                break
+            kf = local[i]
+            i += 1
+            for nb in kf.best_covisibility(10):
+                if not nb.bad and id(nb) not in mark:
+                    local.append(nb)
+                    mark.add(id(nb))
+                    break
+            for ch in sorted(kf.children, key=lambda k: k.id):
+                if not ch.bad and id(ch) not in mark:
+                    local.append(ch)
+                    mark.add(id(ch))
+                    break
+            p = kf.parent
+            if p is not None and id(p) not in mark:
+                local.append(p)
+                mark.add(id(p))
+                break
+        self.local_kfs = local
+        if kfmax is not None:
+            self.ref_kf = kfmax
+            cf.ref_kf = kfmax
+
+    def _update_local_points(self):
+        """Tracking::UpdateLocalPoints (src/Tracking.cc:1421-1450)."""
+        out, mark = [], set()
+        for kf in self.local_kfs:
+            for mp in kf.map_points:
+                if mp is None or id(mp) in mark or mp.bad:
+                    continue
+                out.append(mp)
+                mark.add(id(mp))
+        self.local_mps = out
+
+    def _track_local_map(self, cf: TrackedFrame, st) -> bool:
+        """Tracking::TrackLocalMap (src/Tracking.cc:1075-1104) with UpdateLocalMap and
+        SearchLocalPoints (:1345-1420)."""
+        self._update_local_keyframes(cf)
+        self._update_local_points()
+        seen = getattr(self, "_seen", set())
+        occ = np.zeros(cf.n, np.uint8)
+        for i, mp in enumerate(cf.map_points):   # SearchLocalPoints' first loop
+            if mp is None:
+                continue
+            if mp.bad:
+                cf.map_points[i] = None
+            else:
+                seen.add(id(mp))
+                occ[i] = 1 if mp.nobs > 0 else 0
+        mps = self.local_mps
+        rec = self._mp_records(mps, seen)
+        m_mp, nl = self.backend.search_local_points(self._frame(cf), occ, rec, 1.0)
+        st["local_map_points"] = len(mps)
+        st["local_matches"] = nl
+        m_lf = np.full(cf.n, -1, np.int32)
+        cur = list(cf.map_points)
+        for i, j in enumerate(m_mp):
+            if j >= 0:
+                cur[i] = mps[j]
+        # PoseOptimization over the frame's map points: one record per keypoint
+        lfp = self._lf_records(cur, None)
+        for i, mp in enumerate(cur):
+            if mp is not None:
+                m_lf[i] = i
+        tcw, out = self.backend.pose_optimization(self._frame(cf), m_lf, lfp)
+        cf.tcw = tcw
+        cf.map_points = cur
+        cf.outlier = out.astype(bool)
+        inliers = 0
+        for i, mp in enumerate(cf.map_points):   # (:1087-1101)
+            if mp is None:
+                continue
+            if not cf.outlier[i]:
+                if mp.nobs > 0:
+                    inliers += 1
+            elif cf.u_right[i] >= 0:   # stereo outliers are dropped
+                cf.map_points[i] = None
+        self.matches_inliers = inliers
+        st["inliers"] = inliers
+        return inliers >= 30
+
+    # ---- output (src/System.cc:334-486) ---------------------------------------------------------
+    def _frame_poses(self):
+        """Tcw of every recorded frame, Tcr * Tr(w) with Two of the first keyframe."""
+        if not self.keyframes:
+            return []
+        Two = pose_inverse(sorted(self.keyframes, key=lambda k: k.id)[0].tcw)
+        out = []
+        for Tcr, kf, t, lost in zip(self.rel_poses, self.references, self.frame_times, self.lost):
+            Trw = np.eye(4, dtype=np.float32)
+            while kf.bad:   # keyframe culling is out of scope, kept for the reference's shape
+                Trw = _mul(Trw, kf.tcp)
+                kf = kf.parent
+            Trw = _mul(Trw, kf.tcw, Two)
+            out.append((_mul(Tcr, Trw), t, lost))
+        return out
+
+    def trajectory_twc(self) -> np.ndarray:
+        """(n_frames, 4, 4) float32 Twc as SaveTrajectoryKITTI computes them."""
+        return np.array([pose_inverse(T) for T, _, _ in self._frame_poses()], np.float32).reshape(-1, 4, 4)
+
+    def SaveTrajectoryKITTI(self, filename: str):
+        """System::SaveTrajectoryKITTI (src/System.cc:433-486): 3x4 Twc per frame, fixed, 9 digits."""
+        with open(filename, "w") as f:
+            for Tcw, _, _ in self._frame_poses():
+                Rwc = Tcw[:3, :3].T
+                twc = -_mul(Rwc, Tcw[:3, 3:4])[:, 0]
+                row = [Rwc[0, 0], Rwc[0, 1], Rwc[0, 2], twc[0], Rwc[1, 0], Rwc[1, 1], Rwc[1, 2], twc[1],
+                       Rwc[2, 0], Rwc[2, 1], Rwc[2, 2], twc[2]]
+                f.write(" ".join(f"{float(np.float32(v)):.9f}" for v in row) + "\n")
+
+    def SaveTrajectoryTUM(self, filename: str):
+        """System::SaveTrajectoryTUM (src/System.cc:334-389): lost frames skipped."""
+        with open(filename, "w") as f:
+            for Tcw, t, lost in self._frame_poses():
+                if lost:
+                    continue
+                Rwc = Tcw[:3, :3].T
+                twc = -_mul(Rwc, Tcw[:3, 3:4])[:, 0]
+                q = quaternion_xyzw(Rwc)
+                f.write(f"{t:.6f} " + " ".join(f"{float(v):.9f}" for v in (*twc, *q)) + "\n")
+
+    def SaveKeyFrameTrajectoryTUM(self, filename: str):
+        """System::SaveKeyFrameTrajectoryTUM (src/System.cc:392-431)."""
+        with open(filename, "w") as f:
+            for kf in sorted(self.keyframes, key=lambda k: k.id):
+                if kf.bad:
+                    continue
+                q = quaternion_xyzw(kf.tcw[:3, :3].T)
+                t = kf.Ow
+                f.write(f"{kf.timestamp:.6f} " + " ".join(f"{float(v):.7f}" for v in (*t, *q)) + "\n")
+
+    def Shutdown(self):
+        self.backend.close()
+
+
+def ate_rmse(est_twc: np.ndarray, gt_twc: np.ndarray) -> float:
+    """Absolute trajectory error (translation RMSE, metres) of camera centres, both trajectories
+    expressed relative to their first frame (the reference's files start at the first keyframe)."""
+    est = np.asarray(est_twc, np.float64)
+    gt = np.asarray(gt_twc, np.float64)
+    g0 = np.linalg.inv(gt[0])
+    e0 = np.linalg.inv(est[0])
+    d = [(e0 @ e)[:3, 3] - (g0 @ g)[:3, 3] for e, g in zip(est, gt)]
+    return float(np.sqrt(np.mean(np.sum(np.square(d), axis=1))))
