@@ -18,7 +18,10 @@ scaling) and each step all-gathers the streams' left descriptors + keypoints ove
 matches its descriptors against the other streams' (build-defined cross-stream matching).
 
 Other modes: `--mode extract` (extraction + stereo only), `--mode lba` (config 3 alone),
-`--mode batch` (config 5: EuRoC-shaped 752x480 mono, 5000 features, 64 frames per launch).
+`--mode batch` (config 5: EuRoC-shaped 752x480 mono, 5000 features, 64 frames per launch),
+`--mode system` (SURVEY.md §8(f) rank 4: the whole StereoSLAM host loop -- System::TrackStereo
+with the map, keyframes and synchronous LocalMapping + LocalBA on the host around the GPU
+operators -- over a rendered sequence with exact ground truth; reports frames/s and ATE).
 
 Prints ONE JSON line on rank 0 (contract: task statement; fields documented in DESIGN.md).
 """
@@ -50,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--mode", choices=["track", "extract", "lba", "batch"], default="track")
+    ap.add_argument("--mode", choices=["track", "extract", "lba", "batch", "system"], default="track")
     ap.add_argument("--frames", type=int, default=8, help="distinct stereo frames resident per rank")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--batch", type=int, default=64, help="frames per launch in --mode batch")
@@ -636,6 +639,80 @@ def run_lba(a, rank, world, local, dist):
     return out
 
 
+# --------------------------------------------------------------------------------- system
+def run_system(a, rank, world, local, dist):
+    """StereoSLAM.TrackStereo over a rendered KITTI-shaped sequence (frames rank*1000 + f): W
+    untimed frames (initialisation, the first keyframes), then K timed frames.  Host images in,
+    poses out, like System::TrackStereo; the map lives on the host (system.py)."""
+    import tempfile
+    from orb_slam2_with_comment_amd import synth
+    from orb_slam2_with_comment_amd.settings import load_settings, write_settings
+    from orb_slam2_with_comment_amd.system import StereoSLAM, ate_rmse
+    from orb_slam2_with_comment_amd.vocabulary import Vocabulary
+    W, K = max(a.warmup, 2), max(min(a.steps, 100), 3)
+    frames = [synth.stereo_pair(synth.KITTI, f) for f in range(W + K)]
+    tmp = tempfile.mkdtemp()
+    path = os.path.join(tmp, "KITTI_synth.yaml")
+    write_settings(path, synth.KITTI, n_features=a.nfeatures)
+    s = load_settings(path)
+    voc = Vocabulary.synthetic(k=10, L=5, seed=3)
+
+    def drive(slam, idx):
+        for f in idx:
+            L, R, _ = frames[f]
+            slam.TrackStereo(L, R, 0.1 * f)
+
+    slam = StereoSLAM(s, device=local, vocabulary=voc)
+    drive(slam, range(W))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    drive(slam, range(W, W + K))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
+    gt = np.array([fr[2] for fr in frames])
+    est = slam.trajectory_twc()
+    ate = ate_rmse(est, gt)
+    ok = sum(1 for st in slam.stats if st.get("state") == 2)
+    out = None
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from slam_backends import OracleBackend
+            ref = StereoSLAM(s, backend=OracleBackend(s, voc))
+            n, t1 = 0, time.perf_counter()
+            while n < W + K:
+                L, R, _ = frames[n]
+                ref.TrackStereo(L, R, 0.1 * n)
+                n += 1
+                if time.perf_counter() - t1 > a.cpu_sample_s and n >= W + 3:
+                    break
+            el = time.perf_counter() - t1
+            cpu = {"value": round(n / el, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+                   "sample": f"first {n} frames of the same sequence through the same host logic on the oracle "
+                             f"backend (1 thread), {el:.1f} s"}
+        out = {
+            "metric": "frames/sec (StereoSLAM.TrackStereo, host map + synchronous LocalMapping)",
+            "value": round(K * world / dt, 3), "unit": "frames/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(dt / K * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: ray-cast KITTI-shaped 1241x376 stereo sequence with exact ground truth",
+            "config": {"workload": "System::TrackStereo loop: Frame ctor + Track (motion model / reference KF) + "
+                                   "TrackLocalMap + keyframe insertion + ProcessNewKeyFrame + LocalBA",
+                       "frames": W + K, "parallelism": "one stream per GPU"},
+            "ate_rmse_m": round(ate, 5), "frames_tracked": ok, "keyframes": len(slam.keyframes),
+            "local_ba_calls": len(slam.ba_log),
+            "mappoints": int(sum(1 for m in slam.mappoints if not m.bad)),
+            "cpu_baseline": cpu, "host": host_info(),
+        }
+    slam.Shutdown()
+    return out
+
+
 # --------------------------------------------------------------------------------- batch
 def run_batch(a, rank, world, local, dist):
     """Config 5: EuRoC-shaped 752x480 mono, 8 levels, 5000 features, batch frames per launch."""
@@ -723,7 +800,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    run = {"track": run_track, "extract": run_extract, "lba": run_lba, "batch": run_batch}[a.mode]
+    run = {"track": run_track, "extract": run_extract, "lba": run_lba, "batch": run_batch,
+           "system": run_system}[a.mode]
     out = run(a, rank, world, local, dist)
     if rank == 0 and out is not None:
         print(json.dumps(out), flush=True)

@@ -96,7 +96,7 @@ class PoseOptimizer:
         check("orbmi_pose_optimization_frame",
               lib().orbmi_pose_optimization_frame(self._h, C.addressof(view), sig.ctypes.data, C.addressof(mappoints),
                                                   rp, op))
-        return int(rec["inliers"]) if host else None
+        return int(np.asarray(rec["inliers"]).reshape(-1)[0]) if host else None
 
 
 # ---- minimal map model for the graph assembly (src/Optimizer.cc:486-534) ------------------

@@ -114,7 +114,12 @@ class KeyFrame:
 
     @property
     def Ow(self) -> np.ndarray:
-        return pose_inverse(self.tcw)[:3, 3]
+        """Camera centre, cached per pose array (poses are replaced, never edited in place)."""
+        c = self.__dict__.get("_ow")
+        if c is None or c[0] is not self.tcw:
+            c = (self.tcw, pose_inverse(self.tcw)[:3, 3].copy())
+            self.__dict__["_ow"] = c
+        return c[1]
 
     def tracked_map_points(self, min_obs: int) -> int:
         """KeyFrame::TrackedMapPoints (src/KeyFrame.cc:166-193)."""
@@ -606,26 +611,30 @@ class StereoSLAM:
     def _mp_records(self, mps: list, seen: set) -> np.ndarray:
         """orbmi_mappoint records of local map points (include/orbmi.h)."""
         rec = np.zeros(len(mps), MAPPOINT_DTYPE)
-        for j, mp in enumerate(mps):
-            rec[j]["pos"] = mp.pos
-            rec[j]["normal"] = mp.normal
-            rec[j]["max_distance"] = mp.max_distance
-            rec[j]["min_distance"] = mp.min_distance
-            rec[j]["desc"] = mp.desc
-            fl = (MP_BAD if mp.bad else 0) | (MP_SEEN if id(mp) in seen else 0) | (MP_HAS_OBS if mp.nobs > 0 else 0)
-            rec[j]["flags"] = fl
+        if not mps:
+            return rec
+        rec["pos"] = np.array([mp.pos for mp in mps], np.float32)
+        rec["normal"] = np.array([mp.normal for mp in mps], np.float32)
+        rec["max_distance"] = np.array([mp.max_distance for mp in mps], np.float32)
+        rec["min_distance"] = np.array([mp.min_distance for mp in mps], np.float32)
+        rec["desc"] = np.array([mp.desc for mp in mps], np.uint8)
+        rec["flags"] = np.array([(MP_BAD if mp.bad else 0) | (MP_SEEN if id(mp) in seen else 0) |
+                                 (MP_HAS_OBS if mp.nobs > 0 else 0) for mp in mps], np.uint32)
         return rec
 
     def _lf_records(self, lf_mps: list, outlier) -> np.ndarray:
         """orbmi_lastframe_point records of a frame's mvpMapPoints (include/orbmi.h)."""
         rec = np.zeros(len(lf_mps), LFPOINT_DTYPE)
-        for i, mp in enumerate(lf_mps):
-            if mp is None:
-                continue
-            rec[i]["pos"] = mp.pos
-            rec[i]["desc"] = mp.desc
-            rec[i]["flags"] = LF_HAS_MP | (LF_OUTLIER if outlier is not None and outlier[i] else 0) | \
-                (MP_HAS_OBS if mp.nobs > 0 else 0)
+        idx = [i for i, mp in enumerate(lf_mps) if mp is not None]
+        if not idx:
+            return rec
+        pts = [lf_mps[i] for i in idx]
+        rec["pos"][idx] = np.array([mp.pos for mp in pts], np.float32)
+        rec["desc"][idx] = np.array([mp.desc for mp in pts], np.uint8)
+        fl = np.array([LF_HAS_MP | (MP_HAS_OBS if mp.nobs > 0 else 0) for mp in pts], np.uint32)
+        if outlier is not None:
+            fl |= np.where(np.asarray(outlier)[idx], LF_OUTLIER, 0).astype(np.uint32)
+        rec["flags"][idx] = fl
         return rec
 
     def _discard_outliers(self, cf: TrackedFrame, outlier, seen: set) -> int:
