@@ -157,6 +157,14 @@ void orbmi_matcher_destroy(orbmi_matcher* m);
 int orbmi_matcher_share_stream(orbmi_matcher* m, orbmi_extractor* ex);
 /* The handle's HIP stream (hipStream_t): its own, or the extractor's after share_stream. */
 int orbmi_matcher_get_stream(orbmi_matcher* m, void** stream);
+/* Frame::AssignFeaturesToGrid (src/Frame.cc:232-247), run once per Frame as the Frame
+ * constructor does (src/Frame.cc:98): builds the keypoint grid of F (device-resident keypoints
+ * only, else ORBMI_E_ARG) on the handle's stream and pins it, so the searches on the same frame
+ * (same keys / n / n_device / image bounds) skip their rebuild.  The pin ends with
+ * orbmi_matcher_release_grid or when a search on another frame builds its grid; the caller
+ * re-pins whenever the keypoints behind the pointers change (a new frame in the same buffers). */
+int orbmi_matcher_assign_features_to_grid(orbmi_matcher* m, const orbmi_frame_view* F);
+int orbmi_matcher_release_grid(orbmi_matcher* m);
 
 /* Frame::isInFrustum(pMP, viewingCosLimit) for n_mp points (src/Frame.cc:274-342) with
  * MapPoint::PredictScale (src/MapPoint.cc:421-436).  Points flagged BAD or SEEN are skipped

@@ -199,6 +199,25 @@ int orbmi_matcher_share_stream(orbmi_matcher* h, orbmi_extractor* ex) {
     return ORBMI_OK;
 }
 
+int orbmi_matcher_assign_features_to_grid(orbmi_matcher* h, const orbmi_frame_view* v) {
+    if (!h || !v || (v->n > 0 && !on_device(v->keys_un))) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, false))) return rc;
+    if ((rc = orbmi::pin_grid(m, F))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return ORBMI_OK;
+}
+
+int orbmi_matcher_release_grid(orbmi_matcher* h) {
+    if (!h) return ORBMI_E_ARG;
+    h->m.grid_pinned = false;
+    return ORBMI_OK;
+}
+
 int orbmi_matcher_get_stream(orbmi_matcher* h, void** stream) {
     if (!h || !stream) return ORBMI_E_ARG;
     *stream = (void*)h->m.stream;
@@ -264,13 +283,15 @@ int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const
     const uint8_t* d_occ = dev_in(m, occupied, (size_t)std::max(F.n, 1), &rc);
     const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
     if (rc) return rc;
-    if ((rc = scalars(m))) return rc;
+    // k_greedy stores the match count (slot 0) unconditionally; only the nToMatch counter (slot 1,
+    // atomics in k_frustum) needs zeroing, and only when the caller asks for it
+    if ((rc = n_to_match ? scalars(m) : orbmi::ensure_buf(&m.d_scalars, &m.cap_scalars, 4))) return rc;
     if ((rc = orbmi::ensure_buf(&m.d_track, &m.cap_track, (size_t)std::max(n_mp, 1)))) return rc;
     orbmi_mappoint_track* d_tr = m.d_track;
     std::vector<OutBuf> outs;
     int* d_out = dev_out(m, match_mp, (size_t)F.n, outs);
     // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5); ORBmatcher matcher(0.8)
-    if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, 0.5f, d_tr, m.d_scalars + 1))) return rc;
+    if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, 0.5f, d_tr, n_to_match ? m.d_scalars + 1 : nullptr))) return rc;
     if ((rc = orbmi::launch_local_search(m, F, d_occ, d_mps, d_tr, n_mp, th, 0.8f, d_out, m.d_scalars))) return rc;
     ORBMI_HIP(hipGetLastError());
     int ntm = 0;  // read back (and waited for) only when the caller asks for it

@@ -54,6 +54,14 @@ struct Matcher {
     int* d_cell_start = nullptr; size_t cap_cell_start = 0;
     int* d_cell_list = nullptr; size_t cap_cell_list = 0;
     int* d_kp_cell = nullptr; size_t cap_kp_cell = 0;
+    // grid pinned to one frame by orbmi_matcher_assign_features_to_grid (device keypoints only):
+    // searches on that frame skip the rebuild until the pin is released or another frame's grid
+    // is built
+    bool grid_pinned = false;
+    const orbmi_keypoint* pin_keys = nullptr;
+    const int* pin_ndev = nullptr;
+    int pin_n = 0;
+    float pin_geom[6] = {};
     // candidates / greedy
     unsigned long long* d_cand = nullptr; size_t cap_cand = 0;
     int* d_ncand = nullptr; size_t cap_ncand = 0;
@@ -71,6 +79,7 @@ struct Matcher {
     void release();
 };
 
+int pin_grid(Matcher& m, const DevFrame& F);
 int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int n, float cosl,
                    orbmi_mappoint_track* tr, int* n_in_view);
 int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, const orbmi_mappoint* mps,

@@ -21,6 +21,8 @@
 // induction on q.  A bounded round count falls back to the sequential replay.
 #include <algorithm>
 
+#include <cstring>
+
 #include "matcher.h"
 
 namespace orbmi {
@@ -868,14 +870,37 @@ int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, 
 }
 
 // -------------------------------------------------------------------------- host launchers
+static bool grid_is_pinned_for(const Matcher& m, const DevFrame& F) {
+    const float g[6] = {F.min_x, F.max_x, F.min_y, F.max_y, F.grid_w_inv, F.grid_h_inv};
+    return m.grid_pinned && m.pin_keys == F.keys && m.pin_ndev == F.n_dev && m.pin_n == F.n &&
+           memcmp(m.pin_geom, g, sizeof(g)) == 0;
+}
+
 static int grid_for(Matcher& m, const DevFrame& F, const int* gate = nullptr, int gate_min = 0) {
     if (F.n > kGreedyMaxKp) return ORBMI_E_UNSUPPORTED;
+    // Frame::AssignFeaturesToGrid runs once per Frame (src/Frame.cc:232-247): a pinned grid of
+    // this frame is reused as it is
+    if (grid_is_pinned_for(m, F)) return ORBMI_OK;
+    m.grid_pinned = false;
     int rc;
     if ((rc = ensure_buf(&m.d_cell_start, &m.cap_cell_start, (size_t)kGridCells + 1))) return rc;
     if ((rc = ensure_buf(&m.d_cell_list, &m.cap_cell_list, (size_t)std::max(F.n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_kp_cell, &m.cap_kp_cell, (size_t)std::max(F.n, 1)))) return rc;
     hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.stream, F, m.d_cell_start, m.d_cell_list, m.d_kp_cell,
                        gate, gate_min);
+    return ORBMI_OK;
+}
+
+int pin_grid(Matcher& m, const DevFrame& F) {
+    m.grid_pinned = false;
+    int rc;
+    if ((rc = grid_for(m, F))) return rc;
+    m.grid_pinned = true;
+    m.pin_keys = F.keys;
+    m.pin_ndev = F.n_dev;
+    m.pin_n = F.n;
+    const float g[6] = {F.min_x, F.max_x, F.min_y, F.max_y, F.grid_w_inv, F.grid_h_inv};
+    memcpy(m.pin_geom, g, sizeof(g));
     return ORBMI_OK;
 }
 

@@ -182,6 +182,10 @@ class StereoTracker:
         record 0, outliers discarded -> self.occupied for the local-map search."""
         L = lib()
         cv = self.current_view(tcw)
+        # Frame::AssignFeaturesToGrid once per frame: both last-frame searches and the
+        # local-map search reuse this grid
+        check("orbmi_matcher_assign_features_to_grid",
+              L.orbmi_matcher_assign_features_to_grid(self.matcher._h, C.addressof(cv)))
         mp = self.frame_mappoints(last_view, last_points, None, 0)
         for t, gate in ((th, 0x7FFFFFFF), (2 * th, 20)):  # the first search always runs
             check("orbmi_search_by_projection_last_frame_if", L.orbmi_search_by_projection_last_frame_if(
