@@ -101,3 +101,37 @@ def test_pose_inverse_roundtrip():
     T = synth.pose(7).astype(np.float32)
     Tcw = pose_inverse(T)
     np.testing.assert_allclose(pose_inverse(Tcw), T, atol=1e-6)
+
+
+def test_lost_frames(tmp_path):
+    """A textureless frame loses tracking: it keeps the motion-model pose and is recorded with
+    mlbLost = true (src/Tracking.cc:557-565).  The next frame arrives in LOST state; relocalisation
+    is out of scope, so it has no pose and the trajectory repeats the last relative pose
+    (:566-580).  TUM output skips lost frames.  Runs without LocalBA."""
+    from orb_slam2_with_comment_amd.system import LOST
+    s = sequence_settings(tmp_path)
+    slam = StereoSLAM(s, backend=OracleBackend(s, small_vocabulary()), local_ba=False)
+    for f in range(3):
+        L, R, _ = synth.stereo_pair(synth.KITTI, f)
+        slam.TrackStereo(L, R, 0.1 * f)
+    flat = np.full((synth.KITTI.height, synth.KITTI.width), 128, np.uint8)
+    Tpred = slam.TrackStereo(flat, flat, 0.3)
+    assert slam.state == LOST and slam.lost == [False, False, False, True]
+    assert Tpred is not None and slam.stats[-1]["track"] == "reference_kf"
+    assert slam.TrackStereo(flat, flat, 0.4) is None
+    assert slam.lost[-1] and len(slam.rel_poses) == 5
+    np.testing.assert_array_equal(slam.rel_poses[-1], slam.rel_poses[-2])
+    p = tmp_path / "tum.txt"
+    slam.SaveTrajectoryTUM(str(p))
+    assert len(p.read_text().splitlines()) == 3
+    assert not slam.ba_log
+
+
+def test_not_initialised_until_enough_keypoints(tmp_path):
+    """StereoInitialization needs more than 500 keypoints (src/Tracking.cc:586)."""
+    from orb_slam2_with_comment_amd.system import NOT_INITIALIZED
+    s = sequence_settings(tmp_path)
+    slam = StereoSLAM(s, backend=OracleBackend(s, small_vocabulary()))
+    flat = np.full((synth.KITTI.height, synth.KITTI.width), 90, np.uint8)
+    assert slam.TrackStereo(flat, flat, 0.0) is None
+    assert slam.state == NOT_INITIALIZED and not slam.keyframes and not slam.rel_poses
