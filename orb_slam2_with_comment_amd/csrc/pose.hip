@@ -215,6 +215,32 @@ __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbm
     }
 }
 
+// Edge assembly of PoseOptimization (src/Optimizer.cc:296-375): one edge per keypoint holding a
+// map point, compacted in keypoint order (workgroup scan), plus the frame record.  The map
+// point of keypoint i is mps[match_mp[i]] if match_mp[i] >= 0, else lfp[match_lf[i]] if
+// match_lf[i] >= 0 (orbmi_frame_mappoints); out-of-range indices read as NULL.
+struct PoseGatherArgs {
+    int n;                  // keypoint capacity
+    const int* n_dev;       // device count (optional)
+    const orbmi_keypoint* keys;
+    const float* u_right;   // NULL = monocular
+    const float* tcw_dev;   // initial pose on the device, else tcw
+    float tcw[16];
+    float fx, fy, cx, cy, bf;
+    float inv_sigma2[kMaxLevels];
+    int nlevels;
+    const int* match_lf;
+    const orbmi_lastframe_point* lfp;
+    int n_lf;
+    const int* match_mp;
+    const orbmi_mappoint* mps;
+    int n_mp;
+    orbmi_pose_frame* rec;
+    orbmi_pose_obs* obs;
+    uint8_t* outlier;       // per keypoint, zeroed here
+};
+
+
 // One workgroup per frame.  The Levenberg trial pass is fused with the next iteration's
 // buildSystem: g2o's next iteration starts with computeActiveErrors + buildSystem at the state
 // the accepted trial left (levenberg.cpp:67-85), so the trial pass accumulates J^T W J and b at
@@ -225,11 +251,15 @@ __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbm
 // 2 reduce-scatter written, 3 barrier B passed, 4 (wave 0) totals broadcast, 5 (wave 0) LM
 // update done, 6 (wave 0) next trial pose published; trace[0] = total cycles, [1] = total
 // s_memrealtime ticks, [2] = passes of thread 0's wave.
-template <bool TR>
+// GATHER = the edge assembly (PoseGatherArgs g) runs in the prologue, straight into LDS: the
+// frame record is g.rec, edges are compacted in keypoint order by a workgroup scan, mvbOutlier
+// is written per keypoint (by_index) and zeroed for keypoints without a map point.
+template <bool TR, bool GATHER>
 __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __restrict__ frames,
                                                            const orbmi_pose_obs* __restrict__ obs,
                                                            uint8_t* __restrict__ outlier_out, int by_index,
-                                                           unsigned long long* __restrict__ trace) {
+                                                           unsigned long long* __restrict__ trace,
+                                                           PoseGatherArgs g) {
     __shared__ orbmi_pose_obs sobs[kPoseMaxObs];
     __shared__ float schi[kPoseMaxObs];    // (float) chi2 of the last computeActiveErrors
     __shared__ uint8_t outl[kPoseMaxObs];  // mvbOutlier; the edge's level is the same flag
@@ -246,12 +276,72 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
 #define EV(e)                                                                                    \
     if (TR && (threadIdx.x & 63) == 0 && seq < kPoseTraceSeqs) evp()[e] = __builtin_amdgcn_s_memtime();
     const int tid = threadIdx.x;
-    orbmi_pose_frame& F = frames[blockIdx.x];
-    const int n = F.n_obs;
-    const orbmi_pose_obs* O = obs + F.obs_begin;
+    orbmi_pose_frame& F = GATHER ? *g.rec : frames[blockIdx.x];
+    int n;
+    const orbmi_pose_obs* O = nullptr;
+    float tcw0[12];
+    PoseCam cam;
+    if (GATHER) {  // Optimizer::PoseOptimization's edge loop (src/Optimizer.cc:296-375)
+        __shared__ int gw[kPoseWaves];
+        __shared__ int gbase;
+        const int lane = tid & 63, wid0 = tid >> 6;
+        const int nkp = g.n_dev ? min(*g.n_dev, g.n) : g.n;
+        if (tid == 0) gbase = 0;
+        for (int c0 = 0; c0 < nkp; c0 += kPoseThreads) {
+            const int i = c0 + tid;
+            const float* X = nullptr;
+            if (i < nkp) {
+                const int jm = g.match_mp ? g.match_mp[i] : -1;
+                const int jl = g.match_lf ? g.match_lf[i] : -1;
+                if (jm >= 0 && jm < g.n_mp) X = g.mps[jm].pos;
+                else if (jl >= 0 && jl < g.n_lf) X = g.lfp[jl].pos;
+                g.outlier[i] = 0;
+            }
+            const unsigned long long m = __ballot(X != nullptr);
+            const int before = __popcll(m & ((1ull << lane) - 1));
+            if (lane == 0) gw[wid0] = __popcll(m);
+            __syncthreads();
+            int off = gbase;
+            for (int w = 0; w < wid0; w++) off += gw[w];
+            if (X && off + before < kPoseMaxObs) {
+                const orbmi_keypoint kp = g.keys[i];
+                orbmi_pose_obs o;
+                o.Xw[0] = X[0]; o.Xw[1] = X[1]; o.Xw[2] = X[2];
+                o.u = kp.x;
+                o.v = kp.y;
+                o.ur = g.u_right ? g.u_right[i] : -1.0f;
+                const int oct = min(max(kp.octave, 0), g.nlevels - 1);
+                o.inv_sigma2 = g.inv_sigma2[oct];
+                o.index = i;
+                sobs[off + before] = o;
+                outl[off + before] = 0;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int t = 0;
+                for (int w = 0; w < kPoseWaves; w++) t += gw[w];
+                gbase += t;
+            }
+            __syncthreads();
+        }
+        n = gbase;
+        for (int q = 0; q < 12; q++) tcw0[q] = g.tcw_dev ? g.tcw_dev[q] : g.tcw[q];
+        cam = PoseCam{g.fx, g.fy, g.cx, g.cy, g.bf};
+        if (tid < 16) F.tcw[tid] = tid < 12 ? tcw0[tid] : (tid == 15 ? 1.f : 0.f);
+        if (tid == 0) {
+            F.fx = g.fx; F.fy = g.fy; F.cx = g.cx; F.cy = g.cy; F.bf = g.bf;
+            F.obs_begin = 0;
+            F.n_obs = n;
+        }
+    } else {
+        n = F.n_obs;
+        O = obs + F.obs_begin;
+        for (int q = 0; q < 12; q++) tcw0[q] = F.tcw[q];
+        cam = PoseCam{F.fx, F.fy, F.cx, F.cy, F.bf};
+    }
     // mvbOutlier per observation (orbmi_pose_optimization) or per keypoint (by_index: obs.index)
     auto put_flag = [&](int k, uint8_t v) {
-        if (by_index) outlier_out[O[k].index] = v;
+        if (by_index) outlier_out[GATHER ? sobs[k].index : O[k].index] = v;
         else outlier_out[F.obs_begin + k] = v;
     };
     if (n > kPoseMaxObs) {  // sized for kPoseMaxObs edges per frame (the host path checks first)
@@ -259,21 +349,22 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         return;
     }
     if (n < 3) {  // src/Optimizer.cc:378-379: no optimisation, pose untouched
-        for (int k = tid; k < n; k += kPoseThreads) put_flag(k, 0);
+        if (!GATHER)  // (the gather zeroed every keypoint's flag)
+            for (int k = tid; k < n; k += kPoseThreads) put_flag(k, 0);
         if (tid == 0) { F.inliers = 0; F.iterations = 0; }
         return;
     }
-    for (int k = tid; k < n; k += kPoseThreads) { sobs[k] = O[k]; outl[k] = 0; }
-    const PoseCam cam{F.fx, F.fy, F.cx, F.cy, F.bf};
+    if (!GATHER)
+        for (int k = tid; k < n; k += kPoseThreads) { sobs[k] = O[k]; outl[k] = 0; }
     double T0[8];  // Converter::toSE3Quat(pFrame->mTcw)
     {
         double R[3][3];
         for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++) R[r][c] = F.tcw[4 * r + c];
+            for (int c = 0; c < 3; c++) R[r][c] = tcw0[4 * r + c];
         Q q = q_from_matrix(R);
         q_normalize(q);
         T0[0] = q.x; T0[1] = q.y; T0[2] = q.z; T0[3] = q.w;
-        T0[4] = F.tcw[3]; T0[5] = F.tcw[7]; T0[6] = F.tcw[11]; T0[7] = 0;
+        T0[4] = tcw0[3]; T0[5] = tcw0[7]; T0[6] = tcw0[11]; T0[7] = 0;
     }
     double T[8];
     int nBad = 0, iters = 0, rb = 0;  // rb: alternating reduction buffer
@@ -426,31 +517,6 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
 #undef EV
 }
 
-
-// Edge assembly of PoseOptimization (src/Optimizer.cc:296-375): one edge per keypoint holding a
-// map point, compacted in keypoint order (workgroup scan), plus the frame record.  The map
-// point of keypoint i is mps[match_mp[i]] if match_mp[i] >= 0, else lfp[match_lf[i]] if
-// match_lf[i] >= 0 (orbmi_frame_mappoints); out-of-range indices read as NULL.
-struct PoseGatherArgs {
-    int n;                  // keypoint capacity
-    const int* n_dev;       // device count (optional)
-    const orbmi_keypoint* keys;
-    const float* u_right;   // NULL = monocular
-    const float* tcw_dev;   // initial pose on the device, else tcw
-    float tcw[16];
-    float fx, fy, cx, cy, bf;
-    float inv_sigma2[kMaxLevels];
-    int nlevels;
-    const int* match_lf;
-    const orbmi_lastframe_point* lfp;
-    int n_lf;
-    const int* match_mp;
-    const orbmi_mappoint* mps;
-    int n_mp;
-    orbmi_pose_frame* rec;
-    orbmi_pose_obs* obs;
-    uint8_t* outlier;       // per keypoint, zeroed here
-};
 
 constexpr int kGatherThreads = 1024;
 
@@ -646,8 +712,8 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     if (dev != is_device_ptr(obs) && nobs) return ORBMI_E_ARG;
     if (nobs && dev != is_device_ptr(outlier)) return ORBMI_E_ARG;
     if (dev) {
-        hipLaunchKernelGGL(k_pose_opt<false>, dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0,
-                           nullptr);
+        hipLaunchKernelGGL((k_pose_opt<false, false>), dim3(nframes), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0,
+                           nullptr, PoseGatherArgs{});
         ORBMI_HIP(hipGetLastError());
         return ORBMI_OK;
     }
@@ -670,7 +736,8 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     uint8_t* dFl = h->d_buf + ((fb + 255) & ~(size_t)255) + ((ob + 255) & ~(size_t)255);
     ORBMI_HIP(hipMemcpyAsync(dF, frames, fb, hipMemcpyHostToDevice, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(dO, obs, ob, hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(k_pose_opt<false>, dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl, 0, nullptr);
+    hipLaunchKernelGGL((k_pose_opt<false, false>), dim3(nframes), dim3(kPoseThreads), 0, h->stream, dF, dO, dFl, 0, nullptr,
+                       PoseGatherArgs{});
     ORBMI_HIP(hipGetLastError());
     ORBMI_HIP(hipMemcpyAsync(frames, dF, fb, hipMemcpyDeviceToHost, h->stream));
     if (nobs) ORBMI_HIP(hipMemcpyAsync(outlier, dFl, nobs, hipMemcpyDeviceToHost, h->stream));
@@ -747,12 +814,11 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     a.obs = h->d_obs;
     a.outlier = (uint8_t*)dev_out(outlier, n);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_pose_gather, dim3(1), dim3(kGatherThreads), 0, h->stream, a);
-    ORBMI_HIP(hipGetLastError());
     auto* ev = h->profiling ? next_events(h) : nullptr;
     if (ev) ORBMI_HIP(hipEventRecord(ev->first, h->stream));
-    hipLaunchKernelGGL(k_pose_opt<false>, dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec,
-                       (const orbmi_pose_obs*)h->d_obs, a.outlier, 1, nullptr);
+    // edge assembly fused into the optimiser's prologue (k_pose_gather is the standalone form)
+    hipLaunchKernelGGL((k_pose_opt<false, true>), dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec,
+                       (const orbmi_pose_obs*)nullptr, a.outlier, 1, nullptr, a);
     ORBMI_HIP(hipGetLastError());
     if (ev) ORBMI_HIP(hipEventRecord(ev->second, h->stream));
     if (async) return ORBMI_OK;
@@ -776,7 +842,8 @@ int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_
     ORBMI_HIP(hipMalloc((void**)&d_tr, kPoseTraceWords * sizeof(unsigned long long)));
     hipError_t e = hipMemsetAsync(d_tr, 0, kPoseTraceWords * sizeof(unsigned long long), h->stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_pose_opt<true>, dim3(1), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0, d_tr);
+        hipLaunchKernelGGL((k_pose_opt<true, false>), dim3(1), dim3(kPoseThreads), 0, h->stream, frames, obs, outlier, 0, d_tr,
+                           PoseGatherArgs{});
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(trace, d_tr, kPoseTraceWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream);
