@@ -266,9 +266,10 @@ class StereoTracker:
 
 class LocalMapper:
     """LocalMapping thread: for every queued keyframe, KeyFrame::ComputeBoW (ProcessNewKeyFrame,
-    src/LocalMapping.cc:152-160) when a vocabulary is given, then LocalBundleAdjustment
+    src/LocalMapping.cc:152-160) when a vocabulary is given, and LocalBundleAdjustment
     (src/LocalMapping.cc:89-90), on the GPU on the handles' own streams, concurrently with
-    tracking (src/LocalMapping.cc:47-128)."""
+    tracking (src/LocalMapping.cc:47-128).  The two are data-independent and overlap on the
+    device; the keyframe is done when both are."""
 
     def __init__(self, device=0, vocabulary=None, max_features=8192):
         import torch
@@ -305,8 +306,12 @@ class LocalMapper:
                     self.voc.transform_device(d_desc, n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
                                               b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
                                               b["counts"].data_ptr())
-                    self.voc.synchronize()
+                # LocalBundleAdjustment reads poses, points and observations, never the BowVector,
+                # so the transform (vocabulary stream) and the LocalBA (its own stream) overlap;
+                # both are complete before the next keyframe is taken
                 self.last = self.ba.run(problem)
+                if self.voc is not None and kf_desc is not None:
+                    self.voc.synchronize()
                 self.done += 1
             except Exception as e:  # surfaced by wait()
                 self.error = e
