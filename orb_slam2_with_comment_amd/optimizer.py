@@ -149,16 +149,29 @@ def gather_local_ba(pKF: KeyFrame):
         K[i]["fixed"] = 1 if (i >= len(local_kfs) or k.id == 0) else 0
         K[i]["fx"], K[i]["fy"], K[i]["cx"], K[i]["cy"], K[i]["bf"] = k.cam.fx, k.cam.fy, k.cam.cx, k.cam.cy, k.cam.bf
     P = np.zeros(len(local_mps), BA_PT_DTYPE)
-    edges = []
+    if local_mps:
+        P["pos"] = np.array([mp.pos for mp in local_mps], np.float32)
+        P["id"] = [mp.id for mp in local_mps]
+        P["bad"] = [int(mp.bad) for mp in local_mps]
+    e_pt, e_kf, e_kp = [], [], []
     for pi, mp in enumerate(local_mps):
-        P[pi]["pos"] = mp.pos
-        P[pi]["id"] = mp.id
-        P[pi]["bad"] = int(mp.bad)
         for kf in sorted(mp.observations, key=lambda k: k.id):
-            if kf.bad or id(kf) not in kidx:
+            ki = kidx.get(id(kf))
+            if kf.bad or ki is None:
                 continue
-            j = mp.observations[kf]
-            kp = kf.keys_un[j]
-            edges.append((pi, kidx[id(kf)], kp["x"], kp["y"], kf.u_right[j], kf.inv_level_sigma2[kp["octave"]]))
-    E = np.array(edges, dtype=BA_EDGE_DTYPE) if edges else np.zeros(0, BA_EDGE_DTYPE)
+            e_pt.append(pi)
+            e_kf.append(ki)
+            e_kp.append(mp.observations[kf])
+    E = np.zeros(len(e_pt), BA_EDGE_DTYPE)
+    if e_pt:
+        E["point"], E["kf"] = e_pt, e_kf
+        e_kf, e_kp = np.asarray(e_kf), np.asarray(e_kp)
+        for ki in np.unique(e_kf):   # one gather per keyframe
+            sel = e_kf == ki
+            k, j = kfs[ki], e_kp[sel]
+            kp = k.keys_un[j]
+            E["u"][sel] = kp["x"]
+            E["v"][sel] = kp["y"]
+            E["ur"][sel] = np.asarray(k.u_right, np.float32)[j]
+            E[E.dtype.names[5]][sel] = np.asarray(k.inv_level_sigma2, np.float32)[kp["octave"]]
     return BAProblem(K, P, E), kfs, local_mps

@@ -228,6 +228,37 @@ class MapPoint:
         self.normal = (normal.astype(np.float64) * (1.0 / len(self.observations))).astype(np.float32)
 
 
+def update_normals_and_depths(mps: list):
+    """MapPoint::UpdateNormalAndDepth for many points at once, with the per-point method's exact
+    float32 arithmetic and summation order (observing keyframes in id order)."""
+    pts = [mp for mp in mps if not mp.bad and mp.observations]
+    if not pts:
+        return
+    owner, cen = [], []
+    for j, mp in enumerate(pts):
+        for kf in sorted(mp.observations, key=lambda k: k.id):
+            owner.append(j)
+            cen.append(kf.Ow)
+    owner = np.asarray(owner)
+    pos = np.array([mp.pos for mp in pts], np.float32)
+    v = (pos[owner] - np.asarray(cen, np.float32)).astype(np.float32)
+    v64 = v.astype(np.float64)
+    terms = (v64 * (1.0 / np.sqrt(np.sum(v64 * v64, axis=1)))[:, None]).astype(np.float32)
+    normal = np.zeros((len(pts), 3), np.float32)
+    np.add.at(normal, owner, terms)          # float32, sequential in observation order
+    cnt = np.bincount(owner, minlength=len(pts)).astype(np.float64)
+    normal = (normal.astype(np.float64) * (1.0 / cnt)[:, None]).astype(np.float32)
+    ref_ow = np.array([mp.ref_kf.Ow for mp in pts], np.float32)
+    PC = (pos - ref_ow).astype(np.float32).astype(np.float64)
+    dist = np.sqrt(np.sum(PC * PC, axis=1)).astype(np.float32)
+    for j, mp in enumerate(pts):
+        sf = mp.ref_kf.scale_factors
+        level = int(mp.ref_kf.keys_un[mp.observations[mp.ref_kf]]["octave"])
+        mp.max_distance = np.float32(dist[j] * sf[level])
+        mp.min_distance = np.float32(mp.max_distance / sf[len(sf) - 1])
+        mp.normal = normal[j].copy()
+
+
 # ---- the per-frame state Tracking keeps (include/Frame.h) ----------------------------------
 @dataclasses.dataclass(eq=False)
 class TrackedFrame:
@@ -480,9 +511,9 @@ class StereoSLAM:
             mp.add_observation(kf, i)
             kf.map_points[i] = mp
             mp.desc = cf.desc[i].copy()   # ComputeDistinctiveDescriptors of one observation
-            mp.update_normal_and_depth()
             self.mappoints.append(mp)
             cf.map_points[i] = mp
+        update_normals_and_depths([cf.map_points[i] for i in idx])
 
     def _stereo_initialization(self, cf: TrackedFrame):
         """Tracking::StereoInitialization (src/Tracking.cc:584-636)."""
@@ -573,8 +604,8 @@ class StereoSLAM:
                 continue
             if kf not in mp.observations:
                 mp.add_observation(kf, i)
-                mp.update_normal_and_depth()
                 updated.append(mp)
+        update_normals_and_depths(updated)
         self._distinctive(updated)
         kf.update_connections()
         if self.use_local_ba and len(self.keyframes) > 2:
@@ -605,7 +636,7 @@ class StereoSLAM:
             kfs[i].tcw = np.asarray(res["tcw"][i], np.float32).reshape(4, 4).copy()
         for j, mp in enumerate(mps):
             mp.pos = np.asarray(res["pos"][j], np.float32).copy()
-            mp.update_normal_and_depth()
+        update_normals_and_depths(mps)
 
     # ---- tracking stages --------------------------------------------------------------------
     def _mp_records(self, mps: list, seen: set) -> np.ndarray:
