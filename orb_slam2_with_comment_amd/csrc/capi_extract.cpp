@@ -64,7 +64,9 @@ int orbmi_extract(orbmi_extractor* h, const uint8_t* image, int rows, int cols, 
         ORBMI_HIP(hipMalloc((void**)&e.d_image, bytes));
         e.image_bytes = bytes;
     }
-    ORBMI_HIP(hipMemcpy2DAsync(e.d_image, cols, image, step, cols, rows, hipMemcpyHostToDevice, e.stream));
+    // a contiguous image goes as one copy (a pitched copy from pageable memory runs row by row)
+    if (step == (size_t)cols) ORBMI_HIP(hipMemcpyAsync(e.d_image, image, bytes, hipMemcpyHostToDevice, e.stream));
+    else ORBMI_HIP(hipMemcpy2DAsync(e.d_image, cols, image, step, cols, rows, hipMemcpyHostToDevice, e.stream));
     if ((rc = e.run(e.d_image, 1, cols, bytes, e.d_kps, e.d_desc, e.d_counts, e.out_capacity))) return rc;
     int n = 0;
     ORBMI_HIP(hipMemcpyAsync(&n, e.d_counts, sizeof(int), hipMemcpyDeviceToHost, e.stream));
