@@ -297,7 +297,7 @@ int orbmi_vocabulary_create(int device, const orbmi_vocabulary_desc* d, orbmi_vo
     std::vector<uint8_t> cdesc((size_t)std::max(nch, 1) * 32);
     for (int j = 0; j < nch; j++) memcpy(&cdesc[(size_t)j * 32], d->desc + (size_t)d->children[j] * 32, 32);
     auto fail = [&](int rc) { orbmi_vocabulary_destroy(h); return rc; };
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipSetDevice(device) != hipSuccess || orbmi::stream_create(&h->stream, "VOCAB") != hipSuccess)
         return fail(ORBMI_E_HIP);
     if (hipMalloc(&h->d_vocab, b_desc + b_off + b_ch + b_word + b_w + b_cdesc) != hipSuccess) return fail(ORBMI_E_HIP);
     uint8_t* base = (uint8_t*)h->d_vocab;

@@ -178,7 +178,7 @@ int orbmi_matcher_create(int device, orbmi_matcher** out) {
     orbmi_matcher* h = new (std::nothrow) orbmi_matcher();
     if (!h) return ORBMI_E_ARG;
     h->m.device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->m.stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || orbmi::stream_create(&h->m.stream, "MATCHER") != hipSuccess) {
         delete h;
         return ORBMI_E_HIP;
     }

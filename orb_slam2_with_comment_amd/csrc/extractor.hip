@@ -853,7 +853,7 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
     if (nf < 0 || nl < 1 || nl > kMaxLevels || !(sf > 1.0f)) return ORBMI_E_ARG;
     device = dev; nfeatures = nf; scale_factor = sf; nlevels = nl; ini_th = ini; min_th = mn;
     ORBMI_HIP(hipSetDevice(device));
-    ORBMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    ORBMI_HIP(orbmi::stream_create(&stream, "EXTRACTOR"));
     // ORBextractor::ORBextractor  src/ORBextractor.cc:410-470 (same float/double steps)
     scale.assign(nl, 1.f); sigma2.assign(nl, 1.f); inv_scale.resize(nl); inv_sigma2.resize(nl);
     const double sfd = (double)sf;

@@ -1401,7 +1401,7 @@ int orbmi_ba_create(int device, orbmi_ba** out) {
     orbmi_ba* b = new (std::nothrow) orbmi_ba();
     if (!b) return ORBMI_E_ARG;
     b->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (hipSetDevice(device) != hipSuccess || orbmi::stream_create(&b->stream, "BA") != hipSuccess ||
         hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&b->h_ctl, sizeof(BaCtl)) != hipSuccess ||
         hipHostMalloc((void**)&b->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||

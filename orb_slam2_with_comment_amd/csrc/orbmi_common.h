@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "../../include/orbmi.h"
 
@@ -96,6 +98,21 @@ __device__ inline int block_excl_scan(int v, int* scratch, int* total) {
 __device__ inline int popc256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
     return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Non-blocking stream of one handle.  ORBMI_PRIO_<ROLE>=high|low (ROLE = MATCHER, POSE, BA,
+// VOCAB, EXTRACTOR) selects the device's greatest / least stream priority, else the default.
+inline hipError_t stream_create(hipStream_t* s, const char* role) {
+    char key[64];
+    snprintf(key, sizeof(key), "ORBMI_PRIO_%s", role);
+    const char* v = getenv(key);
+    if (v && (!strcmp(v, "high") || !strcmp(v, "low"))) {
+        int least = 0, greatest = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e != hipSuccess) return e;
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, !strcmp(v, "high") ? greatest : least);
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
 }  // namespace orbmi

@@ -630,7 +630,7 @@ int orbmi_pose_create(int device, orbmi_pose** out) {
     orbmi_pose* h = new (std::nothrow) orbmi_pose();
     if (!h) return ORBMI_E_ARG;
     h->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || orbmi::stream_create(&h->stream, "POSE") != hipSuccess) {
         orbmi_pose_destroy(h);
         return ORBMI_E_HIP;
     }
