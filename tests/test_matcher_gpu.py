@@ -127,3 +127,60 @@ def test_device_resident_inputs(oracle, M):
     m, n = M(0.8).SearchByProjection(DevFrameProxy(), occ, mps, tr, 1.0)
     assert n == n_ref
     np.testing.assert_array_equal(m, m_ref)
+
+
+def test_pinned_grid(oracle, M):
+    """orbmi_matcher_assign_features_to_grid (Frame::AssignFeaturesToGrid once per frame): searches
+    on the pinned frame skip their grid build and still equal the oracle; a search on another
+    frame rebuilds (and unpins), after which the first frame's search rebuilds too; host
+    keypoints cannot be pinned."""
+    import ctypes as C
+    import torch
+    from orb_slam2_with_comment_amd._capi import ORBMI_E_ARG, lib
+
+    def dev_proxy(F):
+        d = (torch.from_numpy(F.keys.view(np.uint8)).cuda(), torch.from_numpy(F.desc).cuda(),
+             torch.from_numpy(F.u_right).cuda())
+
+        class P:
+            keys = F.keys
+            _keep = d
+
+            def view(self):
+                v = F.view()
+                v.keys_un, v.desc, v.u_right = d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()
+                self._v = v
+                return v
+        return P()
+
+    FA, FB = make_frame(3), make_frame(5)
+    PA, PB = dev_proxy(FA), dev_proxy(FB)
+    mps_a, mps_b = local_map((1, 2)), local_map((3, 4))
+    m = M(0.8)
+
+    def ref(F, mps):
+        occ = np.zeros(len(F.keys), np.uint8)
+        return oracle.search_by_projection_local(F, occ, mps, oracle.is_in_frustum(F, mps, 0.5), 1.0, 0.8)
+
+    def run(P, mps):
+        occ = np.zeros(len(P.keys), np.uint8)
+        r, n, _ = m.SearchLocalPoints(P, occ, mps, 1.0)
+        return r, n
+
+    ra, na = ref(FA, mps_a)
+    rb, nb = ref(FB, mps_b)
+    va = PA.view()
+    assert lib().orbmi_matcher_assign_features_to_grid(m._h, C.addressof(va)) == 0
+    for _ in range(2):                        # pinned: no rebuild, same result
+        got, n = run(PA, mps_a)
+        assert n == na and n > 100
+        np.testing.assert_array_equal(got, ra)
+    got, n = run(PB, mps_b)                   # another frame: its own grid
+    assert n == nb
+    np.testing.assert_array_equal(got, rb)
+    got, n = run(PA, mps_a)                   # pin gone: frame A's grid is rebuilt
+    np.testing.assert_array_equal(got, ra)
+    assert lib().orbmi_matcher_release_grid(m._h) == 0
+    vh = FA.view()                            # host keypoints: refused
+    assert lib().orbmi_matcher_assign_features_to_grid(m._h, C.addressof(vh)) == ORBMI_E_ARG
+    m.close()
