@@ -282,28 +282,28 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     float tcw0[12];
     PoseCam cam;
     if (GATHER) {  // Optimizer::PoseOptimization's edge loop (src/Optimizer.cc:296-375)
-        __shared__ int gw[kPoseWaves];
-        __shared__ int gbase;
-        const int lane = tid & 63, wid0 = tid >> 6;
+        __shared__ int gscan[kPoseWaves + 1];
         const int nkp = g.n_dev ? min(*g.n_dev, g.n) : g.n;
-        if (tid == 0) gbase = 0;
-        for (int c0 = 0; c0 < nkp; c0 += kPoseThreads) {
-            const int i = c0 + tid;
-            const float* X = nullptr;
-            if (i < nkp) {
-                const int jm = g.match_mp ? g.match_mp[i] : -1;
-                const int jl = g.match_lf ? g.match_lf[i] : -1;
-                if (jm >= 0 && jm < g.n_mp) X = g.mps[jm].pos;
-                else if (jl >= 0 && jl < g.n_lf) X = g.lfp[jl].pos;
-                g.outlier[i] = 0;
-            }
-            const unsigned long long m = __ballot(X != nullptr);
-            const int before = __popcll(m & ((1ull << lane) - 1));
-            if (lane == 0) gw[wid0] = __popcll(m);
-            __syncthreads();
-            int off = gbase;
-            for (int w = 0; w < wid0; w++) off += gw[w];
-            if (X && off + before < kPoseMaxObs) {
+        // each thread owns a contiguous run of keypoints: count, one block scan, then write in
+        // keypoint order (2 barriers whatever the keypoint count)
+        const int per = (nkp + kPoseThreads - 1) / kPoseThreads;
+        const int i0 = min(tid * per, nkp), i1 = min(i0 + per, nkp);
+        auto point_of = [&](int i) -> const float* {
+            const int jm = g.match_mp ? g.match_mp[i] : -1;
+            const int jl = g.match_lf ? g.match_lf[i] : -1;
+            if (jm >= 0 && jm < g.n_mp) return g.mps[jm].pos;
+            if (jl >= 0 && jl < g.n_lf) return g.lfp[jl].pos;
+            return nullptr;
+        };
+        int cnt = 0;
+        for (int i = i0; i < i1; i++) cnt += point_of(i) != nullptr;
+        int total;
+        int off = block_excl_scan(cnt, gscan, &total);
+        for (int i = i0; i < i1; i++) {
+            const float* X = point_of(i);
+            g.outlier[i] = 0;
+            if (!X) continue;
+            if (off < kPoseMaxObs) {
                 const orbmi_keypoint kp = g.keys[i];
                 orbmi_pose_obs o;
                 o.Xw[0] = X[0]; o.Xw[1] = X[1]; o.Xw[2] = X[2];
@@ -313,18 +313,12 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
                 const int oct = min(max(kp.octave, 0), g.nlevels - 1);
                 o.inv_sigma2 = g.inv_sigma2[oct];
                 o.index = i;
-                sobs[off + before] = o;
-                outl[off + before] = 0;
+                sobs[off] = o;
+                outl[off] = 0;
             }
-            __syncthreads();
-            if (tid == 0) {
-                int t = 0;
-                for (int w = 0; w < kPoseWaves; w++) t += gw[w];
-                gbase += t;
-            }
-            __syncthreads();
+            off++;
         }
-        n = gbase;
+        n = total;
         for (int q = 0; q < 12; q++) tcw0[q] = g.tcw_dev ? g.tcw_dev[q] : g.tcw[q];
         cam = PoseCam{g.fx, g.fy, g.cx, g.cy, g.bf};
         if (tid < 16) F.tcw[tid] = tid < 12 ? tcw0[tid] : (tid == 15 ? 1.f : 0.f);
