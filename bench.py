@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="frames per launch in --mode batch")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -154,7 +156,7 @@ def setup_track(a, rank, local):
 
 def run_track(a, rank, world, local, dist):
     from orb_slam2_with_comment_amd import synth_map as SM
-    from orb_slam2_with_comment_amd.pipeline import LocalMapper, gather_stream_features, match_cross_stream
+    from orb_slam2_with_comment_amd.pipeline import LocalMapper, StreamExchange
     S = setup_track(a, rank, local)
     cam, tr = S["cam"], S["tr"]
     rows, cols = cam.height, cam.width
@@ -169,7 +171,7 @@ def run_track(a, rank, world, local, dist):
     voc = ORBVocabulary(vocab, device=local)
     mapper = LocalMapper(local, vocabulary=voc)
     kf_desc = lambda f: (S["keep"][1][f].data_ptr(), S["n_lf"][f])  # noqa: E731  (the keyframe's descriptors)
-    xmatch = torch.full((tr.cap,), -1, dtype=torch.int32, device=tr.kps.device)
+    xch = StreamExchange(tr, dist, local) if dist is not None else None  # config 4
     ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)        # extraction (E)
     trk = torch.cuda.ExternalStream(tr.track_stream_handle, device=tr.kps.device)  # tracking (T)
 
@@ -177,19 +179,15 @@ def run_track(a, rank, world, local, dist):
         f = 2 + i % F
         tr.track(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols, S["tcws"][f], S["lf_views"][f - 1],
                  S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
-        if dist is not None:  # config 4: exchange left features, match against the other streams
-            cur = torch.cuda.current_stream()
-            cur.wait_stream(trk)  # T already waits for this frame's extraction
-            g_desc, g_kps, g_cnt = gather_stream_features(dist, tr.desc[0], tr.kps[0], tr.counts[:1])
-            trk.wait_stream(cur)
-            match_cross_stream(tr.matcher._h, tr.desc.data_ptr(), tr.cap, tr.counts.data_ptr(), g_desc,
-                               g_cnt.view(-1), rank, xmatch)
-            S["_g"] = (g_desc, g_kps, g_cnt)  # keep alive until the stream has consumed them
+        if xch is not None:  # config 4: exchange left features, match against the other streams
+            xch.exchange()
         if i % KF_EVERY == 0:
             mapper.insert_keyframe(problem, kf_desc(f))
 
     def sync():
         tr.synchronize()
+        if xch is not None:
+            xch.synchronize()
         mapper.wait()
         torch.cuda.synchronize()
 
@@ -276,14 +274,22 @@ def run_track(a, rank, world, local, dist):
     lib.orbmi_pose_set_profiling(tr.pose._h, 0)
     dt = max_over_ranks(dt, dist)
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
+    x_matches = None
+    if xch is not None:
+        xch.synchronize()
+        x_matches = int((xch.xmatch[:int(tr.counts[0])] >= 0).sum())
     value = a.steps * world / dt
     ext_roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic)
     roof = pose_roofline(pose_prof, outcome["recs"], a.traffic)
     out = None
     if rank == 0:
         cpu = None
+        cpu_tp = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline_track(S, problem, a)
+            O = oracle_native()
+            imgs = [x for fr in S["feats"] for x in fr[:2]]
+            cpu_tp = cpu_throughput_extract(O, O.params(a.nfeatures), imgs, min(a.cpu_sample_s, 5))
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
@@ -306,6 +312,7 @@ def run_track(a, rank, world, local, dist):
             "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp, "inliers": outcome["inliers"],
                                   "tracking_ok": outcome["ok"]},
             "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},
+            "cross_stream_matches_last_frame": x_matches,
             "track_only_ms_per_frame_synced": round(track_only_ms, 4),
             "track_only_ms_per_frame_back_to_back": round(track_async_ms, 4),
             "host_enqueue_ms_per_frame": round(enqueue_ms, 4),
@@ -320,8 +327,11 @@ def run_track(a, rank, world, local, dist):
             "extractor_roofline": ext_roof,
             "pipeline_roofline": pipeline_roofline(stage, rows, cols),
             "cpu_baseline": cpu,
+            "cpu_baseline_throughput": cpu_tp,
             "host": host_info(),
         }
+    if xch is not None:
+        xch.close()
     mapper.close()
     tr.close()
     return out
@@ -451,8 +461,18 @@ def max_over_ranks(dt, dist):
     return float(t.item())
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def host_info():
-    return {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count(), "hip": torch.version.hip}
+    return {"cpu": cpu_model(), "nproc": os.cpu_count(), "cpu_share_threads": cpu_threads(), "hip": torch.version.hip}
 
 
 def cpu_baseline_track(S, problem, a):
@@ -460,8 +480,8 @@ def cpu_baseline_track(S, problem, a):
     threading: L/R extraction on two threads (src/Frame.cc:78-81), stereo + TrackWithMotionModel +
     TrackLocalMap serial, LocalBundleAdjustment on a third thread (LocalMapping) every 4th frame."""
     from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle_ctypes as O
     from orb_slam2_with_comment_amd.types import Frame, LFPOINT_DTYPE, MAPPOINT_DTYPE
+    O = oracle_native()
     cam = S["cam"]
     p = O.params(a.nfeatures)
     inv_sigma2 = O.tables(p)["inv_sigma2"]
@@ -499,9 +519,10 @@ def cpu_baseline_track(S, problem, a):
     pool.shutdown()
     lm.shutdown()
     return {"value": round(n / el, 4), "unit": "frames/s", "cores": 3, "kind": "port",
-            "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle extract L||R "
-                      f"(2 threads) + stereo + TrackWithMotionModel + TrackLocalMap (both PoseOptimizations) serial, "
-                      f"{len(futs)} ComputeBoW + LocalBA on a 3rd thread; {el:.1f} s"}
+            "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle (-O3 "
+                      f"-march=native) extract L||R (2 threads) + stereo + TrackWithMotionModel + TrackLocalMap "
+                      f"(both PoseOptimizations) serial, {len(futs)} ComputeBoW + LocalBA on a 3rd thread; {el:.1f} s",
+            "cpu": O.cpu_model()}
 
 
 # --------------------------------------------------------------------------------- extract
@@ -564,7 +585,7 @@ def run_extract(a, rank, world, local, dist):
 
 def cpu_baseline_extract(frames, cam, a):
     from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle_ctypes as O
+    O = oracle_native()
     p = O.params(a.nfeatures)
     pool = ThreadPoolExecutor(2)
     n = 0
@@ -580,7 +601,8 @@ def cpu_baseline_extract(frames, cam, a):
             break
     pool.shutdown()
     return {"value": round(n / el, 4), "unit": "frames/s", "cores": 2, "kind": "port",
-            "sample": f"{n} stereo frames, oracle extract L||R (2 threads) + stereo, {el:.1f} s"}
+            "sample": f"{n} stereo frames, oracle (-O3 -march=native) extract L||R (2 threads) + stereo, {el:.1f} s",
+            "cpu": O.cpu_model()}
 
 
 # --------------------------------------------------------------------------------- lba
@@ -603,9 +625,9 @@ def run_lba(a, rank, world, local, dist):
     dt = max_over_ranks(time.perf_counter() - t0, dist)
     out = None
     if rank == 0:
-        from oracle import oracle_ctypes as O
         cpu = None
         if not a.no_cpu_baseline and world == 1:
+            O = oracle_native()
             n, t0 = 0, time.perf_counter()
             while True:
                 O.local_ba(problem)
@@ -715,15 +737,16 @@ def run_system(a, rank, world, local, dist):
 
 # --------------------------------------------------------------------------------- batch
 def run_batch(a, rank, world, local, dist):
-    """Config 5: EuRoC-shaped 752x480 mono, 8 levels, 5000 features, batch frames per launch."""
+    """Config 5: EuRoC-shaped 752x480 mono, 8 levels, 5000 features, `batch` frames per launch.
+    Frames shard across ranks with no collective: rank r extracts frames
+    [64r, 64r+63] of the sequence (seed 5000 + frame), all distinct."""
     from orb_slam2_with_comment_amd import _capi, synth
     from orb_slam2_with_comment_amd.orb import ORBextractor
     cam = synth.EUROC
     rows, cols = cam.height, cam.width
     nb = a.batch
-    distinct = min(nb, 16)
-    base = [synth.mono(cam, f, seed_base=5000 + 1000 * rank) for f in range(distinct)]
-    imgs = torch.from_numpy(np.stack([base[i % distinct] for i in range(nb)])).cuda()
+    base = [synth.mono(cam, nb * rank + f, seed_base=5000) for f in range(nb)]
+    imgs = torch.from_numpy(np.stack(base)).cuda()
     ex = ORBextractor(5000, 1.2, 8, 20, 7, device=local)
     cap = 5000 + 64
     kps = torch.zeros((nb, cap, 7), dtype=torch.int32, device="cuda")
@@ -743,9 +766,20 @@ def run_batch(a, rank, world, local, dist):
     for i in range(max(a.warmup // 4, 2)):
         step(i)
     sync()
+    # per-stage GPU time of one launch (library event brackets; untimed)
+    lib.orbmi_set_profiling(ex.handle, 0x1FF)
+    reset_profile(ex.handle)
+    for i in range(4):
+        step(i)
+    sync()
+    st_ms, st_n = read_profile(ex.handle)
+    lib.orbmi_set_profiling(ex.handle, 0)
+    stage_ms = {_capi.STAGES[s]: round(st_ms[s] / 4, 5) for s in range(_capi.NUM_STAGES)
+                if st_n[s] and s < len(_capi.STAGES)}
     steps = max(a.steps // 10, 5)
     if dist:
         dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
@@ -760,46 +794,121 @@ def run_batch(a, rank, world, local, dist):
     out = None
     if rank == 0:
         cpu = None
+        cpu_tp = None
         if not a.no_cpu_baseline and world == 1:
-            from oracle import oracle_ctypes as O
+            O = oracle_native()
             p = O.params(5000)
             n, t0 = 0, time.perf_counter()
             while True:
-                O.extract(p, base[n % distinct])
+                O.extract(p, base[n % nb])
                 n += 1
                 if time.perf_counter() - t0 > min(a.cpu_sample_s, 10) and n >= 3:
                     break
             el = time.perf_counter() - t0
             cpu = {"value": round(n / el, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-                   "sample": f"{n} EuRoC-shaped frames on the oracle extractor (1 thread), {el:.1f} s"}
+                   "sample": f"{n} EuRoC-shaped frames on the oracle extractor (-O3 -march=native, 1 thread), "
+                             f"{el:.1f} s", "cpu": O.cpu_model()}
+            cpu_tp = cpu_throughput_extract(O, p, base, min(a.cpu_sample_s, 10))
         gbs = B / (dt / steps) / 1e9
         out = {
             "metric": "frames/s (config 5 batched mono extraction)", "value": round(steps * nb * world / dt, 3),
             "unit": "frames/s", "n_gpus": world, "steps": steps, "warmup": a.warmup,
             "ms_per_step": round(dt / steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic EuRoC-shaped 752x480 mono frames, resident in HBM",
-            "config": {"workload": f"config5: ORBextractor 5000 feat, 8 levels, {nb} frames per launch"},
+            "data": "synthetic EuRoC-shaped 752x480 mono frames (64 distinct per rank), resident in HBM",
+            "config": {"workload": f"config5: ORBextractor 5000 feat, 8 levels, {nb} frames per launch",
+                       "parallelism": f"frames sharded {nb} per GPU x{world}, no collective"},
             "kpts_desc_per_s": round(steps * nb * world * kp / dt, 1), "keypoints_per_frame": round(kp, 1),
+            "stage_ms_per_launch": stage_ms,
             "roofline": {"kernel": "pipeline", "bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": None,
                          "alg_bytes_per_launch": round(B)},
-            "cpu_baseline": cpu, "host": host_info(),
+            "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp, "host": host_info(),
         }
     ex.close()
     return out
 
 
+def oracle_native():
+    """The oracle built -O3 -march=native on this host (bench's cpu_baseline legs only)."""
+    from oracle import oracle_ctypes as O
+    if O._lib is None:
+        O.use_native()
+    return O
+
+
+def cpu_threads():
+    """Host threads for throughput baselines: the job's CPU share (OMP_NUM_THREADS, 16 on the
+    GPU box) bounded by the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+
+def cpu_throughput_extract(O, p, frames, sample_s):
+    """Throughput mode: one oracle extractor per host thread, each on its own
+    frames, for kpts+desc/s."""
+    from concurrent.futures import ThreadPoolExecutor
+    T = cpu_threads()
+    stop = time.perf_counter() + sample_s
+
+    def worker(t):
+        n = kp = 0
+        while True:
+            k, _ = O.extract(p, frames[(t + n * T) % len(frames)])
+            n += 1
+            kp += len(k)
+            if time.perf_counter() > stop:
+                return n, kp
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as pool:
+        res = list(pool.map(worker, range(T)))
+    el = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    kp = sum(r[1] for r in res)
+    return {"value": round(kp / el, 1), "unit": "kpts+desc/s", "frames_per_s": round(n / el, 3), "cores": T,
+            "kind": "port", "sample": f"{n} frames on {T} oracle extractors (one per thread, -O3 -march=native), "
+                                      f"{el:.1f} s", "cpu": O.cpu_model()}
+
+
+def spawn_ranks(a):
+    """`--gpus N` (N > 1) outside torchrun: run the same command as N ranks of one torchrun job
+    (one process per GPU, RCCL over xGMI) as a CHILD process started before this process makes
+    any GPU call, and return its exit code (rank 0 prints the JSON line)."""
+    import socket
+    import subprocess
+    n_dev = torch.cuda.device_count()  # does not initialise the GPU
+    if a.gpus > n_dev and a.dist_backend == "nccl":
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but only {n_dev} GPU(s) visible")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+    if a.dist_backend != "nccl":  # rehearsal: ranks may share a GPU
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.dist_backend)
     run = {"track": run_track, "extract": run_extract, "lba": run_lba, "batch": run_batch,
            "system": run_system}[a.mode]
     out = run(a, rank, world, local, dist)

@@ -383,7 +383,21 @@ struct Optimizer {
 
 }  // namespace
 
+static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, double* edge_chi2);
+
 extern "C" int orc_local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop) {
+    return local_ba(P, R, stop, nullptr);
+}
+
+/* Same, and the chi2 every erase decision of src/Optimizer.cc:758-773 reads (per edge; -1 for
+ * edges of bad points): lets the parity tests show that an erase flag that differs from the
+ * GPU's sits on its threshold within the pose tolerance. */
+extern "C" int orc_local_ba_edge_chi2(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop,
+                                      double* edge_chi2) {
+    return local_ba(P, R, stop, edge_chi2);
+}
+
+static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, double* edge_chi2) {
     Graph g;
     for (int k = 0; k < P->nkf; k++) {
         g.T.push_back(se3_from_tcw(P->kfs[k].tcw));
@@ -434,8 +448,10 @@ extern "C" int orc_local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const
     }
     for (int i = 0; i < P->nedge; i++) {
         const Edge& e = g.E[i];
+        if (edge_chi2) edge_chi2[i] = -1.0;
         if (P->pts[e.pt].bad) continue;
         const double th = e.stereo ? 7.815 : 5.991;
+        if (edge_chi2) edge_chi2[i] = depth_positive(g, e) ? chi2(e) : -2.0;
         if (chi2(e) > th || !depth_positive(g, e)) R->erase[i] = 1;
     }
     for (int k = 0; k < P->nkf; k++) se3_to_tcw(g.T[k], R->tcw + 16 * k);

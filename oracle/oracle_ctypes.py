@@ -52,6 +52,32 @@ def lib():
     return _lib
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def use_native(jobs: int = 8) -> str:
+    """bench.py's cpu_baseline leg only: build the oracle with -O3 -march=native on THIS host
+    (oracle/Makefile `native`) and load it instead of the portable build.  Must
+    be called before anything else loads the oracle.  Returns the library path."""
+    global _lib
+    import hashlib
+    if _lib is not None:
+        raise RuntimeError("oracle already loaded; call use_native() first")
+    tag = hashlib.sha1(cpu_model().encode()).hexdigest()[:10]
+    subprocess.run(["make", "-s", "-C", HERE, f"-j{jobs}", "native", f"TAG={tag}"], check=True)
+    path = os.path.join(HERE, "build", f"native-{tag}", "liborb_oracle.so")
+    _lib = C.CDLL(path)
+    return path
+
+
 def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> Params:
     return Params(nfeatures, scale_factor, nlevels, ini_th, min_th)
 
@@ -224,18 +250,23 @@ def search_by_bow(kf, kf_mp_ok, kf_fv, f, f_fv, nnratio=0.7, check_ori=True):
     return out[:len(f.keys)], n.value
 
 
-def local_ba(problem, stop=False):
-    """Optimizer::LocalBundleAdjustment restatement -> dict(tcw, pos, erase, iterations, chi2, aborted)."""
+def local_ba(problem, stop=False, edge_chi2=False):
+    """Optimizer::LocalBundleAdjustment restatement -> dict(tcw, pos, erase, iterations, chi2, aborted)
+    (+ "edge_chi2": the chi2 each erase decision read, -1 bad point, -2 depth not positive)."""
     L = lib()
-    L.orc_local_ba.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.orc_local_ba_edge_chi2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     r, tcw, pos, erase = problem.result_buffers()
     v = problem.view()
     flag = C.c_int(1 if stop else 0)
-    rc = L.orc_local_ba(C.addressof(v), C.addressof(r), C.addressof(flag))
-    assert rc == 0, rc
     n = len(problem.kfs), len(problem.pts), len(problem.edges)
-    return {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
-            "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+    ec = np.zeros(max(n[2], 1), np.float64)
+    rc = L.orc_local_ba_edge_chi2(C.addressof(v), C.addressof(r), C.addressof(flag), ec.ctypes.data)
+    assert rc == 0, rc
+    out = {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
+           "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+    if edge_chi2:
+        out["edge_chi2"] = ec[:n[2]]
+    return out
 
 
 def pose_optimization(frames, obs):

@@ -53,6 +53,7 @@ int orbmi_extract(orbmi_extractor* h, const uint8_t* image, int rows, int cols, 
     if (rows <= 0 || cols <= 0) return ORBMI_OK;  // src/ORBextractor.cc:1046-1047
     if (!image || step < (size_t)cols || capacity < 0 || (capacity > 0 && (!kps || !desc))) return ORBMI_E_ARG;
     Extractor& e = h->ex;
+    ORBMI_HIP(hipSetDevice(e.device));  // buffers grown below belong to the handle's device
     int rc;
     if ((rc = e.set_geometry(rows, cols))) return rc;
     const int cap = std::max(capacity, e.nfeatures + 64);
@@ -89,6 +90,7 @@ int orbmi_extract_batch_device(orbmi_extractor* h, const uint8_t* d_images, int 
         !d_counts || capacity <= 0)
         return ORBMI_E_ARG;
     Extractor& e = h->ex;
+    ORBMI_HIP(hipSetDevice(e.device));
     int rc;
     if ((rc = e.set_geometry(rows, cols))) return rc;
     if ((rc = e.reserve(batch, 0))) return rc;

@@ -112,6 +112,7 @@ class StereoTracker:
             self._ev_extracted = [torch.cuda.Event() for _ in range(nslots)]
             self._ev_tracked = [torch.cuda.Event() for _ in range(nslots)]
             self._pending = [False] * nslots
+            self._holds = [[] for _ in range(nslots)]  # other consumers' events per slot (hold_slot)
         self.occupied = torch.zeros(cap, dtype=torch.uint8, device=dev)   # after the motion-model stage
         self.no_points = torch.zeros(cap, dtype=torch.uint8, device=dev)  # fill(mvpMapPoints, NULL)
         self.match_lf = torch.full((cap,), -1, dtype=torch.int32, device=dev)
@@ -159,6 +160,8 @@ class StereoTracker:
             _vp(sl["desc"].data_ptr()), _vp(sl["counts"].data_ptr()), self.cap))
         check("orbmi_compute_stereo_matches_batch_device", L.orbmi_compute_stereo_matches_batch_device(
             self.extractor.handle, self.cam.bf, self.cam.fx, _vp(sl["u_right"].data_ptr()), _vp(sl["depth"].data_ptr())))
+        # new keypoints behind the slot's pointers: a grid pinned on an earlier frame is stale
+        check("orbmi_matcher_release_grid", L.orbmi_matcher_release_grid(self.matcher._h))
 
     def search_last_frame(self, tcw, last_view, last_points, th=7.0):
         """ORBmatcher(0.9, true).SearchByProjection(mCurrentFrame, mLastFrame, th, !stereo)
@@ -231,6 +234,9 @@ class StereoTracker:
         self._next ^= 1
         if self._pending[s]:  # the slot's previous frame must be tracked before it is overwritten
             self._E.wait_event(self._ev_tracked[s])
+        for ev in self._holds[s]:  # ... and read by every other consumer (hold_slot)
+            self._E.wait_event(ev)
+        self._holds[s].clear()
         self.extract_stereo(d_left_right, rows, cols, slot=s)
         self._ev_extracted[s].record(self._E)
         self._T.wait_event(self._ev_extracted[s])
@@ -239,6 +245,23 @@ class StereoTracker:
         self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
         self._ev_tracked[s].record(self._T)
         self._pending[s] = True
+
+    def hold_slot(self, stream):
+        """Register another reader of the last tracked frame's slot (e.g. the config-4 exchange
+        on its own stream): the extraction that next overwrites the slot waits for the work
+        enqueued on `stream` so far."""
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        if self.pipelined:
+            self._holds[self.slot].append(ev)
+        else:  # one stream: the next extraction is on E
+            torch.cuda.ExternalStream(self.stream_handle, device=self.kps.device).wait_event(ev)
+
+    def extracted_event(self):
+        """Event recorded on the extraction stream after the last tracked frame's extraction +
+        stereo (pipelined trackers only)."""
+        return self._ev_extracted[self.slot]
 
     def results(self):
         """Synchronise and read the frame's tracking outcome: ok follows the reference's return
@@ -358,3 +381,46 @@ def match_cross_stream(matcher_handle, q_desc, nq, nq_device, g_desc, seg_counts
         matcher_handle, _vp(q_desc), int(nq), _vp(nq_device) if nq_device else None, _vp(g_desc.data_ptr()), world, cap,
         _vp(seg_counts.data_ptr()), int(skip_seg), int(th), float(ratio), _vp(out.data_ptr()),
         C.byref(nmatches) if nmatches is not None else None))
+
+
+class StreamExchange:
+    """Config 4: after each tracked frame, all-gather the stream's left
+    descriptors + keypoints over the process group and match them against the other streams'
+    (orbmi_match_descriptors_segments; build-defined cross-stream matching, no reference
+    counterpart).  The exchange runs on its own stream X (a second matcher handle's): it waits
+    only for the frame's extraction event, so tracking on T never waits for the collective, and
+    the frame's slot is held until X has read it (StereoTracker.hold_slot), so the extraction
+    two frames later cannot overwrite features the gather or the match still reads."""
+
+    def __init__(self, tracker, dist, device=0):
+        import torch
+        from .matcher import ORBmatcher
+        self.tr, self.dist = tracker, dist
+        self.matcher = ORBmatcher(device=device)
+        x = _vp()
+        check("orbmi_matcher_get_stream", lib().orbmi_matcher_get_stream(self.matcher._h, C.byref(x)))
+        self.X = torch.cuda.ExternalStream(x.value, device=torch.device("cuda", device))
+        self.xmatch = torch.full((tracker.cap,), -1, dtype=torch.int32, device=torch.device("cuda", device))
+        self._keep = None
+
+    def exchange(self):
+        """Enqueue the exchange of the frame tracker.track() enqueued last."""
+        import torch
+        tr = self.tr
+        if tr.pipelined:
+            self.X.wait_event(tr.extracted_event())
+        else:
+            self.X.wait_stream(torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device))
+        with torch.cuda.stream(self.X):
+            g_desc, g_kps, g_cnt = gather_stream_features(self.dist, tr.desc[0], tr.kps[0], tr.counts[:1])
+        match_cross_stream(self.matcher._h, tr.desc.data_ptr(), tr.cap, tr.counts.data_ptr(), g_desc,
+                           g_cnt.view(-1), self.dist.get_rank(), self.xmatch)
+        tr.hold_slot(self.X)
+        self._keep = (g_desc, g_kps, g_cnt)  # alive until X has consumed them (next exchange)
+        return self._keep
+
+    def synchronize(self):
+        self.X.synchronize()
+
+    def close(self):
+        self.matcher.close()

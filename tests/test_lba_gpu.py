@@ -9,6 +9,11 @@ from orb_slam2_with_comment_amd import synth_map as SM
 
 pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-4
+# The erase list (src/Optimizer.cc:758-773) is index output and is held exact, except for an
+# edge whose chi2 sits on its threshold (5.991 mono / 7.815 stereo) closer than the rounding
+# differences of the two fp64 reduction orders can resolve: the oracle's chi2 for every
+# differing flag must lie within this relative distance of the threshold.
+ERASE_CHI2_RTOL = 1e-6
 
 
 @pytest.fixture(scope="module")
@@ -17,15 +22,19 @@ def BA():
     return LocalBA()
 
 
-def _compare(r, ref, pt_tol=1e-3):
+def _compare(r, ref, prob, pt_tol=1e-3):
     assert r["aborted"] == ref["aborted"]
     assert r["iterations"] == ref["iterations"], (r["iterations"], ref["iterations"])
     dT = np.abs(r["tcw"] - ref["tcw"]).max()
     assert dT <= POSE_TOL, dT
     dP = np.abs(r["pos"] - ref["pos"]) / np.maximum(1.0, np.abs(ref["pos"]))
     assert dP.max() <= pt_tol, dP.max()
-    mism = (r["erase"] != ref["erase"]).sum()
-    assert mism <= max(2, int(0.002 * len(r["erase"]))), mism
+    mism = np.nonzero(r["erase"] != ref["erase"])[0]
+    if len(mism):
+        th = np.where(prob.edges["ur"][mism] < 0, 5.991, 7.815)
+        margin = np.abs(ref["edge_chi2"][mism] - th) / th
+        print(f"erase flags differing: {len(mism)} of {len(r['erase'])}, chi2 margins {margin.tolist()}")
+        assert (margin <= ERASE_CHI2_RTOL).all(), (mism.tolist(), margin.tolist())
     np.testing.assert_allclose(r["chi2"], ref["chi2"], rtol=1e-6)
 
 
@@ -33,19 +42,19 @@ def _compare(r, ref, pt_tol=1e-3):
                                                  (11, 21, 3, 1500), (5, 27, 2, 2000)])
 def test_lba_parity(oracle, BA, seed, free, fixed, npts):
     prob, _ = SM.local_ba_problem(seed=seed, n_free=free, n_fixed=fixed, n_points=npts)
-    ref = oracle.local_ba(prob)
-    _compare(BA.run(prob), ref)
+    ref = oracle.local_ba(prob, edge_chi2=True)
+    _compare(BA.run(prob), ref, prob)
 
 
 def test_lba_mono_only(oracle, BA):
     prob, _ = SM.local_ba_problem(seed=11, n_free=8, n_fixed=2, n_points=600, stereo_frac=0.0)
-    _compare(BA.run(prob), oracle.local_ba(prob))
+    _compare(BA.run(prob), oracle.local_ba(prob, edge_chi2=True), prob)
 
 
 def test_lba_bad_points(oracle, BA):
     prob, _ = SM.local_ba_problem(seed=12, n_free=8, n_fixed=2, n_points=600)
     prob.pts["bad"][::17] = 1
-    _compare(BA.run(prob), oracle.local_ba(prob))
+    _compare(BA.run(prob), oracle.local_ba(prob, edge_chi2=True), prob)
 
 
 def test_lba_stop_before_start(oracle, BA):
@@ -81,4 +90,4 @@ def test_lba_from_map_model(oracle, BA):
         kf.covisible = [o for o in free if o is not kf]
     problem, order, _ = gather_local_ba(free[-1])
     assert len(problem.edges) > 0 and problem.kfs["fixed"].sum() >= 1
-    _compare(BA.run(problem), oracle.local_ba(problem))
+    _compare(BA.run(problem), oracle.local_ba(problem, edge_chi2=True), problem)
