@@ -1,11 +1,12 @@
 #!/bin/bash
 # One GPU session of round evidence: parity tests, rocprofv3 kernel stats of the default bench,
 # two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, then the bench lines of every mode.
-# Usage (via gpurun): bash tools/gpu_round.sh TAG      -> gpurun_out/TAG/, profiles/TAG/
+# Usage (via gpurun): bash tools/gpu_round.sh TAG      -> gpurun_out/TAG/ (summaries under gpurun_out/TAG/profiles/,
+# which gpurun merges back; copy them into profiles/TAG/ here)
 # Stops at the first step that crashes or times out (exit status other than 0/1).
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
-P=profiles/$TAG
+P=$OUT/profiles
 mkdir -p $OUT $P
 export TMPDIR=/tmp
 run() {  # name timeout cmd...
@@ -23,7 +24,7 @@ cp $OUT/pytest_gpu.log $P/pytest_gpu.log
 run prof_stats 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_stats -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline
 run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline --cpu-sample-s 1
 run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline --cpu-sample-s 1
-python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic_latest.json && cp $OUT/traffic.json $P/traffic.json
+python tools/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json && cp $OUT/traffic.json $P/traffic.json
 find $OUT/prof_stats -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats.csv \;
 cp $OUT/prof_stats.log $P/prof_stats_bench.log 2>/dev/null
 run bench 400 python bench.py
