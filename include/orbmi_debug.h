@@ -23,8 +23,8 @@ int orbmi_debug_octree_level(orbmi_extractor* h, int item, int level, int* xyr, 
  * with an event trace in shader-clock cycles (s_memtime), trace = 16 + 64 * 8 * 8 words:
  * [0] total cycles, [1] total s_memrealtime ticks (100 MHz), [2] edge passes of wave 0; per
  * edge pass s < 64 and wave w, trace[16 + (s * 8 + w) * 8 + e] stamps e = 0 pass start, 1 pass
- * end, 2 reduce-scatter written, 3 barrier passed, 4 (wave 0) totals broadcast, 5 (wave 0)
- * Levenberg update done, 6 (wave 0) next trial pose published; unset stamps are 0. */
+ * end, 2 chi2 barrier passed, 3 Levenberg decision taken, 4 (accepted trial) system reduced,
+ * 5 (wave 0) trial chain published, 6 candidates barrier passed; unset stamps are 0. */
 int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_pose_obs* obs, uint8_t* outlier,
                            unsigned long long* trace);
 

@@ -15,7 +15,9 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB = os.path.join(PKG, "liborbmi.so")
+# ORBMI_LIB / ORBMI_CFLAGS: an alternative library path and extra -D flags, for A/B builds of a
+# kernel variant (tools/gpu_iter.sh); the product build uses neither
+LIB = os.environ.get("ORBMI_LIB") or os.path.join(PKG, "liborbmi.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ORBMI_ARCH", "gfx950")
 
@@ -41,7 +43,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(LIB, deps):
         return LIB
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, *sources()]
+    cmd = [HIPCC, *FLAGS, *os.environ.get("ORBMI_CFLAGS", "").split(), "-o", tmp, *sources()]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

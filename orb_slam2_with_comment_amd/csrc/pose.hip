@@ -29,11 +29,15 @@
 
 namespace orbmi {
 
-constexpr int kPoseThreads = 512;  // 8 waves, 2 per SIMD: the per-edge passes hide fp64 latency
+#ifndef ORBMI_POSE_THREADS
+#define ORBMI_POSE_THREADS 512
+#endif
+constexpr int kPoseThreads = ORBMI_POSE_THREADS;  // 8 waves, 2 per SIMD: the per-edge passes hide fp64 latency
 constexpr int kPoseWaves = kPoseThreads / 64;
+constexpr int kPoseTraceWaves = 8;  // trace layout (orbmi_debug_pose_trace), whatever kPoseWaves
 constexpr int kPoseMaxObs = 4096;
 constexpr int kPoseTraceSeqs = 64;  // passes recorded by orbmi_debug_pose_trace
-constexpr int kPoseTraceWords = 16 + kPoseTraceSeqs * kPoseWaves * 8;
+constexpr int kPoseTraceWords = 16 + kPoseTraceSeqs * kPoseTraceWaves * 8;
 
 struct PoseCam { double fx, fy, cx, cy, bf; };
 
@@ -71,10 +75,10 @@ __device__ inline double pose_chi2(const orbmi_pose_obs& o, const double e[3]) {
 
 // fixed-order workgroup sum of the 28 normal-equation terms into wave 0: every wave
 // reduce-scatters its lanes' terms (DPP / permlane swaps), writes one LDS slot per (wave, value);
-// after the barrier wave 0's lane q sums value q over the waves in wave order and readlane
-// broadcasts the totals to all of wave 0's lanes.  The other waves' acc is left unspecified.
-// ev (trace builds only): this wave's event slots of the current pass, see k_pose_opt
-__device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], unsigned long long* ev = nullptr) {
+// after the barrier wave 0's lane q sums value q over the waves in wave order, stores it in
+// stot[q] and every lane of wave 0 reads the 28 totals back (broadcast LDS reads).  The other
+// waves' acc is left unspecified; stot keeps the system for a later re-solve.
+__device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], double* stot) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double v[32];
 #pragma unroll
@@ -82,16 +86,17 @@ __device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], un
     v[28] = v[29] = v[30] = v[31] = 0;
     const double s = wave_reduce_scatter32(v);
     if (!(lane & 1)) red[wid][lane >> 1] = s;
-    if (ev && lane == 0) ev[2] = __builtin_amdgcn_s_memtime();
     __syncthreads();
-    if (ev && lane == 0) ev[3] = __builtin_amdgcn_s_memtime();
     if (wid == 0) {
         double t = 0;
 #pragma unroll
         for (int w = 0; w < kPoseWaves; w++) t += red[w][lane & 31];
+        if (lane < 28) stot[lane] = t;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int q = 0; q < 28; q++) acc[q] = readlane_d(t, q);
-        if (ev && lane == 0) ev[4] = __builtin_amdgcn_s_memtime();
+        for (int q = 0; q < 28; q++) acc[q] = stot[q];
     }
 }
 
@@ -215,6 +220,63 @@ __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbm
     }
 }
 
+// A trial of the Levenberg chain: the pose oplus(x) * T, scale = x^T (lambda x + b) and whether
+// the damped solve succeeded (else T itself, x = 0: tempChi is then DBL_MAX).
+constexpr int kPoseCands = 16;
+struct PoseCand { double T[8]; double scale; double ok; };
+
+// Wave 0, lane-parallel: lane j < kPoseCands solves (H + lambda_j I) x = b for the damping of the
+// trial after j rejections (lambda *= ni; ni *= 2 per rejection, levenberg.cpp:143-146 -- the
+// same multiplications in the same order) and publishes the trial pose in cand[j].
+__device__ inline void pose_candidates(const double (&hb)[28], double lambda, double ni, const double* T,
+                                       PoseCand* cand) {
+    const int lane = threadIdx.x & 63;
+    double l = lambda, nn = ni;
+#pragma unroll
+    for (int m = 0; m < kPoseCands - 1; m++)
+        if (m < lane) { l *= nn; nn *= 2; }
+    double xv[6], Tt[8];
+    const bool ok = pose_solve6(hb, hb + 21, l, xv);
+    if (ok) se3_oplus(xv, T, Tt);
+    else {
+#pragma unroll
+        for (int q = 0; q < 8; q++) Tt[q] = T[q];
+#pragma unroll
+        for (int q = 0; q < 6; q++) xv[q] = 0;
+    }
+    double scale = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) scale += xv[j] * (l * xv[j] + hb[21 + j]);
+    if (lane < kPoseCands) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) cand[lane].T[q] = Tt[q];
+        cand[lane].scale = scale;
+        cand[lane].ok = ok ? 1.0 : 0.0;
+    }
+}
+
+// computeActiveErrors + activeRobustChi2 only (a trial's evaluation): this thread's robust chi2
+// sum; schi as pose_pass.  The Jacobians are formed only if the trial is accepted.
+__device__ inline double pose_chi_pass(const double* T, const PoseCam& cam, const orbmi_pose_obs* sobs,
+                                       const uint8_t* outl, float* schi, int n, bool robust) {
+    double chi = 0;
+    for (int k = threadIdx.x; k < n; k += kPoseThreads) {
+        if (outl[k]) continue;
+        const orbmi_pose_obs o = sobs[k];
+        double p[3], invz, e[3];
+        pose_error(T, cam, o, p, invz, e);
+        const double c2 = pose_chi2(o, e);
+        schi[k] = (float)c2;
+        double rho0 = c2;
+        if (robust) {
+            const double d = pose_delta(o), dsqr = d * d;
+            if (c2 > dsqr) rho0 = 2 * (c2 * fast_rsqrt(c2)) * d - dsqr;
+        }
+        chi += rho0;
+    }
+    return chi;
+}
+
 // Edge assembly of PoseOptimization (src/Optimizer.cc:296-375): one edge per keypoint holding a
 // map point, compacted in keypoint order (workgroup scan), plus the frame record.  The map
 // point of keypoint i is mps[match_mp[i]] if match_mp[i] >= 0, else lfp[match_lf[i]] if
@@ -247,10 +309,10 @@ struct PoseGatherArgs {
 // the trial pose too, and an accepted trial hands them on (a rejected one keeps H, b: g2o
 // re-solves the same system with a larger lambda).  One edge pass + one reduction per trial.
 // TR = event trace (orbmi_debug_pose_trace): lane 0 of every wave stamps s_memtime per edge
-// pass (seq) into trace[16 + (seq * kPoseWaves + wave) * 8 + e]: e = 0 pass start, 1 pass end,
-// 2 reduce-scatter written, 3 barrier B passed, 4 (wave 0) totals broadcast, 5 (wave 0) LM
-// update done, 6 (wave 0) next trial pose published; trace[0] = total cycles, [1] = total
-// s_memrealtime ticks, [2] = passes of thread 0's wave.
+// pass (seq) into trace[16 + (seq * kPoseTraceWaves + wave) * 8 + e]: e = 0 pass start, 1 pass end,
+// 2 chi2 barrier (B1) passed, 3 Levenberg decision taken, 4 (accepted trial) system reduced,
+// 5 (wave 0) trial chain published, 6 candidates barrier (B3) passed; trace[0] = total cycles,
+// [1] = total s_memrealtime ticks, [2] = passes of thread 0's wave.
 // GATHER = the edge assembly (PoseGatherArgs g) runs in the prologue, straight into LDS: the
 // frame record is g.rec, edges are compacted in keypoint order by a workgroup scan, mvbOutlier
 // is written per keypoint (by_index) and zeroed for keypoints without a map point.
@@ -265,13 +327,15 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     __shared__ uint8_t outl[kPoseMaxObs];  // mvbOutlier; the edge's level is the same flag
     __shared__ double red[2][kPoseWaves][32];
     __shared__ double red1[2][kPoseWaves];
-    __shared__ double sTt[8];  // wave 0's trial (or final) pose, read after the next barrier
-    __shared__ int sCmd;
+    __shared__ PoseCand scand[kPoseCands];  // wave 0's trial chain
+    __shared__ double stot[32];              // wave 0's reduced system (H upper, b, chi2)
+    __shared__ double chiw[2][kPoseWaves];   // per-wave chi2 of a trial pass
+    int cb = 0;                              // chiw buffer
     unsigned long long tstart = 0, rstart = 0;
     if (TR && threadIdx.x == 0) { tstart = __builtin_amdgcn_s_memtime(); rstart = __builtin_amdgcn_s_memrealtime(); }
     int seq = 0;  // passes run by this wave (trace builds)
     auto evp = [&]() -> unsigned long long* {
-        return (TR && seq < kPoseTraceSeqs) ? trace + 16 + (seq * kPoseWaves + (threadIdx.x >> 6)) * 8 : nullptr;
+        return (TR && seq < kPoseTraceSeqs) ? trace + 16 + (seq * kPoseTraceWaves + (threadIdx.x >> 6)) * 8 : nullptr;
     };
 #define EV(e)                                                                                    \
     if (TR && (threadIdx.x & 63) == 0 && seq < kPoseTraceSeqs) evp()[e] = __builtin_amdgcn_s_memtime();
@@ -373,102 +437,103 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         nact = pose_reduce1(nact, red1[rb]);
         rb ^= 1;
         if (nact > 0) {
-            // ---- optimize(10) on the level-0 edges.  Every wave runs the edge passes; wave 0
-            // alone runs the Levenberg control, the damped solve and the exponential map, and
-            // hands each trial pose to the others through LDS (sCmd = 1: evaluate sTt; 0: done,
-            // sTt = the final estimate).
+            // ---- optimize(10) on the level-0 edges.  Every wave runs the edge passes and the
+            // Levenberg decisions (replicated: the same instructions on the same LDS values, so
+            // every wave takes the same branch).  Wave 0 holds the reduced system and publishes,
+            // in scand, the trial poses of the whole rejected-trial chain that follows it (lane j
+            // solves for the lambda after j rejections): a rejected trial needs only the chi2
+            // sum of its pass, and only an accepted trial pays for the 28-value reduction and a
+            // fresh solve.
             double acc[28];
-            EV(0);
-            pose_pass(T, cam, sobs, outl, schi, n, robust, acc);  // computeActiveErrors + buildSystem
-            EV(1);
-            pose_reduce28_w0(acc, red[rb], evp());
-            rb ^= 1;
-            if (wid == 0) {
-                double currentChi = acc[27];
-                // computeLambdaInit, tau = 1e-5
-                double lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
-                                            fmax(fabs(acc[18]), fabs(acc[20])));
-                double ni = 2;
-                int nbadIt = 0;
-                for (int i = 0; i < 10; i++) {
-                    const double iniChi = currentChi;
-                    double rho = 0;
-                    int qmax = 0;
-                    do {
-                        double xv[6], Tt[8];
-                        const bool ok2 = pose_solve6(acc, acc + 21, lambda, xv);
-                        if (ok2) se3_oplus(xv, T, Tt);
-                        else {
+            double lambda = 0, ni = 2;  // meaningful in wave 0 only
+            double currentChi = 0, iniChi = 0;
+            int cj = 0, qmax = 0, nbadIt = 0, i = 0;
+            bool first = true;  // the pass at T: computeActiveErrors + buildSystem of iteration 0
+            for (;;) {
+                bool accept = true, regen = false;
+                if (!first) {
+                    // trial cj of the chain: the pose of oplus(x(lambda_cj)), evaluated by all waves
+                    double Tt[8];
 #pragma unroll
-                            for (int q = 0; q < 8; q++) Tt[q] = T[q];
-#pragma unroll
-                            for (int q = 0; q < 6; q++) xv[q] = 0;
-                        }
-                        if (tid == 0) {
-#pragma unroll
-                            for (int q = 0; q < 8; q++) sTt[q] = Tt[q];
-                            sCmd = 1;
-                        }
-                        EV(6);
-                        seq++;
-                        __syncthreads();  // A: trial published
-                        EV(0);
-                        double tacc2[28];
-                        pose_pass(Tt, cam, sobs, outl, schi, n, robust, tacc2);
-                        EV(1);
-                        pose_reduce28_w0(tacc2, red[rb], evp());
-                        rb ^= 1;
-                        const double tempChi = ok2 ? tacc2[27] : DBL_MAX;
-                        double scale = 0;
-#pragma unroll
-                        for (int j = 0; j < 6; j++) scale += xv[j] * (lambda * xv[j] + acc[21 + j]);
-                        rho = (currentChi - tempChi) * fast_rcp(scale + 1e-3);
-                        if (rho > 0 && isfinite(tempChi)) {
-                            const double t = 2 * rho - 1;
-                            double alpha = 1. - t * t * t;
-                            alpha = fmin(alpha, 2. / 3.);
-                            lambda *= fmax(1. / 3., alpha);
-                            ni = 2;
-                            currentChi = tempChi;
-#pragma unroll
-                            for (int q = 0; q < 8; q++) T[q] = Tt[q];
-#pragma unroll
-                            for (int q = 0; q < 28; q++) acc[q] = tacc2[q];
-                        } else {
-                            lambda *= ni;
-                            ni *= 2;
-                        }
-                        qmax++;
-                        EV(5);
-                    } while (rho < 0 && qmax < 10);
-                    iters++;
-                    if (qmax == 10 || rho == 0) break;
-                    if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
-                    else nbadIt = 0;
-                    if (nbadIt >= 3) break;
-                }
-                if (tid == 0) {
-#pragma unroll
-                    for (int q = 0; q < 8; q++) sTt[q] = T[q];
-                    sCmd = 0;
-                }
-                __syncthreads();  // A: done
-            } else {
-                for (;;) {
+                    for (int q = 0; q < 8; q++) Tt[q] = scand[cj].T[q];
+                    const bool ok2 = scand[cj].ok != 0;
+                    const double scale = scand[cj].scale;
                     seq++;
-                    __syncthreads();  // A
-                    if (sCmd == 0) break;
                     EV(0);
-                    double Tt[8], tacc2[28];
+                    {
+                        const double c = wave_sum(pose_chi_pass(Tt, cam, sobs, outl, schi, n, robust));
+                        EV(1);
+                        if ((tid & 63) == 0) chiw[cb][wid] = c;
+                    }
+                    __syncthreads();  // B1: the trial's chi2 partials
+                    EV(2);
+                    double tempChi = 0;
 #pragma unroll
-                    for (int q = 0; q < 8; q++) Tt[q] = sTt[q];
-                    pose_pass(Tt, cam, sobs, outl, schi, n, robust, tacc2);
-                    EV(1);
-                    pose_reduce28_w0(tacc2, red[rb], evp());
-                    rb ^= 1;
+                    for (int w = 0; w < kPoseWaves; w++) tempChi += chiw[cb][w];
+                    cb ^= 1;
+                    if (!ok2) tempChi = DBL_MAX;
+                    const double rho = (currentChi - tempChi) * fast_rcp(scale + 1e-3);
+                    accept = rho > 0 && isfinite(tempChi);
+                    if (accept) {
+                        const double t = 2 * rho - 1;
+                        double alpha = 1. - t * t * t;
+                        alpha = fmin(alpha, 2. / 3.);
+                        lambda *= fmax(1. / 3., alpha);
+                        ni = 2;
+                        currentChi = tempChi;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) T[q] = Tt[q];
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                        cj++;
+                    }
+                    qmax++;
+                    bool done = false;
+                    if (!(rho < 0 && qmax < 10)) {  // the do-while of iteration i ends
+                        iters++;
+                        if (qmax == 10 || rho == 0) done = true;
+                        else {
+                            if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
+                            else nbadIt = 0;
+                            if (nbadIt >= 3 || ++i >= 10) done = true;
+                            iniChi = currentChi;
+                            qmax = 0;
+                        }
+                    }
+                    EV(3);
+                    if (done) break;
+                    regen = !accept && cj == kPoseCands;  // chain exhausted: continue it
                 }
+                if (accept || regen) {
+                    if (accept) {  // buildSystem at the (new) estimate: the first iteration's, or
+                                   // the next iteration's after an accepted trial
+                        pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
+                        pose_reduce28_w0(acc, red[rb], stot);  // B2 inside
+                        rb ^= 1;
+                    } else {
+                        __syncthreads();  // every wave has read scand
+                        if (wid == 0) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) T[q] = sTt[q];
+                            for (int q = 0; q < 28; q++) acc[q] = stot[q];
+                        }
+                    }
+                    EV(4);
+                    if (wid == 0) {
+                        if (first)  // computeLambdaInit, tau = 1e-5
+                            lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
+                                                 fmax(fabs(acc[18]), fabs(acc[20])));
+                        pose_candidates(acc, lambda, ni, T, scand);
+                        EV(5);
+                    }
+                    cj = 0;
+                    __syncthreads();  // B3: the trial chain published
+                    EV(6);
+                    if (first) {
+                        currentChi = iniChi = stot[27];
+                        first = false;
+                    }
+                }
             }
         }
         // ---- outlier classification (:418-466): stale errors of the inliers, fresh ones of the

@@ -41,26 +41,32 @@ for n in (420, 680):
     tot, real, nseq = int(tr[0]), int(tr[1]), int(tr[2])
     print(f"  traced: {real / 100.0:.1f} us, {tot} cycles ({tot / (real / 100.0):.0f} MHz), {nseq} passes", flush=True)
     ev = tr[16:].reshape(SEQS, WAVES, 8).astype(np.int64)
-    # per pass: duration of each wave's pass, barrier wait, wave-0 phases (cycles)
-    sums = {"pass(max wave)": [], "pass(wave0)": [], "rs(wave0)": [], "B wait(wave0)": [], "gather(wave0)": [],
-            "lm(wave0)": [], "solve+oplus(wave0)": [], "A wait(others)": []}
-    for s in range(min(nseq, SEQS) - 1):
-        e = ev[s]
+    # per trial (seq): pass, chi2 barrier B1, decision; accepted trials add the 28-value
+    # reduction (B2), wave 0's lane-parallel trial chain and the candidates barrier B3 (cycles)
+    sums = {"trial(wave0)": [], "pass(max wave)": [], "pass(wave0)": [], "B1 wait(wave0)": [],
+            "decision(wave0)": [], "reduce+B2(wave0)": [], "chain solve(wave0)": [], "B3 wait(wave1)": []}
+    acc_n = 0
+    for s in range(1, min(nseq, SEQS) - 1):
+        e, nxt = ev[s], ev[s + 1]
         act = [w for w in range(WAVES) if e[w, 0] and e[w, 1]]
         if 0 not in act:
             continue
+        if nxt[0, 0]:
+            sums["trial(wave0)"].append(nxt[0, 0] - e[0, 0])
         sums["pass(max wave)"].append(max(e[w, 1] - e[w, 0] for w in act))
         sums["pass(wave0)"].append(e[0, 1] - e[0, 0])
-        sums["rs(wave0)"].append(e[0, 2] - e[0, 1])
-        sums["B wait(wave0)"].append(e[0, 3] - e[0, 2])
-        sums["gather(wave0)"].append(e[0, 4] - e[0, 3])
-        if e[0, 5]:
-            sums["lm(wave0)"].append(e[0, 5] - e[0, 4])
-        if e[0, 6] and e[0, 5]:
-            sums["solve+oplus(wave0)"].append(e[0, 6] - e[0, 5])
-        nxt = ev[s + 1]
-        if nxt[1, 0] and e[1, 3]:
-            sums["A wait(others)"].append(nxt[1, 0] - e[1, 3])
+        if e[0, 2]:
+            sums["B1 wait(wave0)"].append(e[0, 2] - e[0, 1])
+        if e[0, 3] and e[0, 2]:
+            sums["decision(wave0)"].append(e[0, 3] - e[0, 2])
+        if e[0, 4] and e[0, 3]:
+            acc_n += 1
+            sums["reduce+B2(wave0)"].append(e[0, 4] - e[0, 3])
+            if e[0, 5]:
+                sums["chain solve(wave0)"].append(e[0, 5] - e[0, 4])
+            if e[1, 6] and e[1, 3]:
+                sums["B3 wait(wave1)"].append(e[1, 6] - e[1, 3])
+    print(f"    accepted (or regenerated) trials with a fresh solve: {acc_n}", flush=True)
     for k, v in sums.items():
         if v:
             print(f"    {k:22s} mean {np.mean(v):8.0f} cycles  (n={len(v)})", flush=True)
