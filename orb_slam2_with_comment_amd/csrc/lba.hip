@@ -1,28 +1,37 @@
 // Optimizer::LocalBundleAdjustment (src/Optimizer.cc:483-808) on MI355X, fp64.
 //
 // The g2o schedule -- optimize(5), outlier levels, optimize(10), erase list -- runs as a chain
-// of chip-wide kernels on one stream; the Levenberg control (g2o/core/
-// optimization_algorithm_levenberg.cpp:61-164) stays on the host, which reads one small block
-// of partial sums per trial and launches the next trial.  Per LM iteration:
+// of chip-wide kernels on one stream, with the Levenberg control (g2o/core/
+// optimization_algorithm_levenberg.cpp:61-164) on the device.  Once per optimize():
 //   k_ba_linearize     thread / edge   computeActiveErrors + robust chi2, Jacobians
 //                                      (types_six_dof_expmap.cpp), Huber weights, the edge's
 //                                      Hpl block and its Hll / b_l, Hpp / b_p contributions
 //   k_ba_reduce        thread / point  Hll, b_l (sum over the point's edges, g2o order)
-//                      block / pose    Hpp, b_p (fixed-order sum over the keyframe's edges)
-// per trial (lambda):
+//                      block / pose    max |diag H| for computeLambdaInit
+// per trial (lambda), three launches:
 //   k_ba_schur         block / (pose i <= pose j)  H_schur(i,j) = Hpp + lambda I - sum_points
 //                                      B_i D^-1 B_j^T over observation pairs (lists built once),
-//                                      b_schur = b_p - sum B D^-1 b_l; lambda init on iteration 0
+//                                      Hpp / b_p summed over the keyframe's edges in the diagonal
+//                                      blocks, b_schur = b_p - sum B D^-1 b_l
 //   k_ba_solve         one block       blocked (6x6) LDL^T of the 6K x 6K reduced system with the
 //                                      right-hand side carried through, back substitution,
 //                                      trial poses exp(dx) * T, poses' part of computeScale
-//   k_ba_update_errors thread / point  back substitution x + dx, trial errors, computeScale
+//   k_ba_update_errors thread / point  back substitution x + dx, trial errors, computeScale, and
+//                                      the linearisation at the trial state into the second
+//                                      linear-system buffer (an accepted trial's next iteration
+//                                      starts with computeActiveErrors + buildSystem at exactly
+//                                      that state, so the buffers swap; a rejected trial keeps
+//                                      the current system); its last block runs the Levenberg
+//                                      decision (k_ba_control_body)
 // The g2o semantics kept: lambda init tau = 1e-5, rho test with computeScale + 1e-3, the
 // ORB-SLAM "3 bad iterations" stop, stale edge errors after a rejected trial, push/pop of
 // the estimates (pointer swap of current / trial buffers), Huber kernels removed for the
 // second pass.  Every reduction has a fixed order (deterministic).  Parity with the oracle: 1e-4.
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -56,7 +65,8 @@ struct BaCtl {
     int np, nl;       // free poses / active points of the index mapping
     int unsupported;  // more than kBaMaxPoses active poses
     int steps;        // trial steps executed (diagnostics)
-    int pad;
+    int lin;          // which of the two linear-system buffers holds the current system
+    unsigned arrive;  // blocks of k_ba_update_errors finished (the last one runs the control)
     double lambda, ni, currentChi, iniChi;
     double chi_out[2];  // activeRobustChi2 after optimize(5) / optimize(10)
     int it_out[2];      // iterations of optimize(5) / optimize(10); -1 with an empty mapping
@@ -92,19 +102,36 @@ struct BaDev {
     int* pose_kf;              // kBaMaxPoses
     int* e_pi;                 // nedge: pose index of the edge's keyframe (-1 fixed / inactive)
     int* kf_act;               // nkf: activation generation that saw an active edge of the keyframe
+    // the linear system: Hplb[L] etc. with L = ctl->lin is the current one (ba_sys selects it)
     double* Hpl;               // nedge x 18 (pose rows x point cols)
     double* Hle;               // nedge x 9: edge's Hll upper (6) + b_l (3)
     double* Hpe;               // nedge x 27 in keyframe-CSR order: edge's Hpp upper (21) + b_p (6)
     double* Hll;               // npt x 9
     double* bl;                // npt x 3
+    double* Hplb[2];
+    double* Hleb[2];
+    double* Hpeb[2];
+    double* Hllb[2];
+    double* blb[2];
     double* Hpp;               // kBaMaxPoses x 36
-    double* bp;                // kBaMaxPoses x 6
+    double* bp;                // kBaMaxPoses x 6 (k_ba_schur, read by the solve)
     double* S;                 // packed upper reduced system (kBaPacked)
     double* bs;                // kBaMaxN
     double* xp;                // kBaMaxN
     double* scal;              // [1] poses' computeScale part, [2] solve ok, [3] lambda used
     int* istat;                // [0] np, [1] nl, [2] too many poses, [3] solve ok
 };
+
+// the linear system of buffer L (kernels select ctl->lin on entry)
+struct BaSys { double *Hpl, *Hle, *Hpe, *Hll, *bl; };
+__device__ inline BaSys ba_sys(const BaDev& a, int L) {
+    return BaSys{L ? a.Hplb[1] : a.Hplb[0], L ? a.Hleb[1] : a.Hleb[0], L ? a.Hpeb[1] : a.Hpeb[0],
+                 L ? a.Hllb[1] : a.Hllb[0], L ? a.blb[1] : a.blb[0]};
+}
+__device__ inline void ba_use(BaDev& a, int L) {
+    const BaSys y = ba_sys(a, L);
+    a.Hpl = y.Hpl; a.Hle = y.Hle; a.Hpe = y.Hpe; a.Hll = y.Hll; a.bl = y.bl;
+}
 
 // ---------------------------------------------------------------- edges
 __device__ inline bool edge_stereo(const orbmi_ba_edge& e) { return !(e.ur < 0); }
@@ -156,37 +183,40 @@ __device__ inline void edge_robust(const BaDev& a, int i, double c, double* rho0
 }
 
 // Jacobians (types_six_dof_expmap.cpp:103-134, :188-234)
-__device__ inline void edge_jacobians(const BaDev& a, int i, const double* T, const double* X, double Jl[3][3],
+__device__ inline void edge_jacobians(const BaDev& a, int i, const double* T, const double* Xp, double Jl[3][3],
                                       double Jp[3][6]) {
     const orbmi_ba_edge e = a.edges[i];
     const orbmi_ba_keyframe& kf = a.kfs[e.kf];
     const double* Tk = T + 8 * e.kf;
     double p[3], R[3][3];
-    se3_map(Tk, X + 4 * e.point, p);
+    se3_map(Tk, Xp, p);
     q_to_matrix(load_q(Tk), R);
-    const double x = p[0], y = p[1], z = p[2], z2 = z * z;
+    // one reciprocal per edge (fast_rcp: within an ulp of 1 / z) instead of the reference's
+    // divisions; the Jacobians only steer the Levenberg steps (parity 1e-4), the errors and
+    // chi2 keep the exact divisions
+    const double x = p[0], y = p[1], z = p[2], iz = fast_rcp(z), iz2 = iz * iz;
     const double fx = kf.fx, fy = kf.fy, bf = kf.bf;
     if (!edge_stereo(e)) {
-        const double t02 = -x / z * fx, t12 = -y / z * fy;
+        const double t02 = -x * iz * fx, t12 = -y * iz * fy;
         for (int c = 0; c < 3; c++) {
-            Jl[0][c] = -1. / z * (fx * R[0][c] + 0 * R[1][c] + t02 * R[2][c]);
-            Jl[1][c] = -1. / z * (0 * R[0][c] + fy * R[1][c] + t12 * R[2][c]);
+            Jl[0][c] = -iz * (fx * R[0][c] + t02 * R[2][c]);
+            Jl[1][c] = -iz * (fy * R[1][c] + t12 * R[2][c]);
             Jl[2][c] = 0;
         }
     } else {
         for (int c = 0; c < 3; c++) {
-            Jl[0][c] = -fx * R[0][c] / z + fx * x * R[2][c] / z2;
-            Jl[1][c] = -fy * R[1][c] / z + fy * y * R[2][c] / z2;
-            Jl[2][c] = Jl[0][c] - bf * R[2][c] / z2;
+            Jl[0][c] = -fx * R[0][c] * iz + fx * x * R[2][c] * iz2;
+            Jl[1][c] = -fy * R[1][c] * iz + fy * y * R[2][c] * iz2;
+            Jl[2][c] = Jl[0][c] - bf * R[2][c] * iz2;
         }
     }
-    Jp[0][0] = x * y / z2 * fx; Jp[0][1] = -(1 + (x * x / z2)) * fx; Jp[0][2] = y / z * fx;
-    Jp[0][3] = -1. / z * fx; Jp[0][4] = 0; Jp[0][5] = x / z2 * fx;
-    Jp[1][0] = (1 + y * y / z2) * fy; Jp[1][1] = -x * y / z2 * fy; Jp[1][2] = -x / z * fy;
-    Jp[1][3] = 0; Jp[1][4] = -1. / z * fy; Jp[1][5] = y / z2 * fy;
+    Jp[0][0] = x * y * iz2 * fx; Jp[0][1] = -(1 + (x * x * iz2)) * fx; Jp[0][2] = y * iz * fx;
+    Jp[0][3] = -iz * fx; Jp[0][4] = 0; Jp[0][5] = x * iz2 * fx;
+    Jp[1][0] = (1 + y * y * iz2) * fy; Jp[1][1] = -x * y * iz2 * fy; Jp[1][2] = -x * iz * fy;
+    Jp[1][3] = 0; Jp[1][4] = -iz * fy; Jp[1][5] = y * iz2 * fy;
     if (edge_stereo(e)) {
-        Jp[2][0] = Jp[0][0] - bf * y / z2; Jp[2][1] = Jp[0][1] + bf * x / z2; Jp[2][2] = Jp[0][2];
-        Jp[2][3] = Jp[0][3]; Jp[2][4] = 0; Jp[2][5] = Jp[0][5] - bf / z2;
+        Jp[2][0] = Jp[0][0] - bf * y * iz2; Jp[2][1] = Jp[0][1] + bf * x * iz2; Jp[2][2] = Jp[0][2];
+        Jp[2][3] = Jp[0][3]; Jp[2][4] = 0; Jp[2][5] = Jp[0][5] - bf * iz2;
     } else {
         for (int c = 0; c < 6; c++) Jp[2][c] = 0;
     }
@@ -446,10 +476,10 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a) {
 
 // ---------------------------------------------------------------- linear system
 // D^-1 of the point's damped 3x3 block, Hll + lambda I (cofactors)
-__device__ inline void point_dinv(const BaDev& a, int p, double lam, double Di[9]) {
+__device__ inline void point_dinv(const double* Hll, int p, double lam, double Di[9]) {
     double D[3][3];
     for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) D[r][c] = a.Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
+        for (int c = 0; c < 3; c++) D[r][c] = Hll[9 * p + 3 * r + c] + (r == c ? lam : 0.0);
     const double c00 = D[1][1] * D[2][2] - D[1][2] * D[2][1];
     const double c10 = D[1][2] * D[2][0] - D[1][0] * D[2][2];
     const double c20 = D[1][0] * D[2][1] - D[1][1] * D[2][0];
@@ -468,9 +498,49 @@ __device__ inline void point_dinv(const BaDev& a, int p, double lam, double Di[9
 // BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:55-120): Hpl block, the
 // edge's Hll / b_l and Hpp / b_p contributions.  Inactive edges into free poses write zeros,
 // so the reductions and the Schur products need no activity tests.
+// BaseBinaryEdge::constructQuadraticForm of edge i at (T, point position Xp) into a's linear
+// system (errors already in a.err): Hpl block, the edge's Hll / b_l and Hpp / b_p contributions.
+// Inactive edges into free poses write zeros, so the reductions and the Schur products need no
+// activity tests.  Returns nothing; pi = pose index of the edge's keyframe (-1 fixed).
+__device__ inline void edge_linearize(const BaDev& a, const BaSys& y, int i, int pi, bool active, const double* T,
+                                      const double* Xp, double* He_out = nullptr) {
+    const bool free_pose = pi >= 0;
+    double* Hp = y.Hpe + 27 * (long long)a.kf_pos[i];
+    double* B = y.Hpl + 18 * (long long)i;
+    if (!active) {
+        if (free_pose) {
+            for (int q = 0; q < 27; q++) Hp[q] = 0;
+            for (int q = 0; q < 18; q++) B[q] = 0;
+        }
+        return;
+    }
+    double Jl[3][3], Jp[3][6], w, om[3];
+    edge_jacobians(a, i, T, Xp, Jl, Jp);
+    edge_weights(a, i, &w, om);
+    double* He = He_out ? He_out : y.Hle + 9 * (long long)i;
+    int q = 0;
+    for (int r = 0; r < 3; r++)
+        for (int c = r; c < 3; c++, q++)
+            He[q] = Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
+    for (int r = 0; r < 3; r++) He[6 + r] = Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
+    if (free_pose) {
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 3; c++)
+                B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
+        q = 0;
+        for (int r = 0; r < 6; r++)
+            for (int c = r; c < 6; c++, q++)
+                Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
+        for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
+    }
+}
+
+// thread per edge, the first linearisation of an optimize(): computeActiveErrors + robust chi2
+// (block partials), then the edge's blocks (edge_linearize) into the current linear system
 __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done || !ctl.need_lin) return;  // a retry trial keeps the linear system
+    if (ctl.done || !ctl.need_lin) return;
+    const BaSys y = ba_sys(a, ctl.lin);
     const double* T = a.Tb[ctl.cur];
     const double* X = a.Xb[ctl.cur];
     double* part = a.part_lin;
@@ -480,39 +550,14 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
     if (i < a.nedge) {
         const int pi = a.pose_idx[a.edges[i].kf];
         a.e_pi[i] = pi;  // for k_ba_update_errors (set by the first linearisation of optimize())
-        const bool free_pose = pi >= 0;
-        double* Hp = a.Hpe + 27 * (long long)a.kf_pos[i];
-        double* B = a.Hpl + 18 * (long long)i;
-        if (!(a.eflag[i] & 4)) {
-            if (free_pose) {
-                for (int q = 0; q < 27; q++) Hp[q] = 0;
-                for (int q = 0; q < 18; q++) B[q] = 0;
-            }
-        } else {
+        const bool active = a.eflag[i] & 4;
+        if (active) {
             edge_error(a, i, T, X, a.err + 3 * i);
             double r0, r1;
             edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
             chi = r0;
-            double Jl[3][3], Jp[3][6], w, om[3];
-            edge_jacobians(a, i, T, X, Jl, Jp);
-            edge_weights(a, i, &w, om);
-            double* He = a.Hle + 9 * (long long)i;
-            int q = 0;
-            for (int r = 0; r < 3; r++)
-                for (int c = r; c < 3; c++, q++)
-                    He[q] = Jl[0][r] * w * Jl[0][c] + Jl[1][r] * w * Jl[1][c] + Jl[2][r] * w * Jl[2][c];
-            for (int r = 0; r < 3; r++) He[6 + r] = Jl[0][r] * om[0] + Jl[1][r] * om[1] + Jl[2][r] * om[2];
-            if (free_pose) {
-                for (int r = 0; r < 6; r++)
-                    for (int c = 0; c < 3; c++)
-                        B[r * 3 + c] = Jp[0][r] * w * Jl[0][c] + Jp[1][r] * w * Jl[1][c] + Jp[2][r] * w * Jl[2][c];
-                q = 0;
-                for (int r = 0; r < 6; r++)
-                    for (int c = r; c < 6; c++, q++)
-                        Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
-                for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
-            }
         }
+        edge_linearize(a, y, i, pi, active, T, X + 4 * a.edges[i].point);
     }
     chi = block_sum<kBaBlock>(chi, red);
     if (threadIdx.x == 0) part[blockIdx.x] = chi;
@@ -526,6 +571,7 @@ constexpr int kBaPoseLanes = kBaBlock / 27;  // 9
 __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
     const BaCtl& ctl = *a.ctl;
     if (ctl.done || !ctl.need_lin) return;
+    ba_use(a, ctl.lin);
     const int nb_p = a.nb_p;
     double* part_max = a.part_max;
     __shared__ double red[kBaPoseLanes][27];
@@ -606,9 +652,39 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
 constexpr int kSchurThreads = 512;
 constexpr int kSchurWaves = kSchurThreads / 64;
 
+// sum over keyframe k's edges (keyframe-CSR rows of Hpe) of values [q0, q0 + nq) of the 27,
+// fixed order: thread = (value, lane) with kSchurThreads / nq lanes, then lanes in order;
+// tot[q] for q < nq in LDS after the call (LDS scratch red, >= kSchurThreads doubles)
+template <int NQ>
+__device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red, double* tot) {
+    constexpr int kLanes = kSchurThreads / NQ;
+    const int q = threadIdx.x % NQ, el = threadIdx.x / NQ;
+    const double* base = a.Hpe + 27 * (long long)a.kf_start[k] + q0 + q;
+    const int n = a.kf_start[k + 1] - a.kf_start[k];
+    if (el < kLanes) {
+        double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // eight loads in flight per lane
+        int m = el;
+        for (; m + 7 * kLanes < n; m += 8 * kLanes)
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] += base[27 * (long long)(m + u * kLanes)];
+        for (int u = 0; m < n; m += kLanes, u++) v[u] += base[27 * (long long)m];
+        red[el * NQ + q] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < NQ) {
+        double t = 0;
+        for (int w = 0; w < kLanes; w++) t += red[w * NQ + threadIdx.x];
+        tot[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     const BaCtl& ctl = *a.ctl;
     if (ctl.done) return;
+    ba_use(a, ctl.lin);
+    __shared__ double rows[kSchurThreads];
+    __shared__ double ptot[21];  // Hpp (upper) or b_p of the block's keyframe
     const int N = 6 * ctl.np, nmax = a.nb_p + ctl.np;
     const double* part_max = a.part_max;
     // lambda: computeLambdaInit on the first trial of iteration 0, the LM state otherwise
@@ -631,12 +707,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
         const int ka = a.blk_kf[2 * (r * a.nf - r * (r - 1) / 2)];
         const int i1 = a.pose_idx[ka];
         if (i1 < 0) return;
+        pose_rows_sum<6>(a, ka, 21, rows, ptot);  // b_p of the keyframe (its edges in CSR order)
         double bacc[6] = {0, 0, 0, 0, 0, 0};
         for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
             const int e = a.kf_edges[j];
             const int p = a.kf_pt[j];
             double Di[9];
-            point_dinv(a, p, lam, Di);
+            point_dinv(a.Hll, p, lam, Di);
             const double* blp = a.bl + 3 * p;
             double db[3];
             for (int rr = 0; rr < 3; rr++) db[rr] = Di[rr * 3] * blp[0] + Di[rr * 3 + 1] * blp[1] + Di[rr * 3 + 2] * blp[2];
@@ -653,7 +730,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
         if (threadIdx.x < 6) {
             double t = 0;
             for (int w = 0; w < kSchurWaves; w++) t += red[w][threadIdx.x];
-            a.bs[6 * i1 + threadIdx.x] = a.bp[6 * i1 + threadIdx.x] - t;
+            a.bp[6 * i1 + threadIdx.x] = ptot[threadIdx.x];  // the solve's computeScale reads it
+            a.bs[6 * i1 + threadIdx.x] = ptot[threadIdx.x] - t;
         }
         return;
     }
@@ -662,13 +740,14 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     const int i1 = a.pose_idx[ka], i2 = a.pose_idx[kb];
     if (i1 < 0 || i2 < 0) return;
     const bool diag = ka == kb;
+    if (diag) pose_rows_sum<21>(a, ka, 0, rows, ptot);  // Hpp of the keyframe (upper, row-major)
     double acc[36];
 #pragma unroll
     for (int q = 0; q < 36; q++) acc[q] = 0;
     for (int j = a.blk_start[b] + threadIdx.x; j < a.blk_start[b + 1]; j += blockDim.x) {
         const int2 pr = a.blk_pairs[j];  // inactive edges carry a zero Hpl block
         double Di[9];
-        point_dinv(a, a.edges[pr.x].point, lam, Di);
+        point_dinv(a.Hll, a.edges[pr.x].point, lam, Di);
         const double* B1 = a.Hpl + 18 * (long long)pr.x;
         const double* B2 = a.Hpl + 18 * (long long)pr.y;
         double BD[18];
@@ -704,7 +783,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
         for (int w = 0; w < kSchurWaves; w++) t += red[w][q];
         const int r = q / 6, c = q % 6;
         if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
-        else if (c >= r) a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (a.Hpp[36 * i1 + q] + (r == c ? lam : 0.0)) - t;
+        else if (c >= r)
+            a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (ptot[packed(r, c, 6)] + (r == c ? lam : 0.0)) - t;
     }
 }
 
@@ -1144,66 +1224,6 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
     SOLVE_STAMP_FLUSH();
 }
 
-// ---------------------------------------------------------------- update + trial errors
-// block = 32 points.  Threads 0..31: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
-// part); then every thread takes edges of the block's points: computeActiveErrors on the trial
-// state (T_t from k_ba_pose_trial).  Block partials: robust chi2 and scale.
-constexpr int kBaUpdPts = 32;
-__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
-    const BaCtl& ctl = *a.ctl;
-    if (ctl.done) return;
-    const double lam = a.scal[3];
-    const double* __restrict__ X = a.Xb[ctl.cur];
-    const double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
-    double* __restrict__ Xt = a.Xb[ctl.cur ^ 1];
-    double* __restrict__ part_chi = a.part_tchi;
-    double* __restrict__ part_scale = a.part_tscale;
-    __shared__ double red[kBaBlock / 64];
-    __shared__ double xs[kBaUpdPts][4];
-    const bool ok = a.istat[3] != 0;
-    const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
-    double sc = 0, chi = 0;
-    if (threadIdx.x < kBaUpdPts && p0 + (int)threadIdx.x < p1) {
-        const int p = p0 + threadIdx.x;
-        double xl[3] = {0, 0, 0};
-        if (ok && point_active(a, p)) {
-            double cl[3] = {a.bl[3 * p], a.bl[3 * p + 1], a.bl[3 * p + 2]};
-            for (int e = a.pt_start[p]; e < a.pt_start[p + 1]; e++) {
-                const int i1 = a.e_pi[e];
-                if (i1 < 0) continue;  // inactive edges into free poses carry a zero block
-                const double* B = a.Hpl + 18 * (long long)e;
-                for (int c = 0; c < 3; c++)
-                    for (int r = 0; r < 6; r++) cl[c] -= B[r * 3 + c] * a.xp[6 * i1 + r];
-            }
-            double Di[9];
-            point_dinv(a, p, lam, Di);
-            for (int r = 0; r < 3; r++) xl[r] = Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1] + Di[r * 3 + 2] * cl[2];
-        }
-        for (int r = 0; r < 3; r++) {
-            const double x = X[4 * p + r] + xl[r];
-            Xt[4 * p + r] = x;
-            xs[threadIdx.x][r] = x;
-            if (ok) sc += xl[r] * (lam * xl[r] + a.bl[3 * p + r]);
-        }
-    }
-    __syncthreads();
-    if (p0 < p1)
-        for (int e = a.pt_start[p0] + threadIdx.x; e < a.pt_start[p1]; e += blockDim.x) {
-            if (!(a.eflag[e] & 4)) continue;
-            const orbmi_ba_edge ed = a.edges[e];
-            edge_error_at(a, e, Tt, &xs[ed.point - p0][0], a.err + 3 * e);
-            double r0, r1;
-            edge_robust(a, e, edge_chi2(a, e), &r0, &r1);
-            chi += r0;
-        }
-    chi = block_sum<kBaBlock>(chi, red);
-    sc = block_sum<kBaBlock>(sc, red);
-    if (threadIdx.x == 0) {
-        part_chi[blockIdx.x] = chi;
-        part_scale[blockIdx.x] = sc;
-    }
-}
-
 // ---------------------------------------------------------------- Levenberg control
 // fixed-order sum of n partials by one wave (lane l: l, l + 64, ...; then a fixed xor tree,
 // lane 0's value broadcast): deterministic run to run
@@ -1216,27 +1236,34 @@ __device__ inline double wave_sum_fixed(const double* p, int n) {
 
 // one wave, after each trial: OptimizationAlgorithmLevenberg::solve's decision
 // (levenberg.cpp:104-164) and SparseOptimizer::optimize's loop (sparse_optimizer.cpp:354-419)
-// with ORB-SLAM2's 3-bad-iterations stop; pbStopFlag is read through the host-mapped mirror
-__global__ __launch_bounds__(64) void k_ba_control(BaDev a) {
+// with ORB-SLAM2's 3-bad-iterations stop; pbStopFlag is read through the host-mapped mirror.
+// currentChi of an iteration's computeActiveErrors: the first linearisation's chi2 at
+// iteration 0, the accepted trial's chi2 afterwards (the same errors; an iteration that ends
+// on a rejection keeps the estimate, hence the chi2 and the linear system).
+__device__ inline void k_ba_control_body(const BaDev& a) {
     BaCtl& c = *a.ctl;
-    if (c.done) return;
     const double lin = wave_sum_fixed(a.part_lin, a.nb_e);
     const double tchi = wave_sum_fixed(a.part_tchi, a.nb_q);
     const double tsc = wave_sum_fixed(a.part_tscale, a.nb_q);
     if (threadIdx.x != 0) return;
-    if (c.trial == 0) c.iniChi = c.currentChi = lin;  // computeActiveErrors at iteration entry
+    if (c.trial == 0) {
+        if (c.it == 0) c.currentChi = lin;
+        c.iniChi = c.currentChi;
+    }
     if (c.it == 0 && c.trial == 0) c.lambda = a.scal[3];  // computeLambdaInit (k_ba_schur)
     const bool ok2 = a.scal[2] != 0;
     const double tempChi = ok2 ? tchi : DBL_MAX;
     const double scale = ok2 ? tsc + a.scal[1] : 0.0;
     const double rho = (c.currentChi - tempChi) / (scale + 1e-3);
-    if (rho > 0 && isfinite(tempChi)) {  // accept: the trial buffers become current
-        double alpha = 1. - pow(2 * rho - 1, 3);
+    if (rho > 0 && isfinite(tempChi)) {  // accept: the trial estimate and its linear system become current
+        const double t = 2 * rho - 1;
+        double alpha = 1. - t * t * t;
         alpha = fmin(alpha, 2. / 3.);
         c.lambda *= fmax(1. / 3., alpha);
         c.ni = 2;
         c.currentChi = tempChi;
         c.cur ^= 1;
+        c.lin ^= 1;
     } else {  // reject: pop (the trial buffers are not adopted)
         c.lambda *= c.ni;
         c.ni *= 2;
@@ -1244,10 +1271,7 @@ __global__ __launch_bounds__(64) void k_ba_control(BaDev a) {
     c.trial++;
     c.steps++;
     const bool stop = a.stop && *a.stop;
-    if (rho < 0 && c.trial < 10 && !stop) {  // next trial of the same iteration
-        c.need_lin = 0;
-        return;
-    }
+    if (rho < 0 && c.trial < 10 && !stop) return;  // next trial of the same iteration
     c.it++;
     bool term;
     if (c.trial == 10 || rho == 0) {
@@ -1258,8 +1282,132 @@ __global__ __launch_bounds__(64) void k_ba_control(BaDev a) {
         term = c.nbad >= 3;
     }
     c.trial = 0;
-    c.need_lin = 1;
     if (term || c.it >= c.max_it || stop) c.done = 1;
+}
+
+// ---------------------------------------------------------------- update + trial errors
+// block = 32 points.  Threads 0..31: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
+// part); then every thread takes edges of the block's points: computeActiveErrors on the trial
+// state (T_t from the solve) and the edge's linearisation at that state into the other
+// linear-system buffer; threads 0..31 then sum the points' Hll / b_l there.  Block partials:
+// robust chi2 and scale; the last block to finish runs the Levenberg decision.
+constexpr int kBaUpdPts = 32;
+constexpr int kBaUpdLanes = kBaBlock / kBaUpdPts;  // 8 threads per point
+constexpr int kBaUpdLdsEdges = 512;                // a block's edges whose Hll / b_l terms stay in LDS
+static_assert(kBaUpdLanes == 8, "8-lane segmented sums");
+
+// sum over the 8 lanes of an aligned group (DPP quad xor steps, then the half-row mirror); every
+// lane of the group ends with the same value
+__device__ inline double sum8(double v) {
+    v += dpp_mov<kDppXor1>(v);
+    v += dpp_mov<kDppXor2>(v);
+    return v + dpp_mov<kDppHalfMirror>(v);
+}
+
+__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
+    BaCtl& ctl = *a.ctl;
+    if (ctl.done) return;
+    const int L = ctl.lin;
+    const BaSys y = ba_sys(a, L);      // current linear system
+    const BaSys t = ba_sys(a, L ^ 1);  // trial state's linear system (adopted if accepted)
+    const double lam = a.scal[3];
+    const double* __restrict__ X = a.Xb[ctl.cur];
+    const double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    double* __restrict__ Xt = a.Xb[ctl.cur ^ 1];
+    double* __restrict__ part_chi = a.part_tchi;
+    double* __restrict__ part_scale = a.part_tscale;
+    __shared__ double red[kBaBlock / 64];
+    __shared__ double xs[kBaUpdPts][4];
+    __shared__ double sHe[kBaUpdLdsEdges * 9];
+    __shared__ bool last;
+    const bool ok = a.istat[3] != 0;
+    const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
+    const int tid = threadIdx.x, ps = tid / kBaUpdLanes, j = tid % kBaUpdLanes;
+    const int p = p0 + ps;
+    const bool own = p < p1;
+    const int pe0 = own ? a.pt_start[p] : 0, pe1 = own ? a.pt_start[p + 1] : 0;
+    double sc = 0, chi = 0;
+    {  // back substitution x_l = D^-1 (b_l - sum_e Hpl_e^T x_p), 8 lanes per point
+        double c0 = 0, c1 = 0, c2 = 0, act = 0;
+        for (int e = pe0 + j; e < pe1; e += kBaUpdLanes) {
+            act += (a.eflag[e] & 4) ? 1.0 : 0.0;
+            const int i1 = a.e_pi[e];
+            if (i1 < 0) continue;  // inactive edges into free poses carry a zero block
+            const double* B = y.Hpl + 18 * (long long)e;
+            const double* xp = a.xp + 6 * i1;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                c0 += B[r * 3] * xp[r];
+                c1 += B[r * 3 + 1] * xp[r];
+                c2 += B[r * 3 + 2] * xp[r];
+            }
+        }
+        c0 = sum8(c0); c1 = sum8(c1); c2 = sum8(c2); act = sum8(act);
+        if (own && j == 0) {
+            double xl[3] = {0, 0, 0};
+            if (ok && act > 0) {  // point_active
+                const double cl[3] = {y.bl[3 * p] - c0, y.bl[3 * p + 1] - c1, y.bl[3 * p + 2] - c2};
+                double Di[9];
+                point_dinv(y.Hll, p, lam, Di);
+                for (int r = 0; r < 3; r++) xl[r] = Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1] + Di[r * 3 + 2] * cl[2];
+            }
+            for (int r = 0; r < 3; r++) {
+                const double x = X[4 * p + r] + xl[r];
+                Xt[4 * p + r] = x;
+                xs[ps][r] = x;
+                if (ok) sc += xl[r] * (lam * xl[r] + y.bl[3 * p + r]);
+            }
+        }
+    }
+    __syncthreads();
+    // trial errors (computeActiveErrors) and the trial state's linearisation, thread per edge;
+    // the edges' Hll / b_l terms go to LDS when the block's edges fit
+    const int be0 = p0 < p1 ? a.pt_start[p0] : 0, be1 = p0 < p1 ? a.pt_start[p1] : 0;
+    const bool lds = be1 - be0 <= kBaUpdLdsEdges;
+    for (int e = be0 + tid; e < be1; e += blockDim.x) {
+        const bool active = a.eflag[e] & 4;
+        const orbmi_ba_edge ed = a.edges[e];
+        const double* Xp = &xs[ed.point - p0][0];
+        if (active) {
+            edge_error_at(a, e, Tt, Xp, a.err + 3 * e);
+            double r0, r1;
+            edge_robust(a, e, edge_chi2(a, e), &r0, &r1);
+            chi += r0;
+        }
+        edge_linearize(a, t, e, a.e_pi[e], active, Tt, Xp, lds ? sHe + 9 * (e - be0) : nullptr);
+    }
+    __syncthreads();
+    {  // Hll / b_l at the trial state, 8 lanes per point, edges in order within a lane
+        double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int e = pe0 + j; e < pe1; e += kBaUpdLanes) {
+            if (!(a.eflag[e] & 4)) continue;
+            const double* He = lds ? sHe + 9 * (e - be0) : t.Hle + 9 * (long long)e;
+#pragma unroll
+            for (int k = 0; k < 9; k++) h[k] += He[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; k++) h[k] = sum8(h[k]);
+        if (own && j == 0) {
+            double* H = t.Hll + 9 * p;
+            H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+            H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+            H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+            for (int k = 0; k < 3; k++) t.bl[3 * p + k] = h[6 + k];
+        }
+    }
+    chi = block_sum<kBaBlock>(chi, red);
+    sc = block_sum<kBaBlock>(sc, red);
+    if (tid == 0) {
+        part_chi[blockIdx.x] = chi;
+        part_scale[blockIdx.x] = sc;
+        __threadfence();
+        last = atomicAdd(&ctl.arrive, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (tid < 64) k_ba_control_body(a);
+    if (tid == 0) ctl.arrive = 0;
 }
 
 // activeRobustChi2 after optimize() (k_ba_errors partials) and the iteration count
@@ -1323,6 +1471,25 @@ namespace {
 
 using namespace orbmi;
 
+// ORBMI_BA_TRACE=1: host wall time of the phases of one call on stderr (development aid)
+struct BaTrace {
+    bool on = getenv("ORBMI_BA_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    char buf[512];
+    int n = 0;
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        n += snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.1f", what,
+                      std::chrono::duration<double, std::micro>(t - last).count());
+        last = t;
+    }
+    ~BaTrace() {
+        if (on) fprintf(stderr, "[ba] total %.1f us:%s\n",
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), buf);
+    }
+};
+
 // Trial steps enqueued beyond the iterations still to run: a rejected trial consumes one step
 // without finishing an iteration, so the first readback usually already sees optimize() done.
 constexpr int kBaStepSlack = 1;
@@ -1355,22 +1522,23 @@ struct Runner {
         return wait();
     }
 
-    // one LM trial: [linearize + reduce at an iteration start] + Schur + solve + update + control;
-    // every kernel returns at once when optimize() is done
+    // one LM trial: Schur + solve + update (trial errors, the trial state's linearisation and,
+    // in its last block, the Levenberg decision); every kernel returns at once when optimize()
+    // is done
     void step() {
-        hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
         if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
         if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaBlock), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(64), 0, h.stream, a);
     }
 
     // SparseOptimizer::optimize(iterations) as phase 0 / 1, then activeRobustChi2
     int optimize(int iterations, int phase) {
         hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, phase + 1);
         hipLaunchKernelGGL(k_ba_activate_ctl, dim3(1), dim3(64), 0, h.stream, a, stopped() ? 0 : iterations, phase + 1);
+        // iteration 0's computeActiveErrors + buildSystem (later ones come with the trials)
+        hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
         int todo = stopped() ? 0 : iterations + kBaStepSlack;
         while (todo > 0) {
             for (int k = 0; k < todo; k++) step();
@@ -1433,6 +1601,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     if ((P->nkf && (!P->kfs || !R->tcw)) || (P->npt && (!P->pts || !R->pos)) || (P->nedge && (!P->edges || !R->erase)))
         return ORBMI_E_ARG;
     orbmi_ba& h = *b;
+    BaTrace tr;
     ORBMI_HIP(hipSetDevice(h.device));
     R->aborted = 0;
     R->iterations[0] = R->iterations[1] = 0;
@@ -1506,8 +1675,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_pairs = take(8 * (size_t)npair);
     const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
                  o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_kfact = take(4 * nkf),
-                 o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(144 * (size_t)ne), o_Hle = take(72 * (size_t)ne),
-                 o_Hpe = take(216 * (size_t)ne), o_Hll = take(72 * npt), o_bl = take(24 * npt),
+                 o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(2 * 144 * (size_t)ne), o_Hle = take(2 * 72 * (size_t)ne),
+                 o_Hpe = take(2 * 216 * (size_t)ne), o_Hll = take(2 * 72 * npt), o_bl = take(2 * 24 * npt),
                  o_Hpp = take(288 * kBaMaxPoses), o_bp = take(48 * kBaMaxPoses), o_S = take(8 * (size_t)kBaPacked),
                  o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN), o_scal = take(64), o_plin = take(8 * (size_t)nb_e),
                  o_ptchi = take(8 * (size_t)nb_q), o_ptsc = take(8 * (size_t)nb_q),
@@ -1543,6 +1712,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     put(o_kf_pos, kf_pos.data(), 4 * (size_t)ne);
     put(o_kf_pt, kf_pt.data(), 4 * (size_t)ne);
     put(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk);
+    tr.mark("host_index");
     ORBMI_HIP(hipMemcpyAsync(B, S, up_bytes, hipMemcpyHostToDevice, s));
     ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
     ORBMI_HIP(hipMemsetAsync(B + o_ctl, 0, sizeof(BaCtl), s));
@@ -1572,8 +1742,14 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.blk_pairs = (int2*)(B + o_pairs);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
     a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf); a.kf_act = (int*)(B + o_kfact);
-    a.Hpl = (double*)(B + o_Hpl); a.Hle = (double*)(B + o_Hle); a.Hpe = (double*)(B + o_Hpe);
-    a.Hll = (double*)(B + o_Hll); a.bl = (double*)(B + o_bl);
+    for (int L = 0; L < 2; L++) {  // two linear-system buffers (ctl.lin selects the current one)
+        a.Hplb[L] = (double*)(B + o_Hpl) + (size_t)L * 18 * ne;
+        a.Hleb[L] = (double*)(B + o_Hle) + (size_t)L * 9 * ne;
+        a.Hpeb[L] = (double*)(B + o_Hpe) + (size_t)L * 27 * ne;
+        a.Hllb[L] = (double*)(B + o_Hll) + (size_t)L * 9 * npt;
+        a.blb[L] = (double*)(B + o_bl) + (size_t)L * 3 * npt;
+    }
+    a.Hpl = a.Hplb[0]; a.Hle = a.Hleb[0]; a.Hpe = a.Hpeb[0]; a.Hll = a.Hllb[0]; a.bl = a.blb[0];
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
     a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
@@ -1587,11 +1763,14 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     }
     ORBMI_HIP(hipGetLastError());
     int rc;
+    tr.mark("enqueue_setup");
     if ((rc = r.optimize(5, 0))) return rc;
+    tr.mark("optimize5");
     const bool second = !r.stopped();
     if (second) {  // src/Optimizer.cc:694-737
         hipLaunchKernelGGL(k_ba_levels, dim3(nb_e), dim3(kBaBlock), 0, s, a);
         if ((rc = r.optimize(10, 1))) return rc;
+        tr.mark("optimize10");
     }
     hipLaunchKernelGGL(k_ba_finish, dim3(nb_all), dim3(kBaBlock), 0, s, a, (float*)(B + o_otcw), (float*)(B + o_opos),
                        out_erase);
@@ -1600,6 +1779,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     if (npt) ORBMI_HIP(hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s));
     if (ne) ORBMI_HIP(hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s));
     if ((rc = r.read_ctl())) return rc;
+    tr.mark("finish");
     const BaCtl& c = *h.h_ctl;
     if (c.unsupported) return ORBMI_E_UNSUPPORTED;
     R->iterations[0] = c.it_out[0];
