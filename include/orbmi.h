@@ -468,6 +468,58 @@ int orbmi_search_by_projection_last_frame_if(orbmi_matcher* m, const orbmi_frame
 int orbmi_track_update_matches(orbmi_matcher* m, const orbmi_frame_view* F, int stage, const uint8_t* outlier,
                                const orbmi_frame_mappoints* mp, uint8_t* occupied_out, int* counts);
 
+/* ---- System::TrackStereo: the native stereo SLAM host loop ---------------------------- */
+
+/* The Tracking constructor's view of a settings file (src/Tracking.cc:53-143) for a rectified
+ * stereo rig: Camera.fx/fy/cx/cy, Camera.bf, mThDepth = bf * ThDepth / fx, mMinFrames = 0,
+ * mMaxFrames = fps, the image size and the ORBextractor parameters. */
+typedef struct orbmi_slam_settings {
+    float fx, fy, cx, cy, bf;
+    float th_depth;
+    int min_frames, max_frames;
+    int width, height;
+    int n_features;
+    float scale_factor;
+    int n_levels, ini_th_fast, min_th_fast;
+    int local_ba;                  /* 1: LocalMapping runs LocalBundleAdjustment (:89-90)      */
+} orbmi_slam_settings;
+
+/* Per tracked frame: Tracking's counters (-1 = the stage did not run). track: 0 none, 1
+ * TrackWithMotionModel, 2 TrackReferenceKeyFrame (the last one tried). */
+typedef struct orbmi_slam_frame_stats {
+    int frame, n, state, init, track;
+    int lf_matches, bow_matches, nmatches_map, local_map_points, local_matches, inliers;
+    int need_kf, keyframes, mappoints;
+} orbmi_slam_frame_stats;
+
+typedef struct orbmi_slam orbmi_slam;
+
+/* System(strSettingsFile, STEREO) + Tracking + a synchronous LocalMapping
+ * (src/System.cc:36-107, src/Tracking.cc:53-143, src/LocalMapping.cc:47-128) on `device`: the
+ * map (keyframes, map points, covisibility, spanning tree) is kept natively, every per-keypoint
+ * operator is the MI355X one of this library.  vocabulary (may be NULL: TrackReferenceKeyFrame
+ * then fails with ORBMI_E_STATE) is borrowed and must outlive the handle. */
+int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary* vocabulary, orbmi_slam** out);
+void orbmi_slam_destroy(orbmi_slam* h);
+
+/* System::TrackStereo(imLeft, imRight, timestamp) (src/System.cc:110-159): host u8 gray images
+ * (rows x cols, row pitch step).  tcw_out (16 floats, may be NULL) receives mCurrentFrame.mTcw;
+ * *has_pose = 0 while not initialised / lost (empty Tcw). */
+int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+                            double timestamp, float* tcw_out, int* has_pose);
+
+/* The counters of tracked frame `frame` (0-based). */
+int orbmi_slam_get_stats(orbmi_slam* h, int frame, orbmi_slam_frame_stats* out);
+/* frames tracked, keyframes, non-bad map points, LocalBundleAdjustment calls */
+int orbmi_slam_get_counts(orbmi_slam* h, int* frames, int* keyframes, int* mappoints, int* local_ba_calls);
+/* The poses SaveTrajectoryKITTI / TUM write (src/System.cc:334-486): per recorded frame Tcw =
+ * Tcr * Trw * Two (16 floats), its timestamp and mlbLost.  capacity < n -> ORBMI_E_CAP, *n set. */
+int orbmi_slam_get_trajectory(orbmi_slam* h, float* tcw, double* timestamps, uint8_t* lost, int capacity, int* n);
+/* System::SaveTrajectoryKITTI / SaveTrajectoryTUM / SaveKeyFrameTrajectoryTUM. */
+int orbmi_slam_save_trajectory_kitti(orbmi_slam* h, const char* path);
+int orbmi_slam_save_trajectory_tum(orbmi_slam* h, const char* path);
+int orbmi_slam_save_keyframe_trajectory_tum(orbmi_slam* h, const char* path);
+
 /* ---- per-stage timing (HIP events on the handle's stream) ---------------------------- */
 
 /* Kernel stages of one handle; each is a single kernel launch (resize: one per level). */

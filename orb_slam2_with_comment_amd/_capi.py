@@ -96,6 +96,15 @@ _PROTOS = {
     "orbmi_debug_fast_candidates": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "orbmi_debug_octree_level": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "orbmi_debug_pose_trace": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "orbmi_slam_create": (_i, [_vp, _i, _vp, C.POINTER(_vp)]),
+    "orbmi_slam_destroy": (None, [_vp]),
+    "orbmi_slam_track_stereo": (_i, [_vp, _vp, _vp, _i, _i, _sz, C.c_double, _vp, C.POINTER(_i)]),
+    "orbmi_slam_get_stats": (_i, [_vp, _i, _vp]),
+    "orbmi_slam_get_counts": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
+    "orbmi_slam_get_trajectory": (_i, [_vp, _vp, _vp, _vp, _i, C.POINTER(_i)]),
+    "orbmi_slam_save_trajectory_kitti": (_i, [_vp, C.c_char_p]),
+    "orbmi_slam_save_trajectory_tum": (_i, [_vp, C.c_char_p]),
+    "orbmi_slam_save_keyframe_trajectory_tum": (_i, [_vp, C.c_char_p]),
 }
 
 _lib = None

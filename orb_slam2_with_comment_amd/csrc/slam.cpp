@@ -1,0 +1,1073 @@
+// Native stereo SLAM host loop: System::TrackStereo, the stereo Tracking state machine and a
+// synchronous LocalMapping around the MI355X operators of this library (include/orbmi.h).
+//
+//   System::TrackStereo        -> orbmi_slam_track_stereo         src/System.cc:110-159
+//   Tracking::Track (stereo)   -> Slam::track                     src/Tracking.cc:287-581
+//   StereoInitialization       -> Slam::stereo_initialization     src/Tracking.cc:584-636
+//   TrackReferenceKeyFrame     -> Slam::track_reference_kf        src/Tracking.cc:871-917
+//   TrackWithMotionModel       -> Slam::track_motion_model        src/Tracking.cc:997-1063
+//   TrackLocalMap, UpdateLocalKeyFrames / Points, SearchLocalPoints src/Tracking.cc:1075-1104, 1345-1580
+//   NeedNewKeyFrame / CreateNewKeyFrame                           src/Tracking.cc:1140-1330
+//   LocalMapping::ProcessNewKeyFrame + LocalBundleAdjustment      src/LocalMapping.cc:152-200, :89-90
+//   KeyFrame::UpdateConnections, MapPoint bookkeeping             src/KeyFrame.cc, src/MapPoint.cc
+//   Optimizer::LocalBundleAdjustment's graph assembly             src/Optimizer.cc:486-683
+//   System::SaveTrajectoryKITTI / TUM / SaveKeyFrameTrajectoryTUM src/System.cc:334-486
+//
+// The same host logic as orb_slam2_with_comment_amd/system.py (which the tests also drive with
+// the CPU oracle behind it); this native form is what --mode system measures.  Pose algebra in
+// float32 with double accumulation (cv::Mat CV_32F products, src/Converter.cc); the
+// deterministic replacements of the reference's pointer-ordered containers are the Python
+// module's: keyframe-id order for std::map<KeyFrame*, ...>, covisibility ties to the higher id.
+// Compiled with -ffp-contract=off: one rounding per float operation, as numpy does.
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <set>
+#include <utility>
+#include <vector>
+
+#include "../../include/orbmi.h"
+
+namespace {
+
+using M4 = std::array<float, 16>;
+
+M4 eye4() {
+    M4 m{};
+    m[0] = m[5] = m[10] = m[15] = 1.f;
+    return m;
+}
+
+// float32(float64(a) @ float64(b)), 4x4 row-major
+M4 mul(const M4& a, const M4& b) {
+    M4 o;
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            double s = 0;
+            for (int k = 0; k < 4; k++) s += (double)a[4 * r + k] * (double)b[4 * k + c];
+            o[4 * r + c] = (float)s;
+        }
+    return o;
+}
+
+// Frame::UpdatePoseMatrices: Rwc = Rcw^T, Ow = -Rwc tcw; Twc as a 4x4
+M4 pose_inverse(const M4& T) {
+    M4 o = eye4();
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) o[4 * r + c] = T[4 * c + r];
+    for (int r = 0; r < 3; r++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += (double)o[4 * r + k] * (double)T[4 * k + 3];
+        o[4 * r + 3] = -(float)s;
+    }
+    return o;
+}
+
+void camera_center(const M4& T, float ow[3]) {
+    const M4 i = pose_inverse(T);
+    ow[0] = i[3]; ow[1] = i[7]; ow[2] = i[11];
+}
+
+// Converter::toQuaternion (src/Converter.cc:137-149): Eigen::Quaterniond(Matrix3d) -> x y z w
+void quaternion_xyzw(const float R[9], float q_out[4]) {
+    double m[3][3], q[4] = {0, 0, 0, 0};
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) m[r][c] = R[3 * r + c];
+    double t = m[0][0] + m[1][1] + m[2][2];
+    if (t > 0) {
+        t = std::sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[2][1] - m[1][2]) * t;
+        q[1] = (m[0][2] - m[2][0]) * t;
+        q[2] = (m[1][0] - m[0][1]) * t;
+    } else {
+        int i = m[1][1] > m[0][0] ? 1 : 0;
+        if (m[2][2] > m[i][i]) i = 2;
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        t = std::sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k][j] - m[j][k]) * t;
+        q[j] = (m[j][i] + m[i][j]) * t;
+        q[k] = (m[k][i] + m[i][k]) * t;
+    }
+    for (int k = 0; k < 4; k++) q_out[k] = (float)q[k];
+}
+
+// DBoW2::FeatureVector as CSR (orbmi_feature_vector)
+struct FeatVec {
+    bool valid = false;
+    std::vector<uint32_t> node;
+    std::vector<int32_t> off, feat;
+    orbmi_feature_vector view() const {
+        return orbmi_feature_vector{(int)node.size(), node.data(), off.data(), feat.data()};
+    }
+};
+
+struct KeyFrame {
+    int id = 0, frame_id = 0;
+    double ts = 0;
+    M4 tcw{};
+    std::vector<orbmi_keypoint> keys;
+    std::vector<uint8_t> desc;
+    std::vector<float> ur, depth;
+    std::vector<int> mps;        // map point id per keypoint, -1 = NULL
+    FeatVec fv;
+    std::vector<int> covisible;  // mvpOrderedConnectedKeyFrames
+    std::map<int, int> conn;     // mConnectedKeyFrameWeights (keyframe id order)
+    int parent = -1;
+    std::vector<int> children;
+    bool first_connection = true;
+    bool bad = false;
+};
+
+struct MapPoint {
+    int id = 0;
+    float pos[3] = {0, 0, 0};
+    int ref_kf = -1;
+    uint8_t desc[32] = {};
+    float normal[3] = {0, 0, 0};
+    float max_distance = 0, min_distance = 0;
+    std::map<int, int> obs;      // keyframe id -> keypoint index (keyframe id order)
+    int nobs = 0;
+    bool bad = false;
+};
+
+struct TrackedFrame {
+    int id = 0;
+    double ts = 0;
+    std::vector<orbmi_keypoint> keys;
+    std::vector<uint8_t> desc;
+    std::vector<float> ur, depth;
+    bool has_tcw = false;
+    M4 tcw{};
+    std::vector<int> mps;        // mvpMapPoints (map point ids, -1)
+    std::vector<uint8_t> outlier;
+    int ref_kf = -1;
+    FeatVec fv;
+    int n() const { return (int)keys.size(); }
+};
+
+enum { NO_IMAGES_YET = 0, NOT_INITIALIZED = 1, OK = 2, LOST = 3 };
+
+#define SLAM_CHECK(call)              \
+    do {                              \
+        const int rc_ = (call);       \
+        if (rc_ != ORBMI_OK) return rc_; \
+    } while (0)
+
+}  // namespace
+
+struct orbmi_slam {
+    orbmi_slam_settings s{};
+    int device = 0;
+    orbmi_extractor* left = nullptr;
+    orbmi_extractor* right = nullptr;
+    orbmi_matcher* matcher = nullptr;
+    orbmi_pose* pose = nullptr;
+    orbmi_ba* ba = nullptr;
+    orbmi_vocabulary* voc = nullptr;
+    std::vector<float> scale_factors, inv_level_sigma2;
+    float log_scale_factor = 0;
+
+    int state = NO_IMAGES_YET;
+    std::vector<KeyFrame> kfs;   // index = keyframe id
+    std::vector<MapPoint> mps;   // index = map point id
+    int frame_count = 0;
+    TrackedFrame last_frame;
+    bool have_last = false;
+    bool has_velocity = false;
+    M4 velocity{};
+    int ref_kf = -1;
+    int last_kf_frame_id = 0, last_reloc_frame_id = 0;
+    std::vector<int> local_kfs, local_mps;
+    int matches_inliers = 0;
+    std::set<int> seen;          // mnLastFrameSeen == current frame
+    // mlRelativeFramePoses, mlpReferences, mlFrameTimes, mlbLost
+    std::vector<M4> rel_poses;
+    std::vector<int> references;
+    std::vector<double> frame_times;
+    std::vector<uint8_t> lost;
+    std::vector<orbmi_slam_frame_stats> stats;
+    int ba_calls = 0;
+    // extraction scratch
+    std::vector<orbmi_keypoint> kbuf;
+    std::vector<uint8_t> dbuf;
+
+    // ---- Frame views (include/Frame.h members the matchers read) --------------------------
+    orbmi_frame_view view(const std::vector<orbmi_keypoint>& keys, const std::vector<uint8_t>& desc,
+                          const std::vector<float>& ur, const float* tcw) const {
+        orbmi_frame_view v{};
+        v.n = (int)keys.size();
+        v.keys_un = keys.data();
+        v.u_right = ur.data();
+        v.desc = desc.data();
+        v.tcw = tcw;
+        v.fx = s.fx; v.fy = s.fy; v.cx = s.cx; v.cy = s.cy; v.bf = s.bf;
+        v.mb = s.bf / s.fx;
+        v.min_x = 0.f; v.max_x = (float)s.width; v.min_y = 0.f; v.max_y = (float)s.height;  // no distortion
+        v.grid_w_inv = 64.f / (float)s.width;
+        v.grid_h_inv = 48.f / (float)s.height;
+        v.nlevels = (int)scale_factors.size();
+        v.scale_factors = scale_factors.data();
+        v.log_scale_factor = log_scale_factor;
+        v.n_device = nullptr;
+        return v;
+    }
+    orbmi_frame_view view(const TrackedFrame& f, const float* tcw) const { return view(f.keys, f.desc, f.ur, tcw); }
+
+    // ---- backend operators ------------------------------------------------------------------
+    int extract(orbmi_extractor* ex, const uint8_t* img, int rows, int cols, size_t step, std::vector<orbmi_keypoint>& k,
+                std::vector<uint8_t>& d) {
+        int cap = s.n_features + 16 * s.n_levels + 64, n = 0;
+        for (;;) {
+            kbuf.resize(cap);
+            dbuf.resize((size_t)cap * 32);
+            const int rc = orbmi_extract(ex, img, rows, cols, step, kbuf.data(), dbuf.data(), cap, &n);
+            if (rc == ORBMI_E_CAP) { cap = n; continue; }
+            SLAM_CHECK(rc);
+            break;
+        }
+        k.assign(kbuf.begin(), kbuf.begin() + n);
+        d.assign(dbuf.begin(), dbuf.begin() + (size_t)n * 32);
+        return ORBMI_OK;
+    }
+
+    int compute_bow(const std::vector<uint8_t>& desc, FeatVec& fv) {
+        if (!voc) return ORBMI_E_STATE;  // TrackReferenceKeyFrame needs the vocabulary
+        const int n = (int)(desc.size() / 32), cap = std::max(n, 1);
+        std::vector<uint32_t> word(cap), node(cap);
+        std::vector<double> value(cap);
+        std::vector<int32_t> off(cap + 1), feat(cap);
+        int counts[2] = {0, 0};
+        SLAM_CHECK(orbmi_transform(voc, desc.data(), n, nullptr, 4, word.data(), value.data(), node.data(), off.data(),
+                                   feat.data(), counts));
+        const int nn = counts[1];
+        fv.node.assign(node.begin(), node.begin() + nn);
+        fv.off.assign(off.begin(), off.begin() + nn + 1);
+        fv.feat.assign(feat.begin(), feat.begin() + off[nn]);
+        fv.valid = true;
+        return ORBMI_OK;
+    }
+
+    // Optimizer::PoseOptimization over keypoint i -> lfp[match[i]] (match[i] >= 0)
+    int pose_optimization(const TrackedFrame& cf, const std::vector<int32_t>& match,
+                          const std::vector<orbmi_lastframe_point>& lfp, M4& tcw_out, std::vector<uint8_t>& out) {
+        orbmi_frame_view v = view(cf, cf.tcw.data());
+        orbmi_frame_mappoints fm{};
+        fm.match_lf = const_cast<int32_t*>(match.data());
+        fm.lf_points = lfp.data();
+        fm.n_lf_points = (int)lfp.size();
+        orbmi_pose_frame rec{};
+        out.assign(std::max(cf.n(), 1), 0);
+        SLAM_CHECK(orbmi_pose_optimization_frame(pose, &v, inv_level_sigma2.data(), &fm, &rec, out.data()));
+        std::memcpy(tcw_out.data(), rec.tcw, sizeof(rec.tcw));
+        out.resize(cf.n());
+        return ORBMI_OK;
+    }
+
+    // ---- map model ----------------------------------------------------------------------------
+    void kf_ow(int k, float ow[3]) const { camera_center(kfs[k].tcw, ow); }
+
+    int tracked_map_points(const KeyFrame& kf, int min_obs) const {  // KeyFrame::TrackedMapPoints
+        int n = 0;
+        for (int m : kf.mps)
+            if (m >= 0 && !mps[m].bad && (min_obs <= 0 || mps[m].nobs >= min_obs)) n++;
+        return n;
+    }
+
+    void sort_covisible(KeyFrame& kf) {  // heaviest first, ties to the higher id
+        std::vector<std::pair<int, int>> p;
+        for (auto& c : kf.conn) p.push_back({c.second, c.first});
+        std::sort(p.begin(), p.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+            return a.first != b.first ? a.first > b.first : a.second > b.second;
+        });
+        kf.covisible.clear();
+        for (auto& x : p) kf.covisible.push_back(x.second);
+    }
+
+    void add_connection(int k, int other, int w) {  // KeyFrame::AddConnection + UpdateBestCovisibles
+        kfs[k].conn[other] = w;
+        sort_covisible(kfs[k]);
+    }
+
+    void update_connections(int k) {  // KeyFrame::UpdateConnections (src/KeyFrame.cc:285-371)
+        std::map<int, int> counter;
+        for (int m : kfs[k].mps) {
+            if (m < 0 || mps[m].bad) continue;
+            for (auto& o : mps[m].obs)
+                if (o.first != k) counter[o.first]++;
+        }
+        if (counter.empty()) return;
+        const int th = 15;
+        int nmax = 0, kfmax = -1;
+        std::vector<std::pair<int, int>> pairs;  // (w, id)
+        for (auto& c : counter) {
+            const int w = c.second;
+            if (w > nmax) { nmax = w; kfmax = c.first; }
+            if (w >= th) {
+                pairs.push_back({w, c.first});
+                add_connection(c.first, k, w);
+            }
+        }
+        if (pairs.empty()) {
+            pairs.push_back({nmax, kfmax});
+            add_connection(kfmax, k, nmax);
+        }
+        std::sort(pairs.begin(), pairs.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+            return a.first != b.first ? a.first > b.first : a.second > b.second;
+        });
+        KeyFrame& kf = kfs[k];
+        kf.conn = counter;
+        kf.covisible.clear();
+        for (auto& p : pairs) kf.covisible.push_back(p.second);
+        if (kf.first_connection && kf.id != 0) {
+            kf.parent = kf.covisible[0];
+            kfs[kf.parent].children.push_back(k);
+            kf.first_connection = false;
+        }
+    }
+
+    void add_observation(int m, int k, int idx) {  // MapPoint::AddObservation
+        MapPoint& mp = mps[m];
+        if (mp.obs.count(k)) return;
+        mp.obs[k] = idx;
+        mp.nobs += kfs[k].ur[idx] >= 0 ? 2 : 1;
+    }
+
+    void set_bad(int m) {  // MapPoint::SetBadFlag
+        MapPoint& mp = mps[m];
+        mp.bad = true;
+        for (auto& o : mp.obs)
+            if (kfs[o.first].mps[o.second] == m) kfs[o.first].mps[o.second] = -1;
+        mp.obs.clear();
+    }
+
+    void erase_observation(int m, int k) {  // MapPoint::EraseObservation
+        MapPoint& mp = mps[m];
+        auto it = mp.obs.find(k);
+        if (it == mp.obs.end()) return;
+        const int idx = it->second;
+        mp.obs.erase(it);
+        mp.nobs -= kfs[k].ur[idx] >= 0 ? 2 : 1;
+        if (mp.ref_kf == k && !mp.obs.empty()) mp.ref_kf = mp.obs.begin()->first;  // lowest id
+        if (mp.nobs <= 2) set_bad(m);
+    }
+
+    // MapPoint::UpdateNormalAndDepth (src/MapPoint.cc:339-390), float32 arithmetic as
+    // system.update_normals_and_depths (observing keyframes in id order)
+    void update_normal_and_depth(int m) {
+        MapPoint& mp = mps[m];
+        if (mp.bad || mp.obs.empty()) return;
+        float normal[3] = {0, 0, 0};
+        for (auto& o : mp.obs) {
+            float ow[3];
+            kf_ow(o.first, ow);
+            const float v[3] = {mp.pos[0] - ow[0], mp.pos[1] - ow[1], mp.pos[2] - ow[2]};
+            const double n2 = ((double)v[0] * v[0] + (double)v[1] * v[1]) + (double)v[2] * v[2];
+            const double inv = 1.0 / std::sqrt(n2);
+            for (int r = 0; r < 3; r++) normal[r] = normal[r] + (float)((double)v[r] * inv);
+        }
+        const double ic = 1.0 / (double)mp.obs.size();
+        for (int r = 0; r < 3; r++) mp.normal[r] = (float)((double)normal[r] * ic);
+        float ow[3];
+        kf_ow(mp.ref_kf, ow);
+        const float pc[3] = {mp.pos[0] - ow[0], mp.pos[1] - ow[1], mp.pos[2] - ow[2]};
+        const float dist = (float)std::sqrt(((double)pc[0] * pc[0] + (double)pc[1] * pc[1]) + (double)pc[2] * pc[2]);
+        const KeyFrame& rk = kfs[mp.ref_kf];
+        const int level = rk.keys[mp.obs.at(mp.ref_kf)].octave;
+        mp.max_distance = dist * scale_factors[level];
+        mp.min_distance = mp.max_distance / scale_factors[scale_factors.size() - 1];
+    }
+
+    // MapPoint::ComputeDistinctiveDescriptors for a batch of points (src/MapPoint.cc:247-316)
+    int distinctive(const std::vector<int>& pts) {
+        std::vector<uint8_t> rows;
+        std::vector<int32_t> off{0};
+        for (int m : pts) {
+            for (auto& o : mps[m].obs)
+                if (!kfs[o.first].bad) rows.insert(rows.end(), &kfs[o.first].desc[32 * o.second], &kfs[o.first].desc[32 * o.second] + 32);
+            off.push_back((int32_t)(rows.size() / 32));
+        }
+        if (rows.empty()) return ORBMI_OK;
+        const int np = (int)pts.size();
+        std::vector<int32_t> best(std::max(np, 1));
+        std::vector<uint8_t> out((size_t)std::max(np, 1) * 32);
+        SLAM_CHECK(orbmi_compute_distinctive_descriptors(matcher, rows.data(), off.data(), np, best.data(), out.data()));
+        for (int j = 0; j < np; j++)
+            if (off[j + 1] > off[j]) std::memcpy(mps[pts[j]].desc, &out[32 * j], 32);
+        return ORBMI_OK;
+    }
+
+    // ---- keyframes and map points -------------------------------------------------------------
+    int new_keyframe(const TrackedFrame& cf) {
+        KeyFrame kf;
+        kf.id = (int)kfs.size();
+        kf.frame_id = cf.id;
+        kf.ts = cf.ts;
+        kf.tcw = cf.tcw;
+        kf.keys = cf.keys;
+        kf.desc = cf.desc;
+        kf.ur = cf.ur;
+        kf.depth = cf.depth;
+        kf.mps = cf.mps;
+        kf.fv = cf.fv;
+        kfs.push_back(std::move(kf));
+        return (int)kfs.size() - 1;
+    }
+
+    // Frame::UnprojectStereo (src/Frame.cc:701-715) + new MapPoint + AddObservation + AddMapPoint
+    // + UpdateNormalAndDepth (src/Tracking.cc:602-616, :1308-1320)
+    void create_points(int k, TrackedFrame& cf, const std::vector<int>& idx) {
+        if (idx.empty()) return;
+        const float invfx = 1.f / s.fx, invfy = 1.f / s.fy;
+        const M4 twc = pose_inverse(cf.tcw);
+        std::vector<int> made;
+        for (int i : idx) {
+            const float z = cf.depth[i];
+            const float x = (cf.keys[i].x - s.cx) * z * invfx;
+            const float y = (cf.keys[i].y - s.cy) * z * invfy;
+            MapPoint mp;
+            mp.id = (int)mps.size();
+            for (int r = 0; r < 3; r++) {
+                const double a = (double)twc[4 * r] * (double)x + (double)twc[4 * r + 1] * (double)y +
+                                 (double)twc[4 * r + 2] * (double)z;
+                mp.pos[r] = (float)a + twc[4 * r + 3];
+            }
+            mp.ref_kf = k;
+            std::memcpy(mp.desc, &cf.desc[32 * i], 32);  // ComputeDistinctiveDescriptors of one observation
+            mps.push_back(mp);
+            add_observation(mp.id, k, i);
+            kfs[k].mps[i] = mp.id;
+            cf.mps[i] = mp.id;
+            made.push_back(mp.id);
+        }
+        for (int m : made) update_normal_and_depth(m);
+    }
+
+    int stereo_initialization(TrackedFrame& cf) {  // src/Tracking.cc:584-636
+        if (cf.n() <= 500) return ORBMI_OK;
+        cf.tcw = eye4();
+        cf.has_tcw = true;
+        const int k = new_keyframe(cf);
+        std::vector<int> idx;
+        for (int i = 0; i < cf.n(); i++)
+            if (cf.depth[i] > 0) idx.push_back(i);
+        create_points(k, cf, idx);
+        SLAM_CHECK(local_mapping(k));
+        last_kf_frame_id = cf.id;
+        local_kfs = {k};
+        local_mps.clear();
+        for (auto& m : mps)
+            if (!m.bad) local_mps.push_back(m.id);
+        ref_kf = k;
+        cf.ref_kf = k;
+        state = OK;
+        return ORBMI_OK;
+    }
+
+    bool need_new_keyframe(const TrackedFrame& cf, orbmi_slam_frame_stats& st) {  // src/Tracking.cc:1140-1249
+        const int nkfs = (int)kfs.size();
+        if (cf.id < last_reloc_frame_id + s.max_frames && nkfs > s.max_frames) return false;
+        const int min_obs = nkfs <= 2 ? 2 : 3;
+        const int n_ref = tracked_map_points(kfs[ref_kf], min_obs);
+        int n_tracked_close = 0, n_non_tracked_close = 0;
+        for (int i = 0; i < cf.n(); i++) {
+            if (!(cf.depth[i] > 0 && cf.depth[i] < s.th_depth)) continue;
+            if (cf.mps[i] >= 0 && !cf.outlier[i]) n_tracked_close++;
+            else n_non_tracked_close++;
+        }
+        const bool need_close = n_tracked_close < 100 && n_non_tracked_close > 70;
+        const float th_ref = nkfs < 2 ? 0.4f : 0.75f;
+        const bool c1a = cf.id >= last_kf_frame_id + s.max_frames;
+        const bool c1b = cf.id >= last_kf_frame_id + s.min_frames;  // LocalMapping idle (synchronous)
+        const bool c1c = matches_inliers < n_ref * 0.25 || need_close;
+        const bool c2 = ((float)matches_inliers < (float)n_ref * th_ref || need_close) && matches_inliers > 15;
+        st.need_kf = (c1a || c1b || c1c) && c2;
+        return st.need_kf != 0;
+    }
+
+    int create_new_keyframe(TrackedFrame& cf) {  // src/Tracking.cc:1251-1330
+        const int k = new_keyframe(cf);
+        ref_kf = k;
+        cf.ref_kf = k;
+        std::vector<std::pair<float, int>> order;
+        for (int i = 0; i < cf.n(); i++)
+            if (cf.depth[i] > 0) order.push_back({cf.depth[i], i});
+        std::sort(order.begin(), order.end());
+        std::vector<int> fresh;
+        int npts = 0;
+        for (auto& zi : order) {
+            const int i = zi.second;
+            const int m = cf.mps[i];
+            const bool create = m < 0 || mps[m].nobs < 1;
+            if (create && m >= 0) {
+                cf.mps[i] = -1;
+                kfs[k].mps[i] = -1;
+            }
+            if (create) fresh.push_back(i);
+            npts++;
+            if (zi.first > s.th_depth && npts > 100) break;
+        }
+        create_points(k, cf, fresh);
+        SLAM_CHECK(local_mapping(k));
+        last_kf_frame_id = cf.id;
+        return ORBMI_OK;
+    }
+
+    // ---- LocalMapping (synchronous) -------------------------------------------------------------
+    int local_mapping(int k) {  // ProcessNewKeyFrame (src/LocalMapping.cc:152-200) + LocalBA (:89-90)
+        if (voc && !kfs[k].fv.valid) SLAM_CHECK(compute_bow(kfs[k].desc, kfs[k].fv));
+        std::vector<int> updated;
+        for (int i = 0; i < (int)kfs[k].mps.size(); i++) {
+            const int m = kfs[k].mps[i];
+            if (m < 0 || mps[m].bad) continue;
+            if (!mps[m].obs.count(k)) {
+                add_observation(m, k, i);
+                updated.push_back(m);
+            }
+        }
+        for (int m : updated) update_normal_and_depth(m);
+        SLAM_CHECK(distinctive(updated));
+        update_connections(k);
+        if (s.local_ba && kfs.size() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+        return ORBMI_OK;
+    }
+
+    // Optimizer::LocalBundleAdjustment: the graph as src/Optimizer.cc:486-683 assembles it
+    // (system/optimizer.gather_local_ba), the optimisation on the GPU, the write-back (:776-805)
+    int local_bundle_adjustment(int k) {
+        std::vector<int> lkf{k};
+        std::set<int> local_set{k};
+        for (int c : kfs[k].covisible) {
+            local_set.insert(c);
+            if (!kfs[c].bad) lkf.push_back(c);
+        }
+        std::vector<int> lmp;
+        std::set<int> seen_mp;
+        for (int kk : lkf)
+            for (int m : kfs[kk].mps)
+                if (m >= 0 && !mps[m].bad && seen_mp.insert(m).second) lmp.push_back(m);
+        std::vector<int> fixed;
+        std::set<int> fixed_set;
+        for (int m : lmp)
+            for (auto& o : mps[m].obs)
+                if (!local_set.count(o.first) && fixed_set.insert(o.first).second && !kfs[o.first].bad)
+                    fixed.push_back(o.first);
+        std::vector<int> all = lkf;
+        all.insert(all.end(), fixed.begin(), fixed.end());
+        std::map<int, int> kidx;
+        for (int i = 0; i < (int)all.size(); i++) kidx[all[i]] = i;
+        std::vector<orbmi_ba_keyframe> K(all.size());
+        for (int i = 0; i < (int)all.size(); i++) {
+            const KeyFrame& kf = kfs[all[i]];
+            std::memcpy(K[i].tcw, kf.tcw.data(), sizeof(K[i].tcw));
+            K[i].id = (uint32_t)kf.id;
+            K[i].fixed = (i >= (int)lkf.size() || kf.id == 0) ? 1 : 0;
+            K[i].fx = s.fx; K[i].fy = s.fy; K[i].cx = s.cx; K[i].cy = s.cy; K[i].bf = s.bf;
+        }
+        std::vector<orbmi_ba_point> P(lmp.size());
+        for (int j = 0; j < (int)lmp.size(); j++) {
+            const MapPoint& mp = mps[lmp[j]];
+            std::memcpy(P[j].pos, mp.pos, sizeof(P[j].pos));
+            P[j].id = (uint32_t)mp.id;
+            P[j].bad = mp.bad ? 1 : 0;
+        }
+        std::vector<orbmi_ba_edge> E;
+        std::vector<std::pair<int, int>> e_ref;  // (map point id, keyframe id) per edge
+        for (int j = 0; j < (int)lmp.size(); j++)
+            for (auto& o : mps[lmp[j]].obs) {
+                auto it = kidx.find(o.first);
+                if (kfs[o.first].bad || it == kidx.end()) continue;
+                const KeyFrame& kf = kfs[o.first];
+                const orbmi_keypoint& kp = kf.keys[o.second];
+                E.push_back(orbmi_ba_edge{j, it->second, kp.x, kp.y, kf.ur[o.second], inv_level_sigma2[kp.octave]});
+                e_ref.push_back({lmp[j], o.first});
+            }
+        if (E.empty()) return ORBMI_OK;
+        orbmi_ba_problem prob{(int)K.size(), (int)P.size(), (int)E.size(), K.data(), P.data(), E.data()};
+        std::vector<float> tcw(K.size() * 16), pos(P.size() * 3 + 3);
+        std::vector<uint8_t> erase(E.size());
+        orbmi_ba_result res{};
+        res.tcw = tcw.data();
+        res.pos = pos.data();
+        res.erase = erase.data();
+        SLAM_CHECK(orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr));
+        ba_calls++;
+        for (size_t e = 0; e < E.size(); e++) {
+            if (!erase[e]) continue;
+            const int m = e_ref[e].first, kk = e_ref[e].second;
+            auto it = mps[m].obs.find(kk);
+            if (it != mps[m].obs.end() && kfs[kk].mps[it->second] == m) kfs[kk].mps[it->second] = -1;  // EraseMapPointMatch
+            erase_observation(m, kk);
+        }
+        int n_local = 1;
+        for (int c : kfs[k].covisible)
+            if (!kfs[c].bad) n_local++;
+        for (int i = 0; i < n_local; i++) std::memcpy(kfs[all[i]].tcw.data(), &tcw[16 * i], 16 * sizeof(float));
+        for (int j = 0; j < (int)lmp.size(); j++) std::memcpy(mps[lmp[j]].pos, &pos[3 * j], 3 * sizeof(float));
+        for (int m : lmp) update_normal_and_depth(m);
+        return ORBMI_OK;
+    }
+
+    // ---- tracking stages ----------------------------------------------------------------------
+    std::vector<orbmi_mappoint> mp_records(const std::vector<int>& pts) const {
+        std::vector<orbmi_mappoint> rec(pts.size());
+        for (size_t j = 0; j < pts.size(); j++) {
+            const MapPoint& mp = mps[pts[j]];
+            orbmi_mappoint& r = rec[j];
+            std::memcpy(r.pos, mp.pos, sizeof(r.pos));
+            std::memcpy(r.normal, mp.normal, sizeof(r.normal));
+            r.max_distance = mp.max_distance;
+            r.min_distance = mp.min_distance;
+            r.flags = (mp.bad ? ORBMI_MP_BAD : 0u) | (seen.count(mp.id) ? ORBMI_MP_SEEN : 0u) |
+                      (mp.nobs > 0 ? ORBMI_MP_HAS_OBS : 0u);
+            std::memcpy(r.desc, mp.desc, 32);
+        }
+        return rec;
+    }
+
+    std::vector<orbmi_lastframe_point> lf_records(const std::vector<int>& lf_mps, const std::vector<uint8_t>* outlier) const {
+        std::vector<orbmi_lastframe_point> rec(std::max<size_t>(lf_mps.size(), 1));
+        std::memset(rec.data(), 0, rec.size() * sizeof(orbmi_lastframe_point));
+        for (size_t i = 0; i < lf_mps.size(); i++) {
+            const int m = lf_mps[i];
+            if (m < 0) continue;
+            std::memcpy(rec[i].pos, mps[m].pos, sizeof(rec[i].pos));
+            std::memcpy(rec[i].desc, mps[m].desc, 32);
+            rec[i].flags = ORBMI_LF_HAS_MP | (mps[m].nobs > 0 ? ORBMI_MP_HAS_OBS : 0u) |
+                           (outlier && (*outlier)[i] ? ORBMI_LF_OUTLIER : 0u);
+        }
+        rec.resize(lf_mps.size());
+        return rec;
+    }
+
+    int discard_outliers(TrackedFrame& cf, const std::vector<uint8_t>& outlier) {  // -> nmatchesMap
+        int nmap = 0;
+        for (int i = 0; i < cf.n(); i++) {
+            const int m = cf.mps[i];
+            if (m < 0) continue;
+            if (outlier[i]) {
+                cf.mps[i] = -1;
+                cf.outlier[i] = 0;
+                seen.insert(m);  // pMP->mnLastFrameSeen = mCurrentFrame.mnId
+            } else if (mps[m].nobs > 0) {
+                nmap++;
+            }
+        }
+        return nmap;
+    }
+
+    int track_reference_kf(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:871-917
+        ok = false;
+        SLAM_CHECK(compute_bow(cf.desc, cf.fv));
+        KeyFrame& kf = kfs[ref_kf];
+        if (!kf.fv.valid) SLAM_CHECK(compute_bow(kf.desc, kf.fv));
+        std::vector<uint8_t> ok_mp(std::max<size_t>(kf.mps.size(), 1), 0);
+        for (size_t j = 0; j < kf.mps.size(); j++) ok_mp[j] = kf.mps[j] >= 0 && !mps[kf.mps[j]].bad;
+        const orbmi_frame_view vk = view(kf.keys, kf.desc, kf.ur, kf.tcw.data());
+        const M4 I = eye4();
+        const orbmi_frame_view vf = view(cf, I.data());
+        const orbmi_feature_vector fk = kf.fv.view(), ff = cf.fv.view();
+        std::vector<int32_t> m(std::max(cf.n(), 1));
+        int n = 0;
+        SLAM_CHECK(orbmi_search_by_bow(matcher, &vk, ok_mp.data(), &fk, &vf, &ff, 0.7f, 1, m.data(), &n));
+        st.bow_matches = n;
+        st.track = 2;
+        if (n < 15) return ORBMI_OK;
+        for (int i = 0; i < cf.n(); i++) cf.mps[i] = m[i] >= 0 ? kf.mps[m[i]] : -1;
+        cf.tcw = last_frame.tcw;
+        cf.has_tcw = true;
+        const std::vector<orbmi_lastframe_point> lfp = lf_records(kf.mps, nullptr);
+        m.resize(cf.n());
+        M4 tcw;
+        std::vector<uint8_t> out;
+        SLAM_CHECK(pose_optimization(cf, m, lfp, tcw, out));
+        cf.tcw = tcw;
+        cf.outlier = out;
+        seen.clear();
+        const int nmap = discard_outliers(cf, out);
+        st.nmatches_map = nmap;
+        ok = nmap >= 10;
+        return ORBMI_OK;
+    }
+
+    int track_motion_model(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:997-1063
+        ok = false;
+        TrackedFrame& lf = last_frame;
+        lf.tcw = mul(rel_poses.back(), kfs[lf.ref_kf].tcw);  // UpdateLastFrame (pose only, SLAM mode)
+        cf.tcw = mul(velocity, lf.tcw);
+        cf.has_tcw = true;
+        const std::vector<orbmi_lastframe_point> lfp = lf_records(lf.mps, &lf.outlier);
+        std::vector<uint8_t> occ(std::max(cf.n(), 1), 0);
+        const orbmi_frame_view vc = view(cf, cf.tcw.data()), vl = view(lf, lf.tcw.data());
+        std::vector<int32_t> m(std::max(cf.n(), 1));
+        int n = 0;
+        const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
+        SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1, m.data(), &n));
+        if (n < 20)
+            SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), 2 * th, 0, 1,
+                                                             m.data(), &n));
+        st.track = 1;
+        st.lf_matches = n;
+        if (n < 20) return ORBMI_OK;
+        for (int i = 0; i < cf.n(); i++) cf.mps[i] = m[i] >= 0 ? lf.mps[m[i]] : -1;
+        m.resize(cf.n());
+        M4 tcw;
+        std::vector<uint8_t> out;
+        SLAM_CHECK(pose_optimization(cf, m, lfp, tcw, out));
+        cf.tcw = tcw;
+        cf.outlier = out;
+        seen.clear();
+        const int nmap = discard_outliers(cf, out);
+        st.nmatches_map = nmap;
+        ok = nmap >= 10;
+        return ORBMI_OK;
+    }
+
+    void update_local_keyframes(TrackedFrame& cf) {  // src/Tracking.cc:1452-1580
+        std::map<int, int> counter;
+        for (int i = 0; i < cf.n(); i++) {
+            const int m = cf.mps[i];
+            if (m < 0) continue;
+            if (mps[m].bad) { cf.mps[i] = -1; continue; }
+            for (auto& o : mps[m].obs) counter[o.first]++;
+        }
+        if (counter.empty()) return;
+        int best = 0, kfmax = -1;
+        std::vector<int> local;
+        std::set<int> mark;
+        for (auto& c : counter) {
+            if (kfs[c.first].bad) continue;
+            if (c.second > best) { best = c.second; kfmax = c.first; }
+            local.push_back(c.first);
+            mark.insert(c.first);
+        }
+        size_t i = 0;
+        while (i < local.size()) {
+            if (local.size() > 80) break;
+            const int k = local[i++];
+            const std::vector<int> cov(kfs[k].covisible.begin(),
+                                       kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
+            for (int nb : cov)
+                if (!kfs[nb].bad && !mark.count(nb)) { local.push_back(nb); mark.insert(nb); break; }
+            std::vector<int> ch = kfs[k].children;
+            std::sort(ch.begin(), ch.end());
+            for (int c : ch)
+                if (!kfs[c].bad && !mark.count(c)) { local.push_back(c); mark.insert(c); break; }
+            const int p = kfs[k].parent;
+            if (p >= 0 && !mark.count(p)) {
+                local.push_back(p);
+                mark.insert(p);
+                break;
+            }
+        }
+        local_kfs = local;
+        if (kfmax >= 0) {
+            ref_kf = kfmax;
+            cf.ref_kf = kfmax;
+        }
+    }
+
+    void update_local_points() {  // src/Tracking.cc:1421-1450
+        std::vector<int> out;
+        std::set<int> mark;
+        for (int k : local_kfs)
+            for (int m : kfs[k].mps)
+                if (m >= 0 && !mark.count(m) && !mps[m].bad) {
+                    out.push_back(m);
+                    mark.insert(m);
+                }
+        local_mps = out;
+    }
+
+    int track_local_map(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:1075-1104
+        ok = false;
+        update_local_keyframes(cf);
+        update_local_points();
+        std::vector<uint8_t> occ(std::max(cf.n(), 1), 0);
+        for (int i = 0; i < cf.n(); i++) {  // SearchLocalPoints' first loop
+            const int m = cf.mps[i];
+            if (m < 0) continue;
+            if (mps[m].bad) cf.mps[i] = -1;
+            else {
+                seen.insert(m);
+                occ[i] = mps[m].nobs > 0 ? 1 : 0;
+            }
+        }
+        const std::vector<orbmi_mappoint> rec = mp_records(local_mps);
+        const orbmi_frame_view vc = view(cf, cf.tcw.data());
+        std::vector<int32_t> m_mp(std::max(cf.n(), 1));
+        int nl = 0, ntm = 0;
+        SLAM_CHECK(orbmi_search_local_points(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f, m_mp.data(), &nl,
+                                             &ntm));
+        st.local_map_points = (int)local_mps.size();
+        st.local_matches = nl;
+        std::vector<int> cur = cf.mps;
+        for (int i = 0; i < cf.n(); i++)
+            if (m_mp[i] >= 0) cur[i] = local_mps[m_mp[i]];
+        const std::vector<orbmi_lastframe_point> lfp = lf_records(cur, nullptr);
+        std::vector<int32_t> m_lf(cf.n(), -1);
+        for (int i = 0; i < cf.n(); i++)
+            if (cur[i] >= 0) m_lf[i] = i;
+        M4 tcw;
+        std::vector<uint8_t> out;
+        SLAM_CHECK(pose_optimization(cf, m_lf, lfp, tcw, out));
+        cf.tcw = tcw;
+        cf.mps = cur;
+        cf.outlier = out;
+        int inliers = 0;
+        for (int i = 0; i < cf.n(); i++) {  // (:1087-1101)
+            const int m = cf.mps[i];
+            if (m < 0) continue;
+            if (!cf.outlier[i]) {
+                if (mps[m].nobs > 0) inliers++;
+            } else if (cf.ur[i] >= 0) {
+                cf.mps[i] = -1;  // stereo outliers are dropped
+            }
+        }
+        matches_inliers = inliers;
+        st.inliers = inliers;
+        ok = inliers >= 30;
+        return ORBMI_OK;
+    }
+
+    // ---- Tracking::Track (stereo, SLAM mode) ------------------------------------------------------
+    int track(TrackedFrame& cf) {
+        if (state == NO_IMAGES_YET) state = NOT_INITIALIZED;
+        orbmi_slam_frame_stats st;
+        std::memset(&st, 0xff, sizeof(st));  // -1 = not run
+        st.frame = cf.id;
+        st.n = cf.n();
+        if (state == NOT_INITIALIZED) {
+            SLAM_CHECK(stereo_initialization(cf));
+            st.init = state == OK;
+            if (state != OK) {
+                st.state = state;
+                st.keyframes = (int)kfs.size();
+                st.mappoints = count_mappoints();
+                stats.push_back(st);
+                return ORBMI_OK;
+            }
+        } else {
+            bool ok = false;
+            if (state == OK) {
+                if (!has_velocity || cf.id < last_reloc_frame_id + 2) SLAM_CHECK(track_reference_kf(cf, st, ok));
+                else {
+                    SLAM_CHECK(track_motion_model(cf, st, ok));
+                    if (!ok) SLAM_CHECK(track_reference_kf(cf, st, ok));
+                }
+            }  // else: Relocalization is out of scope
+            cf.ref_kf = ref_kf;
+            if (ok) SLAM_CHECK(track_local_map(cf, st, ok));
+            state = ok ? OK : LOST;
+            if (ok) {
+                if (last_frame.has_tcw) {
+                    velocity = mul(cf.tcw, pose_inverse(last_frame.tcw));
+                    has_velocity = true;
+                } else {
+                    has_velocity = false;
+                }
+                for (int i = 0; i < cf.n(); i++) {  // clean VO matches (:504-513)
+                    const int m = cf.mps[i];
+                    if (m >= 0 && mps[m].nobs < 1) {
+                        cf.outlier[i] = 0;
+                        cf.mps[i] = -1;
+                    }
+                }
+                if (need_new_keyframe(cf, st)) SLAM_CHECK(create_new_keyframe(cf));
+                for (int i = 0; i < cf.n(); i++)  // (:535-539)
+                    if (cf.mps[i] >= 0 && cf.outlier[i]) cf.mps[i] = -1;
+            }
+            if (cf.ref_kf < 0) cf.ref_kf = ref_kf;
+        }
+        last_frame = cf;
+        have_last = true;
+        if (cf.has_tcw) {
+            rel_poses.push_back(mul(cf.tcw, pose_inverse(kfs[cf.ref_kf].tcw)));
+            references.push_back(ref_kf);
+            frame_times.push_back(cf.ts);
+            lost.push_back(state == LOST);
+        } else if (!rel_poses.empty()) {
+            rel_poses.push_back(rel_poses.back());
+            references.push_back(references.back());
+            frame_times.push_back(frame_times.back());
+            lost.push_back(state == LOST);
+        }
+        st.state = state;
+        st.keyframes = (int)kfs.size();
+        st.mappoints = count_mappoints();
+        stats.push_back(st);
+        return ORBMI_OK;
+    }
+
+    int count_mappoints() const {
+        int n = 0;
+        for (auto& m : mps) n += !m.bad;
+        return n;
+    }
+
+    // the poses SaveTrajectory* write: Tcw = Tcr * Trw * Two per recorded frame
+    std::vector<M4> frame_poses() const {
+        std::vector<M4> out;
+        if (kfs.empty()) return out;
+        const M4 Two = pose_inverse(kfs[0].tcw);  // the first keyframe (lowest id)
+        for (size_t f = 0; f < rel_poses.size(); f++) {
+            const M4 Trw = mul(mul(eye4(), kfs[references[f]].tcw), Two);  // keyframe culling out of scope
+            out.push_back(mul(rel_poses[f], Trw));
+        }
+        return out;
+    }
+};
+
+extern "C" {
+
+int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary* vocabulary, orbmi_slam** out) {
+    if (!s || !out || s->width <= 0 || s->height <= 0 || s->n_levels < 1 || s->n_levels > 16 || s->fx == 0.f)
+        return ORBMI_E_ARG;
+    *out = nullptr;
+    orbmi_slam* h = new (std::nothrow) orbmi_slam();
+    if (!h) return ORBMI_E_ARG;
+    h->s = *s;
+    h->device = device;
+    h->voc = vocabulary;
+    int rc = orbmi_extractor_create(device, s->n_features, s->scale_factor, s->n_levels, s->ini_th_fast, s->min_th_fast,
+                                    &h->left);
+    if (!rc) rc = orbmi_extractor_create(device, s->n_features, s->scale_factor, s->n_levels, s->ini_th_fast,
+                                         s->min_th_fast, &h->right);
+    if (!rc) rc = orbmi_matcher_create(device, &h->matcher);
+    if (!rc) rc = orbmi_pose_create(device, &h->pose);
+    if (!rc) rc = orbmi_ba_create(device, &h->ba);
+    if (!rc) {
+        h->scale_factors.resize(s->n_levels);
+        h->inv_level_sigma2.resize(s->n_levels);
+        rc = orbmi_extractor_get_scale_factors(h->left, h->scale_factors.data());
+        if (!rc) rc = orbmi_extractor_get_inverse_scale_sigma_squares(h->left, h->inv_level_sigma2.data());
+        h->log_scale_factor = s->n_levels > 1 ? (float)std::log((double)h->scale_factors[1]) : 0.f;  // mfLogScaleFactor
+    }
+    if (rc) {
+        orbmi_slam_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return ORBMI_OK;
+}
+
+void orbmi_slam_destroy(orbmi_slam* h) {
+    if (!h) return;
+    orbmi_ba_destroy(h->ba);
+    orbmi_pose_destroy(h->pose);
+    orbmi_matcher_destroy(h->matcher);
+    orbmi_extractor_destroy(h->right);
+    orbmi_extractor_destroy(h->left);
+    delete h;
+}
+
+int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+                            double timestamp, float* tcw_out, int* has_pose) {
+    if (!h || !left || !right || rows <= 0 || cols <= 0 || step < (size_t)cols) return ORBMI_E_ARG;
+    TrackedFrame cf;
+    cf.id = h->frame_count;
+    cf.ts = timestamp;
+    // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images, ComputeStereoMatches
+    std::vector<orbmi_keypoint> kr;
+    std::vector<uint8_t> dr;
+    SLAM_CHECK(h->extract(h->left, left, rows, cols, step, cf.keys, cf.desc));
+    SLAM_CHECK(h->extract(h->right, right, rows, cols, step, kr, dr));
+    const int n = cf.n();
+    cf.ur.assign(std::max(n, 1), -1.f);
+    cf.depth.assign(std::max(n, 1), -1.f);
+    SLAM_CHECK(orbmi_compute_stereo_matches(h->left, 0, h->right, 0, h->s.bf, h->s.fx, cf.ur.data(), cf.depth.data(), n));
+    cf.ur.resize(n);
+    cf.depth.resize(n);
+    cf.mps.assign(n, -1);
+    cf.outlier.assign(n, 0);
+    h->frame_count++;
+    SLAM_CHECK(h->track(cf));
+    const TrackedFrame& lf = h->last_frame;
+    if (has_pose) *has_pose = lf.has_tcw ? 1 : 0;
+    if (tcw_out && lf.has_tcw) std::memcpy(tcw_out, lf.tcw.data(), 16 * sizeof(float));
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_stats(orbmi_slam* h, int frame, orbmi_slam_frame_stats* out) {
+    if (!h || !out || frame < 0 || frame >= (int)h->stats.size()) return ORBMI_E_ARG;
+    *out = h->stats[frame];
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_counts(orbmi_slam* h, int* frames, int* keyframes, int* mappoints, int* local_ba_calls) {
+    if (!h) return ORBMI_E_ARG;
+    if (frames) *frames = h->frame_count;
+    if (keyframes) *keyframes = (int)h->kfs.size();
+    if (mappoints) *mappoints = h->count_mappoints();
+    if (local_ba_calls) *local_ba_calls = h->ba_calls;
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_trajectory(orbmi_slam* h, float* tcw, double* timestamps, uint8_t* lost, int capacity, int* n) {
+    if (!h || !n) return ORBMI_E_ARG;
+    const std::vector<M4> P = h->frame_poses();
+    *n = (int)P.size();
+    if (capacity < *n) return ORBMI_E_CAP;
+    for (int f = 0; f < *n; f++) {
+        if (tcw) std::memcpy(tcw + 16 * f, P[f].data(), 16 * sizeof(float));
+        if (timestamps) timestamps[f] = h->frame_times[f];
+        if (lost) lost[f] = h->lost[f];
+    }
+    return ORBMI_OK;
+}
+
+int orbmi_slam_save_trajectory_kitti(orbmi_slam* h, const char* path) {  // src/System.cc:433-486
+    if (!h || !path) return ORBMI_E_ARG;
+    FILE* f = std::fopen(path, "w");
+    if (!f) return ORBMI_E_ARG;
+    for (const M4& T : h->frame_poses()) {
+        const M4 W = pose_inverse(T);  // Rwc = Rcw^T, twc = -Rwc tcw
+        std::fprintf(f, "%.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f\n", W[0], W[1], W[2], W[3], W[4],
+                     W[5], W[6], W[7], W[8], W[9], W[10], W[11]);
+    }
+    std::fclose(f);
+    return ORBMI_OK;
+}
+
+int orbmi_slam_save_trajectory_tum(orbmi_slam* h, const char* path) {  // src/System.cc:334-389
+    if (!h || !path) return ORBMI_E_ARG;
+    FILE* f = std::fopen(path, "w");
+    if (!f) return ORBMI_E_ARG;
+    const std::vector<M4> P = h->frame_poses();
+    for (size_t i = 0; i < P.size(); i++) {
+        if (h->lost[i]) continue;
+        const M4 W = pose_inverse(P[i]);
+        const float R[9] = {W[0], W[1], W[2], W[4], W[5], W[6], W[8], W[9], W[10]};
+        float q[4];
+        quaternion_xyzw(R, q);
+        std::fprintf(f, "%.6f %.9f %.9f %.9f %.9f %.9f %.9f %.9f\n", h->frame_times[i], W[3], W[7], W[11], q[0], q[1],
+                     q[2], q[3]);
+    }
+    std::fclose(f);
+    return ORBMI_OK;
+}
+
+int orbmi_slam_save_keyframe_trajectory_tum(orbmi_slam* h, const char* path) {  // src/System.cc:392-431
+    if (!h || !path) return ORBMI_E_ARG;
+    FILE* f = std::fopen(path, "w");
+    if (!f) return ORBMI_E_ARG;
+    for (const KeyFrame& kf : h->kfs) {
+        if (kf.bad) continue;
+        const M4 W = pose_inverse(kf.tcw);
+        const float R[9] = {W[0], W[1], W[2], W[4], W[5], W[6], W[8], W[9], W[10]};
+        float q[4];
+        quaternion_xyzw(R, q);
+        std::fprintf(f, "%.6f %.7f %.7f %.7f %.7f %.7f %.7f %.7f\n", kf.ts, W[3], W[7], W[11], q[0], q[1], q[2], q[3]);
+    }
+    std::fclose(f);
+    return ORBMI_OK;
+}
+
+}  // extern "C"

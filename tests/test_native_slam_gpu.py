@@ -1,0 +1,85 @@
+"""The native stereo SLAM host loop (csrc/slam.cpp, orbmi_slam_*) on MI355X against the same
+host logic driven by the CPU oracle (system.StereoSLAM + tests/slam_backends.OracleBackend):
+config 1's 200-frame KITTI-shaped sequence gives identical per-frame Tracking
+decisions and the identical trajectory; the writers produce the reference's formats."""
+import numpy as np
+import pytest
+
+from orb_slam2_with_comment_amd.native_slam import NativeStereoSLAM
+from orb_slam2_with_comment_amd.system import OK, StereoSLAM, ate_rmse
+from slam_backends import OracleBackend, render_sequence, sequence_settings, small_vocabulary
+
+pytestmark = pytest.mark.gpu
+
+_DECISIONS = ("n", "init", "track", "bow_matches", "lf_matches", "nmatches_map", "local_map_points",
+              "local_matches", "inliers", "need_kf", "state", "keyframes", "mappoints")
+
+
+def _drive(slam, frames):
+    for f, (L, R, _) in enumerate(frames):
+        slam.TrackStereo(L, R, 0.1 * f)
+
+
+def test_native_matches_oracle_200_frames(tmp_path):
+    n = 200  # config 1: the first 200 frames (stereo_kitti.cc), here of the synthetic sequence
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    gpu = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    _drive(gpu, frames)
+    ref = StereoSLAM(s, backend=OracleBackend(s, voc))
+    _drive(ref, frames)
+    a_all, b_all = gpu.stats, ref.stats
+    assert len(a_all) == len(b_all) == n
+    for a, b in zip(a_all, b_all):
+        assert {k: a.get(k) for k in _DECISIONS} == {k: b.get(k) for k in _DECISIONS}, (a, b)
+    assert all(st["state"] == OK for st in a_all)
+    tg, tr = gpu.trajectory_twc(), ref.trajectory_twc()
+    # the float32 poses agree to the fp64 solves' ~1e-6 relative (bit-identical in practice)
+    np.testing.assert_allclose(tg[:, :3, 3], tr[:, :3, 3], atol=1e-3)
+    np.testing.assert_allclose(tg[:, :3, :3], tr[:, :3, :3], atol=1e-4)
+    gt = np.array([fr[2] for fr in frames])
+    assert abs(ate_rmse(tg, gt) - ate_rmse(tr, gt)) < 1e-3   # identical trajectory RMSE (north_star)
+    assert gpu.counts()["local_ba_calls"] == sum(1 for _ in ref.ba_log)
+    gpu.Shutdown()
+
+
+def test_native_writers_and_counts(tmp_path):
+    n = 16
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    slam = NativeStereoSLAM(s, device=0, vocabulary=small_vocabulary())
+    poses = [slam.TrackStereo(L, R, 0.1 * f) for f, (L, R, _) in enumerate(frames)]
+    assert all(p is not None and p.shape == (4, 4) for p in poses)
+    c = slam.counts()
+    assert c["frames"] == n and c["keyframes"] >= 2 and c["mappoints"] > 500
+    kitti, tum, kf = tmp_path / "k.txt", tmp_path / "t.txt", tmp_path / "kf.txt"
+    slam.SaveTrajectoryKITTI(str(kitti))
+    slam.SaveTrajectoryTUM(str(tum))
+    slam.SaveKeyFrameTrajectoryTUM(str(kf))
+    rows = [list(map(float, l.split())) for l in kitti.read_text().splitlines()]
+    assert len(rows) == n and all(len(r) == 12 for r in rows)
+    np.testing.assert_allclose(np.array(rows).reshape(n, 3, 4), slam.trajectory_twc()[:, :3, :4], atol=1e-8)
+    trows = [l.split() for l in tum.read_text().splitlines()]
+    assert len(trows) == n and all(len(r) == 8 for r in trows)
+    q = np.array([[float(x) for x in r[4:]] for r in trows])
+    np.testing.assert_allclose(np.linalg.norm(q, axis=1), 1.0, atol=1e-5)
+    assert len(kf.read_text().splitlines()) == c["keyframes"]
+    # the current frame's pose is what TrackStereo returned for the last frame
+    T, ts, lost = slam.frame_poses()
+    assert len(T) == n and not lost.any() and ts[-1] == pytest.approx(0.1 * (n - 1))
+    slam.Shutdown()
+
+
+def test_native_needs_vocabulary_for_reference_tracking(tmp_path):
+    frames = render_sequence(3)
+    s = sequence_settings(tmp_path)
+    slam = NativeStereoSLAM(s, device=0, vocabulary=None)
+    L, R, _ = frames[0]
+    slam.TrackStereo(L, R, 0.0)   # initialisation needs no vocabulary
+    L, R, _ = frames[1]
+    from orb_slam2_with_comment_amd._capi import ORBMI_E_STATE, OrbmiError
+    with pytest.raises(OrbmiError) as e:   # TrackReferenceKeyFrame (no velocity yet) needs ComputeBoW
+        slam.TrackStereo(L, R, 0.1)
+    assert e.value.code == ORBMI_E_STATE
+    slam.Shutdown()
