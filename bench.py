@@ -433,7 +433,9 @@ def pose_roofline(prof, recs, traffic_path):
     flops = np.mean([int(r["n_obs"]) * POSE_FLOPS_PER_EDGE_PASS * (int(r["iterations"]) + 4)
                      + int(r["iterations"]) * POSE_FLOPS_PER_TRIAL for r in recs])
     achieved = flops / avg_s / 1e12 if avg_s > 0 else 0.0
-    return {"kernel": "k_pose_opt", "bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS,
+    # the kernel issues fp64 VALU instructions only (no MFMA: a 6x6 system per frame, DESIGN.md
+    # §4 and the MFMA A/B in §4b); the peak is the fp64 vector peak, equal to the fp64 MFMA peak
+    return {"kernel": "k_pose_opt", "bound": "fp64-valu", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFS, 8),
             "traffic": read_traffic(traffic_path, "k_pose_opt"), "alg_flops_per_launch": round(float(flops)),
             "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches),

@@ -35,5 +35,5 @@ run bench_batch 300 python bench.py --mode batch --steps 50 --warmup 4
 tail -1 $OUT/bench_batch.log > $P/bench_batch.json
 run bench_extract 300 python bench.py --mode extract
 tail -1 $OUT/bench_extract.log > $P/bench_extract.json
-run bench_system 300 python bench.py --mode system --steps 40 --warmup 4
+run bench_system 400 python bench.py --mode system
 tail -1 $OUT/bench_system.log > $P/bench_system.json
