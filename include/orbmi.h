@@ -468,6 +468,31 @@ int orbmi_search_by_projection_last_frame_if(orbmi_matcher* m, const orbmi_frame
 int orbmi_track_update_matches(orbmi_matcher* m, const orbmi_frame_view* F, int stage, const uint8_t* outlier,
                                const orbmi_frame_mappoints* mp, uint8_t* occupied_out, int* counts);
 
+/* ---- LocalMapping host geometry (CreateNewMapPoints around SearchForTriangulation) ----- */
+
+/* The KeyFrame members CreateNewMapPoints reads (host arrays): pose, mvKeysUn, mvuRight,
+ * mvDepth, intrinsics, mbf, mb, mvLevelSigma2 and mvScaleFactors (nlevels entries). */
+typedef struct orbmi_tri_keyframe {
+    const float* tcw;              /* 4x4 row-major Tcw                                     */
+    const orbmi_keypoint* keys_un;
+    const float* u_right;
+    const float* depth;
+    float fx, fy, cx, cy, bf, mb;
+    const float* level_sigma2;
+    const float* scale_factors;
+} orbmi_tri_keyframe;
+
+/* LocalMapping::ComputeF12 (src/LocalMapping.cc:676-693): F12 = K1^-T [t12]x R12 K2^-1 (3x3
+ * row-major float), the epipolar constraint SearchForTriangulation takes. */
+int orbmi_compute_f12(const orbmi_tri_keyframe* kf1, const orbmi_tri_keyframe* kf2, float* F12);
+
+/* CreateNewMapPoints' per-match geometry (src/LocalMapping.cc:385-575) for the n matched
+ * keypoint pairs (idx1[k] of kf1, idx2[k] of kf2): ray parallax, linear triangulation or stereo
+ * back-projection, positive depth in both cameras, reprojection error (5.991 / 7.8 sigma^2) and
+ * scale consistency.  ok[k] = 1 with x3d[3k..3k+2] the new point's world position, else 0. */
+int orbmi_triangulate_matches(const orbmi_tri_keyframe* kf1, const orbmi_tri_keyframe* kf2, const int32_t* idx1,
+                              const int32_t* idx2, int n, float* x3d, uint8_t* ok);
+
 /* ---- System::TrackStereo: the native stereo SLAM host loop ---------------------------- */
 
 /* The Tracking constructor's view of a settings file (src/Tracking.cc:53-143) for a rectified
@@ -482,6 +507,7 @@ typedef struct orbmi_slam_settings {
     float scale_factor;
     int n_levels, ini_th_fast, min_th_fast;
     int local_ba;                  /* 1: LocalMapping runs LocalBundleAdjustment (:89-90)      */
+    int local_mapping;             /* 1: and CreateNewMapPoints, SearchInNeighbors, KeyFrameCulling */
 } orbmi_slam_settings;
 
 /* Per tracked frame: Tracking's counters (-1 = the stage did not run). track: 0 none, 1

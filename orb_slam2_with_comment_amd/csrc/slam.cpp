@@ -8,7 +8,9 @@
 //   TrackWithMotionModel       -> Slam::track_motion_model        src/Tracking.cc:997-1063
 //   TrackLocalMap, UpdateLocalKeyFrames / Points, SearchLocalPoints src/Tracking.cc:1075-1104, 1345-1580
 //   NeedNewKeyFrame / CreateNewKeyFrame                           src/Tracking.cc:1140-1330
-//   LocalMapping::ProcessNewKeyFrame + LocalBundleAdjustment      src/LocalMapping.cc:152-200, :89-90
+//   LocalMapping::Run: ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints,
+//     SearchInNeighbors (ORBmatcher::Fuse + replay), LocalBundleAdjustment, KeyFrameCulling
+//                                                                 src/LocalMapping.cc:47-841
 //   KeyFrame::UpdateConnections, MapPoint bookkeeping             src/KeyFrame.cc, src/MapPoint.cc
 //   Optimizer::LocalBundleAdjustment's graph assembly             src/Optimizer.cc:486-683
 //   System::SaveTrajectoryKITTI / TUM / SaveKeyFrameTrajectoryTUM src/System.cc:334-486
@@ -121,9 +123,11 @@ struct KeyFrame {
     std::vector<int> covisible;  // mvpOrderedConnectedKeyFrames
     std::map<int, int> conn;     // mConnectedKeyFrameWeights (keyframe id order)
     int parent = -1;
-    std::vector<int> children;
+    std::vector<int> children;   // mspChildrens (iterated in id order)
     bool first_connection = true;
     bool bad = false;
+    int fuse_target_for_kf = -1;  // mnFuseTargetForKF
+    M4 tcp{};                    // mTcp, set when the keyframe turns bad
 };
 
 struct MapPoint {
@@ -136,6 +140,10 @@ struct MapPoint {
     std::map<int, int> obs;      // keyframe id -> keypoint index (keyframe id order)
     int nobs = 0;
     bool bad = false;
+    int first_kf_id = 0;         // mnFirstKFid
+    int visible = 1, found = 1;  // mnVisible, mnFound
+    int replaced = -1;           // mpReplaced
+    int fuse_candidate_for_kf = -1;
 };
 
 struct TrackedFrame {
@@ -195,6 +203,8 @@ struct orbmi_slam {
     std::vector<uint8_t> lost;
     std::vector<orbmi_slam_frame_stats> stats;
     int ba_calls = 0;
+    std::vector<float> level_sigma2;  // mvLevelSigma2
+    std::vector<int> recent_mps;      // mlpRecentAddedMapPoints
     // extraction scratch
     std::vector<orbmi_keypoint> kbuf;
     std::vector<uint8_t> dbuf;
@@ -440,6 +450,7 @@ struct orbmi_slam {
                 mp.pos[r] = (float)a + twc[4 * r + 3];
             }
             mp.ref_kf = k;
+            mp.first_kf_id = k;
             std::memcpy(mp.desc, &cf.desc[32 * i], 32);  // ComputeDistinctiveDescriptors of one observation
             mps.push_back(mp);
             add_observation(mp.id, k, i);
@@ -472,7 +483,7 @@ struct orbmi_slam {
     }
 
     bool need_new_keyframe(const TrackedFrame& cf, orbmi_slam_frame_stats& st) {  // src/Tracking.cc:1140-1249
-        const int nkfs = (int)kfs.size();
+        const int nkfs = keyframes_in_map();
         if (cf.id < last_reloc_frame_id + s.max_frames && nkfs > s.max_frames) return false;
         const int min_obs = nkfs <= 2 ? 2 : 3;
         const int n_ref = tracked_map_points(kfs[ref_kf], min_obs);
@@ -521,7 +532,10 @@ struct orbmi_slam {
     }
 
     // ---- LocalMapping (synchronous) -------------------------------------------------------------
-    int local_mapping(int k) {  // ProcessNewKeyFrame (src/LocalMapping.cc:152-200) + LocalBA (:89-90)
+    // LocalMapping::Run for one keyframe (src/LocalMapping.cc:47-128), no other keyframe queued and
+    // no stop request: ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints,
+    // SearchInNeighbors, LocalBundleAdjustment (more than 2 keyframes), KeyFrameCulling
+    int local_mapping(int k) {
         if (voc && !kfs[k].fv.valid) SLAM_CHECK(compute_bow(kfs[k].desc, kfs[k].fv));
         std::vector<int> updated;
         for (int i = 0; i < (int)kfs[k].mps.size(); i++) {
@@ -530,13 +544,293 @@ struct orbmi_slam {
             if (!mps[m].obs.count(k)) {
                 add_observation(m, k, i);
                 updated.push_back(m);
+            } else {
+                recent_mps.push_back(m);  // the new stereo points the Tracking inserted
             }
         }
         for (int m : updated) update_normal_and_depth(m);
         SLAM_CHECK(distinctive(updated));
         update_connections(k);
-        if (s.local_ba && kfs.size() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+        map_point_culling(k);
+        if (s.local_mapping) {
+            SLAM_CHECK(create_new_map_points(k));
+            SLAM_CHECK(search_in_neighbors(k));
+        }
+        if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+        if (s.local_mapping) keyframe_culling(k);
         return ORBMI_OK;
+    }
+
+    void map_point_culling(int k) {  // src/LocalMapping.cc:219-263, stereo: nThObs = 3
+        std::vector<int> keep;
+        for (int m : recent_mps) {
+            MapPoint& mp = mps[m];
+            if (mp.bad) continue;
+            if ((float)mp.found / (float)mp.visible < 0.25f) set_bad(m);  // GetFoundRatio
+            else if (k - mp.first_kf_id >= 2 && mp.nobs <= 3) set_bad(m);
+            else if (k - mp.first_kf_id >= 3) continue;
+            else keep.push_back(m);
+        }
+        recent_mps = keep;
+    }
+
+    orbmi_tri_keyframe tri_view(const KeyFrame& kf) const {
+        return orbmi_tri_keyframe{kf.tcw.data(), kf.keys.data(), kf.ur.data(), kf.depth.data(), s.fx, s.fy, s.cx,
+                                  s.cy, s.bf, s.bf / s.fx, level_sigma2.data(), scale_factors.data()};
+    }
+
+    // src/LocalMapping.cc:290-577, stereo: the 10 best covisible keyframes
+    int create_new_map_points(int k) {
+        float ow1[3];
+        kf_ow(k, ow1);
+        const orbmi_tri_keyframe v1 = tri_view(kfs[k]);
+        const float mb = s.bf / s.fx;
+        std::vector<uint8_t> has1(std::max<size_t>(kfs[k].mps.size(), 1), 0);
+        for (size_t i = 0; i < kfs[k].mps.size(); i++) has1[i] = kfs[k].mps[i] >= 0;
+        const std::vector<int> neigh(kfs[k].covisible.begin(),
+                                     kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
+        for (int k2 : neigh) {
+            float ow2[3];
+            kf_ow(k2, ow2);
+            const float d[3] = {ow2[0] - ow1[0], ow2[1] - ow1[1], ow2[2] - ow1[2]};
+            const float baseline = (float)std::sqrt(((double)d[0] * d[0] + (double)d[1] * d[1]) + (double)d[2] * d[2]);
+            if (baseline < mb) continue;
+            const orbmi_tri_keyframe v2 = tri_view(kfs[k2]);
+            float F12[9];
+            SLAM_CHECK(orbmi_compute_f12(&v1, &v2, F12));
+            if (!kfs[k].fv.valid || !kfs[k2].fv.valid) continue;
+            std::vector<uint8_t> has2(std::max<size_t>(kfs[k2].mps.size(), 1), 0);
+            for (size_t i = 0; i < kfs[k2].mps.size(); i++) has2[i] = kfs[k2].mps[i] >= 0;
+            const KeyFrame &K1 = kfs[k], &K2 = kfs[k2];
+            const orbmi_frame_view f1 = view(K1.keys, K1.desc, K1.ur, K1.tcw.data());
+            const orbmi_frame_view f2 = view(K2.keys, K2.desc, K2.ur, K2.tcw.data());
+            const orbmi_feature_vector fv1 = K1.fv.view(), fv2 = K2.fv.view();
+            std::vector<int32_t> m12(std::max<size_t>(K1.keys.size(), 1));
+            int nm = 0;
+            SLAM_CHECK(orbmi_search_for_triangulation(matcher, &f1, has1.data(), &fv1, &f2, has2.data(), &fv2, F12, 0, 0,
+                                                      m12.data(), &nm));
+            std::vector<int32_t> idx1, idx2;
+            for (size_t i = 0; i < K1.keys.size(); i++)
+                if (m12[i] >= 0) { idx1.push_back((int32_t)i); idx2.push_back(m12[i]); }
+            if (idx1.empty()) continue;
+            std::vector<float> x3d(3 * idx1.size());
+            std::vector<uint8_t> ok(idx1.size());
+            SLAM_CHECK(orbmi_triangulate_matches(&v1, &v2, idx1.data(), idx2.data(), (int)idx1.size(), x3d.data(),
+                                                 ok.data()));
+            std::vector<int> fresh;
+            for (size_t q = 0; q < idx1.size(); q++) {
+                if (!ok[q]) continue;
+                const int i1 = idx1[q], i2 = idx2[q];
+                MapPoint mp;
+                mp.id = (int)mps.size();
+                std::memcpy(mp.pos, &x3d[3 * q], 3 * sizeof(float));
+                mp.ref_kf = k;
+                mp.first_kf_id = k;
+                mps.push_back(mp);
+                add_observation(mp.id, k, i1);
+                add_observation(mp.id, k2, i2);
+                kfs[k].mps[i1] = mp.id;
+                kfs[k2].mps[i2] = mp.id;
+                has1[i1] = 1;
+                recent_mps.push_back(mp.id);
+                fresh.push_back(mp.id);
+            }
+            SLAM_CHECK(distinctive(fresh));
+            for (int m : fresh) update_normal_and_depth(m);
+        }
+        return ORBMI_OK;
+    }
+
+    // MapPoint::Replace (src/MapPoint.cc:172-215): `other` takes over m's observations; m turns bad.
+    // Returns true when other gained them (its descriptor is recomputed before the next search).
+    bool replace(int m, int other) {
+        if (m == other) return false;
+        const std::map<int, int> obs = mps[m].obs;
+        mps[m].obs.clear();
+        mps[m].bad = true;
+        mps[m].replaced = other;
+        for (auto& o : obs) {
+            if (!mps[other].obs.count(o.first)) {
+                kfs[o.first].mps[o.second] = other;  // KeyFrame::ReplaceMapPointMatch
+                add_observation(other, o.first, o.second);
+            } else {
+                kfs[o.first].mps[o.second] = -1;     // KeyFrame::EraseMapPointMatch
+            }
+        }
+        mps[other].found += mps[m].found;
+        mps[other].visible += mps[m].visible;
+        return true;
+    }
+
+    // ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for every
+    // point on the GPU, then the map updates in list order
+    int fuse(int k, const std::vector<int>& list, std::set<int>& dirty) {
+        if (!dirty.empty()) {
+            std::vector<int> pts;
+            for (int m : dirty)
+                if (!mps[m].bad) pts.push_back(m);
+            SLAM_CHECK(distinctive(pts));
+            dirty.clear();
+        }
+        std::vector<int> pts;
+        for (int m : list)
+            if (m >= 0) pts.push_back(m);
+        if (pts.empty()) return ORBMI_OK;
+        std::vector<orbmi_mappoint> rec(pts.size());
+        std::vector<uint8_t> in_kf(pts.size());
+        for (size_t j = 0; j < pts.size(); j++) {
+            const MapPoint& mp = mps[pts[j]];
+            orbmi_mappoint& r = rec[j];
+            std::memcpy(r.pos, mp.pos, sizeof(r.pos));
+            std::memcpy(r.normal, mp.normal, sizeof(r.normal));
+            r.max_distance = mp.max_distance;
+            r.min_distance = mp.min_distance;
+            r.flags = (mp.bad ? ORBMI_MP_BAD : 0u) | (mp.nobs > 0 ? ORBMI_MP_HAS_OBS : 0u);
+            std::memcpy(r.desc, mp.desc, 32);
+            in_kf[j] = mp.obs.count(k) ? 1 : 0;
+        }
+        const KeyFrame& kf = kfs[k];
+        const orbmi_frame_view v = view(kf.keys, kf.desc, kf.ur, kf.tcw.data());
+        std::vector<int32_t> best(pts.size()), dist(pts.size());
+        int nc = 0;
+        SLAM_CHECK(orbmi_fuse_search(matcher, &v, rec.data(), in_kf.data(), (int)pts.size(), 3.f, best.data(), dist.data(),
+                                     &nc));
+        for (size_t j = 0; j < pts.size(); j++) {
+            const int m = pts[j], b = best[j];
+            if (mps[m].bad || mps[m].obs.count(k) || b < 0) continue;
+            const int in = kfs[k].mps[b];
+            if (in >= 0) {
+                if (!mps[in].bad) {
+                    if (mps[in].nobs > mps[m].nobs) {
+                        if (replace(m, in)) dirty.insert(in);
+                    } else if (replace(in, m)) {
+                        dirty.insert(m);
+                    }
+                }
+            } else {
+                add_observation(m, k, b);
+                kfs[k].mps[b] = m;
+            }
+        }
+        return ORBMI_OK;
+    }
+
+    int search_in_neighbors(int k) {  // src/LocalMapping.cc:589-674, stereo: nn = 10
+        std::vector<int> targets;
+        const std::vector<int> neigh(kfs[k].covisible.begin(),
+                                     kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
+        for (int k1 : neigh) {
+            if (kfs[k1].bad || kfs[k1].fuse_target_for_kf == k) continue;
+            targets.push_back(k1);
+            kfs[k1].fuse_target_for_kf = k;
+            const std::vector<int> second(kfs[k1].covisible.begin(),
+                                          kfs[k1].covisible.begin() + std::min<size_t>(5, kfs[k1].covisible.size()));
+            for (int k2 : second) {
+                if (kfs[k2].bad || kfs[k2].fuse_target_for_kf == k || k2 == k) continue;
+                targets.push_back(k2);
+            }
+        }
+        std::set<int> dirty;
+        const std::vector<int> matches = kfs[k].mps;
+        for (int t : targets) SLAM_CHECK(fuse(t, matches, dirty));
+        std::vector<int> cands;
+        for (int t : targets)
+            for (int m : kfs[t].mps) {
+                if (m < 0 || mps[m].bad || mps[m].fuse_candidate_for_kf == k) continue;
+                mps[m].fuse_candidate_for_kf = k;
+                cands.push_back(m);
+            }
+        SLAM_CHECK(fuse(k, cands, dirty));
+        dirty.clear();
+        std::vector<int> upd;
+        std::set<int> seen_pt;
+        for (int m : kfs[k].mps)
+            if (m >= 0 && !mps[m].bad && seen_pt.insert(m).second) upd.push_back(m);
+        SLAM_CHECK(distinctive(upd));
+        for (int m : upd) update_normal_and_depth(m);
+        update_connections(k);
+        return ORBMI_OK;
+    }
+
+    // ---- KeyFrameCulling (src/LocalMapping.cc:775-841) and KeyFrame::SetBadFlag -------------------
+    void erase_connection(int k, int other) {  // KeyFrame::EraseConnection + UpdateBestCovisibles
+        if (kfs[k].conn.erase(other)) sort_covisible(kfs[k]);
+    }
+
+    int get_weight(int k, int other) const {
+        auto it = kfs[k].conn.find(other);
+        return it == kfs[k].conn.end() ? 0 : it->second;
+    }
+
+    void change_parent(int k, int p) {
+        kfs[k].parent = p;
+        auto& ch = kfs[p].children;
+        if (std::find(ch.begin(), ch.end(), k) == ch.end()) ch.push_back(k);
+    }
+
+    void set_bad_keyframe(int k) {  // KeyFrame::SetBadFlag (src/KeyFrame.cc:467-559)
+        if (kfs[k].id == 0) return;
+        const std::map<int, int> conn = kfs[k].conn;
+        for (auto& c : conn) erase_connection(c.first, k);
+        for (int m : std::vector<int>(kfs[k].mps))
+            if (m >= 0) erase_observation(m, k);
+        kfs[k].conn.clear();
+        kfs[k].covisible.clear();
+        std::set<int> candidates{kfs[k].parent};
+        std::vector<int> children = kfs[k].children;
+        std::sort(children.begin(), children.end());
+        while (!children.empty()) {
+            bool cont = false;
+            int best = -1, pc = -1, pp = -1;
+            for (int c : children) {
+                if (kfs[c].bad) continue;
+                for (int cv : kfs[c].covisible)
+                    for (int cand : candidates)
+                        if (cv == cand) {
+                            const int w = get_weight(c, cv);
+                            if (w > best) { pc = c; pp = cv; best = w; cont = true; }
+                        }
+            }
+            if (!cont) break;
+            change_parent(pc, pp);
+            candidates.insert(pc);
+            children.erase(std::find(children.begin(), children.end(), pc));
+            auto& own = kfs[k].children;
+            own.erase(std::find(own.begin(), own.end(), pc));
+        }
+        const int parent = kfs[k].parent;
+        for (int c : children) change_parent(c, parent);
+        kfs[k].children.clear();
+        auto& pch = kfs[parent].children;
+        auto it = std::find(pch.begin(), pch.end(), k);
+        if (it != pch.end()) pch.erase(it);
+        kfs[k].tcp = mul(kfs[k].tcw, pose_inverse(kfs[parent].tcw));
+        kfs[k].bad = true;
+    }
+
+    void keyframe_culling(int k) {
+        const std::vector<int> local = kfs[k].covisible;
+        for (int kk : local) {
+            const KeyFrame& kf = kfs[kk];
+            if (kf.id == 0) continue;
+            int n_mps = 0, n_red = 0;
+            for (size_t i = 0; i < kf.mps.size(); i++) {
+                const int m = kf.mps[i];
+                if (m < 0 || mps[m].bad) continue;
+                if (kf.depth[i] > s.th_depth || kf.depth[i] < 0) continue;
+                n_mps++;
+                if (mps[m].nobs > 3) {
+                    const int level = kf.keys[i].octave;
+                    int n = 0;
+                    for (auto& o : mps[m].obs) {
+                        if (o.first == kk) continue;
+                        if (kfs[o.first].keys[o.second].octave <= level + 1 && ++n >= 3) break;
+                    }
+                    if (n >= 3) n_red++;
+                }
+            }
+            if (n_red > 0.9 * n_mps) set_bad_keyframe(kk);
+        }
     }
 
     // Optimizer::LocalBundleAdjustment: the graph as src/Optimizer.cc:486-683 assembles it
@@ -796,16 +1090,24 @@ struct orbmi_slam {
             if (m < 0) continue;
             if (mps[m].bad) cf.mps[i] = -1;
             else {
+                mps[m].visible++;  // IncreaseVisible
                 seen.insert(m);
                 occ[i] = mps[m].nobs > 0 ? 1 : 0;
             }
         }
         const std::vector<orbmi_mappoint> rec = mp_records(local_mps);
         const orbmi_frame_view vc = view(cf, cf.tcw.data());
-        std::vector<int32_t> m_mp(std::max(cf.n(), 1));
-        int nl = 0, ntm = 0;
-        SLAM_CHECK(orbmi_search_local_points(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f, m_mp.data(), &nl,
-                                             &ntm));
+        std::vector<int32_t> m_mp(std::max(cf.n(), 1), -1);
+        int nl = 0;
+        // isInFrustum(0.5) -> IncreaseVisible, then SearchByProjection(F, points, th = 1), 0.8
+        std::vector<orbmi_mappoint_track> tr(std::max<size_t>(rec.size(), 1));
+        SLAM_CHECK(orbmi_is_in_frustum(matcher, &vc, rec.data(), (int)rec.size(), 0.5f, tr.data()));
+        int n_in = 0;
+        for (size_t j = 0; j < rec.size(); j++)
+            if (tr[j].in_view) { mps[local_mps[j]].visible++; n_in++; }
+        if (n_in > 0)
+            SLAM_CHECK(orbmi_search_by_projection_local(matcher, &vc, occ.data(), rec.data(), tr.data(), (int)rec.size(), 1.f,
+                                                        0.8f, m_mp.data(), &nl));
         st.local_map_points = (int)local_mps.size();
         st.local_matches = nl;
         std::vector<int> cur = cf.mps;
@@ -826,6 +1128,7 @@ struct orbmi_slam {
             const int m = cf.mps[i];
             if (m < 0) continue;
             if (!cf.outlier[i]) {
+                mps[m].found++;  // IncreaseFound
                 if (mps[m].nobs > 0) inliers++;
             } else if (cf.ur[i] >= 0) {
                 cf.mps[i] = -1;  // stereo outliers are dropped
@@ -857,6 +1160,8 @@ struct orbmi_slam {
         } else {
             bool ok = false;
             if (state == OK) {
+                for (int& m : last_frame.mps)  // Tracking::CheckReplacedInLastFrame
+                    if (m >= 0 && mps[m].replaced >= 0) m = mps[m].replaced;
                 if (!has_velocity || cf.id < last_reloc_frame_id + 2) SLAM_CHECK(track_reference_kf(cf, st, ok));
                 else {
                     SLAM_CHECK(track_motion_model(cf, st, ok));
@@ -906,6 +1211,12 @@ struct orbmi_slam {
         return ORBMI_OK;
     }
 
+    int keyframes_in_map() const {  // Map::KeyFramesInMap
+        int n = 0;
+        for (auto& k : kfs) n += !k.bad;
+        return n;
+    }
+
     int count_mappoints() const {
         int n = 0;
         for (auto& m : mps) n += !m.bad;
@@ -918,7 +1229,13 @@ struct orbmi_slam {
         if (kfs.empty()) return out;
         const M4 Two = pose_inverse(kfs[0].tcw);  // the first keyframe (lowest id)
         for (size_t f = 0; f < rel_poses.size(); f++) {
-            const M4 Trw = mul(mul(eye4(), kfs[references[f]].tcw), Two);  // keyframe culling out of scope
+            M4 Trw = eye4();
+            int k = references[f];
+            while (kfs[k].bad) {  // a culled reference keyframe: through its parent (Tcp)
+                Trw = mul(Trw, kfs[k].tcp);
+                k = kfs[k].parent;
+            }
+            Trw = mul(mul(Trw, kfs[k].tcw), Two);
             out.push_back(mul(rel_poses[f], Trw));
         }
         return out;
@@ -949,6 +1266,8 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
         rc = orbmi_extractor_get_scale_factors(h->left, h->scale_factors.data());
         if (!rc) rc = orbmi_extractor_get_inverse_scale_sigma_squares(h->left, h->inv_level_sigma2.data());
         h->log_scale_factor = s->n_levels > 1 ? (float)std::log((double)h->scale_factors[1]) : 0.f;  // mfLogScaleFactor
+        h->level_sigma2.resize(s->n_levels);
+        for (int l = 0; l < s->n_levels; l++) h->level_sigma2[l] = h->scale_factors[l] * h->scale_factors[l];
     }
     if (rc) {
         orbmi_slam_destroy(h);

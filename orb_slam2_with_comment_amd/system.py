@@ -28,8 +28,10 @@ Deterministic replacements of the reference's unordered behaviour (documented in
     thread; with LocalMapping always idle NeedNewKeyFrame's c1b holds, as on a fast machine).
   * std::map<KeyFrame*, ...> iteration (pointer order) is keyframe-id order; covisibility ties
     sort by id like ascending heap addresses do.
-  * LocalMapping's MapPointCulling, CreateNewMapPoints, SearchInNeighbors and KeyFrameCulling,
-    relocalisation and loop closing are not part of this path (out of scope).
+  * Relocalisation and loop closing are not part of this path (out of scope).
+  * ORBmatcher::Fuse searches all of a call's points on the backend at once, then replays the
+    map updates in list order (re-checking isBad / IsInKeyFrame); descriptors of points that
+    gained observations by MapPoint::Replace are recomputed before the next Fuse call.
 """
 from __future__ import annotations
 
@@ -87,7 +89,7 @@ def quaternion_xyzw(R) -> np.ndarray:
 
 
 # ---- map model (src/KeyFrame.cc, src/MapPoint.cc) ------------------------------------------
-@dataclasses.dataclass(eq=False)
+@dataclasses.dataclass(eq=False, repr=False)
 class KeyFrame:
     """The fields of ORB_SLAM2::KeyFrame this path reads; also the graph node type of
     optimizer.gather_local_ba (id, tcw, keys_un, u_right, inv_level_sigma2, cam, map_points,
@@ -108,9 +110,11 @@ class KeyFrame:
     covisible: list = dataclasses.field(default_factory=list)  # mvpOrderedConnectedKeyFrames
     conn: dict = dataclasses.field(default_factory=dict)       # mConnectedKeyFrameWeights
     parent: object = None
-    children: list = dataclasses.field(default_factory=list)
+    children: list = dataclasses.field(default_factory=list)  # mspChildrens (iterated in id order)
     first_connection: bool = True
     bad: bool = False
+    fuse_target_for_kf: int = -1    # mnFuseTargetForKF
+    tcp: np.ndarray = None          # mTcp (set when the keyframe turns bad)
 
     @property
     def Ow(self) -> np.ndarray:
@@ -138,6 +142,62 @@ class KeyFrame:
 
     def best_covisibility(self, n: int) -> list:
         return self.covisible[:n]
+
+    def get_weight(self, kf) -> int:
+        return self.conn.get(kf, 0)
+
+    def erase_connection(self, kf):
+        """KeyFrame::EraseConnection + UpdateBestCovisibles (src/KeyFrame.cc:567-581)."""
+        if kf in self.conn:
+            del self.conn[kf]
+            self.covisible = [k for w, _, k in sorted(((w, k.id, k) for k, w in self.conn.items()),
+                                                     key=lambda p: (p[0], p[1]), reverse=True)]
+
+    def change_parent(self, kf):
+        """KeyFrame::ChangeParent (src/KeyFrame.cc): mpParent = pKF; pKF->AddChild(this)."""
+        self.parent = kf
+        if self not in kf.children:
+            kf.children.append(self)
+
+    def set_bad(self):
+        """KeyFrame::SetBadFlag (src/KeyFrame.cc:467-559): drop the covisibility links and the
+        observations, hand the children to the best-connected parent candidates (spanning
+        tree), keep Tcp for the trajectory.  std::set / std::map pointer order -> id order."""
+        if self.id == 0:
+            return
+        for kf in sorted(self.conn, key=lambda k: k.id):
+            kf.erase_connection(self)
+        for mp in self.map_points:
+            if mp is not None:
+                mp.erase_observation(self)
+        self.conn = {}
+        self.covisible = []
+        candidates = {self.parent}
+        children = sorted(self.children, key=lambda k: k.id)
+        while children:
+            cont, best, pc, pp = False, -1, None, None
+            for kf in children:
+                if kf.bad:
+                    continue
+                for c in kf.covisible:
+                    for cand in sorted(candidates, key=lambda k: k.id):
+                        if c.id == cand.id:
+                            w = kf.get_weight(c)
+                            if w > best:
+                                pc, pp, best, cont = kf, c, w, True
+            if not cont:
+                break
+            pc.change_parent(pp)
+            candidates.add(pc)
+            children.remove(pc)
+            self.children.remove(pc)
+        for kf in children:
+            kf.change_parent(self.parent)
+        self.children = []
+        if self in self.parent.children:
+            self.parent.children.remove(self)
+        self.tcp = _mul(self.tcw, pose_inverse(self.parent.tcw))
+        self.bad = True
 
     def update_connections(self):
         """KeyFrame::UpdateConnections (src/KeyFrame.cc:285-371)."""
@@ -172,7 +232,7 @@ class KeyFrame:
             self.first_connection = False
 
 
-@dataclasses.dataclass(eq=False)
+@dataclasses.dataclass(eq=False, repr=False)
 class MapPoint:
     id: int
     pos: np.ndarray                 # float32[3]
@@ -184,6 +244,35 @@ class MapPoint:
     observations: dict = dataclasses.field(default_factory=dict)   # KeyFrame -> keypoint index
     nobs: int = 0
     bad: bool = False
+    first_kf_id: int = 0            # mnFirstKFid
+    visible: int = 1                # mnVisible
+    found: int = 1                  # mnFound
+    replaced: object = None         # mpReplaced
+    fuse_candidate_for_kf: int = -1  # mnFuseCandidateForKF
+
+    def found_ratio(self) -> np.float32:
+        """MapPoint::GetFoundRatio: static_cast<float>(mnFound) / mnVisible."""
+        return np.float32(np.float32(self.found) / np.float32(self.visible))
+
+    def replace(self, other) -> bool:
+        """MapPoint::Replace (src/MapPoint.cc:172-215): other takes over this point's
+        observations (keyframe-id order); this point turns bad.  Returns True when other gained
+        observations (its distinctive descriptor is then recomputed by the caller)."""
+        if other.id == self.id:
+            return False
+        obs = sorted(self.observations.items(), key=lambda o: o[0].id)
+        self.observations = {}
+        self.bad = True
+        self.replaced = other
+        for kf, idx in obs:
+            if kf not in other.observations:
+                kf.map_points[idx] = other              # KeyFrame::ReplaceMapPointMatch
+                other.add_observation(kf, idx)
+            else:
+                kf.map_points[idx] = None               # KeyFrame::EraseMapPointMatch
+        other.found += self.found
+        other.visible += self.visible
+        return True
 
     def add_observation(self, kf: KeyFrame, idx: int):
         """MapPoint::AddObservation (src/MapPoint.cc:90-105): stereo observations count 2."""
@@ -260,7 +349,7 @@ def update_normals_and_depths(mps: list):
 
 
 # ---- the per-frame state Tracking keeps (include/Frame.h) ----------------------------------
-@dataclasses.dataclass(eq=False)
+@dataclasses.dataclass(eq=False, repr=False)
 class TrackedFrame:
     id: int
     timestamp: float
@@ -298,6 +387,7 @@ class GpuBackend:
         self.m_local = ORBmatcher(0.8, True, device=device)  # src/Tracking.cc:1391
         self.m_bow = ORBmatcher(0.7, True, device=device)    # src/Tracking.cc:878
         self.m_util = ORBmatcher(device=device)
+        self.m_tri = ORBmatcher(0.6, False, device=device)   # src/LocalMapping.cc:301
         self.pose = PoseOptimizer(device)
         self.ba = LocalBA(device)
         self.vocab = None
@@ -332,8 +422,22 @@ class GpuBackend:
         return self.m_lf.SearchByProjectionLastFrame(cf, occupied, lf, lfp, th, False)
 
     def search_local_points(self, cf, occupied, mps, th):
-        m, n, _ = self.m_local.SearchLocalPoints(cf, occupied, mps, th)
-        return m, n
+        """Tracking::SearchLocalPoints: isInFrustum(0.5) (-> in-view flags, IncreaseVisible)
+        and SearchByProjection(F, points, th) with nnratio 0.8."""
+        tr = self.m_local.IsInFrustum(cf, mps, 0.5)
+        if not np.any(tr["in_view"]):
+            return np.full(len(cf.keys), -1, np.int32), 0, tr["in_view"].astype(bool)
+        m, n = self.m_local.SearchByProjection(cf, occupied, mps, tr, th)
+        return m, n, tr["in_view"].astype(bool)
+
+    def search_for_triangulation(self, kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12):
+        """ORBmatcher(0.6, false).SearchForTriangulation(pKF1, pKF2, F12, pairs, false)."""
+        return self.m_tri.SearchForTriangulation(kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, False)
+
+    def fuse_search(self, kf, mps, in_kf, th=3.0):
+        """The search of ORBmatcher::Fuse(pKF, vpMapPoints, th) -> (best_idx, best_dist)."""
+        bi, bd, _ = self.m_util.FuseSearch(kf, mps, in_kf, th)
+        return bi, bd
 
     def pose_optimization(self, cf, match_lf=None, lf_points=None, match_mp=None, mps=None):
         from .types import POSE_FRAME_DTYPE
@@ -352,7 +456,7 @@ class GpuBackend:
         return self.ba.run(problem, stop)
 
     def close(self):
-        for h in (self.ba, self.pose, self.m_util, self.m_bow, self.m_local, self.m_lf, self.right, self.left):
+        for h in (self.ba, self.pose, self.m_tri, self.m_util, self.m_bow, self.m_local, self.m_lf, self.right, self.left):
             h.close()
         if self.vocab is not None:
             self.vocab.close()
@@ -382,7 +486,8 @@ class StereoSLAM:
     TrackStereo(imLeft, imRight, timestamp) -> Tcw (4x4 float32, or None while not
     initialised / lost), as System::TrackStereo returns mCurrentFrame.mTcw."""
 
-    def __init__(self, settings, backend=None, device: int = 0, vocabulary=None, local_ba: bool = True):
+    def __init__(self, settings, backend=None, device: int = 0, vocabulary=None, local_ba: bool = True,
+                 local_mapping: bool = True):
         from .settings import Settings, load_settings
         self.settings = settings if isinstance(settings, Settings) else load_settings(settings)
         s = self.settings
@@ -393,6 +498,12 @@ class StereoSLAM:
         if hasattr(self.backend, "bind_camera"):
             self.backend.bind_camera(self.cam)
         self.use_local_ba = local_ba
+        # LocalMapping::Run in full (MapPointCulling, CreateNewMapPoints, SearchInNeighbors,
+        # KeyFrameCulling); False keeps ProcessNewKeyFrame + MapPointCulling + LocalBA only
+        self.local_mapping_full = local_mapping
+        sf = np.asarray(self.backend.scale_factors, np.float32)
+        self.level_sigma2 = np.ascontiguousarray(sf * sf, np.float32)   # mvLevelSigma2
+        self.recent_mps: list[MapPoint] = []   # mlpRecentAddedMapPoints
         self.state = NO_IMAGES_YET
         self.keyframes: list[KeyFrame] = []
         self.mappoints: list[MapPoint] = []
@@ -438,6 +549,7 @@ class StereoSLAM:
             ok = True
         else:
             if self.state == OK:
+                self._check_replaced_in_last_frame()
                 if self.velocity is None or cf.id < self.last_reloc_frame_id + 2:
                     ok = self._track_reference_kf(cf, st)
                 else:
@@ -507,7 +619,7 @@ class StereoSLAM:
             return
         X = self._unproject(cf, np.asarray(idx))
         for j, i in enumerate(idx):
-            mp = MapPoint(len(self.mappoints), X[j].copy(), kf)
+            mp = MapPoint(len(self.mappoints), X[j].copy(), kf, first_kf_id=kf.id)
             mp.add_observation(kf, i)
             kf.map_points[i] = mp
             mp.desc = cf.desc[i].copy()   # ComputeDistinctiveDescriptors of one observation
@@ -535,7 +647,7 @@ class StereoSLAM:
     def _need_new_keyframe(self, cf: TrackedFrame, st) -> bool:
         """Tracking::NeedNewKeyFrame (src/Tracking.cc:1140-1249) with LocalMapping idle."""
         s = self.settings
-        nkfs = len(self.keyframes)
+        nkfs = self._keyframes_in_map()
         if cf.id < self.last_reloc_frame_id + s.max_frames and nkfs > s.max_frames:
             return False
         min_obs = 2 if nkfs <= 2 else 3
@@ -593,9 +705,14 @@ class StereoSLAM:
             if off[j + 1] > off[j]:
                 mp.desc = np.asarray(d[j], np.uint8).copy()
 
+    def _keyframes_in_map(self) -> int:
+        return sum(1 for k in self.keyframes if not k.bad)   # Map::KeyFramesInMap
+
     def _local_mapping(self, kf: KeyFrame):
-        """LocalMapping::Run for one keyframe: ProcessNewKeyFrame (src/LocalMapping.cc:152-200)
-        and Optimizer::LocalBundleAdjustment when the map holds more than 2 keyframes (:89-90)."""
+        """LocalMapping::Run for one keyframe (src/LocalMapping.cc:47-128), with no other keyframe
+        queued and no stop request: ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints,
+        SearchInNeighbors, LocalBundleAdjustment (more than 2 keyframes), KeyFrameCulling."""
+        # ProcessNewKeyFrame (:152-211)
         if self.backend_has_bow():
             kf.feat_vec = kf.feat_vec or self.backend.compute_bow(kf.desc)
         updated = []
@@ -605,11 +722,208 @@ class StereoSLAM:
             if kf not in mp.observations:
                 mp.add_observation(kf, i)
                 updated.append(mp)
+            else:   # the new stereo points the Tracking inserted
+                self.recent_mps.append(mp)
         update_normals_and_depths(updated)
         self._distinctive(updated)
         kf.update_connections()
-        if self.use_local_ba and len(self.keyframes) > 2:
+        self._map_point_culling(kf)
+        if self.local_mapping_full:
+            self._create_new_map_points(kf)
+            self._search_in_neighbors(kf)
+        if self.use_local_ba and self._keyframes_in_map() > 2:
             self._local_bundle_adjustment(kf)
+        if self.local_mapping_full:
+            self._keyframe_culling(kf)
+
+    def _map_point_culling(self, kf: KeyFrame):
+        """LocalMapping::MapPointCulling (src/LocalMapping.cc:219-263), stereo: nThObs = 3."""
+        keep = []
+        for mp in self.recent_mps:
+            if mp.bad:
+                continue
+            if mp.found_ratio() < np.float32(0.25):
+                mp.set_bad()
+            elif kf.id - mp.first_kf_id >= 2 and mp.nobs <= 3:
+                mp.set_bad()
+            elif kf.id - mp.first_kf_id >= 3:
+                continue
+            else:
+                keep.append(mp)
+        self.recent_mps = keep
+
+    def _tri_view(self, kf: KeyFrame):
+        """orbmi_tri_keyframe of a keyframe (host arrays kept alive by the returned tuple)."""
+        from .types import TriKeyFrame
+        tcw = np.ascontiguousarray(kf.tcw, np.float32)
+        keys = np.ascontiguousarray(kf.keys_un)
+        ur = np.ascontiguousarray(kf.u_right, np.float32)
+        depth = np.ascontiguousarray(kf.depth, np.float32)
+        sig2 = self.level_sigma2
+        c = self.cam
+        v = TriKeyFrame(tcw.ctypes.data, keys.ctypes.data, ur.ctypes.data, depth.ctypes.data, c.fx, c.fy, c.cx, c.cy,
+                        c.bf, np.float32(np.float32(c.bf) / np.float32(c.fx)), sig2.ctypes.data,
+                        self.backend.scale_factors.ctypes.data)
+        return v, (tcw, keys, ur, depth, sig2)
+
+    def _kf_frame(self, kf: KeyFrame) -> Frame:
+        return Frame(kf.keys_un, kf.desc, kf.u_right, kf.tcw, self.cam, self.backend.scale_factors,
+                     self.cam.width, self.cam.height)
+
+    def _create_new_map_points(self, kf: KeyFrame):
+        """LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:290-577), stereo: the 10 best
+        covisible keyframes, baseline >= mb, SearchForTriangulation (0.6, no orientation check)
+        on the backend, the triangulation / acceptance geometry on the host
+        (orbmi_triangulate_matches), new points with both observations."""
+        import ctypes as C
+        from ._capi import check, lib
+        ow1 = kf.Ow
+        v1, keep1 = self._tri_view(kf)
+        mb = np.float32(np.float32(self.cam.bf) / np.float32(self.cam.fx))
+        has1 = np.array([mp is not None for mp in kf.map_points], np.uint8)
+        for kf2 in kf.best_covisibility(10):
+            d = (kf2.Ow - ow1).astype(np.float32).astype(np.float64)
+            baseline = np.float32(np.sqrt(np.sum(d * d)))
+            if baseline < mb:
+                continue
+            v2, keep2 = self._tri_view(kf2)
+            F12 = np.zeros(9, np.float32)
+            check("orbmi_compute_f12", lib().orbmi_compute_f12(C.addressof(v1), C.addressof(v2), F12.ctypes.data))
+            if kf.feat_vec is None or kf2.feat_vec is None:
+                continue
+            has2 = np.array([mp is not None for mp in kf2.map_points], np.uint8)
+            m12, _ = self.backend.search_for_triangulation(self._kf_frame(kf), has1, kf.feat_vec, self._kf_frame(kf2),
+                                                           has2, kf2.feat_vec, F12.reshape(3, 3))
+            idx1 = np.nonzero(np.asarray(m12) >= 0)[0].astype(np.int32)
+            if len(idx1) == 0:
+                continue
+            idx2 = np.asarray(m12, np.int32)[idx1]
+            x3d = np.zeros((len(idx1), 3), np.float32)
+            ok = np.zeros(len(idx1), np.uint8)
+            check("orbmi_triangulate_matches", lib().orbmi_triangulate_matches(
+                C.addressof(v1), C.addressof(v2), idx1.ctypes.data, idx2.ctypes.data, len(idx1), x3d.ctypes.data,
+                ok.ctypes.data))
+            new = []
+            for k in np.nonzero(ok)[0]:
+                i1, i2 = int(idx1[k]), int(idx2[k])
+                mp = MapPoint(len(self.mappoints), x3d[k].copy(), kf, first_kf_id=kf.id)
+                mp.add_observation(kf, i1)
+                mp.add_observation(kf2, i2)
+                kf.map_points[i1] = mp
+                kf2.map_points[i2] = mp
+                has1[i1] = 1
+                self.mappoints.append(mp)
+                self.recent_mps.append(mp)
+                new.append(mp)
+            self._distinctive(new)
+            update_normals_and_depths(new)
+            del keep2
+
+    def _mp_fuse_records(self, mps: list) -> np.ndarray:
+        rec = np.zeros(len(mps), MAPPOINT_DTYPE)
+        if not mps:
+            return rec
+        rec["pos"] = np.array([mp.pos for mp in mps], np.float32)
+        rec["normal"] = np.array([mp.normal for mp in mps], np.float32)
+        rec["max_distance"] = np.array([mp.max_distance for mp in mps], np.float32)
+        rec["min_distance"] = np.array([mp.min_distance for mp in mps], np.float32)
+        rec["desc"] = np.array([mp.desc for mp in mps], np.uint8)
+        rec["flags"] = np.array([(MP_BAD if mp.bad else 0) | (MP_HAS_OBS if mp.nobs > 0 else 0) for mp in mps],
+                                np.uint32)
+        return rec
+
+    def _fuse(self, kf: KeyFrame, mps: list, dirty: set):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for
+        every point on the backend, then the map updates in list order."""
+        if dirty:   # descriptors of points that took over observations (MapPoint::Replace)
+            pts = sorted((m for m in dirty if not m.bad), key=lambda m: m.id)
+            self._distinctive(pts)
+            dirty.clear()
+        pts = [mp for mp in mps if mp is not None]
+        if not pts:
+            return
+        in_kf = np.array([kf in mp.observations for mp in pts], np.uint8)
+        best, _ = self.backend.fuse_search(self._kf_frame(kf), self._mp_fuse_records(pts), in_kf, 3.0)
+        for mp, b in zip(pts, best):
+            if mp.bad or kf in mp.observations or b < 0:
+                continue
+            b = int(b)
+            mp_in_kf = kf.map_points[b]
+            if mp_in_kf is not None:
+                if not mp_in_kf.bad:
+                    if mp_in_kf.nobs > mp.nobs:
+                        if mp.replace(mp_in_kf):
+                            dirty.add(mp_in_kf)
+                    elif mp_in_kf.replace(mp):
+                        dirty.add(mp)
+            else:
+                mp.add_observation(kf, b)
+                kf.map_points[b] = mp
+
+    def _search_in_neighbors(self, kf: KeyFrame):
+        """LocalMapping::SearchInNeighbors (src/LocalMapping.cc:589-674), stereo: nn = 10."""
+        targets = []
+        for k in kf.best_covisibility(10):
+            if k.bad or k.fuse_target_for_kf == kf.id:
+                continue
+            targets.append(k)
+            k.fuse_target_for_kf = kf.id
+            for k2 in k.best_covisibility(5):
+                if k2.bad or k2.fuse_target_for_kf == kf.id or k2.id == kf.id:
+                    continue
+                targets.append(k2)
+        dirty = set()
+        matches = list(kf.map_points)
+        for k in targets:
+            self._fuse(k, matches, dirty)
+        cands = []
+        for k in targets:
+            for mp in k.map_points:
+                if mp is None or mp.bad or mp.fuse_candidate_for_kf == kf.id:
+                    continue
+                mp.fuse_candidate_for_kf = kf.id
+                cands.append(mp)
+        self._fuse(kf, cands, dirty)
+        dirty.clear()
+        pts = [mp for mp in kf.map_points if mp is not None and not mp.bad]
+        seen, upd = set(), []
+        for mp in pts:   # one update per point (a point may sit at two keypoints after a Replace)
+            if id(mp) not in seen:
+                seen.add(id(mp))
+                upd.append(mp)
+        self._distinctive(upd)
+        update_normals_and_depths(upd)
+        kf.update_connections()
+
+    def _keyframe_culling(self, kf: KeyFrame):
+        """LocalMapping::KeyFrameCulling (src/LocalMapping.cc:775-841), stereo: close points only;
+        a keyframe is redundant when 90 % of them are seen by >= 3 other keyframes at the same or
+        a finer scale."""
+        th_depth = self.settings.th_depth
+        for k in list(kf.covisible):
+            if k.id == 0:
+                continue
+            n_mps = n_red = 0
+            for i, mp in enumerate(k.map_points):
+                if mp is None or mp.bad:
+                    continue
+                if k.depth[i] > th_depth or k.depth[i] < 0:
+                    continue
+                n_mps += 1
+                if mp.nobs > 3:
+                    level = int(k.keys_un[i]["octave"])
+                    n = 0
+                    for ki in sorted(mp.observations, key=lambda x: x.id):
+                        if ki is k:
+                            continue
+                        if int(ki.keys_un[mp.observations[ki]]["octave"]) <= level + 1:
+                            n += 1
+                            if n >= 3:
+                                break
+                    if n >= 3:
+                        n_red += 1
+            if n_red > 0.9 * n_mps:
+                k.set_bad()
 
     def backend_has_bow(self) -> bool:
         return getattr(self.backend, "vocab", None) is not None
@@ -682,6 +996,13 @@ class StereoSLAM:
             elif mp.nobs > 0:
                 nmap += 1
         return nmap
+
+    def _check_replaced_in_last_frame(self):
+        """Tracking::CheckReplacedInLastFrame: map points the LocalMapping replaced (Fuse)."""
+        lf = self.last_frame
+        for i, mp in enumerate(lf.map_points):
+            if mp is not None and mp.replaced is not None:
+                lf.map_points[i] = mp.replaced
 
     def _update_last_frame(self):
         """Tracking::UpdateLastFrame (src/Tracking.cc:919-995) in SLAM mode: only the pose."""
@@ -811,11 +1132,14 @@ class StereoSLAM:
             if mp.bad:
                 cf.map_points[i] = None
             else:
+                mp.visible += 1   # IncreaseVisible
                 seen.add(id(mp))
                 occ[i] = 1 if mp.nobs > 0 else 0
         mps = self.local_mps
         rec = self._mp_records(mps, seen)
-        m_mp, nl = self.backend.search_local_points(self._frame(cf), occ, rec, 1.0)
+        m_mp, nl, in_view = self.backend.search_local_points(self._frame(cf), occ, rec, 1.0)
+        for j in np.nonzero(np.asarray(in_view))[0]:   # isInFrustum -> IncreaseVisible
+            mps[int(j)].visible += 1
         st["local_map_points"] = len(mps)
         st["local_matches"] = nl
         m_lf = np.full(cf.n, -1, np.int32)
@@ -837,6 +1161,7 @@ class StereoSLAM:
             if mp is None:
                 continue
             if not cf.outlier[i]:
+                mp.found += 1   # IncreaseFound
                 if mp.nobs > 0:
                     inliers += 1
             elif cf.u_right[i] >= 0:   # stereo outliers are dropped

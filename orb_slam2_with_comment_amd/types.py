@@ -134,6 +134,13 @@ POSE_FRAME_DTYPE = np.dtype([("tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"), (
 assert POSE_OBS_DTYPE.itemsize == 32 and POSE_FRAME_DTYPE.itemsize == 100
 
 
+class TriKeyFrame(C.Structure):
+    """orbmi_tri_keyframe: the KeyFrame members CreateNewMapPoints reads (include/orbmi.h)."""
+    _fields_ = [("tcw", C.c_void_p), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("depth", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("mb", C.c_float), ("level_sigma2", C.c_void_p), ("scale_factors", C.c_void_p)]
+
+
 class FrameMapPoints(C.Structure):
     """orbmi_frame_mappoints: Frame::mvpMapPoints as match arrays (include/orbmi.h)."""
     _fields_ = [("match_lf", C.c_void_p), ("lf_points", C.c_void_p), ("n_lf_points", C.c_int),

@@ -52,8 +52,18 @@ class OracleBackend:
         self._count("search_local_points")
         tr = self.O.is_in_frustum(cf, mps, 0.5)
         if not np.any(tr["in_view"]):
-            return np.full(len(cf.keys), -1, np.int32), 0
-        return self.O.search_by_projection_local(cf, occupied, mps, tr, th, 0.8)
+            return np.full(len(cf.keys), -1, np.int32), 0, tr["in_view"].astype(bool)
+        m, n = self.O.search_by_projection_local(cf, occupied, mps, tr, th, 0.8)
+        return m, n, tr["in_view"].astype(bool)
+
+    def search_for_triangulation(self, kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12):
+        self._count("search_for_triangulation")
+        return self.O.search_for_triangulation(kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, False, False)
+
+    def fuse_search(self, kf, mps, in_kf, th=3.0):
+        self._count("fuse_search")
+        bi, bd, _ = self.O.fuse_search(kf, mps, in_kf, th)
+        return bi, bd
 
     def pose_optimization(self, cf, match_lf=None, lf_points=None, match_mp=None, mps=None):
         self._count("pose_optimization")
