@@ -373,10 +373,12 @@ def profile_stages(handle, run_step, n):
     padded = [(w + 38) * (h + 38) for w, h in zip(W, H)]
     cand_img, kp_img = cand / 2, kp / 2
     alg = {
-        "pyr_level0": 2 * (W[0] * H[0] + padded[0]),
+        # k_pyramid builds every level in one launch (stage pyr_level0): the image in, padded levels out
+        "pyr_level0": 2 * (W[0] * H[0] + sum(padded)),
         "pyr_resize": 2 * sum(W[l - 1] * H[l - 1] + padded[l] for l in range(1, 8)) / 7,
         "fast": 2 * (P + 4 * cand_img),
-        "octree": 2 * (4 * cand_img + 8 * kp_img),
+        # k_octree also blurs every level (the blur tiles run as extra workgroups of the launch)
+        "octree": 2 * (4 * cand_img + 8 * kp_img) + 2 * (2 * P),
         "describe": 2 * kp_img * (37 * 37 + 31 * 31 + 60),
         "blur": 2 * (2 * P),
         "stereo_rows": kp_img * 28 * 2,

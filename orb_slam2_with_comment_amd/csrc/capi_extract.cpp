@@ -231,23 +231,28 @@ extern "C" int orbmi_debug_fast_candidates(orbmi_extractor* h, int item, int lev
         return ORBMI_E_STATE;
     ORBMI_HIP(hipSetDevice(e.device));
     ORBMI_HIP(hipStreamSynchronize(e.stream));
-    const orbmi::LevelGeom& g = e.levels[level];
-    const int ncells = (int)e.cells.size();
-    std::vector<int> counts(ncells);
-    std::vector<uint32_t> slots(e.nslots);
-    ORBMI_HIP(hipMemcpy(counts.data(), e.d_cell_counts + (size_t)item * ncells, ncells * sizeof(int),
-                        hipMemcpyDeviceToHost));
-    ORBMI_HIP(hipMemcpy(slots.data(), e.d_slots + (size_t)item * e.nslots, (size_t)e.nslots * 4,
-                        hipMemcpyDeviceToHost));
+    int rc_[orbmi::kFastRegions];
+    ORBMI_HIP(hipMemcpy(rc_, e.d_level_count + ((size_t)item * e.nlevels + level) * orbmi::kFastRegions,
+                        sizeof(rc_), hipMemcpyDeviceToHost));
+    std::vector<uint2> cand;
+    for (int j = 0; j < orbmi::kFastRegions; j++) {
+        if (rc_[j] <= 0) continue;
+        const size_t at = cand.size();
+        cand.resize(at + rc_[j]);
+        ORBMI_HIP(hipMemcpy(cand.data() + at, e.d_cand + (size_t)item * e.keys_cap + e.regbase[level * orbmi::kFastRegions + j],
+                            rc_[j] * sizeof(uint2), hipMemcpyDeviceToHost));
+    }
+    const int count = (int)cand.size();
+    // k_fast's dense array is in cell-completion order; the tags restore the cell loop's order
+    std::sort(cand.begin(), cand.end(), [](const uint2& a, const uint2& b) { return a.y < b.y; });
     int n = 0;
-    for (int c = g.cell_begin; c < g.cell_end; c++)
-        for (int k = 0; k < counts[c]; k++, n++)
-            if (n < cap) {
-                const uint32_t v = slots[e.cells[c].slot_base + k];
-                xyr[3 * n] = v & 0xFFF;
-                xyr[3 * n + 1] = (v >> 12) & 0xFFF;
-                xyr[3 * n + 2] = v >> 24;
-            }
+    for (int k = 0; k < count; k++, n++)
+        if (n < cap) {
+            const uint32_t v = cand[k].x;
+            xyr[3 * n] = v & 0xFFF;
+            xyr[3 * n + 1] = (v >> 12) & 0xFFF;
+            xyr[3 * n + 2] = v >> 24;
+        }
     *n_out = n;
     return n > cap ? ORBMI_E_CAP : ORBMI_OK;
 }

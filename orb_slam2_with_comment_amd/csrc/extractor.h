@@ -31,14 +31,18 @@ struct LevelGeom {
 struct CellGeom {
     short x0, y0, w, h;  // ROI in interior coordinates; w == 0 -> skipped cell
     short sx, sy;        // j*wCell, i*hCell shift added to ROI coordinates
-    int slot_base;       // first candidate slot (per image)
+    int slot_base;       // base of the cell's candidate region (per image; cells of one level
+                         // share kFastRegions regions, cell k of the level writes region k % R)
     int level;
 };
 
 struct XTab { short sx0, sx1, a0, a1; };  // horizontal resize: source taps and 11-bit weights
 struct YTab { short y0, y1, b0, b1; };    // vertical resize
+struct PyrRect { short x0, x1, y0, y1; };  // half-open interior rectangle of one level
+struct PyrTile { PyrRect own, need; };     // k_pyramid tile of one level: written to HBM / computed in LDS
 
 constexpr int kOctNodeCap = 2048;  // live quadtree nodes per level held in LDS
+constexpr int kFastRegions = 16;   // candidate regions per level (spreads k_fast's allocation atomics)
 constexpr int kBlurTW = 128, kBlurTH = 32;  // GaussianBlur output tile
 
 // Grow-only device buffer.
@@ -68,7 +72,7 @@ struct Extractor {
     std::vector<int2> btiles;
     long long pimg = 0;      // bytes of one padded pyramid
     long long bimg = 0;      // bytes of one blurred pyramid
-    int nslots = 0, keys_cap = 0, out_cap = 0;
+    int keys_cap = 0, out_cap = 0;
 
     // device buffers (capacity for `bcap` images)
     int bcap = 0;
@@ -81,10 +85,14 @@ struct Extractor {
     uint8_t* d_blur = nullptr;     // blurred levels: interior only, rows of bstride bytes
     int2* d_btiles = nullptr;      // blur tiles: {level, x0 | y0 << 16}
     int nbtiles = 0;
-    int* d_cell_counts = nullptr;
-    uint32_t* d_slots = nullptr;
-    uint32_t* d_keys = nullptr;
-    uint16_t* d_node_of = nullptr;
+    int* d_level_count = nullptr;   // [b][level][region] FAST candidates (k_fast allocates, k_pyr_level0 clears)
+    int* d_regbase = nullptr;       // [level][region] first slot of each candidate region (per image)
+    std::vector<uint32_t> pyr_blob; // k_pyramid parameter blocks, pyr_blob_words per tile
+    uint32_t* d_pyr_blob = nullptr;
+    int pyr_kx = 0, pyr_ky = 0, pyr_hx = 0, pyr_hy = 0, pyr_blob_words = 0, pyr_lds0 = 0, pyr_lds_half = 0;
+    std::vector<int> regbase;
+    uint2* d_cand = nullptr;        // [b][keys_cap] {x | y << 12 | score << 24, cell << 10 | rank}
+    uint32_t* d_node_of = nullptr;  // octree node | depth << 16 of keys beyond the register-resident ones
     uint2* d_oct = nullptr;        // {x | y << 16 (level coords), score}
     int* d_oct_count = nullptr;    // [b][level]
     // last outputs (host API and stereo input)

@@ -1,6 +1,6 @@
 // MI355X (gfx950) ORB extractor: ORBextractor::operator() (src/ORBextractor.cc:1043-1105)
 // as five kernel stages over a batch of images resident in HBM:
-//   k_pyr_level0 / k_pyr_resize   ComputePyramid            (:1107-1132)    one launch/level
+//   k_pyramid                     ComputePyramid            (:1107-1132)    one WG per tile, all levels
 //   k_fast                        cell FAST + NMS + fallback (:778-829)      one WG per cell
 //   k_octree                      DistributeOctTree          (:539-763)      one WG per level
 //   k_describe                    IC_Angle + GaussianBlur + computeOrbDescriptor (:77-147,
@@ -20,10 +20,145 @@ __constant__ signed char c_circle[768][2];  // (u, v) of the 749 IC_Angle patch 
 __constant__ int c_ncircle;
 
 // ------------------------------------------------------------------------------ pyramid
-// Level 0: copyMakeBorder(image, 19, BORDER_REFLECT_101) (src/ORBextractor.cc:1128-1129).
+// ComputePyramid (src/ORBextractor.cc:1107-1132) in one launch: level 0 = copyMakeBorder(image,
+// 19, BORDER_REFLECT_101); level l = resize(level l-1, INTER_LINEAR) + copyMakeBorder
+// (REFLECT_101|ISOLATED).  One workgroup per (image, tile of the level grid): for every level the
+// tile owns a rectangle (written to HBM, with the border pixels that mirror it) and computes a
+// `need` rectangle into LDS = its own rectangle plus the rows / columns the next level's need
+// rectangle reads (host-built, PyrTile), so the levels chain inside the workgroup with one
+// barrier per level and no HBM round trip.  Halo pixels are computed by every tile that needs
+// them, with the same formula.
+__device__ inline void pyr_store(uint8_t* lvl, int W, int H, int stride, int x, int y, uint8_t v) {
+    // interior (x, y) and every border pixel mirroring it (one reflection: W, H > kEdge)
+    int xs[3], ys[3], nx = 0, ny = 0;
+    xs[nx++] = x;
+    if (x >= 1 && x <= kEdge) xs[nx++] = -x;
+    if (x >= W - 1 - kEdge && x <= W - 2) xs[nx++] = 2 * W - 2 - x;
+    ys[ny++] = y;
+    if (y >= 1 && y <= kEdge) ys[ny++] = -y;
+    if (y >= H - 1 - kEdge && y <= H - 2) ys[ny++] = 2 * H - 2 - y;
+    for (int j = 0; j < ny; j++)
+        for (int i = 0; i < nx; i++) lvl[(long long)(ys[j] + kEdge) * stride + xs[i] + kEdge] = v;
+}
+
+// cv::resize INTER_LINEAR 8U of one pixel from its four taps (pinned P2: the SSE2 vertical pass
+// for x < resize_xv, the scalar tail after it).
+__device__ inline int pyr_resize_px(int p00, int p01, int p10, int p11, const XTab& x, const YTab& y, bool vec) {
+    const int h0 = p00 * x.a0 + p01 * x.a1;
+    const int h1 = p10 * x.a0 + p11 * x.a1;
+    int v;
+    if (vec)  // VResizeLinearVec_32s8u lanes
+        v = ((((h0 >> 4) * y.b0) >> 16) + (((h1 >> 4) * y.b1) >> 16) + 2) >> 2;
+    else
+        v = (h0 * y.b0 + h1 * y.b1 + (1 << 21)) >> 22;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+constexpr int kPyrThreads = 1024;  // 64 columns x 16 rows per step
+constexpr int kPyrRows = kPyrThreads / 64;
+constexpr int kPyrTiledMaxBatch = 8;  // larger batches build the pyramid level by level
+constexpr int kPyrLevelWords = 10; // per level in a tile's parameter block (PyrBlob, host)
+
+// global -> LDS copy of n elements with kInFlight loads issued before the first store
+template <int kInFlight, class T, class F>
+__device__ inline void pyr_stage(T* dst, int n, F&& load) {
+    for (int i0 = 0; i0 < n; i0 += kInFlight * kPyrThreads) {
+        T v[kInFlight];
+#pragma unroll
+        for (int k = 0; k < kInFlight; k++) {
+            const int i = i0 + k * kPyrThreads + (int)threadIdx.x;
+            v[k] = i < n ? load(i) : T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < kInFlight; k++) {
+            const int i = i0 + k * kPyrThreads + (int)threadIdx.x;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
+// The tile's level-0 need rectangle is its own rectangle grown by (hx, hy) (host: the largest
+// halo of any tile), so it follows from blockIdx alone and the image loads go out together with
+// the tile's parameter block (rectangles, level geometry, the resize taps of its need
+// rectangles): one HBM round trip before all levels run out of LDS.
+// It also clears the image's per-level candidate counters (k_fast allocates from them).
+__global__ __launch_bounds__(kPyrThreads) void k_pyramid(const uint8_t* __restrict__ img, size_t step,
+                                                         size_t img_stride, uint8_t* __restrict__ pyr, long long pimg,
+                                                         const uint32_t* __restrict__ blobs, int blob_words,
+                                                         int nlevels, int KX, int KY, int W0, int H0, int hx, int hy,
+                                                         int* __restrict__ level_count, int lds0, int lds_half) {
+    extern __shared__ uint32_t pw[];  // parameter block | level-0 rectangle | two need rectangles
+    uint32_t* B = pw;
+    uint8_t* L0 = reinterpret_cast<uint8_t*>(pw + blob_words);
+    uint8_t* H2 = L0 + lds0;
+    const int t = blockIdx.x, b = blockIdx.z, tid = threadIdx.x;
+    const int tx = tid & 63, ty = tid >> 6;
+    if (t == 0 && tid < nlevels * kFastRegions) level_count[b * nlevels * kFastRegions + tid] = 0;
+    const uint8_t* im = img + b * img_stride;
+    uint8_t* P = pyr + b * pimg;
+    const int cx = t % KX, cy = t / KX;
+    const int ox0 = W0 * cx / KX, ox1 = W0 * (cx + 1) / KX, oy0 = H0 * cy / KY, oy1 = H0 * (cy + 1) / KY;
+    const int nx0 = max(ox0 - hx, 0), nx1 = min(ox1 + hx, W0), ny0 = max(oy0 - hy, 0), ny1 = min(oy1 + hy, H0);
+    const int w0 = nx1 - nx0, a0 = w0 * (ny1 - ny0);
+    const uint32_t* bl = blobs + (size_t)t * blob_words;
+    pyr_stage<4>(B, blob_words, [&](int i) { return bl[i]; });
+    pyr_stage<24>(L0, a0, [&](int i) {
+        const int r = i / w0;
+        return im[(size_t)(ny0 + r) * step + nx0 + (i - r * w0)];
+    });
+    __syncthreads();
+    auto lo16 = [](uint32_t w) { return (int)(short)(w & 0xFFFF); };
+    auto hi16 = [](uint32_t w) { return (int)(short)(w >> 16); };
+    {   // level 0: the own rectangle with its border mirrors
+        const uint32_t* G = B;
+        const int W = lo16(G[4]), H = hi16(G[4]), stride = (int)G[5];
+        uint8_t* lvl = P + G[6];
+        for (int y = oy0 + ty; y < oy1; y += kPyrRows)
+            for (int x = ox0 + tx; x < ox1; x += 64) pyr_store(lvl, W, H, stride, x, y, L0[(y - ny0) * w0 + x - nx0]);
+    }
+    int snx0 = nx0, sny0 = ny0, sw = w0;  // the source need rectangle of the next level
+    for (int l = 1; l < nlevels; l++) {
+        const uint32_t* G = B + l * kPyrLevelWords;
+        const int o_x0 = lo16(G[0]), o_x1 = hi16(G[0]), o_y0 = lo16(G[1]), o_y1 = hi16(G[1]);
+        const int n_x0 = lo16(G[2]), n_x1 = hi16(G[2]), n_y0 = lo16(G[3]), n_y1 = hi16(G[3]);
+        const int W = lo16(G[4]), H = hi16(G[4]), stride = (int)G[5], rxv = (int)G[7];
+        uint8_t* lvl = P + G[6];
+        const uint32_t* XT = B + G[8];  // 2 words per column of the need rectangle
+        const uint32_t* YT = B + G[9];  // 2 words per row
+        const uint8_t* src = l == 1 ? L0 : H2 + ((l - 1) & 1) * lds_half;
+        uint8_t* dst = H2 + (l & 1) * lds_half;
+        const int nw = n_x1 - n_x0;
+        const bool keep = l + 1 < nlevels;
+        for (int y = n_y0 + ty; y < n_y1; y += kPyrRows) {
+            const uint32_t y0w = YT[2 * (y - n_y0)], y1w = YT[2 * (y - n_y0) + 1];
+            const YTab yy{(short)lo16(y0w), (short)hi16(y0w), (short)lo16(y1w), (short)hi16(y1w)};
+            const uint8_t* r0 = src + (yy.y0 - sny0) * sw - snx0;
+            const uint8_t* r1 = src + (yy.y1 - sny0) * sw - snx0;
+            for (int x = n_x0 + tx; x < n_x1; x += 64) {
+                const uint32_t x0w = XT[2 * (x - n_x0)], x1w = XT[2 * (x - n_x0) + 1];
+                const XTab xx{(short)lo16(x0w), (short)hi16(x0w), (short)lo16(x1w), (short)hi16(x1w)};
+                const uint8_t v = (uint8_t)pyr_resize_px(r0[xx.sx0], r0[xx.sx1], r1[xx.sx0], r1[xx.sx1], xx, yy, x < rxv);
+                if (keep) dst[(y - n_y0) * nw + (x - n_x0)] = v;
+                if (x >= o_x0 && x < o_x1 && y >= o_y0 && y < o_y1) pyr_store(lvl, W, H, stride, x, y, v);
+            }
+        }
+        snx0 = n_x0;
+        sny0 = n_y0;
+        sw = nw;
+        __syncthreads();
+    }
+}
+
+// Large batches: one launch per level, a thread per padded output byte (the tiles' halo
+// recomputation costs more than the launches once the batch fills the chip).
+// Level 0: copyMakeBorder(image, 19, BORDER_REFLECT_101) (src/ORBextractor.cc:1128-1129); it
+// also clears the per-level candidate counters.
 __global__ void k_pyr_level0(const uint8_t* __restrict__ img, size_t step, size_t img_stride,
-                             uint8_t* __restrict__ pyr, long long pimg, LevelGeom g) {
+                             uint8_t* __restrict__ pyr, long long pimg, LevelGeom g, int* __restrict__ level_count,
+                             int nlevels) {
     const int xp = blockIdx.x * blockDim.x + threadIdx.x, yp = blockIdx.y, b = blockIdx.z;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nlevels * kFastRegions)
+        level_count[b * nlevels * kFastRegions + threadIdx.x] = 0;
     if (xp >= g.W + 2 * kEdge) return;
     const int ix = reflect101(xp - kEdge, g.W), iy = reflect101(yp - kEdge, g.H);
     pyr[b * pimg + g.off + (long long)yp * g.stride + xp] = img[b * img_stride + (size_t)iy * step + ix];
@@ -41,19 +176,15 @@ __global__ void k_pyr_resize(uint8_t* __restrict__ pyr, long long pimg, LevelGeo
     const YTab y = yt[iy];
     const uint8_t* r0 = src + (long long)y.y0 * s.stride;
     const uint8_t* r1 = src + (long long)y.y1 * s.stride;
-    const int h0 = r0[x.sx0] * x.a0 + r0[x.sx1] * x.a1;
-    const int h1 = r1[x.sx0] * x.a0 + r1[x.sx1] * x.a1;
-    int v;
-    if (ix < d.resize_xv)  // VResizeLinearVec_32s8u (SSE2) lanes
-        v = ((((h0 >> 4) * y.b0) >> 16) + (((h1 >> 4) * y.b1) >> 16) + 2) >> 2;
-    else
-        v = (h0 * y.b0 + h1 * y.b1 + (1 << 21)) >> 22;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    pyr[b * pimg + d.off + (long long)yp * d.stride + xp] = (uint8_t)v;
+    pyr[b * pimg + d.off + (long long)yp * d.stride + xp] =
+        (uint8_t)pyr_resize_px(r0[x.sx0], r0[x.sx1], r1[x.sx0], r1[x.sx1], x, y, ix < d.resize_xv);
 }
 
 // ------------------------------------------------------------------------------ FAST
-constexpr int kTile = 64;  // max cell ROI edge (wCell+6, hCell+6)
+constexpr int kTile = 64;               // max cell ROI edge (wCell+6, hCell+6)
+constexpr int kTileS = 68;              // LDS row pitch of a staged ROI row (17 dwords)
+constexpr int kFastCells = 2;           // waves (cells) per workgroup
+constexpr int kFastList = 58 * 58;      // scored pixels of the largest ROI
 
 // LDS writes of this wave visible to its own later reads (wave-private LDS regions)
 __device__ inline void wave_sync_lds_ex() {
@@ -63,16 +194,21 @@ __device__ inline void wave_sync_lds_ex() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ inline int fast_score16_p(const uint8_t* t, int pitch, int x, int y, int th) {
-    // OpenCV offsets16: (dx,dy) of the radius-3 Bresenham circle.
+// The 16 pixels of OpenCV's offsets16 (radius-3 Bresenham circle, (dx, dy)) around (x, y).
+__device__ inline void fast_circle(const uint8_t* t, int pitch, int x, int y, int p[16]) {
     const int o[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
                           {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
-    const int v = t[y * pitch + x];
-    int p[16];
+    const uint8_t* c = t + y * pitch + x;
+#pragma unroll
+    for (int k = 0; k < 16; k++) p[k] = c[o[k][1] * pitch + o[k][0]];
+}
+
+// FAST_t's segment test: 9 contiguous circle pixels (the 25-long wrapped scan) all brighter
+// than v + th or all darker than v - th.
+__device__ inline bool fast_segment(int v, const int p[16], int th) {
     unsigned bright = 0, dark = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        p[k] = t[(y + o[k][1]) * pitch + x + o[k][0]];
         bright |= (unsigned)(p[k] > v + th) << k;
         dark |= (unsigned)(p[k] < v - th) << k;
     }
@@ -82,8 +218,14 @@ __device__ inline int fast_score16_p(const uint8_t* t, int pitch, int x, int y, 
         for (int s = 1; s <= 8; s++) r &= m2 >> s;
         return (r & 0xFFFFu) != 0;
     };
-    if (!arc9(bright) && !arc9(dark)) return 0;
-    // cornerScore<16>  (OpenCV fast_score.cpp), d[k] = v - p[k mod 16], k < 25
+    return arc9(bright) || arc9(dark);
+}
+
+// cornerScore<16> (OpenCV fast_score.cpp), d[k] = v - p[k mod 16], k < 25, stored as uchar.
+// For a pixel that passes the segment test at th the value does not depend on th, and the
+// pixel passes at any t >= th exactly when the value is >= t (checked exhaustively against the
+// scalar restatement over 7.5e7 patches): one score per pixel serves both thresholds.
+__device__ inline int fast_corner_score(int v, const int p[16], int th) {
     int d[25];
 #pragma unroll
     for (int k = 0; k < 25; k++) d[k] = v - p[k & 15];
@@ -115,39 +257,43 @@ __device__ inline int fast_score16_p(const uint8_t* t, int pitch, int x, int y, 
         b0 = min(b0, max(bb, d[k]));
         b0 = min(b0, max(bb, d[k + 9]));
     }
-    return (-b0 - 1) & 0xFF;  // stored as uchar (FAST_t: curr[j] = (uchar)cornerScore)
+    return (-b0 - 1) & 0xFF;
 }
 
-__device__ inline bool nms_keep(const uint8_t* sc, int x, int y) {
-    const int s = sc[y * kTile + x];
-    if (!s) return false;
-    return s > sc[(y - 1) * kTile + x - 1] && s > sc[(y - 1) * kTile + x] && s > sc[(y - 1) * kTile + x + 1] &&
-           s > sc[y * kTile + x - 1] && s > sc[y * kTile + x + 1] &&
-           s > sc[(y + 1) * kTile + x - 1] && s > sc[(y + 1) * kTile + x] && s > sc[(y + 1) * kTile + x + 1];
+__device__ inline int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// One wave per (image, cell), four cells per workgroup, so every step syncs at wave level only.
-// The cell ROI (<= 64 x 64) is staged in the wave's LDS as aligned dwords (its first byte at a
-// per-cell offset 0..3); scores, strict 3x3 NMS, and a ballot compaction that emits the
-// survivors row-major (FAST_t emission order) as x | y << 12 | score << 24 with x, y relative to
-// minBorder (:820-825).  A cell retries with min_th when ini_th finds nothing (:804-817).
-constexpr int kFastCells = 4;           // waves (cells) per workgroup
-constexpr int kTileS = 68;              // LDS row pitch of a staged ROI row (17 dwords)
+// One wave per (image, cell), kFastCells cells per workgroup, so every step syncs at wave level
+// only.  The cell ROI (<= 64 x 64) is staged in the wave's LDS as aligned dwords (its first byte
+// at a per-cell offset 0..3).  FAST with nonmax at ini_th, then at min_th when that finds
+// nothing (src/ORBextractor.cc:804-817), as four compaction stages over a row-major pixel list
+// (u16 y << 6 | x, ballot-compacted in place, so the order is FAST_t's emission order):
+//   A  every scored pixel: two cyclically adjacent compass pixels (0, 4, 8, 12) both brighter or
+//      both darker at t = min(ini_th, min_th) -- necessary for a 9-arc (any 9 consecutive of 16
+//      hold two adjacent multiples of 4);
+//   B  the survivors: the full segment test at t;
+//   C  the corners: cornerScore into the cell's score map;
+//   D  strict 3x3 NMS of the corners at ini_th (score >= ini_th; neighbours below it count 0),
+//      compacted in place; when none survives, the same at min_th.
+// The survivors go to one of the level's kFastRegions dense candidate regions (cell k of the
+// level: region k % R) at an offset taken with one atomic per cell, as {x | y << 12 | score << 24
+// (x, y relative to minBorder, :820-825), cell << 10 | rank}: the tag orders them as the
+// reference's cell loop does, so their position does not matter.
 __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restrict__ pyr, long long pimg,
                                                           const LevelGeom* __restrict__ levels,
                                                           const CellGeom* __restrict__ cells, int ncells,
-                                                          uint32_t* __restrict__ slots, int nslots,
-                                                          int* __restrict__ cell_counts, int ini_th, int min_th) {
+                                                          uint2* __restrict__ cand, int keys_cap,
+                                                          int* __restrict__ level_count, int nlevels, int ini_th,
+                                                          int min_th) {
     __shared__ unsigned tiles[kFastCells][kTile * kTileS / 4];
-    __shared__ uint8_t scores[kFastCells][kTile * kTile];
+    __shared__ uint4 scores4[kFastCells][kTile * kTile / 16];
+    __shared__ unsigned short lists[kFastCells][kFastList];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.x * kFastCells + wid, b = blockIdx.y;
     if (c >= ncells) return;
     const CellGeom cg = cells[c];
-    if (cg.w == 0) {
-        if (lane == 0) cell_counts[b * ncells + c] = 0;
-        return;
-    }
+    if (cg.w == 0) return;
     const LevelGeom lg = levels[cg.level];
     const long long a = b * pimg + lg.off + (long long)(kEdge + cg.y0) * lg.stride + kEdge + cg.x0;
     const int o = (int)(a & 3);  // stride is a multiple of 64: the same offset on every row
@@ -167,45 +313,107 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
             if (r < h) t4[r * (kTileS / 4) + d] = v[k];
         }
     }
-    // fast_score16 / nms_keep address a kTile-pitched tile: re-pack the staged rows
-    uint8_t* sc = scores[wid];
+#pragma unroll
+    for (int k = 0; k < kTile * kTile / 16 / 64; k++) scores4[wid][lane + 64 * k] = make_uint4(0u, 0u, 0u, 0u);
+    uint8_t* sc = reinterpret_cast<uint8_t*>(scores4[wid]);  // sc[y * kTile + x]
+    unsigned short* L = lists[wid];
     wave_sync_lds_ex();
     const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * kTileS + x]
     const int dw = w - 6, dh = h - 6, npix = dw > 0 && dh > 0 ? dw * dh : 0;
+    const int ti = min(max(ini_th, 0), 255), tm = min(max(min_th, 0), 255), tl = min(ti, tm);
+    // A: compass pre-test over the ROI's scored pixels, row-major
+    int n = 0;
+    if (npix > 0) {
+        int y = lane / dw, x = lane - y * dw;
+        const int q = 64 / dw, r = 64 - q * dw;
+        for (int p0 = 0; p0 < npix; p0 += 64) {
+            bool pass = false;
+            const int X = x + 3, Y = y + 3;
+            if (p0 + lane < npix) {
+                const uint8_t* cp = tb + Y * kTileS + X;
+                const int v = cp[0], hi = v + tl, lo = v - tl;
+                const int pa = cp[3 * kTileS], pb = cp[3], pc = cp[-3 * kTileS], pd = cp[-3];
+                const bool ba = pa > hi, bb = pb > hi, bc = pc > hi, bd = pd > hi;
+                const bool da = pa < lo, db = pb < lo, dc = pc < lo, dd = pd < lo;
+                pass = (ba & bb) | (bb & bc) | (bc & bd) | (bd & ba) | (da & db) | (db & dc) | (dc & dd) | (dd & da);
+            }
+            const unsigned long long m = __ballot(pass);
+            if (pass) L[n + lanes_below(m)] = (unsigned short)(Y << 6 | X);
+            n += __popcll(m);
+            x += r;
+            y += q;
+            if (x >= dw) { x -= dw; y++; }
+        }
+    }
+    wave_sync_lds_ex();
+    // B: full segment test, compacted in place (a lane writes at or below the entry it read)
+    int nc = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        bool pass = false;
+        unsigned short e = 0;
+        if (i < n) {
+            e = L[i];
+            const int X = e & 63, Y = e >> 6;
+            int p[16];
+            fast_circle(tb, kTileS, X, Y, p);
+            pass = fast_segment(tb[Y * kTileS + X], p, tl);
+        }
+        const unsigned long long m = __ballot(pass);
+        if (pass) L[nc + lanes_below(m)] = e;
+        nc += __popcll(m);
+    }
+    wave_sync_lds_ex();
+    // C: scores of the corners
+    for (int i = lane; i < nc; i += 64) {
+        const unsigned short e = L[i];
+        const int X = e & 63, Y = e >> 6;
+        int p[16];
+        fast_circle(tb, kTileS, X, Y, p);
+        sc[Y * kTile + X] = (uint8_t)fast_corner_score(tb[Y * kTileS + X], p, tl);
+    }
+    wave_sync_lds_ex();
+    // D: strict NMS at ini_th, then at min_th if nothing survived; survivors compacted in place
     int total = 0;
     for (int pass = 0; pass < 2; pass++) {
-        int th = pass == 0 ? ini_th : min_th;
-        th = min(max(th, 0), 255);
-        for (int i = lane; i < kTile * h; i += 64) sc[i] = 0;
-        wave_sync_lds_ex();
-        for (int p = lane; p < npix; p += 64) {
-            const int y = 3 + p / dw, x = 3 + p % dw;
-            sc[y * kTile + x] = (uint8_t)fast_score16_p(tb, kTileS, x, y, th);
-        }
-        wave_sync_lds_ex();
-        total = 0;
-        for (int p0 = 0; p0 < npix; p0 += 64) {
-            const int p = p0 + lane;
-            const bool k = p < npix && nms_keep(sc, 3 + p % dw, 3 + p / dw);
-            total += __popcll(__ballot(k));
-        }
-        if (total > 0) break;
-    }
-    if (total > 0) {
-        uint32_t* out = slots + (long long)b * nslots + cg.slot_base;
-        int r = 0;
-        for (int p0 = 0; p0 < npix; p0 += 64) {
-            const int p = p0 + lane;
-            const int y = 3 + p / dw, x = 3 + p % dw;
-            const bool k = p < npix && nms_keep(sc, x, y);
-            const unsigned long long m = __ballot(k);
-            if (k)
-                out[r + __popcll(m & ((1ull << lane) - 1))] =
-                    (uint32_t)(x + cg.sx) | ((uint32_t)(y + cg.sy) << 12) | ((uint32_t)sc[y * kTile + x] << 24);
-            r += __popcll(m);
+        if (pass == 1 && (total > 0 || tm == ti)) break;
+        const int t = pass == 0 ? ti : tm;
+        for (int i0 = 0; i0 < nc; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            unsigned short e = 0;
+            if (i < nc) {
+                e = L[i];
+                const uint8_t* q = sc + (e >> 6) * kTile + (e & 63);
+                const int s = q[0];
+                if (s >= t && s != 0) {
+                    auto nb = [&](int off) {
+                        const int u = q[off];
+                        return u >= t ? u : 0;
+                    };
+                    keep = s > nb(-kTile - 1) && s > nb(-kTile) && s > nb(-kTile + 1) && s > nb(-1) && s > nb(1) &&
+                           s > nb(kTile - 1) && s > nb(kTile) && s > nb(kTile + 1);
+                }
+            }
+            const unsigned long long m = __ballot(keep);
+            if (keep) L[total + lanes_below(m)] = e;
+            total += __popcll(m);
         }
     }
-    if (lane == 0) cell_counts[b * ncells + c] = total;
+    if (total == 0) return;
+    wave_sync_lds_ex();
+    int base = 0;
+    if (lane == 0)
+        base = atomicAdd(&level_count[(b * nlevels + cg.level) * kFastRegions + (c - lg.cell_begin) % kFastRegions], total);
+    base = __shfl(base, 0);
+    uint2* dst = cand + (long long)b * keys_cap + cg.slot_base + base;
+    const unsigned tag = (unsigned)(c - lg.cell_begin) << 10;
+    for (int i = lane; i < total; i += 64) {
+        const unsigned short e = L[i];
+        const int X = e & 63, Y = e >> 6;
+        dst[i] = make_uint2((uint32_t)(X + cg.sx) | ((uint32_t)(Y + cg.sy) << 12) | ((uint32_t)sc[Y * kTile + X] << 24),
+                            tag | (unsigned)i);
+    }
 }
 
 // ------------------------------------------------------------------------------ octree
@@ -216,7 +424,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
 // -- two prefix scans.  Keys never move: each key carries the index of its node, remapped
 // after every pass through the parent's (node, quadrant) -> child table.
 constexpr int kOctThreads = 1024;
-constexpr int kOctRegKeys = 16;  // candidates per thread held in registers (16,384 per level)
+constexpr int kOctRegKeys = 12;  // candidates per thread held in registers (12,288 per level; 13 spills)
 #ifdef ORBMI_OCT_TRACE  // tools/octree_trace.hip: s_memtime stamps of (level 0, image 0)
 __device__ unsigned long long g_oct_trace[256];
 #define OCT_STAMP(i, v)                                                                      \
@@ -230,7 +438,6 @@ __device__ unsigned long long g_oct_trace[256];
 #endif
 
 struct OctShared {
-    short4 box[2][kOctNodeCap];          // x0, y0, x1, y1 (UL = (x0,y0), BR = (x1,y1))
     int cnt[2][kOctNodeCap];
     int ccnt[kOctNodeCap][4];            // child key counts; reused as best-key words
     short remap[kOctNodeCap][4];         // (old node, quadrant) -> new index
@@ -240,23 +447,41 @@ struct OctShared {
     unsigned char dflag[kOctNodeCap];
     int scratch[kOctThreads / 64 + 2];
     int misc[8];
+    int rpre[kFastRegions + 1];          // candidate regions: prefix of counts, first slots
+    int rbase[kFastRegions];
+    unsigned tagl[kOctThreads * kOctRegKeys];  // order tags of the register-resident keys
 };
 
-__device__ inline int quadrant(short4 bx, int x, int y) {
-    const int halfX = (int)ceilf((float)(bx.z - bx.x) / 2);
-    const int halfY = (int)ceilf((float)(bx.w - bx.y) / 2);
-    return (x >= bx.x + halfX ? 1 : 0) | (y >= bx.y + halfY ? 2 : 0);
+// Quadrant decisions of one axis down the quadtree's fixed geometry: bit d is the decision at
+// depth d (coordinate >= the box's mid, mid = lo + ceil((hi - lo) / 2)).  A child's extent on an
+// axis depends only on the parent's extent on that axis and the decision
+// (ExtractorNode::DivideNode, src/ORBextractor.cc:481-537), so each axis descends alone and a
+// key's quadrant in its node at depth d is ((px >> d) & 1) | ((py >> d) & 1) << 1.  Coordinates
+// are < 4096, so two keys are separated within 13 divisions; 16 are kept.
+__device__ inline unsigned oct_axis(int v, int lo, int hi) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int d = 0; d < 16; d++) {
+        const int mid = lo + ((hi - lo + 1) >> 1);
+        const bool up = v >= mid;
+        bits |= (unsigned)up << d;
+        lo = up ? mid : lo;
+        hi = up ? hi : mid;
+    }
+    return bits;
 }
 
-__device__ inline short4 child_box(short4 bx, int q) {
-    const short mx = (short)(bx.x + (int)ceilf((float)(bx.z - bx.x) / 2));
-    const short my = (short)(bx.y + (int)ceilf((float)(bx.w - bx.y) / 2));
-    switch (q) {
-        case 0: return make_short4(bx.x, bx.y, mx, my);
-        case 1: return make_short4(mx, bx.y, bx.z, my);
-        case 2: return make_short4(bx.x, my, mx, bx.w);
-        default: return make_short4(mx, my, bx.z, bx.w);
-    }
+// Root node of a key (src/ORBextractor.cc:573-579) and its path bits (x low half, y high half).
+__device__ inline int oct_root(uint32_t key, const LevelGeom& g) {
+    return min((int)((float)(key & 0xFFF) / g.hX), g.nIni - 1);
+}
+__device__ inline unsigned oct_path(uint32_t key, const LevelGeom& g) {
+    const int n = oct_root(key, g);
+    const int x0 = (int)(g.hX * (float)n), x1 = (int)(g.hX * (float)(n + 1));
+    return oct_axis((int)(key & 0xFFF), x0, x1) | oct_axis((int)((key >> 12) & 0xFFF), 0, g.height) << 16;
+}
+__device__ inline int oct_quad(unsigned path, int depth) {
+    return (int)(((path >> depth) & 1u) | (((path >> (16 + depth)) & 1u) << 1));
 }
 
 // Exclusive scan of n <= kOctNodeCap ints in place (2 per thread); returns the total.
@@ -286,79 +511,84 @@ __device__ inline void bitonic_sort(unsigned long long* k, int n) {  // n power 
         }
 }
 
-__global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restrict__ levels,
-                                                         int nlevels, int ncells,
-                                                         const int* __restrict__ cell_counts,
-                                                         const CellGeom* __restrict__ cells,
-                                                         const uint32_t* __restrict__ slots, int nslots,
-                                                         uint32_t* __restrict__ keys,
-                                                         uint16_t* __restrict__ node_of, int keys_cap,
+// Bitonic sort of n <= blockDim.x keys, one per thread (v), ascending by thread index: stages
+// with a partner in the same wave exchange through lane shuffles, the others through LDS (lds,
+// >= blockDim.x entries) with block barriers; every thread of the block takes part.
+__device__ inline unsigned long long bitonic_sort_block(unsigned long long v, int n, unsigned long long* lds) {
+    const int i = threadIdx.x;
+    for (int size = 2; size <= n; size <<= 1)
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            unsigned long long other;
+            if (j >= 64) {
+                lds[i] = v;
+                __syncthreads();
+                other = lds[i ^ j];
+                __syncthreads();
+            } else {
+                other = __shfl_xor(v, j, 64);
+            }
+            const bool lower = (i & j) == 0, asc = (i & size) == 0;
+            v = (lower == asc) ? (v < other ? v : other) : (v < other ? other : v);
+        }
+    return v;
+}
+
+__device__ __forceinline__ void octree_body(OctShared& S, int level, int b, const LevelGeom* __restrict__ levels,
+                                            int nlevels, const uint2* __restrict__ cand,
+                                            const int* __restrict__ level_count, const int* __restrict__ regbase,
+                                            uint32_t* __restrict__ node_of, int keys_cap,
                                                          uint2* __restrict__ oct_out, int out_cap,
                                                          int* __restrict__ oct_count) {
-    __shared__ OctShared S;
-    const int level = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const LevelGeom g = levels[level];
-    const int c0 = g.cell_begin, nc = g.cell_end - g.cell_begin;
-    const int* cnts = cell_counts + b * ncells + c0;
-    uint32_t* K = keys + (long long)b * keys_cap + g.key_base;
-    uint16_t* NO = node_of + (long long)b * keys_cap + g.key_base;
+    const uint2* CK = cand + (long long)b * keys_cap;                 // {key, order tag}, regions
+    uint32_t* NO = node_of + (long long)b * keys_cap + g.key_base;     // node | depth << 16
 
     OCT_STAMP(0, __builtin_amdgcn_s_memtime());
-    // ---- gather candidates in original order (cells row-major, FAST order inside a cell):
-    // thread t holds keys t R .. t R + R - 1 in registers (R = kOctRegKeys, neighbours in the
-    // image, so a thread's increments mostly hit one counter); keys from kOctThreads R on
-    // spill to K / NO in global memory.  A key finds its cell by a binary search over
-    // the prefix of the cell counts, so every load of the gather is in flight at once.
+    // ---- the level's candidates (k_fast's dense array, in cell-completion order): thread t
+    // holds keys t R .. t R + R - 1 in registers (R = kOctRegKeys; a cell's keys are contiguous,
+    // so a thread's increments mostly hit one counter); keys from kOctThreads R on stay in CK
+    // with their node in NO.  Nothing below depends on the keys' order except through the tags.
+    // key k lives in region j with rpre[j] <= k < rpre[j + 1], at rbase[j] + k - rpre[j]
+    if (tid < 64) {
+        const int cnt = tid < kFastRegions ? level_count[(b * nlevels + level) * kFastRegions + tid] : 0;
+        const int incl = wave_incl_scan(cnt);
+        if (tid < kFastRegions) {
+            S.rpre[tid + 1] = incl;
+            S.rbase[tid] = regbase[level * kFastRegions + tid];
+        }
+        if (tid == 0) S.rpre[0] = 0;
+    }
+    __syncthreads();
+    const int nkeys = min(S.rpre[kFastRegions], g.key_cap);
+    auto key_slot = [&](int k, int& j) {  // j: a region at or before k's (walks forward)
+        while (j < kFastRegions - 1 && S.rpre[j + 1] <= k) j++;
+        return S.rbase[j] + (k - S.rpre[j]);
+    };
+    int j0 = 0;  // region of the thread's first key: the largest j with rpre[j] <= k
+    {
+        const int k0 = tid * kOctRegKeys;
+        int lo = 0, hi = kFastRegions - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.rpre[mid] <= k0) lo = mid;
+            else hi = mid - 1;
+        }
+        j0 = lo;
+    }
     uint32_t kreg[kOctRegKeys];
     int nreg[kOctRegKeys];
+    {
+        int j = j0;
 #pragma unroll
-    for (int r = 0; r < kOctRegKeys; r++) { kreg[r] = 0; nreg[r] = 0; }
-    int nkeys = 0;
-    for (int base = 0; base < nc; base += kOctNodeCap) {
-        const int n = min(kOctNodeCap, nc - base);
-        for (int i = tid; i < n; i += blockDim.x) {
-            S.tmp[i] = cnts[base + i];
-            S.newpos[i] = cells[c0 + base + i].slot_base;
+        for (int r = 0; r < kOctRegKeys; r++) {
+            const int k = tid * kOctRegKeys + r;
+            uint2 kv = make_uint2(0u, 0u);
+            if (k < nkeys) kv = CK[key_slot(k, j)];
+            kreg[r] = kv.x;
+            S.tagl[k] = kv.y;
+            nreg[r] = 0;
         }
-        __syncthreads();
-        const int tot = block_scan_array(S.tmp, n, S.scratch);
-        auto cell_of = [&](int kk) {  // kk in [0, tot): upper_bound over the prefix, minus one
-            int lo = 0, hi = n;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (S.tmp[mid] <= kk) lo = mid;
-                else hi = mid;
-            }
-            return lo;
-        };
-        auto fetch = [&](int kk) -> uint32_t {
-            const int lo = cell_of(kk);
-            return slots[(long long)b * nslots + S.newpos[lo] + (kk - S.tmp[lo])];
-        };
-        {
-            // one search for the thread's first key, then walk the cells forward; all slot
-            // addresses first, then the loads
-            const int k0 = tid * kOctRegKeys;
-            const int kk0 = max(k0 - nkeys, 0);
-            int lo = kk0 < tot ? cell_of(kk0) : 0;
-            long long addr[kOctRegKeys];
-#pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++) {
-                const int kk = k0 + r - nkeys;
-                addr[r] = -1;
-                if (kk >= 0 && kk < tot) {
-                    while (lo + 1 < n && S.tmp[lo + 1] <= kk) lo++;
-                    addr[r] = (long long)b * nslots + S.newpos[lo] + (kk - S.tmp[lo]);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++)
-                if (addr[r] >= 0) kreg[r] = slots[addr[r]];
-        }
-        for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys + tot; k += kOctThreads)
-            if (k >= nkeys) K[k] = fetch(k - nkeys);
-        nkeys += tot;
-        __syncthreads();
     }
     // f(k, key, node&) for every key, in increasing k per thread: the register-resident
     // ones, then the global spill
@@ -369,28 +599,45 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
             if (k < nkeys) f(k, kreg[r], nreg[r]);
         }
         for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
-            int no = NO[k];
-            f(k, K[k], no);
-            NO[k] = (uint16_t)no;
+            int no = (int)NO[k], j = 0;
+            f(k, CK[key_slot(k, j)].x, no);
+            NO[k] = (uint32_t)no;
         }
     };
 
+    // path bits of the register keys through per-axis tables (x: its own root's extent, y: the
+    // level height), built in the LDS of the careful-mode sort keys before any pass uses them
+    unsigned preg[kOctRegKeys];
+    {
+        unsigned short* xpath = reinterpret_cast<unsigned short*>(S.skey);
+        unsigned short* ypath = xpath + 4096;
+        const int wx = min(g.width, 4095), hy = min(g.height, 4095);
+        for (int v = tid; v <= wx + 1 + hy; v += blockDim.x) {
+            if (v <= wx) {
+                const int n = oct_root((uint32_t)v, g);
+                xpath[v] = (unsigned short)oct_axis(v, (int)(g.hX * (float)n), (int)(g.hX * (float)(n + 1)));
+            } else {
+                const int y = v - wx - 1;
+                ypath[y] = (unsigned short)oct_axis(y, 0, g.height);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++)
+            preg[r] = xpath[min((int)(kreg[r] & 0xFFF), wx)] | (unsigned)ypath[min((int)((kreg[r] >> 12) & 0xFFF), hy)] << 16;
+        __syncthreads();
+    }
     OCT_STAMP(1, __builtin_amdgcn_s_memtime());
     OCT_STAMP(62, nkeys);
     // ---- initial nodes (:543-579)
     const int nIni = g.nIni;
     int cur = 0;
-    for (int i = tid; i < nIni; i += blockDim.x) {
-        S.box[cur][i] = make_short4((short)(int)(g.hX * (float)i), 0, (short)(int)(g.hX * (float)(i + 1)),
-                                    (short)g.height);
-        S.cnt[cur][i] = 0;
-    }
+    for (int i = tid; i < nIni; i += blockDim.x) S.cnt[cur][i] = 0;
     __syncthreads();
     {
         int run = -1, rc = 0;  // consecutive keys of a thread share a node: one atomic per run
         for_keys([&](int, uint32_t key, int& no) {
-            int n = (int)((float)(key & 0xFFF) / g.hX);
-            n = min(n, nIni - 1);
+            const int n = oct_root(key, g);
             no = n;
             if (n != run) {
                 if (rc) atomicAdd(&S.cnt[cur][run], rc);
@@ -409,7 +656,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
     for (int i = tid; i < nIni; i += blockDim.x) {
         const short ni = S.cnt[cur][i] > 0 ? (short)S.tmp[i] : (short)-1;
         S.remap[i][0] = S.remap[i][1] = S.remap[i][2] = S.remap[i][3] = ni;
-        if (ni >= 0) { S.box[cur ^ 1][ni] = S.box[cur][i]; S.cnt[cur ^ 1][ni] = S.cnt[cur][i]; }
+        if (ni >= 0) S.cnt[cur ^ 1][ni] = S.cnt[cur][i];
     }
     cur ^= 1;
     __syncthreads();
@@ -424,37 +671,24 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         for (int i = tid; i < L; i += blockDim.x) {
             S.ccnt[i][0] = S.ccnt[i][1] = S.ccnt[i][2] = S.ccnt[i][3] = 0;
         }
+        if (tid == 0) S.misc[2 + (iter & 1)] = 0;  // read at the end of pass iter - 2
         __syncthreads();
         OCT_SUB(iter, 0);
-        // keys: apply the previous pass's remap, then histogram children of nodes with >1 key
+        // keys: apply the previous pass's remap (an entry with bit 14 set means the node was
+        // divided: the key moved one level down), then histogram the key's quadrant in its new
+        // node.  Nodes with one key get counts too; only nodes with >= 2 keys read them.
         {
-            // register keys: every LDS read of the pass first (independent across keys), then
-            // one atomic per run of equal (node, quadrant) -- atomics would serialise the reads
-            // branch-free (absent keys read node 0 and are masked), so the compiler can
-            // interleave the LDS round trips of all kOctRegKeys keys
-            // staged: all box reads, then all remap reads, then all child reads (absent keys
-            // carry key 0 / node 0 and are masked at the end)
             int tgt[kOctRegKeys];
-            short4 bx[kOctRegKeys];
 #pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++) bx[r] = S.box[prv][nreg[r]];
-#pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++)
-                tgt[r] = S.remap[nreg[r]][quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF)];
-            int cn[kOctRegKeys];
-#pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++) {
-                nreg[r] = max(tgt[r], 0);
-                bx[r] = S.box[cur][nreg[r]];
-                cn[r] = S.cnt[cur][nreg[r]];
-            }
-#pragma unroll
-            for (int r = 0; r < kOctRegKeys; r++) {
-                const bool v = tid * kOctRegKeys + r < nkeys;
-                const int t = 4 * nreg[r] + quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF);
-                tgt[r] = (v && cn[r] >= 2) ? t : -1;
-            }
+            for (int r = 0; r < kOctRegKeys; r++) tgt[r] = S.remap[nreg[r] & 0xFFFF][oct_quad(preg[r], nreg[r] >> 16)];
             OCT_SUB(iter, 6);
+#pragma unroll
+            for (int r = 0; r < kOctRegKeys; r++) {
+                const bool v = tid * kOctRegKeys + r < nkeys;  // absent keys stay on node 0
+                const int e = tgt[r], node = e & 0x3FFF, dep = (nreg[r] >> 16) + ((e >> 14) & 1);
+                nreg[r] = v ? node | dep << 16 : 0;
+                tgt[r] = v ? 4 * node + oct_quad(preg[r], dep) : -1;
+            }
             int run = -1, rc = 0;
 #pragma unroll
             for (int r = 0; r < kOctRegKeys; r++) {
@@ -469,12 +703,13 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
             OCT_SUB(iter, 7);
             // spilled keys
             for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
-                const uint32_t key = K[k];
-                const int x = key & 0xFFF, y = (key >> 12) & 0xFFF;
-                const int o = NO[k];
-                const int n = S.remap[o][quadrant(S.box[prv][o], x, y)];
-                NO[k] = (uint16_t)n;
-                if (S.cnt[cur][n] >= 2) atomicAdd(&S.ccnt[n][quadrant(S.box[cur][n], x, y)], 1);
+                int j = 0;
+                const unsigned path = oct_path(CK[key_slot(k, j)].x, g);
+                const int no = (int)NO[k];
+                const int e = S.remap[no & 0xFFFF][oct_quad(path, no >> 16)];
+                const int node = e & 0x3FFF, dep = (no >> 16) + ((e >> 14) & 1);
+                NO[k] = (uint32_t)(node | dep << 16);
+                atomicAdd(&S.ccnt[node][oct_quad(path, dep)], 1);
             }
             OCT_SUB(iter, 8);
         }
@@ -482,20 +717,25 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
         OCT_SUB(iter, 1);
         // which nodes divide, and in which push order
         int ncand = 0, kdiv = 0;
-        if (!careful) {
-            for (int i = tid; i < L; i += blockDim.x) {
-                const bool d = S.cnt[cur][i] >= 2;
-                S.dflag[i] = d;
-                S.tmp[i] = d ? (S.ccnt[i][0] > 0) + (S.ccnt[i][1] > 0) + (S.ccnt[i][2] > 0) + (S.ccnt[i][3] > 0) : 0;
-            }
-            __syncthreads();
-            block_scan_array(S.tmp, L, S.scratch);  // push base in list order
-            for (int i = tid; i < L; i += blockDim.x) S.newpos[i] = S.tmp[i];
-        } else {
+        if (careful) {
             // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733)
-            {
-                int np2 = 2;
-                while (np2 < L) np2 <<= 1;
+            int np2 = 2;
+            while (np2 < L) np2 <<= 1;
+            if (np2 <= kOctThreads) {
+                const bool c2 = tid < L && S.cnt[cur][tid] >= 2;
+                const unsigned long long key =
+                    c2 ? ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][tid]) << 32) | (unsigned)tid : ~0ull;
+                const int nw = __popcll(__ballot(c2));
+                if (tid == 0) S.misc[0] = 0;
+                __syncthreads();
+                if ((tid & 63) == 0 && nw) atomicAdd(&S.misc[0], nw);
+                const unsigned long long sorted = bitonic_sort_block(key, np2, S.skey);
+                __syncthreads();
+                if (tid < np2) S.skey[tid] = sorted;
+                for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
+                ncand = S.misc[0];
+                __syncthreads();
+            } else {
                 for (int i = tid; i < np2; i += blockDim.x) {
                     unsigned long long key = ~0ull;
                     if (i < L && S.cnt[cur][i] >= 2)
@@ -504,83 +744,103 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
                 }
                 if (tid == 0) S.misc[0] = 0;
                 __syncthreads();
-                for (int i = tid; i < L; i += blockDim.x)
+                for (int i = tid; i < L; i += blockDim.x) {
                     if (S.cnt[cur][i] >= 2) atomicAdd(&S.misc[0], 1);
+                    S.dflag[i] = 0;
+                }
                 bitonic_sort(S.skey, np2);
                 ncand = S.misc[0];
             }
-            for (int r = tid; r < ncand; r += blockDim.x) {
-                const int n = (int)(S.skey[r] & 0xFFFFFFFFu);
-                S.tmp[r] = (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0) - 1;
+            // wave 0 walks the sorted candidates in chunks of 64 with wave scans: kdiv = 1 + the
+            // first r whose division brings the list to N (L + sum_{r' <= r} (m_r' - 1) >= N),
+            // then the divided nodes' push bases (prefix of m in sorted order)
+            if (tid < 64) {
+                auto m_of = [&](int n) {
+                    return (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
+                };
+                int run = 0, kd = ncand;
+                for (int r0 = 0; r0 < ncand; r0 += 64) {
+                    const int r = r0 + tid;
+                    const int m = r < ncand ? m_of((int)(S.skey[r] & 0xFFFFFFFFu)) : 1;
+                    const int incl = wave_incl_scan(m - 1);
+                    const unsigned long long hit = __ballot(r < ncand && L + run + incl >= N);
+                    if (hit) {
+                        kd = r0 + __ffsll((long long)hit);
+                        break;
+                    }
+                    run += __shfl(incl, 63);
+                }
+                int push = 0;
+                for (int r0 = 0; r0 < kd; r0 += 64) {
+                    const int r = r0 + tid;
+                    const int n = r < kd ? (int)(S.skey[r] & 0xFFFFFFFFu) : 0;
+                    const int m = r < kd ? m_of(n) : 0;
+                    const int incl = wave_incl_scan(m);
+                    if (r < kd) {
+                        S.dflag[n] = 1;
+                        S.newpos[n] = push + incl - m;
+                    }
+                    push += __shfl(incl, 63);
+                }
+                kdiv = kd;
             }
-            if (tid == 0) S.misc[1] = ncand;
             __syncthreads();
-            block_scan_array(S.tmp, ncand, S.scratch);  // exclusive prefix of (m - 1)
-            for (int r = tid; r < ncand; r += blockDim.x) {
-                const int n = (int)(S.skey[r] & 0xFFFFFFFFu);
-                const int m = (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
-                if (L + S.tmp[r] + m - 1 >= N) atomicMin(&S.misc[1], r + 1);
-            }
-            __syncthreads();
-            kdiv = S.misc[1];
-            for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
-            __syncthreads();
-            for (int r = tid; r < ncand; r += blockDim.x) {
-                const int n = (int)(S.skey[r] & 0xFFFFFFFFu);
-                const int m = (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
-                S.tmp[r] = r < kdiv ? m : 0;
-                if (r < kdiv) S.dflag[n] = 1;
-            }
-            __syncthreads();
-            block_scan_array(S.tmp, ncand, S.scratch);
-            for (int r = tid; r < kdiv; r += blockDim.x) S.newpos[(int)(S.skey[r] & 0xFFFFFFFFu)] = S.tmp[r];
         }
-        __syncthreads();
         OCT_SUB(iter, 2);
-        // P = total pushes; survivors ranked in list order
-        int P = 0;
-        {
-            int local = 0;
-            for (int i = tid; i < L; i += blockDim.x)
-                if (S.dflag[i]) local += (S.ccnt[i][0] > 0) + (S.ccnt[i][1] > 0) + (S.ccnt[i][2] > 0) + (S.ccnt[i][3] > 0);
-            block_excl_scan(local, S.scratch, &P);
-        }
-        for (int i = tid; i < L; i += blockDim.x) S.tmp[i] = !S.dflag[i];
-        __syncthreads();
-        const int nsurv = block_scan_array(S.tmp, L, S.scratch);
+        // one packed scan over the list, two nodes per thread: child pushes of the dividing nodes
+        // (outside the careful mode their push base in list order) | survivors << 16; the
+        // children with more than one key go to one atomic per wave
+        const int i0 = 2 * tid, i1 = i0 + 1;
+        int ne = 0;
+        auto classify = [&](int i) -> int {
+            if (i >= L) return 0;
+            const bool d = careful ? S.dflag[i] != 0 : S.cnt[cur][i] >= 2;
+            if (!careful) S.dflag[i] = d;
+            if (!d) return 1 << 16;
+            int m = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = S.ccnt[i][q];
+                m += c > 0;
+                ne += c > 1;
+            }
+            return m;
+        };
+        const int v0 = classify(i0), v1 = classify(i1);
+        ne = wave_sum_i32(ne);
+        if ((tid & 63) == 0 && ne) atomicAdd(&S.misc[2 + (iter & 1)], ne);
+        int total;
+        const int e0 = block_excl_scan(v0 + v1, S.scratch, &total);
+        const int P = total & 0xFFFF, nsurv = total >> 16;
+        const int nToExpand = S.misc[2 + (iter & 1)];  // every atomic precedes the scan's barriers
         OCT_SUB(iter, 3);
-        int nexp_local = 0;
-        for (int i = tid; i < L; i += blockDim.x) {
+        auto rewrite = [&](int i, int e) {
+            if (i >= L) return;
             if (S.dflag[i]) {
-                int p = S.newpos[i];
-                const short4 bx = S.box[cur][i];
+                int p = careful ? S.newpos[i] : (e & 0xFFFF);
+#pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int c = S.ccnt[i][q];
                     if (c > 0) {
                         const int ni = P - 1 - p++;
-                        if (ni < kOctNodeCap) {  // bound proven in DESIGN.md; guard LDS anyway
-                            S.box[prv][ni] = child_box(bx, q);
-                            S.cnt[prv][ni] = c;
-                        }
-                        S.remap[i][q] = (short)min(ni, kOctNodeCap - 1);
-                        nexp_local += c > 1;
+                        if (ni < kOctNodeCap) S.cnt[prv][ni] = c;  // bound proven in DESIGN.md; guard LDS anyway
+                        S.remap[i][q] = (short)(min(ni, kOctNodeCap - 1) | 0x4000);
                     } else {
                         S.remap[i][q] = -1;
                     }
                 }
             } else {
-                const int ni = min(P + S.tmp[i], kOctNodeCap - 1);
-                S.box[prv][ni] = S.box[cur][i];
+                const int ni = min(P + (e >> 16), kOctNodeCap - 1);
                 S.cnt[prv][ni] = S.cnt[cur][i];
                 S.remap[i][0] = S.remap[i][1] = S.remap[i][2] = S.remap[i][3] = (short)ni;
             }
-        }
+        };
+        rewrite(i0, e0);
+        rewrite(i1, e0 + v0);
+        __syncthreads();  // the next pass clears ccnt and reads cnt[prv] / remap
         OCT_SUB(iter, 4);
-        int nToExpand = 0;
-        block_excl_scan(nexp_local, S.scratch, &nToExpand);
-        OCT_SUB(iter, 5);
         const int newL = min(P + nsurv, kOctNodeCap);
-        // the remap just written refers to the boxes of list `cur`; keys apply it next pass
+        // the remap just written maps list `cur` to list `prv`; keys apply it next pass
         cur = prv;
         if (newL >= N || newL == L) finish = true;
         else if (!careful && newL + nToExpand * 3 > N) careful = true;
@@ -594,36 +854,36 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
     OCT_STAMP(60, L);
 
     // ---- keep the max-response key per node, first in original order on ties (:744-760):
-    // one 64-bit max per node over score << 56 | (2^20 - 1 - k) << 24 | (y << 12 | x)
-    const int prv = cur ^ 1;
+    // one 64-bit max per node over score << 56 | (2^24 - 1 - tag) << 24 | (y << 12 | x)
     unsigned long long* best = reinterpret_cast<unsigned long long*>(&S.ccnt[0][0]);  // 2 per row
     for (int i = tid; i < L; i += blockDim.x) best[2 * i] = 0;
     __syncthreads();
     {
         int fn[kOctRegKeys];  // final node of each register key, all reads first
-        short4 bx[kOctRegKeys];
-#pragma unroll
-        for (int r = 0; r < kOctRegKeys; r++) bx[r] = S.box[prv][nreg[r]];
 #pragma unroll
         for (int r = 0; r < kOctRegKeys; r++) {
             const bool v = tid * kOctRegKeys + r < nkeys;
-            const int n = S.remap[nreg[r]][quadrant(bx[r], kreg[r] & 0xFFF, (kreg[r] >> 12) & 0xFFF)];
-            fn[r] = v ? n : -1;
+            const int e = S.remap[nreg[r] & 0xFFFF][oct_quad(preg[r], nreg[r] >> 16)];
+            fn[r] = v ? (e & 0x3FFF) : -1;
         }
+        uint32_t treg[kOctRegKeys];  // order tags
+#pragma unroll
+        for (int r = 0; r < kOctRegKeys; r++) treg[r] = S.tagl[tid * kOctRegKeys + r];
 #pragma unroll
         for (int r = 0; r < kOctRegKeys; r++) {
-            const int k = tid * kOctRegKeys + r;
             const uint32_t key = kreg[r];
             if (fn[r] >= 0)
                 atomicMax(&best[2 * fn[r]], ((unsigned long long)(key >> 24) << 56) |
-                                                ((unsigned long long)(0xFFFFFu - (unsigned)k) << 24) | (key & 0xFFFFFFu));
+                                                ((unsigned long long)(0xFFFFFFu - treg[r]) << 24) | (key & 0xFFFFFFu));
         }
         for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
-            const uint32_t key = K[k];
-            const int o = NO[k];
-            const int n = S.remap[o][quadrant(S.box[prv][o], key & 0xFFF, (key >> 12) & 0xFFF)];
+            int j = 0;
+            const uint2 kv = CK[key_slot(k, j)];
+            const uint32_t key = kv.x, tg = kv.y;
+            const int no = (int)NO[k];
+            const int n = S.remap[no & 0xFFFF][oct_quad(oct_path(key, g), no >> 16)] & 0x3FFF;
             atomicMax(&best[2 * n], ((unsigned long long)(key >> 24) << 56) |
-                                        ((unsigned long long)(0xFFFFFu - (unsigned)k) << 24) | (key & 0xFFFFFFu));
+                                        ((unsigned long long)(0xFFFFFFu - tg) << 24) | (key & 0xFFFFFFu));
         }
     }
     __syncthreads();
@@ -647,25 +907,29 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
 // into the interior-only blurred layout.
 constexpr int kBlurInH = kBlurTH + 6, kBlurChunks = (kBlurTW + 6 + 15) / 16;  // 38 rows x 9 x 16 B
 constexpr int kBlurInS = 16 * kBlurChunks;                                     // 144
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                              long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
-                                              const int2* __restrict__ tiles) {
-    __shared__ uint4 in4[kBlurInH * kBlurChunks];
-    __shared__ int rs[kBlurInH][kBlurTW];
+struct BlurShared {
+    uint4 in4[kBlurInH * kBlurChunks];
+    int rs[kBlurInH][kBlurTW];
+};
+// One tile on a 256-thread slice of the workgroup (tid = 0..255).  The slice's two block-wide
+// barriers are reached by every slice, also one without a tile (valid = false).
+__device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                          long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
+                                          int2 t, int b, int tid, bool valid) {
+    uint4* in4 = B.in4;
+    int(*rs)[kBlurTW] = B.rs;
     const uint8_t* in = reinterpret_cast<const uint8_t*>(in4);
-    const int2 t = tiles[blockIdx.x];
-    const int b = blockIdx.y, tid = threadIdx.x;
-    const LevelGeom g = levels[t.x];
+    const LevelGeom g = levels[valid ? t.x : 0];
     const int x0 = t.y & 0xFFFF, y0 = t.y >> 16;
     const uint8_t* lvl = pyr + b * pimg + g.off + kEdge - 3 + x0;  // column x0 - 3 of padded row 0
-    for (int i = tid; i < kBlurInH * kBlurChunks; i += 256) {
+    for (int i = tid; valid && i < kBlurInH * kBlurChunks; i += 256) {
         const int r = i / kBlurChunks, ch = i - r * kBlurChunks;
         const int yy = min(y0 - 3 + r, g.H + 2);  // rows past H + 2 feed only discarded outputs
         in4[i] = *reinterpret_cast<const uint4*>(lvl + (long long)(kEdge + yy) * g.stride + 16 * ch);
     }
     __syncthreads();
     // row sums: one (row, 16 columns) run per task
-    for (int task = tid; task < kBlurInH * (kBlurTW / 16); task += 256) {
+    for (int task = tid; valid && task < kBlurInH * (kBlurTW / 16); task += 256) {
         const int r = task / (kBlurTW / 16), c0 = 16 * (task - r * (kBlurTW / 16));
         const uint8_t* q = in + r * kBlurInS + c0;  // q[k] = input column c0 + k - 3
         int v[22];
@@ -677,6 +941,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, u
                             18 * (v[c] + v[c + 6]);
     }
     __syncthreads();
+    if (!valid) return;
     const int cq = 4 * (tid & 31), rb = 4 * (tid >> 5);  // 4 columns x 4 rows per thread
     uint8_t* dst = blur + b * bimg + g.boff;
 #pragma unroll
@@ -704,6 +969,41 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, u
         if (x0 + cq < g.bstride)
             *reinterpret_cast<unsigned*>(dst + (long long)y * g.bstride + x0 + cq) = packedv;
     }
+}
+
+// DistributeOctTree and GaussianBlur in one launch: blocks [0, nlevels) run one pyramid level's
+// octree each (16 workgroups for a stereo pair), the remaining blocks blur four 128x32 tiles
+// each on the CUs the octree leaves idle.  Both only read the pyramid; the blur slices reuse
+// the octree's LDS.
+static_assert(sizeof(OctShared) >= 4 * sizeof(BlurShared), "blur slices overlay the octree LDS");
+constexpr int kFuseBlurMaxOctrees = 64;  // octree workgroups up to which the blur rides along
+__global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restrict__ levels, int nlevels,
+                                                         const uint2* __restrict__ cand,
+                                                         const int* __restrict__ level_count,
+                                                         const int* __restrict__ regbase,
+                                                         uint32_t* __restrict__ node_of,
+                                                         int keys_cap, uint2* __restrict__ oct_out, int out_cap,
+                                                         int* __restrict__ oct_count, const uint8_t* __restrict__ pyr,
+                                                         uint8_t* __restrict__ blur, long long pimg, long long bimg,
+                                                         const int2* __restrict__ btiles, int nbtiles) {
+    __shared__ OctShared S;
+    if ((int)blockIdx.x < nlevels) {
+        octree_body(S, blockIdx.x, blockIdx.y, levels, nlevels, cand, level_count, regbase, node_of, keys_cap, oct_out,
+                    out_cap, oct_count);
+        return;
+    }
+    const int slice = threadIdx.x >> 8, ti = ((int)blockIdx.x - nlevels) * 4 + slice;
+    BlurShared* B = reinterpret_cast<BlurShared*>(&S) + slice;
+    blur_tile(*B, pyr, blur, pimg, bimg, levels, ti < nbtiles ? btiles[ti] : make_int2(0, 0), blockIdx.y,
+              threadIdx.x & 255, ti < nbtiles);
+}
+
+// GaussianBlur alone: one 128x32 tile per 256-thread workgroup.
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                              long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
+                                              const int2* __restrict__ tiles) {
+    __shared__ BlurShared B;
+    blur_tile(B, pyr, blur, pimg, bimg, levels, tiles[blockIdx.x], blockIdx.y, threadIdx.x, true);
 }
 
 // ------------------------------------------------------------------------------ describe
@@ -919,6 +1219,7 @@ int Extractor::set_geometry(int r, int c) {
     std::vector<YTab> yt;
     long long off = 0, boff = 0;
     int slot = 0, key = 0, outb = 0;
+    regbase.assign((size_t)nlevels * kFastRegions, 0);
     for (int l = 0; l < nlevels; l++) {
         LevelGeom& g = levels[l];
         g.W = cv_round_host((float)c * inv_scale[l]);
@@ -960,7 +1261,6 @@ int Extractor::set_geometry(int r, int c) {
                     cg.x0 = (short)(int)iniX; cg.y0 = (short)(int)iniY;
                     cg.w = (short)((int)maxX - (int)iniX); cg.h = (short)((int)maxY - (int)iniY);
                     cg.sx = (short)(j * wCell); cg.sy = (short)(i * hCell);
-                    cg.slot_base = slot;
                     slot += cap;
                     key += cap;
                 }
@@ -969,7 +1269,19 @@ int Extractor::set_geometry(int r, int c) {
         }
         g.cell_end = (int)cells.size();
         g.key_cap = key - g.key_base;
-        if (g.key_cap > (1 << 20)) return ORBMI_E_UNSUPPORTED;
+        {   // candidate regions: region j holds the cells k % R == j of the level, sized for their caps
+            int rcap[kFastRegions] = {0}, base = g.key_base;
+            for (int k = 0; k < g.cell_end - g.cell_begin; k++)
+                if (cells[g.cell_begin + k].w) rcap[k % kFastRegions] += cap;
+            for (int j = 0; j < kFastRegions; j++) {
+                regbase[l * kFastRegions + j] = base;
+                base += rcap[j];
+            }
+            for (int k = 0; k < g.cell_end - g.cell_begin; k++)
+                cells[g.cell_begin + k].slot_base = regbase[l * kFastRegions + k % kFastRegions];
+        }
+        // order tags: cell index within the level (14 bits) << 10 | rank in the cell (< 1024)
+        if (g.key_cap > (1 << 20) || g.cell_end - g.cell_begin >= (1 << 14) || cap >= 1024) return ORBMI_E_UNSUPPORTED;
         g.width = maxBX - minB;
         g.height = maxBY - minB;
         g.nIni = (int)roundf((float)g.width / (float)g.height);
@@ -1018,6 +1330,105 @@ int Extractor::set_geometry(int r, int c) {
             }
         }
     }
+    // pyramid tiles: own rectangles split every level KX x KY ways; need rectangles from the top
+    // level down (need_{l-1} = own_{l-1} U the taps of need_l); level 0's need rectangle is the
+    // own one grown by the largest halo (hx, hy) of any tile.  The grid grows until a tile's LDS
+    // (parameter block, level-0 rectangle, two need rectangles) fits in 48 KB.  Each tile's
+    // parameter block: kPyrLevelWords words per level (own, need, W | H << 16, stride, offset,
+    // resize_xv, word offsets of the x / y taps), then the taps of its need rectangles.
+    {
+        int KX = 16, KY = 8;
+        for (;;) {
+            std::vector<PyrTile> tl((size_t)KX * KY * nlevels);
+            int maxarea = 0, hx = 0, hy = 0, words = 0;
+            for (int ty = 0; ty < KY; ty++)
+                for (int tx = 0; tx < KX; tx++) {
+                    PyrTile* T = &tl[((size_t)ty * KX + tx) * nlevels];
+                    for (int l = 0; l < nlevels; l++) {
+                        const LevelGeom& g = levels[l];
+                        T[l].own = PyrRect{(short)(g.W * tx / KX), (short)(g.W * (tx + 1) / KX), (short)(g.H * ty / KY),
+                                           (short)(g.H * (ty + 1) / KY)};
+                    }
+                    T[nlevels - 1].need = T[nlevels - 1].own;
+                    for (int l = nlevels - 1; l >= 1; l--) {
+                        const LevelGeom& g = levels[l];
+                        PyrRect n = T[l].need, o = T[l - 1].own, r = o;
+                        if (n.x1 > n.x0 && n.y1 > n.y0) {
+                            const XTab* X = xt.data() + g.xtab_off;
+                            const YTab* Y = yt.data() + g.ytab_off;
+                            r.x0 = std::min<short>(o.x0, X[n.x0].sx0);
+                            r.x1 = std::max<short>(o.x1, (short)(X[n.x1 - 1].sx1 + 1));
+                            r.y0 = std::min<short>(o.y0, Y[n.y0].y0);
+                            r.y1 = std::max<short>(o.y1, (short)(Y[n.y1 - 1].y1 + 1));
+                        }
+                        T[l - 1].need = r;
+                    }
+                    int w = kPyrLevelWords * nlevels;
+                    for (int l = 1; l < nlevels; l++) {
+                        const PyrRect& n = T[l].need;
+                        maxarea = std::max(maxarea, (n.x1 - n.x0) * (n.y1 - n.y0));
+                        w += 2 * (n.x1 - n.x0) + 2 * (n.y1 - n.y0);
+                    }
+                    words = std::max(words, w);
+                    hx = std::max(hx, std::max(T[0].own.x0 - T[0].need.x0, T[0].need.x1 - T[0].own.x1));
+                    hy = std::max(hy, std::max(T[0].own.y0 - T[0].need.y0, T[0].need.y1 - T[0].own.y1));
+                }
+            int area0 = 0;
+            for (int ty = 0; ty < KY; ty++)
+                for (int tx = 0; tx < KX; tx++) {
+                    const int x0 = std::max(levels[0].W * tx / KX - hx, 0), x1 = std::min(levels[0].W * (tx + 1) / KX + hx, levels[0].W);
+                    const int y0 = std::max(levels[0].H * ty / KY - hy, 0), y1 = std::min(levels[0].H * (ty + 1) / KY + hy, levels[0].H);
+                    area0 = std::max(area0, (x1 - x0) * (y1 - y0));
+                }
+            const int half = (maxarea + 15) & ~15, a0 = (area0 + 15) & ~15;
+            const int lds = 4 * words + a0 + 2 * half;
+            if (lds <= 48 * 1024 || KX * KY >= 4096) {
+                if (lds > 64 * 1024) return ORBMI_E_UNSUPPORTED;
+                pyr_blob.assign((size_t)KX * KY * words, 0u);
+                for (int t = 0; t < KX * KY; t++) {
+                    const PyrTile* T = &tl[(size_t)t * nlevels];
+                    uint32_t* B = &pyr_blob[(size_t)t * words];
+                    auto pk = [](int lo, int hi) { return (uint32_t)(uint16_t)lo | (uint32_t)(uint16_t)hi << 16; };
+                    int at = kPyrLevelWords * nlevels;
+                    for (int l = 0; l < nlevels; l++) {
+                        const LevelGeom& g = levels[l];
+                        uint32_t* G = B + l * kPyrLevelWords;
+                        G[0] = pk(T[l].own.x0, T[l].own.x1);
+                        G[1] = pk(T[l].own.y0, T[l].own.y1);
+                        G[2] = pk(T[l].need.x0, T[l].need.x1);
+                        G[3] = pk(T[l].need.y0, T[l].need.y1);
+                        G[4] = pk(g.W, g.H);
+                        G[5] = (uint32_t)g.stride;
+                        G[6] = (uint32_t)g.off;
+                        G[7] = (uint32_t)g.resize_xv;
+                        if (l == 0) continue;
+                        const XTab* X = xt.data() + g.xtab_off;
+                        const YTab* Y = yt.data() + g.ytab_off;
+                        G[8] = (uint32_t)at;
+                        for (int x = T[l].need.x0; x < T[l].need.x1; x++) {
+                            B[at++] = pk(X[x].sx0, X[x].sx1);
+                            B[at++] = pk(X[x].a0, X[x].a1);
+                        }
+                        G[9] = (uint32_t)at;
+                        for (int y = T[l].need.y0; y < T[l].need.y1; y++) {
+                            B[at++] = pk(Y[y].y0, Y[y].y1);
+                            B[at++] = pk(Y[y].b0, Y[y].b1);
+                        }
+                    }
+                }
+                pyr_kx = KX;
+                pyr_ky = KY;
+                pyr_hx = hx;
+                pyr_hy = hy;
+                pyr_blob_words = words;
+                pyr_lds_half = half;
+                pyr_lds0 = a0;
+                break;
+            }
+            if (KX <= 2 * KY) KX *= 2;
+            else KY *= 2;
+        }
+    }
     pimg = off;
     bimg = boff;
     btiles.clear();
@@ -1025,13 +1436,17 @@ int Extractor::set_geometry(int r, int c) {
         for (int y0 = 0; y0 < levels[l].H; y0 += kBlurTH)
             for (int x0 = 0; x0 < levels[l].W; x0 += kBlurTW) btiles.push_back(make_int2(l, x0 | (y0 << 16)));
     nbtiles = (int)btiles.size();
-    nslots = slot;
+    (void)slot;
     keys_cap = key;
     out_cap = outb;
     rows = r; cols = c;
     int rc;
     if ((rc = dev_alloc(&d_levels, levels.size()))) return rc;
     if ((rc = dev_alloc(&d_cells, cells.size()))) return rc;
+    if ((rc = dev_alloc(&d_regbase, regbase.size()))) return rc;
+    if ((rc = dev_alloc(&d_pyr_blob, pyr_blob.size()))) return rc;
+    ORBMI_HIP(hipMemcpy(d_pyr_blob, pyr_blob.data(), pyr_blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ORBMI_HIP(hipMemcpy(d_regbase, regbase.data(), regbase.size() * sizeof(int), hipMemcpyHostToDevice));
     if ((rc = dev_alloc(&d_btiles, btiles.size()))) return rc;
     ORBMI_HIP(hipMemcpy(d_btiles, btiles.data(), btiles.size() * sizeof(int2), hipMemcpyHostToDevice));
     if ((rc = dev_alloc(&d_xtab, xt.size()))) return rc;
@@ -1049,9 +1464,8 @@ int Extractor::reserve(int batch, int capacity) {
     if (batch > bcap) {
         if ((rc = dev_alloc(&d_pyr, (size_t)batch * pimg))) return rc;
         if ((rc = dev_alloc(&d_blur, (size_t)batch * bimg))) return rc;
-        if ((rc = dev_alloc(&d_cell_counts, (size_t)batch * cells.size()))) return rc;
-        if ((rc = dev_alloc(&d_slots, (size_t)batch * nslots))) return rc;
-        if ((rc = dev_alloc(&d_keys, (size_t)batch * keys_cap))) return rc;
+        if ((rc = dev_alloc(&d_level_count, (size_t)batch * nlevels * kFastRegions))) return rc;
+        if ((rc = dev_alloc(&d_cand, (size_t)batch * keys_cap))) return rc;
         if ((rc = dev_alloc(&d_node_of, (size_t)batch * keys_cap))) return rc;
         if ((rc = dev_alloc(&d_oct, (size_t)batch * out_cap))) return rc;
         if ((rc = dev_alloc(&d_oct_count, (size_t)batch * nlevels))) return rc;
@@ -1071,34 +1485,47 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                    orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity) {
     ORBMI_HIP(hipSetDevice(device));
     const int ncells = (int)cells.size();
-    for (int l = 0; l < nlevels; l++) {
-        const LevelGeom& g = levels[l];
-        dim3 grid((g.W + 2 * kEdge + 255) / 256, g.ph, batch);
-        if (l == 0) {
-            hipEvent_t ev = prof_begin(ORBMI_STAGE_PYR_LEVEL0);
-            hipLaunchKernelGGL(k_pyr_level0, grid, dim3(256), 0, stream, d_images, step, image_stride, d_pyr, pimg, g);
-            prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
-        } else {
-            hipEvent_t ev = prof_begin(ORBMI_STAGE_PYR_RESIZE);
-            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), 0, stream, d_pyr, pimg, levels[l - 1], g,
-                               d_xtab + g.xtab_off, d_ytab + g.ytab_off);
-            prof_end(ORBMI_STAGE_PYR_RESIZE, ev);
+    if (batch > kPyrTiledMaxBatch) {
+        for (int l = 0; l < nlevels; l++) {
+            const LevelGeom& g = levels[l];
+            dim3 grid((g.W + 2 * kEdge + 255) / 256, g.ph, batch);
+            hipEvent_t ev = prof_begin(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE);
+            if (l == 0)
+                hipLaunchKernelGGL(k_pyr_level0, grid, dim3(256), 0, stream, d_images, step, image_stride, d_pyr, pimg, g,
+                                   d_level_count, nlevels);
+            else
+                hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), 0, stream, d_pyr, pimg, levels[l - 1], g,
+                                   d_xtab + g.xtab_off, d_ytab + g.ytab_off);
+            prof_end(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE, ev);
         }
+    } else {
+        hipEvent_t ev = prof_begin(ORBMI_STAGE_PYR_LEVEL0);  // the whole pyramid
+        hipLaunchKernelGGL(k_pyramid, dim3(pyr_kx * pyr_ky, 1, batch), dim3(kPyrThreads),
+                           4 * pyr_blob_words + pyr_lds0 + 2 * pyr_lds_half, stream, d_images, step, image_stride, d_pyr,
+                           pimg, d_pyr_blob, pyr_blob_words, nlevels, pyr_kx, pyr_ky, levels[0].W, levels[0].H, pyr_hx,
+                           pyr_hy, d_level_count, pyr_lds0, pyr_lds_half);
+        prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
     hipLaunchKernelGGL(k_fast, dim3((ncells + kFastCells - 1) / kFastCells, batch), dim3(64 * kFastCells), 0, stream,
                        d_pyr, pimg, d_levels, d_cells,
-                       ncells, d_slots, nslots, d_cell_counts, ini_th, min_th);
+                       ncells, d_cand, keys_cap, d_level_count, nlevels, ini_th, min_th);
     prof_end(ORBMI_STAGE_FAST, ev);
+    // small batches: the blur runs inside the octree launch on the CUs its nlevels x batch
+    // workgroups leave idle; large batches fill the chip with octrees, so the blur gets its own
+    // launch at full occupancy
+    const bool fuse_blur = batch * nlevels <= kFuseBlurMaxOctrees;
     ev = prof_begin(ORBMI_STAGE_OCTREE);
-    hipLaunchKernelGGL(k_octree, dim3(nlevels, batch), dim3(kOctThreads), 0, stream, d_levels, nlevels, ncells,
-                       d_cell_counts, d_cells, d_slots, nslots, d_keys, d_node_of, keys_cap, d_oct, out_cap,
-                       d_oct_count);
+    hipLaunchKernelGGL(k_octree, dim3(nlevels + (fuse_blur ? (nbtiles + 3) / 4 : 0), batch), dim3(kOctThreads), 0, stream,
+                       d_levels, nlevels, d_cand, d_level_count, d_regbase, d_node_of, keys_cap, d_oct, out_cap, d_oct_count, d_pyr,
+                       d_blur, pimg, bimg, d_btiles, nbtiles);
     prof_end(ORBMI_STAGE_OCTREE, ev);
-    ev = prof_begin(ORBMI_STAGE_BLUR);
-    hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg, d_levels,
-                       d_btiles);
-    prof_end(ORBMI_STAGE_BLUR, ev);
+    if (!fuse_blur) {
+        ev = prof_begin(ORBMI_STAGE_BLUR);
+        hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg, d_levels,
+                           d_btiles);
+        prof_end(ORBMI_STAGE_BLUR, ev);
+    }
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
     hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
                        d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity);
@@ -1137,7 +1564,7 @@ void Extractor::release() {
     prof_pending.clear();
     prof_pool.clear();
     if (device >= 0) (void)hipSetDevice(device);
-    void* ptrs[] = {d_levels, d_cells, d_btiles, d_blur, d_xtab, d_ytab, d_pyr, d_cell_counts, d_slots, d_keys, d_node_of,
+    void* ptrs[] = {d_levels, d_cells, d_regbase, d_pyr_blob, d_btiles, d_blur, d_xtab, d_ytab, d_pyr, d_level_count, d_cand, d_node_of,
                     d_oct, d_oct_count, d_kps, d_desc, d_counts, d_image, d_scale_tab, d_row_start,
                     d_row_list, d_sad, d_stereo_u, d_stereo_d};
     for (void* p : ptrs)

@@ -177,32 +177,68 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoArgs a) {
 }
 
 // sort(vDistIdx); median = vDistIdx[size/2].first; drop dist >= 1.5f*1.4f*median
+// The median is a two-pass radix select over the SAD values (0 <= SAD <= 121 * 255 < 2^15):
+// a 256-bin histogram of v >> 7 finds the bin holding rank size/2, a 128-bin histogram of the
+// low bits inside it finds the value.  The values stay in registers between the passes.
+constexpr int kFilterRegs = 8;  // values per thread held in registers (8192 keypoints)
 __global__ __launch_bounds__(1024) void k_stereo_filter(const int* __restrict__ countL, int capL,
                                                         const int* __restrict__ sad, float* __restrict__ u_right,
                                                         float* __restrict__ depth) {
-    __shared__ int scratch[20];
+    __shared__ int h1[256], h2[128], sel[2];
     const int tid = threadIdx.x;
     const int n = min(*countL, capL);
-    int local = 0;
-    for (int i = tid; i < n; i += blockDim.x) local += sad[i] >= 0;
-    int M;
-    block_excl_scan(local, scratch, &M);
-    if (M == 0) return;  // reference: median of an empty vector (UB); defined as "no filter"
-    const int rank = M / 2;
-    int lo = 0, hi = 1 << 17;  // smallest v with #(sad <= v) > rank
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        int c = 0;
-        for (int i = tid; i < n; i += blockDim.x) c += sad[i] >= 0 && sad[i] <= mid;
-        int tot;
-        block_excl_scan(c, scratch, &tot);
-        if (tot > rank) hi = mid;
-        else lo = mid + 1;
+    int v[kFilterRegs];
+#pragma unroll
+    for (int k = 0; k < kFilterRegs; k++) {
+        const int i = tid + k * 1024;
+        v[k] = i < n ? sad[i] : -1;
     }
-    const float median = (float)lo;
+    auto for_values = [&](auto&& f) {
+#pragma unroll
+        for (int k = 0; k < kFilterRegs; k++) f(tid + k * 1024, v[k]);
+        for (int i = tid + kFilterRegs * 1024; i < n; i += 1024) f(i, sad[i]);
+    };
+    if (tid < 256) h1[tid] = 0;
+    if (tid < 128) h2[tid] = 0;
+    __syncthreads();
+    for_values([&](int, int x) { if (x >= 0) atomicAdd(&h1[min(x >> 7, 255)], 1); });
+    __syncthreads();
+    auto select = [&](const int* h, int nb, int rank_in, int* bin, int* rest, int* total) {
+        // wave 0: bins in lane order (nb / 64 per lane), prefix, the bin holding rank_in
+        const int per = nb / 64;
+        int c[4], s = 0;
+        for (int j = 0; j < per; j++) { c[j] = h[tid * per + j]; s += c[j]; }
+        const int incl = wave_incl_scan(s);
+        *total = __shfl(incl, 63);
+        const int rank = rank_in < 0 ? *total / 2 : rank_in;
+        int before = incl - s;
+        for (int j = 0; j < per; j++) {
+            if (rank >= before && rank < before + c[j]) { *bin = tid * per + j; *rest = rank - before; }
+            before += c[j];
+        }
+    };
+    if (tid < 64) {
+        int bin = -1, rest = 0, M = 0;
+        select(h1, 256, -1, &bin, &rest, &M);
+        if (M == 0 && tid == 0) sel[0] = -1;  // reference: median of an empty vector (UB); "no filter"
+        if (bin >= 0) { sel[0] = bin; sel[1] = rest; }
+    }
+    __syncthreads();
+    const int b1 = sel[0], r1 = sel[1];
+    if (b1 < 0) return;
+    for_values([&](int, int x) { if (x >= 0 && (x >> 7) == b1) atomicAdd(&h2[x & 127], 1); });
+    __syncthreads();
+    if (tid < 64) {
+        int bin = -1, rest = 0, M = 0;
+        select(h2, 128, r1, &bin, &rest, &M);
+        if (bin >= 0) sel[0] = (b1 << 7) | bin;
+    }
+    __syncthreads();
+    const float median = (float)sel[0];
     const float thDist = 1.5f * 1.4f * median;
-    for (int i = tid; i < n; i += blockDim.x)
-        if (sad[i] >= 0 && !((float)sad[i] < thDist)) { u_right[i] = -1; depth[i] = -1; }
+    for_values([&](int i, int x) {
+        if (i < n && x >= 0 && !((float)x < thDist)) { u_right[i] = -1; depth[i] = -1; }
+    });
 }
 
 int stereo_run(Extractor& Lx, int itemL, Extractor& Rx, int itemR, float bf, float fx, float* d_u,

@@ -15,7 +15,7 @@ import os
 import sys
 from collections import defaultdict
 
-STAGE_OF = [("k_pyr_level0", "pyr_level0"), ("k_pyr_resize", "pyr_resize"), ("k_fast", "fast"),
+STAGE_OF = [("k_pyramid", "pyr_level0"), ("k_pyr_level0", "pyr_level0"), ("k_pyr_resize", "pyr_resize"), ("k_fast", "fast"),
             ("k_octree", "octree"), ("k_describe", "describe"), ("k_stereo_rows", "stereo_rows"),
             ("k_stereo_match", "stereo_match"), ("k_stereo_filter", "stereo_filter")]
 
