@@ -656,7 +656,7 @@ def run_lba(a, rank, world, local, dist):
             "config": {"workload": "config3: Optimizer::LocalBundleAdjustment, 5+10 LM iterations, Huber",
                        "edges": E, "points": M, "free_keyframes": K},
             "iterations": list(it), "chi2": list(res["chi2"]),
-            "roofline": {"kernel": "LocalBA kernel chain", "bound": "latency (6 dependent launches per LM trial, device-side LM control)",
+            "roofline": {"kernel": "LocalBA kernel chain", "bound": "latency (3 dependent launches per LM trial: Schur, solve, update + device-side LM decision)",
                          "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP64_PEAK_TFS, 8), "traffic": None},
             "cpu_baseline": cpu, "host": host_info(),
