@@ -744,7 +744,8 @@ def run_system(a, rank, world, local, dist):
             "data": "synthetic: ray-cast KITTI-shaped 1241x376 stereo sequence with exact ground truth",
             "config": {"workload": "config 1: System::TrackStereo over the first 200 frames (Frame ctor + Track "
                                    "(motion model / reference KF) + TrackLocalMap + keyframe insertion + "
-                                   "ProcessNewKeyFrame + LocalBA), 2000 features", "frames": N,
+                                   "LocalMapping::Run [ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints, "
+                                   "SearchInNeighbors, LocalBA, KeyFrameCulling]), 2000 features", "frames": N,
                        "parallelism": "one stream per GPU"},
             "frame_ms": {"median": round(float(np.median(times[W:])) * 1e3, 3),
                          "mean": round(float(np.mean(times[W:])) * 1e3, 3),
