@@ -169,6 +169,9 @@ def run_track(a, rank, world, local, dist):
     vocab = Vocabulary.synthetic(k=10, L=6, seed=7)
     S["vocab"] = vocab
     voc = ORBVocabulary(vocab, device=local)
+    # (ComputeBoW on the extraction stream, orbmi_vocabulary_share_stream, was measured slower:
+    # 1,489 vs 2,517 frames/s -- the transform then queues behind the frames the host enqueued
+    # ahead, and the LocalMapping thread waits for it)
     mapper = LocalMapper(local, vocabulary=voc)
     kf_desc = lambda f: (S["keep"][1][f].data_ptr(), S["n_lf"][f])  # noqa: E731  (the keyframe's descriptors)
     xch = StreamExchange(tr, dist, local) if dist is not None else None  # config 4
@@ -262,8 +265,11 @@ def run_track(a, rank, world, local, dist):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    host_s = 0.0  # time the host spends enqueueing (a host-bound step shows host ~ wall)
     for i in range(a.steps):
+        th = time.perf_counter()
         step(i)
+        host_s += time.perf_counter() - th
     sync()
     if dist:
         dist.barrier()
@@ -309,6 +315,7 @@ def run_track(a, rank, world, local, dist):
             },
             "kpts_desc_per_s": round(value * kp_per_frame, 1),
             "keypoints_per_frame": round(kp_per_frame, 1),
+            "host_enqueue_ms_per_step_timed": round(host_s / a.steps * 1e3, 4),
             "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp, "inliers": outcome["inliers"],
                                   "tracking_ok": outcome["ok"]},
             "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},

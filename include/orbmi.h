@@ -285,6 +285,11 @@ typedef struct orbmi_vocabulary orbmi_vocabulary;
 int orbmi_vocabulary_create(int device, const orbmi_vocabulary_desc* d, orbmi_vocabulary** out);
 void orbmi_vocabulary_destroy(orbmi_vocabulary* v);
 int orbmi_vocabulary_synchronize(orbmi_vocabulary* v);
+/* Run the handle on `ex`'s stream (like orbmi_matcher_share_stream): a keyframe's ComputeBoW then
+ * follows its extraction on the extraction stream, beside the LocalBA on the mapper's stream. */
+int orbmi_vocabulary_share_stream(orbmi_vocabulary* v, orbmi_extractor* ex);
+/* The handle's HIP stream (hipStream_t): its own, or the extractor's after share_stream. */
+int orbmi_vocabulary_get_stream(orbmi_vocabulary* v, void** stream);
 
 /* TemplatedVocabulary::transform(features, BowVector& v, FeatureVector& fv, levelsup)
  * (TemplatedVocabulary.h:1126-1194, per feature :1217-1259) as Frame::ComputeBoW calls it

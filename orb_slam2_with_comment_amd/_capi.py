@@ -83,6 +83,8 @@ _PROTOS = {
     "orbmi_vocabulary_create": (_i, [_i, _vp, C.POINTER(_vp)]),
     "orbmi_vocabulary_destroy": (None, [_vp]),
     "orbmi_vocabulary_synchronize": (_i, [_vp]),
+    "orbmi_vocabulary_share_stream": (_i, [_vp, _vp]),
+    "orbmi_vocabulary_get_stream": (_i, [_vp, C.POINTER(_vp)]),
     "orbmi_transform": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_fuse_search": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, _vp, C.POINTER(_i)]),

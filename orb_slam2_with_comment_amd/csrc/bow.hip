@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(
 struct orbmi_vocabulary {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;           // false after orbmi_vocabulary_share_stream
     orbmi::VocDev v{};
     void* d_vocab = nullptr;          // one allocation for all vocabulary arrays
     uint8_t* d_work = nullptr;        // keys, weights and staging of one transform
@@ -326,8 +327,27 @@ void orbmi_vocabulary_destroy(orbmi_vocabulary* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->d_vocab) (void)hipFree(h->d_vocab);
     if (h->d_work) (void)hipFree(h->d_work);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
+}
+
+int orbmi_vocabulary_get_stream(orbmi_vocabulary* h, void** stream) {
+    if (!h || !stream) return ORBMI_E_ARG;
+    *stream = (void*)h->stream;
+    return ORBMI_OK;
+}
+
+int orbmi_vocabulary_share_stream(orbmi_vocabulary* h, orbmi_extractor* ex) {
+    if (!h || !ex) return ORBMI_E_ARG;
+    void* s = nullptr;
+    int rc = orbmi_extractor_get_stream(ex, &s);
+    if (rc) return rc;
+    ORBMI_HIP(hipSetDevice(h->device));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) ORBMI_HIP(hipStreamDestroy(h->stream));
+    h->stream = (hipStream_t)s;
+    h->own_stream = false;
+    return ORBMI_OK;
 }
 
 int orbmi_vocabulary_synchronize(orbmi_vocabulary* h) {

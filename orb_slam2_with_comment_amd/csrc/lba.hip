@@ -74,7 +74,7 @@ struct BaCtl {
 
 struct BaDev {
     int nkf, npt, nedge, nblk, nf;  // nf = non-fixed keyframes (nblk = nf (nf + 1) / 2)
-    int nb_e, nb_p, nb_q;           // blocks: edges (256), points (256), points (32 per block)
+    int nb_e, nb_p, nb_q;           // blocks: edges (256), points (256), points (kBaUpdPts per block)
     BaCtl* ctl;
     const volatile int* stop;  // host-mapped mirror of pbStopFlag (may be null)
     double* Tb[2];             // poses: SE3Quat (x, y, z, w, tx, ty, tz, -), current / trial
@@ -96,6 +96,7 @@ struct BaDev {
     int* blk_cnt;              // nblk: pairs per block (k_ba_pairs_count)
     int* blk_start;            // nblk + 1 (k_ba_pairs_fill)
     int2* blk_pairs;           // (e_a, e_b): edges of one point into keyframes a and b
+    int* blk_pt;               // the pair's point (so k_ba_schur's loads of a pair go out together)
     double* err;               // nedge x 3 (stale semantics)
     unsigned char* eflag;      // bit0 level-1, bit1 no robust kernel, bit2 active
     int* pose_idx;             // nkf
@@ -451,7 +452,11 @@ __global__ __launch_bounds__(kPairThreads) void k_ba_pairs_fill(BaDev a) {
         const int o = off + block_excl_scan(r.y - r.x, scratch, &total);
         if (j < a1) {
             const int ea = a.kf_edges[j];
-            for (int t = r.x; t < r.y; t++) a.blk_pairs[o + t - r.x] = make_int2(ea, a.kf_edges[b0 + t]);
+            const int pt = a.kf_pt[j];
+            for (int t = r.x; t < r.y; t++) {
+                a.blk_pairs[o + t - r.x] = make_int2(ea, a.kf_edges[b0 + t]);
+                a.blk_pt[o + t - r.x] = pt;
+            }
         }
         off += total;
     }
@@ -662,12 +667,16 @@ __device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
     const double* base = a.Hpe + 27 * (long long)a.kf_start[k] + q0 + q;
     const int n = a.kf_start[k + 1] - a.kf_start[k];
     if (el < kLanes) {
-        double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // eight loads in flight per lane
-        int m = el;
-        for (; m + 7 * kLanes < n; m += 8 * kLanes)
+        double v[16];  // sixteen loads in flight per lane
 #pragma unroll
-            for (int u = 0; u < 8; u++) v[u] += base[27 * (long long)(m + u * kLanes)];
+        for (int u = 0; u < 16; u++) v[u] = 0;
+        int m = el;
+        for (; m + 15 * kLanes < n; m += 16 * kLanes)
+#pragma unroll
+            for (int u = 0; u < 16; u++) v[u] += base[27 * (long long)(m + u * kLanes)];
         for (int u = 0; m < n; m += kLanes, u++) v[u] += base[27 * (long long)m];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] += v[u + 8];
         red[el * NQ + q] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
     }
     __syncthreads();
@@ -747,7 +756,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     for (int j = a.blk_start[b] + threadIdx.x; j < a.blk_start[b + 1]; j += blockDim.x) {
         const int2 pr = a.blk_pairs[j];  // inactive edges carry a zero Hpl block
         double Di[9];
-        point_dinv(a.Hll, a.edges[pr.x].point, lam, Di);
+        point_dinv(a.Hll, a.blk_pt[j], lam, Di);
         const double* B1 = a.Hpl + 18 * (long long)pr.x;
         const double* B2 = a.Hpl + 18 * (long long)pr.y;
         double BD[18];
@@ -1286,13 +1295,14 @@ __device__ inline void k_ba_control_body(const BaDev& a) {
 }
 
 // ---------------------------------------------------------------- update + trial errors
-// block = 32 points.  Threads 0..31: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
+// block = kBaUpdPts points, 8 lanes each: x_l = D^-1 (b_l - Hpl^T x_p), X_t = X + x_l (computeScale
 // part); then every thread takes edges of the block's points: computeActiveErrors on the trial
 // state (T_t from the solve) and the edge's linearisation at that state into the other
 // linear-system buffer; threads 0..31 then sum the points' Hll / b_l there.  Block partials:
 // robust chi2 and scale; the last block to finish runs the Levenberg decision.
-constexpr int kBaUpdPts = 32;
-constexpr int kBaUpdLanes = kBaBlock / kBaUpdPts;  // 8 threads per point
+constexpr int kBaUpdPts = 32;                      // (16 per block, 188 blocks for config 3, measured slower)
+constexpr int kBaUpdLanes = 8;                     // threads per point
+constexpr int kBaUpdThreads = kBaUpdPts * kBaUpdLanes;
 constexpr int kBaUpdLdsEdges = 512;                // a block's edges whose Hll / b_l terms stay in LDS
 static_assert(kBaUpdLanes == 8, "8-lane segmented sums");
 
@@ -1304,7 +1314,7 @@ __device__ inline double sum8(double v) {
     return v + dpp_mov<kDppHalfMirror>(v);
 }
 
-__global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
+__global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     BaCtl& ctl = *a.ctl;
     if (ctl.done) return;
     const int L = ctl.lin;
@@ -1316,7 +1326,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
     double* __restrict__ Xt = a.Xb[ctl.cur ^ 1];
     double* __restrict__ part_chi = a.part_tchi;
     double* __restrict__ part_scale = a.part_tscale;
-    __shared__ double red[kBaBlock / 64];
+    __shared__ double red[kBaUpdThreads / 64];
     __shared__ double xs[kBaUpdPts][4];
     __shared__ double sHe[kBaUpdLdsEdges * 9];
     __shared__ bool last;
@@ -1395,8 +1405,8 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_update_errors(BaDev a) {
             for (int k = 0; k < 3; k++) t.bl[3 * p + k] = h[6 + k];
         }
     }
-    chi = block_sum<kBaBlock>(chi, red);
-    sc = block_sum<kBaBlock>(sc, red);
+    chi = block_sum<kBaUpdThreads>(chi, red);
+    sc = block_sum<kBaUpdThreads>(sc, red);
     if (tid == 0) {
         part_chi[blockIdx.x] = chi;
         part_scale[blockIdx.x] = sc;
@@ -1529,7 +1539,7 @@ struct Runner {
         if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
         if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaBlock), 0, h.stream, a);
+        hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaUpdThreads), 0, h.stream, a);
     }
 
     // SparseOptimizer::optimize(iterations) as phase 0 / 1, then activeRobustChi2
@@ -1672,7 +1682,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk);
     const size_t up_bytes = off;
     const size_t o_blk_cnt = take(4 * (size_t)nblk), o_blk_start = take(4 * ((size_t)nblk + 1)),
-                 o_pairs = take(8 * (size_t)npair);
+                 o_pairs = take(8 * (size_t)npair), o_pairpt = take(4 * (size_t)npair);
     const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
                  o_X1 = take(32 * npt), o_err = take(24 * (size_t)ne), o_eflag = take(ne), o_pidx = take(4 * nkf), o_kfact = take(4 * nkf),
                  o_pkf = take(4 * kBaMaxPoses), o_Hpl = take(2 * 144 * (size_t)ne), o_Hle = take(2 * 72 * (size_t)ne),
@@ -1740,6 +1750,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.blk_cnt = (int*)(B + o_blk_cnt);
     a.blk_start = (int*)(B + o_blk_start);
     a.blk_pairs = (int2*)(B + o_pairs);
+    a.blk_pt = (int*)(B + o_pairpt);
     a.err = (double*)(B + o_err); a.eflag = B + o_eflag;
     a.pose_idx = (int*)(B + o_pidx); a.pose_kf = (int*)(B + o_pkf); a.kf_act = (int*)(B + o_kfact);
     for (int L = 0; L < 2; L++) {  // two linear-system buffers (ctl.lin selects the current one)

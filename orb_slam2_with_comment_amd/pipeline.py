@@ -297,6 +297,7 @@ class LocalMapper:
     def __init__(self, device=0, vocabulary=None, max_features=8192):
         import torch
         from .optimizer import LocalBA
+        self.device = device
         self.ba = LocalBA(device)
         self.voc = vocabulary  # ORBVocabulary (device handle) or None
         if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
@@ -329,16 +330,27 @@ class LocalMapper:
                     self.voc.transform_device(d_desc, n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
                                               b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
                                               b["counts"].data_ptr())
+                    bow_done = self._bow_event()
                 # LocalBundleAdjustment reads poses, points and observations, never the BowVector,
                 # so the transform (vocabulary stream) and the LocalBA (its own stream) overlap;
-                # both are complete before the next keyframe is taken
+                # both are complete before the next keyframe is taken (an event, not a stream
+                # sync: the vocabulary may share the extraction stream, which runs ahead)
                 self.last = self.ba.run(problem)
                 if self.voc is not None and kf_desc is not None:
-                    self.voc.synchronize()
+                    bow_done.synchronize()
                 self.done += 1
             except Exception as e:  # surfaced by wait()
                 self.error = e
             self.q.task_done()
+
+    def _bow_event(self):
+        """Event recorded on the vocabulary's stream after the transform just enqueued."""
+        import torch
+        s = C.c_void_p()
+        check("orbmi_vocabulary_get_stream", lib().orbmi_vocabulary_get_stream(self.voc._h, C.byref(s)))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.ExternalStream(s.value, device=torch.device("cuda", self.device)))
+        return ev
 
     def insert_keyframe(self, problem, kf_desc=None):
         """Queue a keyframe: its LocalBA problem and, for ComputeBoW, (device address of its
