@@ -559,6 +559,21 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         }
         if (tid == 0) S.rpre[0] = 0;
     }
+    // per-axis path tables (x: its own root's extent, y: the level height), in the LDS of the
+    // careful-mode sort keys, built while the counts above are in flight
+    unsigned short* xpath = reinterpret_cast<unsigned short*>(S.skey);
+    unsigned short* ypath = xpath + 4096;
+    const int wx = min(g.width, 4095), hy = min(g.height, 4095);
+    for (int v = tid; v <= wx + 1 + hy; v += blockDim.x) {
+        if (v <= wx) {
+            const int n = oct_root((uint32_t)v, g);
+            xpath[v] = (unsigned short)oct_axis(v, (int)(g.hX * (float)n), (int)(g.hX * (float)(n + 1)));
+        } else {
+            const int y = v - wx - 1;
+            ypath[y] = (unsigned short)oct_axis(y, 0, g.height);
+        }
+    }
+    for (int i = tid; i < g.nIni; i += blockDim.x) S.cnt[0][i] = 0;  // root counts (init below)
     __syncthreads();
     const int nkeys = min(S.rpre[kFastRegions], g.key_cap);
     auto key_slot = [&](int k, int& j) {  // j: a region at or before k's (walks forward)
@@ -605,23 +620,9 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         }
     };
 
-    // path bits of the register keys through per-axis tables (x: its own root's extent, y: the
-    // level height), built in the LDS of the careful-mode sort keys before any pass uses them
+    // path bits of the register keys (tables built above)
     unsigned preg[kOctRegKeys];
     {
-        unsigned short* xpath = reinterpret_cast<unsigned short*>(S.skey);
-        unsigned short* ypath = xpath + 4096;
-        const int wx = min(g.width, 4095), hy = min(g.height, 4095);
-        for (int v = tid; v <= wx + 1 + hy; v += blockDim.x) {
-            if (v <= wx) {
-                const int n = oct_root((uint32_t)v, g);
-                xpath[v] = (unsigned short)oct_axis(v, (int)(g.hX * (float)n), (int)(g.hX * (float)(n + 1)));
-            } else {
-                const int y = v - wx - 1;
-                ypath[y] = (unsigned short)oct_axis(y, 0, g.height);
-            }
-        }
-        __syncthreads();
 #pragma unroll
         for (int r = 0; r < kOctRegKeys; r++)
             preg[r] = xpath[min((int)(kreg[r] & 0xFFF), wx)] | (unsigned)ypath[min((int)((kreg[r] >> 12) & 0xFFF), hy)] << 16;
@@ -629,11 +630,9 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
     }
     OCT_STAMP(1, __builtin_amdgcn_s_memtime());
     OCT_STAMP(62, nkeys);
-    // ---- initial nodes (:543-579)
+    // ---- initial nodes (:543-579): counts per root (zeroed before the first barrier)
     const int nIni = g.nIni;
     int cur = 0;
-    for (int i = tid; i < nIni; i += blockDim.x) S.cnt[cur][i] = 0;
-    __syncthreads();
     {
         int run = -1, rc = 0;  // consecutive keys of a thread share a node: one atomic per run
         for_keys([&](int, uint32_t key, int& no) {
@@ -649,17 +648,33 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         if (rc) atomicAdd(&S.cnt[cur][run], rc);
     }
     __syncthreads();
-    // drop empty initial nodes (:581-593)
-    for (int i = tid; i < nIni; i += blockDim.x) S.tmp[i] = S.cnt[cur][i] > 0;
-    __syncthreads();
-    int L = block_scan_array(S.tmp, nIni, S.scratch);
-    for (int i = tid; i < nIni; i += blockDim.x) {
-        const short ni = S.cnt[cur][i] > 0 ? (short)S.tmp[i] : (short)-1;
-        S.remap[i][0] = S.remap[i][1] = S.remap[i][2] = S.remap[i][3] = ni;
-        if (ni >= 0) S.cnt[cur ^ 1][ni] = S.cnt[cur][i];
+    // drop empty initial nodes (:581-593): a ballot scan in wave 0 (nIni <= 64), else block scans
+    int L;
+    if (nIni <= 64) {
+        if (tid < 64) {
+            const int c = tid < nIni ? S.cnt[cur][tid] : 0;
+            const unsigned long long m = __ballot(c > 0);
+            const int ni = c > 0 ? __popcll(m & ((1ull << tid) - 1)) : -1;
+            if (tid < nIni) {
+                S.remap[tid][0] = S.remap[tid][1] = S.remap[tid][2] = S.remap[tid][3] = (short)ni;
+                if (ni >= 0) S.cnt[cur ^ 1][ni] = c;
+            }
+            if (tid == 0) S.misc[4] = __popcll(m);
+        }
+        __syncthreads();
+        L = S.misc[4];
+    } else {
+        for (int i = tid; i < nIni; i += blockDim.x) S.tmp[i] = S.cnt[cur][i] > 0;
+        __syncthreads();
+        L = block_scan_array(S.tmp, nIni, S.scratch);
+        for (int i = tid; i < nIni; i += blockDim.x) {
+            const short ni = S.cnt[cur][i] > 0 ? (short)S.tmp[i] : (short)-1;
+            S.remap[i][0] = S.remap[i][1] = S.remap[i][2] = S.remap[i][3] = ni;
+            if (ni >= 0) S.cnt[cur ^ 1][ni] = S.cnt[cur][i];
+        }
+        __syncthreads();
     }
     cur ^= 1;
-    __syncthreads();
 
     const int N = g.nfeat;
     bool careful = false, finish = false;

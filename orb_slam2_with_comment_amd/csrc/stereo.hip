@@ -21,15 +21,36 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(const orbmi_keypoint* __re
                                                       int list_cap) {
     __shared__ int cnt[kStereoRowsMax];
     __shared__ int scratch[20];
+    constexpr int kRegs = 4;  // right keypoints per thread kept in registers (4096)
     const int tid = threadIdx.x;
     const int nR = min(*countR, capR);
     for (int i = tid; i < nrows; i += blockDim.x) cnt[i] = 0;
-    __syncthreads();
-    for (int i = tid; i < nR; i += blockDim.x) {
+    // the row band of each right keypoint, loaded once (:514-527)
+    int lo[kRegs], hi[kRegs];
+#pragma unroll
+    for (int k = 0; k < kRegs; k++) {
+        const int i = tid + k * 1024;
+        lo[k] = 0;
+        hi[k] = -1;
+        if (i < nR) {
+            const orbmi_keypoint kp = kpsR[i];
+            const float r = 2.0f * scale[kp.octave];
+            lo[k] = max((int)floorf(kp.y - r), 0);
+            hi[k] = min((int)ceilf(kp.y + r), nrows - 1);
+        }
+    }
+    auto band = [&](int k, int i, int& a, int& b) {
+        if (k < kRegs) { a = lo[k]; b = hi[k]; return; }
         const orbmi_keypoint kp = kpsR[i];
         const float r = 2.0f * scale[kp.octave];
-        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++) atomicAdd(&cnt[yi], 1);
+        a = max((int)floorf(kp.y - r), 0);
+        b = min((int)ceilf(kp.y + r), nrows - 1);
+    };
+    __syncthreads();
+    for (int i = tid, k = 0; i < nR; i += blockDim.x, k++) {
+        int a, b;
+        band(k, i, a, b);
+        for (int yi = a; yi <= b; yi++) atomicAdd(&cnt[yi], 1);
     }
     __syncthreads();
     // exclusive scan of cnt (4 rows per thread)
@@ -44,11 +65,10 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(const orbmi_keypoint* __re
     }
     if (tid == 0) row_start[nrows] = total;
     __syncthreads();
-    for (int i = tid; i < nR; i += blockDim.x) {
-        const orbmi_keypoint kp = kpsR[i];
-        const float r = 2.0f * scale[kp.octave];
-        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++) {
+    for (int i = tid, k = 0; i < nR; i += blockDim.x, k++) {
+        int a, b;
+        band(k, i, a, b);
+        for (int yi = a; yi <= b; yi++) {
             const int p = atomicAdd(&cnt[yi], 1);
             if (p < list_cap) row_list[p] = i;
         }
