@@ -1624,26 +1624,14 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const int nkf = P->nkf, npt = P->npt, ne = P->nedge;
     if (nkf > kBaMaxKf) return ORBMI_E_UNSUPPORTED;
     // host-side graph indexing: edges grouped by point (the reference inserts them point by
-    // point), CSR by keyframe, keyframes ordered by id (SparseOptimizer vertex order)
+    // point), CSR by keyframe, keyframes ordered by id (SparseOptimizer vertex order).  The index
+    // arrays are written straight into the pinned staging buffer that goes up in one copy.
     for (int i = 0; i < ne; i++) {
         const orbmi_ba_edge& e = P->edges[i];
         if (e.point < 0 || e.point >= npt || e.kf < 0 || e.kf >= nkf) return ORBMI_E_ARG;
         if (i && e.point < P->edges[i - 1].point) return ORBMI_E_ARG;
     }
-    std::vector<int> pt_start(npt + 1, 0), kf_start(nkf + 1, 0), kf_edges(std::max(ne, 1)), order(std::max(nkf, 1));
-    for (int i = 0; i < ne; i++) { pt_start[P->edges[i].point + 1]++; kf_start[P->edges[i].kf + 1]++; }
-    for (int p = 0; p < npt; p++) pt_start[p + 1] += pt_start[p];
-    for (int k = 0; k < nkf; k++) kf_start[k + 1] += kf_start[k];
-    std::vector<int> kf_pos(std::max(ne, 1)), kf_pt(std::max(ne, 1));
-    {
-        std::vector<int> fill(kf_start.begin(), kf_start.end() - 1);
-        for (int i = 0; i < ne; i++) {
-            const int j = fill[P->edges[i].kf]++;
-            kf_pos[i] = j;
-            kf_edges[j] = i;
-            kf_pt[j] = P->edges[i].point;
-        }
-    }
+    std::vector<int> order(std::max(nkf, 1));
     for (int k = 0; k < nkf; k++) order[k] = k;
     std::stable_sort(order.begin(), order.begin() + nkf, [&](int x, int y) { return P->kfs[x].id < P->kfs[y].id; });
     // Schur pair lists: blocks = pairs of non-fixed keyframes (a, b) with rank(a) <= rank(b)
@@ -1657,18 +1645,6 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     if (nblk_ll > (1 << 20)) return ORBMI_E_UNSUPPORTED;
     const int nblk = (int)nblk_ll;
     auto blk_of = [nf](int ra, int rb) { return ra * nf - ra * (ra - 1) / 2 + (rb - ra); };
-    std::vector<int> blk_kf(2 * std::max(nblk, 1));
-    for (int ra = 0; ra < nf; ra++)
-        for (int rb = ra; rb < nf; rb++) { blk_kf[2 * blk_of(ra, rb)] = free_kf[ra]; blk_kf[2 * blk_of(ra, rb) + 1] = free_kf[rb]; }
-    // capacity of the pair lists (built on the device): sum over points of (free edges)^2
-    long long npair_cap = 0;
-    for (int p = 0; p < npt; p++) {
-        long long m = 0;
-        for (int e = pt_start[p]; e < pt_start[p + 1]; e++) m += rank[P->edges[e].kf] >= 0;
-        npair_cap += m * m;
-    }
-    if (npair_cap > (1LL << 28)) return ORBMI_E_UNSUPPORTED;
-    const int npair = (int)npair_cap;
     // ---- one device arena; the graph and its index arrays go up in one copy
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
     const int nb_q = std::max(1, (npt + kBaUpdPts - 1) / kBaUpdPts);
@@ -1681,6 +1657,56 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne),
                  o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk);
     const size_t up_bytes = off;
+    hipStream_t s = h.stream;
+    // the previous call's upload may still be reading the staging buffer
+    ORBMI_HIP(hipStreamSynchronize(s));
+    if (up_bytes > h.cap_stage) {
+        if (h.h_stage) (void)hipHostFree(h.h_stage);
+        h.h_stage = nullptr;
+        h.cap_stage = 0;
+        ORBMI_HIP(hipHostMalloc((void**)&h.h_stage, up_bytes));
+        h.cap_stage = up_bytes;
+    }
+    uint8_t* S = h.h_stage;
+    int* pt_start = (int*)(S + o_pts_start);
+    int* kf_start = (int*)(S + o_kfs_start);
+    int* kf_edges = (int*)(S + o_kf_edges);
+    int* kf_pos = (int*)(S + o_kf_pos);
+    int* kf_pt = (int*)(S + o_kf_pt);
+    std::memset(pt_start, 0, 4 * (size_t)(npt + 1));
+    std::memset(kf_start, 0, 4 * (size_t)(nkf + 1));
+    for (int i = 0; i < ne; i++) { pt_start[P->edges[i].point + 1]++; kf_start[P->edges[i].kf + 1]++; }
+    for (int p = 0; p < npt; p++) pt_start[p + 1] += pt_start[p];
+    for (int k = 0; k < nkf; k++) kf_start[k + 1] += kf_start[k];
+    // capacity of the pair lists (built on the device): sum over points of (free edges)^2
+    long long npair_cap = 0;
+    {
+        std::vector<int> fill(kf_start, kf_start + nkf);
+        int p = -1;
+        long long m = 0;
+        for (int i = 0; i < ne; i++) {
+            const orbmi_ba_edge& e = P->edges[i];
+            const int j = fill[e.kf]++;
+            kf_pos[i] = j;
+            kf_edges[j] = i;
+            kf_pt[j] = e.point;
+            if (e.point != p) { npair_cap += m * m; m = 0; p = e.point; }
+            m += rank[e.kf] >= 0;
+        }
+        npair_cap += m * m;
+    }
+    if (npair_cap > (1LL << 28)) return ORBMI_E_UNSUPPORTED;
+    const int npair = (int)npair_cap;
+    if (nkf) std::memcpy(S + o_order, order.data(), 4 * (size_t)nkf);
+    {
+        int* bk = (int*)(S + o_blk_kf);
+        for (int ra = 0; ra < nf; ra++)
+            for (int rb = ra; rb < nf; rb++) { bk[2 * blk_of(ra, rb)] = free_kf[ra]; bk[2 * blk_of(ra, rb) + 1] = free_kf[rb]; }
+    }
+    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(S + o, src, bytes); };
+    put(o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf);
+    put(o_pts, P->pts, sizeof(orbmi_ba_point) * npt);
+    put(o_edges, P->edges, sizeof(orbmi_ba_edge) * ne);
     const size_t o_blk_cnt = take(4 * (size_t)nblk), o_blk_start = take(4 * ((size_t)nblk + 1)),
                  o_pairs = take(8 * (size_t)npair), o_pairpt = take(4 * (size_t)npair);
     const size_t o_e_pi = take(4 * (size_t)ne), o_T0 = take(64 * nkf), o_T1 = take(64 * nkf), o_X0 = take(32 * npt),
@@ -1699,29 +1725,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         ORBMI_HIP(hipMalloc((void**)&h.d_buf, off));
         h.cap = off;
     }
-    if (up_bytes > h.cap_stage) {
-        if (h.h_stage) (void)hipHostFree(h.h_stage);
-        h.h_stage = nullptr;
-        h.cap_stage = 0;
-        ORBMI_HIP(hipHostMalloc((void**)&h.h_stage, up_bytes));
-        h.cap_stage = up_bytes;
-    }
     uint8_t* B = h.d_buf;
-    uint8_t* S = h.h_stage;
-    hipStream_t s = h.stream;
-    // the previous call's upload may still be reading the staging buffer
-    ORBMI_HIP(hipStreamSynchronize(s));
-    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(S + o, src, bytes); };
-    put(o_kfs, P->kfs, sizeof(orbmi_ba_keyframe) * nkf);
-    put(o_pts, P->pts, sizeof(orbmi_ba_point) * npt);
-    put(o_edges, P->edges, sizeof(orbmi_ba_edge) * ne);
-    put(o_order, order.data(), 4 * nkf);
-    put(o_pts_start, pt_start.data(), 4 * (npt + 1));
-    put(o_kfs_start, kf_start.data(), 4 * (nkf + 1));
-    put(o_kf_edges, kf_edges.data(), 4 * (size_t)ne);
-    put(o_kf_pos, kf_pos.data(), 4 * (size_t)ne);
-    put(o_kf_pt, kf_pt.data(), 4 * (size_t)ne);
-    put(o_blk_kf, blk_kf.data(), 8 * (size_t)nblk);
     tr.mark("host_index");
     ORBMI_HIP(hipMemcpyAsync(B, S, up_bytes, hipMemcpyHostToDevice, s));
     ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
