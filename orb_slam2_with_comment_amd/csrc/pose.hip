@@ -34,6 +34,14 @@ namespace orbmi {
 #endif
 constexpr int kPoseThreads = ORBMI_POSE_THREADS;  // 8 waves, 2 per SIMD: the per-edge passes hide fp64 latency
 constexpr int kPoseWaves = kPoseThreads / 64;
+// buildSystem runs on one wave per SIMD: its pass is VALU-issue-bound, so two waves per SIMD
+// take as long for the same edges, and each extra wave pays ~250 instructions of reduce-scatter
+#ifndef ORBMI_POSE_FULL_WAVES
+#define ORBMI_POSE_FULL_WAVES 4
+#endif
+constexpr int kPoseFullWaves = ORBMI_POSE_FULL_WAVES;
+constexpr int kPoseFullThreads = kPoseFullWaves * 64;
+static_assert(kPoseFullWaves >= 1 && kPoseFullWaves <= kPoseWaves, "buildSystem waves");
 constexpr int kPoseTraceWaves = 8;  // trace layout (orbmi_debug_pose_trace), whatever kPoseWaves
 constexpr int kPoseMaxObs = 4096;
 constexpr int kPoseTraceSeqs = 64;  // passes recorded by orbmi_debug_pose_trace
@@ -73,24 +81,27 @@ __device__ inline double pose_chi2(const orbmi_pose_obs& o, const double e[3]) {
     return e[0] * (info * e[0]) + e[1] * (info * e[1]) + (o.ur < 0 ? 0.0 : e[2] * (info * e[2]));
 }
 
-// fixed-order workgroup sum of the 28 normal-equation terms into wave 0: every wave
-// reduce-scatters its lanes' terms (DPP / permlane swaps), writes one LDS slot per (wave, value);
-// after the barrier wave 0's lane q sums value q over the waves in wave order, stores it in
-// stot[q] and every lane of wave 0 reads the 28 totals back (broadcast LDS reads).  The other
-// waves' acc is left unspecified; stot keeps the system for a later re-solve.
+// fixed-order workgroup sum of the 28 normal-equation terms into wave 0: each of the first
+// kPoseFullWaves waves (the ones that ran buildSystem) reduce-scatters its lanes' terms (DPP /
+// permlane swaps) and writes one LDS slot per (wave, value); after the barrier wave 0's lane q
+// sums value q over those waves in wave order, stores it in stot[q] and every lane of wave 0
+// reads the 28 totals back (broadcast LDS reads).  The other waves' acc is left unspecified;
+// stot keeps the system for a later re-solve.
 __device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], double* stot) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double v[32];
+    if (wid < kPoseFullWaves) {
+        double v[32];
 #pragma unroll
-    for (int q = 0; q < 28; q++) v[q] = acc[q];
-    v[28] = v[29] = v[30] = v[31] = 0;
-    const double s = wave_reduce_scatter32(v);
-    if (!(lane & 1)) red[wid][lane >> 1] = s;
+        for (int q = 0; q < 28; q++) v[q] = acc[q];
+        v[28] = v[29] = v[30] = v[31] = 0;
+        const double s = wave_reduce_scatter32(v);
+        if (!(lane & 1)) red[wid][lane >> 1] = s;
+    }
     __syncthreads();
     if (wid == 0) {
         double t = 0;
 #pragma unroll
-        for (int w = 0; w < kPoseWaves; w++) t += red[w][lane & 31];
+        for (int w = 0; w < kPoseFullWaves; w++) t += red[w][lane & 31];
         if (lane < 28) stot[lane] = t;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -162,14 +173,61 @@ __device__ inline bool pose_solve6(const double H[21], const double b[6], double
     return ok;
 }
 
-// computeActiveErrors + activeRobustChi2 + buildSystem at T for this thread's level-0 edges:
+// linearizeOplus + constructQuadraticForm of one edge at its camera-frame point p (1/z = invz),
+// error e and weight wsel = rho' * information
+__device__ inline void pose_quadratic(const PoseCam& cam, bool stereo, const double p[3], double invz, const double e[3],
+                                      double wsel, double (&acc)[28]) {
+    // linearizeOplus (types_six_dof_expmap.cpp:266-290, :332-364) in normalised coordinates
+    // X = x / z, Y = y / z; J[0][4] = J[1][3] = J[2][4] = 0 and the third row is zero for
+    // monocular edges: those products are skipped.  Every term is one FMA into its
+    // accumulator (the contraction order differs from g2o's by rounding only).
+    const double iz = invz, X = p[0] * iz, Y = p[1] * iz;
+    const double Xfx = X * cam.fx, Yfy = Y * cam.fy;
+    const double a0 = Xfx * Y, a1 = -(cam.fx + X * Xfx), a2 = Y * cam.fx, a3 = -iz * cam.fx, a5 = Xfx * iz;
+    const double b0 = cam.fy + Y * Yfy, b1 = -X * Yfy, b2 = -X * cam.fy, b4 = -iz * cam.fy, b5 = Yfy * iz;
+    const double w = wsel;  // robustInformation
+    const double wa0 = w * a0, wa1 = w * a1, wa2 = w * a2, wa3 = w * a3, wa5 = w * a5;
+    const double wb0 = w * b0, wb1 = w * b1, wb2 = w * b2, wb4 = w * b4, wb5 = w * b5;
+    const double ea = w * e[0], eb = w * e[1];
+    // upper triangle, row-major: (0,0..5) (1,1..5) (2,2..5) (3,3..5) (4,4..5) (5,5)
+    acc[0] += a0 * wa0;  acc[0] += b0 * wb0;  acc[1] += a0 * wa1;  acc[1] += b0 * wb1;
+    acc[2] += a0 * wa2;  acc[2] += b0 * wb2;  acc[3] += a0 * wa3;  acc[4] += b0 * wb4;
+    acc[5] += a0 * wa5;  acc[5] += b0 * wb5;
+    acc[6] += a1 * wa1;  acc[6] += b1 * wb1;  acc[7] += a1 * wa2;  acc[7] += b1 * wb2;
+    acc[8] += a1 * wa3;  acc[9] += b1 * wb4;  acc[10] += a1 * wa5; acc[10] += b1 * wb5;
+    acc[11] += a2 * wa2; acc[11] += b2 * wb2; acc[12] += a2 * wa3; acc[13] += b2 * wb4;
+    acc[14] += a2 * wa5; acc[14] += b2 * wb5;
+    acc[15] += a3 * wa3; acc[17] += a3 * wa5;  // acc[16] = H(3,4) = 0
+    acc[18] += b4 * wb4; acc[19] += b4 * wb5;
+    acc[20] += a5 * wa5; acc[20] += b5 * wb5;
+    acc[21] -= a0 * ea;  acc[21] -= b0 * eb;  acc[22] -= a1 * ea;  acc[22] -= b1 * eb;
+    acc[23] -= a2 * ea;  acc[23] -= b2 * eb;  acc[24] -= a3 * ea;  acc[25] -= b4 * eb;
+    acc[26] -= a5 * ea;  acc[26] -= b5 * eb;
+    {  // stereo: third row, J[2] = J[0] + bf / z^2 * (-y, x, 0, 0, 0, -1); weight 0 for a
+       // monocular edge (branch-free: a wave with both kinds runs both paths anyway)
+        const double bfz = cam.bf * iz, wm = stereo ? w : 0.0;
+        const double c0 = a0 - bfz * Y, c1 = a1 + bfz * X, c2_ = a2, c3 = a3, c5 = a5 - bfz * iz;
+        const double wc0 = wm * c0, wc1 = wm * c1, wc2 = wm * c2_, wc3 = wm * c3, wc5 = wm * c5;
+        const double ec = wm * e[2];
+        acc[0] += c0 * wc0;  acc[1] += c0 * wc1;  acc[2] += c0 * wc2;  acc[3] += c0 * wc3;  acc[5] += c0 * wc5;
+        acc[6] += c1 * wc1;  acc[7] += c1 * wc2;  acc[8] += c1 * wc3;  acc[10] += c1 * wc5;
+        acc[11] += c2_ * wc2; acc[12] += c2_ * wc3; acc[14] += c2_ * wc5;
+        acc[15] += c3 * wc3; acc[17] += c3 * wc5;
+        acc[20] += c5 * wc5;
+        acc[21] -= c0 * ec;  acc[22] -= c1 * ec;  acc[23] -= c2_ * ec; acc[24] -= c3 * ec;  acc[26] -= c5 * ec;
+    }
+}
+
+// computeActiveErrors + activeRobustChi2 + buildSystem at T for this thread's level-0 edges
+// (threads < kPoseFullThreads):
 // acc[0..20] = upper 6x6 of J^T W J, acc[21..26] = b, acc[27] = robust chi2; schi = (float) chi2
 // of each edge (the stale errors the outlier test reads).
 __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbmi_pose_obs* sobs, const uint8_t* outl,
                                  float* schi, int n, bool robust, double (&acc)[28]) {
 #pragma unroll
     for (int q = 0; q < 28; q++) acc[q] = 0;
-    for (int k = threadIdx.x; k < n; k += kPoseThreads) {
+    const int k0 = threadIdx.x < kPoseFullThreads ? (int)threadIdx.x : n;  // the other waves: no edges
+    for (int k = k0; k < n; k += kPoseFullThreads) {
         if (outl[k]) continue;
         const orbmi_pose_obs o = sobs[k];
         double p[3], invz, e[3];
@@ -182,41 +240,7 @@ __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbm
             if (c2 > dsqr) { const double r = fast_rsqrt(c2), sq = c2 * r; rho0 = 2 * sq * d - dsqr; rho1 = d * r; }
         }
         acc[27] += rho0;
-        // linearizeOplus (types_six_dof_expmap.cpp:266-290, :332-364); J[0][4] = J[1][3] =
-        // J[2][4] = 0 and the third row is zero for monocular edges: those products are skipped
-        const double x = p[0], y = p[1], invz_2 = invz * invz;
-        const double a0 = x * y * invz_2 * cam.fx, a1 = -(1 + (x * x * invz_2)) * cam.fx, a2 = y * invz * cam.fx;
-        const double a3 = -invz * cam.fx, a5 = x * invz_2 * cam.fx;
-        const double b0 = (1 + y * y * invz_2) * cam.fy, b1 = -x * y * invz_2 * cam.fy, b2 = -x * invz * cam.fy;
-        const double b4 = -invz * cam.fy, b5 = y * invz_2 * cam.fy;
-        const double w = rho1 * info;  // robustInformation
-        const double wa0 = w * a0, wa1 = w * a1, wa2 = w * a2, wa3 = w * a3, wa5 = w * a5;
-        const double wb0 = w * b0, wb1 = w * b1, wb2 = w * b2, wb4 = w * b4, wb5 = w * b5;
-        const double ea = rho1 * (info * e[0]), eb = rho1 * (info * e[1]);
-        // upper triangle, row-major: (0,0..5) (1,1..5) (2,2..5) (3,3..5) (4,4..5) (5,5)
-        acc[0] += a0 * wa0 + b0 * wb0;  acc[1] += a0 * wa1 + b0 * wb1;  acc[2] += a0 * wa2 + b0 * wb2;
-        acc[3] += a0 * wa3;             acc[4] += b0 * wb4;             acc[5] += a0 * wa5 + b0 * wb5;
-        acc[6] += a1 * wa1 + b1 * wb1;  acc[7] += a1 * wa2 + b1 * wb2;  acc[8] += a1 * wa3;
-        acc[9] += b1 * wb4;             acc[10] += a1 * wa5 + b1 * wb5;
-        acc[11] += a2 * wa2 + b2 * wb2; acc[12] += a2 * wa3;            acc[13] += b2 * wb4;
-        acc[14] += a2 * wa5 + b2 * wb5;
-        acc[15] += a3 * wa3;            acc[17] += a3 * wa5;            // acc[16] = H(3,4) = 0
-        acc[18] += b4 * wb4;            acc[19] += b4 * wb5;
-        acc[20] += a5 * wa5 + b5 * wb5;
-        acc[21] -= a0 * ea + b0 * eb;   acc[22] -= a1 * ea + b1 * eb;   acc[23] -= a2 * ea + b2 * eb;
-        acc[24] -= a3 * ea;             acc[25] -= b4 * eb;             acc[26] -= a5 * ea + b5 * eb;
-        if (!(o.ur < 0)) {  // stereo: third row
-            const double c0 = a0 - cam.bf * y * invz_2, c1 = a1 + cam.bf * x * invz_2, c2_ = a2, c3 = a3;
-            const double c5 = a5 - cam.bf * invz_2;
-            const double wc0 = w * c0, wc1 = w * c1, wc2 = w * c2_, wc3 = w * c3, wc5 = w * c5;
-            const double ec = rho1 * (info * e[2]);
-            acc[0] += c0 * wc0;  acc[1] += c0 * wc1;  acc[2] += c0 * wc2;  acc[3] += c0 * wc3;  acc[5] += c0 * wc5;
-            acc[6] += c1 * wc1;  acc[7] += c1 * wc2;  acc[8] += c1 * wc3;  acc[10] += c1 * wc5;
-            acc[11] += c2_ * wc2; acc[12] += c2_ * wc3; acc[14] += c2_ * wc5;
-            acc[15] += c3 * wc3; acc[17] += c3 * wc5;
-            acc[20] += c5 * wc5;
-            acc[21] -= c0 * ec;  acc[22] -= c1 * ec;  acc[23] -= c2_ * ec; acc[24] -= c3 * ec;  acc[26] -= c5 * ec;
-        }
+        pose_quadratic(cam, !(o.ur < 0), p, invz, e, rho1 * info, acc);
     }
 }
 
@@ -311,7 +335,8 @@ struct PoseGatherArgs {
 // TR = event trace (orbmi_debug_pose_trace): lane 0 of every wave stamps s_memtime per edge
 // pass (seq) into trace[16 + (seq * kPoseTraceWaves + wave) * 8 + e]: e = 0 pass start, 1 pass end,
 // 2 chi2 barrier (B1) passed, 3 Levenberg decision taken, 4 (accepted trial) system reduced,
-// 5 (wave 0) trial chain published, 6 candidates barrier (B3) passed; trace[0] = total cycles,
+// 5 (wave 0) trial chain published, 6 candidates barrier (B3) passed, 7 (accepted trial) full
+// pass done; trace[0] = total cycles,
 // [1] = total s_memrealtime ticks, [2] = passes of thread 0's wave.
 // GATHER = the edge assembly (PoseGatherArgs g) runs in the prologue, straight into LDS: the
 // frame record is g.rec, edges are compacted in keypoint order by a workgroup scan, mvbOutlier
@@ -509,6 +534,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
                     if (accept) {  // buildSystem at the (new) estimate: the first iteration's, or
                                    // the next iteration's after an accepted trial
                         pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
+                        EV(7);
                         pose_reduce28_w0(acc, red[rb], stot);  // B2 inside
                         rb ^= 1;
                     } else {

@@ -44,7 +44,8 @@ for n in (420, 680):
     # per trial (seq): pass, chi2 barrier B1, decision; accepted trials add the 28-value
     # reduction (B2), wave 0's lane-parallel trial chain and the candidates barrier B3 (cycles)
     sums = {"trial(wave0)": [], "pass(max wave)": [], "pass(wave0)": [], "B1 wait(wave0)": [],
-            "decision(wave0)": [], "reduce+B2(wave0)": [], "chain solve(wave0)": [], "B3 wait(wave1)": []}
+            "decision(wave0)": [], "reduce+B2(wave0)": [], "  full pass(wave0)": [], "  full pass(max wave)": [],
+            "  reduce28+B2(wave0)": [], "chain solve(wave0)": [], "B3 wait(wave1)": []}
     acc_n = 0
     for s in range(1, min(nseq, SEQS) - 1):
         e, nxt = ev[s], ev[s + 1]
@@ -62,6 +63,10 @@ for n in (420, 680):
         if e[0, 4] and e[0, 3]:
             acc_n += 1
             sums["reduce+B2(wave0)"].append(e[0, 4] - e[0, 3])
+            if e[0, 7]:
+                sums["  full pass(wave0)"].append(e[0, 7] - e[0, 3])
+                sums["  reduce28+B2(wave0)"].append(e[0, 4] - e[0, 7])
+                sums["  full pass(max wave)"].append(max(e[w, 7] - e[w, 3] for w in act if e[w, 7] and e[w, 3]))
             if e[0, 5]:
                 sums["chain solve(wave0)"].append(e[0, 5] - e[0, 4])
             if e[1, 6] and e[1, 3]:
