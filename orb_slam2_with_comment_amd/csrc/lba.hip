@@ -137,12 +137,17 @@ __device__ inline void ba_use(BaDev& a, int L) {
 // ---------------------------------------------------------------- edges
 __device__ inline bool edge_stereo(const orbmi_ba_edge& e) { return !(e.ur < 0); }
 
-// error of edge i with the point's position at Xp (3 doubles)
-__device__ inline void edge_error_at(const BaDev& a, int i, const double* T, const double* Xp, double* err) {
-    const orbmi_ba_edge e = a.edges[i];
-    const orbmi_ba_keyframe& kf = a.kfs[e.kf];
+// The edge math works on values (the edge record, its keyframe's camera, the pose Tk) so that a
+// kernel can load them once, early, and keep them in registers; the a-based helpers below load
+// them from the arrays.
+struct BaCam { float fx, fy, cx, cy, bf; };
+__device__ inline BaCam ba_cam(const orbmi_ba_keyframe& k) { return BaCam{k.fx, k.fy, k.cx, k.cy, k.bf}; }
+
+// error of edge e with the point's position at Xp (3 doubles)
+__device__ inline void edge_err_math(const orbmi_ba_edge& e, const BaCam& kf, const double* Tk, const double* Xp,
+                                     double* err) {
     double p[3];
-    se3_map(T + 8 * e.kf, Xp, p);
+    se3_map(Tk, Xp, p);
     if (!edge_stereo(e)) {
         const double px = p[0] / p[2], py = p[1] / p[2];
         err[0] = (double)e.u - (px * (double)kf.fx + (double)kf.cx);
@@ -159,14 +164,9 @@ __device__ inline void edge_error_at(const BaDev& a, int i, const double* T, con
     }
 }
 
-__device__ inline void edge_error(const BaDev& a, int i, const double* T, const double* X, double* err) {
-    edge_error_at(a, i, T, X + 4 * a.edges[i].point, err);
-}
-
-__device__ inline double edge_chi2(const BaDev& a, int i) {
-    const double* r = a.err + 3 * i;
-    const double info = (double)a.edges[i].inv_sigma2;
-    return r[0] * (info * r[0]) + r[1] * (info * r[1]) + (edge_stereo(a.edges[i]) ? r[2] * (info * r[2]) : 0.0);
+__device__ inline double edge_chi2_math(const orbmi_ba_edge& e, const double* r) {
+    const double info = (double)e.inv_sigma2;
+    return r[0] * (info * r[0]) + r[1] * (info * r[1]) + (edge_stereo(e) ? r[2] * (info * r[2]) : 0.0);
 }
 
 __device__ inline double huber_delta(const orbmi_ba_edge& e) {
@@ -175,20 +175,17 @@ __device__ inline double huber_delta(const orbmi_ba_edge& e) {
     return (double)th;
 }
 
-// robustified chi2 and weight rho' (RobustKernelHuber::robustify)
-__device__ inline void edge_robust(const BaDev& a, int i, double c, double* rho0, double* rho1) {
-    if (a.eflag[i] & 2) { *rho0 = c; *rho1 = 1.0; return; }
-    const double d = huber_delta(a.edges[i]), dsqr = d * d;
+// robustified chi2 and weight rho' (RobustKernelHuber::robustify); fl = the edge's eflag
+__device__ inline void edge_robust_math(unsigned char fl, const orbmi_ba_edge& e, double c, double* rho0, double* rho1) {
+    if (fl & 2) { *rho0 = c; *rho1 = 1.0; return; }
+    const double d = huber_delta(e), dsqr = d * d;
     if (c <= dsqr) { *rho0 = c; *rho1 = 1.0; }
     else { const double s = sqrt(c); *rho0 = 2 * s * d - dsqr; *rho1 = d / s; }
 }
 
 // Jacobians (types_six_dof_expmap.cpp:103-134, :188-234)
-__device__ inline void edge_jacobians(const BaDev& a, int i, const double* T, const double* Xp, double Jl[3][3],
-                                      double Jp[3][6]) {
-    const orbmi_ba_edge e = a.edges[i];
-    const orbmi_ba_keyframe& kf = a.kfs[e.kf];
-    const double* Tk = T + 8 * e.kf;
+__device__ inline void edge_jac_math(const orbmi_ba_edge& e, const BaCam& kf, const double* Tk, const double* Xp,
+                                     double Jl[3][3], double Jp[3][6]) {
     double p[3], R[3][3];
     se3_map(Tk, Xp, p);
     q_to_matrix(load_q(Tk), R);
@@ -223,15 +220,32 @@ __device__ inline void edge_jacobians(const BaDev& a, int i, const double* T, co
     }
 }
 
-// weight W = rho' * info and omega_r = -info * e * rho' (constructQuadraticForm)
-__device__ inline void edge_weights(const BaDev& a, int i, double* w, double om[3]) {
-    const double info = (double)a.edges[i].inv_sigma2;
+// weight W = rho' * info and omega_r = -info * e * rho' (constructQuadraticForm), err = the
+// edge's current error
+__device__ inline void edge_weights_math(unsigned char fl, const orbmi_ba_edge& ed, const double* err, double* w,
+                                         double om[3]) {
+    const double info = (double)ed.inv_sigma2;
     double r0, r1;
-    edge_robust(a, i, edge_chi2(a, i), &r0, &r1);
-    *w = (a.eflag[i] & 2) ? info : r1 * info;
-    const double s = (a.eflag[i] & 2) ? 1.0 : r1;
-    const double* e = a.err + 3 * i;
-    for (int k = 0; k < 3; k++) om[k] = -(info * e[k]) * s;
+    edge_robust_math(fl, ed, edge_chi2_math(ed, err), &r0, &r1);
+    *w = (fl & 2) ? info : r1 * info;
+    const double s = (fl & 2) ? 1.0 : r1;
+    for (int k = 0; k < 3; k++) om[k] = -(info * err[k]) * s;
+}
+
+// the a-based forms (they load the edge, its keyframe and pose from the arrays)
+__device__ inline void edge_error_at(const BaDev& a, int i, const double* T, const double* Xp, double* err) {
+    const orbmi_ba_edge e = a.edges[i];
+    edge_err_math(e, ba_cam(a.kfs[e.kf]), T + 8 * e.kf, Xp, err);
+}
+
+__device__ inline void edge_error(const BaDev& a, int i, const double* T, const double* X, double* err) {
+    edge_error_at(a, i, T, X + 4 * a.edges[i].point, err);
+}
+
+__device__ inline double edge_chi2(const BaDev& a, int i) { return edge_chi2_math(a.edges[i], a.err + 3 * i); }
+
+__device__ inline void edge_robust(const BaDev& a, int i, double c, double* rho0, double* rho1) {
+    edge_robust_math(a.eflag[i], a.edges[i], c, rho0, rho1);
 }
 
 // ---------------------------------------------------------------- block helpers
@@ -507,10 +521,11 @@ __device__ inline void point_dinv(const double* Hll, int p, double lam, double D
 // system (errors already in a.err): Hpl block, the edge's Hll / b_l and Hpp / b_p contributions.
 // Inactive edges into free poses write zeros, so the reductions and the Schur products need no
 // activity tests.  Returns nothing; pi = pose index of the edge's keyframe (-1 fixed).
-__device__ inline void edge_linearize(const BaDev& a, const BaSys& y, int i, int pi, bool active, const double* T,
-                                      const double* Xp, double* He_out = nullptr) {
+__device__ inline void edge_linearize_math(const BaSys& y, int i, int pi, int kpos, bool active, const orbmi_ba_edge& ed,
+                                           const BaCam& kf, const double* Tk, unsigned char fl, const double* err,
+                                           const double* Xp, double* He_out) {
     const bool free_pose = pi >= 0;
-    double* Hp = y.Hpe + 27 * (long long)a.kf_pos[i];
+    double* Hp = y.Hpe + 27 * (long long)kpos;
     double* B = y.Hpl + 18 * (long long)i;
     if (!active) {
         if (free_pose) {
@@ -520,8 +535,8 @@ __device__ inline void edge_linearize(const BaDev& a, const BaSys& y, int i, int
         return;
     }
     double Jl[3][3], Jp[3][6], w, om[3];
-    edge_jacobians(a, i, T, Xp, Jl, Jp);
-    edge_weights(a, i, &w, om);
+    edge_jac_math(ed, kf, Tk, Xp, Jl, Jp);
+    edge_weights_math(fl, ed, err, &w, om);
     double* He = He_out ? He_out : y.Hle + 9 * (long long)i;
     int q = 0;
     for (int r = 0; r < 3; r++)
@@ -538,6 +553,49 @@ __device__ inline void edge_linearize(const BaDev& a, const BaSys& y, int i, int
                 Hp[q] = Jp[0][r] * w * Jp[0][c] + Jp[1][r] * w * Jp[1][c] + Jp[2][r] * w * Jp[2][c];
         for (int r = 0; r < 6; r++) Hp[21 + r] = Jp[0][r] * om[0] + Jp[1][r] * om[1] + Jp[2][r] * om[2];
     }
+}
+
+__device__ inline void edge_linearize(const BaDev& a, const BaSys& y, int i, int pi, bool active, const double* T,
+                                      const double* Xp, double* He_out = nullptr) {
+    const orbmi_ba_edge ed = a.edges[i];
+    edge_linearize_math(y, i, pi, a.kf_pos[i], active, ed, ba_cam(a.kfs[ed.kf]), T + 8 * ed.kf, a.eflag[i], a.err + 3 * i,
+                        Xp, He_out);
+}
+
+// An edge of k_ba_update_errors with everything its trial pass reads except the point position,
+// loaded in one round (the keyframe's camera and trial pose right behind the record)
+struct EdgeIn {
+    orbmi_ba_edge e;
+    BaCam cam;
+    double T[8];
+    int pi, kpos;
+    unsigned char fl;
+};
+__device__ inline void edge_in(const BaDev& a, int i, const double* T, EdgeIn& s) {
+    s.e = a.edges[i];
+    s.fl = a.eflag[i];
+    s.pi = a.e_pi[i];
+    s.kpos = a.kf_pos[i];
+    s.cam = ba_cam(a.kfs[s.e.kf]);
+#pragma unroll
+    for (int q = 0; q < 8; q++) s.T[q] = T[8 * s.e.kf + q];
+}
+
+// computeActiveErrors + robust chi2 + the linearisation of one edge at the trial state from
+// registers (the error goes to a.err and stays in registers for the weights)
+__device__ inline double edge_trial(const BaDev& a, const BaSys& t, int i, const EdgeIn& s, const double* Xp,
+                                    double* He_out) {
+    const bool active = s.fl & 4;
+    double err[3] = {0, 0, 0}, r0 = 0;
+    if (active) {
+        edge_err_math(s.e, s.cam, s.T, Xp, err);
+        double* eo = a.err + 3 * i;
+        eo[0] = err[0]; eo[1] = err[1]; eo[2] = err[2];
+        double r1;
+        edge_robust_math(s.fl, s.e, edge_chi2_math(s.e, err), &r0, &r1);
+    }
+    edge_linearize_math(t, i, s.pi, s.kpos, active, s.e, s.cam, s.T, s.fl, err, Xp, He_out);
+    return r0;
 }
 
 // thread per edge, the first linearisation of an optimize(): computeActiveErrors + robust chi2
@@ -1336,6 +1394,12 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     const int p = p0 + ps;
     const bool own = p < p1;
     const int pe0 = own ? a.pt_start[p] : 0, pe1 = own ? a.pt_start[p + 1] : 0;
+    // the block's edges (thread per edge in the trial pass): the first one's record, camera and
+    // trial pose are loaded now, under the back substitution's loads
+    const int be0 = p0 < p1 ? a.pt_start[p0] : 0, be1 = p0 < p1 ? a.pt_start[p1] : 0;
+    const int e_pre = be0 + tid;
+    EdgeIn pre;
+    if (e_pre < be1) edge_in(a, e_pre, Tt, pre);
     double sc = 0, chi = 0;
     {  // back substitution x_l = D^-1 (b_l - sum_e Hpl_e^T x_p), 8 lanes per point
         double c0 = 0, c1 = 0, c2 = 0, act = 0;
@@ -1372,19 +1436,12 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     __syncthreads();
     // trial errors (computeActiveErrors) and the trial state's linearisation, thread per edge;
     // the edges' Hll / b_l terms go to LDS when the block's edges fit
-    const int be0 = p0 < p1 ? a.pt_start[p0] : 0, be1 = p0 < p1 ? a.pt_start[p1] : 0;
     const bool lds = be1 - be0 <= kBaUpdLdsEdges;
-    for (int e = be0 + tid; e < be1; e += blockDim.x) {
-        const bool active = a.eflag[e] & 4;
-        const orbmi_ba_edge ed = a.edges[e];
-        const double* Xp = &xs[ed.point - p0][0];
-        if (active) {
-            edge_error_at(a, e, Tt, Xp, a.err + 3 * e);
-            double r0, r1;
-            edge_robust(a, e, edge_chi2(a, e), &r0, &r1);
-            chi += r0;
-        }
-        edge_linearize(a, t, e, a.e_pi[e], active, Tt, Xp, lds ? sHe + 9 * (e - be0) : nullptr);
+    for (int e = e_pre; e < be1; e += blockDim.x) {
+        EdgeIn s;
+        if (e == e_pre) s = pre;
+        else edge_in(a, e, Tt, s);
+        chi += edge_trial(a, t, e, s, &xs[s.e.point - p0][0], lds ? sHe + 9 * (e - be0) : nullptr);
     }
     __syncthreads();
     {  // Hll / b_l at the trial state, 8 lanes per point, edges in order within a lane
