@@ -70,9 +70,14 @@ struct BaCtl {
     double lambda, ni, currentChi, iniChi;
     double chi_out[2];  // activeRobustChi2 after optimize(5) / optimize(10)
     int it_out[2];      // iterations of optimize(5) / optimize(10); -1 with an empty mapping
+    // The whole call is enqueued at once (Runner); these gate each kernel to its optimize():
+    int gen;          // the optimize() the LM state belongs to (1: optimize(5), 2: optimize(10))
+    int phases_done;  // optimize() calls finished (k_ba_chi)
+    int do_more;      // optimize(10) runs: pbStopFlag was clear after optimize(5) (:689-692)
 };
 
 struct BaDev {
+    int run_gen;                    // the optimize() (BaCtl::gen) a launch belongs to
     int nkf, npt, nedge, nblk, nf;  // nf = non-fixed keyframes (nblk = nf (nf + 1) / 2)
     int nb_e, nb_p, nb_q;           // blocks: edges (256), points (256), points (kBaUpdPts per block)
     BaCtl* ctl;
@@ -309,6 +314,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restri
 // outlier levels, kernels off before the second optimisation (src/Optimizer.cc:701-732);
 // chi2 from the stale errors, depth from the current estimate
 __global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a) {
+    if (!(a.ctl->phases_done >= 1 && a.ctl->do_more)) return;  // optimize(5) pending or no optimize(10)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const double* T = a.Tb[a.ctl->cur];
     const double* X = a.Xb[a.ctl->cur];
@@ -330,6 +336,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a) {
 // which the next linearisation overwrites).  Bit 0 is never rewritten, so reading it from the
 // point's other edges while they are updated is safe.
 __global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int gen) {
+    if (gen > 1 && !(a.ctl->phases_done >= gen - 1 && a.ctl->do_more)) return;
     __shared__ double red[kBaBlock / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     int first = 0;
@@ -353,6 +360,8 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int gen
 // ballot scan over the id-ordered keyframes, and the LM state of levenberg.cpp:61-70.  The
 // edges' pose indices (e_pi) are written by the next k_ba_linearize.
 __global__ __launch_bounds__(64) void k_ba_activate_ctl(BaDev a, int max_it, int gen) {
+    if (gen > 1 && !(a.ctl->phases_done >= gen - 1 && a.ctl->do_more)) return;
+    if (a.stop && *a.stop) max_it = 0;  // pbStopFlag raised meanwhile: optimize() returns at once
     const int lane = threadIdx.x;
     double c = 0;
     for (int b = lane; b < a.nb_e; b += 64) c += a.part_lin[b];
@@ -390,6 +399,7 @@ __global__ __launch_bounds__(64) void k_ba_activate_ctl(BaDev a, int max_it, int
         c2.lambda = 0;
         c2.ni = 2;
         c2.done = (n + nl == 0) || c2.unsupported || max_it <= 0;
+        c2.gen = gen;
     }
 }
 
@@ -480,6 +490,7 @@ __global__ __launch_bounds__(kPairThreads) void k_ba_pairs_fill(BaDev a) {
 // computeActiveErrors (recompute = 1) + activeRobustChi2; per-block partial sums
 // activeRobustChi2 on the stored (possibly stale) errors; per-block partial sums
 __global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a) {
+    if (!(a.ctl->done && a.ctl->gen == a.run_gen)) return;  // its optimize() still running
     __shared__ double red[kBaBlock / 64];
     double* part = a.part_lin;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -602,7 +613,7 @@ __device__ inline double edge_trial(const BaDev& a, const BaSys& t, int i, const
 // (block partials), then the edge's blocks (edge_linearize) into the current linear system
 __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done || !ctl.need_lin) return;
+    if (ctl.done || !ctl.need_lin || ctl.gen != a.run_gen) return;
     const BaSys y = ba_sys(a, ctl.lin);
     const double* T = a.Tb[ctl.cur];
     const double* X = a.Xb[ctl.cur];
@@ -633,7 +644,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_linearize(BaDev a) {
 constexpr int kBaPoseLanes = kBaBlock / 27;  // 9
 __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done || !ctl.need_lin) return;
+    if (ctl.done || !ctl.need_lin || ctl.gen != a.run_gen) return;
     ba_use(a, ctl.lin);
     const int nb_p = a.nb_p;
     double* part_max = a.part_max;
@@ -748,7 +759,7 @@ __device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
 
 __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done) return;
+    if (ctl.done || ctl.gen != a.run_gen) return;
     ba_use(a, ctl.lin);
     __shared__ double rows[kSchurThreads];
     __shared__ double ptot[21];  // Hpp (upper) or b_p of the block's keyframe
@@ -935,7 +946,7 @@ __device__ inline bool ldl6(double F[36], double inv6[6]) {
 template <int TPT>  // threads per tile: 2 (np <= 21) or 1 (np <= kBaMaxPoses)
 __global__ __launch_bounds__(kBaSolveThreads) void k_ba_solve(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done) return;
+    if (ctl.done || ctl.gen != a.run_gen) return;
     const int np = ctl.np;
     double lam = a.scal[3];
     const double* __restrict__ T = a.Tb[ctl.cur];
@@ -1128,7 +1139,7 @@ static_assert(3 * kBaSolveRowsMaxPoses + 2 <= 64, "a row pair must fit one wave"
 __device__ inline int solve_rows_wave(int row, int np) { return row <= np - row ? row : np - row; }
 __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) {
     const BaCtl& ctl = *a.ctl;
-    if (ctl.done) return;
+    if (ctl.done || ctl.gen != a.run_gen) return;
     const int np = ctl.np;
     double lam = a.scal[3];
     const double* __restrict__ T = a.Tb[ctl.cur];
@@ -1374,7 +1385,7 @@ __device__ inline double sum8(double v) {
 
 __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     BaCtl& ctl = *a.ctl;
-    if (ctl.done) return;
+    if (ctl.done || ctl.gen != a.run_gen) return;
     const int L = ctl.lin;
     const BaSys y = ba_sys(a, L);      // current linear system
     const BaSys t = ba_sys(a, L ^ 1);  // trial state's linear system (adopted if accepted)
@@ -1479,11 +1490,14 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
 
 // activeRobustChi2 after optimize() (k_ba_errors partials) and the iteration count
 __global__ __launch_bounds__(64) void k_ba_chi(BaDev a, int phase) {
+    if (!(a.ctl->done && a.ctl->gen == a.run_gen)) return;
     const double chi = wave_sum_fixed(a.part_lin, a.nb_e);
     if (threadIdx.x == 0) {
         BaCtl& c = *a.ctl;
         c.chi_out[phase] = chi;
         c.it_out[phase] = (c.np + c.nl == 0) ? -1 : c.it;
+        c.phases_done = phase + 1;
+        if (phase == 0) c.do_more = !(a.stop && *a.stop);
     }
 }
 
@@ -1558,9 +1572,13 @@ struct BaTrace {
 };
 
 // Trial steps enqueued beyond the iterations still to run: a rejected trial consumes one step
-// without finishing an iteration, so the first readback usually already sees optimize() done.
+// without finishing an iteration, so the steps enqueued up front usually finish optimize().
 constexpr int kBaStepSlack = 1;
 
+// The whole g2o schedule -- optimize(5), levels, optimize(10), write-back -- is enqueued at once
+// and read back once: every kernel checks on the device that its optimize() is the current one
+// (BaCtl::gen, phases_done), so launches past an optimize() that ran out of enqueued trials do
+// nothing, and the host resumes from there (more trials, then the rest of the schedule).
 struct Runner {
     orbmi_ba& h;
     BaDev a;
@@ -1589,38 +1607,33 @@ struct Runner {
         return wait();
     }
 
-    // one LM trial: Schur + solve + update (trial errors, the trial state's linearisation and,
-    // in its last block, the Levenberg decision); every kernel returns at once when optimize()
-    // is done
-    void step() {
+    // one LM trial of optimize() gen: Schur + solve + update (trial errors, the trial state's
+    // linearisation and, in its last block, the Levenberg decision); every kernel returns at once
+    // when that optimize() is done or not the current one
+    void step(int gen) {
+        a.run_gen = gen;
         if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
         if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaUpdThreads), 0, h.stream, a);
     }
 
-    // SparseOptimizer::optimize(iterations) as phase 0 / 1, then activeRobustChi2
-    int optimize(int iterations, int phase) {
-        hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, phase + 1);
-        hipLaunchKernelGGL(k_ba_activate_ctl, dim3(1), dim3(64), 0, h.stream, a, stopped() ? 0 : iterations, phase + 1);
+    // SparseOptimizer::initializeOptimization + the first linearisation of optimize() gen
+    void prologue(int iterations, int gen) {
+        a.run_gen = gen;
+        if (gen == 2) hipLaunchKernelGGL(k_ba_levels, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);  // :694-737
+        hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, gen);
+        hipLaunchKernelGGL(k_ba_activate_ctl, dim3(1), dim3(64), 0, h.stream, a, iterations, gen);
         // iteration 0's computeActiveErrors + buildSystem (later ones come with the trials)
         hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
-        int todo = stopped() ? 0 : iterations + kBaStepSlack;
-        while (todo > 0) {
-            for (int k = 0; k < todo; k++) step();
-            ORBMI_HIP(hipGetLastError());
-            int rc;
-            if ((rc = read_ctl())) return rc;
-            const BaCtl& c = *h.h_ctl;
-            if (c.unsupported) return ORBMI_E_UNSUPPORTED;
-            if (c.done || stopped()) break;
-            todo = c.max_it - c.it;  // rejected trials used up the slack
-        }
+    }
+
+    // activeRobustChi2 after optimize() gen
+    void epilogue(int gen) {
+        a.run_gen = gen;
         hipLaunchKernelGGL(k_ba_errors, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_chi, dim3(1), dim3(64), 0, h.stream, a, phase);
-        ORBMI_HIP(hipGetLastError());
-        return ORBMI_OK;
+        hipLaunchKernelGGL(k_ba_chi, dim3(1), dim3(64), 0, h.stream, a, gen - 1);
     }
 };
 
@@ -1834,26 +1847,44 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         hipLaunchKernelGGL(k_ba_pairs_fill, dim3(nblk), dim3(kPairThreads), 0, s, a);
     }
     ORBMI_HIP(hipGetLastError());
-    int rc;
     tr.mark("enqueue_setup");
-    if ((rc = r.optimize(5, 0))) return rc;
-    tr.mark("optimize5");
-    const bool second = !r.stopped();
-    if (second) {  // src/Optimizer.cc:694-737
-        hipLaunchKernelGGL(k_ba_levels, dim3(nb_e), dim3(kBaBlock), 0, s, a);
-        if ((rc = r.optimize(10, 1))) return rc;
-        tr.mark("optimize10");
+    // optimize(5), levels, optimize(10), write-back, enqueued at once (stages from `from` on:
+    // 0 = optimize(5)'s prologue, 1 = more trials of optimize(5), 2 = more trials of optimize(10))
+    const char* slack_env = getenv("ORBMI_BA_SLACK");  // test hook: 0 forces the resume path
+    const int slack = slack_env ? std::max(0, atoi(slack_env)) : kBaStepSlack;
+    auto enqueue = [&](int from, int more) {
+        if (from == 0) r.prologue(r.stopped() ? 0 : 5, 1);
+        if (from <= 1) {
+            for (int k = 0; k < (from == 0 ? 5 + slack : more); k++) r.step(1);
+            r.epilogue(1);
+            r.prologue(10, 2);
+        }
+        for (int k = 0; k < (from <= 1 ? 10 + slack : more); k++) r.step(2);
+        r.epilogue(2);
+        hipLaunchKernelGGL(k_ba_finish, dim3(nb_all), dim3(kBaBlock), 0, s, a, (float*)(B + o_otcw), (float*)(B + o_opos),
+                           out_erase);
+        hipError_t e = hipSuccess;
+        if (nkf && e == hipSuccess) e = hipMemcpyAsync(R->tcw, B + o_otcw, 64 * nkf, hipMemcpyDeviceToHost, s);
+        if (npt && e == hipSuccess) e = hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s);
+        if (ne && e == hipSuccess) e = hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s);
+        return e;
+    };
+    int rc, from = 0, more = 0;
+    for (;;) {
+        ORBMI_HIP(enqueue(from, more));
+        ORBMI_HIP(hipGetLastError());
+        if ((rc = r.read_ctl())) return rc;
+        const BaCtl& c = *h.h_ctl;
+        if (c.unsupported) return ORBMI_E_UNSUPPORTED;
+        if (c.phases_done >= 2 || (c.phases_done == 1 && !c.do_more)) break;
+        // an optimize() ran out of enqueued trials (rejections beyond the slack): resume it
+        from = c.phases_done == 0 ? 1 : 2;
+        more = std::max(1, c.max_it - c.it);
+        tr.mark(from == 1 ? "resume5" : "resume10");
     }
-    hipLaunchKernelGGL(k_ba_finish, dim3(nb_all), dim3(kBaBlock), 0, s, a, (float*)(B + o_otcw), (float*)(B + o_opos),
-                       out_erase);
-    ORBMI_HIP(hipGetLastError());
-    if (nkf) ORBMI_HIP(hipMemcpyAsync(R->tcw, B + o_otcw, 64 * nkf, hipMemcpyDeviceToHost, s));
-    if (npt) ORBMI_HIP(hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s));
-    if (ne) ORBMI_HIP(hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s));
-    if ((rc = r.read_ctl())) return rc;
-    tr.mark("finish");
+    tr.mark("optimize+finish");
     const BaCtl& c = *h.h_ctl;
-    if (c.unsupported) return ORBMI_E_UNSUPPORTED;
+    const bool second = c.do_more != 0;
     R->iterations[0] = c.it_out[0];
     R->iterations[1] = second ? c.it_out[1] : 0;
     R->chi2[0] = c.chi_out[0];

@@ -46,6 +46,21 @@ def test_lba_parity(oracle, BA, seed, free, fixed, npts):
     _compare(BA.run(prob), ref, prob)
 
 
+def test_lba_resume_after_rejections(oracle, BA, monkeypatch):
+    """The call is enqueued at once with a few spare trials per optimize(); with none
+    (ORBMI_BA_SLACK=0) every rejected trial leaves an optimize() short of trials, the gated
+    launches after it do nothing and the host resumes it: results bitwise equal to the default
+    schedule's, and parity with the oracle."""
+    prob, _ = SM.local_ba_problem(seed=42, n_free=20, n_fixed=4, n_points=3000)
+    base = BA.run(prob)
+    monkeypatch.setenv("ORBMI_BA_SLACK", "0")
+    r = BA.run(prob)
+    for k in ("tcw", "pos", "erase"):
+        np.testing.assert_array_equal(r[k], base[k])
+    assert r["iterations"] == base["iterations"] and list(r["chi2"]) == list(base["chi2"])
+    _compare(r, oracle.local_ba(prob, edge_chi2=True), prob)
+
+
 def test_lba_mono_only(oracle, BA):
     prob, _ = SM.local_ba_problem(seed=11, n_free=8, n_fixed=2, n_points=600, stereo_frac=0.0)
     _compare(BA.run(prob), oracle.local_ba(prob, edge_chi2=True), prob)
