@@ -14,6 +14,8 @@
 // from the LM's last computeActiveErrors (a rejected trial leaves its errors behind).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -147,6 +149,12 @@ struct PoseOpt {
         for (int j = 0; j < 6; j++) s += x[j] * (lambda * x[j] + b[j]);
         return s;
     }
+    // ORC_POSE_TRACE=1: the accept (A) / reject (R) sequence of the trials on stderr, '|' per
+    // iteration (a measurement aid for the device kernel's trial schedule)
+    static bool trace_trials() {
+        static const bool on = std::getenv("ORC_POSE_TRACE") != nullptr;
+        return on;
+    }
     enum Result { OK, Terminate };
     Result lm_solve(int iteration) {  // OptimizationAlgorithmLevenberg::solve
         compute_active_errors();
@@ -183,7 +191,9 @@ struct PoseOpt {
                 T = T0;
             }
             qmax++;
+            if (trace_trials()) std::fputc(rho > 0 && std::isfinite(tempChi) ? 'A' : 'R', stderr);
         } while (rho < 0 && qmax < 10);
+        if (trace_trials()) std::fputc('|', stderr);
         if (qmax == 10 || rho == 0) return Terminate;
         if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
         else nBad = 0;
