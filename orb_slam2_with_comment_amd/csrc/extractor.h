@@ -85,6 +85,7 @@ struct Extractor {
     uint8_t* d_blur = nullptr;     // blurred levels: interior only, rows of bstride bytes
     int2* d_btiles = nullptr;      // blur tiles: {level, x0 | y0 << 16}
     int nbtiles = 0;
+    int fast_maxw = 0, fast_maxh = 0, fast_wave_bytes = 0;  // largest cell ROI, k_fast's LDS per wave
     int* d_level_count = nullptr;   // [b][level][region] FAST candidates (k_fast allocates, k_pyr_level0 clears)
     int* d_regbase = nullptr;       // [level][region] first slot of each candidate region (per image)
     std::vector<uint32_t> pyr_blob; // k_pyramid parameter blocks, pyr_blob_words per tile

@@ -149,42 +149,110 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(const uint8_t* __restri
     }
 }
 
-// Large batches: one launch per level, a thread per padded output byte (the tiles' halo
-// recomputation costs more than the launches once the batch fills the chip).
+// Large batches: one launch per level (the tiles' halo recomputation costs more than the
+// launches once the batch fills the chip).  A 256-thread workgroup makes kPyrBRows padded rows of
+// one level: the source rows they read are staged in LDS with aligned 16-B (level 0: 4-B) loads,
+// then every thread forms 8 consecutive output bytes from LDS byte reads and stores them as one
+// 8-B word (byte stores only at the row's end).  Global byte loads would bind on the texture
+// addresser (one 64-lane address batch per byte).
+constexpr int kPyrBRows = 4;
+constexpr int kPyrBThreads = 256;
+
 // Level 0: copyMakeBorder(image, 19, BORDER_REFLECT_101) (src/ORBextractor.cc:1128-1129); it
-// also clears the per-level candidate counters.
-__global__ void k_pyr_level0(const uint8_t* __restrict__ img, size_t step, size_t img_stride,
-                             uint8_t* __restrict__ pyr, long long pimg, LevelGeom g, int* __restrict__ level_count,
-                             int nlevels) {
-    const int xp = blockIdx.x * blockDim.x + threadIdx.x, yp = blockIdx.y, b = blockIdx.z;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nlevels * kFastRegions)
-        level_count[b * nlevels * kFastRegions + threadIdx.x] = 0;
-    if (xp >= g.W + 2 * kEdge) return;
-    const int ix = reflect101(xp - kEdge, g.W), iy = reflect101(yp - kEdge, g.H);
-    pyr[b * pimg + g.off + (long long)yp * g.stride + xp] = img[b * img_stride + (size_t)iy * step + ix];
+// also clears the per-level candidate counters.  LDS: kPyrBRows image rows of `lrow` bytes.
+__global__ __launch_bounds__(kPyrBThreads) void k_pyr_level0(const uint8_t* __restrict__ img, size_t step,
+                                                             size_t img_stride, uint8_t* __restrict__ pyr, long long pimg,
+                                                             LevelGeom g, int* __restrict__ level_count, int nlevels,
+                                                             int lrow) {
+    extern __shared__ uint32_t srow4[];
+    const int b = blockIdx.z, yp0 = blockIdx.x * kPyrBRows, tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < nlevels * kFastRegions) level_count[b * nlevels * kFastRegions + tid] = 0;
+    const int PW = g.W + 2 * kEdge, nrow = min(kPyrBRows, g.ph - yp0);
+    const int nd = (g.W + 3 + 3) / 4;  // dwords covering a row from its aligned start
+    int o[kPyrBRows];
+#pragma unroll
+    for (int r = 0; r < kPyrBRows; r++) {
+        const uint8_t* row = img + b * img_stride + (size_t)reflect101(min(yp0 + r, g.ph - 1) - kEdge, g.H) * step;
+        o[r] = (int)((uintptr_t)row & 3);
+    }
+    for (int i = tid; i < nrow * nd; i += kPyrBThreads) {
+        const int r = i / nd, d = i - r * nd;
+        const uint8_t* row = img + b * img_stride + (size_t)reflect101(yp0 + r - kEdge, g.H) * step;
+        srow4[r * (lrow / 4) + d] = reinterpret_cast<const uint32_t*>(row - ((uintptr_t)row & 3))[d];
+    }
+    __syncthreads();
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(srow4);
+    const int nch = (PW + 7) / 8;
+    for (int t = tid; t < nrow * nch; t += kPyrBThreads) {
+        const int r = t / nch, xp = 8 * (t - r * nch);
+        const uint8_t* src = sb + r * lrow + o[r];
+        uint8_t* dst = pyr + b * pimg + g.off + (long long)(yp0 + r) * g.stride + xp;
+        uint32_t w[2] = {0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 8; i++) w[i >> 2] |= (uint32_t)src[reflect101(min(xp + i, PW - 1) - kEdge, g.W)] << (8 * (i & 3));
+        if (xp + 8 <= PW) *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+        else
+            for (int i = 0; i < PW - xp; i++) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
 }
 
 // Level l: resize(level l-1, INTER_LINEAR) then copyMakeBorder(REFLECT_101|ISOLATED)
 // (src/ORBextractor.cc:1118-1124).  Border pixels recompute the interior pixel they mirror.
-__global__ void k_pyr_resize(uint8_t* __restrict__ pyr, long long pimg, LevelGeom s, LevelGeom d,
-                             const XTab* __restrict__ xt, const YTab* __restrict__ yt) {
-    const int xp = blockIdx.x * blockDim.x + threadIdx.x, yp = blockIdx.y, b = blockIdx.z;
-    if (xp >= d.W + 2 * kEdge) return;
-    const int ix = reflect101(xp - kEdge, d.W), iy = reflect101(yp - kEdge, d.H);
-    const uint8_t* src = pyr + b * pimg + s.off + (long long)kEdge * s.stride + kEdge;
-    const XTab x = xt[ix];
-    const YTab y = yt[iy];
-    const uint8_t* r0 = src + (long long)y.y0 * s.stride;
-    const uint8_t* r1 = src + (long long)y.y1 * s.stride;
-    pyr[b * pimg + d.off + (long long)yp * d.stride + xp] =
-        (uint8_t)pyr_resize_px(r0[x.sx0], r0[x.sx1], r1[x.sx0], r1[x.sx1], x, y, ix < d.resize_xv);
+// LDS: the two source rows of each output row (whole padded rows of level l-1, `lrow` bytes).
+__global__ __launch_bounds__(kPyrBThreads) void k_pyr_resize(uint8_t* __restrict__ pyr, long long pimg, LevelGeom s,
+                                                             LevelGeom d, const XTab* __restrict__ xt,
+                                                             const YTab* __restrict__ yt, int lrow) {
+    extern __shared__ uint4 srow16[];
+    const int b = blockIdx.z, yp0 = blockIdx.x * kPyrBRows, tid = threadIdx.x;
+    const int PW = d.W + 2 * kEdge, nrow = min(kPyrBRows, d.ph - yp0);
+    const uint8_t* S = pyr + b * pimg + s.off;
+    const int n16 = s.stride / 16;
+    for (int i = tid; i < 2 * nrow * n16; i += kPyrBThreads) {
+        const int rr = i / n16, c = i - rr * n16;  // rr = 2 * output row + tap
+        const YTab y = yt[reflect101(yp0 + (rr >> 1) - kEdge, d.H)];
+        const int sy = (rr & 1) ? y.y1 : y.y0;
+        srow16[rr * (lrow / 16) + c] = reinterpret_cast<const uint4*>(S + (long long)(kEdge + sy) * s.stride)[c];
+    }
+    __syncthreads();
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(srow16) + kEdge;
+    const int nch = (PW + 7) / 8;
+    for (int t = tid; t < nrow * nch; t += kPyrBThreads) {
+        const int r = t / nch, xp = 8 * (t - r * nch);
+        const YTab y = yt[reflect101(yp0 + r - kEdge, d.H)];
+        const uint8_t* r0 = sb + (2 * r) * lrow;
+        const uint8_t* r1 = r0 + lrow;
+        uint8_t* dst = pyr + b * pimg + d.off + (long long)(yp0 + r) * d.stride + xp;
+        uint32_t w[2] = {0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int ix = reflect101(min(xp + i, PW - 1) - kEdge, d.W);
+            const XTab x = xt[ix];
+            w[i >> 2] |= (uint32_t)pyr_resize_px(r0[x.sx0], r0[x.sx1], r1[x.sx0], r1[x.sx1], x, y, ix < d.resize_xv)
+                         << (8 * (i & 3));
+        }
+        if (xp + 8 <= PW) *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+        else
+            for (int i = 0; i < PW - xp; i++) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
 }
 
 // ------------------------------------------------------------------------------ FAST
-constexpr int kTile = 64;               // max cell ROI edge (wCell+6, hCell+6)
-constexpr int kTileS = 68;              // LDS row pitch of a staged ROI row (17 dwords)
+constexpr int kTile = 64;               // max cell ROI edge (wCell+6, hCell+6): list entries are y << 6 | x
 constexpr int kFastCells = 2;           // waves (cells) per workgroup
-constexpr int kFastList = 58 * 58;      // scored pixels of the largest ROI
+// A wave's LDS (dynamic, sized by the host for the level geometry's largest cell ROI maxW x maxH:
+// ~37 x 37 for the 30-px cells of every level, so a CU holds ~3x the waves of a 64 x 64 sizing):
+//   tile    maxH rows of tsd dwords (the ROI row from its aligned start: tsd = (maxW + 6) / 4)
+//   scores  maxH rows of sp bytes (sp = maxW rounded up to 16)
+//   list    (maxW - 6)(maxH - 6) u16 entries
+struct FastLds { int tsd, sp, list, wave_bytes; };
+__host__ __device__ inline FastLds fast_lds_layout(int maxW, int maxH) {
+    FastLds f;
+    f.tsd = (maxW + 6) / 4;
+    f.sp = (maxW + 15) & ~15;
+    f.list = (maxW - 6) * (maxH - 6);
+    f.wave_bytes = ((4 * f.tsd * maxH + 15) & ~15) + ((maxH * f.sp + 15) & ~15) + ((2 * f.list + 15) & ~15);
+    return f;
+}
 
 // LDS writes of this wave visible to its own later reads (wave-private LDS regions)
 __device__ inline void wave_sync_lds_ex() {
@@ -285,11 +353,10 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
                                                           const CellGeom* __restrict__ cells, int ncells,
                                                           uint2* __restrict__ cand, int keys_cap,
                                                           int* __restrict__ level_count, int nlevels, int ini_th,
-                                                          int min_th) {
-    __shared__ unsigned tiles[kFastCells][kTile * kTileS / 4];
-    __shared__ uint4 scores4[kFastCells][kTile * kTile / 16];
-    __shared__ unsigned short lists[kFastCells][kFastList];
+                                                          int min_th, int maxW, int maxH) {
+    extern __shared__ uint4 fast_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const FastLds F = fast_lds_layout(maxW, maxH);
     const int c = blockIdx.x * kFastCells + wid, b = blockIdx.y;
     if (c >= ncells) return;
     const CellGeom cg = cells[c];
@@ -299,26 +366,31 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     const int o = (int)(a & 3);  // stride is a multiple of 64: the same offset on every row
     const unsigned* src = reinterpret_cast<const unsigned*>(pyr + (a - o));
     const int w = cg.w, h = cg.h, nd = (w + o + 3) >> 2, s4 = lg.stride >> 2;
-    unsigned* t4 = tiles[wid];
+    uint8_t* wl = reinterpret_cast<uint8_t*>(fast_lds) + wid * F.wave_bytes;
+    unsigned* t4 = reinterpret_cast<unsigned*>(wl);
+    uint4* scores4 = reinterpret_cast<uint4*>(wl + ((4 * F.tsd * maxH + 15) & ~15));
+    unsigned short* L = reinterpret_cast<unsigned short*>(reinterpret_cast<uint8_t*>(scores4) + ((maxH * F.sp + 15) & ~15));
+    const int TS = 4 * F.tsd, SP = F.sp;
     {
-        unsigned v[(kTile * 17 + 63) / 64];
+        constexpr int kLd = 8;  // loads in flight per lane (a 37 x 37 ROI: 370 dwords, one round)
+        for (int i0 = 0; i0 < nd * h; i0 += 64 * kLd) {
+            unsigned v[kLd];
 #pragma unroll
-        for (int k = 0; k < (kTile * 17 + 63) / 64; k++) {
-            const int i = lane + 64 * k, r = i / nd, d = i - r * nd;
-            v[k] = r < h ? src[(long long)r * s4 + d] : 0u;
-        }
+            for (int k = 0; k < kLd; k++) {
+                const int i = i0 + lane + 64 * k, r = i / nd, d = i - r * nd;
+                v[k] = r < h ? src[(long long)r * s4 + d] : 0u;
+            }
 #pragma unroll
-        for (int k = 0; k < (kTile * 17 + 63) / 64; k++) {
-            const int i = lane + 64 * k, r = i / nd, d = i - r * nd;
-            if (r < h) t4[r * (kTileS / 4) + d] = v[k];
+            for (int k = 0; k < kLd; k++) {
+                const int i = i0 + lane + 64 * k, r = i / nd, d = i - r * nd;
+                if (r < h) t4[r * F.tsd + d] = v[k];
+            }
         }
     }
-#pragma unroll
-    for (int k = 0; k < kTile * kTile / 16 / 64; k++) scores4[wid][lane + 64 * k] = make_uint4(0u, 0u, 0u, 0u);
-    uint8_t* sc = reinterpret_cast<uint8_t*>(scores4[wid]);  // sc[y * kTile + x]
-    unsigned short* L = lists[wid];
+    for (int k = lane; k < (maxH * SP) / 16; k += 64) scores4[k] = make_uint4(0u, 0u, 0u, 0u);
+    uint8_t* sc = reinterpret_cast<uint8_t*>(scores4);  // sc[y * SP + x]
     wave_sync_lds_ex();
-    const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * kTileS + x]
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * TS + x]
     const int dw = w - 6, dh = h - 6, npix = dw > 0 && dh > 0 ? dw * dh : 0;
     const int ti = min(max(ini_th, 0), 255), tm = min(max(min_th, 0), 255), tl = min(ti, tm);
     // A: compass pre-test over the ROI's scored pixels, row-major
@@ -330,9 +402,9 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
             bool pass = false;
             const int X = x + 3, Y = y + 3;
             if (p0 + lane < npix) {
-                const uint8_t* cp = tb + Y * kTileS + X;
+                const uint8_t* cp = tb + Y * TS + X;
                 const int v = cp[0], hi = v + tl, lo = v - tl;
-                const int pa = cp[3 * kTileS], pb = cp[3], pc = cp[-3 * kTileS], pd = cp[-3];
+                const int pa = cp[3 * TS], pb = cp[3], pc = cp[-3 * TS], pd = cp[-3];
                 const bool ba = pa > hi, bb = pb > hi, bc = pc > hi, bd = pd > hi;
                 const bool da = pa < lo, db = pb < lo, dc = pc < lo, dd = pd < lo;
                 pass = (ba & bb) | (bb & bc) | (bc & bd) | (bd & ba) | (da & db) | (db & dc) | (dc & dd) | (dd & da);
@@ -356,8 +428,8 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
             e = L[i];
             const int X = e & 63, Y = e >> 6;
             int p[16];
-            fast_circle(tb, kTileS, X, Y, p);
-            pass = fast_segment(tb[Y * kTileS + X], p, tl);
+            fast_circle(tb, TS, X, Y, p);
+            pass = fast_segment(tb[Y * TS + X], p, tl);
         }
         const unsigned long long m = __ballot(pass);
         if (pass) L[nc + lanes_below(m)] = e;
@@ -369,8 +441,8 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
         const unsigned short e = L[i];
         const int X = e & 63, Y = e >> 6;
         int p[16];
-        fast_circle(tb, kTileS, X, Y, p);
-        sc[Y * kTile + X] = (uint8_t)fast_corner_score(tb[Y * kTileS + X], p, tl);
+        fast_circle(tb, TS, X, Y, p);
+        sc[Y * SP + X] = (uint8_t)fast_corner_score(tb[Y * TS + X], p, tl);
     }
     wave_sync_lds_ex();
     // D: strict NMS at ini_th, then at min_th if nothing survived; survivors compacted in place
@@ -384,15 +456,15 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
             unsigned short e = 0;
             if (i < nc) {
                 e = L[i];
-                const uint8_t* q = sc + (e >> 6) * kTile + (e & 63);
+                const uint8_t* q = sc + (e >> 6) * SP + (e & 63);
                 const int s = q[0];
                 if (s >= t && s != 0) {
                     auto nb = [&](int off) {
                         const int u = q[off];
                         return u >= t ? u : 0;
                     };
-                    keep = s > nb(-kTile - 1) && s > nb(-kTile) && s > nb(-kTile + 1) && s > nb(-1) && s > nb(1) &&
-                           s > nb(kTile - 1) && s > nb(kTile) && s > nb(kTile + 1);
+                    keep = s > nb(-SP - 1) && s > nb(-SP) && s > nb(-SP + 1) && s > nb(-1) && s > nb(1) &&
+                           s > nb(SP - 1) && s > nb(SP) && s > nb(SP + 1);
                 }
             }
             const unsigned long long m = __ballot(keep);
@@ -411,7 +483,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     for (int i = lane; i < total; i += 64) {
         const unsigned short e = L[i];
         const int X = e & 63, Y = e >> 6;
-        dst[i] = make_uint2((uint32_t)(X + cg.sx) | ((uint32_t)(Y + cg.sy) << 12) | ((uint32_t)sc[Y * kTile + X] << 24),
+        dst[i] = make_uint2((uint32_t)(X + cg.sx) | ((uint32_t)(Y + cg.sy) << 12) | ((uint32_t)sc[Y * SP + X] << 24),
                             tag | (unsigned)i);
     }
 }
@@ -922,9 +994,12 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
 // into the interior-only blurred layout.
 constexpr int kBlurInH = kBlurTH + 6, kBlurChunks = (kBlurTW + 6 + 15) / 16;  // 38 rows x 9 x 16 B
 constexpr int kBlurInS = 16 * kBlurChunks;                                     // 144
+// row-sum pitch kBlurTW + 4 ints: the 8 rows a wave's row-sum tasks write start on different
+// banks (a pitch of 128 put all of them on one: 16-way conflicts on every store)
+constexpr int kBlurRsPitch = kBlurTW + 4;
 struct BlurShared {
     uint4 in4[kBlurInH * kBlurChunks];
-    int rs[kBlurInH][kBlurTW];
+    int rs[kBlurInH][kBlurRsPitch];
 };
 // One tile on a 256-thread slice of the workgroup (tid = 0..255).  The slice's two block-wide
 // barriers are reached by every slice, also one without a tile (valid = false).
@@ -932,7 +1007,7 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
                                           long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
                                           int2 t, int b, int tid, bool valid) {
     uint4* in4 = B.in4;
-    int(*rs)[kBlurTW] = B.rs;
+    int(*rs)[kBlurRsPitch] = B.rs;
     const uint8_t* in = reinterpret_cast<const uint8_t*>(in4);
     const LevelGeom g = levels[valid ? t.x : 0];
     const int x0 = t.y & 0xFFFF, y0 = t.y >> 16;
@@ -1445,6 +1520,10 @@ int Extractor::set_geometry(int r, int c) {
         }
     }
     pimg = off;
+    fast_maxw = 7; fast_maxh = 7;  // k_fast's LDS: the largest cell ROI of the geometry
+    for (const CellGeom& cg : cells)
+        if (cg.w) { fast_maxw = std::max(fast_maxw, (int)cg.w); fast_maxh = std::max(fast_maxh, (int)cg.h); }
+    fast_wave_bytes = fast_lds_layout(fast_maxw, fast_maxh).wave_bytes;
     bimg = boff;
     btiles.clear();
     for (int l = 0; l < nlevels; l++)
@@ -1503,14 +1582,17 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     if (batch > kPyrTiledMaxBatch) {
         for (int l = 0; l < nlevels; l++) {
             const LevelGeom& g = levels[l];
-            dim3 grid((g.W + 2 * kEdge + 255) / 256, g.ph, batch);
+            dim3 grid((g.ph + kPyrBRows - 1) / kPyrBRows, 1, batch);
             hipEvent_t ev = prof_begin(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE);
-            if (l == 0)
-                hipLaunchKernelGGL(k_pyr_level0, grid, dim3(256), 0, stream, d_images, step, image_stride, d_pyr, pimg, g,
-                                   d_level_count, nlevels);
-            else
-                hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), 0, stream, d_pyr, pimg, levels[l - 1], g,
-                                   d_xtab + g.xtab_off, d_ytab + g.ytab_off);
+            if (l == 0) {
+                const int lrow = (g.W + 3 + 3 + 15) & ~15;  // an image row from its aligned start
+                hipLaunchKernelGGL(k_pyr_level0, grid, dim3(kPyrBThreads), kPyrBRows * lrow, stream, d_images, step,
+                                   image_stride, d_pyr, pimg, g, d_level_count, nlevels, lrow);
+            } else {
+                const int lrow = levels[l - 1].stride;  // a padded source row (64-B multiple)
+                hipLaunchKernelGGL(k_pyr_resize, grid, dim3(kPyrBThreads), 2 * kPyrBRows * lrow, stream, d_pyr, pimg,
+                                   levels[l - 1], g, d_xtab + g.xtab_off, d_ytab + g.ytab_off, lrow);
+            }
             prof_end(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE, ev);
         }
     } else {
@@ -1522,9 +1604,9 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
-    hipLaunchKernelGGL(k_fast, dim3((ncells + kFastCells - 1) / kFastCells, batch), dim3(64 * kFastCells), 0, stream,
-                       d_pyr, pimg, d_levels, d_cells,
-                       ncells, d_cand, keys_cap, d_level_count, nlevels, ini_th, min_th);
+    hipLaunchKernelGGL(k_fast, dim3((ncells + kFastCells - 1) / kFastCells, batch), dim3(64 * kFastCells),
+                       kFastCells * fast_wave_bytes, stream, d_pyr, pimg, d_levels, d_cells, ncells, d_cand, keys_cap,
+                       d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
     prof_end(ORBMI_STAGE_FAST, ev);
     // small batches: the blur runs inside the octree launch on the CUs its nlevels x batch
     // workgroups leave idle; large batches fill the chip with octrees, so the blur gets its own

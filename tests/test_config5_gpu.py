@@ -35,8 +35,12 @@ def test_config5_batch64_bit_exact(oracle):
         C.c_void_p(d_k.data_ptr()), C.c_void_p(d_d.data_ptr()), C.c_void_p(d_n.data_ptr()), cap))
     _capi.check("sync", _capi.lib().orbmi_extractor_synchronize(ex.handle))
     counts, kk, dd = d_n.cpu().numpy(), d_k.cpu().numpy(), d_d.cpu().numpy()
-    ex.close()
     p = oracle.params(C5.NFEAT)
+    for i in (0, 37, 63):  # the level-by-level pyramid of the batch path
+        ref = oracle.pyramid(p, imgs[i])
+        for l in range(8):
+            np.testing.assert_array_equal(ex.pyramid_level(l, padded=True, item=i), ref[l], err_msg=f"{i} {l}")
+    ex.close()
     with ThreadPoolExecutor(16) as pool:
         ref = list(pool.map(lambda im: oracle.extract(p, im), imgs))
     gold = np.load(GOLD)
