@@ -990,25 +990,22 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
 // as P3: separable integer taps {18,34,49,55,49,34,18}, float column pass for x < blur_xv,
 // integer tail.  The reflect-101 border of the padded pyramid supplies the taps outside the
 // image.  One 128x32 output tile per workgroup: 16-B loads of the padded rows (interior column
-// x0 - 3 sits at a 16-B boundary), row sums in LDS, 4x4 outputs per thread stored as dwords
+// x0 - 3 sits at a 16-B boundary) staged in LDS, row sums in registers, 4x4 outputs per thread stored as dwords
 // into the interior-only blurred layout.
 constexpr int kBlurInH = kBlurTH + 6, kBlurChunks = (kBlurTW + 6 + 15) / 16;  // 38 rows x 9 x 16 B
 constexpr int kBlurInS = 16 * kBlurChunks;                                     // 144
-// row-sum pitch kBlurTW + 4 ints: the 8 rows a wave's row-sum tasks write start on different
-// banks (a pitch of 128 put all of them on one: 16-way conflicts on every store)
-constexpr int kBlurRsPitch = kBlurTW + 4;
 struct BlurShared {
     uint4 in4[kBlurInH * kBlurChunks];
-    int rs[kBlurInH][kBlurRsPitch];
 };
-// One tile on a 256-thread slice of the workgroup (tid = 0..255).  The slice's two block-wide
-// barriers are reached by every slice, also one without a tile (valid = false).
+// One tile on a 256-thread slice of the workgroup (tid = 0..255).  The slice's block-wide barrier
+// is reached by every slice, also one without a tile (valid = false).  The input rows are staged
+// in LDS; thread (column group cg, row group rg) then forms the integer row sums of its 4 columns
+// for the 10 input rows its 4 output rows read (3 aligned dword reads per row) in registers and
+// the column pass from them: no row-sum array round-trips LDS.
 __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                           long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
                                           int2 t, int b, int tid, bool valid) {
     uint4* in4 = B.in4;
-    int(*rs)[kBlurRsPitch] = B.rs;
-    const uint8_t* in = reinterpret_cast<const uint8_t*>(in4);
     const LevelGeom g = levels[valid ? t.x : 0];
     const int x0 = t.y & 0xFFFF, y0 = t.y >> 16;
     const uint8_t* lvl = pyr + b * pimg + g.off + kEdge - 3 + x0;  // column x0 - 3 of padded row 0
@@ -1018,21 +1015,26 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
         in4[i] = *reinterpret_cast<const uint4*>(lvl + (long long)(kEdge + yy) * g.stride + 16 * ch);
     }
     __syncthreads();
-    // row sums: one (row, 16 columns) run per task
-    for (int task = tid; valid && task < kBlurInH * (kBlurTW / 16); task += 256) {
-        const int r = task / (kBlurTW / 16), c0 = 16 * (task - r * (kBlurTW / 16));
-        const uint8_t* q = in + r * kBlurInS + c0;  // q[k] = input column c0 + k - 3
-        int v[22];
-#pragma unroll
-        for (int k = 0; k < 22; k++) v[k] = q[k];
-#pragma unroll
-        for (int c = 0; c < 16; c++)
-            rs[r][c0 + c] = 55 * v[c + 3] + 49 * (v[c + 2] + v[c + 4]) + 34 * (v[c + 1] + v[c + 5]) +
-                            18 * (v[c] + v[c + 6]);
-    }
-    __syncthreads();
     if (!valid) return;
-    const int cq = 4 * (tid & 31), rb = 4 * (tid >> 5);  // 4 columns x 4 rows per thread
+    const int cq = 4 * (tid & 31), rb = 4 * (tid >> 5);  // 4 columns x 4 output rows per thread
+    if (y0 + rb >= g.H) return;
+    const unsigned* in = reinterpret_cast<const unsigned*>(in4);
+    int rs[10][4];  // row sums of input rows rb .. rb + 9 (output row rb + rr reads rb + rr .. + 6)
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const unsigned* q = in + (rb + r) * (kBlurInS / 4) + cq / 4;  // bytes = input columns cq - 3 ..
+        const unsigned w0 = q[0], w1 = q[1], w2 = q[2];
+        int v[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = (w0 >> (8 * k)) & 255;
+            v[4 + k] = (w1 >> (8 * k)) & 255;
+            v[8 + k] = (w2 >> (8 * k)) & 255;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            rs[r][c] = 55 * v[c + 3] + 49 * (v[c + 2] + v[c + 4]) + 34 * (v[c + 1] + v[c + 5]) + 18 * (v[c] + v[c + 6]);
+    }
     uint8_t* dst = blur + b * bimg + g.boff;
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
@@ -1041,9 +1043,9 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
         unsigned packedv = 0;
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
-            const int c = cq + cc, x = x0 + c, r = rb + rr;
-            const int c3 = rs[r + 3][c], p1 = rs[r + 2][c] + rs[r + 4][c], p2 = rs[r + 1][c] + rs[r + 5][c],
-                      p3 = rs[r][c] + rs[r + 6][c];
+            const int x = x0 + cq + cc;
+            const int c3 = rs[rr + 3][cc], p1 = rs[rr + 2][cc] + rs[rr + 4][cc], p2 = rs[rr + 1][cc] + rs[rr + 5][cc],
+                      p3 = rs[rr][cc] + rs[rr + 6][cc];
             int v;
             if (x < g.blur_xv) {  // SymmColumnVec_32s8u float path
                 float sacc = (float)c3 * (55.f / 65536.f) + 0.0f;
