@@ -198,15 +198,19 @@ __global__ __launch_bounds__(kPyrBThreads) void k_pyr_level0(const uint8_t* __re
 
 // Level l: resize(level l-1, INTER_LINEAR) then copyMakeBorder(REFLECT_101|ISOLATED)
 // (src/ORBextractor.cc:1118-1124).  Border pixels recompute the interior pixel they mirror.
-// LDS: the two source rows of each output row (whole padded rows of level l-1, `lrow` bytes).
+// LDS: the two source rows of each output row (whole padded rows of level l-1, `lrow` bytes),
+// then the level's horizontal taps (d.W entries): read per output byte, they are 8x the bytes
+// written, and from global memory every 8-B lane load of a wave touched its own cache line.
 __global__ __launch_bounds__(kPyrBThreads) void k_pyr_resize(uint8_t* __restrict__ pyr, long long pimg, LevelGeom s,
-                                                             LevelGeom d, const XTab* __restrict__ xt,
+                                                             LevelGeom d, const XTab* __restrict__ xtg,
                                                              const YTab* __restrict__ yt, int lrow) {
     extern __shared__ uint4 srow16[];
     const int b = blockIdx.z, yp0 = blockIdx.x * kPyrBRows, tid = threadIdx.x;
     const int PW = d.W + 2 * kEdge, nrow = min(kPyrBRows, d.ph - yp0);
     const uint8_t* S = pyr + b * pimg + s.off;
     const int n16 = s.stride / 16;
+    XTab* xt = reinterpret_cast<XTab*>(srow16 + 2 * kPyrBRows * (lrow / 16));
+    for (int i = tid; i < d.W; i += kPyrBThreads) xt[i] = xtg[i];
     for (int i = tid; i < 2 * nrow * n16; i += kPyrBThreads) {
         const int rr = i / n16, c = i - rr * n16;  // rr = 2 * output row + tap
         const YTab y = yt[reflect101(yp0 + (rr >> 1) - kEdge, d.H)];
@@ -1592,7 +1596,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                                    image_stride, d_pyr, pimg, g, d_level_count, nlevels, lrow);
             } else {
                 const int lrow = levels[l - 1].stride;  // a padded source row (64-B multiple)
-                hipLaunchKernelGGL(k_pyr_resize, grid, dim3(kPyrBThreads), 2 * kPyrBRows * lrow, stream, d_pyr, pimg,
+                hipLaunchKernelGGL(k_pyr_resize, grid, dim3(kPyrBThreads), 2 * kPyrBRows * lrow + 8 * g.W, stream, d_pyr, pimg,
                                    levels[l - 1], g, d_xtab + g.xtab_off, d_ytab + g.ytab_off, lrow);
             }
             prof_end(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE, ev);
