@@ -34,6 +34,10 @@ struct CellGeom {
     int slot_base;       // base of the cell's candidate region (per image; cells of one level
                          // share kFastRegions regions, cell k of the level writes region k % R)
     int level;
+    long long roi_off;   // byte offset of the ROI's first pixel in one image's pyramid (level plane,
+                         // border, stride folded in: k_fast needs no LevelGeom load)
+    int stride;          // the level's row stride
+    int lcell;           // index of the cell within its level
 };
 
 struct XTab { short sx0, sx1, a0, a1; };  // horizontal resize: source taps and 11-bit weights

@@ -12,6 +12,7 @@
 
 #include "../../include/orbmi_pattern.h"
 #include "extractor.h"
+#include "trig_f64.h"
 
 namespace orbmi {
 
@@ -365,11 +366,10 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     if (c >= ncells) return;
     const CellGeom cg = cells[c];
     if (cg.w == 0) return;
-    const LevelGeom lg = levels[cg.level];
-    const long long a = b * pimg + lg.off + (long long)(kEdge + cg.y0) * lg.stride + kEdge + cg.x0;
+    const long long a = b * pimg + cg.roi_off;
     const int o = (int)(a & 3);  // stride is a multiple of 64: the same offset on every row
     const unsigned* src = reinterpret_cast<const unsigned*>(pyr + (a - o));
-    const int w = cg.w, h = cg.h, nd = (w + o + 3) >> 2, s4 = lg.stride >> 2;
+    const int w = cg.w, h = cg.h, nd = (w + o + 3) >> 2, s4 = cg.stride >> 2;
     uint8_t* wl = reinterpret_cast<uint8_t*>(fast_lds) + wid * F.wave_bytes;
     unsigned* t4 = reinterpret_cast<unsigned*>(wl);
     uint4* scores4 = reinterpret_cast<uint4*>(wl + ((4 * F.tsd * maxH + 15) & ~15));
@@ -480,10 +480,10 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     wave_sync_lds_ex();
     int base = 0;
     if (lane == 0)
-        base = atomicAdd(&level_count[(b * nlevels + cg.level) * kFastRegions + (c - lg.cell_begin) % kFastRegions], total);
+        base = atomicAdd(&level_count[(b * nlevels + cg.level) * kFastRegions + cg.lcell % kFastRegions], total);
     base = __shfl(base, 0);
     uint2* dst = cand + (long long)b * keys_cap + cg.slot_base + base;
-    const unsigned tag = (unsigned)(c - lg.cell_begin) << 10;
+    const unsigned tag = (unsigned)cg.lcell << 10;
     for (int i = lane; i < total; i += 64) {
         const unsigned short e = L[i];
         const int X = e & 63, Y = e >> 6;
@@ -1212,7 +1212,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const float angle = fast_atan2_deg((float)m01, (float)m10);
     // computeOrbDescriptor on the blurred level (src/ORBextractor.cc:108-147), pinned P6
     const float ang = angle * (float)(3.14159265358979323846 / 180.0);
-    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    double sd, cd;  // (float)cos((double)ang), (float)sin((double)ang), checked exhaustively (trig_f64.h)
+    orbmi_sincos_f64((double)ang, &sd, &cd);
+    const float ca = (float)cd, sa = (float)sd;
     unsigned long long masks[4];
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
@@ -1338,7 +1340,7 @@ int Extractor::set_geometry(int r, int c) {
         const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
         const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
         const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
-        if (wCell + 6 > 64 || hCell + 6 > 64) return ORBMI_E_UNSUPPORTED;
+        if (wCell + 6 > kTile || hCell + 6 > kTile) return ORBMI_E_UNSUPPORTED;  // list entries y << 6 | x
         const int cap = ((wCell + 1) / 2) * ((hCell + 1) / 2);
         g.cell_begin = (int)cells.size();
         g.key_base = key;
@@ -1360,6 +1362,9 @@ int Extractor::set_geometry(int r, int c) {
                     slot += cap;
                     key += cap;
                 }
+                cg.roi_off = g.off + (long long)(kEdge + cg.y0) * g.stride + kEdge + cg.x0;
+                cg.stride = g.stride;
+                cg.lcell = (int)cells.size() - g.cell_begin;
                 cells.push_back(cg);
             }
         }
