@@ -440,26 +440,56 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
         nc += __popcll(m);
     }
     wave_sync_lds_ex();
-    // C: scores of the corners
-    for (int i = lane; i < nc; i += 64) {
-        const unsigned short e = L[i];
-        const int X = e & 63, Y = e >> 6;
-        int p[16];
-        fast_circle(tb, TS, X, Y, p);
-        sc[Y * SP + X] = (uint8_t)fast_corner_score(tb[Y * TS + X], p, tl);
-    }
-    wave_sync_lds_ex();
-    // D: strict NMS at ini_th, then at min_th if nothing survived; survivors compacted in place
-    int total = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        if (pass == 1 && (total > 0 || tm == ti)) break;
-        const int t = pass == 0 ? ti : tm;
+    // B': with more corners than one pass of the wave scores (nc > 64) and ini_th > min_th, the
+    // corners at ini_th among them (segment test again, listed after them, L2 = L + nc, when the
+    // list has room for both): a corner passes at t exactly
+    // when its score is >= t, so the NMS at ini_th needs the scores of those only (the others
+    // count 0 as neighbours); the rest are scored only if the cell falls back to min_th.  With
+    // nc <= 64 the scoring pass costs the wave the same for any subset.
+    const bool split = ti > tl && nc > 64 && 2 * nc <= F.list;
+    unsigned short* L2 = L + nc;
+    unsigned short* LH = L;
+    int nh = nc;
+    if (split) {
+        LH = L2;
+        nh = 0;
         for (int i0 = 0; i0 < nc; i0 += 64) {
             const int i = i0 + lane;
-            bool keep = false;
+            bool pass = false;
             unsigned short e = 0;
             if (i < nc) {
                 e = L[i];
+                const int X = e & 63, Y = e >> 6;
+                int p[16];
+                fast_circle(tb, TS, X, Y, p);
+                pass = fast_segment(tb[Y * TS + X], p, ti);
+            }
+            const unsigned long long m = __ballot(pass);
+            if (pass) L2[nh + lanes_below(m)] = e;
+            nh += __popcll(m);
+        }
+        wave_sync_lds_ex();
+    }
+    // C: scores of the corners (of LH)
+    auto score = [&](const unsigned short* Ls, int ns) {
+        for (int i = lane; i < ns; i += 64) {
+            const unsigned short e = Ls[i];
+            const int X = e & 63, Y = e >> 6;
+            int p[16];
+            fast_circle(tb, TS, X, Y, p);
+            sc[Y * SP + X] = (uint8_t)fast_corner_score(tb[Y * TS + X], p, tl);
+        }
+        wave_sync_lds_ex();
+    };
+    // D: strict NMS at threshold t over Ls, survivors compacted in place
+    auto nms = [&](unsigned short* Ls, int ns, int t) {
+        int kept = 0;
+        for (int i0 = 0; i0 < ns; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            unsigned short e = 0;
+            if (i < ns) {
+                e = Ls[i];
                 const uint8_t* q = sc + (e >> 6) * SP + (e & 63);
                 const int s = q[0];
                 if (s >= t && s != 0) {
@@ -472,9 +502,18 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
                 }
             }
             const unsigned long long m = __ballot(keep);
-            if (keep) L[total + lanes_below(m)] = e;
-            total += __popcll(m);
+            if (keep) Ls[kept + lanes_below(m)] = e;
+            kept += __popcll(m);
         }
+        return kept;
+    };
+    score(LH, nh);
+    int total = nms(LH, nh, ti);  // at ini_th, then at min_th if nothing survived
+    const unsigned short* LO = LH;
+    if (total == 0 && tm != ti) {
+        if (split) score(L, nc);
+        total = nms(L, nc, tm);
+        LO = L;
     }
     if (total == 0) return;
     wave_sync_lds_ex();
@@ -485,7 +524,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     uint2* dst = cand + (long long)b * keys_cap + cg.slot_base + base;
     const unsigned tag = (unsigned)cg.lcell << 10;
     for (int i = lane; i < total; i += 64) {
-        const unsigned short e = L[i];
+        const unsigned short e = LO[i];
         const int X = e & 63, Y = e >> 6;
         dst[i] = make_uint2((uint32_t)(X + cg.sx) | ((uint32_t)(Y + cg.sy) << 12) | ((uint32_t)sc[Y * SP + X] << 24),
                             tag | (unsigned)i);
