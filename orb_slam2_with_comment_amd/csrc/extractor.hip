@@ -346,7 +346,8 @@ __device__ inline int lanes_below(unsigned long long m) {
 //      both darker at t = min(ini_th, min_th) -- necessary for a 9-arc (any 9 consecutive of 16
 //      hold two adjacent multiples of 4);
 //   B  the survivors: the full segment test at t;
-//   C  the corners: cornerScore into the cell's score map;
+//   C  the corners: cornerScore into the cell's score map (with > 64 corners, first only those at
+//      ini_th, found by a second segment test; the others if the cell falls back to min_th);
 //   D  strict 3x3 NMS of the corners at ini_th (score >= ini_th; neighbours below it count 0),
 //      compacted in place; when none survives, the same at min_th.
 // The survivors go to one of the level's kFastRegions dense candidate regions (cell k of the
