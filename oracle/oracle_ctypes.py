@@ -269,32 +269,61 @@ def local_ba(problem, stop=False, edge_chi2=False):
     return out
 
 
-def pose_optimization(frames, obs):
+def pose_optimization(frames, obs, diag=False):
     """Optimizer::PoseOptimization restatement over POSE_FRAME_DTYPE frames (updated in place:
-    tcw, inliers, iterations) and POSE_OBS_DTYPE observations -> outlier flags (bool, per obs)."""
+    tcw, inliers, iterations) and POSE_OBS_DTYPE observations -> outlier flags (bool, per obs).
+    diag=True also returns, per observation, the float chi2 it was classified with in each of
+    the 4 rounds (4 x n_obs, NaN where a round did not run) and per frame 8 margins: the 4 rounds'
+    smallest relative distance of the 3-bad-iterations stop test from its threshold, then the 4
+    rounds' smallest relative chi2 change of a trial (the accept / reject decision's distance
+    from a tie) (nframes x 8)."""
     L = lib()
     L.orc_pose_optimization.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_pose_optimization.restype = C.c_int
+    L.orc_pose_set_diag.argtypes = [C.c_void_p, C.c_void_p]
     assert frames.flags.c_contiguous and obs.flags.c_contiguous
     out = np.zeros(len(obs), np.uint8)
+    chi2 = np.full((4, len(obs)), np.nan, np.float32)
+    stop = np.full((len(frames), 8), np.inf)
     for f in range(len(frames)):
+        n = int(frames[f]["n_obs"])
+        b = int(frames[f]["obs_begin"])
+        buf = np.full(4 * max(n, 1), np.nan, np.float32)
+        if diag:
+            L.orc_pose_set_diag(buf.ctypes.data, stop[f].ctypes.data)
         L.orc_pose_optimization(frames[f:f + 1].ctypes.data, obs.ctypes.data, out.ctypes.data)
+        L.orc_pose_set_diag(None, None)
+        chi2[:, b:b + n] = buf[:4 * n].reshape(4, n)
+    if diag:
+        return out.astype(bool), chi2, stop
     return out.astype(bool)
 
 
-def pose_optimization_frame(frame, inv_level_sigma2, match_lf=None, lf_points=None, match_mp=None, mps=None):
+def pose_optimization_frame(frame, inv_level_sigma2, match_lf=None, lf_points=None, match_mp=None, mps=None,
+                            diag=False):
     """Optimizer::PoseOptimization(Frame*) with edge assembly (oracle/track_oracle.cpp) ->
-    (POSE_FRAME_DTYPE record, per-keypoint outlier flags)."""
+    (POSE_FRAME_DTYPE record, per-keypoint outlier flags); diag=True adds the per-round
+    classification chi2 by keypoint (4 x n, NaN without an edge) and the 8 margins of
+    pose_optimization."""
     from orb_slam2_with_comment_amd.types import POSE_FRAME_DTYPE
     L = lib()
     L.orc_pose_optimization_frame.argtypes = [C.c_void_p] * 5
+    L.orc_pose_set_frame_diag.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     mp, keep = _mappoints(match_lf, lf_points, match_mp, mps)
     rec = np.zeros(1, POSE_FRAME_DTYPE)
-    out = np.zeros(max(len(frame.keys), 1), np.uint8)
+    nk = len(frame.keys)
+    out = np.zeros(max(nk, 1), np.uint8)
     sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+    chi2 = np.full(4 * max(nk, 1), np.nan, np.float32)
+    stop = np.full(8, np.inf)
     v = frame.view()
+    if diag:
+        L.orc_pose_set_frame_diag(chi2.ctypes.data, nk, stop.ctypes.data)
     L.orc_pose_optimization_frame(C.addressof(v), sig.ctypes.data, C.addressof(mp), rec.ctypes.data, out.ctypes.data)
-    return rec[0], out[:len(frame.keys)]
+    L.orc_pose_set_frame_diag(None, 0, None)
+    if diag:
+        return rec[0], out[:nk], chi2[:4 * nk].reshape(4, nk), stop
+    return rec[0], out[:nk]
 
 
 def _mappoints(match_lf, lf_points, match_mp, mps):

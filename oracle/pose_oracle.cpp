@@ -26,6 +26,17 @@ namespace {
 
 using namespace g2o_oracle;
 
+// Parity diagnostics for tests/test_pose_gpu.py (orc_pose_set_diag): the float chi2 each
+// observation was classified with in each of the 4 rounds (round-major, n_obs per round, NaN
+// where a round did not run), and per round the smallest relative distance
+// |(iniChi - currentChi) * 1e3 - iniChi| / iniChi of the 3-bad-iterations stop test
+// (optimization_algorithm_levenberg.cpp:154-161) over the round's iterations, then per round the
+// smallest |currentChi - tempChi| / currentChi over its trials (how close an accept / reject
+// decision came to a tie: converged rounds decide on rounding noise, and 10 rejections in a row
+// end the optimisation, :163).  Null = off.
+thread_local float* g_diag_chi2 = nullptr;
+thread_local double* g_diag_stop = nullptr;
+
 struct UEdge {
     double Xw[3];
     double obs[3];
@@ -100,6 +111,7 @@ struct PoseOpt {
     double lambda = 0, ni = 2;
     int nBad = 0;
     int iters = 0;
+    double* stop_margin = nullptr;
 
     explicit PoseOpt(std::vector<UEdge>& e) : E(e) {}
 
@@ -179,6 +191,8 @@ struct PoseOpt {
             double tempChi = active_robust_chi2();
             if (!ok2) tempChi = std::numeric_limits<double>::max();
             rho = (currentChi - tempChi) / (compute_scale() + 1e-3);
+            if (stop_margin && currentChi > 0 && ok2)
+                stop_margin[4] = std::min(stop_margin[4], std::fabs(currentChi - tempChi) / currentChi);
             if (rho > 0 && std::isfinite(tempChi)) {
                 double alpha = 1. - std::pow((2 * rho - 1), 3);
                 alpha = std::min(alpha, 2. / 3.);
@@ -195,6 +209,8 @@ struct PoseOpt {
         } while (rho < 0 && qmax < 10);
         if (trace_trials()) std::fputc('|', stderr);
         if (qmax == 10 || rho == 0) return Terminate;
+        if (stop_margin && iniChi > 0)
+            *stop_margin = std::min(*stop_margin, std::fabs((iniChi - currentChi) * 1e3 - iniChi) / iniChi);
         if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
         else nBad = 0;
         return nBad >= 3 ? Terminate : OK;
@@ -235,11 +251,16 @@ extern "C" int orc_pose_optimization(orbmi_pose_frame* f, const orbmi_pose_obs* 
     if (n < 3) return 0;  // :378-379, pose untouched
     PoseOpt P(E);
     P.cam = Cam{f->fx, f->fy, f->cx, f->cy, f->bf};
+    if (g_diag_chi2)
+        for (int k = 0; k < 4 * n; k++) g_diag_chi2[k] = std::numeric_limits<float>::quiet_NaN();
+    if (g_diag_stop)
+        for (int r = 0; r < 8; r++) g_diag_stop[r] = std::numeric_limits<double>::infinity();
     const float chi2Mono[4] = {5.991f, 5.991f, 5.991f, 5.991f};
     const float chi2Stereo[4] = {7.815f, 7.815f, 7.815f, 7.815f};
     int nBad = 0;
     for (int it = 0; it < 4; it++) {
         P.T = se3_from_tcw(f->tcw);
+        P.stop_margin = g_diag_stop ? &g_diag_stop[it] : nullptr;
         P.optimize(10);
         nBad = 0;
         // mono edges first, then stereo (the reference's two loops; order is immaterial here)
@@ -249,6 +270,7 @@ extern "C" int orc_pose_optimization(orbmi_pose_frame* f, const orbmi_pose_obs* 
                 if ((int)e.stereo != pass) continue;
                 if (outlier[f->obs_begin + k]) compute_error(P.T, P.cam, e);
                 const float c2 = (float)chi2(e);
+                if (g_diag_chi2) g_diag_chi2[it * n + k] = c2;
                 if (c2 > (e.stereo ? chi2Stereo[it] : chi2Mono[it])) {
                     outlier[f->obs_begin + k] = 1;
                     e.level = 1;
@@ -265,4 +287,10 @@ extern "C" int orc_pose_optimization(orbmi_pose_frame* f, const orbmi_pose_obs* 
     f->iterations = P.iters;
     f->inliers = n - nBad;
     return f->inliers;
+}
+
+// Diagnostics on (buffers of 4 * n_obs floats and 8 doubles for the next frame) or off (nulls).
+extern "C" void orc_pose_set_diag(float* chi2_rounds, double* stop_margin) {
+    g_diag_chi2 = chi2_rounds;
+    g_diag_stop = stop_margin;
 }

@@ -10,6 +10,7 @@
 // UpdateLastFrame / UpdateLocalMap (map management, out of scope) are the caller's inputs:
 // the last frame's points and the local map arrive as flat arrays (include/orbmi.h).
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "../include/orbmi.h"
@@ -24,6 +25,7 @@ int orc_search_by_projection_last_frame(const orbmi_frame_view* CF, const uint8_
                                         const orbmi_frame_view* LF, const orbmi_lastframe_point* lfp, float th,
                                         int mono, int check_ori, int* out, int* nmatches);
 int orc_pose_optimization(orbmi_pose_frame* f, const orbmi_pose_obs* obs, uint8_t* outlier);
+void orc_pose_set_diag(float* chi2_rounds, double* stop_margin);
 }
 
 namespace {
@@ -51,7 +53,19 @@ int* slot_of(const orbmi_frame_mappoints& mp, int i) {
 
 }  // namespace
 
+// Parity diagnostics (orc_pose_set_frame_diag): pose_oracle.cpp's per-round classification
+// chi2, scattered to keypoint indices (4 x n_kp, NaN for keypoints without an edge).
+thread_local float* g_frame_diag_chi2 = nullptr;
+thread_local int g_frame_diag_n = 0;
+thread_local double* g_frame_diag_stop = nullptr;
+
 extern "C" {
+
+void orc_pose_set_frame_diag(float* chi2_kp_rounds, int n_kp, double* stop_margin) {
+    g_frame_diag_chi2 = chi2_kp_rounds;
+    g_frame_diag_n = n_kp;
+    g_frame_diag_stop = stop_margin;
+}
 
 // Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:257-481): edges in keypoint order
 // (:296-375), then the 4-round optimisation of pose_oracle.cpp.  outlier: F->n entries.
@@ -78,7 +92,19 @@ int orc_pose_optimization_frame(const orbmi_frame_view* F, const float* inv_leve
     rec->obs_begin = 0;
     rec->n_obs = (int)obs.size();
     std::vector<uint8_t> fl(obs.size() + 1);
+    std::vector<float> diag;
+    if (g_frame_diag_chi2) {
+        diag.assign(4 * obs.size() + 1, std::numeric_limits<float>::quiet_NaN());
+        for (int k = 0; k < 4 * g_frame_diag_n; k++) g_frame_diag_chi2[k] = std::numeric_limits<float>::quiet_NaN();
+        orc_pose_set_diag(diag.data(), g_frame_diag_stop);
+    }
     orc_pose_optimization(rec, obs.data(), fl.data());
+    if (g_frame_diag_chi2) {
+        orc_pose_set_diag(nullptr, nullptr);
+        const size_t no = obs.size();
+        for (int r = 0; r < 4; r++)
+            for (size_t k = 0; k < no; k++) g_frame_diag_chi2[r * g_frame_diag_n + obs[k].index] = diag[r * no + k];
+    }
     for (size_t k = 0; k < obs.size(); k++) outlier[obs[k].index] = fl[k];
     return rec->inliers;
 }

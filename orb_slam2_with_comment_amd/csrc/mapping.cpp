@@ -91,17 +91,17 @@ void null_vector4(const float* A, double v[4]) {
     for (int k = 0; k < 4; k++) v[k] = V[k][m];
 }
 
-// Frame / KeyFrame::UnprojectStereo (src/KeyFrame.cc, Frame.cc:701-715): Rwc x3Dc + Ow
+// Frame / KeyFrame::UnprojectStereo (src/KeyFrame.cc, Frame.cc:701-715): `Rwc*x3Dc + Ow` is one
+// cv::gemm(Rwc, x3Dc, 1, Ow, 1) MatExpr, so Ow is added before the single rounding to float
 void unproject(const orbmi_tri_keyframe& K, int i, float* x3d) {
     const float z = K.depth[i];
     const float invfx = 1.f / K.fx, invfy = 1.f / K.fy;
     const float xc[3] = {(K.keys_un[i].x - K.cx) * z * invfx, (K.keys_un[i].y - K.cy) * z * invfy, z};
-    float R[9], Rt[9], p[3], ow[3];
+    float R[9], Rt[9], ow[3];
     rot(K.tcw, R);
     transpose3(R, Rt);
-    matmul(Rt, xc, p, 3, 3, 1);
     center(K.tcw, ow);
-    for (int r = 0; r < 3; r++) x3d[r] = p[r] + ow[r];
+    for (int r = 0; r < 3; r++) x3d[r] = (float)(dot3(Rt + 3 * r, xc) + (double)ow[r]);
 }
 
 }  // namespace
@@ -186,15 +186,16 @@ int orbmi_triangulate_matches(const orbmi_tri_keyframe* kf1, const orbmi_tri_key
         } else {
             continue;  // no stereo and very low parallax
         }
-        // in front of both cameras (:474-482)
-        const float z1 = (float)dot3(Rcw1 + 6, x) + tcw1[2];
+        // in front of both cameras (:474-482); cv::Mat::dot returns double, so `dot + tcw` is a
+        // double sum rounded to float once
+        const float z1 = (float)(dot3(Rcw1 + 6, x) + (double)tcw1[2]);
         if (z1 <= 0) continue;
-        const float z2 = (float)dot3(Rcw2 + 6, x) + tcw2[2];
+        const float z2 = (float)(dot3(Rcw2 + 6, x) + (double)tcw2[2]);
         if (z2 <= 0) continue;
         // reprojection error in the first keyframe (:484-510)
         const float sigmaSquare1 = K1.level_sigma2[kp1.octave];
-        const float x1 = (float)dot3(Rcw1, x) + tcw1[0];
-        const float y1 = (float)dot3(Rcw1 + 3, x) + tcw1[1];
+        const float x1 = (float)(dot3(Rcw1, x) + (double)tcw1[0]);
+        const float y1 = (float)(dot3(Rcw1 + 3, x) + (double)tcw1[1]);
         const float invz1 = (float)(1.0 / z1);
         if (!bStereo1) {
             const float u1 = K1.fx * x1 * invz1 + K1.cx, v1 = K1.fy * y1 * invz1 + K1.cy;
@@ -209,8 +210,8 @@ int orbmi_triangulate_matches(const orbmi_tri_keyframe* kf1, const orbmi_tri_key
         }
         // ... and in the second (:512-537); the right coordinate uses the first keyframe's mbf
         const float sigmaSquare2 = K2.level_sigma2[kp2.octave];
-        const float x2 = (float)dot3(Rcw2, x) + tcw2[0];
-        const float y2 = (float)dot3(Rcw2 + 3, x) + tcw2[1];
+        const float x2 = (float)(dot3(Rcw2, x) + (double)tcw2[0]);
+        const float y2 = (float)(dot3(Rcw2 + 3, x) + (double)tcw2[1]);
         const float invz2 = (float)(1.0 / z2);
         if (!bStereo2) {
             const float u2 = K2.fx * x2 * invz2 + K2.cx, v2 = K2.fy * y2 * invz2 + K2.cy;

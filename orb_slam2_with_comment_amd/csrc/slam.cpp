@@ -239,7 +239,9 @@ struct orbmi_slam {
             kbuf.resize(cap);
             dbuf.resize((size_t)cap * 32);
             const int rc = orbmi_extract(ex, img, rows, cols, step, kbuf.data(), dbuf.data(), cap, &n);
-            if (rc == ORBMI_E_CAP) { cap = n; continue; }
+            // grow only when the call asked for more room than it had: an E_CAP that does not
+            // come from this capacity (the extractor's own output capacity) is an error
+            if (rc == ORBMI_E_CAP && n > cap) { cap = n; continue; }
             SLAM_CHECK(rc);
             break;
         }
@@ -447,7 +449,7 @@ struct orbmi_slam {
             for (int r = 0; r < 3; r++) {
                 const double a = (double)twc[4 * r] * (double)x + (double)twc[4 * r + 1] * (double)y +
                                  (double)twc[4 * r + 2] * (double)z;
-                mp.pos[r] = (float)a + twc[4 * r + 3];
+                mp.pos[r] = (float)(a + (double)twc[4 * r + 3]);  // one gemm(Rwc, x3Dc, 1, Ow, 1)
             }
             mp.ref_kf = k;
             mp.first_kf_id = k;

@@ -610,7 +610,8 @@ class StereoSLAM:
         y = ((f.keys["y"][idx] - np.float32(c.cy)) * z * invfy).astype(np.float32)
         Twc = pose_inverse(f.tcw)
         pc = np.stack([x, y, z], 0).astype(np.float64)
-        return ((Twc[:3, :3].astype(np.float64) @ pc).astype(np.float32) + Twc[:3, 3:4]).T.astype(np.float32)
+        # mRwc*x3Dc+mOw is one cv::gemm(Rwc, x3Dc, 1, Ow, 1): Ow added before the one rounding
+        return (Twc[:3, :3].astype(np.float64) @ pc + Twc[:3, 3:4].astype(np.float64)).T.astype(np.float32)
 
     def _create_points(self, kf: KeyFrame, cf: TrackedFrame, idx: list):
         """new MapPoint(x3D, pKF, pMap) + AddObservation + AddMapPoint + ComputeDistinctive +

@@ -57,3 +57,7 @@ def test_config5_batch64_bit_exact(oracle):
             assert C5.digest(k, dd[i, :n]) == gold["output_sha256"][i].tobytes().decode(), i
             assert n == gold["n"][i]
     print(f"config 5: 64 frames bit-exact vs oracle; {pinned}/64 also match the committed digests")
+    # the renderer is deterministic: every frame's image must still be the one the digests were
+    # made from, or the golden file pins nothing
+    assert pinned == B, f"only {pinned}/{B} rendered frames match the committed image digests"
+

@@ -1,8 +1,19 @@
 """GPU parity: Optimizer::PoseOptimization on MI355X (fp64, one workgroup per frame) vs the g2o
-restatement (oracle/pose_oracle.cpp).  Bars: pose within 1e-4 (BASELINE.json north_star), the
-mvbOutlier flags and the returned inlier count identical up to a chi2-on-the-threshold flip
-(<= 0.2 % of the edges), LM iteration counts within 2 over the 4 rounds (the stop tests of
-converged rounds sit on rounding)."""
+restatement (oracle/pose_oracle.cpp, src/Optimizer.cc:257-481).
+
+Bars:
+  * pose within 1e-4 (BASELINE.json north_star);
+  * mvbOutlier flags (index output: they drive Tracking's mvpMapPoints pass and every later
+    frame) and the returned inlier count EXACT, except for an observation whose oracle chi2 in
+    the final classification round (src/Optimizer.cc:418-466) lies within CHI2_RTOL of its
+    5.991 / 7.815 threshold -- closer than two fp64 reduction orders can resolve (the LocalBA
+    erase-list rule, tests/test_lba_gpu.py);
+  * LM iteration counts identical, unless the oracle's run had a decision that rounding can
+    flip: a 3-bad-iterations stop test within STOP_RTOL of its threshold
+    ((iniChi - chi) * 1e3 vs iniChi, optimization_algorithm_levenberg.cpp:154-161), or a trial
+    whose relative chi2 change was below TIE_RTOL (converged rounds accept / reject on rounding
+    noise, and 10 rejections in a row end the round, :163).  Every difference is printed with
+    its margins."""
 import numpy as np
 import pytest
 
@@ -10,6 +21,34 @@ from orb_slam2_with_comment_amd import synth_map as SM
 
 pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-4
+CHI2_RTOL = 1e-6
+STOP_RTOL = 1e-6
+TIE_RTOL = 1e-9
+CHI2_TH = (5.991, 7.815)
+
+
+def check_flags(got, ref, chi2_rounds, stereo, tag=""):
+    """Differing outlier flags are allowed only where the oracle's final-round chi2 sits on the
+    threshold (within CHI2_RTOL); returns the number of differing flags."""
+    mism = np.nonzero(np.asarray(got, bool) != np.asarray(ref, bool))[0]
+    if len(mism):
+        ran = ~np.isnan(chi2_rounds).all(axis=1)
+        last = int(np.nonzero(ran)[0][-1])
+        c = chi2_rounds[last, mism].astype(np.float64)
+        th = np.where(stereo[mism], CHI2_TH[1], CHI2_TH[0])
+        margin = np.abs(c - th) / th
+        print(f"{tag} outlier flags differing: {len(mism)}, oracle chi2 {c.tolist()}, margins {margin.tolist()}")
+        assert (margin <= CHI2_RTOL).all(), (tag, mism.tolist(), margin.tolist())
+    return len(mism)
+
+
+def check_iterations(got_it, ref_it, margins, tag=""):
+    if int(got_it) == int(ref_it):
+        return
+    stop, tie = float(np.min(margins[:4])), float(np.min(margins[4:]))
+    print(f"{tag} LM iterations {int(got_it)} vs oracle {int(ref_it)}: stop-test margin {stop:.3e}, "
+          f"smallest trial chi2 change {tie:.3e}")
+    assert stop <= STOP_RTOL or tie <= TIE_RTOL, (tag, int(got_it), int(ref_it), stop, tie)
 
 
 @pytest.fixture(scope="module")
@@ -18,18 +57,25 @@ def PO():
     return PoseOptimizer()
 
 
-def _compare(fr, out, ref_fr, ref_out):
+def _compare(fr, out, ref_fr, ref_out, ob, chi2, margins):
     for f in range(len(fr)):
         d = np.abs(fr[f]["tcw"] - ref_fr[f]["tcw"]).max()
         assert d <= POSE_TOL, (f, d)
         n = int(fr[f]["n_obs"])
-        s = slice(int(fr[f]["obs_begin"]), int(fr[f]["obs_begin"]) + n)
-        mism = int((out[s] != ref_out[s]).sum())
-        assert mism <= max(1, int(0.002 * n)), (f, mism)
-        assert abs(int(fr[f]["inliers"]) - int(ref_fr[f]["inliers"])) <= max(1, int(0.002 * n))
-        # the 3-bad-iterations stop compares (iniChi - chi) * 1e3 with iniChi: a chi summed in
-        # another order can end a converged round one iteration earlier or later
-        assert abs(int(fr[f]["iterations"]) - int(ref_fr[f]["iterations"])) <= 2
+        b = int(fr[f]["obs_begin"])
+        s = slice(b, b + n)
+        nd = check_flags(out[s], ref_out[s], chi2[:, s], ~(ob["ur"][s] < 0), tag=f"frame {f}")
+        if n >= 3:  # the inlier count is n minus the final round's outliers (:466-480)
+            assert int(fr[f]["inliers"]) == n - int(np.asarray(out[s], bool).sum())
+        assert abs(int(fr[f]["inliers"]) - int(ref_fr[f]["inliers"])) <= nd
+        check_iterations(fr[f]["iterations"], ref_fr[f]["iterations"], margins[f], tag=f"frame {f}")
+
+
+def _run(oracle, PO, fr, ob):
+    ref = fr.copy()
+    ref_out, chi2, margins = oracle.pose_optimization(ref, ob, diag=True)
+    out = PO.run(fr, ob)
+    _compare(fr, out, ref, ref_out, ob, chi2, margins)
 
 
 @pytest.mark.parametrize("seed,n,stereo,outl,frames", [(1, 600, 0.7, 0.1, 1), (2, 2000, 0.8, 0.1, 1),
@@ -37,17 +83,12 @@ def _compare(fr, out, ref_fr, ref_out):
                                                         (5, 300, 0.5, 0.3, 8), (6, 1200, 0.7, 0.05, 4)])
 def test_pose_parity(oracle, PO, seed, n, stereo, outl, frames):
     fr, ob, _ = SM.pose_problem(seed=seed, n_obs=n, stereo_frac=stereo, outlier_frac=outl, nframes=frames)
-    ref = fr.copy()
-    ref_out = oracle.pose_optimization(ref, ob)
-    out = PO.run(fr, ob)
-    _compare(fr, out, ref, ref_out)
+    _run(oracle, PO, fr, ob)
 
 
 def test_pose_large_initial_error(oracle, PO):
     fr, ob, _ = SM.pose_problem(seed=7, n_obs=800, pose_noise=(0.05, 0.5))
-    ref = fr.copy()
-    ref_out = oracle.pose_optimization(ref, ob)
-    _compare(fr, PO.run(fr, ob), ref, ref_out)
+    _run(oracle, PO, fr, ob)
 
 
 @pytest.mark.parametrize("n", [0, 2, 5, 9])
@@ -58,10 +99,7 @@ def test_pose_small(oracle, PO, n):
         fr["n_obs"] = 0
         ob = ob[:0].copy()
     t0 = fr["tcw"].copy()
-    ref = fr.copy()
-    ref_out = oracle.pose_optimization(ref, ob)
-    out = PO.run(fr, ob)
-    _compare(fr, out, ref, ref_out)
+    _run(oracle, PO, fr, ob)
     if n < 3:
         np.testing.assert_array_equal(fr["tcw"], t0)
         assert fr[0]["inliers"] == 0

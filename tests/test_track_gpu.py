@@ -5,12 +5,15 @@ the device and the optimised pose handed to the local-map search through device 
 Stage by stage, every integer output is compared exactly with the oracle given the GPU's
 float inputs of that stage (searches at the GPU's pose, bookkeeping with the GPU's outlier
 flags); each pose is compared with the oracle's PoseOptimization within 1e-4 (BASELINE.json
-north_star) with outlier flags equal up to chi2-on-threshold flips (<= 0.2 % of the edges, as
-tests/test_pose_gpu.py).  End to end, the final pose matches the oracle's full chain within 1e-4."""
+north_star), its outlier flags and inlier count exactly up to an oracle chi2 on the threshold and
+its iteration count up to a rounding-decided LM decision (the bars of tests/test_pose_gpu.py).
+End to end, the final pose matches the oracle's full chain within 1e-4 and every count and match
+array is exact."""
 import numpy as np
 import pytest
 
 from scenario import frame_data, lastframe, local_map
+from test_pose_gpu import check_flags, check_iterations
 
 pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-4
@@ -42,13 +45,14 @@ def _setup(f, lfp_keep=None, dt=(0.03, -0.02, 0.05)):
     return tr, d, tcw, lf, lfp, mps, Frame(kl, dl, u, tcw, cam)
 
 
-def _cmp_pose(got_rec, ref_rec, got_out, ref_out):
+def _cmp_pose(got_rec, ref, got_out, u_right):
+    ref_rec, ref_out, chi2, margins = ref
     assert np.abs(got_rec["tcw"] - ref_rec["tcw"]).max() <= POSE_TOL
     n = int(ref_rec["n_obs"])
     assert int(got_rec["n_obs"]) == n
-    tol = max(1, int(0.002 * n))
-    assert int((got_out != ref_out).sum()) <= tol
-    assert abs(int(got_rec["inliers"]) - int(ref_rec["inliers"])) <= tol
+    nd = check_flags(got_out, ref_out, chi2, np.asarray(u_right) >= 0, tag="PoseOptimization")
+    assert abs(int(got_rec["inliers"]) - int(ref_rec["inliers"])) <= nd
+    check_iterations(got_rec["iterations"], ref_rec["iterations"], margins, tag="PoseOptimization")
 
 
 @pytest.mark.parametrize("f", [3, 6])
@@ -72,8 +76,8 @@ def test_track_chain_stagewise(oracle, f):
     ref_lf = np.ascontiguousarray(ref_lf, np.int32)
     assert g_cnt[0] == ref_nm
     # PoseOptimization: 1e-4
-    ref_rec0, ref_out0 = oracle.pose_optimization_frame(cf, sig, ref_lf.copy(), lfp)
-    _cmp_pose(rec0, ref_rec0, g_out, ref_out0)
+    ref0 = oracle.pose_optimization_frame(cf, sig, ref_lf.copy(), lfp, diag=True)
+    _cmp_pose(rec0, ref0, g_out, cf.u_right)
     # discard outliers with the GPU's flags: exact
     upd = ref_lf.copy()
     occ, cnt = oracle.track_update_matches(cf, 0, g_out, upd, lfp)
@@ -92,8 +96,8 @@ def test_track_chain_stagewise(oracle, f):
     trk = oracle.is_in_frustum(cf2, mps, 0.5)
     ref_mp, _ = oracle.search_by_projection_local(cf2, g_occ, mps, trk, 1.0, 0.8)
     ref_mp = np.ascontiguousarray(ref_mp, np.int32)
-    ref_rec1, ref_out1 = oracle.pose_optimization_frame(cf2, sig, g_lf.copy(), lfp, ref_mp.copy(), mps)
-    _cmp_pose(rec1, ref_rec1, g_out2, ref_out1)
+    ref1 = oracle.pose_optimization_frame(cf2, sig, g_lf.copy(), lfp, ref_mp.copy(), mps, diag=True)
+    _cmp_pose(rec1, ref1, g_out2, cf.u_right)
     up_lf, up_mp = g_lf.copy(), ref_mp.copy()
     _, cnt = oracle.track_update_matches(cf2, 1, g_out2, up_lf, lfp, up_mp, mps)
     np.testing.assert_array_equal(g_mp, up_mp)
@@ -118,10 +122,13 @@ def test_track_chain_end_to_end(oracle, f):
     n = len(cf.keys)
     st = ref["stats"]
     assert res["search_matches"] == st[0]
-    tol = max(2, int(0.005 * n))
-    assert abs(res["nmatches_map"] - st[1]) <= tol and abs(res["inliers"] - st[2]) <= tol
-    got_mp = tr.match_mp[:n].cpu().numpy()
-    assert int((got_mp != ref["match_mp"]).sum()) <= tol
+    # the local-map search runs at the GPU's pose, 1e-4-close to the oracle's: its matches and
+    # both counts are index output and held exact (a map point on a search-window edge at one
+    # pose and not the other would show here)
+    assert res["nmatches_map"] == st[1] and res["inliers"] == st[2], (res, st)
+    np.testing.assert_array_equal(tr.match_mp[:n].cpu().numpy(), ref["match_mp"])
+    np.testing.assert_array_equal(tr.match_lf[:n].cpu().numpy(), ref["match_lf"])
+    np.testing.assert_array_equal(tr.outlier[:n].cpu().numpy().astype(bool), ref["outlier"])
     tr.close()
 
 

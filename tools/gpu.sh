@@ -1,0 +1,85 @@
+#!/bin/bash
+# The one GPU runner (via gpurun): bash tools/gpu.sh TAG STEP [STEP ...]
+# Each step runs under its own time limit; the script stops at the first step that crashes or
+# times out (exit status other than 0/1) and starts nothing more on the GPU.  Output goes to
+# gpurun_out/TAG/ (summaries worth keeping under gpurun_out/TAG/profiles/, which gpurun merges
+# back: copy them into profiles/TAG/ here).
+#
+# Steps:
+#   tests            pytest -m gpu (whole suite)
+#   tests=EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            bench.py (default track mode, with the CPU baseline)
+#   bench_quick      bench.py --steps 60 --warmup 8 --no-cpu-baseline
+#   bench_MODE       bench.py --mode MODE (lba, batch, extract, system)
+#   gloo2            bench.py --gpus 2 --dist-backend gloo (config 4 rehearsal on one device)
+#   prof             rocprofv3 --kernel-trace --stats of the default bench
+#   prof_MODE        the same for --mode MODE
+#   pmc              FETCH_SIZE and WRITE_SIZE passes of the default bench -> traffic.json
+#   pmc_MODE         the same for --mode MODE
+#   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
+TAG=${1:-run}
+shift
+OUT=gpurun_out/$TAG
+P=$OUT/profiles
+mkdir -p $OUT $P
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+    local name=$1 t=$2; shift 2
+    timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+    local rc=$?
+    echo "$name exit $rc" | tee -a $OUT/status.txt
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; tail -40 $OUT/$name.log; exit $rc; fi
+    return 0
+}
+modeargs() {  # MODE -> bench args
+    case $1 in
+        track) echo "";;
+        lba) echo "--mode lba --steps 50 --warmup 10";;
+        batch) echo "--mode batch --steps 50 --warmup 4";;
+        extract) echo "--mode extract";;
+        system) echo "--mode system";;
+    esac
+}
+python -c "import torch; print(torch.cuda.get_device_name(0))" > $OUT/device.txt 2>&1
+for step in "$@"; do
+    case $step in
+        tests)
+            run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
+            tail -4 $OUT/pytest_gpu.log; cp $OUT/pytest_gpu.log $P/;;
+        tests=*)
+            run pytest_sel 600 python -u -m pytest tests -m gpu -v -rf -s --timeout 300 --timeout-method thread -k "${step#tests=}"
+            tail -30 $OUT/pytest_sel.log;;
+        smoke)
+            run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; cat $OUT/smoke.log;;
+        bench)
+            run bench 500 python bench.py; tail -1 $OUT/bench.log | tee $P/bench.json;;
+        bench_quick)
+            run bench_quick 300 python bench.py --steps 60 --warmup 8 --no-cpu-baseline; tail -1 $OUT/bench_quick.log;;
+        bench_*)
+            m=${step#bench_}
+            run bench_$m 500 python bench.py $(modeargs $m); tail -1 $OUT/bench_$m.log | tee $P/bench_$m.json;;
+        gloo2)
+            run gloo2 500 python bench.py --gpus 2 --dist-backend gloo --steps 40 --warmup 8 --no-cpu-baseline
+            tail -1 $OUT/gloo2.log | tee $P/bench_config4_gloo2.json;;
+        prof|prof_*)
+            m=${step#prof}; m=${m#_}; m=${m:-track}
+            run prof_$m 500 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$m -o stats -- python3 bench.py $(modeargs $m) --steps 100 --warmup 10 --no-cpu-baseline
+            find $OUT/prof_$m -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats_$m.csv \;
+            cp $OUT/prof_$m.log $P/prof_stats_$m.log
+            cut -d, -f1-5 $P/kernel_stats_$m.csv | head -25;;
+        pmc|pmc_*)
+            m=${step#pmc}; m=${m#_}; m=${m:-track}
+            run pmc_fetch_$m 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch_$m -o fetch -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
+            run pmc_write_$m 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write_$m -o write -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
+            python tools/pmc_traffic.py $OUT/pmc_fetch_$m $OUT/pmc_write_$m $P/traffic_$m.json && head -40 $P/traffic_$m.json;;
+        ab=*)
+            pair=${step#ab=}; A=${pair%,*}; B=${pair#*,}
+            for i in 1 2 3; do
+                ORBMI_LIB=$A run ab_A$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+                ORBMI_LIB=$B run ab_B$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+                echo "A $(tail -1 $OUT/ab_A$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')  B $(tail -1 $OUT/ab_B$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')" | tee -a $OUT/ab.txt
+            done;;
+        *) echo "unknown step $step"; exit 2;;
+    esac
+done
