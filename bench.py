@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="frames per launch in --mode batch")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lm-chain", choices=["full", "bow-ba"], default="full",
+                    help="per-keyframe LocalMapping work: the whole LocalMapping::Run body, or ComputeBoW + LocalBA")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -154,6 +156,85 @@ def setup_track(a, rank, local):
                 n_mp=n_mp, feats=feats2, keep=(lf_keys, lf_desc, lf_u, lf_tcw, sf), nF=nF)
 
 
+def setup_local_mapping(S, voc, vocab, rank, problem, n_neighbours=9, n_target_maps=4):
+    """LocalMapping jobs (pipeline.LocalMappingJob) for the resident frames: keyframe f's
+    neighbours are the other resident frames (their FeatureVectors computed once), its map points
+    the back-projected local map of frame f, the fuse targets' points the local maps of its
+    n_target_maps nearest neighbours, and its points' observation descriptors bit-flipped copies
+    of the point descriptor (2-6 per point).  Host mirrors ride along for the CPU baseline."""
+    from orb_slam2_with_comment_amd.pipeline import KeyFrameData, LocalMappingJob
+    from orb_slam2_with_comment_amd.types import MAPPOINT_DTYPE, Frame
+    tr, cam = S["tr"], S["cam"]
+    dev = tr.kps.device
+    sf = np.ascontiguousarray(tr.scale_factors, np.float32)
+    sig2 = np.ascontiguousarray(tr.extractor.GetScaleSigmaSquares(), np.float32)
+    lf_keys, lf_desc, lf_u, lf_tcw, _ = S["keep"]
+    nF, cap = S["nF"], tr.cap
+    rng = np.random.default_rng(11 + rank)
+    has_mp_h = (rng.random((nF, cap)) < 0.4).astype(np.uint8)  # GetMapPoint(i) != NULL
+    has_mp = torch.from_numpy(has_mp_h).to(dev)
+    kfd, host = [], []
+    for f in range(nF):
+        _, _, _, kl, dl, u, d = S["feats"][f]
+        _, _, fv = voc.transform(dl, 4)
+        kfd.append(KeyFrameData(cam, sf, sig2, len(kl), lf_keys[f].data_ptr(), lf_desc[f].data_ptr(),
+                                lf_u[f].data_ptr(), has_mp[f].data_ptr(), kl, u, d, lf_tcw[f], fv=fv))
+        host.append(dict(frame=Frame(kl, dl, u, lf_tcw[f], cam), has_mp=has_mp_h[f, :len(kl)].copy(), fv=fv))
+    jobs, keep = {}, [has_mp]
+    for f in range(2, nF):
+        nbrs = sorted((g for g in range(nF) if g != f), key=lambda g: (abs(g - f), g))[:n_neighbours]
+        mp_h = S["mps"][f].cpu().numpy().view(MAPPOINT_DTYPE)
+        tgt = [g for g in nbrs if S["mps"][g] is not None][:n_target_maps]
+        tp_h = np.concatenate([S["mps"][g].cpu().numpy().view(MAPPOINT_DTYPE) for g in tgt])
+        d_tp = torch.from_numpy(tp_h.view(np.uint8).copy()).to(dev)
+        nobs = rng.integers(2, 7, len(mp_h))
+        off = np.concatenate([[0], np.cumsum(nobs)]).astype(np.int32)
+        obs = np.repeat(mp_h["desc"], nobs, axis=0)
+        flip = (rng.random(obs.shape) < 0.08) * (1 << rng.integers(0, 8, obs.shape))  # one bit in ~8 % of bytes
+        obs = (obs ^ flip.astype(np.uint8)).astype(np.uint8)
+        d_obs, d_off = torch.from_numpy(obs.copy()).to(dev), torch.from_numpy(off).to(dev)
+        keep += [d_tp, d_obs, d_off]
+        job = LocalMappingJob(kfd[f], lf_desc[f].data_ptr(), [kfd[g] for g in nbrs],
+                              (S["mps"][f].data_ptr(), len(mp_h)), (d_tp.data_ptr(), len(tp_h)),
+                              (d_obs.data_ptr(), d_off.data_ptr(), len(mp_h)), problem)
+        job.host = dict(kf=host[f], neighbours=[host[g] for g in nbrs], kf_points=mp_h, target_points=tp_h,
+                        obs_desc=obs, obs_off=off, desc=S["feats"][f][4])
+        jobs[f] = job
+    torch.cuda.synchronize()
+    return jobs, (kfd, keep)
+
+
+def cpu_local_mapping(O, vocab, job):
+    """The same LocalMapping::Run iteration as pipeline.LocalMapper.run_job on the oracle
+    (the host triangulation geometry is liborbmi.so's host code, shared with the GPU loop)."""
+    import ctypes as C_
+    from orb_slam2_with_comment_amd._capi import check, lib
+    from orb_slam2_with_comment_amd.types import FeatureVector
+    h = job.host
+    _, _, node, off, feat = O.transform(vocab, h["desc"], 4)
+    fv = FeatureVector.from_csr(node, off, feat)
+    O.compute_distinctive_descriptors(h["obs_desc"], h["obs_off"])
+    n_new = 0
+    for j, nb in enumerate(h["neighbours"]):
+        m12, _ = O.search_for_triangulation(h["kf"]["frame"], h["kf"]["has_mp"], fv, nb["frame"], nb["has_mp"], nb["fv"],
+                                            job.F12[j].reshape(3, 3), False, False)
+        idx1 = np.nonzero(m12 >= 0)[0].astype(np.int32)
+        if len(idx1):
+            idx2 = np.ascontiguousarray(m12[idx1], np.int32)
+            x3d = np.zeros((len(idx1), 3), np.float32)
+            ok = np.zeros(len(idx1), np.uint8)
+            check("orbmi_triangulate_matches", lib().orbmi_triangulate_matches(
+                C_.addressof(job.kf.tri), C_.addressof(job.neighbours[j].tri), idx1.ctypes.data, idx2.ctypes.data,
+                len(idx1), x3d.ctypes.data, ok.ctypes.data))
+            n_new += int(ok.sum())
+    for nb in h["neighbours"]:
+        O.fuse_search(nb["frame"], h["kf_points"], None, 3.0)
+    O.fuse_search(h["kf"]["frame"], h["target_points"], None, 3.0)
+    O.compute_distinctive_descriptors(h["obs_desc"], h["obs_off"])
+    O.local_ba(job.problem)
+    return n_new
+
+
 def run_track(a, rank, world, local, dist):
     from orb_slam2_with_comment_amd import synth_map as SM
     from orb_slam2_with_comment_amd.pipeline import LocalMapper, StreamExchange
@@ -174,6 +255,13 @@ def run_track(a, rank, world, local, dist):
     # ahead, and the LocalMapping thread waits for it)
     mapper = LocalMapper(local, vocabulary=voc)
     kf_desc = lambda f: (S["keep"][1][f].data_ptr(), S["n_lf"][f])  # noqa: E731  (the keyframe's descriptors)
+    # the whole LocalMapping::Run body per keyframe (ProcessNewKeyFrame, CreateNewMapPoints,
+    # SearchInNeighbors, LocalBundleAdjustment); --lm-chain bow-ba keeps round 2's ComputeBoW + LocalBA
+    jobs, S["lm_keep"] = setup_local_mapping(S, voc, vocab, rank, problem)
+    S["jobs"] = jobs
+    full_chain = a.lm_chain == "full"
+    keyframe = (lambda f: mapper.insert_keyframe(jobs[f])) if full_chain else \
+        (lambda f: mapper.insert_keyframe(problem, kf_desc(f)))
     xch = StreamExchange(tr, dist, local) if dist is not None else None  # config 4
     ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)        # extraction (E)
     trk = torch.cuda.ExternalStream(tr.track_stream_handle, device=tr.kps.device)  # tracking (T)
@@ -185,7 +273,7 @@ def run_track(a, rank, world, local, dist):
         if xch is not None:  # config 4: exchange left features, match against the other streams
             xch.exchange()
         if i % KF_EVERY == 0:
-            mapper.insert_keyframe(problem, kf_desc(f))
+            keyframe(f)
 
     def sync():
         tr.synchronize()
@@ -197,12 +285,13 @@ def run_track(a, rank, world, local, dist):
     for i in range(a.warmup):
         step(i)
     sync()
-    # one keyframe alone (ComputeBoW + LocalBA): its latency on an otherwise idle GPU
+    # one keyframe alone (the LocalMapping chain): its latency on an otherwise idle GPU
     t0 = time.perf_counter()
-    mapper.insert_keyframe(problem, kf_desc(2))
+    keyframe(2)
     mapper.wait()
     lba_ms = (time.perf_counter() - t0) * 1e3
     lba_info = mapper.last
+    chain_info = mapper.last_chain if full_chain else None
     t0 = time.perf_counter()
     for _ in range(10):
         b = mapper.bow
@@ -307,8 +396,13 @@ def run_track(a, rank, world, local, dist):
                             "+ ComputeStereoMatches + TrackWithMotionModel [SearchByProjection(CF,LF,th=7), "
                             "PoseOptimization] + TrackLocalMap [SearchLocalPoints(th=1, "
                             f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
-                            "+ KeyFrame::ComputeBoW + LocalBundleAdjustment(config 3) "
-                            f"every {KF_EVERY}th frame on the concurrent LocalMapping thread"
+                            + (f"+ LocalMapping::Run every {KF_EVERY}th frame on the concurrent LocalMapping thread "
+                               "[ProcessNewKeyFrame: KeyFrame::ComputeBoW + ComputeDistinctiveDescriptors; "
+                               "CreateNewMapPoints: SearchForTriangulation x9 neighbours + host triangulation; "
+                               "SearchInNeighbors: Fuse x9 targets + Fuse(KF, targets' points) + "
+                               "ComputeDistinctiveDescriptors; LocalBundleAdjustment(config 3)]" if full_chain else
+                               "+ KeyFrame::ComputeBoW + LocalBundleAdjustment(config 3) "
+                               f"every {KF_EVERY}th frame on the concurrent LocalMapping thread")
                             + ("; + RCCL all-gather of left desc/kps and cross-stream matching (config 4)"
                                if world > 1 else ""),
                 "frames_resident": F, "parallelism": f"one stereo stream per GPU x{world}",
@@ -325,7 +419,9 @@ def run_track(a, rank, world, local, dist):
             "host_enqueue_ms_per_frame": round(enqueue_ms, 4),
             "compute_bow": {"us_per_keyframe_synced": round(bow_us, 1), "words": bow_words,
                             "vocabulary": "synthetic k=10 L=6 (1,111,111 nodes), L1 / TF-IDF, levelsup 4"},
-            "local_ba": {"ms_per_keyframe_idle_gpu (ComputeBoW + LocalBA)": round(lba_ms, 3), "calls_in_timed_region": n_lba,
+            "local_mapping": {"ms_per_keyframe_idle_gpu": round(lba_ms, 3), "chain": a.lm_chain,
+                              "keyframes_in_timed_region": n_lba, "last_keyframe": chain_info},
+            "local_ba": {"calls_in_timed_region": n_lba,
                          "iterations": list(lba_info["iterations"]) if lba_info else None,
                          "edges": int(len(problem.edges)), "points": int(len(problem.pts)),
                          "keyframes": int(len(problem.kfs))},
@@ -518,8 +614,11 @@ def cpu_baseline_track(S, problem, a):
         u, d = O.stereo(p, L, R, cam.bf, cam.fx, kl, dl, kr, dr)
         cf = Frame(kl, dl, u, S["tcws"][f], cam)
         O.track_frame(cf, lf_frames[f - 1], lf_points[f - 1], mps[f], inv_sigma2, 7.0)
-        if n % KF_EVERY == 0:  # LocalMapping: KeyFrame::ComputeBoW, then LocalBundleAdjustment
-            futs.append(lm.submit(lambda dl_=dl: (O.transform(S["vocab"], dl_, 4), O.local_ba(problem))))
+        if n % KF_EVERY == 0:  # LocalMapping::Run for the new keyframe (the GPU bench's chain)
+            if a.lm_chain == "full":
+                futs.append(lm.submit(cpu_local_mapping, O, S["vocab"], S["jobs"][f]))
+            else:
+                futs.append(lm.submit(lambda dl_=dl: (O.transform(S["vocab"], dl_, 4), O.local_ba(problem))))
         n += 1
         el = time.perf_counter() - t0
         if (el >= a.cpu_sample_s and n >= KF_EVERY) or n >= 10000:
@@ -532,7 +631,9 @@ def cpu_baseline_track(S, problem, a):
     return {"value": round(n / el, 4), "unit": "frames/s", "cores": 3, "kind": "port",
             "sample": f"{n} tracked frames (same synthetic frames, local maps and BA graph), oracle (-O3 "
                       f"-march=native) extract L||R (2 threads) + stereo + TrackWithMotionModel + TrackLocalMap "
-                      f"(both PoseOptimizations) serial, {len(futs)} ComputeBoW + LocalBA on a 3rd thread; {el:.1f} s",
+                      f"(both PoseOptimizations) serial, {len(futs)} LocalMapping keyframes "
+                      f"({'full LocalMapping::Run chain' if a.lm_chain == 'full' else 'ComputeBoW + LocalBA'}) "
+                      f"on a 3rd thread; {el:.1f} s",
             "cpu": O.cpu_model()}
 
 

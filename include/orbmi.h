@@ -235,6 +235,18 @@ int orbmi_search_for_triangulation(orbmi_matcher* m, const orbmi_frame_view* KF1
                                    const orbmi_feature_vector* fv2, const float* F12, int only_stereo, int check_ori,
                                    int32_t* match12, int* nmatches);
 
+/* SearchForTriangulation of one keyframe against npairs neighbours in one launch, as
+ * LocalMapping::CreateNewMapPoints calls it in its loop over the best covisible keyframes
+ * (src/LocalMapping.cc:326-384): pair j is (KF1, KF2[j]) with has_mp2[j], fv2[j] and
+ * F12[9 j .. 9 j + 8]; its matches go to match12[j * KF1.n .. (j + 1) * KF1.n) and, when nmatches
+ * is not NULL, its count to nmatches[j] (host, synchronises).  Per pair identical to
+ * orbmi_search_for_triangulation; asynchronous when match12 is device memory and nmatches NULL. */
+int orbmi_search_for_triangulation_batch(orbmi_matcher* m, const orbmi_frame_view* KF1, const uint8_t* has_mp1,
+                                         const orbmi_feature_vector* fv1, int npairs, const orbmi_frame_view* KF2,
+                                         const uint8_t* const* has_mp2, const orbmi_feature_vector* fv2,
+                                         const float* F12, int only_stereo, int check_ori, int32_t* match12,
+                                         int* nmatches);
+
 /* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th)
  * (src/ORBmatcher.cc:977-1127), its search: for each of the n_mp candidate map points (in
  * vpMapPoints order; NULL entries left out by the caller, isBad() as ORBMI_MP_BAD, in_kf[i] =
@@ -249,6 +261,15 @@ int orbmi_search_for_triangulation(orbmi_matcher* m, const orbmi_frame_view* KF1
  * the replay skips none). */
 int orbmi_fuse_search(orbmi_matcher* m, const orbmi_frame_view* KF, const orbmi_mappoint* mps, const uint8_t* in_kf,
                       int n_mp, float th, int32_t* best_idx, int32_t* best_dist, int* ncandidates);
+
+/* The search of Fuse(pKFi, vpMapPointMatches) for every target keyframe of SearchInNeighbors
+ * (src/LocalMapping.cc:631-641) in one launch: the same n_mp candidates against each of the nkf
+ * keyframes kfs[k]; keyframe k's results at best_idx / best_dist[k * n_mp ..) (in_kf, when not
+ * NULL, likewise nkf x n_mp) and its candidate count at ncandidates[k] (host, synchronises; may
+ * be NULL).  Per keyframe identical to orbmi_fuse_search. */
+int orbmi_fuse_search_batch(orbmi_matcher* m, int nkf, const orbmi_frame_view* kfs, const orbmi_mappoint* mps,
+                            const uint8_t* in_kf, int n_mp, float th, int32_t* best_idx, int32_t* best_dist,
+                            int* ncandidates);
 
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for np map points: the
  * observation descriptors of point p are rows obs_off[p] .. obs_off[p + 1] - 1 of obs_desc

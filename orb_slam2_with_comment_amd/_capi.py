@@ -89,6 +89,8 @@ _PROTOS = {
     "orbmi_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_fuse_search": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, _vp, C.POINTER(_i)]),
     "orbmi_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, C.POINTER(_i)]),
+    "orbmi_search_for_triangulation_batch": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
+    "orbmi_fuse_search_batch": (_i, [_vp, _i, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp]),
     "orbmi_pose_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_pose_optimization_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "orbmi_search_by_projection_last_frame_if": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _i]),

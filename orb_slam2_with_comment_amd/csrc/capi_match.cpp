@@ -9,6 +9,8 @@
 using orbmi::DevFrame;
 using orbmi::DevFV;
 using orbmi::Matcher;
+using orbmi::FuseKF;
+using orbmi::TriPair;
 
 struct orbmi_matcher {
     Matcher m;
@@ -20,6 +22,7 @@ namespace orbmi {
 
 void* Matcher::stage(size_t bytes) {
     bytes = (bytes + 255) & ~(size_t)255;
+    std::vector<Block>& arena = gens[gen].blocks;
     for (Block& b : arena)
         if (b.size - b.used >= bytes) { void* p = b.p + b.used; b.used += bytes; return p; }
     Block b{nullptr, std::max(bytes, (size_t)(4 << 20)), 0};
@@ -30,21 +33,43 @@ void* Matcher::stage(size_t bytes) {
 }
 
 void Matcher::arena_reset() {
-    // a previous asynchronous call may still read staged inputs: order behind it
+    // the generation just used may still be read by the work enqueued so far: mark it with an
+    // event, move on, and wait only for the generation about to be reused
     bool used = false;
-    for (Block& b : arena) used |= b.used > 0;
-    if (used) (void)hipStreamSynchronize(stream);
-    for (Block& b : arena) b.used = 0;
+    for (Block& b : gens[gen].blocks) used |= b.used > 0;
+    if (used) {
+        if (!gens[gen].ev && hipEventCreateWithFlags(&gens[gen].ev, hipEventDisableTiming) != hipSuccess) {
+            gens[gen].ev = nullptr;
+            (void)hipStreamSynchronize(stream);  // no event: fall back to a full wait
+        } else if (gens[gen].ev) {
+            (void)hipEventRecord(gens[gen].ev, stream);
+            gens[gen].pending = true;
+        }
+        gen = (gen + 1) % kArenaGens;
+    }
+    Gen& g = gens[gen];
+    if (g.pending) {
+        (void)hipEventSynchronize(g.ev);
+        g.pending = false;
+    }
+    for (Block& b : g.blocks) b.used = 0;
 }
 
 void Matcher::release() {
     (void)hipSetDevice(device);
     if (own_stream && stream) (void)hipStreamSynchronize(stream);
-    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_cand, d_ncand, d_top, d_res, d_bin_of, d_hist, d_scalars, d_track};
+    if (!own_stream && stream) (void)hipStreamSynchronize(stream);  // staged inputs may still be read
+    void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_mcell_start, d_mcell_list, d_mkp_cell, d_cand, d_ncand, d_top,
+                    d_res, d_bin_of, d_hist, d_scalars, d_track};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    for (Block& b : arena) (void)hipFree(b.p);
-    arena.clear();
+    for (Gen& g : gens) {
+        for (Block& b : g.blocks) (void)hipFree(b.p);
+        g.blocks.clear();
+        if (g.ev) (void)hipEventDestroy(g.ev);
+        g.ev = nullptr;
+        g.pending = false;
+    }
     if (stream && own_stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
 }
@@ -146,12 +171,12 @@ int make_fv(Matcher& m, const orbmi_feature_vector* v, DevFV* d) {
     int rc = 0;
     d->nnodes = v->nnodes;
     if (v->nnodes == 0) { d->node_id = nullptr; d->off = nullptr; d->feat = nullptr; return ORBMI_OK; }
-    // total features = off[nnodes]
+    // total features = off[nnodes], needed only to stage a host feature list (a device one is
+    // used in place: no read-back)
     int total = 0;
-    if (on_device(v->off)) {
-        ORBMI_HIP(hipMemcpy(&total, v->off + v->nnodes, sizeof(int), hipMemcpyDeviceToHost));
-    } else {
-        total = v->off[v->nnodes];
+    if (!on_device(v->feat)) {
+        if (on_device(v->off)) ORBMI_HIP(hipMemcpy(&total, v->off + v->nnodes, sizeof(int), hipMemcpyDeviceToHost));
+        else total = v->off[v->nnodes];
     }
     d->node_id = dev_in(m, v->node_id, (size_t)v->nnodes, &rc);
     d->off = dev_in(m, v->off, (size_t)v->nnodes + 1, &rc);
@@ -461,32 +486,65 @@ int orbmi_search_for_triangulation(orbmi_matcher* h, const orbmi_frame_view* kf1
                                    const orbmi_feature_vector* fv1, const orbmi_frame_view* kf2, const uint8_t* has_mp2,
                                    const orbmi_feature_vector* fv2, const float* F12, int only_stereo, int check_ori,
                                    int32_t* match12, int* nmatches) {
-    if (!h || !has_mp1 || !has_mp2 || !F12 || !match12 || !kf1 || !kf2 || !kf1->u_right || !kf2->u_right)
+    if (!kf2 || !has_mp2 || !fv2 || !F12) return ORBMI_E_ARG;
+    const uint8_t* mp2[1] = {has_mp2};
+    return orbmi_search_for_triangulation_batch(h, kf1, has_mp1, fv1, 1, kf2, mp2, fv2, F12, only_stereo, check_ori,
+                                                match12, nmatches);
+}
+
+int orbmi_search_for_triangulation_batch(orbmi_matcher* h, const orbmi_frame_view* kf1, const uint8_t* has_mp1,
+                                         const orbmi_feature_vector* fv1, int npairs, const orbmi_frame_view* kf2,
+                                         const uint8_t* const* has_mp2, const orbmi_feature_vector* fv2,
+                                         const float* F12, int only_stereo, int check_ori, int32_t* match12,
+                                         int* nmatches) {
+    if (!h || !has_mp1 || !fv1 || !kf1 || !kf1->u_right || npairs < 0 || (npairs > 0 && (!kf2 || !has_mp2 || !fv2 ||
+                                                                                      !F12 || !match12)))
         return ORBMI_E_ARG;
+    if (npairs == 0) return ORBMI_OK;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
-    DevFrame K1, K2;
-    DevFV f1, f2;
+    DevFrame K1;
+    DevFV f1;
     int rc;
     if ((rc = make_frame(m, kf1, &K1, true))) return rc;
-    if ((rc = make_frame(m, kf2, &K2, true))) return rc;
     if ((rc = make_fv(m, fv1, &f1))) return rc;
-    if ((rc = make_fv(m, fv2, &f2))) return rc;
     const uint8_t* d_mp1 = dev_in(m, has_mp1, (size_t)std::max(K1.n, 1), &rc);
-    const uint8_t* d_mp2 = dev_in(m, has_mp2, (size_t)std::max(K2.n, 1), &rc);
     if (rc) return rc;
-    float F[9];
-    if (on_device(F12)) ORBMI_HIP(hipMemcpy(F, F12, sizeof(F), hipMemcpyDeviceToHost));
-    else memcpy(F, F12, sizeof(F));
-    if ((rc = scalars(m))) return rc;
+    std::vector<TriPair> pairs(npairs);
+    const bool F_dev = on_device(F12);
+    std::vector<float> Fh((size_t)9 * npairs);
+    if (F_dev) ORBMI_HIP(hipMemcpy(Fh.data(), F12, Fh.size() * sizeof(float), hipMemcpyDeviceToHost));
+    else memcpy(Fh.data(), F12, Fh.size() * sizeof(float));
+    int* d_counts = nullptr;
+    if (nmatches) d_counts = (int*)m.stage((size_t)npairs * sizeof(int));
+    for (int j = 0; j < npairs; j++) {
+        TriPair& P = pairs[j];
+        memset(&P, 0, sizeof(P));
+        if (!kf2[j].u_right || !has_mp2[j]) return ORBMI_E_ARG;
+        if ((rc = make_frame(m, &kf2[j], &P.KF2, true))) return rc;
+        if ((rc = make_fv(m, &fv2[j], &P.fv2))) return rc;
+        P.has_mp2 = dev_in(m, has_mp2[j], (size_t)std::max(P.KF2.n, 1), &rc);
+        if (rc) return rc;
+        for (int q = 0; q < 9; q++) P.F12.m[q] = Fh[9 * j + q];
+        P.nmatches = d_counts ? d_counts + j : nullptr;
+    }
+    TriPair* d_pairs = (TriPair*)m.stage(sizeof(TriPair) * npairs);
     std::vector<OutBuf> outs;
-    int* d_out = dev_out(m, match12, (size_t)K1.n, outs);
-    if ((rc = orbmi::launch_triangulation(m, K1, d_mp1, f1, K2, d_mp2, f2, F, only_stereo, check_ori, d_out,
-                                          m.d_scalars)))
+    int* d_out = dev_out(m, match12, (size_t)K1.n * npairs, outs);
+    if (!d_pairs || !d_out) return ORBMI_E_HIP;
+    if ((rc = orbmi::launch_triangulation(m, K1, d_mp1, f1, npairs, pairs.data(), d_pairs, only_stereo, check_ori,
+                                          d_out)))
         return rc;
-    ORBMI_HIP(hipGetLastError());
-    return finish(m, outs, m.d_scalars, nmatches);
+    bool wait = false;
+    for (OutBuf& o : outs)
+        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
+    if (nmatches) {
+        ORBMI_HIP(hipMemcpyAsync(nmatches, d_counts, (size_t)npairs * sizeof(int), hipMemcpyDeviceToHost, m.stream));
+        wait = true;
+    }
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    return ORBMI_OK;
 }
 
 int orbmi_fuse_search(orbmi_matcher* h, const orbmi_frame_view* kf, const orbmi_mappoint* mps, const uint8_t* in_kf,
@@ -507,6 +565,43 @@ int orbmi_fuse_search(orbmi_matcher* h, const orbmi_frame_view* kf, const orbmi_
     int* d_bd = dev_out(m, best_dist, (size_t)n_mp, outs);
     if ((rc = orbmi::launch_fuse(m, F, d_mps, d_in, n_mp, th, d_bi, d_bd, m.d_scalars))) return rc;
     return finish(m, outs, m.d_scalars, ncandidates);
+}
+
+int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* kfs, const orbmi_mappoint* mps,
+                            const uint8_t* in_kf, int n_mp, float th, int32_t* best_idx, int32_t* best_dist,
+                            int* ncandidates) {
+    if (!h || nkf < 0 || n_mp < 0 || (nkf > 0 && !kfs) || (nkf > 0 && n_mp > 0 && (!mps || !best_idx || !best_dist)))
+        return ORBMI_E_ARG;
+    if (nkf == 0) return ORBMI_OK;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    int rc = 0;
+    std::vector<FuseKF> K(nkf);
+    const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
+    const uint8_t* d_in = dev_in(m, in_kf, in_kf ? (size_t)std::max(n_mp, 1) * nkf : 0, &rc);
+    if (rc) return rc;
+    for (int k = 0; k < nkf; k++) {
+        memset(&K[k], 0, sizeof(FuseKF));
+        if ((rc = make_frame(m, &kfs[k], &K[k].F, true))) return rc;
+        K[k].in_kf = d_in ? d_in + (size_t)k * n_mp : nullptr;
+    }
+    FuseKF* d_k = (FuseKF*)m.stage(sizeof(FuseKF) * nkf);
+    int* d_cnt = (int*)m.stage(sizeof(int) * nkf);
+    std::vector<OutBuf> outs;
+    int* d_bi = dev_out(m, best_idx, (size_t)n_mp * nkf, outs);
+    int* d_bd = dev_out(m, best_dist, (size_t)n_mp * nkf, outs);
+    if (!d_k || !d_cnt) return ORBMI_E_HIP;
+    if ((rc = orbmi::launch_fuse_multi(m, nkf, K.data(), d_k, d_mps, n_mp, th, d_bi, d_bd, d_cnt))) return rc;
+    bool wait = false;
+    for (OutBuf& o : outs)
+        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
+    if (ncandidates) {
+        ORBMI_HIP(hipMemcpyAsync(ncandidates, d_cnt, sizeof(int) * nkf, hipMemcpyDeviceToHost, m.stream));
+        wait = true;
+    }
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    return ORBMI_OK;
 }
 
 }  // extern "C"

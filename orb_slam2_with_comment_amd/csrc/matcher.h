@@ -45,6 +45,32 @@ struct DevFV {
     const int32_t* feat;
 };
 
+struct Mat3f { float m[9]; };  // row-major 3x3 (by value)
+
+// One (KF1, KF2) pair of SearchForTriangulation, read by the kernels from device memory so that
+// one launch serves all of a keyframe's neighbours (grid row = pair)
+struct TriPair {
+    DevFrame KF2;
+    const uint8_t* has_mp2;
+    DevFV fv2;
+    Mat3f F12;
+    int* match;     // KF1.n entries
+    int* bin_of;    // KF1.n entries (rotation bins)
+    int* hist;      // HISTO_LENGTH
+    int* nmatches;  // one int (may be null)
+};
+
+// One keyframe of a batched Fuse search (grid row = keyframe): its frame, grid and outputs
+struct FuseKF {
+    DevFrame F;
+    const int* cs;          // cell_start (kGridCells + 1)
+    const int* cl;          // cell_list
+    const uint8_t* in_kf;   // IsInKeyFrame per candidate (may be null)
+    int* best_idx;          // n candidates
+    int* best_dist;
+    int* ncand;             // one int
+};
+
 struct Matcher {
     static constexpr int kCandCap = 96;  // candidates kept per query; overflow re-enumerates
     int device = 0;
@@ -54,6 +80,10 @@ struct Matcher {
     int* d_cell_start = nullptr; size_t cap_cell_start = 0;
     int* d_cell_list = nullptr; size_t cap_cell_list = 0;
     int* d_kp_cell = nullptr; size_t cap_kp_cell = 0;
+    // grids of several keyframes (batched Fuse)
+    int* d_mcell_start = nullptr; size_t cap_mcell_start = 0;
+    int* d_mcell_list = nullptr; size_t cap_mcell_list = 0;
+    int* d_mkp_cell = nullptr; size_t cap_mkp_cell = 0;
     // grid pinned to one frame by orbmi_matcher_assign_features_to_grid (device keypoints only):
     // searches on that frame skip the rebuild until the pin is released or another frame's grid
     // is built
@@ -71,9 +101,15 @@ struct Matcher {
     int* d_hist = nullptr; size_t cap_hist = 0;
     int* d_scalars = nullptr; size_t cap_scalars = 0;   // small per-call outputs
     orbmi_mappoint_track* d_track = nullptr; size_t cap_track = 0;  // fused frustum output
-    // staging arena for host inputs/outputs (reset per call)
+    // staging arena for host inputs/outputs, in kArenaGens generations: each call stages into
+    // the next generation, and waits only when that generation's last use (an event recorded
+    // when the call after it began) has not finished -- so back-to-back asynchronous calls with
+    // host inputs do not serialise on the host
+    static constexpr int kArenaGens = 4;
     struct Block { uint8_t* p; size_t size, used; };
-    std::vector<Block> arena;
+    struct Gen { std::vector<Block> blocks; hipEvent_t ev = nullptr; bool pending = false; };
+    Gen gens[kArenaGens];
+    int gen = 0;
     void* stage(size_t bytes);
     void arena_reset();
     void release();
@@ -92,11 +128,12 @@ int launch_track_update(Matcher& m, const DevFrame& F, int stage, const uint8_t*
                         int n_mp, uint8_t* occ_out, int* counts);
 int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV& kfv, const DevFrame& F,
                const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
-int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1,
-                         const DevFrame& KF2, const uint8_t* has_mp2, const DevFV& fv2, const float* F12,
-                         int only_stereo, int check_ori, int* match, int* nmatches);
+int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
+                         TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match);
 int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
                 int* best_idx, int* best_dist, int* ncand);
+int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, const orbmi_mappoint* mps, int n,
+                      float th, int* best_idx, int* best_dist, int* ncand);
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
                   int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches);

@@ -30,7 +30,6 @@ namespace orbmi {
 constexpr int kGridCols = 64, kGridRows = 48, kGridCells = kGridCols * kGridRows;
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
 
-struct Mat3f { float m[9]; };  // row-major 3x3 (by value)
 
 __device__ inline int popc_desc(const uint8_t* a, const uint8_t* b) {
     const uint4* x = reinterpret_cast<const uint4*>(a);
@@ -39,10 +38,8 @@ __device__ inline int popc_desc(const uint8_t* a, const uint8_t* b) {
 }
 
 // -------------------------------------------------------------------------- grid
-__global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict__ cell_start,
-                                                     int* __restrict__ cell_list, int* __restrict__ kp_cell,
-                                                     const int* gate, int gate_min) {
-    if (gate && *gate >= gate_min) return;
+__device__ inline void grid_build_block(const DevFrame& F, int* __restrict__ cell_start, int* __restrict__ cell_list,
+                                        int* __restrict__ kp_cell) {
     __shared__ int cnt[kGridCells + 1];
     __shared__ int scratch[20];
     const int tid = threadIdx.x;
@@ -69,6 +66,20 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict
         const int c = kp_cell[i];
         if (c >= 0) cell_list[atomicAdd(&cnt[c], 1)] = i;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict__ cell_start,
+                                                     int* __restrict__ cell_list, int* __restrict__ kp_cell,
+                                                     const int* gate, int gate_min) {
+    if (gate && *gate >= gate_min) return;
+    grid_build_block(F, cell_start, cell_list, kp_cell);
+}
+
+// the grids of several keyframes (one workgroup each; keyframe k's arrays at k * stride)
+__global__ __launch_bounds__(1024) void k_grid_build_multi(const FuseKF* __restrict__ kfs, int* __restrict__ kp_cell,
+                                                           int ncap) {
+    const FuseKF& K = kfs[blockIdx.x];
+    grid_build_block(K.F, const_cast<int*>(K.cs), const_cast<int*>(K.cl), kp_cell + (size_t)blockIdx.x * ncap);
 }
 
 // Frame::GetFeaturesInArea (src/Frame.cc:353-410): calls fn(idx) for every keypoint in the
@@ -743,9 +754,11 @@ __global__ __launch_bounds__(256) void k_bow_match(DevFrame KF, const uint8_t* _
     }
 }
 
-__global__ __launch_bounds__(1024) void k_bow_finalize(DevFrame F, int check_ori, const int* __restrict__ hist,
-                                                       const int* __restrict__ bin_of, int* __restrict__ match,
-                                                       int* __restrict__ nmatches) {
+// rotation-histogram filter (ComputeThreeMaxima, src/ORBmatcher.cc:1854-1895) of one search's
+// matches and their count, one workgroup
+__device__ inline void finalize_block(int n, int check_ori, const int* __restrict__ hist,
+                                      const int* __restrict__ bin_of, int* __restrict__ match,
+                                      int* __restrict__ nmatches) {
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
@@ -761,7 +774,6 @@ __global__ __launch_bounds__(1024) void k_bow_finalize(DevFrame F, int check_ori
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
     }
-    const int n = frame_n(F);
     int local = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         if (match[i] < 0) continue;
@@ -773,7 +785,13 @@ __global__ __launch_bounds__(1024) void k_bow_finalize(DevFrame F, int check_ori
     }
     atomicAdd(&cnt, local);
     __syncthreads();
-    if (threadIdx.x == 0) *nmatches = cnt;
+    if (threadIdx.x == 0 && nmatches) *nmatches = cnt;
+}
+
+__global__ __launch_bounds__(1024) void k_bow_finalize(DevFrame F, int check_ori, const int* __restrict__ hist,
+                                                       const int* __restrict__ bin_of, int* __restrict__ match,
+                                                       int* __restrict__ nmatches) {
+    finalize_block(frame_n(F), check_ori, hist, bin_of, match, nmatches);
 }
 
 
@@ -993,16 +1011,20 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
 // CheckDistEpipolarLine (:173-196) compares in double (3.84 * sigma2); the epipole and the
 // keyframe-1 centre follow the P10 float order.  The rotation histogram is k_bow_finalize's.
 __global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* __restrict__ has_mp1, DevFV fv1,
-                                                   DevFrame KF2, const uint8_t* __restrict__ has_mp2, DevFV fv2,
-                                                   Mat3f F12, int only_stereo, int check_ori, int* __restrict__ match,
-                                                   int* __restrict__ bin_of, int* __restrict__ hist) {
+                                                   const TriPair* __restrict__ pairs, int only_stereo, int check_ori) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int a = blockIdx.x * 4 + wid;
     if (a >= fv1.nnodes) return;
+    const TriPair& P = pairs[blockIdx.y];  // the pair (KF1, KF2 = P.KF2) of this grid row
+    const DevFV fv2 = P.fv2;
+    const uint8_t* __restrict__ has_mp2 = P.has_mp2;
+    int* __restrict__ match = P.match;
     const unsigned id = fv1.node_id[a];
     int lo = 0, hi = fv2.nnodes;  // lower_bound
     while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv2.node_id[mid] < id) lo = mid + 1; else hi = mid; }
     if (lo >= fv2.nnodes || fv2.node_id[lo] != id) return;
+    const DevFrame& KF2 = P.KF2;
+    const Mat3f F12 = P.F12;
     const int f0 = fv2.off[lo], nf = fv2.off[lo + 1] - f0;
     // epipole of KF1's centre in KF2
     const Pose34 T1 = frame_pose(KF1), T2 = frame_pose(KF2);
@@ -1056,29 +1078,40 @@ __global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* 
             match[idx1] = idx2;
             if (check_ori) {
                 const int bin = rot_bin(kp1.angle, KF2.keys[idx2].angle);
-                bin_of[idx1] = bin;
-                atomicAdd(&hist[bin], 1);
+                P.bin_of[idx1] = bin;
+                atomicAdd(&P.hist[bin], 1);
             }
         }
     }
 }
 
-int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1,
-                         const DevFrame& KF2, const uint8_t* has_mp2, const DevFV& fv2, const float* F12,
-                         int only_stereo, int check_ori, int* match, int* nmatches) {
+// one workgroup per pair: the rotation histogram and the count of SearchForTriangulation
+__global__ __launch_bounds__(1024) void k_tri_finalize(int n1, const TriPair* __restrict__ pairs, int check_ori) {
+    const TriPair& P = pairs[blockIdx.x];
+    finalize_block(n1, check_ori, P.hist, P.bin_of, P.match, P.nmatches);
+}
+
+int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
+                         TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
+    if (npairs <= 0) return ORBMI_OK;
+    const size_t n1 = (size_t)std::max(KF1.n, 1);
     int rc;
-    if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, (size_t)std::max(KF1.n, 1)))) return rc;
-    if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH))) return rc;
-    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, HISTO_LENGTH * sizeof(int), m.stream));
-    ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)std::max(KF1.n, 1) * sizeof(int), m.stream));
-    Mat3f F;
-    for (int q = 0; q < 9; q++) F.m[q] = F12[q];
+    if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, n1 * npairs))) return rc;
+    if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH * npairs))) return rc;
+    // per-pair scratch and outputs: match rows are consecutive (pair j at match + j * KF1.n)
+    for (int j = 0; j < npairs; j++) {
+        pairs_host[j].match = match + (size_t)j * KF1.n;
+        pairs_host[j].bin_of = m.d_bin_of + (size_t)j * n1;
+        pairs_host[j].hist = m.d_hist + (size_t)j * HISTO_LENGTH;
+    }
+    ORBMI_HIP(hipMemcpyAsync(pairs_dev, pairs_host, sizeof(TriPair) * npairs, hipMemcpyHostToDevice, m.stream));
+    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
+    if (KF1.n > 0) ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)KF1.n * npairs * sizeof(int), m.stream));
     if (fv1.nnodes > 0)
-        hipLaunchKernelGGL(k_tri_match, dim3((fv1.nnodes + 3) / 4), dim3(256), 0, m.stream, KF1, has_mp1, fv1, KF2, has_mp2,
-                           fv2, F, only_stereo, check_ori, match, m.d_bin_of, m.d_hist);
-    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, KF1, check_ori, m.d_hist, m.d_bin_of, match,
-                       nmatches);
-    return ORBMI_OK;
+        hipLaunchKernelGGL(k_tri_match, dim3((fv1.nnodes + 3) / 4, npairs), dim3(256), 0, m.stream, KF1, has_mp1, fv1,
+                           pairs_dev, only_stereo, check_ori);
+    hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.stream, KF1.n, pairs_dev, check_ori);
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 
 // -------------------------------------------------------------------------- Fuse
@@ -1090,12 +1123,10 @@ int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1
 // the reference's grid order wins ties (key dist << 40 | cell << 20 | idx).  The map updates
 // (Replace / AddObservation) are the caller's sequential replay of (best_idx, best_dist) in
 // list order (include/orbmi.h).
-__global__ __launch_bounds__(256) void k_fuse(DevFrame F, const int* __restrict__ cs, const int* __restrict__ cl,
-                                              const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf,
-                                              int n, float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
-                                              int* __restrict__ ncand) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, const int* __restrict__ cl,
+                                const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf, int i,
+                                float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
+                                int* __restrict__ ncand) {
     int bi = -1, bd = 256;
     const orbmi_mappoint mp = mps[i];
     const Pose34 T = frame_pose(F);
@@ -1161,6 +1192,24 @@ __global__ __launch_bounds__(256) void k_fuse(DevFrame F, const int* __restrict_
     if (fused) atomicAdd(ncand, 1);
 }
 
+__global__ __launch_bounds__(256) void k_fuse(DevFrame F, const int* __restrict__ cs, const int* __restrict__ cl,
+                                              const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf,
+                                              int n, float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
+                                              int* __restrict__ ncand) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fuse_one(F, cs, cl, mps, in_kf, i, th, best_idx, best_dist, ncand);
+}
+
+// the same candidate list against several keyframes (grid row = keyframe)
+__global__ __launch_bounds__(256) void k_fuse_multi(const FuseKF* __restrict__ kfs, const orbmi_mappoint* __restrict__ mps,
+                                                    int n, float th) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const FuseKF& K = kfs[blockIdx.y];
+    fuse_one(K.F, K.cs, K.cl, mps, K.in_kf, i, th, K.best_idx, K.best_dist, K.ncand);
+}
+
 int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
                 int* best_idx, int* best_dist, int* ncand) {
     int rc;
@@ -1168,6 +1217,34 @@ int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const 
     if (n > 0)
         hipLaunchKernelGGL(k_fuse, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start, m.d_cell_list,
                            mps, in_kf, n, th, best_idx, best_dist, ncand);
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+}
+
+int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, const orbmi_mappoint* mps, int n,
+                      float th, int* best_idx, int* best_dist, int* ncand) {
+    if (nkf <= 0) return ORBMI_OK;
+    int ncap = 1;
+    for (int k = 0; k < nkf; k++) {
+        if (kfs_host[k].F.n > kGreedyMaxKp) return ORBMI_E_UNSUPPORTED;
+        ncap = std::max(ncap, kfs_host[k].F.n);
+    }
+    int rc;
+    if ((rc = ensure_buf(&m.d_mcell_start, &m.cap_mcell_start, (size_t)(kGridCells + 1) * nkf))) return rc;
+    if ((rc = ensure_buf(&m.d_mcell_list, &m.cap_mcell_list, (size_t)ncap * nkf))) return rc;
+    if ((rc = ensure_buf(&m.d_mkp_cell, &m.cap_mkp_cell, (size_t)ncap * nkf))) return rc;
+    for (int k = 0; k < nkf; k++) {
+        FuseKF& K = kfs_host[k];
+        K.cs = m.d_mcell_start + (size_t)k * (kGridCells + 1);
+        K.cl = m.d_mcell_list + (size_t)k * ncap;
+        K.best_idx = best_idx + (size_t)k * n;
+        K.best_dist = best_dist + (size_t)k * n;
+        K.ncand = ncand + k;
+    }
+    ORBMI_HIP(hipMemcpyAsync(kfs_dev, kfs_host, sizeof(FuseKF) * nkf, hipMemcpyHostToDevice, m.stream));
+    ORBMI_HIP(hipMemsetAsync(ncand, 0, sizeof(int) * nkf, m.stream));
+    hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.stream, kfs_dev, m.d_mkp_cell, ncap);
+    if (n > 0)
+        hipLaunchKernelGGL(k_fuse_multi, dim3((n + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n, th);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 

@@ -287,34 +287,105 @@ class StereoTracker:
         self.extractor.close()
 
 
+class KeyFrameData:
+    """One keyframe as LocalMapping's operators read it: device-resident keypoints (cv::KeyPoint
+    layout), descriptors and u_right for the GPU searches, host copies (keys, u_right, depth,
+    Tcw) for the host geometry of CreateNewMapPoints, has_mp (GetMapPoint(i) != NULL, device),
+    and, for a neighbour, its FeatureVector (host CSR)."""
+
+    def __init__(self, cam, scale_factors, level_sigma2, n, d_keys, d_desc, d_ur, d_has_mp, keys, ur, depth, tcw,
+                 fv=None):
+        from .types import TriKeyFrame
+        self.n = int(n)
+        self.tcw = np.ascontiguousarray(tcw, np.float32).reshape(4, 4)
+        self.keys = np.ascontiguousarray(keys)
+        self.ur = np.ascontiguousarray(ur, np.float32)
+        self.depth = np.ascontiguousarray(depth, np.float32)
+        self.d_has_mp = d_has_mp
+        self.fv = fv
+        self.sf = np.ascontiguousarray(scale_factors, np.float32)
+        self.sig2 = np.ascontiguousarray(level_sigma2, np.float32)
+        self.view = frame_view(self.n, d_keys, d_ur, d_desc, self.tcw, cam, self.sf, cam.width, cam.height)
+        self.tri = TriKeyFrame(self.tcw.ctypes.data, self.keys.ctypes.data, self.ur.ctypes.data, self.depth.ctypes.data,
+                               cam.fx, cam.fy, cam.cx, cam.cy, cam.bf, np.float32(np.float32(cam.bf) / np.float32(cam.fx)),
+                               self.sig2.ctypes.data, self.sf.ctypes.data)
+
+
+class LocalMappingJob:
+    """The inputs of one LocalMapping::Run iteration (src/LocalMapping.cc:47-128) for a new
+    keyframe: the keyframe (its descriptors for ComputeBoW), its covisible neighbours with their
+    FeatureVectors and F12 (CreateNewMapPoints / SearchInNeighbors targets), the keyframe's map
+    points and the targets' map points (orbmi_mappoint records, device) for the two Fuse
+    directions, the observation descriptors of the keyframe's map points for
+    ComputeDistinctiveDescriptors (device CSR), and the LocalBundleAdjustment problem."""
+
+    def __init__(self, kf, d_desc, neighbours, kf_points, target_points, obs, problem):
+        self.kf, self.d_desc, self.neighbours = kf, d_desc, neighbours
+        self.kf_points, self.target_points = kf_points, target_points  # (device address, count) each
+        self.obs = obs                                      # (d_obs_desc, d_obs_off, n_points)
+        self.problem = problem
+        self.F12 = []
+        for nb in neighbours:  # LocalMapping::ComputeF12 (src/LocalMapping.cc:676-693), host
+            F = np.zeros(9, np.float32)
+            check("orbmi_compute_f12", lib().orbmi_compute_f12(C.addressof(kf.tri), C.addressof(nb.tri), F.ctypes.data))
+            self.F12.append(F)
+
+
 class LocalMapper:
-    """LocalMapping thread: for every queued keyframe, KeyFrame::ComputeBoW (ProcessNewKeyFrame,
-    src/LocalMapping.cc:152-160) when a vocabulary is given, and LocalBundleAdjustment
-    (src/LocalMapping.cc:89-90), on the GPU on the handles' own streams, concurrently with
-    tracking (src/LocalMapping.cc:47-128).  The two are data-independent and overlap on the
-    device; the keyframe is done when both are."""
+    """LocalMapping thread (src/LocalMapping.cc:47-128), concurrent with tracking as in the
+    reference.  For every queued keyframe, in the reference's order, on the mapper's own GPU
+    streams:
+      ProcessNewKeyFrame    KeyFrame::ComputeBoW (DBoW2 transform) and
+                            MapPoint::ComputeDistinctiveDescriptors of the keyframe's points
+                            (:135-198)
+      CreateNewMapPoints    SearchForTriangulation(0.6, no orientation check) against every
+                            neighbour with its F12, then the host triangulation / acceptance
+                            geometry (orbmi_triangulate_matches) of the pairs (:290-577)
+      SearchInNeighbors     Fuse(neighbour, keyframe's points) for every target, Fuse(keyframe,
+                            targets' points), ComputeDistinctiveDescriptors again (:589-674)
+      LocalBundleAdjustment (:89-90)
+    The map updates of the replayed keyframes (new points, fusions) are not applied: each job is
+    self-contained, like the LocalBA problem it carries.  A job given as (problem, kf_desc) runs
+    only ComputeBoW + LocalBA (the round-2 chain)."""
 
     def __init__(self, device=0, vocabulary=None, max_features=8192):
         import torch
+        from .matcher import ORBmatcher
         from .optimizer import LocalBA
         self.device = device
         self.ba = LocalBA(device)
+        self.matcher = ORBmatcher(device=device)
         self.voc = vocabulary  # ORBVocabulary (device handle) or None
+        dev = torch.device("cuda", device)
+        cap = max_features
+        self.cap = cap
         if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
-            dev = torch.device("cuda", device)
-            cap = max_features
             self.bow = dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
                             value=torch.zeros(cap, dtype=torch.float64, device=dev),
                             node=torch.zeros(cap, dtype=torch.int32, device=dev),
                             off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
                             feat=torch.zeros(cap, dtype=torch.int32, device=dev),
                             counts=torch.zeros(2, dtype=torch.int32, device=dev))
+        self._dev = dev
+        self._bufs = {}
+        ms = _vp()
+        check("orbmi_matcher_get_stream", lib().orbmi_matcher_get_stream(self.matcher._h, C.byref(ms)))
+        self._ms = torch.cuda.ExternalStream(ms.value, device=dev)  # the mapper's search stream
         self.q: queue.Queue = queue.Queue()
         self.done = 0
         self.last = None
+        self.last_chain = None
         self.error = None
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
+
+    def _buf(self, name, shape, dtype):
+        import torch
+        b = self._bufs.get(name)
+        if b is None or b.numel() < int(np.prod(shape)) or b.dtype != dtype:
+            b = torch.empty(int(np.prod(shape)), dtype=dtype, device=self._dev)
+            self._bufs[name] = b
+        return b
 
     def _run(self):
         while True:
@@ -323,25 +394,105 @@ class LocalMapper:
                 self.q.task_done()
                 return
             try:
-                problem, kf_desc = job
-                if self.voc is not None and kf_desc is not None:
-                    d_desc, n = kf_desc
-                    b = self.bow
-                    self.voc.transform_device(d_desc, n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
-                                              b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
-                                              b["counts"].data_ptr())
-                    bow_done = self._bow_event()
-                # LocalBundleAdjustment reads poses, points and observations, never the BowVector,
-                # so the transform (vocabulary stream) and the LocalBA (its own stream) overlap;
-                # both are complete before the next keyframe is taken (an event, not a stream
-                # sync: the vocabulary may share the extraction stream, which runs ahead)
-                self.last = self.ba.run(problem)
-                if self.voc is not None and kf_desc is not None:
-                    bow_done.synchronize()
+                if isinstance(job, LocalMappingJob):
+                    self.last_chain = self.run_job(job)
+                else:
+                    self._bow_and_ba(*job)
                 self.done += 1
             except Exception as e:  # surfaced by wait()
                 self.error = e
             self.q.task_done()
+
+    def _bow_and_ba(self, problem, kf_desc):
+        if self.voc is not None and kf_desc is not None:
+            d_desc, n = kf_desc
+            b = self.bow
+            self.voc.transform_device(d_desc, n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                                      b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
+                                      b["counts"].data_ptr())
+            bow_done = self._bow_event()
+        # LocalBundleAdjustment reads poses, points and observations, never the BowVector, so
+        # the transform (vocabulary stream) and the LocalBA (its own stream) overlap
+        self.last = self.ba.run(problem)
+        if self.voc is not None and kf_desc is not None:
+            bow_done.synchronize()
+
+    def run_job(self, job: LocalMappingJob):
+        """One LocalMapping::Run iteration (see the class doc) -> counts of what it found."""
+        import torch
+        from .types import FeatureVector
+        L = lib()
+        m = self.matcher._h
+        kf = job.kf
+        out = {}
+        # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors)
+        b = self.bow
+        self.voc.transform_device(job.d_desc, kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                                  b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
+        self.voc.synchronize()
+        counts = b["counts"].cpu().numpy()  # mBowVec / mFeatVec sizes; the vectors stay in HBM
+        nn = int(counts[1])
+        out["bow_words"] = int(counts[0])
+        # ... and ComputeDistinctiveDescriptors of the keyframe's map points
+        d_obs, d_off, npts = job.obs
+        best = self._buf("best", (max(npts, 1),), torch.int32)
+        dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
+        check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
+            m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
+        # ---- CreateNewMapPoints: SearchForTriangulation against every neighbour, one launch
+        from .types import FeatureVectorView
+        nnb = len(job.neighbours)
+        tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
+        fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
+        if nnb:
+            kf2 = (FrameView * nnb)(*[nb.view for nb in job.neighbours])
+            mp2 = (C.c_void_p * nnb)(*[nb.d_has_mp for nb in job.neighbours])
+            fv2 = (FeatureVectorView * nnb)(*[nb.fv.view() for nb in job.neighbours])
+            F12 = np.ascontiguousarray(np.concatenate(job.F12), np.float32)
+            check("orbmi_search_for_triangulation_batch", L.orbmi_search_for_triangulation_batch(
+                m, C.addressof(kf.view), _vp(kf.d_has_mp), C.addressof(fv1), nnb, kf2, mp2, fv2, F12.ctypes.data, 0, 0,
+                _vp(tri.data_ptr()), None))
+        self._ms.synchronize()
+        tri_h = tri[:nnb * kf.n].cpu().numpy().reshape(nnb, kf.n)
+        n_pairs = n_new = 0
+        for j, nb in enumerate(job.neighbours):  # host geometry: triangulation + acceptance tests
+            idx1 = np.nonzero(tri_h[j] >= 0)[0].astype(np.int32)
+            if len(idx1) == 0:
+                continue
+            idx2 = np.ascontiguousarray(tri_h[j][idx1], np.int32)
+            x3d = np.zeros((len(idx1), 3), np.float32)
+            ok = np.zeros(len(idx1), np.uint8)
+            check("orbmi_triangulate_matches", L.orbmi_triangulate_matches(
+                C.addressof(kf.tri), C.addressof(nb.tri), idx1.ctypes.data, idx2.ctypes.data, len(idx1), x3d.ctypes.data,
+                ok.ctypes.data))
+            n_pairs += len(idx1)
+            n_new += int(ok.sum())
+        out["triangulation_pairs"], out["new_points"] = n_pairs, n_new
+        # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
+        d_kp, n_kp = job.kf_points
+        d_tp, n_tp = job.target_points
+        bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
+        bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
+        if nnb:
+            check("orbmi_fuse_search_batch", L.orbmi_fuse_search_batch(
+                m, nnb, kf2, _vp(d_kp), None, int(n_kp), 3.0, _vp(bi.data_ptr()), _vp(bd.data_ptr()), None))
+        o = nnb * n_kp
+        check("orbmi_fuse_search", L.orbmi_fuse_search(
+            m, C.addressof(kf.view), _vp(d_tp), None, int(n_tp), 3.0, _vp(bi.data_ptr() + 4 * o),
+            _vp(bd.data_ptr() + 4 * o), None))
+        # ComputeDistinctiveDescriptors + UpdateNormalAndDepth of the keyframe's points after fusion
+        check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
+            m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
+        self._ms.synchronize()
+        out["fuse_candidates"] = int((bi[:o + n_tp] >= 0).sum())
+        # ---- LocalBundleAdjustment
+        self.last = self.ba.run(job.problem)
+        out["local_ba_iterations"] = list(self.last["iterations"])
+        self._out = dict(tri=tri_h, best=best, dsc=dsc, bi=bi, bd=bd, n_fuse=o + n_tp,
+                         fv=lambda: FeatureVector.from_csr(b["node"][:nn].cpu().numpy().view(np.uint32),
+                                                           b["off"][:nn + 1].cpu().numpy(),
+                                                           b["feat"][:kf.n].cpu().numpy()))
+        return out
 
     def _bow_event(self):
         """Event recorded on the vocabulary's stream after the transform just enqueued."""
@@ -352,10 +503,13 @@ class LocalMapper:
         ev.record(torch.cuda.ExternalStream(s.value, device=torch.device("cuda", self.device)))
         return ev
 
-    def insert_keyframe(self, problem, kf_desc=None):
-        """Queue a keyframe: its LocalBA problem and, for ComputeBoW, (device address of its
-        n x 32 descriptors, n)."""
-        self.q.put((problem, kf_desc))
+    def insert_keyframe(self, problem_or_job, kf_desc=None):
+        """Queue a keyframe: a LocalMappingJob (the whole LocalMapping chain), or (LocalBA
+        problem, (device address of its n x 32 descriptors, n)) for ComputeBoW + LocalBA only."""
+        if isinstance(problem_or_job, LocalMappingJob):
+            self.q.put(problem_or_job)
+        else:
+            self.q.put((problem_or_job, kf_desc))
 
     def wait(self):
         self.q.join()
@@ -366,6 +520,7 @@ class LocalMapper:
         self.q.put(None)
         self.t.join()
         self.ba.close()
+        self.matcher.close()
 
 
 def gather_stream_features(dist, desc, kps, count):

@@ -1,0 +1,79 @@
+"""GPU parity of the LocalMapping chain the headline bench runs per keyframe
+(pipeline.LocalMapper.run_job, src/LocalMapping.cc:47-128): ComputeBoW (DBoW2 transform),
+ComputeDistinctiveDescriptors, SearchForTriangulation against every neighbour + the host
+triangulation, Fuse in both directions of SearchInNeighbors, LocalBundleAdjustment -- each
+output compared with the oracle on the same inputs (bench.setup_local_mapping's job).  Index and
+descriptor outputs are exact; LocalBA's iteration counts are identical (its numeric bars are
+tests/test_lba_gpu.py's)."""
+import argparse
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_local_mapping_chain_matches_oracle(oracle):
+    import bench
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd._capi import check, lib
+    from orb_slam2_with_comment_amd.pipeline import LocalMapper
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary, Vocabulary
+    S = bench.setup_track(argparse.Namespace(frames=4, nfeatures=2000), 0, 0)
+    vocab = Vocabulary.synthetic(k=10, L=5, seed=7)
+    voc = ORBVocabulary(vocab, device=0)
+    problem, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
+    jobs, keep = bench.setup_local_mapping(S, voc, vocab, 0, problem)
+    mapper = LocalMapper(0, vocabulary=voc)
+    try:
+        for f in (3, 5):
+            job = jobs[f]
+            out = mapper.run_job(job)  # synchronous, on this thread
+            o, h = mapper._out, job.host
+            o["fv"] = o["fv"]()  # the keyframe's FeatureVector, read back from HBM
+            # ProcessNewKeyFrame: ComputeBoW -> FeatureVector
+            _, _, node, off, feat = oracle.transform(vocab, h["desc"], 4)
+            np.testing.assert_array_equal(o["fv"].node_id, node)
+            np.testing.assert_array_equal(o["fv"].off, off)
+            np.testing.assert_array_equal(o["fv"].feat, feat)
+            # ComputeDistinctiveDescriptors
+            npts = len(h["obs_off"]) - 1
+            best_ref, dsc_ref = oracle.compute_distinctive_descriptors(h["obs_desc"], h["obs_off"])
+            np.testing.assert_array_equal(o["best"][:npts].cpu().numpy(), best_ref)
+            np.testing.assert_array_equal(o["dsc"][:32 * npts].cpu().numpy().reshape(npts, 32), dsc_ref)
+            # CreateNewMapPoints: the searches (exact) and the points the host geometry accepts
+            n_new = 0
+            for j, nb in enumerate(h["neighbours"]):
+                m12, _ = oracle.search_for_triangulation(h["kf"]["frame"], h["kf"]["has_mp"], o["fv"], nb["frame"],
+                                                         nb["has_mp"], nb["fv"], job.F12[j].reshape(3, 3), False,
+                                                         False)
+                np.testing.assert_array_equal(o["tri"][j], m12, err_msg=f"keyframe {f} neighbour {j}")
+                idx1 = np.nonzero(m12 >= 0)[0].astype(np.int32)
+                if len(idx1):
+                    idx2 = np.ascontiguousarray(m12[idx1], np.int32)
+                    x3d = np.zeros((len(idx1), 3), np.float32)
+                    ok = np.zeros(len(idx1), np.uint8)
+                    check("tri", lib().orbmi_triangulate_matches(
+                        C.addressof(job.kf.tri), C.addressof(job.neighbours[j].tri), idx1.ctypes.data,
+                        idx2.ctypes.data, len(idx1), x3d.ctypes.data, ok.ctypes.data))
+                    n_new += int(ok.sum())
+            assert out["new_points"] == n_new and n_new > 0
+            # SearchInNeighbors: Fuse(target, KF points) per target, then Fuse(KF, targets' points)
+            n_kp = len(h["kf_points"])
+            bi, bd = o["bi"].cpu().numpy(), o["bd"].cpu().numpy()
+            for j, nb in enumerate(h["neighbours"]):
+                bi_ref, bd_ref, _ = oracle.fuse_search(nb["frame"], h["kf_points"], None, 3.0)
+                np.testing.assert_array_equal(bi[j * n_kp:(j + 1) * n_kp], bi_ref, err_msg=f"fuse target {j}")
+                np.testing.assert_array_equal(bd[j * n_kp:(j + 1) * n_kp], bd_ref, err_msg=f"fuse target {j}")
+            o0 = len(h["neighbours"]) * n_kp
+            bi_ref, bd_ref, _ = oracle.fuse_search(h["kf"]["frame"], h["target_points"], None, 3.0)
+            np.testing.assert_array_equal(bi[o0:o0 + len(bi_ref)], bi_ref)
+            np.testing.assert_array_equal(bd[o0:o0 + len(bd_ref)], bd_ref)
+            assert out["fuse_candidates"] == int((bi[:o0 + len(bi_ref)] >= 0).sum()) > 0
+            # LocalBundleAdjustment
+            assert tuple(out["local_ba_iterations"]) == tuple(oracle.local_ba(problem)["iterations"])
+    finally:
+        mapper.close()
+        voc.close()
+        S["tr"].close()
