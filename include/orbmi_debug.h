@@ -28,6 +28,11 @@ int orbmi_debug_octree_level(orbmi_extractor* h, int item, int level, int* xyr, 
 int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_pose_obs* obs, uint8_t* outlier,
                            unsigned long long* trace);
 
+/* k_greedy (the order-dependent exclusion of SearchByProjection) since the last reset, summed
+ * over every matcher of the process: out = {calls, rounds, largest round count, slow-path query
+ * evaluations, calls that fell back to the sequential replay}; synchronises the device. */
+int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,10 +11,11 @@
 //                  so a node's children are contiguous, and a DPP min; fan-out > 16 falls back to
 //                  k_bow_descend (thread per descriptor).  Outputs (word, weight, node at level
 //                  L - levelsup).
-//   k_bow_build    one 1024-thread workgroup: bitonic sort in LDS of (word << 32 | feature) keys,
-//                  segment heads -> BowVector entries in word order with the per-word weight
-//                  accumulated sequentially in feature order (as addWeight does), the L1 / L2 norm
-//                  summed sequentially in word order (as normalize does); then the same sort on
+//   k_bow_build    two 1024-thread workgroups side by side.  Block 0: sort of (word << 32 |
+//                  feature) keys in LDS (bitonic, stages of stride < 128 inside a wave), segment
+//                  heads -> BowVector entries in word order with the per-word weight accumulated
+//                  sequentially in feature order (as addWeight does), the L1 / L2 norm summed
+//                  sequentially in word order (as normalize does).  Block 1: the same sort on
 //                  (node << 32 | feature) -> FeatureVector CSR.  Every sum has the reference's
 //                  order, so the BowVector values are bit-exact, not merely close.
 #include <algorithm>
@@ -126,10 +127,46 @@ __global__ __launch_bounds__(256) void k_bow_descend16(VocDev v, const uint4* __
     wv[i] = w;
 }
 
-// ascending bitonic sort of m (power of two) keys in LDS
-__device__ void bitonic_sort(unsigned long long* s, int m) {
-    for (int size = 2; size <= m; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+// ---- sort of m (power of two, 64 <= m <= kBowMaxFeatures) u64 keys in LDS, ascending: bitonic,
+// with every stage of stride < 128 done inside a wave on a 128-key chunk held 2 keys per lane
+// (lane l: chunk positions 2l, 2l + 1; the partner of a stride-s pair sits in lane l ^ s/2), and
+// only the stages of stride >= 128 through LDS with a barrier: for 2048 keys 10 barriered stages
+// instead of 66
+__device__ inline unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const int lo = __shfl_xor((int)(unsigned)v, m, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), m, 64);
+    return (unsigned long long)(unsigned)hi << 32 | (unsigned)lo;
+}
+
+// stages of bitonic level `size` with strides smax .. 1 on the lane's two keys (global index g0 of x0)
+__device__ inline void chunk_stages(unsigned long long& x0, unsigned long long& x1, int g0, int size, int smax) {
+    const int lane = threadIdx.x & 63;
+    const bool up = (g0 & size) == 0;
+    for (int stride = smax; stride >= 2; stride >>= 1) {
+        const int lm = stride >> 1;
+        const unsigned long long y0 = shfl_xor_u64(x0, lm), y1 = shfl_xor_u64(x1, lm);
+        const bool keep_min = ((lane & lm) == 0) == up;
+        x0 = keep_min ? (x0 < y0 ? x0 : y0) : (x0 < y0 ? y0 : x0);
+        x1 = keep_min ? (x1 < y1 ? x1 : y1) : (x1 < y1 ? y1 : x1);
+    }
+    if ((x0 > x1) == up) { const unsigned long long t = x0; x0 = x1; x1 = t; }  // stride 1
+}
+
+__device__ void sort_keys(unsigned long long* s, int m) {
+    const int C = m < 128 ? m : 128, lanes = C / 2, nchunks = m / C;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
+    // levels 2 .. C entirely inside chunks
+    for (int c = wid; c < nchunks; c += nwv) {
+        if (lane < lanes) {
+            const int g0 = c * C + 2 * lane;
+            unsigned long long x0 = s[g0], x1 = s[g0 + 1];
+            for (int size = 2; size <= C; size <<= 1) chunk_stages(x0, x1, g0, size, size >> 1);
+            s[g0] = x0;
+            s[g0 + 1] = x1;
+        }
+    }
+    __syncthreads();
+    for (int size = 2 * C; size <= m; size <<= 1) {
+        for (int stride = size >> 1; stride >= C; stride >>= 1) {  // across chunks: LDS
             for (int t = threadIdx.x; t < (m >> 1); t += blockDim.x) {
                 const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
                 const bool up = (lo & size) == 0;
@@ -138,6 +175,16 @@ __device__ void bitonic_sort(unsigned long long* s, int m) {
             }
             __syncthreads();
         }
+        for (int c = wid; c < nchunks; c += nwv) {  // strides C / 2 .. 1 inside chunks
+            if (lane < lanes) {
+                const int g0 = c * C + 2 * lane;
+                unsigned long long x0 = s[g0], x1 = s[g0 + 1];
+                chunk_stages(x0, x1, g0, size, C >> 1);
+                s[g0] = x0;
+                s[g0 + 1] = x1;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -166,6 +213,9 @@ __device__ int segment_heads(const unsigned long long* s, int m, int* pos, int* 
     return total;
 }
 
+// Two workgroups that run side by side: block 0 builds the BowVector (sort of the word keys,
+// per-word weights summed in feature order, the norm), block 1 the FeatureVector (sort of the
+// node keys, CSR).  The norm is the one sequential chain (bit-exact: the reference's order).
 __global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(
     const unsigned long long* __restrict__ key_w, const unsigned long long* __restrict__ key_n,
     const double* __restrict__ wv, int n, int weighting, int scoring, unsigned* __restrict__ bow_word,
@@ -177,71 +227,109 @@ __global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(
     __shared__ double norm_s;
     int m = 64;
     while (m < n) m <<= 1;
+    constexpr int PER = kBowMaxFeatures / kBowBuildThreads;
+    if (blockIdx.x == 1) {  // ---- FeatureVector
+        for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_n[j] : kNoKey;
+        __syncthreads();
+        sort_keys(s, m);
+        const int nnod = segment_heads(s, m, pos, scratch);
+        for (int j = threadIdx.x; j < m; j += blockDim.x) {
+            if (s[j] == kNoKey) continue;
+            fv_feat[j] = (int)(unsigned)s[j];  // valid keys sort first: j is the CSR position
+            const int k = pos[j];
+            if (k >= 0) {
+                fv_node[k] = (unsigned)(s[j] >> 32);
+                fv_off[k] = j;
+            }
+            if (j + 1 == m || s[j + 1] == kNoKey) fv_off[nnod] = j + 1;
+        }
+        if (threadIdx.x == 0) {
+            if (nnod == 0) fv_off[0] = 0;
+            counts[1] = nnod;
+        }
+        return;
+    }
     // ---- BowVector
     for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_w[j] : kNoKey;
     __syncthreads();
-    bitonic_sort(s, m);
+    sort_keys(s, m);
     const int nw = segment_heads(s, m, pos, scratch);
     const bool tf = weighting == 0 || weighting == 1;  // TF_IDF, TF: addWeight; IDF, BINARY: addIfNotExist
     int nrm = 1;
     const bool must = must_normalize(scoring, &nrm);
-    constexpr int PER = kBowMaxFeatures / kBowBuildThreads;
+    // every element's weight gathered once (in parallel), then kept in LDS in sorted order
+    double w[PER];
+    int nvalid = 0;  // valid keys sort first
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = threadIdx.x + q * kBowBuildThreads;
+        w[q] = 0;
+        if (j < m && s[j] != kNoKey) {
+            w[q] = wv[(unsigned)s[j]];
+            nvalid = j + 1;
+            if (pos[j] >= 0) bow_word[pos[j]] = (unsigned)(s[j] >> 32);
+        }
+    }
+    __shared__ int nvalid_s;
+    if (threadIdx.x == 0) nvalid_s = 0;
+    __syncthreads();
+    atomicMax(&nvalid_s, nvalid);
+    double* ws = reinterpret_cast<double*>(s);  // the keys are dead once words and weights are out
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = threadIdx.x + q * kBowBuildThreads;
+        if (j < m) ws[j] = w[q];
+    }
+    __syncthreads();
+    const int nv = nvalid_s;
     double val[PER];
     int slot[PER];
 #pragma unroll
-    for (int q = 0; q < PER; q++) {  // segment heads: one BowVector entry each
+    for (int q = 0; q < PER; q++) {  // segment heads: one BowVector entry each, summed in feature order
         const int j = threadIdx.x + q * kBowBuildThreads;
         slot[q] = (j < m) ? pos[j] : -1;
         val[q] = 0;
         if (slot[q] < 0) continue;
-        const unsigned word = (unsigned)(s[j] >> 32);
-        double x = wv[(unsigned)s[j]];
+        double x = ws[j];
         if (tf)
-            for (int r = j + 1; r < m && s[r] != kNoKey && (unsigned)(s[r] >> 32) == word; r++) x += wv[(unsigned)s[r]];
+            for (int r = j + 1; r < nv && pos[r] < 0; r++) x += ws[r];
         if (tf && !must) x /= (double)nw;  // "unnecessary when normalizing": divide by v.size()
-        bow_word[slot[q]] = word;
         val[q] = x;
     }
-    __syncthreads();  // the keys are dead: their LDS holds the values, in word order
-    double* vals = reinterpret_cast<double*>(s);
+    __syncthreads();  // the weights are dead: the LDS holds the values, in word order
 #pragma unroll
     for (int q = 0; q < PER; q++)
-        if (slot[q] >= 0) vals[slot[q]] = val[q];
+        if (slot[q] >= 0) ws[slot[q]] = val[q];
     __syncthreads();
     if (must && threadIdx.x == 0) {  // BowVector::normalize: sequential in word order
         double norm = 0.0;
+        int k = 0;
         if (nrm == 1) {
-            for (int k = 0; k < nw; k++) norm += fabs(vals[k]);
+            for (; k + 4 <= nw; k += 4) {
+                const double a0 = ws[k], a1 = ws[k + 1], a2 = ws[k + 2], a3 = ws[k + 3];
+                norm += fabs(a0);
+                norm += fabs(a1);
+                norm += fabs(a2);
+                norm += fabs(a3);
+            }
+            for (; k < nw; k++) norm += fabs(ws[k]);
         } else {
-            for (int k = 0; k < nw; k++) norm += vals[k] * vals[k];
+            for (; k + 4 <= nw; k += 4) {
+                const double a0 = ws[k], a1 = ws[k + 1], a2 = ws[k + 2], a3 = ws[k + 3];
+                norm += a0 * a0;
+                norm += a1 * a1;
+                norm += a2 * a2;
+                norm += a3 * a3;
+            }
+            for (; k < nw; k++) norm += ws[k] * ws[k];
             norm = sqrt(norm);
         }
         norm_s = norm;
     }
     __syncthreads();
     const double norm = must ? norm_s : 0.0;
-    for (int k = threadIdx.x; k < nw; k += blockDim.x) bow_value[k] = norm > 0.0 ? vals[k] / norm : vals[k];
-    __syncthreads();
-    // ---- FeatureVector
-    for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = j < n ? key_n[j] : kNoKey;
-    __syncthreads();
-    bitonic_sort(s, m);
-    const int nnod = segment_heads(s, m, pos, scratch);
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        if (s[j] == kNoKey) continue;
-        fv_feat[j] = (int)(unsigned)s[j];  // valid keys sort first: j is the CSR position
-        const int k = pos[j];
-        if (k >= 0) {
-            fv_node[k] = (unsigned)(s[j] >> 32);
-            fv_off[k] = j;
-        }
-        if (j + 1 == m || s[j + 1] == kNoKey) fv_off[nnod] = j + 1;
-    }
-    if (threadIdx.x == 0) {
-        if (nnod == 0) fv_off[0] = 0;
-        counts[0] = nw;
-        counts[1] = nnod;
-    }
+    for (int k = threadIdx.x; k < nw; k += blockDim.x) bow_value[k] = norm > 0.0 ? ws[k] / norm : ws[k];
+    if (threadIdx.x == 0) counts[0] = nw;
 }
 
 }  // namespace orbmi
@@ -416,7 +504,7 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
                                n, n_device, nid_level, key_w, key_n, wv);
         ORBMI_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bow_build, dim3(1), dim3(kBowBuildThreads), 0, h->stream, key_w, key_n, wv, n,
+    hipLaunchKernelGGL(k_bow_build, dim3(2), dim3(kBowBuildThreads), 0, h->stream, key_w, key_n, wv, n,
                        h->v.weighting, h->v.scoring, (unsigned*)o_word, o_value, (unsigned*)o_node, (int*)o_off,
                        (int*)o_feat, o_cnt);
     ORBMI_HIP(hipGetLastError());

@@ -604,4 +604,9 @@ int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* k
     return ORBMI_OK;
 }
 
+int orbmi_debug_greedy_stats(unsigned long long* out, int reset) {
+    if (!out) return ORBMI_E_ARG;
+    return orbmi::greedy_stats(out, reset);
+}
+
 }  // extern "C"

@@ -479,6 +479,10 @@ __device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int
 
 constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = 4;
 
+// k_greedy statistics (orbmi_debug_greedy_stats): calls, rounds summed, largest round count,
+// slow-path query evaluations summed, calls that fell back to the sequential replay
+__device__ unsigned long long g_greedy_stats[5];
+
 // Each thread keeps its queries (q = tid + k * 1024) in registers: current result, candidate
 // count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
 // octave and the initial occupancy live in LDS.  A round then touches LDS only, except for
@@ -527,7 +531,9 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         for (int q = tid; q < nq; q += blockDim.x) a.res[q] = -1;
     __syncthreads();
     bool converged = false;
+    int rounds = 0, nslow = 0;
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
+        rounds++;
         for (int i = tid; i < n; i += blockDim.x) claim[i] = 0x7FFFFFFF;
         if (tid == 0) flag[0] = 0;
         __syncthreads();
@@ -563,6 +569,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                 if (i2 < 0 && nc[k] > kGreedyPre) slow |= 1u << k;  // prefix exhausted
                 else fast[k] = greedy_decide(a, oct, d1, i1, d2, i2);
             }
+            nslow += __builtin_popcount(slow);
             for (int k = 0; k < kGreedyQPer; k++)  // not unrolled: one copy of the slow path
                 if (slow >> k & 1) {
                     const int q = tid + k * kGreedyThreads;
@@ -642,6 +649,23 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     }
     for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
     if (tid == 0) *a.nmatches = flag[1];
+    if (nslow) atomicAdd(&g_greedy_stats[3], (unsigned long long)nslow);
+    if (tid == 0) {
+        atomicAdd(&g_greedy_stats[0], 1ull);
+        atomicAdd(&g_greedy_stats[1], (unsigned long long)rounds);
+        atomicMax(&g_greedy_stats[2], (unsigned long long)rounds);
+        if (!converged) atomicAdd(&g_greedy_stats[4], 1ull);
+    }
+}
+
+int greedy_stats(unsigned long long out[5], int reset) {
+    ORBMI_HIP(hipDeviceSynchronize());
+    ORBMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_greedy_stats), sizeof(unsigned long long) * 5));
+    if (reset) {
+        const unsigned long long z[5] = {0, 0, 0, 0, 0};
+        ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_greedy_stats), z, sizeof(z)));
+    }
+    return ORBMI_OK;
 }
 
 // -------------------------------------------------------------------------- Tracking
