@@ -534,6 +534,9 @@ typedef struct orbmi_slam_settings {
     int n_levels, ini_th_fast, min_th_fast;
     int local_ba;                  /* 1: LocalMapping runs LocalBundleAdjustment (:89-90)      */
     int local_mapping;             /* 1: and CreateNewMapPoints, SearchInNeighbors, KeyFrameCulling */
+    int async_local_mapping;       /* 1: LocalMapping on its own thread, concurrent with Tracking as
+                                      in the reference (keyframe decisions then depend on timing);
+                                      0: synchronous after each keyframe (deterministic) */
 } orbmi_slam_settings;
 
 /* Per tracked frame: Tracking's counters (-1 = the stage did not run). track: 0 none, 1
@@ -552,6 +555,9 @@ typedef struct orbmi_slam orbmi_slam;
  * operator is the MI355X one of this library.  vocabulary (may be NULL: TrackReferenceKeyFrame
  * then fails with ORBMI_E_STATE) is borrowed and must outlive the handle. */
 int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary* vocabulary, orbmi_slam** out);
+/* System::Shutdown's wait for LocalMapping (src/System.cc:300-314): returns when no keyframe is
+ * queued or being processed (immediately in synchronous mode); the mapping thread's first error. */
+int orbmi_slam_wait_local_mapping(orbmi_slam* h);
 void orbmi_slam_destroy(orbmi_slam* h);
 
 /* System::TrackStereo(imLeft, imRight, timestamp) (src/System.cc:110-159): host u8 gray images

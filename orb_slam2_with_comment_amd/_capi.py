@@ -105,6 +105,7 @@ _PROTOS = {
     "orbmi_triangulate_matches": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_slam_create": (_i, [_vp, _i, _vp, C.POINTER(_vp)]),
     "orbmi_slam_destroy": (None, [_vp]),
+    "orbmi_slam_wait_local_mapping": (_i, [_vp]),
     "orbmi_slam_track_stereo": (_i, [_vp, _vp, _vp, _i, _i, _sz, C.c_double, _vp, C.POINTER(_i)]),
     "orbmi_slam_get_stats": (_i, [_vp, _i, _vp]),
     "orbmi_slam_get_counts": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),

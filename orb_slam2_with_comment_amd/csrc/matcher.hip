@@ -24,6 +24,7 @@
 #include <cstring>
 
 #include "matcher.h"
+#include "wave_ops.h"
 
 namespace orbmi {
 
@@ -84,9 +85,9 @@ __global__ __launch_bounds__(1024) void k_grid_build_multi(const FuseKF* __restr
 
 // Frame::GetFeaturesInArea (src/Frame.cc:353-410): calls fn(idx) for every keypoint in the
 // window passing the level filter, in arbitrary order.
-template <class Fn>
+template <int G = 1, class Fn>
 __device__ inline void for_features_in_area(const DevFrame& F, const int* cell_start, const int* cell_list,
-                                            float x, float y, float r, int minLevel, int maxLevel, Fn fn) {
+                                            float x, float y, float r, int minLevel, int maxLevel, int glane, Fn fn) {
     const int nMinCellX = max(0, (int)floorf((x - F.min_x - r) * F.grid_w_inv));
     if (nMinCellX >= kGridCols) return;
     const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - F.min_x + r) * F.grid_w_inv));
@@ -96,20 +97,25 @@ __device__ inline void for_features_in_area(const DevFrame& F, const int* cell_s
     const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - F.min_y + r) * F.grid_h_inv));
     if (nMaxCellY < 0) return;
     const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
-        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
-            const int c = ix * kGridRows + iy;
-            for (int j = cell_start[c]; j < cell_start[c + 1]; j++) {
-                const int idx = cell_list[j];
-                const orbmi_keypoint kp = F.keys[idx];
-                if (bCheckLevels) {
-                    if (kp.octave < minLevel) continue;
-                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
-                }
-                const float distx = kp.x - x, disty = kp.y - y;
-                if (fabsf(distx) < r && fabsf(disty) < r) fn(idx, c);
+    const int ny = nMaxCellY - nMinCellY + 1, ncell = (nMaxCellX - nMinCellX + 1) * ny;
+    for (int ci = glane; ci < ncell; ci += G) {  // G = 1: ix-major, iy-minor (the visit order)
+        const int c = (nMinCellX + ci / ny) * kGridRows + nMinCellY + ci % ny;
+        for (int j = cell_start[c]; j < cell_start[c + 1]; j++) {
+            const int idx = cell_list[j];
+            const orbmi_keypoint kp = F.keys[idx];
+            if (bCheckLevels) {
+                if (kp.octave < minLevel) continue;
+                if (maxLevel >= 0 && kp.octave > maxLevel) continue;
             }
+            const float distx = kp.x - x, disty = kp.y - y;
+            if (fabsf(distx) < r && fabsf(disty) < r) fn(idx, c);
         }
+    }
+}
+template <class Fn>
+__device__ inline void for_features_in_area(const DevFrame& F, const int* cell_start, const int* cell_list,
+                                            float x, float y, float r, int minLevel, int maxLevel, Fn fn) {
+    for_features_in_area<1>(F, cell_start, cell_list, x, y, r, minLevel, maxLevel, 0, fn);
 }
 
 __device__ inline unsigned long long cand_entry(int dist, int cell, int idx) {
@@ -1050,6 +1056,7 @@ __global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* 
     const DevFrame& KF2 = P.KF2;
     const Mat3f F12 = P.F12;
     const int f0 = fv2.off[lo], nf = fv2.off[lo + 1] - f0;
+    const int a0 = fv1.off[a], n1 = fv1.off[a + 1] - a0;
     // epipole of KF1's centre in KF2
     const Pose34 T1 = frame_pose(KF1), T2 = frame_pose(KF2);
     float Ow[3], C2[3];
@@ -1061,6 +1068,114 @@ __global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* 
     const float invz = 1.0f / C2[2];
     const float ex = KF2.fx * C2[0] * invz + KF2.cx;
     const float ey = KF2.fy * C2[1] * invz + KF2.cy;
+    if (nf <= 128) {
+        // The node's KF2 candidates sit in registers (lane p holds candidates p and p + 64), the
+        // KF1 features in chunks of 64 (lane p holds feature p of the chunk), each loaded in one
+        // round; the KF1 features are then visited in order by broadcasting lane i's (readlane),
+        // so the inner loop issues no memory access.
+        bool okc[2], stc[2];
+        int idxc[2];
+        uint4 e0[2], e1[2];
+        float kx[2], ky[2], sc2[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int pos = lane + 64 * h;
+            okc[h] = pos < nf;
+            stc[h] = false;
+            idxc[h] = 0;
+            e0[h] = make_uint4(0, 0, 0, 0);
+            e1[h] = e0[h];
+            kx[h] = ky[h] = 0.f;
+            sc2[h] = 1.f;
+            if (okc[h]) {
+                const int i2 = fv2.feat[f0 + pos];
+                idxc[h] = i2;
+                stc[h] = KF2.u_right[i2] >= 0;
+                okc[h] = !has_mp2[i2] && !(only_stereo && !stc[h]);
+                const uint4* d2 = reinterpret_cast<const uint4*>(KF2.desc + 32 * (long long)i2);
+                e0[h] = d2[0];
+                e1[h] = d2[1];
+                const orbmi_keypoint k2 = KF2.keys[i2];
+                kx[h] = k2.x;
+                ky[h] = k2.y;
+                sc2[h] = KF2.scale[min(max(k2.octave, 0), kMaxLevels - 1)];
+            }
+        }
+        for (int c1 = 0; c1 < n1; c1 += 64) {
+            bool ok1 = c1 + lane < n1;
+            int idx1l = 0;
+            uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0;
+            orbmi_keypoint kp1l{};
+            bool st1l = false;
+            if (ok1) {
+                idx1l = fv1.feat[a0 + c1 + lane];
+                st1l = KF1.u_right[idx1l] >= 0;
+                ok1 = !has_mp1[idx1l] && !(only_stereo && !st1l);
+                const uint4* d1 = reinterpret_cast<const uint4*>(KF1.desc + 32 * (long long)idx1l);
+                g0 = d1[0];
+                g1 = d1[1];
+                kp1l = KF1.keys[idx1l];
+            }
+            unsigned long long todo = __ballot(ok1);
+            while (todo) {
+                const int i = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const int idx1 = __builtin_amdgcn_readlane(idx1l, i);
+                const bool st1 = __builtin_amdgcn_readlane((int)st1l, i) != 0;
+                const float k1x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.x), i));
+                const float k1y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.y), i));
+                const uint4 d0 = make_uint4(__builtin_amdgcn_readlane(g0.x, i), __builtin_amdgcn_readlane(g0.y, i),
+                                            __builtin_amdgcn_readlane(g0.z, i), __builtin_amdgcn_readlane(g0.w, i));
+                const uint4 d1 = make_uint4(__builtin_amdgcn_readlane(g1.x, i), __builtin_amdgcn_readlane(g1.y, i),
+                                            __builtin_amdgcn_readlane(g1.z, i), __builtin_amdgcn_readlane(g1.w, i));
+                // epipolar line of kp1 in KF2: l = x1' F12
+                const float la = k1x * F12.m[0] + k1y * F12.m[3] + F12.m[6];
+                const float lb = k1x * F12.m[1] + k1y * F12.m[4] + F12.m[7];
+                const float lc = k1x * F12.m[2] + k1y * F12.m[5] + F12.m[8];
+                unsigned long long key = ~0ull;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    if (!okc[h]) continue;
+                    const int dist = popc256(d0, d1, e0[h], e1[h]);
+                    bool pass = dist <= TH_LOW;
+                    if (pass && !st1 && !stc[h]) {
+                        const float distex = ex - kx[h];
+                        const float distey = ey - ky[h];
+                        pass = !(distex * distex + distey * distey < 100 * sc2[h]);
+                    }
+                    if (pass) {
+                        const float num = la * kx[h] + lb * ky[h] + lc;
+                        const float den = la * la + lb * lb;
+                        if (den == 0) pass = false;
+                        else {
+                            const float dsqr = num * num / den;
+                            const float sigma2 = sc2[h] * sc2[h];
+                            pass = (double)dsqr < 3.84 * (double)sigma2;
+                        }
+                    }
+                    const unsigned long long k =
+                        (unsigned long long)dist << 32 | (unsigned)(0xFFFFFFFFu - (unsigned)(lane + 64 * h));
+                    if (pass && k < key) key = k;
+                }
+                key = wave_min_u64_dpp(key);
+                if (key != ~0ull) {
+                    const int pos = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFu)));
+                    const int i2 = pos < 64 ? __builtin_amdgcn_readlane(idxc[0], pos)
+                                            : __builtin_amdgcn_readlane(idxc[1], pos - 64);
+                    if (lane == 0) {
+                        match[idx1] = i2;
+                        if (check_ori) {
+                            const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.angle), i));
+                            const int bin = rot_bin(a1, KF2.keys[i2].angle);
+                            P.bin_of[idx1] = bin;
+                            atomicAdd(&P.hist[bin], 1);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
     for (int ia = fv1.off[a]; ia < fv1.off[a + 1]; ia++) {
         const int idx1 = fv1.feat[ia];
         if (has_mp1[idx1]) continue;
@@ -1147,15 +1262,32 @@ int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1
 // the reference's grid order wins ties (key dist << 40 | cell << 20 | idx).  The map updates
 // (Replace / AddObservation) are the caller's sequential replay of (best_idx, best_dist) in
 // list order (include/orbmi.h).
+// minimum over the G lanes of a group (G = 1 or 8, groups aligned inside a DPP row)
+template <int G>
+__device__ inline unsigned long long group_min_u64(unsigned long long v) {
+    if constexpr (G == 8) {
+        unsigned long long w;
+        w = dpp_mov_u64<kDppXor1>(v); v = w < v ? w : v;
+        w = dpp_mov_u64<kDppXor2>(v); v = w < v ? w : v;
+        w = dpp_mov_u64<kDppHalfMirror>(v); v = w < v ? w : v;
+    }
+    return v;
+}
+
+// candidate i of Fuse on G lanes: every lane runs the projection and the tests, the window's
+// grid cells are shared out among the G lanes (cell ci on lane ci mod G), the keys meet in a
+// group minimum; lane 0 of the group writes.  valid = false: the lanes only take part in the
+// group minimum.
+template <int G>
 __device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, const int* __restrict__ cl,
                                 const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf, int i,
-                                float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
-                                int* __restrict__ ncand) {
+                                bool valid, int glane, float th, int* __restrict__ best_idx,
+                                int* __restrict__ best_dist, int* __restrict__ ncand) {
     int bi = -1, bd = 256;
-    const orbmi_mappoint mp = mps[i];
+    const orbmi_mappoint mp = mps[valid ? i : 0];
     const Pose34 T = frame_pose(F);
     float Pc[3];
-    bool ok = !(mp.flags & ORBMI_MP_BAD) && !(in_kf && in_kf[i]);
+    bool ok = valid && !(mp.flags & ORBMI_MP_BAD) && !(in_kf && in_kf[i]);
     if (ok) {
         transform(T.m, mp.pos, Pc);
         ok = !(Pc[2] < 0.0f);
@@ -1180,6 +1312,7 @@ __device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, c
             ok = !(dot < 0.5 * (double)dist3D);
         }
     }
+    unsigned long long best = ~0ull;
     if (ok) {
         const float ratio = mp.max_distance / dist3D;  // MapPoint::PredictScale(dist, KeyFrame*)
         int nPredictedLevel = (int)ceilf((float)log((double)ratio) / F.log_scale_factor);
@@ -1187,8 +1320,7 @@ __device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, c
         else if (nPredictedLevel >= F.nlevels) nPredictedLevel = F.nlevels - 1;
         const float radius = th * F.scale[nPredictedLevel];
         const float ur = u - F.bf * invz;
-        unsigned long long best = ~0ull;
-        for_features_in_area(F, cs, cl, u, v, radius, -1, -1, [&](int idx, int cell) {
+        for_features_in_area<G>(F, cs, cl, u, v, radius, -1, -1, glane, [&](int idx, int cell) {
             const orbmi_keypoint kp = F.keys[idx];
             const int kpLevel = kp.octave;
             if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) return;
@@ -1205,33 +1337,37 @@ __device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, c
             const unsigned long long e = cand_entry(popc_desc(mp.desc, F.desc + 32 * (long long)idx), cell, idx);
             best = e < best ? e : best;
         });
-        if (best != ~0ull) {
-            bd = (int)(best >> 40);
-            bi = (int)(best & 0xFFFFF);
-        }
+    }
+    best = group_min_u64<G>(best);
+    if (!valid || glane != 0) return;
+    if (best != ~0ull) {
+        bd = (int)(best >> 40);
+        bi = (int)(best & 0xFFFFF);
     }
     const bool fused = bi >= 0 && bd <= TH_LOW;
     best_idx[i] = fused ? bi : -1;
     best_dist[i] = bi >= 0 ? bd : 256;
-    if (fused) atomicAdd(ncand, 1);
+    // one atomic per wave: a counter shared by the whole grid serialises per-thread atomics
+    const unsigned long long m = __ballot(fused);
+    if (fused && (threadIdx.x & 63) == __ffsll((long long)m) - 1) atomicAdd(ncand, (int)__popcll(m));
 }
+
+constexpr int kFuseLanes = 8;  // lanes per candidate map point (a window spans a few grid cells)
 
 __global__ __launch_bounds__(256) void k_fuse(DevFrame F, const int* __restrict__ cs, const int* __restrict__ cl,
                                               const orbmi_mappoint* __restrict__ mps, const uint8_t* __restrict__ in_kf,
                                               int n, float th, int* __restrict__ best_idx, int* __restrict__ best_dist,
                                               int* __restrict__ ncand) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fuse_one(F, cs, cl, mps, in_kf, i, th, best_idx, best_dist, ncand);
+    const int t = blockIdx.x * blockDim.x + threadIdx.x, i = t / kFuseLanes;
+    fuse_one<kFuseLanes>(F, cs, cl, mps, in_kf, i, i < n, t % kFuseLanes, th, best_idx, best_dist, ncand);
 }
 
 // the same candidate list against several keyframes (grid row = keyframe)
 __global__ __launch_bounds__(256) void k_fuse_multi(const FuseKF* __restrict__ kfs, const orbmi_mappoint* __restrict__ mps,
                                                     int n, float th) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x, i = t / kFuseLanes;
     const FuseKF& K = kfs[blockIdx.y];
-    fuse_one(K.F, K.cs, K.cl, mps, K.in_kf, i, th, K.best_idx, K.best_dist, K.ncand);
+    fuse_one<kFuseLanes>(K.F, K.cs, K.cl, mps, K.in_kf, i, i < n, t % kFuseLanes, th, K.best_idx, K.best_dist, K.ncand);
 }
 
 int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
@@ -1239,7 +1375,7 @@ int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const 
     int rc;
     if ((rc = grid_for(m, F))) return rc;
     if (n > 0)
-        hipLaunchKernelGGL(k_fuse, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start, m.d_cell_list,
+        hipLaunchKernelGGL(k_fuse, dim3((n * kFuseLanes + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start, m.d_cell_list,
                            mps, in_kf, n, th, best_idx, best_dist, ncand);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
@@ -1268,7 +1404,8 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
     ORBMI_HIP(hipMemsetAsync(ncand, 0, sizeof(int) * nkf, m.stream));
     hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.stream, kfs_dev, m.d_mkp_cell, ncap);
     if (n > 0)
-        hipLaunchKernelGGL(k_fuse_multi, dim3((n + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n, th);
+        hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n,
+                           th);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 

@@ -24,6 +24,10 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -31,6 +35,8 @@
 #include <set>
 #include <utility>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../../include/orbmi.h"
 
@@ -158,6 +164,7 @@ struct TrackedFrame {
     std::vector<uint8_t> outlier;
     int ref_kf = -1;
     FeatVec fv;
+    int dslot = -1;              // device slot holding keys / desc / u_right (orbmi_slam::Dev)
     int n() const { return (int)keys.size(); }
 };
 
@@ -208,6 +215,47 @@ struct orbmi_slam {
     // extraction scratch
     std::vector<orbmi_keypoint> kbuf;
     std::vector<uint8_t> dbuf;
+    // Device-resident frames: the image pair goes up once, both images are extracted as one
+    // batch with the stereo match behind them on the extractor's stream, and the outputs stay
+    // in one of two slots (current frame, last frame), so the searches and the pose
+    // optimisations read the frames in place instead of staging them per call; the host gets its
+    // copy of the left outputs with one read-back.
+    struct Dev {
+        uint8_t* img = nullptr;  // 2 x rows x cols
+        size_t img_bytes = 0;
+        uint8_t* h_img = nullptr;  // pinned staging of the pair
+        int cap = 0;               // keypoints per item
+        orbmi_keypoint* kps[2] = {};
+        uint8_t* desc[2] = {};
+        int* cnt[2] = {};
+        float* ur[2] = {};
+        float* dep[2] = {};
+        // pinned host mirror of a slot's left outputs
+        orbmi_keypoint* h_kps = nullptr;
+        uint8_t* h_desc = nullptr;
+        int* h_cnt = nullptr;
+        float* h_ur = nullptr;
+        float* h_dep = nullptr;
+    } dev;
+    hipStream_t xstream = nullptr;  // the left extractor's stream
+
+    // ---- LocalMapping on its own thread (settings.async_local_mapping, src/LocalMapping.cc:47-128)
+    // The map and the handles both threads call (matcher, vocabulary) are guarded by map_mtx:
+    // Tracking holds it for Track() (the Frame constructor's extraction runs outside it), the
+    // mapping thread for a keyframe's LocalMapping::Run except the LocalBundleAdjustment's GPU
+    // solve, which -- as the reference's mMutexMapUpdate does (src/Optimizer.cc:776) -- locks
+    // only for the graph assembly and the write-back, so tracking proceeds while it runs.
+    std::mutex map_mtx;
+    std::mutex q_mtx;
+    std::condition_variable q_cv, idle_cv;
+    std::deque<int> lm_queue;   // mlNewKeyFrames
+    bool lm_busy = false;       // !mbAcceptKeyFrames
+    bool lm_quit = false;
+    int lm_rc = ORBMI_OK;       // the first error of the mapping thread
+    volatile int abort_ba = 0;  // mbAbortBA
+    std::thread lm_thread;
+    std::unique_lock<std::mutex>* lm_lock = nullptr;  // the mapping thread's hold on map_mtx
+    bool async_lm() const { return s.async_local_mapping != 0; }
 
     // ---- Frame views (include/Frame.h members the matchers read) --------------------------
     orbmi_frame_view view(const std::vector<orbmi_keypoint>& keys, const std::vector<uint8_t>& desc,
@@ -229,7 +277,92 @@ struct orbmi_slam {
         v.n_device = nullptr;
         return v;
     }
-    orbmi_frame_view view(const TrackedFrame& f, const float* tcw) const { return view(f.keys, f.desc, f.ur, tcw); }
+    orbmi_frame_view view(const TrackedFrame& f, const float* tcw) const {
+        orbmi_frame_view v = view(f.keys, f.desc, f.ur, tcw);
+        if (f.dslot >= 0) {  // the frame's arrays in HBM (left item of its slot)
+            v.keys_un = dev.kps[f.dslot];
+            v.desc = dev.desc[f.dslot];
+            v.u_right = dev.ur[f.dslot];
+        }
+        return v;
+    }
+
+    // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images (one batch on the
+    // left handle) and ComputeStereoMatches, into device slot cf.id & 1; host copies of the left
+    // keypoints, descriptors, u_right and depth
+    int frame_stereo(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step) {
+        const size_t img = (size_t)rows * cols;
+        if (2 * img > dev.img_bytes) {
+            if (dev.img) (void)hipFree(dev.img);
+            if (dev.h_img) (void)hipHostFree(dev.h_img);
+            dev.img = nullptr;
+            dev.h_img = nullptr;
+            if (hipMalloc((void**)&dev.img, 2 * img) != hipSuccess) return ORBMI_E_HIP;
+            if (hipHostMalloc((void**)&dev.h_img, 2 * img, hipHostMallocDefault) != hipSuccess) return ORBMI_E_HIP;
+            dev.img_bytes = 2 * img;
+        }
+        if (!dev.kps[0]) {
+            const int cap = s.n_features + 16 * s.n_levels + 64;
+            dev.cap = cap;
+            for (int k = 0; k < 2; k++) {
+                if (hipMalloc((void**)&dev.kps[k], 2 * (size_t)cap * sizeof(orbmi_keypoint)) != hipSuccess ||
+                    hipMalloc((void**)&dev.desc[k], 2 * (size_t)cap * 32) != hipSuccess ||
+                    hipMalloc((void**)&dev.cnt[k], 2 * sizeof(int)) != hipSuccess ||
+                    hipMalloc((void**)&dev.ur[k], 2 * (size_t)cap * sizeof(float)) != hipSuccess ||
+                    hipMalloc((void**)&dev.dep[k], 2 * (size_t)cap * sizeof(float)) != hipSuccess)
+                    return ORBMI_E_HIP;
+            }
+            if (hipHostMalloc((void**)&dev.h_kps, (size_t)cap * sizeof(orbmi_keypoint), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&dev.h_desc, (size_t)cap * 32, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&dev.h_cnt, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&dev.h_ur, (size_t)cap * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&dev.h_dep, (size_t)cap * sizeof(float), hipHostMallocDefault) != hipSuccess)
+                return ORBMI_E_HIP;
+        }
+        for (int r = 0; r < rows; r++) {
+            std::memcpy(dev.h_img + (size_t)r * cols, L + (size_t)r * step, cols);
+            std::memcpy(dev.h_img + img + (size_t)r * cols, R + (size_t)r * step, cols);
+        }
+        if (hipMemcpyAsync(dev.img, dev.h_img, 2 * img, hipMemcpyHostToDevice, xstream) != hipSuccess) return ORBMI_E_HIP;
+        const int k = cf.id & 1, cap = dev.cap;
+        SLAM_CHECK(orbmi_extract_batch_device(left, dev.img, 2, rows, cols, cols, img, dev.kps[k], dev.desc[k], dev.cnt[k],
+                                              cap));
+        SLAM_CHECK(orbmi_compute_stereo_matches_batch_device(left, s.bf, s.fx, dev.ur[k], dev.dep[k]));
+        if (hipMemcpyAsync(dev.h_cnt, dev.cnt[k], 2 * sizeof(int), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
+            hipMemcpyAsync(dev.h_kps, dev.kps[k], (size_t)cap * sizeof(orbmi_keypoint), hipMemcpyDeviceToHost, xstream) !=
+                hipSuccess ||
+            hipMemcpyAsync(dev.h_desc, dev.desc[k], (size_t)cap * 32, hipMemcpyDeviceToHost, xstream) != hipSuccess ||
+            hipMemcpyAsync(dev.h_ur, dev.ur[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
+            hipMemcpyAsync(dev.h_dep, dev.dep[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
+            hipStreamSynchronize(xstream) != hipSuccess)
+            return ORBMI_E_HIP;
+        const int n = std::min(dev.h_cnt[0], cap);
+        cf.keys.assign(dev.h_kps, dev.h_kps + n);
+        cf.desc.assign(dev.h_desc, dev.h_desc + (size_t)n * 32);
+        cf.ur.assign(dev.h_ur, dev.h_ur + n);
+        cf.depth.assign(dev.h_dep, dev.h_dep + n);
+        cf.dslot = k;
+        // new keypoints behind the slot's pointers: a grid pinned on the frame two back is stale
+        return orbmi_matcher_release_grid(matcher);
+    }
+
+    void free_dev() {
+        for (int k = 0; k < 2; k++) {
+            (void)hipFree(dev.kps[k]);
+            (void)hipFree(dev.desc[k]);
+            (void)hipFree(dev.cnt[k]);
+            (void)hipFree(dev.ur[k]);
+            (void)hipFree(dev.dep[k]);
+        }
+        (void)hipFree(dev.img);
+        (void)hipHostFree(dev.h_img);
+        (void)hipHostFree(dev.h_kps);
+        (void)hipHostFree(dev.h_desc);
+        (void)hipHostFree(dev.h_cnt);
+        (void)hipHostFree(dev.h_ur);
+        (void)hipHostFree(dev.h_dep);
+        dev = Dev{};
+    }
 
     // ---- backend operators ------------------------------------------------------------------
     int extract(orbmi_extractor* ex, const uint8_t* img, int rows, int cols, size_t step, std::vector<orbmi_keypoint>& k,
@@ -472,7 +605,7 @@ struct orbmi_slam {
         for (int i = 0; i < cf.n(); i++)
             if (cf.depth[i] > 0) idx.push_back(i);
         create_points(k, cf, idx);
-        SLAM_CHECK(local_mapping(k));
+        SLAM_CHECK(insert_keyframe(k));
         last_kf_frame_id = cf.id;
         local_kfs = {k};
         local_mps.clear();
@@ -497,12 +630,22 @@ struct orbmi_slam {
         }
         const bool need_close = n_tracked_close < 100 && n_non_tracked_close > 70;
         const float th_ref = nkfs < 2 ? 0.4f : 0.75f;
+        bool idle = true;  // LocalMapping::AcceptKeyFrames (always, when it runs synchronously)
+        size_t queued = 0;
+        if (async_lm()) {
+            std::lock_guard<std::mutex> g(q_mtx);
+            idle = !lm_busy;
+            queued = lm_queue.size();
+        }
         const bool c1a = cf.id >= last_kf_frame_id + s.max_frames;
-        const bool c1b = cf.id >= last_kf_frame_id + s.min_frames;  // LocalMapping idle (synchronous)
+        const bool c1b = cf.id >= last_kf_frame_id + s.min_frames && idle;
         const bool c1c = matches_inliers < n_ref * 0.25 || need_close;
         const bool c2 = ((float)matches_inliers < (float)n_ref * th_ref || need_close) && matches_inliers > 15;
         st.need_kf = (c1a || c1b || c1c) && c2;
-        return st.need_kf != 0;
+        if (!st.need_kf) return false;
+        if (idle) return true;
+        abort_ba = 1;       // mpLocalMapper->InterruptBA()
+        return queued < 3;  // stereo: KeyframesInQueue() < 3
     }
 
     int create_new_keyframe(TrackedFrame& cf) {  // src/Tracking.cc:1251-1330
@@ -528,9 +671,63 @@ struct orbmi_slam {
             if (zi.first > s.th_depth && npts > 100) break;
         }
         create_points(k, cf, fresh);
-        SLAM_CHECK(local_mapping(k));
+        SLAM_CHECK(insert_keyframe(k));
         last_kf_frame_id = cf.id;
         return ORBMI_OK;
+    }
+
+    // LocalMapping::InsertKeyFrame: run it now (synchronous mode) or queue it for the thread
+    int insert_keyframe(int k) {
+        if (!async_lm()) return local_mapping(k);
+        {
+            std::lock_guard<std::mutex> g(q_mtx);
+            if (lm_rc) return lm_rc;
+            lm_queue.push_back(k);
+            abort_ba = 1;  // a new keyframe interrupts the running BA (src/LocalMapping.cc:148)
+        }
+        q_cv.notify_one();
+        return ORBMI_OK;
+    }
+
+    bool new_keyframes_queued() {  // LocalMapping::CheckNewKeyFrames
+        if (!async_lm()) return false;
+        std::lock_guard<std::mutex> g(q_mtx);
+        return !lm_queue.empty();
+    }
+
+    // the mapping thread: one keyframe at a time, holding map_mtx except inside the BA solve
+    void lm_run() {
+        for (;;) {
+            int k;
+            {
+                std::unique_lock<std::mutex> g(q_mtx);
+                q_cv.wait(g, [&] { return lm_quit || !lm_queue.empty(); });
+                if (lm_queue.empty()) return;  // quit with nothing left
+                k = lm_queue.front();
+                lm_queue.pop_front();
+                lm_busy = true;
+            }
+            int rc;
+            {
+                std::unique_lock<std::mutex> m(map_mtx);
+                lm_lock = &m;
+                rc = local_mapping(k);
+                lm_lock = nullptr;
+            }
+            {
+                std::lock_guard<std::mutex> g(q_mtx);
+                lm_busy = false;
+                if (rc && !lm_rc) lm_rc = rc;
+            }
+            idle_cv.notify_all();
+        }
+    }
+
+    int wait_local_mapping() {  // until the queue is empty and the thread idle
+        if (!async_lm()) return ORBMI_OK;
+        std::unique_lock<std::mutex> g(q_mtx);
+        idle_cv.wait(g, [&] { return lm_queue.empty() && !lm_busy; });
+        return lm_rc;
     }
 
     // ---- LocalMapping (synchronous) -------------------------------------------------------------
@@ -556,10 +753,13 @@ struct orbmi_slam {
         map_point_culling(k);
         if (s.local_mapping) {
             SLAM_CHECK(create_new_map_points(k));
-            SLAM_CHECK(search_in_neighbors(k));
+            if (!new_keyframes_queued()) SLAM_CHECK(search_in_neighbors(k));
         }
-        if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
-        if (s.local_mapping) keyframe_culling(k);
+        abort_ba = 0;
+        if (!new_keyframes_queued()) {
+            if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+            if (s.local_mapping) keyframe_culling(k);
+        }
         return ORBMI_OK;
     }
 
@@ -893,7 +1093,15 @@ struct orbmi_slam {
         res.tcw = tcw.data();
         res.pos = pos.data();
         res.erase = erase.data();
-        SLAM_CHECK(orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr));
+        int rc;
+        if (lm_lock) {  // the mapping thread: tracking runs while the GPU solves (mMutexMapUpdate)
+            lm_lock->unlock();
+            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
+            lm_lock->lock();
+        } else {
+            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
+        }
+        SLAM_CHECK(rc);
         ba_calls++;
         for (size_t e = 0; e < E.size(); e++) {
             if (!erase[e]) continue;
@@ -1259,6 +1467,11 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
                                     &h->left);
     if (!rc) rc = orbmi_extractor_create(device, s->n_features, s->scale_factor, s->n_levels, s->ini_th_fast,
                                          s->min_th_fast, &h->right);
+    if (!rc) {
+        void* xs = nullptr;
+        rc = orbmi_extractor_get_stream(h->left, &xs);
+        h->xstream = (hipStream_t)xs;
+    }
     if (!rc) rc = orbmi_matcher_create(device, &h->matcher);
     if (!rc) rc = orbmi_pose_create(device, &h->pose);
     if (!rc) rc = orbmi_ba_create(device, &h->ba);
@@ -1275,12 +1488,28 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
         orbmi_slam_destroy(h);
         return rc;
     }
+    if (h->async_lm()) h->lm_thread = std::thread([h] { h->lm_run(); });
     *out = h;
     return ORBMI_OK;
 }
 
+int orbmi_slam_wait_local_mapping(orbmi_slam* h) {
+    if (!h) return ORBMI_E_ARG;
+    return h->wait_local_mapping();
+}
+
 void orbmi_slam_destroy(orbmi_slam* h) {
     if (!h) return;
+    if (h->lm_thread.joinable()) {  // RequestFinish: the queued keyframes are processed first
+        {
+            std::lock_guard<std::mutex> g(h->q_mtx);
+            h->lm_quit = true;
+        }
+        h->q_cv.notify_all();
+        h->lm_thread.join();
+    }
+    if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+    h->free_dev();
     orbmi_ba_destroy(h->ba);
     orbmi_pose_destroy(h->pose);
     orbmi_matcher_destroy(h->matcher);
@@ -1296,16 +1525,14 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     cf.id = h->frame_count;
     cf.ts = timestamp;
     // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images, ComputeStereoMatches
-    std::vector<orbmi_keypoint> kr;
-    std::vector<uint8_t> dr;
-    SLAM_CHECK(h->extract(h->left, left, rows, cols, step, cf.keys, cf.desc));
-    SLAM_CHECK(h->extract(h->right, right, rows, cols, step, kr, dr));
+    // (touches no map state: outside the map lock)
+    SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    {
+        std::lock_guard<std::mutex> g(h->q_mtx);
+        if (h->lm_rc) return h->lm_rc;
+    }
     const int n = cf.n();
-    cf.ur.assign(std::max(n, 1), -1.f);
-    cf.depth.assign(std::max(n, 1), -1.f);
-    SLAM_CHECK(orbmi_compute_stereo_matches(h->left, 0, h->right, 0, h->s.bf, h->s.fx, cf.ur.data(), cf.depth.data(), n));
-    cf.ur.resize(n);
-    cf.depth.resize(n);
     cf.mps.assign(n, -1);
     cf.outlier.assign(n, 0);
     h->frame_count++;
@@ -1318,12 +1545,14 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
 
 int orbmi_slam_get_stats(orbmi_slam* h, int frame, orbmi_slam_frame_stats* out) {
     if (!h || !out || frame < 0 || frame >= (int)h->stats.size()) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     *out = h->stats[frame];
     return ORBMI_OK;
 }
 
 int orbmi_slam_get_counts(orbmi_slam* h, int* frames, int* keyframes, int* mappoints, int* local_ba_calls) {
     if (!h) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     if (frames) *frames = h->frame_count;
     if (keyframes) *keyframes = (int)h->kfs.size();
     if (mappoints) *mappoints = h->count_mappoints();
@@ -1333,6 +1562,7 @@ int orbmi_slam_get_counts(orbmi_slam* h, int* frames, int* keyframes, int* mappo
 
 int orbmi_slam_get_trajectory(orbmi_slam* h, float* tcw, double* timestamps, uint8_t* lost, int capacity, int* n) {
     if (!h || !n) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     const std::vector<M4> P = h->frame_poses();
     *n = (int)P.size();
     if (capacity < *n) return ORBMI_E_CAP;
@@ -1346,6 +1576,7 @@ int orbmi_slam_get_trajectory(orbmi_slam* h, float* tcw, double* timestamps, uin
 
 int orbmi_slam_save_trajectory_kitti(orbmi_slam* h, const char* path) {  // src/System.cc:433-486
     if (!h || !path) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     FILE* f = std::fopen(path, "w");
     if (!f) return ORBMI_E_ARG;
     for (const M4& T : h->frame_poses()) {
@@ -1359,6 +1590,7 @@ int orbmi_slam_save_trajectory_kitti(orbmi_slam* h, const char* path) {  // src/
 
 int orbmi_slam_save_trajectory_tum(orbmi_slam* h, const char* path) {  // src/System.cc:334-389
     if (!h || !path) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     FILE* f = std::fopen(path, "w");
     if (!f) return ORBMI_E_ARG;
     const std::vector<M4> P = h->frame_poses();
@@ -1377,6 +1609,7 @@ int orbmi_slam_save_trajectory_tum(orbmi_slam* h, const char* path) {  // src/Sy
 
 int orbmi_slam_save_keyframe_trajectory_tum(orbmi_slam* h, const char* path) {  // src/System.cc:392-431
     if (!h || !path) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
     FILE* f = std::fopen(path, "w");
     if (!f) return ORBMI_E_ARG;
     for (const KeyFrame& kf : h->kfs) {

@@ -63,6 +63,45 @@ __device__ inline double wave_reduce_scatter32(double (&v)[32]) {
     return v[0] + dpp_mov<kDppXor1>(v[0]);
 }
 
+// u64 DPP move inside a row of 16 lanes (both halves with the same control)
+template <int CTRL>
+__device__ inline unsigned long long dpp_mov_u64(unsigned long long u) {
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return (unsigned long long)hi << 32 | lo;
+}
+
+// the partner's value across rows (lane ^ 16 for W = 16, lane ^ 32 for W = 32)
+template <int W>
+__device__ inline unsigned long long swap_partner_u64(unsigned long long u) {
+    unsigned xl = (unsigned)u, xh = (unsigned)(u >> 32), yl = xl, yh = xh;
+    if constexpr (W == 32) {
+        auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+        auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+        xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
+    } else {
+        auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+        auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+        xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
+    }
+    // one of the pair is the own value, the other the partner's: min / max need no order
+    const unsigned long long a = (unsigned long long)xh << 32 | xl, b = (unsigned long long)yh << 32 | yl;
+    return a == u ? b : a;
+}
+
+// wave minimum of a u64 key (every lane ends with it) by DPP and permlane swaps: no LDS
+// round trip (a __shfl_xor butterfly is 12 ds_bpermute)
+__device__ inline unsigned long long wave_min_u64_dpp(unsigned long long v) {
+    unsigned long long w;
+    w = dpp_mov_u64<kDppXor1>(v); v = w < v ? w : v;
+    w = dpp_mov_u64<kDppXor2>(v); v = w < v ? w : v;
+    w = dpp_mov_u64<kDppHalfMirror>(v); v = w < v ? w : v;
+    w = dpp_mov_u64<kDppRor8>(v); v = w < v ? w : v;
+    w = swap_partner_u64<16>(v); v = w < v ? w : v;
+    w = swap_partner_u64<32>(v); v = w < v ? w : v;
+    return v;
+}
+
 // all-reduce of one value over the wave (every lane ends with the same sum: each step adds the
 // partner's value, and a + b == b + a)
 __device__ inline double wave_sum(double v) {

@@ -18,7 +18,8 @@ class SlamSettings(C.Structure):
     _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
                 ("th_depth", C.c_float), ("min_frames", C.c_int), ("max_frames", C.c_int), ("width", C.c_int),
                 ("height", C.c_int), ("n_features", C.c_int), ("scale_factor", C.c_float), ("n_levels", C.c_int),
-                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int), ("local_ba", C.c_int), ("local_mapping", C.c_int)]
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int), ("local_ba", C.c_int), ("local_mapping", C.c_int),
+                ("async_local_mapping", C.c_int)]
 
 
 class FrameStats(C.Structure):
@@ -34,7 +35,8 @@ class NativeStereoSLAM:
     """StereoSLAM with the host loop in C++ (orbmi_slam).  `stats` mirrors system.StereoSLAM.stats:
     one dict per frame with the counters the stage that ran produced."""
 
-    def __init__(self, settings, device: int = 0, vocabulary=None, local_ba: bool = True, local_mapping: bool = True):
+    def __init__(self, settings, device: int = 0, vocabulary=None, local_ba: bool = True, local_mapping: bool = True,
+                 async_local_mapping: bool = False):
         from .settings import Settings, load_settings
         s = settings if isinstance(settings, Settings) else load_settings(settings)
         if s.width <= 0 or s.height <= 0:
@@ -47,7 +49,7 @@ class NativeStereoSLAM:
         c = SlamSettings(float(s.fx), float(s.fy), float(s.cx), float(s.cy), float(s.bf), float(s.th_depth),
                          int(s.min_frames), int(s.max_frames), int(s.width), int(s.height), int(s.n_features),
                          float(s.scale_factor), int(s.n_levels), int(s.ini_th_fast), int(s.min_th_fast),
-                         1 if local_ba else 0, 1 if local_mapping else 0)
+                         1 if local_ba else 0, 1 if local_mapping else 0, 1 if async_local_mapping else 0)
         h = C.c_void_p()
         check("orbmi_slam_create", lib().orbmi_slam_create(C.addressof(c), device,
                                                            self._voc._h if self._voc else None, C.byref(h)))
@@ -113,6 +115,10 @@ class NativeStereoSLAM:
     def SaveKeyFrameTrajectoryTUM(self, filename: str):
         check("orbmi_slam_save_keyframe_trajectory_tum",
               lib().orbmi_slam_save_keyframe_trajectory_tum(self._h, filename.encode()))
+
+    def WaitLocalMapping(self):
+        """Block until the mapping thread has processed every queued keyframe (async mode)."""
+        check("orbmi_slam_wait_local_mapping", lib().orbmi_slam_wait_local_mapping(self._h))
 
     def Shutdown(self):
         if getattr(self, "_h", None):

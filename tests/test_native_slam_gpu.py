@@ -83,3 +83,30 @@ def test_native_needs_vocabulary_for_reference_tracking(tmp_path):
         slam.TrackStereo(L, R, 0.1)
     assert e.value.code == ORBMI_E_STATE
     slam.Shutdown()
+
+
+def test_native_concurrent_local_mapping(tmp_path):
+    """LocalMapping on its own thread (the reference's threading, src/System.cc:84-92): keyframe
+    decisions then depend on timing (AcceptKeyFrames, InterruptBA), so the check is the outcome:
+    every frame tracked, keyframes inserted and mapped, LocalBAs run (some possibly interrupted),
+    the trajectory as accurate as the synchronous loop's, and a clean shutdown."""
+    n = 200
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    gt = np.array([fr[2] for fr in frames])
+    sync = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    _drive(sync, frames)
+    ate_sync = ate_rmse(sync.trajectory_twc(), gt)
+    sync.Shutdown()
+    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
+    _drive(slam, frames)
+    slam.WaitLocalMapping()
+    st = slam.stats
+    assert len(st) == n and all(x["state"] == OK for x in st)
+    c = slam.counts()
+    assert c["keyframes"] >= 10 and c["local_ba_calls"] >= 5 and c["mappoints"] > 1000, c
+    ate = ate_rmse(slam.trajectory_twc(), gt)
+    print(f"concurrent LocalMapping: ATE {ate:.4f} m (synchronous {ate_sync:.4f} m), {c}")
+    assert ate < max(2.0 * ate_sync, 0.6), (ate, ate_sync)
+    slam.Shutdown()
