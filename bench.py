@@ -819,6 +819,7 @@ def run_system(a, rank, world, local, dist):
         st = slam.stats
         ok = sum(1 for x in st if x.get("state") == 2)
         counts = slam.counts()
+        counts["phase_ms_per_frame"] = slam.phase_ms()
         slam.Shutdown()
         return times, wait_s, ate, ok, counts
 
@@ -872,6 +873,7 @@ def run_system(a, rank, world, local, dist):
             "ate_rmse_m": round(ate, 5), "frames_tracked": ok, "keyframes": counts["keyframes"],
             "local_ba_calls": counts["local_ba_calls"], "mappoints": counts["mappoints"],
             "local_mapping": "own thread, concurrent with Tracking (the reference's threading)",
+            "phase_ms_per_frame": counts["phase_ms_per_frame"],
             "final_local_mapping_wait_ms": round(wait_s * 1e3, 3),
             "synchronous_local_mapping": {
                 "frames_per_s": round((N - W) / (float(s_times[W:].sum()) + s_wait), 3),
@@ -879,7 +881,7 @@ def run_system(a, rank, world, local, dist):
                              "mean": round(float(np.mean(s_times[W:])) * 1e3, 3),
                              "p90": round(float(np.percentile(s_times[W:], 90)) * 1e3, 3)},
                 "ate_rmse_m": round(s_ate, 5), "frames_tracked": s_ok, "keyframes": s_counts["keyframes"],
-                "local_ba_calls": s_counts["local_ba_calls"]},
+                "local_ba_calls": s_counts["local_ba_calls"], "phase_ms_per_frame": s_counts["phase_ms_per_frame"]},
             "python_host_loop_on_gpu": py, "cpu_baseline": cpu, "host": host_info(),
         }
     return out

@@ -185,6 +185,11 @@ int orbmi_search_by_projection_local(orbmi_matcher* m, const orbmi_frame_view* F
 int orbmi_search_local_points(orbmi_matcher* m, const orbmi_frame_view* F, const uint8_t* occupied,
                               const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp,
                               int* nmatches, int* n_to_match);
+/* The same, also returning every point's isInFrustum outputs (mbTrackInView etc., n_mp entries;
+ * host or device): the caller's IncreaseVisible for the points in view needs no second call. */
+int orbmi_search_local_points_track(orbmi_matcher* m, const orbmi_frame_view* F, const uint8_t* occupied,
+                                    const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp,
+                                    int* nmatches, int* n_to_match, orbmi_mappoint_track* track_out);
 
 /* Last-frame map point view for SearchByProjection(CF, LF): one entry per LF keypoint. */
 #define ORBMI_LF_HAS_MP 1u         /* LastFrame.mvpMapPoints[i] != NULL             */

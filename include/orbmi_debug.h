@@ -33,6 +33,14 @@ int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_
  * evaluations, calls that fell back to the sequential replay}; synchronises the device. */
 int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
 
+/* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame
+ * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
+ * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,
+ * [3] its PoseOptimization, [4] UpdateLocalKeyFrames + UpdateLocalPoints, [5] the local map
+ * points' records, [6] isInFrustum, [7] SearchByProjection(F, local points), [8] its
+ * PoseOptimization, [9] CreateNewKeyFrame (+ LocalMapping when synchronous), [10] total. */
+int orbmi_slam_get_phase_ms(orbmi_slam* h, double* ms, int n, long* frames);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,7 @@ _PROTOS = {
     "orbmi_is_in_frustum": (_i, [_vp, _vp, _vp, _i, _f, _vp]),
     "orbmi_search_by_projection_local": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _f, _f, _vp, C.POINTER(_i)]),
     "orbmi_search_local_points": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, C.POINTER(_i), C.POINTER(_i)]),
+    "orbmi_search_local_points_track": (_i, [_vp, _vp, _vp, _vp, _i, _f, _vp, C.POINTER(_i), C.POINTER(_i), _vp]),
     "orbmi_search_by_projection_last_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, C.POINTER(_i)]),
     "orbmi_search_by_bow": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, C.POINTER(_i)]),
     "orbmi_ba_create": (_i, [_i, C.POINTER(_vp)]),
@@ -106,6 +107,7 @@ _PROTOS = {
     "orbmi_slam_create": (_i, [_vp, _i, _vp, C.POINTER(_vp)]),
     "orbmi_slam_destroy": (None, [_vp]),
     "orbmi_slam_wait_local_mapping": (_i, [_vp]),
+    "orbmi_slam_get_phase_ms": (_i, [_vp, _vp, _i, C.POINTER(C.c_long)]),
     "orbmi_slam_track_stereo": (_i, [_vp, _vp, _vp, _i, _i, _sz, C.c_double, _vp, C.POINTER(_i)]),
     "orbmi_slam_get_stats": (_i, [_vp, _i, _vp]),
     "orbmi_slam_get_counts": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),

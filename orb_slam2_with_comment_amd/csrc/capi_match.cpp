@@ -298,6 +298,12 @@ int orbmi_search_by_projection_local(orbmi_matcher* h, const orbmi_frame_view* v
 int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
                               const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp, int* nmatches,
                               int* n_to_match) {
+    return orbmi_search_local_points_track(h, v, occupied, mps, n_mp, th, match_mp, nmatches, n_to_match, nullptr);
+}
+
+int orbmi_search_local_points_track(orbmi_matcher* h, const orbmi_frame_view* v, const uint8_t* occupied,
+                                    const orbmi_mappoint* mps, int n_mp, float th, int32_t* match_mp, int* nmatches,
+                                    int* n_to_match, orbmi_mappoint_track* track_out) {
     if (!h || !occupied || !match_mp || n_mp < 0 || (n_mp > 0 && !mps)) return ORBMI_E_ARG;
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
@@ -311,9 +317,14 @@ int orbmi_search_local_points(orbmi_matcher* h, const orbmi_frame_view* v, const
     // k_greedy stores the match count (slot 0) unconditionally; only the nToMatch counter (slot 1,
     // atomics in k_frustum) needs zeroing, and only when the caller asks for it
     if ((rc = n_to_match ? scalars(m) : orbmi::ensure_buf(&m.d_scalars, &m.cap_scalars, 4))) return rc;
-    if ((rc = orbmi::ensure_buf(&m.d_track, &m.cap_track, (size_t)std::max(n_mp, 1)))) return rc;
-    orbmi_mappoint_track* d_tr = m.d_track;
     std::vector<OutBuf> outs;
+    orbmi_mappoint_track* d_tr = nullptr;
+    if (track_out) {  // the isInFrustum outputs go to the caller (host: copied back with the matches)
+        d_tr = dev_out(m, track_out, (size_t)std::max(n_mp, 1), outs);
+    } else {
+        if ((rc = orbmi::ensure_buf(&m.d_track, &m.cap_track, (size_t)std::max(n_mp, 1)))) return rc;
+        d_tr = m.d_track;
+    }
     int* d_out = dev_out(m, match_mp, (size_t)F.n, outs);
     // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5); ORBmatcher matcher(0.8)
     if ((rc = orbmi::launch_frustum(m, F, d_mps, n_mp, 0.5f, d_tr, n_to_match ? m.d_scalars + 1 : nullptr))) return rc;

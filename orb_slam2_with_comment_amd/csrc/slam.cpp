@@ -23,6 +23,7 @@
 // Compiled with -ffp-contract=off: one rounding per float operation, as numpy does.
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <deque>
@@ -134,6 +135,11 @@ struct KeyFrame {
     bool bad = false;
     int fuse_target_for_kf = -1;  // mnFuseTargetForKF
     M4 tcp{};                    // mTcp, set when the keyframe turns bad
+    // device copies of keys / desc / u_right (one block): the searches read the keyframe in place
+    uint8_t* d_block = nullptr;
+    const orbmi_keypoint* d_keys = nullptr;
+    const uint8_t* d_desc = nullptr;
+    const float* d_ur = nullptr;
 };
 
 struct MapPoint {
@@ -170,11 +176,24 @@ struct TrackedFrame {
 
 enum { NO_IMAGES_YET = 0, NOT_INITIALIZED = 1, OK = 2, LOST = 3 };
 
+// wall time per phase of orbmi_slam_track_stereo (orbmi_slam_get_phase_ms; names in orbmi_debug.h)
+enum Phase { PH_FRAME, PH_LOCK, PH_LF_SEARCH, PH_LF_POSE, PH_LOCAL_UPDATE, PH_LOCAL_RECORDS, PH_FRUSTUM,
+             PH_LOCAL_SEARCH, PH_LOCAL_POSE, PH_KEYFRAME, PH_TOTAL, PH_COUNT };
+struct PhaseTimer {
+    double* acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit PhaseTimer(double* a) : acc(a) {}
+    ~PhaseTimer() { *acc += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
 #define SLAM_CHECK(call)              \
     do {                              \
         const int rc_ = (call);       \
         if (rc_ != ORBMI_OK) return rc_; \
     } while (0)
+
+// the mapping thread's hold on its system's map_mtx (null on every other thread)
+thread_local std::unique_lock<std::mutex>* lm_lock = nullptr;
 
 }  // namespace
 
@@ -202,7 +221,20 @@ struct orbmi_slam {
     int last_kf_frame_id = 0, last_reloc_frame_id = 0;
     std::vector<int> local_kfs, local_mps;
     int matches_inliers = 0;
-    std::set<int> seen;          // mnLastFrameSeen == current frame
+    // mnLastFrameSeen == current frame, as a generation stamp per map point (O(1) insert / test /
+    // clear instead of a std::set over thousands of points per frame)
+    struct SeenSet {
+        std::vector<int> mark;
+        int gen = 1;
+        void clear() { gen++; }
+        void insert(int m) {
+            if (m >= (int)mark.size()) mark.resize(std::max<size_t>(2 * mark.size(), m + 1), 0);
+            mark[m] = gen;
+        }
+        bool count(int m) const { return m < (int)mark.size() && mark[m] == gen; }
+    } seen;
+    SeenSet local_mark;           // UpdateLocalPoints' mnTrackReferenceForFrame
+    std::vector<int> kf_counter;  // UpdateLocalKeyFrames' keyframe counter (indexed by id)
     // mlRelativeFramePoses, mlpReferences, mlFrameTimes, mlbLost
     std::vector<M4> rel_poses;
     std::vector<int> references;
@@ -238,6 +270,8 @@ struct orbmi_slam {
         float* h_dep = nullptr;
     } dev;
     hipStream_t xstream = nullptr;  // the left extractor's stream
+    double phase_ms[PH_COUNT] = {};
+    long phase_frames = 0;
 
     // ---- LocalMapping on its own thread (settings.async_local_mapping, src/LocalMapping.cc:47-128)
     // The map and the handles both threads call (matcher, vocabulary) are guarded by map_mtx:
@@ -254,7 +288,6 @@ struct orbmi_slam {
     int lm_rc = ORBMI_OK;       // the first error of the mapping thread
     volatile int abort_ba = 0;  // mbAbortBA
     std::thread lm_thread;
-    std::unique_lock<std::mutex>* lm_lock = nullptr;  // the mapping thread's hold on map_mtx
     bool async_lm() const { return s.async_local_mapping != 0; }
 
     // ---- Frame views (include/Frame.h members the matchers read) --------------------------
@@ -543,7 +576,10 @@ struct orbmi_slam {
         const int np = (int)pts.size();
         std::vector<int32_t> best(std::max(np, 1));
         std::vector<uint8_t> out((size_t)std::max(np, 1) * 32);
-        SLAM_CHECK(orbmi_compute_distinctive_descriptors(matcher, rows.data(), off.data(), np, best.data(), out.data()));
+        orbmi_matcher* mt = lmm();
+        SLAM_CHECK(unlocked([&] {
+            return orbmi_compute_distinctive_descriptors(mt, rows.data(), off.data(), np, best.data(), out.data());
+        }));
         for (int j = 0; j < np; j++)
             if (off[j + 1] > off[j]) std::memcpy(mps[pts[j]].desc, &out[32 * j], 32);
         return ORBMI_OK;
@@ -562,8 +598,48 @@ struct orbmi_slam {
         kf.depth = cf.depth;
         kf.mps = cf.mps;
         kf.fv = cf.fv;
+        // the keyframe's arrays in HBM, copied once (from the frame's device slot when it has one)
+        const size_t n = kf.keys.size(), bk = n * sizeof(orbmi_keypoint), bd = n * 32, bu = n * sizeof(float);
+        if (n > 0 && hipMalloc((void**)&kf.d_block, bk + bd + bu) == hipSuccess) {
+            const bool dslot = cf.dslot >= 0;
+            const hipMemcpyKind kind = dslot ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+            const void* sk = dslot ? (const void*)dev.kps[cf.dslot] : (const void*)kf.keys.data();
+            const void* sd = dslot ? (const void*)dev.desc[cf.dslot] : (const void*)kf.desc.data();
+            const void* su = dslot ? (const void*)dev.ur[cf.dslot] : (const void*)kf.ur.data();
+            if (hipMemcpy(kf.d_block, sk, bk, kind) == hipSuccess && hipMemcpy(kf.d_block + bk, sd, bd, kind) == hipSuccess &&
+                hipMemcpy(kf.d_block + bk + bd, su, bu, kind) == hipSuccess) {
+                kf.d_keys = (const orbmi_keypoint*)kf.d_block;
+                kf.d_desc = kf.d_block + bk;
+                kf.d_ur = (const float*)(kf.d_block + bk + bd);
+            }
+        }
         kfs.push_back(std::move(kf));
         return (int)kfs.size() - 1;
+    }
+
+    // KeyFrame view for the searches: its HBM copy when there is one; tcw points at `tcw_copy`
+    // (the caller's copy: the keyframe's own pose may move while the map lock is released)
+    orbmi_frame_view kf_view(const KeyFrame& kf, const float* tcw) const {
+        orbmi_frame_view v = view(kf.keys, kf.desc, kf.ur, tcw);
+        if (kf.d_keys) {
+            v.keys_un = kf.d_keys;
+            v.desc = kf.d_desc;
+            v.u_right = kf.d_ur;
+        }
+        return v;
+    }
+
+    // LocalMapping's GPU calls: on the mapping thread they use its own matcher and run with the
+    // map lock released (their inputs are the caller's copies or the keyframes' HBM copies)
+    orbmi_matcher* lm_matcher = nullptr;
+    orbmi_matcher* lmm() const { return lm_lock ? lm_matcher : matcher; }
+    template <class F>
+    int unlocked(F f) {
+        if (!lm_lock) return f();
+        lm_lock->unlock();
+        const int rc = f();
+        lm_lock->lock();
+        return rc;
     }
 
     // Frame::UnprojectStereo (src/Frame.cc:701-715) + new MapPoint + AddObservation + AddMapPoint
@@ -781,44 +857,53 @@ struct orbmi_slam {
                                   s.cy, s.bf, s.bf / s.fx, level_sigma2.data(), scale_factors.data()};
     }
 
-    // src/LocalMapping.cc:290-577, stereo: the 10 best covisible keyframes
+    // src/LocalMapping.cc:290-577, stereo: the 10 best covisible keyframes.  Each pair's search
+    // runs on the keyframes' HBM copies with the map lock released (on the mapping thread); the
+    // views into `kfs` are taken again after it, as the tracker may have grown the vector.
     int create_new_map_points(int k) {
         float ow1[3];
         kf_ow(k, ow1);
-        const orbmi_tri_keyframe v1 = tri_view(kfs[k]);
         const float mb = s.bf / s.fx;
         std::vector<uint8_t> has1(std::max<size_t>(kfs[k].mps.size(), 1), 0);
         for (size_t i = 0; i < kfs[k].mps.size(); i++) has1[i] = kfs[k].mps[i] >= 0;
         const std::vector<int> neigh(kfs[k].covisible.begin(),
                                      kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
+        const size_t n1 = kfs[k].keys.size();
         for (int k2 : neigh) {
             float ow2[3];
             kf_ow(k2, ow2);
             const float d[3] = {ow2[0] - ow1[0], ow2[1] - ow1[1], ow2[2] - ow1[2]};
             const float baseline = (float)std::sqrt(((double)d[0] * d[0] + (double)d[1] * d[1]) + (double)d[2] * d[2]);
             if (baseline < mb) continue;
-            const orbmi_tri_keyframe v2 = tri_view(kfs[k2]);
             float F12[9];
-            SLAM_CHECK(orbmi_compute_f12(&v1, &v2, F12));
+            {
+                const orbmi_tri_keyframe v1 = tri_view(kfs[k]), v2 = tri_view(kfs[k2]);
+                SLAM_CHECK(orbmi_compute_f12(&v1, &v2, F12));
+            }
             if (!kfs[k].fv.valid || !kfs[k2].fv.valid) continue;
             std::vector<uint8_t> has2(std::max<size_t>(kfs[k2].mps.size(), 1), 0);
             for (size_t i = 0; i < kfs[k2].mps.size(); i++) has2[i] = kfs[k2].mps[i] >= 0;
-            const KeyFrame &K1 = kfs[k], &K2 = kfs[k2];
-            const orbmi_frame_view f1 = view(K1.keys, K1.desc, K1.ur, K1.tcw.data());
-            const orbmi_frame_view f2 = view(K2.keys, K2.desc, K2.ur, K2.tcw.data());
-            const orbmi_feature_vector fv1 = K1.fv.view(), fv2 = K2.fv.view();
-            std::vector<int32_t> m12(std::max<size_t>(K1.keys.size(), 1));
+            const M4 tcw1 = kfs[k].tcw, tcw2 = kfs[k2].tcw;
+            const orbmi_frame_view f1 = kf_view(kfs[k], tcw1.data()), f2 = kf_view(kfs[k2], tcw2.data());
+            const orbmi_feature_vector fv1 = kfs[k].fv.view(), fv2 = kfs[k2].fv.view();
+            std::vector<int32_t> m12(std::max<size_t>(n1, 1));
             int nm = 0;
-            SLAM_CHECK(orbmi_search_for_triangulation(matcher, &f1, has1.data(), &fv1, &f2, has2.data(), &fv2, F12, 0, 0,
-                                                      m12.data(), &nm));
+            orbmi_matcher* mt = lmm();
+            SLAM_CHECK(unlocked([&] {
+                return orbmi_search_for_triangulation(mt, &f1, has1.data(), &fv1, &f2, has2.data(), &fv2, F12, 0, 0,
+                                                      m12.data(), &nm);
+            }));
             std::vector<int32_t> idx1, idx2;
-            for (size_t i = 0; i < K1.keys.size(); i++)
+            for (size_t i = 0; i < n1; i++)
                 if (m12[i] >= 0) { idx1.push_back((int32_t)i); idx2.push_back(m12[i]); }
             if (idx1.empty()) continue;
             std::vector<float> x3d(3 * idx1.size());
             std::vector<uint8_t> ok(idx1.size());
-            SLAM_CHECK(orbmi_triangulate_matches(&v1, &v2, idx1.data(), idx2.data(), (int)idx1.size(), x3d.data(),
-                                                 ok.data()));
+            {
+                const orbmi_tri_keyframe v1 = tri_view(kfs[k]), v2 = tri_view(kfs[k2]);
+                SLAM_CHECK(orbmi_triangulate_matches(&v1, &v2, idx1.data(), idx2.data(), (int)idx1.size(), x3d.data(),
+                                                     ok.data()));
+            }
             std::vector<int> fresh;
             for (size_t q = 0; q < idx1.size(); q++) {
                 if (!ok[q]) continue;
@@ -891,12 +976,14 @@ struct orbmi_slam {
             std::memcpy(r.desc, mp.desc, 32);
             in_kf[j] = mp.obs.count(k) ? 1 : 0;
         }
-        const KeyFrame& kf = kfs[k];
-        const orbmi_frame_view v = view(kf.keys, kf.desc, kf.ur, kf.tcw.data());
+        const M4 tcw = kfs[k].tcw;
+        const orbmi_frame_view v = kf_view(kfs[k], tcw.data());
         std::vector<int32_t> best(pts.size()), dist(pts.size());
         int nc = 0;
-        SLAM_CHECK(orbmi_fuse_search(matcher, &v, rec.data(), in_kf.data(), (int)pts.size(), 3.f, best.data(), dist.data(),
-                                     &nc));
+        orbmi_matcher* mt = lmm();
+        SLAM_CHECK(unlocked([&] {
+            return orbmi_fuse_search(mt, &v, rec.data(), in_kf.data(), (int)pts.size(), 3.f, best.data(), dist.data(), &nc);
+        }));
         for (size_t j = 0; j < pts.size(); j++) {
             const int m = pts[j], b = best[j];
             if (mps[m].bad || mps[m].obs.count(k) || b < 0) continue;
@@ -1213,10 +1300,14 @@ struct orbmi_slam {
         std::vector<int32_t> m(std::max(cf.n(), 1));
         int n = 0;
         const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
-        SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1, m.data(), &n));
-        if (n < 20)
-            SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), 2 * th, 0, 1,
-                                                             m.data(), &n));
+        {
+            PhaseTimer pt(&phase_ms[PH_LF_SEARCH]);
+            SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1, m.data(),
+                                                             &n));
+            if (n < 20)
+                SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), 2 * th, 0, 1,
+                                                                 m.data(), &n));
+        }
         st.track = 1;
         st.lf_matches = n;
         if (n < 20) return ORBMI_OK;
@@ -1224,7 +1315,10 @@ struct orbmi_slam {
         m.resize(cf.n());
         M4 tcw;
         std::vector<uint8_t> out;
-        SLAM_CHECK(pose_optimization(cf, m, lfp, tcw, out));
+        {
+            PhaseTimer pt(&phase_ms[PH_LF_POSE]);
+            SLAM_CHECK(pose_optimization(cf, m, lfp, tcw, out));
+        }
         cf.tcw = tcw;
         cf.outlier = out;
         seen.clear();
@@ -1235,22 +1329,29 @@ struct orbmi_slam {
     }
 
     void update_local_keyframes(TrackedFrame& cf) {  // src/Tracking.cc:1452-1580
-        std::map<int, int> counter;
+        // keyframe counter in keyframe-id order (the std::map<KeyFrame*, int> of the reference,
+        // id-ordered here): counts per id, touched ids sorted
+        if (kf_counter.size() < kfs.size()) kf_counter.resize(kfs.size(), 0);
+        std::vector<int> touched;
         for (int i = 0; i < cf.n(); i++) {
             const int m = cf.mps[i];
             if (m < 0) continue;
             if (mps[m].bad) { cf.mps[i] = -1; continue; }
-            for (auto& o : mps[m].obs) counter[o.first]++;
+            for (auto& o : mps[m].obs)
+                if (kf_counter[o.first]++ == 0) touched.push_back(o.first);
         }
-        if (counter.empty()) return;
+        if (touched.empty()) return;
+        std::sort(touched.begin(), touched.end());
         int best = 0, kfmax = -1;
         std::vector<int> local;
         std::set<int> mark;
-        for (auto& c : counter) {
-            if (kfs[c.first].bad) continue;
-            if (c.second > best) { best = c.second; kfmax = c.first; }
-            local.push_back(c.first);
-            mark.insert(c.first);
+        for (int id : touched) {
+            const int cnt = kf_counter[id];
+            kf_counter[id] = 0;
+            if (kfs[id].bad) continue;
+            if (cnt > best) { best = cnt; kfmax = id; }
+            local.push_back(id);
+            mark.insert(id);
         }
         size_t i = 0;
         while (i < local.size()) {
@@ -1280,20 +1381,23 @@ struct orbmi_slam {
 
     void update_local_points() {  // src/Tracking.cc:1421-1450
         std::vector<int> out;
-        std::set<int> mark;
+        local_mark.clear();
         for (int k : local_kfs)
             for (int m : kfs[k].mps)
-                if (m >= 0 && !mark.count(m) && !mps[m].bad) {
+                if (m >= 0 && !local_mark.count(m) && !mps[m].bad) {
                     out.push_back(m);
-                    mark.insert(m);
+                    local_mark.insert(m);
                 }
-        local_mps = out;
+        local_mps.swap(out);
     }
 
     int track_local_map(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:1075-1104
         ok = false;
-        update_local_keyframes(cf);
-        update_local_points();
+        {
+            PhaseTimer pt(&phase_ms[PH_LOCAL_UPDATE]);
+            update_local_keyframes(cf);
+            update_local_points();
+        }
         std::vector<uint8_t> occ(std::max(cf.n(), 1), 0);
         for (int i = 0; i < cf.n(); i++) {  // SearchLocalPoints' first loop
             const int m = cf.mps[i];
@@ -1305,19 +1409,22 @@ struct orbmi_slam {
                 occ[i] = mps[m].nobs > 0 ? 1 : 0;
             }
         }
+        PhaseTimer* ptr = new PhaseTimer(&phase_ms[PH_LOCAL_RECORDS]);
         const std::vector<orbmi_mappoint> rec = mp_records(local_mps);
+        delete ptr;
         const orbmi_frame_view vc = view(cf, cf.tcw.data());
         std::vector<int32_t> m_mp(std::max(cf.n(), 1), -1);
         int nl = 0;
-        // isInFrustum(0.5) -> IncreaseVisible, then SearchByProjection(F, points, th = 1), 0.8
+        // isInFrustum(0.5) -> IncreaseVisible, then SearchByProjection(F, points, th = 1), 0.8: one
+        // fused call (with no point in view the search finds nothing, as the reference's skipped one)
         std::vector<orbmi_mappoint_track> tr(std::max<size_t>(rec.size(), 1));
-        SLAM_CHECK(orbmi_is_in_frustum(matcher, &vc, rec.data(), (int)rec.size(), 0.5f, tr.data()));
-        int n_in = 0;
+        {
+            PhaseTimer pt(&phase_ms[PH_LOCAL_SEARCH]);
+            SLAM_CHECK(orbmi_search_local_points_track(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f,
+                                                       m_mp.data(), &nl, nullptr, tr.data()));
+        }
         for (size_t j = 0; j < rec.size(); j++)
-            if (tr[j].in_view) { mps[local_mps[j]].visible++; n_in++; }
-        if (n_in > 0)
-            SLAM_CHECK(orbmi_search_by_projection_local(matcher, &vc, occ.data(), rec.data(), tr.data(), (int)rec.size(), 1.f,
-                                                        0.8f, m_mp.data(), &nl));
+            if (tr[j].in_view) mps[local_mps[j]].visible++;
         st.local_map_points = (int)local_mps.size();
         st.local_matches = nl;
         std::vector<int> cur = cf.mps;
@@ -1329,7 +1436,10 @@ struct orbmi_slam {
             if (cur[i] >= 0) m_lf[i] = i;
         M4 tcw;
         std::vector<uint8_t> out;
-        SLAM_CHECK(pose_optimization(cf, m_lf, lfp, tcw, out));
+        {
+            PhaseTimer pt(&phase_ms[PH_LOCAL_POSE]);
+            SLAM_CHECK(pose_optimization(cf, m_lf, lfp, tcw, out));
+        }
         cf.tcw = tcw;
         cf.mps = cur;
         cf.outlier = out;
@@ -1395,7 +1505,10 @@ struct orbmi_slam {
                         cf.mps[i] = -1;
                     }
                 }
-                if (need_new_keyframe(cf, st)) SLAM_CHECK(create_new_keyframe(cf));
+                if (need_new_keyframe(cf, st)) {
+                    PhaseTimer pt(&phase_ms[PH_KEYFRAME]);
+                    SLAM_CHECK(create_new_keyframe(cf));
+                }
                 for (int i = 0; i < cf.n(); i++)  // (:535-539)
                     if (cf.mps[i] >= 0 && cf.outlier[i]) cf.mps[i] = -1;
             }
@@ -1473,6 +1586,7 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
         h->xstream = (hipStream_t)xs;
     }
     if (!rc) rc = orbmi_matcher_create(device, &h->matcher);
+    if (!rc && s->async_local_mapping) rc = orbmi_matcher_create(device, &h->lm_matcher);
     if (!rc) rc = orbmi_pose_create(device, &h->pose);
     if (!rc) rc = orbmi_ba_create(device, &h->ba);
     if (!rc) {
@@ -1513,6 +1627,9 @@ void orbmi_slam_destroy(orbmi_slam* h) {
     orbmi_ba_destroy(h->ba);
     orbmi_pose_destroy(h->pose);
     orbmi_matcher_destroy(h->matcher);
+    if (h->lm_matcher) orbmi_matcher_destroy(h->lm_matcher);
+    for (auto& kf : h->kfs)
+        if (kf.d_block) (void)hipFree(kf.d_block);
     orbmi_extractor_destroy(h->right);
     orbmi_extractor_destroy(h->left);
     delete h;
@@ -1526,8 +1643,15 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     cf.ts = timestamp;
     // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images, ComputeStereoMatches
     // (touches no map state: outside the map lock)
-    SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
+    PhaseTimer total(&h->phase_ms[PH_TOTAL]);
+    h->phase_frames++;
+    {
+        PhaseTimer pt(&h->phase_ms[PH_FRAME]);
+        SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
+    }
+    PhaseTimer* lock_t = new PhaseTimer(&h->phase_ms[PH_LOCK]);
     std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    delete lock_t;
     {
         std::lock_guard<std::mutex> g(h->q_mtx);
         if (h->lm_rc) return h->lm_rc;
@@ -1621,6 +1745,13 @@ int orbmi_slam_save_keyframe_trajectory_tum(orbmi_slam* h, const char* path) {  
         std::fprintf(f, "%.6f %.7f %.7f %.7f %.7f %.7f %.7f %.7f\n", kf.ts, W[3], W[7], W[11], q[0], q[1], q[2], q[3]);
     }
     std::fclose(f);
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_phase_ms(orbmi_slam* h, double* ms, int n, long* frames) {
+    if (!h || !ms || n < 0) return ORBMI_E_ARG;
+    for (int i = 0; i < n && i < PH_COUNT; i++) ms[i] = h->phase_ms[i];
+    if (frames) *frames = h->phase_frames;
     return ORBMI_OK;
 }
 

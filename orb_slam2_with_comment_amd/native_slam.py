@@ -116,6 +116,16 @@ class NativeStereoSLAM:
         check("orbmi_slam_save_keyframe_trajectory_tum",
               lib().orbmi_slam_save_keyframe_trajectory_tum(self._h, filename.encode()))
 
+    PHASES = ("frame_ctor", "map_lock_wait", "lf_search", "lf_pose", "local_kf_points", "local_records",
+              "frustum", "local_search", "local_pose", "keyframe", "total")
+
+    def phase_ms(self):
+        """Mean wall ms per tracked frame of each phase of TrackStereo (orbmi_slam_get_phase_ms)."""
+        ms = np.zeros(len(self.PHASES))
+        n = C.c_long()
+        check("orbmi_slam_get_phase_ms", lib().orbmi_slam_get_phase_ms(self._h, ms.ctypes.data, len(ms), C.byref(n)))
+        return {k: round(float(v) / max(n.value, 1), 4) for k, v in zip(self.PHASES, ms)}
+
     def WaitLocalMapping(self):
         """Block until the mapping thread has processed every queued keyframe (async mode)."""
         check("orbmi_slam_wait_local_mapping", lib().orbmi_slam_wait_local_mapping(self._h))
