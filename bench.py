@@ -819,7 +819,11 @@ def run_system(a, rank, world, local, dist):
         st = slam.stats
         ok = sum(1 for x in st if x.get("state") == 2)
         counts = slam.counts()
-        counts["phase_ms_per_frame"] = slam.phase_ms()
+        ph = slam.phase_ms()
+        counts["phase_ms_per_frame"] = {k: v for k, v in ph.items() if not k.startswith("lm_")}
+        per_kf = len(st) / max(counts["keyframes"] - 1, 1)  # the first keyframe is not mapped
+        counts["local_mapping_ms_per_keyframe"] = {k[3:]: round(v * per_kf, 4) for k, v in ph.items()
+                                                   if k.startswith("lm_")}
         slam.Shutdown()
         return times, wait_s, ate, ok, counts
 
@@ -874,6 +878,7 @@ def run_system(a, rank, world, local, dist):
             "local_ba_calls": counts["local_ba_calls"], "mappoints": counts["mappoints"],
             "local_mapping": "own thread, concurrent with Tracking (the reference's threading)",
             "phase_ms_per_frame": counts["phase_ms_per_frame"],
+            "local_mapping_ms_per_keyframe": counts["local_mapping_ms_per_keyframe"],
             "final_local_mapping_wait_ms": round(wait_s * 1e3, 3),
             "synchronous_local_mapping": {
                 "frames_per_s": round((N - W) / (float(s_times[W:].sum()) + s_wait), 3),
@@ -881,7 +886,8 @@ def run_system(a, rank, world, local, dist):
                              "mean": round(float(np.mean(s_times[W:])) * 1e3, 3),
                              "p90": round(float(np.percentile(s_times[W:], 90)) * 1e3, 3)},
                 "ate_rmse_m": round(s_ate, 5), "frames_tracked": s_ok, "keyframes": s_counts["keyframes"],
-                "local_ba_calls": s_counts["local_ba_calls"], "phase_ms_per_frame": s_counts["phase_ms_per_frame"]},
+                "local_ba_calls": s_counts["local_ba_calls"], "phase_ms_per_frame": s_counts["phase_ms_per_frame"],
+                "local_mapping_ms_per_keyframe": s_counts["local_mapping_ms_per_keyframe"]},
             "python_host_loop_on_gpu": py, "cpu_baseline": cpu, "host": host_info(),
         }
     return out

@@ -276,6 +276,19 @@ int orbmi_fuse_search_batch(orbmi_matcher* m, int nkf, const orbmi_frame_view* k
                             const uint8_t* in_kf, int n_mp, float th, int32_t* best_idx, int32_t* best_dist,
                             int* ncandidates);
 
+/* SearchInNeighbors between two Fuse targets (src/LocalMapping.cc:620-628): the
+ * ComputeDistinctiveDescriptors that MapPoint::Replace owes its survivors (src/MapPoint.cc:212),
+ * then the Fuse searches of the records whose descriptor that changed -- one synchronisation.
+ * orbmi_compute_distinctive_descriptors of nd points (obs_desc, obs_off, best, desc_out as
+ * there; nd may be 0), then orbmi_fuse_search_batch of n_mp records against nkf keyframes
+ * (kfs, in_kf, th, best_idx, best_dist as there), record i searched with descriptor
+ * desc_out[desc_from[i]] when desc_from (may be NULL) has desc_from[i] >= 0.  `mps` is read,
+ * not written. */
+int orbmi_fuse_search_refresh(orbmi_matcher* m, const uint8_t* obs_desc, const int32_t* obs_off, int nd, int32_t* best,
+                              uint8_t* desc_out, int nkf, const orbmi_frame_view* kfs, const orbmi_mappoint* mps,
+                              const int32_t* desc_from, const uint8_t* in_kf, int n_mp, float th, int32_t* best_idx,
+                              int32_t* best_dist);
+
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:247-316) for np map points: the
  * observation descriptors of point p are rows obs_off[p] .. obs_off[p + 1] - 1 of obs_desc
  * (x 32 B), in mObservations order with bad keyframes left out by the caller (the reference
@@ -523,6 +536,34 @@ int orbmi_compute_f12(const orbmi_tri_keyframe* kf1, const orbmi_tri_keyframe* k
  * scale consistency.  ok[k] = 1 with x3d[3k..3k+2] the new point's world position, else 0. */
 int orbmi_triangulate_matches(const orbmi_tri_keyframe* kf1, const orbmi_tri_keyframe* kf2, const int32_t* idx1,
                               const int32_t* idx2, int n, float* x3d, uint8_t* ok);
+
+/* cos(2 atan2(mb / 2, depth[i])) as float for n keypoints: CreateNewMapPoints' stereo parallax
+ * of a stereo keypoint (src/LocalMapping.cc:409-412), a per-keyframe table for
+ * orbmi_create_new_map_points. */
+int orbmi_stereo_parallax_cos(float mb, const float* depth, int n, float* out);
+
+/* LocalMapping::CreateNewMapPoints' searches and geometry (src/LocalMapping.cc:290-577) for one
+ * keyframe and npairs neighbours (in the order the reference visits them, the baseline test
+ * already applied), all on the device with one synchronisation: pair j's SearchForTriangulation
+ * (as orbmi_search_for_triangulation with bOnlyStereo = false and the matcher's
+ * mbCheckOrientation = false, ORBmatcher matcher(0.6, false) at :306) sees KF1's map points as
+ * the pairs before it left them -- a KF1 keypoint whose match an earlier pair's triangulation
+ * accepted counts as having a map point, exactly as in the reference's loop -- and the pair's
+ * matches are then tested as orbmi_triangulate_matches does.
+ * kf1 / kf2[j]: frame views (keys_un, u_right, desc host or device; tcw host); tri1 / tri2[j]:
+ * the geometry, of which tcw, depth (host or device, n entries), the intrinsics, level_sigma2
+ * and scale_factors (host, nlevels of the frame view) are read; cos1 / cos2[j]: the keyframe's
+ * orbmi_stereo_parallax_cos table (host or device), or NULL to compute it here from a host depth.
+ * has_mp1 / has_mp2[j]: the keyframes' map points on entry (not modified).
+ * Outputs (host or device), row j * kf1->n + i for pair j and KF1 keypoint i: match12 = the
+ * KF2 keypoint SearchForTriangulation paired with i, or -1; ok = 1 when the geometry accepted a
+ * new map point; x3d[3 * row ..] = its world position (unspecified where ok = 0). */
+int orbmi_create_new_map_points(orbmi_matcher* m, const orbmi_frame_view* kf1, const orbmi_tri_keyframe* tri1,
+                                const float* cos1, const uint8_t* has_mp1, const orbmi_feature_vector* fv1,
+                                int npairs, const orbmi_frame_view* kf2, const orbmi_tri_keyframe* tri2,
+                                const float* const* cos2, const uint8_t* const* has_mp2,
+                                const orbmi_feature_vector* fv2, const float* F12, int32_t* match12, uint8_t* ok,
+                                float* x3d);
 
 /* ---- System::TrackStereo: the native stereo SLAM host loop ---------------------------- */
 

@@ -37,8 +37,13 @@ int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
  * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
  * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,
  * [3] its PoseOptimization, [4] UpdateLocalKeyFrames + UpdateLocalPoints, [5] the local map
- * points' records, [6] isInFrustum, [7] SearchByProjection(F, local points), [8] its
- * PoseOptimization, [9] CreateNewKeyFrame (+ LocalMapping when synchronous), [10] total. */
+ * points' records, [6] unused (isInFrustum runs inside [7]), [7] SearchByProjection(F, local
+ * points), [8] its PoseOptimization, [9] CreateNewKeyFrame (+ LocalMapping when synchronous),
+ * [10] total; then LocalMapping::Run on whichever thread runs it: [11] ProcessNewKeyFrame,
+ * [12] MapPointCulling, [13] CreateNewMapPoints, [14] SearchInNeighbors, [15]
+ * LocalBundleAdjustment, [16] KeyFrameCulling, [17] all of LocalMapping::Run; within those,
+ * [18] the orbmi_create_new_map_points calls, [19] the Fuse search calls, [20] the
+ * ComputeDistinctiveDescriptors calls. */
 int orbmi_slam_get_phase_ms(orbmi_slam* h, double* ms, int n, long* frames);
 
 #ifdef __cplusplus

@@ -104,6 +104,10 @@ _PROTOS = {
     "orbmi_debug_greedy_stats": (_i, [_vp, _i]),
     "orbmi_compute_f12": (_i, [_vp, _vp, _vp]),
     "orbmi_triangulate_matches": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
+    "orbmi_stereo_parallax_cos": (_i, [C.c_float, _vp, _i, _vp]),
+    "orbmi_fuse_search_refresh": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, C.c_float, _vp, _vp]),
+    "orbmi_create_new_map_points": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                         _vp]),
     "orbmi_slam_create": (_i, [_vp, _i, _vp, C.POINTER(_vp)]),
     "orbmi_slam_destroy": (None, [_vp]),
     "orbmi_slam_wait_local_mapping": (_i, [_vp]),

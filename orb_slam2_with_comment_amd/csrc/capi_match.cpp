@@ -5,6 +5,7 @@
 #include <new>
 
 #include "matcher.h"
+#include "tri_geom.h"
 
 using orbmi::DevFrame;
 using orbmi::DevFV;
@@ -558,6 +559,83 @@ int orbmi_search_for_triangulation_batch(orbmi_matcher* h, const orbmi_frame_vie
     return ORBMI_OK;
 }
 
+int orbmi_create_new_map_points(orbmi_matcher* h, const orbmi_frame_view* kf1, const orbmi_tri_keyframe* tri1,
+                                const float* cos1, const uint8_t* has_mp1, const orbmi_feature_vector* fv1,
+                                int npairs, const orbmi_frame_view* kf2, const orbmi_tri_keyframe* tri2,
+                                const float* const* cos2, const uint8_t* const* has_mp2,
+                                const orbmi_feature_vector* fv2, const float* F12, int32_t* match12, uint8_t* ok,
+                                float* x3d) {
+    if (!h || !kf1 || !tri1 || !has_mp1 || !fv1 || !kf1->u_right || npairs < 0 ||
+        (npairs > 0 && (!kf2 || !tri2 || !has_mp2 || !fv2 || !F12 || !match12 || !ok || !x3d)))
+        return ORBMI_E_ARG;
+    if (npairs == 0) return ORBMI_OK;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    DevFrame K1;
+    DevFV f1;
+    int rc;
+    if ((rc = make_frame(m, kf1, &K1, true))) return rc;
+    if ((rc = make_fv(m, fv1, &f1))) return rc;
+    const size_t n1 = (size_t)std::max(K1.n, 1);
+    const uint8_t* has1 = dev_in(m, has_mp1, n1, &rc);
+    if (rc) return rc;
+    std::vector<std::vector<float>> cos_tmp;  // tables computed here, alive until the copies ran
+    cos_tmp.reserve((size_t)npairs + 1);
+    // the triangulation side of a keyframe: keys / u_right from its frame view (device), the rest
+    // from its tri view
+    auto side = [&](const orbmi_tri_keyframe* T, const orbmi_frame_view* v, const DevFrame& D, const float* cs,
+                    orbmi::tri::Side* S) -> int {
+        if (!T->tcw || !T->depth || !T->level_sigma2 || !T->scale_factors || on_device(T->level_sigma2) ||
+            on_device(T->scale_factors) || v->nlevels > orbmi::tri::kLevels)
+            return ORBMI_E_ARG;
+        orbmi::tri::make_side(*T, v->nlevels, S);
+        S->keys = D.keys;
+        S->ur = D.u_right;
+        int r = 0;
+        S->depth = dev_in(m, T->depth, (size_t)D.n, &r);
+        if (r) return r;
+        if (!cs) {
+            if (on_device(T->depth)) return ORBMI_E_ARG;
+            cos_tmp.emplace_back((size_t)std::max(D.n, 1));
+            if ((r = orbmi_stereo_parallax_cos(T->mb, T->depth, D.n, cos_tmp.back().data()))) return r;
+            cs = cos_tmp.back().data();
+        }
+        S->cos_stereo = dev_in(m, cs, (size_t)D.n, &r);
+        return r;
+    };
+    orbmi::tri::Side S1;
+    if ((rc = side(tri1, kf1, K1, cos1, &S1))) return rc;
+    std::vector<orbmi::tri::Side> S2(npairs);
+    std::vector<TriPair> pairs(npairs);
+    const bool F_dev = on_device(F12);
+    std::vector<float> Fh((size_t)9 * npairs);
+    if (F_dev) ORBMI_HIP(hipMemcpy(Fh.data(), F12, Fh.size() * sizeof(float), hipMemcpyDeviceToHost));
+    else memcpy(Fh.data(), F12, Fh.size() * sizeof(float));
+    for (int j = 0; j < npairs; j++) {
+        TriPair& P = pairs[j];
+        memset(&P, 0, sizeof(P));
+        if (!kf2[j].u_right || !has_mp2[j]) return ORBMI_E_ARG;
+        if ((rc = make_frame(m, &kf2[j], &P.KF2, true))) return rc;
+        if ((rc = make_fv(m, &fv2[j], &P.fv2))) return rc;
+        P.has_mp2 = dev_in(m, has_mp2[j], (size_t)std::max(P.KF2.n, 1), &rc);
+        if (rc) return rc;
+        for (int q = 0; q < 9; q++) P.F12.m[q] = Fh[9 * j + q];
+        if ((rc = side(&tri2[j], &kf2[j], P.KF2, cos2 ? cos2[j] : nullptr, &S2[j]))) return rc;
+    }
+    TriPair* d_pairs = (TriPair*)m.stage(sizeof(TriPair) * npairs);
+    const orbmi::tri::Side* d_S2 = dev_in(m, S2.data(), (size_t)npairs, &rc);
+    std::vector<OutBuf> outs;
+    int* d_match = dev_out(m, match12, (size_t)K1.n * npairs, outs);
+    uint8_t* d_ok = dev_out(m, ok, (size_t)K1.n * npairs, outs);
+    float* d_x3d = dev_out(m, x3d, (size_t)3 * K1.n * npairs, outs);
+    if (rc || !d_pairs || !d_match || !d_ok || !d_x3d) return rc ? rc : ORBMI_E_HIP;
+    if ((rc = orbmi::launch_create_points(m, K1, has1, f1, npairs, pairs.data(), d_pairs, S1, d_S2, d_match, d_ok,
+                                          d_x3d)))
+        return rc;
+    return finish(m, outs, nullptr, nullptr);
+}
+
 int orbmi_fuse_search(orbmi_matcher* h, const orbmi_frame_view* kf, const orbmi_mappoint* mps, const uint8_t* in_kf,
                       int n_mp, float th, int32_t* best_idx, int32_t* best_dist, int* ncandidates) {
     if (!h || !kf || n_mp < 0 || (n_mp > 0 && (!mps || !best_idx || !best_dist))) return ORBMI_E_ARG;
@@ -613,6 +691,63 @@ int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* k
     }
     if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
     return ORBMI_OK;
+}
+
+int orbmi_fuse_search_refresh(orbmi_matcher* h, const uint8_t* obs_desc, const int32_t* obs_off, int nd, int32_t* best,
+                              uint8_t* desc_out, int nkf, const orbmi_frame_view* kfs, const orbmi_mappoint* mps,
+                              const int32_t* desc_from, const uint8_t* in_kf, int n_mp, float th, int32_t* best_idx,
+                              int32_t* best_dist) {
+    if (!h || nd < 0 || nkf < 0 || n_mp < 0 || (nd > 0 && (!obs_off || !best || !desc_out)) ||
+        (nkf > 0 && !kfs) || (nkf > 0 && n_mp > 0 && (!mps || !best_idx || !best_dist)))
+        return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    m.arena_reset();
+    int rc = 0;
+    std::vector<OutBuf> outs;
+    // ComputeDistinctiveDescriptors of the nd due points
+    uint8_t* d_dout = nullptr;
+    if (nd > 0) {
+        int total = 0;
+        if (on_device(obs_off)) ORBMI_HIP(hipMemcpy(&total, obs_off + nd, sizeof(int), hipMemcpyDeviceToHost));
+        else total = obs_off[nd];
+        if (total < 0 || (total > 0 && !obs_desc)) return ORBMI_E_ARG;
+        const uint8_t* d_desc = dev_in(m, obs_desc, (size_t)total * 32, &rc);
+        const int* d_off = dev_in(m, obs_off, (size_t)nd + 1, &rc);
+        if (rc) return rc;
+        int* d_best = dev_out(m, best, (size_t)nd, outs);
+        d_dout = dev_out(m, desc_out, (size_t)nd * 32, outs);
+        if (!on_device(desc_out))
+            ORBMI_HIP(hipMemcpyAsync(d_dout, desc_out, (size_t)nd * 32, hipMemcpyHostToDevice, m.stream));
+        if ((rc = orbmi::launch_distinctive(m, d_desc, d_off, nd, d_best, d_dout))) return rc;
+    }
+    // the Fuse searches on records patched with the new descriptors
+    if (nkf > 0 && n_mp > 0) {
+        orbmi_mappoint* d_mps = (orbmi_mappoint*)m.stage(sizeof(orbmi_mappoint) * n_mp);
+        if (!d_mps) return ORBMI_E_HIP;
+        ORBMI_HIP(hipMemcpyAsync(d_mps, mps, sizeof(orbmi_mappoint) * n_mp,
+                                 on_device(mps) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, m.stream));
+        if (desc_from && nd > 0) {
+            const int* d_from = dev_in(m, desc_from, (size_t)n_mp, &rc);
+            if (rc) return rc;
+            if ((rc = orbmi::launch_patch_desc(m, d_mps, d_from, d_dout, n_mp))) return rc;
+        }
+        const uint8_t* d_in = dev_in(m, in_kf, in_kf ? (size_t)n_mp * nkf : 0, &rc);
+        if (rc) return rc;
+        std::vector<FuseKF> K(nkf);
+        for (int k = 0; k < nkf; k++) {
+            memset(&K[k], 0, sizeof(FuseKF));
+            if ((rc = make_frame(m, &kfs[k], &K[k].F, true))) return rc;
+            K[k].in_kf = d_in ? d_in + (size_t)k * n_mp : nullptr;
+        }
+        FuseKF* d_k = (FuseKF*)m.stage(sizeof(FuseKF) * nkf);
+        int* d_cnt = (int*)m.stage(sizeof(int) * nkf);
+        int* d_bi = dev_out(m, best_idx, (size_t)n_mp * nkf, outs);
+        int* d_bd = dev_out(m, best_dist, (size_t)n_mp * nkf, outs);
+        if (!d_k || !d_cnt) return ORBMI_E_HIP;
+        if ((rc = orbmi::launch_fuse_multi(m, nkf, K.data(), d_k, d_mps, n_mp, th, d_bi, d_bd, d_cnt))) return rc;
+    }
+    return finish(m, outs, nullptr, nullptr);
 }
 
 int orbmi_debug_greedy_stats(unsigned long long* out, int reset) {

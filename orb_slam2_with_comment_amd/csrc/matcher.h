@@ -130,10 +130,15 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
                const DevFV& fv, float nnratio, int check_ori, int* match, int* nmatches);
 int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
                          TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match);
+namespace tri { struct Side; }
+int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, const DevFV& fv1, int npairs,
+                         TriPair* pairs_host, TriPair* pairs_dev, const tri::Side& S1, const tri::Side* S2_dev,
+                         int* match, uint8_t* ok, float* x3d);
 int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const uint8_t* in_kf, int n, float th,
                 int* best_idx, int* best_dist, int* ncand);
 int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, const orbmi_mappoint* mps, int n,
                       float th, int* best_idx, int* best_dist, int* ncand);
+int launch_patch_desc(Matcher& m, orbmi_mappoint* mps, const int* desc_from, const uint8_t* desc, int n);
 int greedy_stats(unsigned long long out[5], int reset);
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,

@@ -24,6 +24,7 @@
 #include <cstring>
 
 #include "matcher.h"
+#include "tri_geom.h"
 #include "wave_ops.h"
 
 namespace orbmi {
@@ -1032,173 +1033,168 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
 }
 
 // ------------------------------------------------------------- SearchForTriangulation
-// ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:783-975): one wave per KF1 vocabulary
-// node (merge-join partner found by lower_bound), KF1 features of the node in order, KF2
-// features of the node across the lanes.  The reference keeps no exclusion state (vbMatched2
-// is never set), so features are independent; its scan `if (dist > bestDist) continue; ...
-// if (CheckDistEpipolarLine) {bestIdx2 = idx2; bestDist = dist;}` ends on the smallest distance
-// <= TH_LOW among the candidates that pass, the LAST one on ties: key (dist << 32 | ~pos), min.
-// CheckDistEpipolarLine (:173-196) compares in double (3.84 * sigma2); the epipole and the
-// keyframe-1 centre follow the P10 float order.  The rotation histogram is k_bow_finalize's.
-__global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* __restrict__ has_mp1, DevFV fv1,
-                                                   const TriPair* __restrict__ pairs, int only_stereo, int check_ori) {
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int a = blockIdx.x * 4 + wid;
-    if (a >= fv1.nnodes) return;
-    const TriPair& P = pairs[blockIdx.y];  // the pair (KF1, KF2 = P.KF2) of this grid row
-    const DevFV fv2 = P.fv2;
-    const uint8_t* __restrict__ has_mp2 = P.has_mp2;
-    int* __restrict__ match = P.match;
-    const unsigned id = fv1.node_id[a];
-    int lo = 0, hi = fv2.nnodes;  // lower_bound
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv2.node_id[mid] < id) lo = mid + 1; else hi = mid; }
-    if (lo >= fv2.nnodes || fv2.node_id[lo] != id) return;
-    const DevFrame& KF2 = P.KF2;
-    const Mat3f F12 = P.F12;
-    const int f0 = fv2.off[lo], nf = fv2.off[lo + 1] - f0;
-    const int a0 = fv1.off[a], n1 = fv1.off[a + 1] - a0;
-    // epipole of KF1's centre in KF2
-    const Pose34 T1 = frame_pose(KF1), T2 = frame_pose(KF2);
-    float Ow[3], C2[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) Ow[i] = -(((T1.m[0 * 4 + i] * T1.m[3]) + T1.m[1 * 4 + i] * T1.m[7]) + T1.m[2 * 4 + i] * T1.m[11]);
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-        C2[i] = (((T2.m[i * 4 + 0] * Ow[0]) + T2.m[i * 4 + 1] * Ow[1]) + T2.m[i * 4 + 2] * Ow[2]) + T2.m[i * 4 + 3];
-    const float invz = 1.0f / C2[2];
-    const float ex = KF2.fx * C2[0] * invz + KF2.cx;
-    const float ey = KF2.fy * C2[1] * invz + KF2.cy;
-    if (nf <= 128) {
-        // The node's KF2 candidates sit in registers (lane p holds candidates p and p + 64), the
-        // KF1 features in chunks of 64 (lane p holds feature p of the chunk), each loaded in one
-        // round; the KF1 features are then visited in order by broadcasting lane i's (readlane),
-        // so the inner loop issues no memory access.
-        bool okc[2], stc[2];
-        int idxc[2];
-        uint4 e0[2], e1[2];
-        float kx[2], ky[2], sc2[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int pos = lane + 64 * h;
-            okc[h] = pos < nf;
-            stc[h] = false;
-            idxc[h] = 0;
-            e0[h] = make_uint4(0, 0, 0, 0);
-            e1[h] = e0[h];
-            kx[h] = ky[h] = 0.f;
-            sc2[h] = 1.f;
-            if (okc[h]) {
-                const int i2 = fv2.feat[f0 + pos];
-                idxc[h] = i2;
-                stc[h] = KF2.u_right[i2] >= 0;
-                okc[h] = !has_mp2[i2] && !(only_stereo && !stc[h]);
-                const uint4* d2 = reinterpret_cast<const uint4*>(KF2.desc + 32 * (long long)i2);
-                e0[h] = d2[0];
-                e1[h] = d2[1];
-                const orbmi_keypoint k2 = KF2.keys[i2];
-                kx[h] = k2.x;
-                ky[h] = k2.y;
-                sc2[h] = KF2.scale[min(max(k2.octave, 0), kMaxLevels - 1)];
-            }
-        }
-        for (int c1 = 0; c1 < n1; c1 += 64) {
-            bool ok1 = c1 + lane < n1;
-            int idx1l = 0;
-            uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0;
-            orbmi_keypoint kp1l{};
-            bool st1l = false;
-            if (ok1) {
-                idx1l = fv1.feat[a0 + c1 + lane];
-                st1l = KF1.u_right[idx1l] >= 0;
-                ok1 = !has_mp1[idx1l] && !(only_stereo && !st1l);
-                const uint4* d1 = reinterpret_cast<const uint4*>(KF1.desc + 32 * (long long)idx1l);
-                g0 = d1[0];
-                g1 = d1[1];
-                kp1l = KF1.keys[idx1l];
-            }
-            unsigned long long todo = __ballot(ok1);
-            while (todo) {
-                const int i = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                const int idx1 = __builtin_amdgcn_readlane(idx1l, i);
-                const bool st1 = __builtin_amdgcn_readlane((int)st1l, i) != 0;
-                const float k1x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.x), i));
-                const float k1y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.y), i));
-                const uint4 d0 = make_uint4(__builtin_amdgcn_readlane(g0.x, i), __builtin_amdgcn_readlane(g0.y, i),
-                                            __builtin_amdgcn_readlane(g0.z, i), __builtin_amdgcn_readlane(g0.w, i));
-                const uint4 d1 = make_uint4(__builtin_amdgcn_readlane(g1.x, i), __builtin_amdgcn_readlane(g1.y, i),
-                                            __builtin_amdgcn_readlane(g1.z, i), __builtin_amdgcn_readlane(g1.w, i));
-                // epipolar line of kp1 in KF2: l = x1' F12
-                const float la = k1x * F12.m[0] + k1y * F12.m[3] + F12.m[6];
-                const float lb = k1x * F12.m[1] + k1y * F12.m[4] + F12.m[7];
-                const float lc = k1x * F12.m[2] + k1y * F12.m[5] + F12.m[8];
-                unsigned long long key = ~0ull;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    if (!okc[h]) continue;
-                    const int dist = popc256(d0, d1, e0[h], e1[h]);
-                    bool pass = dist <= TH_LOW;
-                    if (pass && !st1 && !stc[h]) {
-                        const float distex = ex - kx[h];
-                        const float distey = ey - ky[h];
-                        pass = !(distex * distex + distey * distey < 100 * sc2[h]);
-                    }
-                    if (pass) {
-                        const float num = la * kx[h] + lb * ky[h] + lc;
-                        const float den = la * la + lb * lb;
-                        if (den == 0) pass = false;
-                        else {
-                            const float dsqr = num * num / den;
-                            const float sigma2 = sc2[h] * sc2[h];
-                            pass = (double)dsqr < 3.84 * (double)sigma2;
-                        }
-                    }
-                    const unsigned long long k =
-                        (unsigned long long)dist << 32 | (unsigned)(0xFFFFFFFFu - (unsigned)(lane + 64 * h));
-                    if (pass && k < key) key = k;
-                }
-                key = wave_min_u64_dpp(key);
-                if (key != ~0ull) {
-                    const int pos = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFu)));
-                    const int i2 = pos < 64 ? __builtin_amdgcn_readlane(idxc[0], pos)
-                                            : __builtin_amdgcn_readlane(idxc[1], pos - 64);
-                    if (lane == 0) {
-                        match[idx1] = i2;
-                        if (check_ori) {
-                            const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.angle), i));
-                            const int bin = rot_bin(a1, KF2.keys[i2].angle);
-                            P.bin_of[idx1] = bin;
-                            atomicAdd(&P.hist[bin], 1);
-                        }
-                    }
-                }
-            }
-        }
-        return;
+// ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:783-975).  The reference keeps no
+// exclusion state (vbMatched2 is never set), so KF1 features are independent: a wave takes one
+// slice of a KF1 vocabulary node's features (`splits` slices per node, so that a keyframe pair
+// with a few large nodes -- a coarse vocabulary level -- still fills the chip), finds the node in
+// KF2 by lower_bound, and for each of its features in order scans the node's KF2 features across
+// the lanes.  The scan `if (dist > bestDist) continue; ... if (CheckDistEpipolarLine) {bestIdx2 =
+// idx2; bestDist = dist;}` ends on the smallest distance <= TH_LOW among the candidates that
+// pass, the LAST one on ties: key (dist << 32 | ~pos), min.  CheckDistEpipolarLine (:173-196)
+// compares in double (3.84 * sigma2); the epipole and the keyframe-1 centre follow the P10 float
+// order.  The rotation histogram is k_bow_finalize's.
+
+struct TriNode {  // one wave's work: KF1 features feat1[0..n1) against KF2 node features f0..f0+nf
+    const int* feat1;
+    int n1, f0, nf;
+    float ex, ey;  // the epipole (KF1's centre in KF2)
+};
+
+__device__ inline void tri_record(const TriPair& P, int check_ori, int idx1, int i2, float angle1) {
+    P.match[idx1] = i2;
+    if (check_ori) {
+        const int bin = rot_bin(angle1, P.KF2.keys[i2].angle);
+        P.bin_of[idx1] = bin;
+        atomicAdd(&P.hist[bin], 1);
     }
-    for (int ia = fv1.off[a]; ia < fv1.off[a + 1]; ia++) {
-        const int idx1 = fv1.feat[ia];
+}
+
+// the node's KF2 candidates in registers (lane p holds candidates p, p + 64, ..., H of them), the
+// KF1 features in chunks of 64 (lane p holds feature p of the chunk), each loaded in one round;
+// the KF1 features are then visited in order by broadcasting lane i's (readlane), so the inner
+// loop issues no memory access
+template <int H>
+__device__ void tri_node_regs(const DevFrame& KF1, const uint8_t* __restrict__ has_mp1, const TriPair& P,
+                              const TriNode& T, int only_stereo, int check_ori, int lane) {
+    const DevFrame& KF2 = P.KF2;
+    const DevFV& fv2 = P.fv2;
+    const Mat3f F12 = P.F12;
+    bool okc[H], stc[H];
+    int idxc[H];
+    uint4 e0[H], e1[H];
+    float kx[H], ky[H], sc2[H];
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+        const int pos = lane + 64 * h;
+        okc[h] = pos < T.nf;
+        stc[h] = false;
+        idxc[h] = 0;
+        e0[h] = make_uint4(0, 0, 0, 0);
+        e1[h] = e0[h];
+        kx[h] = ky[h] = 0.f;
+        sc2[h] = 1.f;
+        if (okc[h]) {
+            const int i2 = fv2.feat[T.f0 + pos];
+            idxc[h] = i2;
+            stc[h] = KF2.u_right[i2] >= 0;
+            okc[h] = !P.has_mp2[i2] && !(only_stereo && !stc[h]);
+            const uint4* d2 = reinterpret_cast<const uint4*>(KF2.desc + 32 * (long long)i2);
+            e0[h] = d2[0];
+            e1[h] = d2[1];
+            const orbmi_keypoint k2 = KF2.keys[i2];
+            kx[h] = k2.x;
+            ky[h] = k2.y;
+            sc2[h] = KF2.scale[min(max(k2.octave, 0), kMaxLevels - 1)];
+        }
+    }
+    for (int c1 = 0; c1 < T.n1; c1 += 64) {
+        bool ok1 = c1 + lane < T.n1;
+        int idx1l = 0;
+        uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0;
+        orbmi_keypoint kp1l{};
+        bool st1l = false;
+        if (ok1) {
+            idx1l = T.feat1[c1 + lane];
+            st1l = KF1.u_right[idx1l] >= 0;
+            ok1 = !has_mp1[idx1l] && !(only_stereo && !st1l);
+            const uint4* d1 = reinterpret_cast<const uint4*>(KF1.desc + 32 * (long long)idx1l);
+            g0 = d1[0];
+            g1 = d1[1];
+            kp1l = KF1.keys[idx1l];
+        }
+        unsigned long long todo = __ballot(ok1);
+        while (todo) {
+            const int i = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const int idx1 = __builtin_amdgcn_readlane(idx1l, i);
+            const bool st1 = __builtin_amdgcn_readlane((int)st1l, i) != 0;
+            const float k1x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.x), i));
+            const float k1y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.y), i));
+            const uint4 d0 = make_uint4(__builtin_amdgcn_readlane(g0.x, i), __builtin_amdgcn_readlane(g0.y, i),
+                                        __builtin_amdgcn_readlane(g0.z, i), __builtin_amdgcn_readlane(g0.w, i));
+            const uint4 d1 = make_uint4(__builtin_amdgcn_readlane(g1.x, i), __builtin_amdgcn_readlane(g1.y, i),
+                                        __builtin_amdgcn_readlane(g1.z, i), __builtin_amdgcn_readlane(g1.w, i));
+            // epipolar line of kp1 in KF2: l = x1' F12
+            const float la = k1x * F12.m[0] + k1y * F12.m[3] + F12.m[6];
+            const float lb = k1x * F12.m[1] + k1y * F12.m[4] + F12.m[7];
+            const float lc = k1x * F12.m[2] + k1y * F12.m[5] + F12.m[8];
+            unsigned long long key = ~0ull;
+#pragma unroll
+            for (int h = 0; h < H; h++) {
+                if (!okc[h]) continue;
+                const int dist = popc256(d0, d1, e0[h], e1[h]);
+                bool pass = dist <= TH_LOW;
+                if (pass && !st1 && !stc[h]) {
+                    const float distex = T.ex - kx[h];
+                    const float distey = T.ey - ky[h];
+                    pass = !(distex * distex + distey * distey < 100 * sc2[h]);
+                }
+                if (pass) {
+                    const float num = la * kx[h] + lb * ky[h] + lc;
+                    const float den = la * la + lb * lb;
+                    if (den == 0) pass = false;
+                    else {
+                        const float dsqr = num * num / den;
+                        const float sigma2 = sc2[h] * sc2[h];
+                        pass = (double)dsqr < 3.84 * (double)sigma2;
+                    }
+                }
+                const unsigned long long k =
+                    (unsigned long long)dist << 32 | (unsigned)(0xFFFFFFFFu - (unsigned)(lane + 64 * h));
+                if (pass && k < key) key = k;
+            }
+            key = wave_min_u64_dpp(key);
+            if (key != ~0ull) {
+                const int pos = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFu)));
+                int i2 = 0;
+#pragma unroll
+                for (int h = 0; h < H; h++)
+                    if ((pos >> 6) == h) i2 = __builtin_amdgcn_readlane(idxc[h], pos & 63);
+                const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kp1l.angle), i));
+                if (lane == 0) tri_record(P, check_ori, idx1, i2, a1);
+            }
+        }
+    }
+}
+
+// nodes with more than 256 KF2 features: the candidates are read from memory per KF1 feature
+__device__ void tri_node_mem(const DevFrame& KF1, const uint8_t* __restrict__ has_mp1, const TriPair& P,
+                             const TriNode& T, int only_stereo, int check_ori, int lane) {
+    const DevFrame& KF2 = P.KF2;
+    const DevFV& fv2 = P.fv2;
+    const Mat3f F12 = P.F12;
+    for (int ia = 0; ia < T.n1; ia++) {
+        const int idx1 = T.feat1[ia];
         if (has_mp1[idx1]) continue;
         const bool st1 = KF1.u_right[idx1] >= 0;
         if (only_stereo && !st1) continue;
         const orbmi_keypoint kp1 = KF1.keys[idx1];
         const uint8_t* d1 = KF1.desc + 32 * (long long)idx1;
-        // epipolar line of kp1 in KF2: l = x1' F12
         const float la = kp1.x * F12.m[0] + kp1.y * F12.m[3] + F12.m[6];
         const float lb = kp1.x * F12.m[1] + kp1.y * F12.m[4] + F12.m[7];
         const float lc = kp1.x * F12.m[2] + kp1.y * F12.m[5] + F12.m[8];
         unsigned long long key = ~0ull;
-        for (int pos = lane; pos < nf; pos += 64) {
-            const int idx2 = fv2.feat[f0 + pos];
-            if (has_mp2[idx2]) continue;
+        for (int pos = lane; pos < T.nf; pos += 64) {
+            const int idx2 = fv2.feat[T.f0 + pos];
+            if (P.has_mp2[idx2]) continue;
             const bool st2 = KF2.u_right[idx2] >= 0;
             if (only_stereo && !st2) continue;
             const int dist = popc_desc(d1, KF2.desc + 32 * (long long)idx2);
             if (dist > TH_LOW) continue;
             const orbmi_keypoint kp2 = KF2.keys[idx2];
             if (!st1 && !st2) {
-                const float distex = ex - kp2.x;
-                const float distey = ey - kp2.y;
+                const float distex = T.ex - kp2.x;
+                const float distey = T.ey - kp2.y;
                 if (distex * distex + distey * distey < 100 * KF2.scale[kp2.octave]) continue;
             }
             const float num = la * kp2.x + lb * kp2.y + lc;
@@ -1213,15 +1209,47 @@ __global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* 
         key = wave_min_u64(key);
         if (key != ~0ull && lane == 0) {
             const int pos = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFu));
-            const int idx2 = fv2.feat[f0 + pos];
-            match[idx1] = idx2;
-            if (check_ori) {
-                const int bin = rot_bin(kp1.angle, KF2.keys[idx2].angle);
-                P.bin_of[idx1] = bin;
-                atomicAdd(&P.hist[bin], 1);
-            }
+            tri_record(P, check_ori, idx1, fv2.feat[T.f0 + pos], kp1.angle);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_tri_match(DevFrame KF1, const uint8_t* __restrict__ has_mp1, DevFV fv1,
+                                                   const TriPair* __restrict__ pairs, int only_stereo, int check_ori,
+                                                   int splits) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + wid;
+    const int a = w / splits, sl = w - a * splits;
+    if (a >= fv1.nnodes) return;
+    const TriPair& P = pairs[blockIdx.y];  // the pair (KF1, KF2 = P.KF2) of this grid row
+    const DevFV fv2 = P.fv2;
+    const int A0 = fv1.off[a], N1 = fv1.off[a + 1] - A0;
+    const int lo1 = A0 + (int)(((long long)N1 * sl) / splits), hi1 = A0 + (int)(((long long)N1 * (sl + 1)) / splits);
+    if (lo1 >= hi1) return;
+    const unsigned id = fv1.node_id[a];
+    int lo = 0, hi = fv2.nnodes;  // lower_bound
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv2.node_id[mid] < id) lo = mid + 1; else hi = mid; }
+    if (lo >= fv2.nnodes || fv2.node_id[lo] != id) return;
+    const DevFrame& KF2 = P.KF2;
+    TriNode T;
+    T.feat1 = fv1.feat + lo1;
+    T.n1 = hi1 - lo1;
+    T.f0 = fv2.off[lo];
+    T.nf = fv2.off[lo + 1] - T.f0;
+    // epipole of KF1's centre in KF2
+    const Pose34 T1 = frame_pose(KF1), T2 = frame_pose(KF2);
+    float Ow[3], C2[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) Ow[i] = -(((T1.m[0 * 4 + i] * T1.m[3]) + T1.m[1 * 4 + i] * T1.m[7]) + T1.m[2 * 4 + i] * T1.m[11]);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        C2[i] = (((T2.m[i * 4 + 0] * Ow[0]) + T2.m[i * 4 + 1] * Ow[1]) + T2.m[i * 4 + 2] * Ow[2]) + T2.m[i * 4 + 3];
+    const float invz = 1.0f / C2[2];
+    T.ex = KF2.fx * C2[0] * invz + KF2.cx;
+    T.ey = KF2.fy * C2[1] * invz + KF2.cy;
+    if (T.nf <= 128) tri_node_regs<2>(KF1, has_mp1, P, T, only_stereo, check_ori, lane);
+    else if (T.nf <= 256) tri_node_regs<4>(KF1, has_mp1, P, T, only_stereo, check_ori, lane);
+    else tri_node_mem(KF1, has_mp1, P, T, only_stereo, check_ori, lane);
 }
 
 // one workgroup per pair: the rotation histogram and the count of SearchForTriangulation
@@ -1230,9 +1258,17 @@ __global__ __launch_bounds__(1024) void k_tri_finalize(int n1, const TriPair* __
     finalize_block(n1, check_ori, P.hist, P.bin_of, P.match, P.nmatches);
 }
 
-int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
-                         TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
-    if (npairs <= 0) return ORBMI_OK;
+// slices per node: enough waves for the chip (~4096 over all pairs) while a slice keeps ~16 KF1
+// features to amortise loading the node's KF2 candidates
+static int tri_splits(const DevFrame& KF1, const DevFV& fv1, int npairs) {
+    const int nodes = std::max(fv1.nnodes, 1);
+    const int by_chip = 4096 / std::max(nodes * npairs, 1);
+    const int by_size = std::max(KF1.n / nodes / 16, 1);
+    return std::max(1, std::min(std::min(by_chip, by_size), 64));
+}
+
+static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
+                             TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
     const size_t n1 = (size_t)std::max(KF1.n, 1);
     int rc;
     if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, n1 * npairs))) return rc;
@@ -1246,10 +1282,70 @@ int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1
     ORBMI_HIP(hipMemcpyAsync(pairs_dev, pairs_host, sizeof(TriPair) * npairs, hipMemcpyHostToDevice, m.stream));
     ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
     if (KF1.n > 0) ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)KF1.n * npairs * sizeof(int), m.stream));
-    if (fv1.nnodes > 0)
-        hipLaunchKernelGGL(k_tri_match, dim3((fv1.nnodes + 3) / 4, npairs), dim3(256), 0, m.stream, KF1, has_mp1, fv1,
-                           pairs_dev, only_stereo, check_ori);
+    if (fv1.nnodes > 0) {
+        const int splits = tri_splits(KF1, fv1, npairs);
+        const int waves = fv1.nnodes * splits;
+        hipLaunchKernelGGL(k_tri_match, dim3((waves + 3) / 4, npairs), dim3(256), 0, m.stream, KF1, has_mp1, fv1,
+                           pairs_dev, only_stereo, check_ori, splits);
+    }
     hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.stream, KF1.n, pairs_dev, check_ori);
+    return ORBMI_OK;
+}
+
+int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
+                         TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
+    if (npairs <= 0) return ORBMI_OK;
+    int rc;
+    if ((rc = launch_tri_search(m, KF1, has_mp1, fv1, npairs, pairs_host, pairs_dev, only_stereo, check_ori, match)))
+        return rc;
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+}
+
+// CreateNewMapPoints' triangulation on the device (tri_geom.h's tests, the code the host runs):
+// thread per KF1 keypoint, visiting the pairs in the reference's order.  A keypoint whose match
+// an earlier pair accepted has a map point from then on, so the reference's search of the later
+// pairs skips it (`if (pMP1) continue;`): its later matches are dropped -- the searches, which
+// are independent per KF1 keypoint, ran for all pairs at once on the entry flags.
+__global__ __launch_bounds__(256) void k_triangulate(tri::Side K1, const tri::Side* __restrict__ K2s, int npairs,
+                                                     int* __restrict__ match, int n1, uint8_t* __restrict__ ok,
+                                                     float* __restrict__ x3d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n1) return;
+    bool claimed = false;
+    const float cps1 = K1.ur[i] >= 0 ? K1.cos_stereo[i] : 0.f;
+    for (int j = 0; j < npairs; j++) {
+        const size_t r = (size_t)j * n1 + i;
+        const int i2 = match[r];
+        uint8_t o = 0;
+        if (i2 >= 0) {
+            if (claimed) {
+                match[r] = -1;
+            } else {
+                const tri::Side& K2 = K2s[j];
+                const float cps2 = K2.ur[i2] >= 0 ? K2.cos_stereo[i2] : 0.f;
+                float x[3];
+                if (tri::triangulate_one(K1, K2, i, i2, cps1, cps2, x)) {
+                    o = 1;
+                    claimed = true;
+                    x3d[3 * r] = x[0];
+                    x3d[3 * r + 1] = x[1];
+                    x3d[3 * r + 2] = x[2];
+                }
+            }
+        }
+        ok[r] = o;
+    }
+}
+
+int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, const DevFV& fv1, int npairs,
+                         TriPair* pairs_host, TriPair* pairs_dev, const tri::Side& S1, const tri::Side* S2_dev,
+                         int* match, uint8_t* ok, float* x3d) {
+    if (npairs <= 0) return ORBMI_OK;
+    int rc;
+    if ((rc = launch_tri_search(m, KF1, has1, fv1, npairs, pairs_host, pairs_dev, 0, 0, match))) return rc;
+    if (KF1.n > 0)
+        hipLaunchKernelGGL(k_triangulate, dim3((KF1.n + 255) / 256), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
+                           KF1.n, ok, x3d);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 
@@ -1406,6 +1502,22 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
     if (n > 0)
         hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n,
                            th);
+    return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+}
+
+// records whose descriptor was just recomputed (desc_from[i] >= 0: row of `desc`) take it
+__global__ __launch_bounds__(256) void k_patch_desc(orbmi_mappoint* __restrict__ mps, const int* __restrict__ desc_from,
+                                                    const uint8_t* __restrict__ desc, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // 8 threads per record, 4 bytes each
+    const int i = t >> 3, w = t & 7;
+    if (i >= n) return;
+    const int r = desc_from[i];
+    if (r < 0) return;
+    reinterpret_cast<uint32_t*>(mps[i].desc)[w] = reinterpret_cast<const uint32_t*>(desc + 32 * (size_t)r)[w];
+}
+
+int launch_patch_desc(Matcher& m, orbmi_mappoint* mps, const int* desc_from, const uint8_t* desc, int n) {
+    if (n > 0) hipLaunchKernelGGL(k_patch_desc, dim3((8 * n + 255) / 256), dim3(256), 0, m.stream, mps, desc_from, desc, n);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 

@@ -40,6 +40,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/orbmi.h"
+#include "tri_geom.h"
 
 namespace {
 
@@ -140,6 +141,8 @@ struct KeyFrame {
     const orbmi_keypoint* d_keys = nullptr;
     const uint8_t* d_desc = nullptr;
     const float* d_ur = nullptr;
+    const float* d_depth = nullptr;
+    const float* d_cos = nullptr;  // orbmi_stereo_parallax_cos per keypoint (CreateNewMapPoints)
 };
 
 struct MapPoint {
@@ -178,7 +181,13 @@ enum { NO_IMAGES_YET = 0, NOT_INITIALIZED = 1, OK = 2, LOST = 3 };
 
 // wall time per phase of orbmi_slam_track_stereo (orbmi_slam_get_phase_ms; names in orbmi_debug.h)
 enum Phase { PH_FRAME, PH_LOCK, PH_LF_SEARCH, PH_LF_POSE, PH_LOCAL_UPDATE, PH_LOCAL_RECORDS, PH_FRUSTUM,
-             PH_LOCAL_SEARCH, PH_LOCAL_POSE, PH_KEYFRAME, PH_TOTAL, PH_COUNT };
+             PH_LOCAL_SEARCH, PH_LOCAL_POSE, PH_KEYFRAME, PH_TOTAL,
+             // LocalMapping::Run per keyframe (either thread): ProcessNewKeyFrame, MapPointCulling,
+             // CreateNewMapPoints, SearchInNeighbors, LocalBundleAdjustment, KeyFrameCulling, all
+             PH_LM_PROCESS, PH_LM_CULL, PH_LM_CREATE, PH_LM_FUSE, PH_LM_BA, PH_LM_KFCULL, PH_LM_TOTAL,
+             // inside them: the device calls of CreateNewMapPoints, of the Fuse searches, and of
+             // ComputeDistinctiveDescriptors (each with its staging and read-back)
+             PH_LM_CREATE_CALL, PH_LM_FUSE_CALL, PH_LM_DISTINCTIVE_CALL, PH_COUNT };
 struct PhaseTimer {
     double* acc;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
@@ -192,8 +201,10 @@ struct PhaseTimer {
         if (rc_ != ORBMI_OK) return rc_; \
     } while (0)
 
-// the mapping thread's hold on its system's map_mtx (null on every other thread)
-thread_local std::unique_lock<std::mutex>* lm_lock = nullptr;
+// this thread's hold on its system's map_mtx when the GPU calls may release it (the mapping
+// thread, and the tracking thread with the mapping thread running); null otherwise
+thread_local std::unique_lock<std::mutex>* held_lock = nullptr;
+thread_local bool on_mapping_thread = false;
 
 }  // namespace
 
@@ -443,7 +454,7 @@ struct orbmi_slam {
         fm.n_lf_points = (int)lfp.size();
         orbmi_pose_frame rec{};
         out.assign(std::max(cf.n(), 1), 0);
-        SLAM_CHECK(orbmi_pose_optimization_frame(pose, &v, inv_level_sigma2.data(), &fm, &rec, out.data()));
+        SLAM_CHECK(unlocked([&] { return orbmi_pose_optimization_frame(pose, &v, inv_level_sigma2.data(), &fm, &rec, out.data()); }));
         std::memcpy(tcw_out.data(), rec.tcw, sizeof(rec.tcw));
         out.resize(cf.n());
         return ORBMI_OK;
@@ -564,20 +575,28 @@ struct orbmi_slam {
     }
 
     // MapPoint::ComputeDistinctiveDescriptors for a batch of points (src/MapPoint.cc:247-316)
-    int distinctive(const std::vector<int>& pts) {
-        std::vector<uint8_t> rows;
-        std::vector<int32_t> off{0};
+    // the observation descriptors of the points (CSR, mObservations order, bad keyframes left out)
+    void obs_rows(const std::vector<int>& pts, std::vector<uint8_t>& rows, std::vector<int32_t>& off) const {
+        rows.clear();
+        off.assign(1, 0);
         for (int m : pts) {
             for (auto& o : mps[m].obs)
                 if (!kfs[o.first].bad) rows.insert(rows.end(), &kfs[o.first].desc[32 * o.second], &kfs[o.first].desc[32 * o.second] + 32);
             off.push_back((int32_t)(rows.size() / 32));
         }
+    }
+
+    int distinctive(const std::vector<int>& pts) {
+        std::vector<uint8_t> rows;
+        std::vector<int32_t> off;
+        obs_rows(pts, rows, off);
         if (rows.empty()) return ORBMI_OK;
         const int np = (int)pts.size();
         std::vector<int32_t> best(std::max(np, 1));
         std::vector<uint8_t> out((size_t)std::max(np, 1) * 32);
         orbmi_matcher* mt = lmm();
         SLAM_CHECK(unlocked([&] {
+            PhaseTimer pt(&phase_ms[PH_LM_DISTINCTIVE_CALL]);
             return orbmi_compute_distinctive_descriptors(mt, rows.data(), off.data(), np, best.data(), out.data());
         }));
         for (int j = 0; j < np; j++)
@@ -600,17 +619,26 @@ struct orbmi_slam {
         kf.fv = cf.fv;
         // the keyframe's arrays in HBM, copied once (from the frame's device slot when it has one)
         const size_t n = kf.keys.size(), bk = n * sizeof(orbmi_keypoint), bd = n * 32, bu = n * sizeof(float);
-        if (n > 0 && hipMalloc((void**)&kf.d_block, bk + bd + bu) == hipSuccess) {
+        std::vector<float> dc(2 * n);  // depth, then the stereo parallax table
+        const float mb = s.bf / s.fx;
+        for (size_t i = 0; i < n; i++) {
+            dc[i] = kf.depth[i];
+            dc[n + i] = kf.ur[i] >= 0 ? orbmi::tri::stereo_parallax_cos(mb, kf.depth[i]) : 0.f;
+        }
+        if (n > 0 && hipMalloc((void**)&kf.d_block, bk + bd + 3 * bu) == hipSuccess) {
             const bool dslot = cf.dslot >= 0;
             const hipMemcpyKind kind = dslot ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
             const void* sk = dslot ? (const void*)dev.kps[cf.dslot] : (const void*)kf.keys.data();
             const void* sd = dslot ? (const void*)dev.desc[cf.dslot] : (const void*)kf.desc.data();
             const void* su = dslot ? (const void*)dev.ur[cf.dslot] : (const void*)kf.ur.data();
             if (hipMemcpy(kf.d_block, sk, bk, kind) == hipSuccess && hipMemcpy(kf.d_block + bk, sd, bd, kind) == hipSuccess &&
-                hipMemcpy(kf.d_block + bk + bd, su, bu, kind) == hipSuccess) {
+                hipMemcpy(kf.d_block + bk + bd, su, bu, kind) == hipSuccess &&
+                hipMemcpy(kf.d_block + bk + bd + bu, dc.data(), 2 * bu, hipMemcpyHostToDevice) == hipSuccess) {
                 kf.d_keys = (const orbmi_keypoint*)kf.d_block;
                 kf.d_desc = kf.d_block + bk;
                 kf.d_ur = (const float*)(kf.d_block + bk + bd);
+                kf.d_depth = (const float*)(kf.d_block + bk + bd + bu);
+                kf.d_cos = (const float*)(kf.d_block + bk + bd + 2 * bu);
             }
         }
         kfs.push_back(std::move(kf));
@@ -632,13 +660,18 @@ struct orbmi_slam {
     // LocalMapping's GPU calls: on the mapping thread they use its own matcher and run with the
     // map lock released (their inputs are the caller's copies or the keyframes' HBM copies)
     orbmi_matcher* lm_matcher = nullptr;
-    orbmi_matcher* lmm() const { return lm_lock ? lm_matcher : matcher; }
+    orbmi_matcher* lmm() const { return on_mapping_thread ? lm_matcher : matcher; }
     template <class F>
     int unlocked(F f) {
-        if (!lm_lock) return f();
-        lm_lock->unlock();
+        if (!held_lock) return f();
+        held_lock->unlock();
         const int rc = f();
-        lm_lock->lock();
+        if (on_mapping_thread) {
+            held_lock->lock();
+        } else {
+            PhaseTimer pt(&phase_ms[PH_LOCK]);
+            held_lock->lock();
+        }
         return rc;
     }
 
@@ -773,6 +806,7 @@ struct orbmi_slam {
 
     // the mapping thread: one keyframe at a time, holding map_mtx except inside the BA solve
     void lm_run() {
+        on_mapping_thread = true;
         for (;;) {
             int k;
             {
@@ -786,9 +820,9 @@ struct orbmi_slam {
             int rc;
             {
                 std::unique_lock<std::mutex> m(map_mtx);
-                lm_lock = &m;
+                held_lock = &m;
                 rc = local_mapping(k);
-                lm_lock = nullptr;
+                held_lock = nullptr;
             }
             {
                 std::lock_guard<std::mutex> g(q_mtx);
@@ -811,6 +845,19 @@ struct orbmi_slam {
     // no stop request: ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints,
     // SearchInNeighbors, LocalBundleAdjustment (more than 2 keyframes), KeyFrameCulling
     int local_mapping(int k) {
+        PhaseTimer all(&phase_ms[PH_LM_TOTAL]);
+        auto* pt = new PhaseTimer(&phase_ms[PH_LM_PROCESS]);
+        auto next = [&](Phase p) {
+            delete pt;
+            pt = new PhaseTimer(&phase_ms[p]);
+        };
+        const int rc = local_mapping_steps(k, next);
+        delete pt;
+        return rc;
+    }
+
+    template <class Next>
+    int local_mapping_steps(int k, Next&& next) {
         if (voc && !kfs[k].fv.valid) SLAM_CHECK(compute_bow(kfs[k].desc, kfs[k].fv));
         std::vector<int> updated;
         for (int i = 0; i < (int)kfs[k].mps.size(); i++) {
@@ -826,14 +873,19 @@ struct orbmi_slam {
         for (int m : updated) update_normal_and_depth(m);
         SLAM_CHECK(distinctive(updated));
         update_connections(k);
+        next(PH_LM_CULL);
         map_point_culling(k);
         if (s.local_mapping) {
+            next(PH_LM_CREATE);
             SLAM_CHECK(create_new_map_points(k));
+            next(PH_LM_FUSE);
             if (!new_keyframes_queued()) SLAM_CHECK(search_in_neighbors(k));
         }
         abort_ba = 0;
         if (!new_keyframes_queued()) {
+            next(PH_LM_BA);
             if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+            next(PH_LM_KFCULL);
             if (s.local_mapping) keyframe_culling(k);
         }
         return ORBMI_OK;
@@ -857,10 +909,113 @@ struct orbmi_slam {
                                   s.cy, s.bf, s.bf / s.fx, level_sigma2.data(), scale_factors.data()};
     }
 
-    // src/LocalMapping.cc:290-577, stereo: the 10 best covisible keyframes.  Each pair's search
-    // runs on the keyframes' HBM copies with the map lock released (on the mapping thread); the
-    // views into `kfs` are taken again after it, as the tracker may have grown the vector.
+    // src/LocalMapping.cc:290-577, stereo: the 10 best covisible keyframes.  The neighbours that
+    // pass the baseline test go to the device in one orbmi_create_new_map_points call (searches and
+    // triangulation pair by pair, the keypoints earlier pairs claimed excluded on the device), run
+    // on the keyframes' HBM copies with the map lock released; the new points are then made here in
+    // the reference's order.
     int create_new_map_points(int k) {
+        float ow1[3];
+        kf_ow(k, ow1);
+        const float mb = s.bf / s.fx;
+        const std::vector<int> neigh(kfs[k].covisible.begin(),
+                                     kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
+        if (!kfs[k].fv.valid || !kfs[k].d_keys) return create_new_map_points_host(k);
+        std::vector<int> pk, pos;  // the neighbours searched, and their index in `neigh`
+        std::vector<M4> tcw2;
+        std::vector<float> F12;
+        std::vector<std::vector<uint8_t>> has2;
+        const M4 tcw1 = kfs[k].tcw;
+        for (size_t i = 0; i < neigh.size(); i++) {
+            const int k2 = neigh[i];
+            float ow2[3];
+            kf_ow(k2, ow2);
+            const float d[3] = {ow2[0] - ow1[0], ow2[1] - ow1[1], ow2[2] - ow1[2]};
+            const float baseline = (float)std::sqrt(((double)d[0] * d[0] + (double)d[1] * d[1]) + (double)d[2] * d[2]);
+            if (baseline < mb) continue;
+            if (!kfs[k2].fv.valid) continue;
+            if (!kfs[k2].d_keys) return create_new_map_points_host(k);
+            float F[9];
+            const orbmi_tri_keyframe v1 = tri_view(kfs[k]), v2 = tri_view(kfs[k2]);
+            SLAM_CHECK(orbmi_compute_f12(&v1, &v2, F));
+            pk.push_back(k2);
+            pos.push_back((int)i);
+            tcw2.push_back(kfs[k2].tcw);
+            F12.insert(F12.end(), F, F + 9);
+            has2.emplace_back(std::max<size_t>(kfs[k2].mps.size(), 1), 0);
+            for (size_t q = 0; q < kfs[k2].mps.size(); q++) has2.back()[q] = kfs[k2].mps[q] >= 0;
+        }
+        const int np = (int)pk.size();
+        if (np == 0) return ORBMI_OK;
+        const size_t n1 = kfs[k].keys.size();
+        std::vector<uint8_t> has1(std::max<size_t>(n1, 1), 0);
+        for (size_t i = 0; i < n1; i++) has1[i] = kfs[k].mps[i] >= 0;
+        // views on copies of the poses and on HBM arrays: valid while the lock is released
+        auto tri_dev = [&](const KeyFrame& kf, const M4& tcw) {
+            orbmi_tri_keyframe t = tri_view(kf);
+            t.tcw = tcw.data();
+            t.keys_un = kf.d_keys;
+            t.u_right = kf.d_ur;
+            t.depth = kf.d_depth;
+            return t;
+        };
+        const orbmi_frame_view f1 = kf_view(kfs[k], tcw1.data());
+        const orbmi_tri_keyframe t1 = tri_dev(kfs[k], tcw1);
+        const orbmi_feature_vector fv1 = kfs[k].fv.view();
+        const float* cos1 = kfs[k].d_cos;
+        std::vector<orbmi_frame_view> f2(np);
+        std::vector<orbmi_tri_keyframe> t2(np);
+        std::vector<orbmi_feature_vector> fv2(np);
+        std::vector<const float*> cos2(np);
+        std::vector<const uint8_t*> mp2(np);
+        for (int j = 0; j < np; j++) {
+            const KeyFrame& K2 = kfs[pk[j]];
+            f2[j] = kf_view(K2, tcw2[j].data());
+            t2[j] = tri_dev(K2, tcw2[j]);
+            fv2[j] = K2.fv.view();
+            cos2[j] = K2.d_cos;
+            mp2[j] = has2[j].data();
+        }
+        std::vector<int32_t> m12(std::max<size_t>(n1 * np, 1));
+        std::vector<uint8_t> ok(std::max<size_t>(n1 * np, 1));
+        std::vector<float> x3d(std::max<size_t>(3 * n1 * np, 1));
+        orbmi_matcher* mt = lmm();
+        SLAM_CHECK(unlocked([&] {
+            PhaseTimer pt(&phase_ms[PH_LM_CREATE_CALL]);
+            return orbmi_create_new_map_points(mt, &f1, &t1, cos1, has1.data(), &fv1, np, f2.data(), t2.data(),
+                                               cos2.data(), mp2.data(), fv2.data(), F12.data(), m12.data(), ok.data(),
+                                               x3d.data());
+        }));
+        std::vector<int> fresh;
+        for (int j = 0; j < np; j++) {
+            if (pos[j] > 0 && new_keyframes_queued()) break;  // src/LocalMapping.cc:331
+            const int k2 = pk[j];
+            for (size_t i = 0; i < n1; i++) {
+                const size_t r = (size_t)j * n1 + i;
+                if (!ok[r]) continue;
+                const int i2 = m12[r];
+                MapPoint mp;
+                mp.id = (int)mps.size();
+                std::memcpy(mp.pos, &x3d[3 * r], 3 * sizeof(float));
+                mp.ref_kf = k;
+                mp.first_kf_id = k;
+                mps.push_back(mp);
+                add_observation(mp.id, k, (int)i);
+                add_observation(mp.id, k2, i2);
+                kfs[k].mps[i] = mp.id;
+                kfs[k2].mps[i2] = mp.id;
+                recent_mps.push_back(mp.id);
+                fresh.push_back(mp.id);
+            }
+        }
+        // per point, so one batch for all pairs gives the reference's per-pair results
+        SLAM_CHECK(distinctive(fresh));
+        for (int m : fresh) update_normal_and_depth(m);
+        return ORBMI_OK;
+    }
+
+    // the same loop with a search call per pair and the host geometry (keyframes without HBM copies)
+    int create_new_map_points_host(int k) {
         float ow1[3];
         kf_ow(k, ow1);
         const float mb = s.bf / s.fx;
@@ -869,7 +1024,9 @@ struct orbmi_slam {
         const std::vector<int> neigh(kfs[k].covisible.begin(),
                                      kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
         const size_t n1 = kfs[k].keys.size();
-        for (int k2 : neigh) {
+        for (size_t i = 0; i < neigh.size(); i++) {
+            if (i > 0 && new_keyframes_queued()) return ORBMI_OK;  // src/LocalMapping.cc:331
+            const int k2 = neigh[i];
             float ow2[3];
             kf_ow(k2, ow2);
             const float d[3] = {ow2[0] - ow1[0], ow2[1] - ow1[1], ow2[2] - ow1[2]};
@@ -949,41 +1106,42 @@ struct orbmi_slam {
         return true;
     }
 
-    // ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for every
-    // point on the GPU, then the map updates in list order
-    int fuse(int k, const std::vector<int>& list, std::set<int>& dirty) {
-        if (!dirty.empty()) {
-            std::vector<int> pts;
-            for (int m : dirty)
-                if (!mps[m].bad) pts.push_back(m);
-            SLAM_CHECK(distinctive(pts));
-            dirty.clear();
-        }
-        std::vector<int> pts;
-        for (int m : list)
-            if (m >= 0) pts.push_back(m);
-        if (pts.empty()) return ORBMI_OK;
+    // the search record of a map point (orbmi_mappoint)
+    orbmi_mappoint fuse_record(int m) const {
+        const MapPoint& mp = mps[m];
+        orbmi_mappoint r;
+        std::memset(&r, 0, sizeof(r));
+        std::memcpy(r.pos, mp.pos, sizeof(r.pos));
+        std::memcpy(r.normal, mp.normal, sizeof(r.normal));
+        r.max_distance = mp.max_distance;
+        r.min_distance = mp.min_distance;
+        r.flags = (mp.bad ? ORBMI_MP_BAD : 0u) | (mp.nobs > 0 ? ORBMI_MP_HAS_OBS : 0u);
+        std::memcpy(r.desc, mp.desc, 32);
+        return r;
+    }
+
+    // the search of Fuse(k, pts) on the GPU (map lock released on the mapping thread)
+    int fuse_search(int k, const std::vector<int>& pts, std::vector<int32_t>& best) {
         std::vector<orbmi_mappoint> rec(pts.size());
         std::vector<uint8_t> in_kf(pts.size());
         for (size_t j = 0; j < pts.size(); j++) {
-            const MapPoint& mp = mps[pts[j]];
-            orbmi_mappoint& r = rec[j];
-            std::memcpy(r.pos, mp.pos, sizeof(r.pos));
-            std::memcpy(r.normal, mp.normal, sizeof(r.normal));
-            r.max_distance = mp.max_distance;
-            r.min_distance = mp.min_distance;
-            r.flags = (mp.bad ? ORBMI_MP_BAD : 0u) | (mp.nobs > 0 ? ORBMI_MP_HAS_OBS : 0u);
-            std::memcpy(r.desc, mp.desc, 32);
-            in_kf[j] = mp.obs.count(k) ? 1 : 0;
+            rec[j] = fuse_record(pts[j]);
+            in_kf[j] = mps[pts[j]].obs.count(k) ? 1 : 0;
         }
         const M4 tcw = kfs[k].tcw;
         const orbmi_frame_view v = kf_view(kfs[k], tcw.data());
-        std::vector<int32_t> best(pts.size()), dist(pts.size());
+        best.assign(pts.size(), -1);
+        std::vector<int32_t> dist(pts.size());
         int nc = 0;
         orbmi_matcher* mt = lmm();
-        SLAM_CHECK(unlocked([&] {
+        return unlocked([&] {
+            PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
             return orbmi_fuse_search(mt, &v, rec.data(), in_kf.data(), (int)pts.size(), 3.f, best.data(), dist.data(), &nc);
-        }));
+        });
+    }
+
+    // the map updates of Fuse(k, pts) (src/ORBmatcher.cc:1096-1124) in list order
+    void fuse_replay(int k, const std::vector<int>& pts, const int32_t* best, std::set<int>& dirty) {
         for (size_t j = 0; j < pts.size(); j++) {
             const int m = pts[j], b = best[j];
             if (mps[m].bad || mps[m].obs.count(k) || b < 0) continue;
@@ -1000,6 +1158,134 @@ struct orbmi_slam {
                 add_observation(m, k, b);
                 kfs[k].mps[b] = m;
             }
+        }
+    }
+
+    // ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for every
+    // point on the GPU, then the map updates in list order.  `dirty`: the survivors of Replace
+    // whose ComputeDistinctiveDescriptors (MapPoint::Replace, src/MapPoint.cc:212) is still due.
+    int fuse(int k, const std::vector<int>& list, std::set<int>& dirty) {
+        if (!dirty.empty()) {
+            std::vector<int> pts;
+            for (int m : dirty)
+                if (!mps[m].bad) pts.push_back(m);
+            SLAM_CHECK(distinctive(pts));
+            dirty.clear();
+        }
+        std::vector<int> pts;
+        for (int m : list)
+            if (m >= 0) pts.push_back(m);
+        if (pts.empty()) return ORBMI_OK;
+        std::vector<int32_t> best;
+        SLAM_CHECK(fuse_search(k, pts, best));
+        fuse_replay(k, pts, best.data(), dirty);
+        return ORBMI_OK;
+    }
+
+    // Fuse(target, the keyframe's points) for every target in order (src/LocalMapping.cc:620-628).
+    // The searches of all targets run in one orbmi_fuse_search_batch on the records as they are
+    // before the first target; a point's search depends only on its own record, its IsInKeyFrame
+    // and the target, so a target's batch result is the reference's wherever neither changed in
+    // the earlier targets' replays -- the points where one did (a Replace survivor's descriptor or
+    // observations) are searched again before that target's replay.  ComputeDistinctiveDescriptors
+    // of a survivor is done before the first read of its record (a survivor gains no observation
+    // from AddObservation before then: only listed points do, and a listed dirty point is
+    // recomputed before the target that could add one).
+    int fuse_targets(const std::vector<int>& targets, const std::vector<int>& list, std::set<int>& dirty) {
+        std::vector<int> pts;
+        for (int m : list)
+            if (m >= 0) pts.push_back(m);
+        const int nt = (int)targets.size(), np = (int)pts.size();
+        if (nt == 0 || np == 0) return ORBMI_OK;
+        std::vector<orbmi_mappoint> rec0(np);
+        for (int j = 0; j < np; j++) rec0[j] = fuse_record(pts[j]);
+        std::vector<uint8_t> in0((size_t)nt * np);
+        std::vector<M4> tcw(nt);
+        std::vector<orbmi_frame_view> views(nt);
+        for (int t = 0; t < nt; t++) {
+            for (int j = 0; j < np; j++) in0[(size_t)t * np + j] = mps[pts[j]].obs.count(targets[t]) ? 1 : 0;
+            tcw[t] = kfs[targets[t]].tcw;
+            views[t] = kf_view(kfs[targets[t]], tcw[t].data());
+        }
+        std::vector<int32_t> best((size_t)nt * np), dist((size_t)nt * np);
+        orbmi_matcher* mt = lmm();
+        SLAM_CHECK(unlocked([&] {
+            PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
+            return orbmi_fuse_search_batch(mt, nt, views.data(), rec0.data(), in0.data(), np, 3.f, best.data(),
+                                           dist.data(), nullptr);
+        }));
+        std::map<int, int> listed;  // point -> its (first) position in pts
+        for (int j = np - 1; j >= 0; j--) listed[pts[j]] = j;
+        for (int t = 0; t < nt; t++) {
+            const int kt = targets[t];
+            std::vector<int> due;
+            for (auto it = dirty.begin(); it != dirty.end();) {
+                if (listed.count(*it)) {
+                    if (!mps[*it].bad) due.push_back(*it);
+                    it = dirty.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            if (!due.empty()) {
+                // one device call: the due descriptors, and the searches of the listed records that
+                // take them against this and every later target (their batch rows are stale)
+                std::vector<uint8_t> rows;
+                std::vector<int32_t> off;
+                obs_rows(due, rows, off);
+                const int nd = (int)due.size();
+                std::vector<int> rj;  // positions in pts of the listed occurrences of due points
+                std::vector<int32_t> from;
+                for (int d = 0; d < nd; d++)
+                    for (int j = 0; j < np; j++)
+                        if (pts[j] == due[d]) {
+                            rj.push_back(j);
+                            from.push_back(off[d + 1] > off[d] ? d : -1);
+                        }
+                const int nr = (int)rj.size(), ntr = nt - t;
+                std::vector<orbmi_mappoint> rrec(std::max(nr, 1));
+                std::vector<uint8_t> rin(std::max((size_t)nr * ntr, (size_t)1));
+                std::vector<orbmi_frame_view> rv(views.begin() + t, views.end());
+                for (int q = 0; q < nr; q++) {
+                    rrec[q] = fuse_record(pts[rj[q]]);
+                    for (int u = 0; u < ntr; u++) rin[(size_t)u * nr + q] = mps[pts[rj[q]]].obs.count(targets[t + u]) ? 1 : 0;
+                }
+                std::vector<int32_t> dbest(nd), bi((size_t)std::max(nr * ntr, 1)), bd((size_t)std::max(nr * ntr, 1));
+                std::vector<uint8_t> dout((size_t)nd * 32);
+                for (int d = 0; d < nd; d++) std::memcpy(&dout[32 * d], mps[due[d]].desc, 32);
+                orbmi_matcher* mt2 = lmm();
+                SLAM_CHECK(unlocked([&] {
+                    PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
+                    return orbmi_fuse_search_refresh(mt2, rows.empty() ? nullptr : rows.data(), off.data(), nd,
+                                                     dbest.data(), dout.data(), ntr, rv.data(), rrec.data(),
+                                                     from.data(), rin.data(), nr, 3.f, bi.data(), bd.data());
+                }));
+                for (int d = 0; d < nd; d++)
+                    if (off[d + 1] > off[d]) std::memcpy(mps[due[d]].desc, &dout[32 * d], 32);
+                for (int q = 0; q < nr; q++) {
+                    rec0[rj[q]] = fuse_record(pts[rj[q]]);
+                    for (int u = 0; u < ntr; u++) best[(size_t)(t + u) * np + rj[q]] = bi[(size_t)u * nr + q];
+                }
+            }
+            int32_t* row = best.data() + (size_t)t * np;
+            std::vector<int> redo_pts, redo_j;
+            for (int j = 0; j < np; j++) {
+                const int m = pts[j];
+                // the replay skips bad points and points already in the target (observations are
+                // only gained here, so a point in the target now was in it or is skipped anyway)
+                if (mps[m].bad || mps[m].obs.count(kt)) continue;
+                const orbmi_mappoint r = fuse_record(m);
+                if (std::memcmp(&r, &rec0[j], sizeof(r)) != 0) {
+                    redo_pts.push_back(m);
+                    redo_j.push_back(j);
+                }
+            }
+            if (!redo_pts.empty()) {
+                std::vector<int32_t> b2;
+                SLAM_CHECK(fuse_search(kt, redo_pts, b2));
+                for (size_t q = 0; q < redo_j.size(); q++) row[redo_j[q]] = b2[q];
+            }
+            fuse_replay(kt, pts, row, dirty);
         }
         return ORBMI_OK;
     }
@@ -1021,7 +1307,7 @@ struct orbmi_slam {
         }
         std::set<int> dirty;
         const std::vector<int> matches = kfs[k].mps;
-        for (int t : targets) SLAM_CHECK(fuse(t, matches, dirty));
+        SLAM_CHECK(fuse_targets(targets, matches, dirty));
         std::vector<int> cands;
         for (int t : targets)
             for (int m : kfs[t].mps) {
@@ -1181,10 +1467,8 @@ struct orbmi_slam {
         res.pos = pos.data();
         res.erase = erase.data();
         int rc;
-        if (lm_lock) {  // the mapping thread: tracking runs while the GPU solves (mMutexMapUpdate)
-            lm_lock->unlock();
-            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
-            lm_lock->lock();
+        if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves (mMutexMapUpdate)
+            rc = unlocked([&] { return orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba); });
         } else {
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
         }
@@ -1261,20 +1545,22 @@ struct orbmi_slam {
         if (!kf.fv.valid) SLAM_CHECK(compute_bow(kf.desc, kf.fv));
         std::vector<uint8_t> ok_mp(std::max<size_t>(kf.mps.size(), 1), 0);
         for (size_t j = 0; j < kf.mps.size(); j++) ok_mp[j] = kf.mps[j] >= 0 && !mps[kf.mps[j]].bad;
-        const orbmi_frame_view vk = view(kf.keys, kf.desc, kf.ur, kf.tcw.data());
+        const M4 kf_tcw = kf.tcw;
+        const orbmi_frame_view vk = kf_view(kf, kf_tcw.data());
         const M4 I = eye4();
         const orbmi_frame_view vf = view(cf, I.data());
         const orbmi_feature_vector fk = kf.fv.view(), ff = cf.fv.view();
+        const std::vector<int> kf_mps = kf.mps;  // the keyframe's matches when the search ran
         std::vector<int32_t> m(std::max(cf.n(), 1));
         int n = 0;
-        SLAM_CHECK(orbmi_search_by_bow(matcher, &vk, ok_mp.data(), &fk, &vf, &ff, 0.7f, 1, m.data(), &n));
+        SLAM_CHECK(unlocked([&] { return orbmi_search_by_bow(matcher, &vk, ok_mp.data(), &fk, &vf, &ff, 0.7f, 1, m.data(), &n); }));
         st.bow_matches = n;
         st.track = 2;
         if (n < 15) return ORBMI_OK;
-        for (int i = 0; i < cf.n(); i++) cf.mps[i] = m[i] >= 0 ? kf.mps[m[i]] : -1;
+        for (int i = 0; i < cf.n(); i++) cf.mps[i] = m[i] >= 0 ? kf_mps[m[i]] : -1;
         cf.tcw = last_frame.tcw;
         cf.has_tcw = true;
-        const std::vector<orbmi_lastframe_point> lfp = lf_records(kf.mps, nullptr);
+        const std::vector<orbmi_lastframe_point> lfp = lf_records(kf_mps, nullptr);
         m.resize(cf.n());
         M4 tcw;
         std::vector<uint8_t> out;
@@ -1302,11 +1588,14 @@ struct orbmi_slam {
         const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
         {
             PhaseTimer pt(&phase_ms[PH_LF_SEARCH]);
-            SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1, m.data(),
-                                                             &n));
-            if (n < 20)
-                SLAM_CHECK(orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), 2 * th, 0, 1,
-                                                                 m.data(), &n));
+            SLAM_CHECK(unlocked([&] {
+                int rc = orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1,
+                                                               m.data(), &n);
+                if (!rc && n < 20)
+                    rc = orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), 2 * th, 0, 1,
+                                                               m.data(), &n);
+                return rc;
+            }));
         }
         st.track = 1;
         st.lf_matches = n;
@@ -1420,8 +1709,10 @@ struct orbmi_slam {
         std::vector<orbmi_mappoint_track> tr(std::max<size_t>(rec.size(), 1));
         {
             PhaseTimer pt(&phase_ms[PH_LOCAL_SEARCH]);
-            SLAM_CHECK(orbmi_search_local_points_track(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f,
-                                                       m_mp.data(), &nl, nullptr, tr.data()));
+            SLAM_CHECK(unlocked([&] {
+                return orbmi_search_local_points_track(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f,
+                                                       m_mp.data(), &nl, nullptr, tr.data());
+            }));
         }
         for (size_t j = 0; j < rec.size(); j++)
             if (tr[j].in_view) mps[local_mps[j]].visible++;
@@ -1650,8 +1941,14 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
         SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
     }
     PhaseTimer* lock_t = new PhaseTimer(&h->phase_ms[PH_LOCK]);
-    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    std::unique_lock<std::mutex> map_guard(h->map_mtx);
     delete lock_t;
+    // with the mapping thread running, Tracking's GPU calls release the map lock (their inputs
+    // are this thread's copies); the reference's Tracking and LocalMapping likewise interleave
+    struct Hold {
+        explicit Hold(std::unique_lock<std::mutex>* l) { held_lock = l; }
+        ~Hold() { held_lock = nullptr; }
+    } hold(h->async_lm() ? &map_guard : nullptr);
     {
         std::lock_guard<std::mutex> g(h->q_mtx);
         if (h->lm_rc) return h->lm_rc;

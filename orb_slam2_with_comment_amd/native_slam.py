@@ -117,7 +117,9 @@ class NativeStereoSLAM:
               lib().orbmi_slam_save_keyframe_trajectory_tum(self._h, filename.encode()))
 
     PHASES = ("frame_ctor", "map_lock_wait", "lf_search", "lf_pose", "local_kf_points", "local_records",
-              "frustum", "local_search", "local_pose", "keyframe", "total")
+              "frustum", "local_search", "local_pose", "keyframe", "total", "lm_process", "lm_point_culling",
+              "lm_create_points", "lm_search_in_neighbors", "lm_local_ba", "lm_keyframe_culling", "lm_total",
+              "lm_create_points_call", "lm_fuse_search_calls", "lm_distinctive_calls")
 
     def phase_ms(self):
         """Mean wall ms per tracked frame of each phase of TrackStereo (orbmi_slam_get_phase_ms)."""

@@ -1,0 +1,108 @@
+"""GPU parity of orbmi_create_new_map_points: LocalMapping::CreateNewMapPoints' neighbour loop
+(src/LocalMapping.cc:290-577) with every pair's search and triangulation on the device and the
+KF1 keypoints claimed by earlier pairs' new points excluded from later searches.  The expected
+values come from the reference's loop restated on the host: the oracle's SearchForTriangulation
+with KF1's map-point flags as the earlier pairs left them, then the host geometry
+(orbmi_triangulate_matches, the same tri_geom.h code the device kernel compiles).  Matches, the
+accept flags and the new points' positions are exact."""
+import argparse
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _tri_host(kf1, kf2, m12):
+    from orb_slam2_with_comment_amd._capi import check, lib
+    idx1 = np.nonzero(m12 >= 0)[0].astype(np.int32)
+    ok = np.zeros(len(m12), np.uint8)
+    x = np.zeros((len(m12), 3), np.float32)
+    if len(idx1):
+        idx2 = np.ascontiguousarray(m12[idx1], np.int32)
+        xo = np.zeros((len(idx1), 3), np.float32)
+        oo = np.zeros(len(idx1), np.uint8)
+        check("tri", lib().orbmi_triangulate_matches(C.addressof(kf1.tri), C.addressof(kf2.tri), idx1.ctypes.data,
+                                                     idx2.ctypes.data, len(idx1), xo.ctypes.data, oo.ctypes.data))
+        ok[idx1], x[idx1] = oo, xo
+    return ok, x
+
+
+@pytest.mark.parametrize("host_cos", [False, True])
+def test_create_new_map_points_matches_sequential_loop(oracle, host_cos):
+    import bench
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd._capi import check, lib
+    from orb_slam2_with_comment_amd.matcher import ORBmatcher
+    from orb_slam2_with_comment_amd.types import FeatureVectorView, FrameView, TriKeyFrame
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary, Vocabulary
+    S = bench.setup_track(argparse.Namespace(frames=4, nfeatures=2000), 0, 0)
+    vocab = Vocabulary.synthetic(k=10, L=5, seed=7)
+    voc = ORBVocabulary(vocab, device=0)
+    problem, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
+    jobs, keep = bench.setup_local_mapping(S, voc, vocab, 0, problem)
+    mt = ORBmatcher()
+    try:
+        total_new = total_claimed = 0
+        for f in (3, 5):
+            job, h = jobs[f], jobs[f].host
+            kf, nbs = job.kf, job.neighbours
+            n1, npairs = kf.n, len(nbs)
+            # the reference's loop on the host
+            has1 = h["kf"]["has_mp"].copy()
+            exp_m = np.full((npairs, n1), -1, np.int32)
+            exp_ok = np.zeros((npairs, n1), np.uint8)
+            exp_x = np.zeros((npairs, n1, 3), np.float32)
+            for j, nb in enumerate(h["neighbours"]):
+                m12, _ = oracle.search_for_triangulation(h["kf"]["frame"], has1, h["kf"]["fv"], nb["frame"],
+                                                         nb["has_mp"], nb["fv"], job.F12[j].reshape(3, 3), False, False)
+                ok, x = _tri_host(kf, nbs[j], m12)
+                exp_m[j], exp_ok[j], exp_x[j] = m12, ok, x
+                free, _ = oracle.search_for_triangulation(h["kf"]["frame"], h["kf"]["has_mp"], h["kf"]["fv"],
+                                                          nb["frame"], nb["has_mp"], nb["fv"],
+                                                          job.F12[j].reshape(3, 3), False, False)
+                total_claimed += int(((free >= 0) & (h["kf"]["has_mp"] == 0) & (has1 == 1)).sum())
+                has1[ok == 1] = 1
+            # one device call
+            cos1 = None
+            cos2 = None
+            tables = []
+            if not host_cos:  # the keyframes' parallax tables passed in (host arrays)
+                def table(k):
+                    t = np.zeros(max(k.n, 1), np.float32)
+                    check("cos", lib().orbmi_stereo_parallax_cos(C.c_float(k.tri.mb), k.depth.ctypes.data, k.n,
+                                                                 t.ctypes.data))
+                    tables.append(t)
+                    return t.ctypes.data
+                cos1 = table(kf)
+                cos2 = (C.c_void_p * npairs)(*[table(nb) for nb in nbs])
+            kf2 = (FrameView * npairs)(*[nb.view for nb in nbs])
+            tri2 = (TriKeyFrame * npairs)(*[nb.tri for nb in nbs])
+            has2_arr = [np.ascontiguousarray(hn["has_mp"], np.uint8) for hn in h["neighbours"]]
+            has2 = (C.c_void_p * npairs)(*[a.ctypes.data for a in has2_arr])
+            fv2 = (FeatureVectorView * npairs)(*[nb.fv.view() for nb in nbs])
+            fv1 = h["kf"]["fv"].view()
+            has1_in = np.ascontiguousarray(h["kf"]["has_mp"], np.uint8)
+            F12 = np.ascontiguousarray(np.concatenate(job.F12), np.float32)
+            got_m = np.zeros((npairs, n1), np.int32)
+            got_ok = np.zeros((npairs, n1), np.uint8)
+            got_x = np.zeros((npairs, n1, 3), np.float32)
+            check("orbmi_create_new_map_points", lib().orbmi_create_new_map_points(
+                mt._h, C.addressof(kf.view), C.addressof(kf.tri), cos1, has1_in.ctypes.data, C.addressof(fv1), npairs,
+                kf2, tri2, cos2, has2, fv2, F12.ctypes.data, got_m.ctypes.data, got_ok.ctypes.data,
+                got_x.ctypes.data))
+            np.testing.assert_array_equal(has1_in, h["kf"]["has_mp"])  # the input is not modified
+            for j in range(npairs):
+                np.testing.assert_array_equal(got_m[j], exp_m[j], err_msg=f"keyframe {f} pair {j} matches")
+                np.testing.assert_array_equal(got_ok[j], exp_ok[j], err_msg=f"keyframe {f} pair {j} accepted")
+                sel = exp_ok[j] == 1
+                np.testing.assert_array_equal(got_x[j][sel].view(np.uint32), exp_x[j][sel].view(np.uint32),
+                                              err_msg=f"keyframe {f} pair {j} positions")
+            total_new += int(exp_ok.sum())
+        # the sequential dependence is exercised: later pairs matched keypoints earlier pairs claimed
+        assert total_new > 0 and total_claimed > 0, (total_new, total_claimed)
+    finally:
+        mt.close()
+        voc.close()
+        S["tr"].close()

@@ -17,6 +17,8 @@
 #   prof_MODE        the same for --mode MODE
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the default bench -> traffic.json
 #   pmc_MODE         the same for --mode MODE
+#   native[_async]   tools/native_probe.py (sync / concurrent LocalMapping)
+#   nativeprof[_async] its rocprofv3 kernel stats
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 TAG=${1:-run}
 shift
@@ -73,6 +75,14 @@ for step in "$@"; do
             run pmc_fetch_$m 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch_$m -o fetch -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
             run pmc_write_$m 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write_$m -o write -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
             python tools/pmc_traffic.py $OUT/pmc_fetch_$m $OUT/pmc_write_$m $P/traffic_$m.json && head -40 $P/traffic_$m.json;;
+        native|native_async)
+            a=${step#native}; a=${a#_}
+            run native_probe$a 300 python tools/native_probe.py 200 $a; cat $OUT/native_probe$a.log;;
+        nativeprof|nativeprof_async)
+            a=${step#nativeprof}; a=${a#_}
+            run native_prof$a 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/native_prof$a -o np -- python3 tools/native_probe.py 200 $a
+            find $OUT/native_prof$a -name "*kernel_stats.csv" -exec cp {} $P/native${a}_kernel_stats.csv \;
+            cut -d, -f1-5 $P/native${a}_kernel_stats.csv | head -30;;
         ab=*)
             pair=${step#ab=}; A=${pair%,*}; B=${pair#*,}
             for i in 1 2 3; do
