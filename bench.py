@@ -215,8 +215,9 @@ def cpu_local_mapping(O, vocab, job):
     fv = FeatureVector.from_csr(node, off, feat)
     O.compute_distinctive_descriptors(h["obs_desc"], h["obs_off"])
     n_new = 0
+    has1 = h["kf"]["has_mp"].copy()  # KF1's map points as the earlier pairs leave them
     for j, nb in enumerate(h["neighbours"]):
-        m12, _ = O.search_for_triangulation(h["kf"]["frame"], h["kf"]["has_mp"], fv, nb["frame"], nb["has_mp"], nb["fv"],
+        m12, _ = O.search_for_triangulation(h["kf"]["frame"], has1, fv, nb["frame"], nb["has_mp"], nb["fv"],
                                             job.F12[j].reshape(3, 3), False, False)
         idx1 = np.nonzero(m12 >= 0)[0].astype(np.int32)
         if len(idx1):
@@ -226,6 +227,7 @@ def cpu_local_mapping(O, vocab, job):
             check("orbmi_triangulate_matches", lib().orbmi_triangulate_matches(
                 C_.addressof(job.kf.tri), C_.addressof(job.neighbours[j].tri), idx1.ctypes.data, idx2.ctypes.data,
                 len(idx1), x3d.ctypes.data, ok.ctypes.data))
+            has1[idx1[ok == 1]] = 1
             n_new += int(ok.sum())
     for nb in h["neighbours"]:
         O.fuse_search(nb["frame"], h["kf_points"], None, 3.0)

@@ -306,9 +306,19 @@ class KeyFrameData:
         self.sf = np.ascontiguousarray(scale_factors, np.float32)
         self.sig2 = np.ascontiguousarray(level_sigma2, np.float32)
         self.view = frame_view(self.n, d_keys, d_ur, d_desc, self.tcw, cam, self.sf, cam.width, cam.height)
+        mb = np.float32(np.float32(cam.bf) / np.float32(cam.fx))
         self.tri = TriKeyFrame(self.tcw.ctypes.data, self.keys.ctypes.data, self.ur.ctypes.data, self.depth.ctypes.data,
-                               cam.fx, cam.fy, cam.cx, cam.cy, cam.bf, np.float32(np.float32(cam.bf) / np.float32(cam.fx)),
-                               self.sig2.ctypes.data, self.sf.ctypes.data)
+                               cam.fx, cam.fy, cam.cx, cam.cy, cam.bf, mb, self.sig2.ctypes.data, self.sf.ctypes.data)
+        # HBM copies for orbmi_create_new_map_points: mvDepth and the stereo-parallax table
+        import torch
+        cos = np.zeros(max(self.n, 1), np.float32)
+        check("orbmi_stereo_parallax_cos", lib().orbmi_stereo_parallax_cos(C.c_float(mb), self.depth.ctypes.data, self.n,
+                                                                         cos.ctypes.data))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.d_depth = torch.from_numpy(np.ascontiguousarray(np.resize(self.depth, max(self.n, 1)))).to(dev)
+        self.d_cos = torch.from_numpy(cos).to(dev)
+        self.tri_dev = TriKeyFrame(self.tcw.ctypes.data, None, None, self.d_depth.data_ptr(), cam.fx, cam.fy, cam.cx,
+                                   cam.cy, cam.bf, mb, self.sig2.ctypes.data, self.sf.ctypes.data)
 
 
 class LocalMappingJob:
@@ -339,8 +349,8 @@ class LocalMapper:
                             MapPoint::ComputeDistinctiveDescriptors of the keyframe's points
                             (:135-198)
       CreateNewMapPoints    SearchForTriangulation(0.6, no orientation check) against every
-                            neighbour with its F12, then the host triangulation / acceptance
-                            geometry (orbmi_triangulate_matches) of the pairs (:290-577)
+                            neighbour with its F12 and the triangulation / acceptance geometry,
+                            pair by pair on the device (orbmi_create_new_map_points, :290-577)
       SearchInNeighbors     Fuse(neighbour, keyframe's points) for every target, Fuse(keyframe,
                             targets' points), ComputeDistinctiveDescriptors again (:589-674)
       LocalBundleAdjustment (:89-90)
@@ -439,35 +449,29 @@ class LocalMapper:
         dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
-        # ---- CreateNewMapPoints: SearchForTriangulation against every neighbour, one launch
-        from .types import FeatureVectorView
+        # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
+        # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
+        from .types import FeatureVectorView, TriKeyFrame
         nnb = len(job.neighbours)
         tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
+        tri_ok = self._buf("tri_ok", (max(nnb, 1) * kf.n,), torch.uint8)
+        x3d = self._buf("tri_x3d", (max(nnb, 1) * kf.n * 3,), torch.float32)
         fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
         if nnb:
             kf2 = (FrameView * nnb)(*[nb.view for nb in job.neighbours])
+            tri2 = (TriKeyFrame * nnb)(*[nb.tri_dev for nb in job.neighbours])
+            cos2 = (C.c_void_p * nnb)(*[nb.d_cos.data_ptr() for nb in job.neighbours])
             mp2 = (C.c_void_p * nnb)(*[nb.d_has_mp for nb in job.neighbours])
             fv2 = (FeatureVectorView * nnb)(*[nb.fv.view() for nb in job.neighbours])
             F12 = np.ascontiguousarray(np.concatenate(job.F12), np.float32)
-            check("orbmi_search_for_triangulation_batch", L.orbmi_search_for_triangulation_batch(
-                m, C.addressof(kf.view), _vp(kf.d_has_mp), C.addressof(fv1), nnb, kf2, mp2, fv2, F12.ctypes.data, 0, 0,
-                _vp(tri.data_ptr()), None))
+            check("orbmi_create_new_map_points", L.orbmi_create_new_map_points(
+                m, C.addressof(kf.view), C.addressof(kf.tri_dev), _vp(kf.d_cos.data_ptr()), _vp(kf.d_has_mp),
+                C.addressof(fv1), nnb, kf2, tri2, cos2, mp2, fv2, F12.ctypes.data, _vp(tri.data_ptr()),
+                _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         self._ms.synchronize()
-        tri_h = tri[:nnb * kf.n].cpu().numpy().reshape(nnb, kf.n)
-        n_pairs = n_new = 0
-        for j, nb in enumerate(job.neighbours):  # host geometry: triangulation + acceptance tests
-            idx1 = np.nonzero(tri_h[j] >= 0)[0].astype(np.int32)
-            if len(idx1) == 0:
-                continue
-            idx2 = np.ascontiguousarray(tri_h[j][idx1], np.int32)
-            x3d = np.zeros((len(idx1), 3), np.float32)
-            ok = np.zeros(len(idx1), np.uint8)
-            check("orbmi_triangulate_matches", L.orbmi_triangulate_matches(
-                C.addressof(kf.tri), C.addressof(nb.tri), idx1.ctypes.data, idx2.ctypes.data, len(idx1), x3d.ctypes.data,
-                ok.ctypes.data))
-            n_pairs += len(idx1)
-            n_new += int(ok.sum())
-        out["triangulation_pairs"], out["new_points"] = n_pairs, n_new
+        nt = nnb * kf.n
+        counts = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64)]).cpu().numpy()
+        out["triangulation_pairs"], out["new_points"] = int(counts[0]), int(counts[1])
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
         d_kp, n_kp = job.kf_points
         d_tp, n_tp = job.target_points
@@ -488,7 +492,10 @@ class LocalMapper:
         # ---- LocalBundleAdjustment
         self.last = self.ba.run(job.problem)
         out["local_ba_iterations"] = list(self.last["iterations"])
-        self._out = dict(tri=tri_h, best=best, dsc=dsc, bi=bi, bd=bd, n_fuse=o + n_tp,
+        self._out = dict(tri=lambda: tri[:nt].cpu().numpy().reshape(nnb, kf.n),
+                         tri_ok=lambda: tri_ok[:nt].cpu().numpy().reshape(nnb, kf.n),
+                         x3d=lambda: x3d[:3 * nt].cpu().numpy().reshape(nnb, kf.n, 3),
+                         best=best, dsc=dsc, bi=bi, bd=bd, n_fuse=o + n_tp,
                          fv=lambda: FeatureVector.from_csr(b["node"][:nn].cpu().numpy().view(np.uint32),
                                                            b["off"][:nn + 1].cpu().numpy(),
                                                            b["feat"][:kf.n].cpu().numpy()))

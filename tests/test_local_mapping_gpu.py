@@ -1,7 +1,7 @@
 """GPU parity of the LocalMapping chain the headline bench runs per keyframe
 (pipeline.LocalMapper.run_job, src/LocalMapping.cc:47-128): ComputeBoW (DBoW2 transform),
-ComputeDistinctiveDescriptors, SearchForTriangulation against every neighbour + the host
-triangulation, Fuse in both directions of SearchInNeighbors, LocalBundleAdjustment -- each
+ComputeDistinctiveDescriptors, CreateNewMapPoints (every neighbour's SearchForTriangulation +
+triangulation on the device, in the reference's pair order), Fuse in both directions of SearchInNeighbors, LocalBundleAdjustment -- each
 output compared with the oracle on the same inputs (bench.setup_local_mapping's job).  Index and
 descriptor outputs are exact; LocalBA's iteration counts are identical (its numeric bars are
 tests/test_lba_gpu.py's)."""
@@ -42,13 +42,17 @@ def test_local_mapping_chain_matches_oracle(oracle):
             best_ref, dsc_ref = oracle.compute_distinctive_descriptors(h["obs_desc"], h["obs_off"])
             np.testing.assert_array_equal(o["best"][:npts].cpu().numpy(), best_ref)
             np.testing.assert_array_equal(o["dsc"][:32 * npts].cpu().numpy().reshape(npts, 32), dsc_ref)
-            # CreateNewMapPoints: the searches (exact) and the points the host geometry accepts
+            # CreateNewMapPoints: the reference's loop (the oracle's search with KF1's map points as
+            # the earlier pairs left them, the host geometry) -- matches, accepts and positions exact
             n_new = 0
+            has1 = h["kf"]["has_mp"].copy()
+            tri, tri_ok, x3d_d = o["tri"](), o["tri_ok"](), o["x3d"]()
             for j, nb in enumerate(h["neighbours"]):
-                m12, _ = oracle.search_for_triangulation(h["kf"]["frame"], h["kf"]["has_mp"], o["fv"], nb["frame"],
+                m12, _ = oracle.search_for_triangulation(h["kf"]["frame"], has1, o["fv"], nb["frame"],
                                                          nb["has_mp"], nb["fv"], job.F12[j].reshape(3, 3), False,
                                                          False)
-                np.testing.assert_array_equal(o["tri"][j], m12, err_msg=f"keyframe {f} neighbour {j}")
+                np.testing.assert_array_equal(tri[j], m12, err_msg=f"keyframe {f} neighbour {j}")
+                ok_ref = np.zeros(len(m12), np.uint8)
                 idx1 = np.nonzero(m12 >= 0)[0].astype(np.int32)
                 if len(idx1):
                     idx2 = np.ascontiguousarray(m12[idx1], np.int32)
@@ -57,7 +61,12 @@ def test_local_mapping_chain_matches_oracle(oracle):
                     check("tri", lib().orbmi_triangulate_matches(
                         C.addressof(job.kf.tri), C.addressof(job.neighbours[j].tri), idx1.ctypes.data,
                         idx2.ctypes.data, len(idx1), x3d.ctypes.data, ok.ctypes.data))
+                    ok_ref[idx1] = ok
+                    sel = ok == 1
+                    np.testing.assert_array_equal(x3d_d[j][idx1[sel]].view(np.uint32), x3d[sel].view(np.uint32))
+                    has1[idx1[sel]] = 1
                     n_new += int(ok.sum())
+                np.testing.assert_array_equal(tri_ok[j], ok_ref, err_msg=f"keyframe {f} neighbour {j} accepted")
             assert out["new_points"] == n_new and n_new > 0
             # SearchInNeighbors: Fuse(target, KF points) per target, then Fuse(KF, targets' points)
             n_kp = len(h["kf_points"])

@@ -19,6 +19,8 @@
 #   pmc_MODE         the same for --mode MODE
 #   native[_async]   tools/native_probe.py (sync / concurrent LocalMapping)
 #   nativeprof[_async] its rocprofv3 kernel stats
+#   lmprobe          tools/lm_chain_probe.py (per-call split of the LocalMapping chain)
+#   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 TAG=${1:-run}
 shift
@@ -83,6 +85,13 @@ for step in "$@"; do
             run native_prof$a 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/native_prof$a -o np -- python3 tools/native_probe.py 200 $a
             find $OUT/native_prof$a -name "*kernel_stats.csv" -exec cp {} $P/native${a}_kernel_stats.csv \;
             cut -d, -f1-5 $P/native${a}_kernel_stats.csv | head -30;;
+        lmprobe)
+            run lmprobe 300 python tools/lm_chain_probe.py 20; tail -14 $OUT/lmprobe.log;;
+        mfma_pmc)
+            # MFMA A/B of the Schur products: MFMA issue / busy counters of each variant's kernel
+            run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur
+            find $OUT/mfma_pmc -name "*counter_collection.csv" -exec cp {} $P/mfma_schur_pmc.csv \;
+            cp $OUT/mfma_pmc.log $P/mfma_schur_pmc.log; tail -12 $OUT/mfma_pmc.log;;
         ab=*)
             pair=${step#ab=}; A=${pair%,*}; B=${pair#*,}
             for i in 1 2 3; do

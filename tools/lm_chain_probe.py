@@ -38,7 +38,8 @@ def main():
     from orb_slam2_with_comment_amd import _capi
     L = _capi.lib()
     names = ["orbmi_transform", "orbmi_compute_distinctive_descriptors", "orbmi_search_for_triangulation",
-             "orbmi_search_for_triangulation_batch", "orbmi_triangulate_matches", "orbmi_fuse_search",
+             "orbmi_search_for_triangulation_batch", "orbmi_triangulate_matches", "orbmi_create_new_map_points",
+             "orbmi_fuse_search",
              "orbmi_fuse_search_batch", "orbmi_local_bundle_adjustment"]
 
     class Wrap:
