@@ -327,6 +327,12 @@ int orbmi_vocabulary_synchronize(orbmi_vocabulary* v);
 /* Run the handle on `ex`'s stream (like orbmi_matcher_share_stream): a keyframe's ComputeBoW then
  * follows its extraction on the extraction stream, beside the LocalBA on the mapper's stream. */
 int orbmi_vocabulary_share_stream(orbmi_vocabulary* v, orbmi_extractor* ex);
+/* Run the handle on a caller's HIP stream (hipStream_t, e.g. orbmi_matcher_get_stream's), or on
+ * a new stream of its own when `stream` is NULL.  The stream must outlive its use here.  Every
+ * stream a process creates beyond the device's hardware queues (GPU_MAX_HW_QUEUES) shares a
+ * queue with another and serialises behind its work: an in-order chain of operators (the
+ * LocalMapping thread's) belongs on one stream. */
+int orbmi_vocabulary_set_stream(orbmi_vocabulary* v, void* stream);
 /* The handle's HIP stream (hipStream_t): its own, or the extractor's after share_stream. */
 int orbmi_vocabulary_get_stream(orbmi_vocabulary* v, void** stream);
 
@@ -404,6 +410,9 @@ typedef struct orbmi_ba_result {
 typedef struct orbmi_ba orbmi_ba;
 int orbmi_ba_create(int device, orbmi_ba** out);
 void orbmi_ba_destroy(orbmi_ba* h);
+/* Run the handle on a caller's HIP stream, or its own new one when `stream` is NULL (as
+ * orbmi_vocabulary_set_stream). */
+int orbmi_ba_set_stream(orbmi_ba* b, void* stream);
 
 /* Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (include/Optimizer.h:62,
  * src/Optimizer.cc:483-808) on the assembled graph: LM (g2o OptimizationAlgorithmLevenberg,

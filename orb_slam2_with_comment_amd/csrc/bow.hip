@@ -438,6 +438,18 @@ int orbmi_vocabulary_share_stream(orbmi_vocabulary* h, orbmi_extractor* ex) {
     return ORBMI_OK;
 }
 
+int orbmi_vocabulary_set_stream(orbmi_vocabulary* h, void* stream) {
+    if (!h) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(h->device));
+    ORBMI_HIP(hipStreamSynchronize(h->stream));
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) ORBMI_HIP(orbmi::stream_create(&s, "VOCAB"));
+    if (h->own_stream) ORBMI_HIP(hipStreamDestroy(h->stream));
+    h->stream = s;
+    h->own_stream = stream == nullptr;
+    return ORBMI_OK;
+}
+
 int orbmi_vocabulary_synchronize(orbmi_vocabulary* h) {
     if (!h) return ORBMI_E_ARG;
     ORBMI_HIP(hipStreamSynchronize(h->stream));

@@ -1538,6 +1538,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_finish(BaDev a, float* __restri
 struct orbmi_ba {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;  // false after orbmi_ba_set_stream(b, s != NULL)
     hipEvent_t done = nullptr;
     uint8_t* d_buf = nullptr;
     size_t cap = 0;
@@ -1671,8 +1672,20 @@ void orbmi_ba_destroy(orbmi_ba* b) {
     if (b->h_ctl) (void)hipHostFree(b->h_ctl);
     if (b->h_stop) (void)hipHostFree(b->h_stop);
     if (b->done) (void)hipEventDestroy(b->done);
-    if (b->stream) (void)hipStreamDestroy(b->stream);
+    if (b->stream && b->own_stream) (void)hipStreamDestroy(b->stream);
     delete b;
+}
+
+int orbmi_ba_set_stream(orbmi_ba* b, void* stream) {
+    if (!b) return ORBMI_E_ARG;
+    ORBMI_HIP(hipSetDevice(b->device));
+    ORBMI_HIP(hipStreamSynchronize(b->stream));
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) ORBMI_HIP(orbmi::stream_create(&s, "BA"));
+    if (b->own_stream) ORBMI_HIP(hipStreamDestroy(b->stream));
+    b->stream = s;
+    b->own_stream = stream == nullptr;
+    return ORBMI_OK;
 }
 
 int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_ba_result* R,

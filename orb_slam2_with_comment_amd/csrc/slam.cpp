@@ -1880,6 +1880,14 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
     if (!rc && s->async_local_mapping) rc = orbmi_matcher_create(device, &h->lm_matcher);
     if (!rc) rc = orbmi_pose_create(device, &h->pose);
     if (!rc) rc = orbmi_ba_create(device, &h->ba);
+    // each thread's operators in order on one stream (Tracking: searches + PoseOptimization;
+    // LocalMapping: searches + LocalBA), so the streams stay within the hardware queues
+    if (!rc) rc = orbmi_pose_share_matcher_stream(h->pose, h->matcher);
+    if (!rc) {
+        void* st = nullptr;
+        rc = orbmi_matcher_get_stream(h->lm_matcher ? h->lm_matcher : h->matcher, &st);
+        if (!rc) rc = orbmi_ba_set_stream(h->ba, st);
+    }
     if (!rc) {
         h->scale_factors.resize(s->n_levels);
         h->inv_level_sigma2.resize(s->n_levels);

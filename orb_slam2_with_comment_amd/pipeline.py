@@ -26,6 +26,7 @@ overlapping tracking as in the reference.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import queue
 import threading
 
@@ -381,6 +382,13 @@ class LocalMapper:
         ms = _vp()
         check("orbmi_matcher_get_stream", lib().orbmi_matcher_get_stream(self.matcher._h, C.byref(ms)))
         self._ms = torch.cuda.ExternalStream(ms.value, device=dev)  # the mapper's search stream
+        # the whole chain (ComputeBoW, searches, LocalBA) is in order: one stream, so that the
+        # process's streams stay within the device's hardware queues (orbmi_ba_set_stream)
+        self._one_stream = os.environ.get("ORBMI_LM_STREAMS", "one") == "one"
+        if self._one_stream:
+            check("orbmi_ba_set_stream", lib().orbmi_ba_set_stream(self.ba._h, ms))
+            if vocabulary is not None:
+                check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(vocabulary._h, ms))
         self.q: queue.Queue = queue.Queue()
         self.done = 0
         self.last = None
@@ -421,8 +429,8 @@ class LocalMapper:
                                       b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
                                       b["counts"].data_ptr())
             bow_done = self._bow_event()
-        # LocalBundleAdjustment reads poses, points and observations, never the BowVector, so
-        # the transform (vocabulary stream) and the LocalBA (its own stream) overlap
+        # LocalBundleAdjustment reads poses, points and observations, never the BowVector (both
+        # run in order on the mapper's stream)
         self.last = self.ba.run(problem)
         if self.voc is not None and kf_desc is not None:
             bow_done.synchronize()
@@ -526,6 +534,8 @@ class LocalMapper:
     def close(self):
         self.q.put(None)
         self.t.join()
+        if self._one_stream and self.voc is not None and getattr(self.voc, "_h", None):  # it outlives the mapper
+            check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(self.voc._h, None))
         self.ba.close()
         self.matcher.close()
 
