@@ -478,12 +478,16 @@ int orbmi_compute_distinctive_descriptors(orbmi_matcher* h, const uint8_t* obs_d
     Matcher& m = h->m;
     ORBMI_HIP(hipSetDevice(m.device));
     m.arena_reset();
+    // the row count is needed only to stage host descriptors (a device array is used in place)
     int total = 0;
-    if (on_device(obs_off)) ORBMI_HIP(hipMemcpy(&total, obs_off + np, sizeof(int), hipMemcpyDeviceToHost));
-    else total = obs_off[np];
-    if (total < 0 || (total > 0 && !obs_desc)) return ORBMI_E_ARG;
+    const bool desc_dev = on_device(obs_desc);
+    if (!desc_dev) {
+        if (on_device(obs_off)) ORBMI_HIP(hipMemcpy(&total, obs_off + np, sizeof(int), hipMemcpyDeviceToHost));
+        else total = obs_off[np];
+        if (total < 0 || (total > 0 && !obs_desc)) return ORBMI_E_ARG;
+    }
     int rc = 0;
-    const uint8_t* d_desc = dev_in(m, obs_desc, (size_t)total * 32, &rc);
+    const uint8_t* d_desc = desc_dev ? obs_desc : dev_in(m, obs_desc, (size_t)total * 32, &rc);
     const int* d_off = dev_in(m, obs_off, (size_t)np + 1, &rc);
     if (rc) return rc;
     std::vector<OutBuf> outs;

@@ -320,6 +320,13 @@ class KeyFrameData:
         self.d_cos = torch.from_numpy(cos).to(dev)
         self.tri_dev = TriKeyFrame(self.tcw.ctypes.data, None, None, self.d_depth.data_ptr(), cam.fx, cam.fy, cam.cx,
                                    cam.cy, cam.bf, mb, self.sig2.ctypes.data, self.sf.ctypes.data)
+        # the FeatureVector in HBM too (a keyframe's is computed there by its ComputeBoW and stays)
+        self.fv_dev = None
+        if fv is not None:
+            from .types import FeatureVectorView
+            self._fv_t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
+                          (fv.node_id.view(np.int32), fv.off, np.resize(fv.feat, max(len(fv.feat), 1)))]
+            self.fv_dev = FeatureVectorView(len(fv.node_id), *[t.data_ptr() for t in self._fv_t])
 
 
 class LocalMappingJob:
@@ -340,6 +347,16 @@ class LocalMappingJob:
             F = np.zeros(9, np.float32)
             check("orbmi_compute_f12", lib().orbmi_compute_f12(C.addressof(kf.tri), C.addressof(nb.tri), F.ctypes.data))
             self.F12.append(F)
+        # the neighbours as the C ABI takes them (views of their HBM arrays)
+        from .types import FeatureVectorView, TriKeyFrame
+        nnb = len(neighbours)
+        self.c_kf2 = (FrameView * max(nnb, 1))(*[nb.view for nb in neighbours])
+        self.c_tri2 = (TriKeyFrame * max(nnb, 1))(*[nb.tri_dev for nb in neighbours])
+        self.c_cos2 = (C.c_void_p * max(nnb, 1))(*[nb.d_cos.data_ptr() for nb in neighbours])
+        self.c_mp2 = (C.c_void_p * max(nnb, 1))(*[nb.d_has_mp for nb in neighbours])
+        self.c_fv2 = (FeatureVectorView * max(nnb, 1))(*[nb.fv_dev if nb.fv_dev is not None else nb.fv.view()
+                                                          for nb in neighbours])
+        self.c_F12 = np.ascontiguousarray(np.concatenate(self.F12) if nnb else np.zeros(9), np.float32)
 
 
 class LocalMapper:
@@ -459,23 +476,18 @@ class LocalMapper:
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
-        from .types import FeatureVectorView, TriKeyFrame
+        from .types import FeatureVectorView
         nnb = len(job.neighbours)
         tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
         tri_ok = self._buf("tri_ok", (max(nnb, 1) * kf.n,), torch.uint8)
         x3d = self._buf("tri_x3d", (max(nnb, 1) * kf.n * 3,), torch.float32)
         fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
+        kf2 = job.c_kf2
         if nnb:
-            kf2 = (FrameView * nnb)(*[nb.view for nb in job.neighbours])
-            tri2 = (TriKeyFrame * nnb)(*[nb.tri_dev for nb in job.neighbours])
-            cos2 = (C.c_void_p * nnb)(*[nb.d_cos.data_ptr() for nb in job.neighbours])
-            mp2 = (C.c_void_p * nnb)(*[nb.d_has_mp for nb in job.neighbours])
-            fv2 = (FeatureVectorView * nnb)(*[nb.fv.view() for nb in job.neighbours])
-            F12 = np.ascontiguousarray(np.concatenate(job.F12), np.float32)
             check("orbmi_create_new_map_points", L.orbmi_create_new_map_points(
                 m, C.addressof(kf.view), C.addressof(kf.tri_dev), _vp(kf.d_cos.data_ptr()), _vp(kf.d_has_mp),
-                C.addressof(fv1), nnb, kf2, tri2, cos2, mp2, fv2, F12.ctypes.data, _vp(tri.data_ptr()),
-                _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
+                C.addressof(fv1), nnb, kf2, job.c_tri2, job.c_cos2, job.c_mp2, job.c_fv2, job.c_F12.ctypes.data,
+                _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         self._ms.synchronize()
         nt = nnb * kf.n
         counts = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64)]).cpu().numpy()
