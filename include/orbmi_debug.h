@@ -33,6 +33,11 @@ int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_
  * evaluations, calls that fell back to the sequential replay}; synchronises the device. */
 int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
 
+/* k_greedy's s_memtime cycles summed over calls since the last reset: out[0] prologue (queries'
+ * prefixes and the keypoints' octave / occupancy loaded), [1] the rounds to the fixpoint,
+ * [2] the outputs (rotation histogram, last assignment per keypoint). */
+int orbmi_debug_greedy_cycles(unsigned long long* out, int reset);
+
 /* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame
  * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
  * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,

@@ -102,6 +102,7 @@ _PROTOS = {
     "orbmi_debug_octree_level": (_i, [_vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "orbmi_debug_pose_trace": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "orbmi_debug_greedy_stats": (_i, [_vp, _i]),
+    "orbmi_debug_greedy_cycles": (_i, [_vp, _i]),
     "orbmi_compute_f12": (_i, [_vp, _vp, _vp]),
     "orbmi_triangulate_matches": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_stereo_parallax_cos": (_i, [C.c_float, _vp, _i, _vp]),

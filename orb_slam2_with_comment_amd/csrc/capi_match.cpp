@@ -759,4 +759,9 @@ int orbmi_debug_greedy_stats(unsigned long long* out, int reset) {
     return orbmi::greedy_stats(out, reset);
 }
 
+int orbmi_debug_greedy_cycles(unsigned long long* out, int reset) {
+    if (!out) return ORBMI_E_ARG;
+    return orbmi::greedy_cycles(out, reset);
+}
+
 }  // extern "C"

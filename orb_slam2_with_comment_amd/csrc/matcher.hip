@@ -436,8 +436,17 @@ __device__ inline int greedy_eval(const GreedyArgs& a, int q, const float* Tc, b
     if (b2 == ~0ull && nc > kTopK) {
         b1 = b2 = ~0ull;
         if (nc <= a.cap) {
+            // the list in chunks of 16 loads in flight (one dependent load per entry made a
+            // query's slow path, and the whole workgroup's round with it, ~100 load latencies)
             const unsigned long long* c = a.cand + (long long)q * a.cap;
-            for (int k = 0; k < nc; k++) take(c[k]);
+            for (int k0 = 0; k0 < nc; k0 += 16) {
+                unsigned long long e[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) e[j] = k0 + j < nc ? c[k0 + j] : ~0ull;
+#pragma unroll
+                for (int j = 0; j < 16; j++)
+                    if (e[j] != ~0ull) take(e[j]);
+            }
         } else if (a.mode == 0) {  // overflowed list: enumerate again
             local_candidates(a.F, a.cs, a.cl, a.mps[q], a.tr[q], a.th, take);
         } else {
@@ -484,11 +493,17 @@ __device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int
     return d1 <= TH_HIGH ? i1 : -1;
 }
 
-constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = 4;
+#ifndef ORBMI_GREEDY_PRE
+#define ORBMI_GREEDY_PRE 4
+#endif
+constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = ORBMI_GREEDY_PRE;
 
 // k_greedy statistics (orbmi_debug_greedy_stats): calls, rounds summed, largest round count,
 // slow-path query evaluations summed, calls that fell back to the sequential replay
 __device__ unsigned long long g_greedy_stats[5];
+// development aid: s_memtime cycles of k_greedy's phases summed over calls (prologue, rounds,
+// epilogue), read with the statistics (orbmi_debug_greedy_stats out[5..7] when asked for 8)
+__device__ unsigned long long g_greedy_cycles[3];
 
 // Each thread keeps its queries (q = tid + k * 1024) in registers: current result, candidate
 // count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
@@ -502,6 +517,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int flag[4];
     if (a.gate && *a.gate >= a.gate_min) return;  // uniform: every thread reads before any write
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
     const int tid = threadIdx.x, n = frame_n(a.F);
     const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;  // (the by-value argument stays unmodified)
     bool fw = false, bw = false;
@@ -537,11 +553,13 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     if (!regs)
         for (int q = tid; q < nq; q += blockDim.x) a.res[q] = -1;
     __syncthreads();
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     bool converged = false;
     int rounds = 0, nslow = 0;
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
         rounds++;
-        for (int i = tid; i < n; i += blockDim.x) claim[i] = 0x7FFFFFFF;
+        // the initial occupancy folded in (-1 < every query): one LDS read per candidate test
+        for (int i = tid; i < n; i += blockDim.x) claim[i] = occ0[i] ? -1 : 0x7FFFFFFF;
         if (tid == 0) flag[0] = 0;
         __syncthreads();
         if (regs) {
@@ -570,7 +588,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                 for (int j = 0; j < kGreedyPre; j++) {
                     if (j >= kk || i2 >= 0) continue;
                     const int idx = (int)(pre[k][j] & 0xFFFF), d = (int)(pre[k][j] >> 16);
-                    if (occ0[idx] || claim[idx] < q) continue;
+                    if (claim[idx] < q) continue;
                     if (i1 < 0) { d1 = d; i1 = idx; } else { d2 = d; i2 = idx; }
                 }
                 if (i2 < 0 && nc[k] > kGreedyPre) slow |= 1u << k;  // prefix exhausted
@@ -580,8 +598,29 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             for (int k = 0; k < kGreedyQPer; k++)  // not unrolled: one copy of the slow path
                 if (slow >> k & 1) {
                     const int q = tid + k * kGreedyThreads;
-                    slowres[k * kGreedyThreads + tid] =
-                        greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                    auto occ = [&](int idx) { return claim[idx] < q; };
+                    int r;
+                    if (nc[k] <= a.cap) {
+                        // the whole list, 16 loads in flight; octaves from LDS
+                        unsigned long long b1 = ~0ull, b2 = ~0ull;
+                        const unsigned long long* c = a.cand + (long long)q * a.cap;
+                        for (int k0 = 0; k0 < nc[k]; k0 += 16) {
+                            unsigned long long e[16];
+#pragma unroll
+                            for (int j = 0; j < 16; j++) e[j] = k0 + j < nc[k] ? c[k0 + j] : ~0ull;
+#pragma unroll
+                            for (int j = 0; j < 16; j++) {
+                                if (e[j] == ~0ull || occ((int)(e[j] & 0xFFFFF))) continue;
+                                if (e[j] < b1) { b2 = b1; b1 = e[j]; }
+                                else if (e[j] < b2) b2 = e[j];
+                            }
+                        }
+                        r = greedy_decide(a, oct, (int)(b1 >> 40), b1 == ~0ull ? -1 : (int)(b1 & 0xFFFFF), (int)(b2 >> 40),
+                                          b2 == ~0ull ? -1 : (int)(b2 & 0xFFFFF));
+                    } else {  // overflowed list: enumerate again
+                        r = greedy_eval(a, q, Tc.m, fw, bw, occ);
+                    }
+                    slowres[k * kGreedyThreads + tid] = r;
                 }
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++) {
@@ -590,7 +629,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             }
         } else {
             for (int q = tid; q < nq; q += blockDim.x) {
-                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return occ0[idx] || claim[idx] < q; });
+                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return claim[idx] < q; });
                 if (r != a.res[q]) { a.res[q] = r; changed = 1; }
             }
         }
@@ -619,6 +658,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         }
         __syncthreads();
     }
+    const unsigned long long c2 = __builtin_amdgcn_s_memtime();
     // outputs: last assignment per keypoint (claim[] reused); rotation consistency (mode 1),
     // rejected keypoints flagged in occ0[]
     int* last = claim;
@@ -627,13 +667,40 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     if (tid < HISTO_LENGTH) hist[tid] = 0;
     if (tid == 0) flag[1] = 0;
     __syncthreads();
-    for (int q = tid; q < nq; q += blockDim.x) {
-        const int r = a.res[q];
-        if (r < 0) continue;
+    // the final assignments (registers when the queries fit them) and, for the rotation check,
+    // each query's bin, computed once
+    int fbin[kGreedyQPer];
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) fbin[k] = -1;
+    if (!converged && regs) {  // the sequential replay's results
+#pragma unroll
+        for (int k = 0; k < kGreedyQPer; k++) {
+            const int q = tid + k * kGreedyThreads;
+            if (q < nq) res[k] = a.res[q];
+        }
+    }
+    auto each_query = [&](auto&& f) {
+        if (regs) {
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++) {
+                const int q = tid + k * kGreedyThreads;
+                if (q < nq) f(k, q, res[k]);
+            }
+        } else {
+            for (int q = tid; q < nq; q += blockDim.x) f(-1, q, a.res[q]);
+        }
+    };
+    const bool ori = a.mode == 1 && a.check_ori;
+    each_query([&](int k, int q, int r) {
+        if (r < 0) return;
         atomicMax(&last[r], q);
         atomicAdd(&flag[1], 1);
-        if (a.mode == 1 && a.check_ori) atomicAdd(&hist[rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle)], 1);
-    }
+        if (ori) {
+            const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
+            atomicAdd(&hist[bin], 1);
+            if (k >= 0) fbin[k] = bin;
+        }
+    });
     __syncthreads();
     int ind1 = -1, ind2 = -1, ind3 = -1;
     if (a.mode == 1 && a.check_ori) {  // ComputeThreeMaxima (:1854-1895), same in every thread
@@ -646,23 +713,43 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         }
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-        for (int q = tid; q < nq; q += blockDim.x) {
-            const int r = a.res[q];
-            if (r < 0) continue;
-            const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
+        each_query([&](int k, int q, int r) {
+            if (r < 0) return;
+            int bin = -1;
+            if (k >= 0) {
+#pragma unroll
+                for (int kk = 0; kk < kGreedyQPer; kk++)
+                    if (kk == k) bin = fbin[kk];
+            } else {
+                bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
+            }
             if (bin != ind1 && bin != ind2 && bin != ind3) { rejected[r] = 1; atomicSub(&flag[1], 1); }
-        }
+        });
         __syncthreads();
     }
     for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
     if (tid == 0) *a.nmatches = flag[1];
     if (nslow) atomicAdd(&g_greedy_stats[3], (unsigned long long)nslow);
     if (tid == 0) {
+        const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&g_greedy_cycles[0], c1 - c0);
+        atomicAdd(&g_greedy_cycles[1], c2 - c1);
+        atomicAdd(&g_greedy_cycles[2], c3 - c2);
         atomicAdd(&g_greedy_stats[0], 1ull);
         atomicAdd(&g_greedy_stats[1], (unsigned long long)rounds);
         atomicMax(&g_greedy_stats[2], (unsigned long long)rounds);
         if (!converged) atomicAdd(&g_greedy_stats[4], 1ull);
     }
+}
+
+int greedy_cycles(unsigned long long out[3], int reset) {
+    ORBMI_HIP(hipDeviceSynchronize());
+    ORBMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_greedy_cycles), sizeof(unsigned long long) * 3));
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_greedy_cycles), z, sizeof(z)));
+    }
+    return ORBMI_OK;
 }
 
 int greedy_stats(unsigned long long out[5], int reset) {

@@ -27,6 +27,8 @@ def main():
                  S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
     tr.synchronize()
     L.orbmi_debug_greedy_stats(st, 1)
+    cyc = (C.c_ulonglong * 3)()
+    L.orbmi_debug_greedy_cycles(cyc, 1)
     for i in range(nfr):
         f = 2 + i % 8
         tr.track(S["imgs"].data_ptr() + f * 2 * rows * cols, rows, cols, S["tcws"][f], S["lf_views"][f - 1],
@@ -36,6 +38,9 @@ def main():
     calls = max(st[0], 1)
     print(f"k_greedy: {st[0]} calls, rounds mean {st[1] / calls:.2f}, max {st[2]}, slow evaluations per call "
           f"{st[3] / calls:.1f}, sequential fallbacks {st[4]}")
+    L.orbmi_debug_greedy_cycles(cyc, 0)
+    print("k_greedy s_memtime cycles per call: prologue %.0f, rounds %.0f, "
+          "outputs %.0f" % tuple(c / calls for c in cyc))
     print("result:", tr.results()["search_matches"], tr.results()["inliers"])
     tr.close()
 
