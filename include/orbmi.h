@@ -600,6 +600,8 @@ typedef struct orbmi_slam_frame_stats {
     int frame, n, state, init, track;
     int lf_matches, bow_matches, nmatches_map, local_map_points, local_matches, inliers;
     int need_kf, keyframes, mappoints;
+    int reset; /* 1: the frame was lost with <= 5 keyframes in the map and the system reset
+                * (src/Tracking.cc:540-551); the map and the trajectory lists start over */
 } orbmi_slam_frame_stats;
 
 typedef struct orbmi_slam orbmi_slam;
@@ -621,9 +623,10 @@ void orbmi_slam_destroy(orbmi_slam* h);
 int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
                             double timestamp, float* tcw_out, int* has_pose);
 
-/* The counters of tracked frame `frame` (0-based). */
+/* The counters of the `frame`-th TrackStereo call (0-based; the record stays across a reset,
+ * while frame ids restart); ORBMI_E_ARG past the last call. */
 int orbmi_slam_get_stats(orbmi_slam* h, int frame, orbmi_slam_frame_stats* out);
-/* frames tracked, keyframes, non-bad map points, LocalBundleAdjustment calls */
+/* frames since the last reset (Frame::nNextId), keyframes, non-bad map points, LocalBundleAdjustment calls */
 int orbmi_slam_get_counts(orbmi_slam* h, int* frames, int* keyframes, int* mappoints, int* local_ba_calls);
 /* The poses SaveTrajectoryKITTI / TUM write (src/System.cc:334-486): per recorded frame Tcw =
  * Tcr * Trw * Two (16 floats), its timestamp and mlbLost.  capacity < n -> ORBMI_E_CAP, *n set. */

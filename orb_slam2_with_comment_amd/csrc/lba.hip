@@ -921,6 +921,13 @@ __device__ inline double rcp_f64(double d) {
     return fma(r, e, r);
 }
 
+// lane `l`'s value of v, in every lane (l wave-uniform)
+__device__ inline double readlane_f64(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 // LDL^T of a 6x6 tile (full row-major, upper triangle used): on return F[j][c] = U_jc (c > j),
 // F[j][j] = d_j, inv6 = 1 / d.  False on a zero or non-finite pivot.
 __device__ inline bool ldl6(double F[36], double inv6[6]) {
@@ -1151,7 +1158,6 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
     SOLVE_STAMP(threadIdx.x == 0, 250);
     __shared__ __attribute__((aligned(16))) double Ap[2][kRowSlots * kSlot], Rp[2][kRowSlots * kSlot];
     __shared__ __attribute__((aligned(16))) double Mp[2][kBaSolveRowsMaxPoses * kSlot];
-    __shared__ __attribute__((aligned(16))) double Dg[2][36];
     __shared__ double bs[6 * kBaSolveRowsMaxPoses];
     __shared__ int fail;
     const int N = 6 * np;
@@ -1187,17 +1193,14 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
     // pivot row k: the diagonal tile's owners publish it, every lane of the wave factors it, then
     // tiles (k, j > k) and the right-hand side publish A_kj and R_kj into buffer k & 1
     auto pivot_row = [&](int k) {
-        double* __restrict__ D = Dg[k & 1];
-        if (dg && bi == k) {
-#pragma unroll
-            for (int q = 0; q < 6 * CPT; q++) D[(q / CPT) * 6 + c0 + q % CPT] = A[q];
-        }
-        wave_sync_lds();
+        // the diagonal tile from its three owner lanes (lane base + h holds columns 2h, 2h + 1)
+        // by readlane: no LDS round trip on the elimination's critical path
+        const int base = __builtin_amdgcn_readfirstlane(k == ra ? 0 : na);
         double F[36], inv6[6];
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = r; c < 6; c++) F[r * 6 + c] = D[r * 6 + c];
+            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_f64(A[r * CPT + c % 2], base + c / 2);
         const bool ok = ldl6(F, inv6);
         if (dg && bi == k && h == 0 && !ok) fail = 1;
         if (!(own && bi == k && bj > k)) return;
@@ -1226,8 +1229,9 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
     if (wv == 0) pivot_row(0);  // prologue: pivot row 0
     __syncthreads();
     SOLVE_STAMP(tid == 0, 251);
+    // a failed pivot (fail) is acted on after the loop: the remaining steps then only carry
+    // non-finite values, and no step waits on an LDS read of the flag
     for (int k = 0; k < np; k++) {
-        if (fail) break;
         const bool crit = k + 1 < np && wv == solve_rows_wave(k + 1, np);  // wave-uniform
         if (crit) __builtin_amdgcn_s_setprio(3);
         // ---- A(k): eliminate column k from every other row
@@ -1238,6 +1242,7 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
             for (int q = 0; q < 6 * CPT; q++) u[q] = Rp[k & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
 #pragma unroll
             for (int q = 0; q < 36; q++) w[q] = Lp[bi * kSlot + q];  // w[t * 6 + r] = L(t, r)
+            __builtin_amdgcn_sched_barrier(0);  // all 24 LDS reads in flight before the first FMA
 #pragma unroll
             for (int t = 0; t < 6; t++)
 #pragma unroll
@@ -1291,6 +1296,225 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
         }
     }
     double sc = 0;  // lane partials in index order, then a fixed-order wave sum
+    for (int q = lane; q < N; q += 64) sc += bs[q] * (lam * bs[q] + a.bp[q]);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+        a.scal[1] = sc;
+        a.scal[2] = 1;
+        a.istat[3] = 1;
+    }
+    SOLVE_STAMP(lane == 0, 253);
+    SOLVE_STAMP_FLUSH();
+}
+
+// k_ba_solve_rows' elimination with the pivot rows formed by a dedicated wave P (the last one),
+// so that the chain from pivot row k to pivot row k + 1 holds no LDS round trip of the update and
+// no wave switch.  P's lanes are column slices (lane 3 j + h: tile column j, columns 2h, 2h + 1;
+// lane 3 np: the right-hand side) and hold, during step k, row k + 1:
+//   step k, P:    A_{k+1,j} -= A_{k,k+1}^T R_{k,j} with R_k kept in P's registers from step k - 1
+//                 and A_{k,k+1} read back from the pivot-row buffer P wrote; then the LDL^T of the
+//                 updated diagonal tile (readlane) and pivot row k + 1 (A and R) into buffer
+//                 (k + 1) & 1; row k + 2 arrives from its owner through LDS at the start of step
+//                 k + 1 (its owner writes it during step k, after applying pivot k).
+//   step k, bulk: the owners of row k load R_k (the pivot row, now normalised) into their
+//                 registers; every other row except k + 1 (P's) applies pivot k as before.
+// One barrier per step.  np <= kBaSolveRowsMaxPoses.
+constexpr int kBaSolvePipeThreads = kBaSolveRowsThreads + 64;
+__global__ __launch_bounds__(kBaSolvePipeThreads) void k_ba_solve_pipe(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done || ctl.gen != a.run_gen) return;
+    const int np = ctl.np;
+    double lam = a.scal[3];
+    const double* __restrict__ T = a.Tb[ctl.cur];
+    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    constexpr int CPT = 2;
+    constexpr int kSlot = 38;
+    constexpr int kRowSlots = kBaSolveRowsMaxPoses + 1;
+    constexpr int kPivotWave = kBaSolveRowsThreads / 64;
+    SOLVE_STAMP_DECL;
+    SOLVE_STAMP(threadIdx.x == 0, 250);
+    __shared__ __attribute__((aligned(16))) double Ap[2][kRowSlots * kSlot], Rp[2][kRowSlots * kSlot];
+    __shared__ __attribute__((aligned(16))) double Nx[2][kRowSlots * kSlot];  // row k + 2 for P
+    __shared__ __attribute__((aligned(16))) double Mp[2][kBaSolveRowsMaxPoses * kSlot];
+    __shared__ double bs[6 * kBaSolveRowsMaxPoses];
+    __shared__ int fail;
+    const int N = 6 * np;
+    const int tid = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const bool P = wv == kPivotWave;
+    // bulk lanes: the row-pair layout of k_ba_solve_rows; P lanes: column slices
+    int bi = -1, bj = 0, h = 0;
+    const int ra = wv, rb = np - wv, na = 3 * (np - ra) + 1;
+    if (P) {
+        if (lane <= 3 * np) {
+            bj = lane < 3 * np ? lane / 3 : np;
+            h = lane < 3 * np ? lane % 3 : 0;
+        }
+    } else if (ra < np && (wv == 0 || ra <= rb)) {
+        int l = lane, r = ra;
+        if (l >= na && wv > 0 && rb > ra) { l -= na; r = rb; }
+        if (l < 3 * (np - r) + 1) {
+            bi = r;
+            bj = l < 3 * (np - r) ? r + l / 3 : np;
+            h = l < 3 * (np - r) ? l % 3 : 0;
+        }
+    }
+    const int c0 = CPT * h;
+    const bool own = bi >= 0;
+    const bool rhs = bj == np;
+    const bool plane = P && lane <= 3 * np;  // a P lane with a column slice
+    // element (r, c0 + cc) of tile (row, bj) from the packed system (upper part of a diagonal tile)
+    auto load_tile = [&](int row, double* A) {
+        const bool dg = !rhs && row == bj;
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) {
+            const int r = q / CPT, c = c0 + q % CPT;
+            const bool mat = !rhs && bj >= row && (!dg || c >= r), vec = rhs && c == 0;
+            const double* src = vec ? a.bs + 6 * row + r : a.S + (mat ? packed(6 * row + r, 6 * bj + c, N) : 0);
+            const double v = *src;
+            A[q] = (mat || vec) ? v : 0.0;
+        }
+    };
+    double A[6 * CPT];   // bulk: its tile slice; P: row k + 1's slice
+    double Rk[6 * CPT];  // P: R_{k,bj} slice (pivot row k, normalised)
+#pragma unroll
+    for (int q = 0; q < 6 * CPT; q++) { A[q] = 0.0; Rk[q] = 0.0; }
+    if (own) load_tile(bi, A);
+    if (tid == 0) fail = 0;
+    // P: factor the diagonal tile of the row it holds (row k), publish A_k and R_k into buffer
+    // k & 1, keep R_k in Rk
+    auto pivot = [&](int k) {
+        const int base = 3 * k;
+        double F[36], inv6[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_f64(A[r * CPT + c % 2], base + c / 2);
+        const bool ok = ldl6(F, inv6);
+        if (lane == 0 && !ok) fail = 1;
+        double R[6 * CPT];
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) R[q] = A[q];
+#pragma unroll
+        for (int cc = 0; cc < CPT; cc++)
+#pragma unroll
+            for (int t = 1; t < 6; t++)
+#pragma unroll
+                for (int s2 = 0; s2 < t; s2++) R[t * CPT + cc] -= F[s2 * 6 + t] * R[s2 * CPT + cc];
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) R[q] *= inv6[q / CPT];
+#pragma unroll
+        for (int cc = 0; cc < CPT; cc++)
+#pragma unroll
+            for (int t = 4; t >= 0; t--)
+#pragma unroll
+                for (int s2 = t + 1; s2 < 6; s2++) R[t * CPT + cc] -= F[t * 6 + s2] * R[s2 * CPT + cc];
+        if (plane && bj > k) {
+            double* __restrict__ Ao = Ap[k & 1];
+            double* __restrict__ Ro = Rp[k & 1];
+#pragma unroll
+            for (int q = 0; q < 6 * CPT; q++) {
+                Ao[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = A[q];
+                Ro[bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = R[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 6 * CPT; q++) Rk[q] = R[q];
+    };
+    __syncthreads();
+    if (P && np > 0) {  // prologue: row 0 -> pivot row 0; row 1 stays in A for step 0
+        __builtin_amdgcn_s_setprio(3);
+        if (plane) load_tile(0, A);
+        pivot(0);
+        if (np > 1 && plane) load_tile(1, A);
+    }
+    __syncthreads();
+    SOLVE_STAMP(tid == 0, 251);
+    for (int k = 0; k < np; k++) {
+        if (P) {
+            if (k + 1 < np) {
+                if (k >= 1 && plane) {  // row k + 1 with pivots < k applied, from its owner
+#pragma unroll
+                    for (int q = 0; q < 6 * CPT; q++) A[q] = Nx[(k - 1) & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
+                }
+                double w[36];  // L = A_{k,k+1} (w[t * 6 + r] = L(t, r)), as P published it
+#pragma unroll
+                for (int q = 0; q < 36; q++) w[q] = Ap[k & 1][(k + 1) * kSlot + q];
+                __builtin_amdgcn_sched_barrier(0);
+                if (plane && bj > k) {
+#pragma unroll
+                    for (int t = 0; t < 6; t++)
+#pragma unroll
+                        for (int r = 0; r < 6; r++)
+#pragma unroll
+                            for (int cc = 0; cc < CPT; cc++) A[r * CPT + cc] -= w[t * 6 + r] * Rk[t * CPT + cc];
+                }
+                SOLVE_STAMP(lane == 0, 4 * k);
+                pivot(k + 1);
+                SOLVE_STAMP(lane == 0, 4 * k + 2);
+            }
+        } else if (own) {
+            if (bi == k) {  // pivot row k: its normalised tiles
+                if (bj > k) {
+#pragma unroll
+                    for (int q = 0; q < 6 * CPT; q++) A[q] = Rp[k & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
+                }
+            } else if (bj > k && bi != k + 1) {
+                const double* Lp = bi > k ? Ap[k & 1] : Mp[k & 1];
+                double u[6 * CPT], w[36];
+#pragma unroll
+                for (int q = 0; q < 6 * CPT; q++) u[q] = Rp[k & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT];
+#pragma unroll
+                for (int q = 0; q < 36; q++) w[q] = Lp[bi * kSlot + q];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < 6; t++)
+#pragma unroll
+                    for (int r = 0; r < 6; r++)
+#pragma unroll
+                        for (int cc = 0; cc < CPT; cc++) A[r * CPT + cc] -= w[t * 6 + r] * u[t * CPT + cc];
+                if (bi == k + 2) {  // P's row at step k + 1
+#pragma unroll
+                    for (int q = 0; q < 6 * CPT; q++) Nx[k & 1][bj * kSlot + (q / CPT) * 6 + c0 + q % CPT] = A[q];
+                }
+            }
+            if (k + 1 < np && !rhs && bj == k + 1 && bi <= k) {  // M_{i,k+1}, stored transposed
+#pragma unroll
+                for (int q = 0; q < 6 * CPT; q++) Mp[(k + 1) & 1][bi * kSlot + (c0 + q % CPT) * 6 + q / CPT] = A[q];
+            }
+        }
+        __syncthreads();
+        SOLVE_STAMP(tid == 0, 4 * k + 3);
+    }
+    if (P) __builtin_amdgcn_s_setprio(0);
+    if (fail) {  // pop: trial poses = current ones, computeScale = 0
+        for (int k = tid; k < a.nkf; k += blockDim.x)
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
+        return;
+    }
+    if (own && rhs) {  // x = the right-hand side column
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            bs[6 * bi + r] = A[r * CPT];
+            a.xp[6 * bi + r] = A[r * CPT];
+        }
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    SOLVE_STAMP(lane == 0, 252);
+    for (int k = lane; k < a.nkf; k += 64) {
+        const int pi = a.pose_idx[k];
+        if (pi >= 0) {
+            double u[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) u[q] = bs[6 * pi + q];
+            se3_oplus(u, T + 8 * k, Tt + 8 * k);
+        } else {
+            for (int q = 0; q < 8; q++) Tt[8 * k + q] = T[8 * k + q];
+        }
+    }
+    double sc = 0;
     for (int q = lane; q < N; q += 64) sc += bs[q] * (lam * bs[q] + a.bp[q]);
     sc = wave_sum(sc);
     if (lane == 0) {
@@ -1585,6 +1809,8 @@ struct Runner {
     BaDev a;
     const volatile int* stop;
     bool solve_rows;  // nf <= kBaSolveRowsMaxPoses: k_ba_solve_rows, else k_ba_solve<1>
+    bool solve_pipe;  // k_ba_solve_pipe (a dedicated pivot wave) in place of k_ba_solve_rows
+                      // (ORBMI_BA_SOLVE=rows selects the latter, for A/B runs)
 
     bool stopped() const { return stop && *stop; }
 
@@ -1614,7 +1840,9 @@ struct Runner {
     void step(int gen) {
         a.run_gen = gen;
         if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
-        if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
+        if (solve_rows && solve_pipe)
+            hipLaunchKernelGGL(k_ba_solve_pipe, dim3(1), dim3(kBaSolvePipeThreads), 0, h.stream, a);
+        else if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_update_errors, dim3(a.nb_q), dim3(kBaUpdThreads), 0, h.stream, a);
     }
@@ -1851,7 +2079,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.Hpp = (double*)(B + o_Hpp); a.bp = (double*)(B + o_bp);
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
     a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
-    Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses};
+    const char* sv = getenv("ORBMI_BA_SOLVE");
+    Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses, !(sv && !strcmp(sv, "rows"))};
     unsigned char* out_erase = B + o_oerase;
     const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
     hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);

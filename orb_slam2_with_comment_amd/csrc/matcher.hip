@@ -601,9 +601,12 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                     auto occ = [&](int idx) { return claim[idx] < q; };
                     int r;
                     if (nc[k] <= a.cap) {
-                        // the whole list, 16 loads in flight; octaves from LDS
+                        // the whole list, 16 loads in flight; octaves from LDS.  k_candidates
+                        // writes the list only past kTopK entries: below that the sorted prefix
+                        // holds all of them
                         unsigned long long b1 = ~0ull, b2 = ~0ull;
-                        const unsigned long long* c = a.cand + (long long)q * a.cap;
+                        const unsigned long long* c =
+                            nc[k] <= kTopK ? a.top + (long long)q * kTopK : a.cand + (long long)q * a.cap;
                         for (int k0 = 0; k0 < nc[k]; k0 += 16) {
                             unsigned long long e[16];
 #pragma unroll

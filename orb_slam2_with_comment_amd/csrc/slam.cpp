@@ -253,6 +253,7 @@ struct orbmi_slam {
     std::vector<uint8_t> lost;
     std::vector<orbmi_slam_frame_stats> stats;
     int ba_calls = 0;
+    int resets = 0;  // Tracking::Reset calls (lost with <= 5 keyframes in the map)
     std::vector<float> level_sigma2;  // mvLevelSigma2
     std::vector<int> recent_mps;      // mlpRecentAddedMapPoints
     // extraction scratch
@@ -1803,6 +1804,18 @@ struct orbmi_slam {
                 for (int i = 0; i < cf.n(); i++)  // (:535-539)
                     if (cf.mps[i] >= 0 && cf.outlier[i]) cf.mps[i] = -1;
             }
+            // Reset if the camera gets lost soon after initialisation (src/Tracking.cc:540-551):
+            // the map is cleared and the next frame initialises again; this frame is not recorded
+            if (state == LOST && keyframes_in_map() <= 5) {
+                SLAM_CHECK(reset());
+                resets++;
+                st.reset = 1;
+                st.state = state;
+                st.keyframes = 0;
+                st.mappoints = 0;
+                stats.push_back(st);
+                return ORBMI_OK;
+            }
             if (cf.ref_kf < 0) cf.ref_kf = ref_kf;
         }
         last_frame = cf;
@@ -1822,6 +1835,46 @@ struct orbmi_slam {
         st.keyframes = (int)kfs.size();
         st.mappoints = count_mappoints();
         stats.push_back(st);
+        return ORBMI_OK;
+    }
+
+    // Tracking::Reset (src/Tracking.cc:1780-1826): LocalMapping drops its queue and finishes the
+    // keyframe in hand (RequestReset; the tracking thread lets go of the map lock meanwhile), then
+    // the map, the tracking state, the frame / keyframe ids and the trajectory lists start over
+    int reset() {
+        if (async_lm()) {
+            {
+                std::lock_guard<std::mutex> g(q_mtx);
+                lm_queue.clear();
+            }
+            if (held_lock) held_lock->unlock();
+            {
+                std::unique_lock<std::mutex> g(q_mtx);
+                idle_cv.wait(g, [&] { return lm_queue.empty() && !lm_busy; });
+            }
+            if (held_lock) held_lock->lock();
+        }
+        for (auto& kf : kfs)
+            if (kf.d_block) (void)hipFree(kf.d_block);
+        kfs.clear();
+        mps.clear();
+        recent_mps.clear();
+        local_kfs.clear();
+        local_mps.clear();
+        kf_counter.assign(kf_counter.size(), 0);
+        last_frame = TrackedFrame();
+        have_last = false;
+        has_velocity = false;
+        ref_kf = -1;
+        last_kf_frame_id = 0;
+        last_reloc_frame_id = 0;
+        matches_inliers = 0;
+        frame_count = 0;  // Frame::nNextId = 0 (KeyFrame ids restart with the emptied map)
+        state = NO_IMAGES_YET;
+        rel_poses.clear();
+        references.clear();
+        frame_times.clear();
+        lost.clear();
         return ORBMI_OK;
     }
 

@@ -25,7 +25,7 @@ class SlamSettings(C.Structure):
 class FrameStats(C.Structure):
     _fields_ = [(k, C.c_int) for k in ("frame", "n", "state", "init", "track", "lf_matches", "bow_matches",
                                        "nmatches_map", "local_map_points", "local_matches", "inliers", "need_kf",
-                                       "keyframes", "mappoints")]
+                                       "keyframes", "mappoints", "reset")]
 
 
 _TRACK = {1: "motion_model", 2: "reference_kf"}
@@ -76,9 +76,12 @@ class NativeStereoSLAM:
     @property
     def stats(self) -> list:
         out = []
-        for f in range(self.counts()["frames"]):
+        f = 0
+        while True:  # one record per TrackStereo call (frame ids restart after a reset)
             st = FrameStats()
-            check("orbmi_slam_get_stats", lib().orbmi_slam_get_stats(self._h, f, C.byref(st)))
+            if lib().orbmi_slam_get_stats(self._h, f, C.byref(st)) != 0:
+                break
+            f += 1
             d = {k: getattr(st, k) for k, _ in FrameStats._fields_}
             d = {k: v for k, v in d.items() if v != -1}
             if "track" in d:

@@ -488,10 +488,7 @@ class LocalMapper:
                 m, C.addressof(kf.view), C.addressof(kf.tri_dev), _vp(kf.d_cos.data_ptr()), _vp(kf.d_has_mp),
                 C.addressof(fv1), nnb, kf2, job.c_tri2, job.c_cos2, job.c_mp2, job.c_fv2, job.c_F12.ctypes.data,
                 _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
-        self._ms.synchronize()
         nt = nnb * kf.n
-        counts = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64)]).cpu().numpy()
-        out["triangulation_pairs"], out["new_points"] = int(counts[0]), int(counts[1])
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
         d_kp, n_kp = job.kf_points
         d_tp, n_tp = job.target_points
@@ -507,11 +504,15 @@ class LocalMapper:
         # ComputeDistinctiveDescriptors + UpdateNormalAndDepth of the keyframe's points after fusion
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
-        self._ms.synchronize()
-        out["fuse_candidates"] = int((bi[:o + n_tp] >= 0).sum())
-        # ---- LocalBundleAdjustment
+        # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
         out["local_ba_iterations"] = list(self.last["iterations"])
+        # counts of what the searches found: read after the chain (the BA call has synchronised
+        # the stream; no round trip between the stages for statistics only)
+        self._ms.synchronize()
+        counts = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64),
+                              (bi[:o + n_tp] >= 0).sum()]).cpu().numpy()
+        out["triangulation_pairs"], out["new_points"], out["fuse_candidates"] = (int(c) for c in counts)
         self._out = dict(tri=lambda: tri[:nt].cpu().numpy().reshape(nnb, kf.n),
                          tri_ok=lambda: tri_ok[:nt].cpu().numpy().reshape(nnb, kf.n),
                          x3d=lambda: x3d[:3 * nt].cpu().numpy().reshape(nnb, kf.n, 3),

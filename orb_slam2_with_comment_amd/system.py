@@ -576,6 +576,15 @@ class StereoSLAM:
                 for i, mp in enumerate(cf.map_points):   # (:535-539)
                     if mp is not None and cf.outlier[i]:
                         cf.map_points[i] = None
+            # Reset if the camera gets lost soon after initialisation (src/Tracking.cc:540-551)
+            if self.state == LOST and sum(1 for k in self.keyframes if not k.bad) <= 5:
+                self._reset()
+                st["reset"] = 1
+                st["state"] = self.state
+                st["keyframes"] = 0
+                st["mappoints"] = 0
+                self.stats.append(st)
+                return
             if cf.ref_kf is None:
                 cf.ref_kf = self.ref_kf
         self.last_frame = cf
@@ -593,6 +602,21 @@ class StereoSLAM:
         st["keyframes"] = len(self.keyframes)
         st["mappoints"] = sum(1 for m in self.mappoints if not m.bad)
         self.stats.append(st)
+
+    def _reset(self):
+        """Tracking::Reset (src/Tracking.cc:1780-1826): map, tracking state, frame / keyframe ids
+        and the trajectory lists start over; the next frame initialises again."""
+        self.state = NO_IMAGES_YET
+        self.keyframes, self.mappoints, self.recent_mps = [], [], []
+        self.frame_count = 0
+        self.last_frame = None
+        self.velocity = None
+        self.ref_kf = None
+        self.last_kf_frame_id = 0
+        self.last_reloc_frame_id = 0
+        self.local_kfs, self.local_mps = [], []
+        self.matches_inliers = 0
+        self.rel_poses, self.references, self.frame_times, self.lost = [], [], [], []
 
     # ---- initialisation and keyframes ---------------------------------------------------------
     def _new_keyframe(self, cf: TrackedFrame) -> KeyFrame:

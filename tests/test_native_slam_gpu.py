@@ -110,3 +110,28 @@ def test_native_concurrent_local_mapping(tmp_path):
     print(f"concurrent LocalMapping: ATE {ate:.4f} m (synchronous {ate_sync:.4f} m), {c}")
     assert ate < max(2.0 * ate_sync, 0.6), (ate, ate_sync)
     slam.Shutdown()
+
+
+def test_native_reset_after_loss_matches_oracle(tmp_path):
+    """A frame lost with <= 5 keyframes resets the system (src/Tracking.cc:540-551) in the native
+    loop exactly as in the oracle-driven loop; the flat frame (no keypoints) goes through every
+    stage with empty inputs."""
+    from test_system_oracle import _loss_sequence
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    seq = _loss_sequence()
+    gpu = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    ref = StereoSLAM(s, backend=OracleBackend(s, voc))
+    for i, (L, R) in enumerate(seq):
+        gpu.TrackStereo(L, R, 0.1 * i)
+        ref.TrackStereo(L, R, 0.1 * i)
+    a_all, b_all = gpu.stats, ref.stats
+    assert len(a_all) == len(b_all) == len(seq)
+    for a, b in zip(a_all, b_all):
+        assert {k: a.get(k) for k in _DECISIONS + ("reset", "frame")} == \
+            {k: b.get(k) for k in _DECISIONS + ("reset", "frame")}, (a, b)
+    assert a_all[1]["reset"] == 1 and a_all[2]["init"]
+    assert gpu.counts()["frames"] == 2 and gpu.counts()["keyframes"] == 1
+    T, _, lost = gpu.frame_poses()
+    assert len(T) == 2 and not lost.any()
+    gpu.Shutdown()

@@ -123,23 +123,27 @@ def test_lost_frames(tmp_path):
     """A textureless frame loses tracking: it keeps the motion-model pose and is recorded with
     mlbLost = true (src/Tracking.cc:557-565).  The next frame arrives in LOST state; relocalisation
     is out of scope, so it has no pose and the trajectory repeats the last relative pose
-    (:566-580).  TUM output skips lost frames.  Runs without LocalBA."""
+    (:566-580).  TUM output skips lost frames.  Ten frames first, so that the map holds more than
+    5 keyframes and the loss does not reset the system (:540-551).  Runs without LocalBA."""
     from orb_slam2_with_comment_amd.system import LOST
     s = sequence_settings(tmp_path)
     slam = StereoSLAM(s, backend=OracleBackend(s, small_vocabulary()), local_ba=False)
-    for f in range(3):
+    n = 10
+    for f in range(n):
         L, R, _ = synth.stereo_pair(synth.KITTI, f)
         slam.TrackStereo(L, R, 0.1 * f)
+    assert sum(1 for k in slam.keyframes if not k.bad) > 5
     flat = np.full((synth.KITTI.height, synth.KITTI.width), 128, np.uint8)
-    Tpred = slam.TrackStereo(flat, flat, 0.3)
-    assert slam.state == LOST and slam.lost == [False, False, False, True]
+    Tpred = slam.TrackStereo(flat, flat, 0.1 * n)
+    assert slam.state == LOST and slam.lost == [False] * n + [True]
     assert Tpred is not None and slam.stats[-1]["track"] == "reference_kf"
-    assert slam.TrackStereo(flat, flat, 0.4) is None
-    assert slam.lost[-1] and len(slam.rel_poses) == 5
+    assert "reset" not in slam.stats[-1]
+    assert slam.TrackStereo(flat, flat, 0.1 * n + 0.1) is None
+    assert slam.lost[-1] and len(slam.rel_poses) == n + 2
     np.testing.assert_array_equal(slam.rel_poses[-1], slam.rel_poses[-2])
     p = tmp_path / "tum.txt"
     slam.SaveTrajectoryTUM(str(p))
-    assert len(p.read_text().splitlines()) == 3
+    assert len(p.read_text().splitlines()) == n
     assert not slam.ba_log
 
 
@@ -151,3 +155,27 @@ def test_not_initialised_until_enough_keypoints(tmp_path):
     flat = np.full((synth.KITTI.height, synth.KITTI.width), 90, np.uint8)
     assert slam.TrackStereo(flat, flat, 0.0) is None
     assert slam.state == NOT_INITIALIZED and not slam.keyframes and not slam.rel_poses
+
+
+def _loss_sequence():
+    """Frame 0 initialises, frame 1 is a flat image (no keypoints: TrackReferenceKeyFrame finds
+    nothing, the frame is LOST with one keyframe in the map), frames 2-3 are the sequence's."""
+    fr = [synth.stereo_pair(synth.KITTI, f) for f in (0, 2, 3)]
+    flat = np.full_like(fr[0][0], 128)
+    return [fr[0][:2], (flat, flat), fr[1][:2], fr[2][:2]]
+
+
+def test_tracking_loss_resets(tmp_path):
+    """Tracking::Track's reset when tracking is lost with <= 5 keyframes in the map
+    (src/Tracking.cc:540-551, Tracking::Reset :1780-1826): the map and the trajectory start over
+    and the next frame initialises again with frame id 0."""
+    s = sequence_settings(tmp_path)
+    slam = StereoSLAM(s, backend=OracleBackend(s, small_vocabulary()))
+    for i, (L, R) in enumerate(_loss_sequence()):
+        slam.TrackStereo(L, R, 0.1 * i)
+    st = slam.stats
+    assert st[0]["init"] and st[0]["state"] == OK
+    assert st[1]["reset"] == 1 and st[1]["state"] == 0 and st[1]["n"] == 0
+    assert st[2]["init"] and st[2]["frame"] == 0 and st[2]["keyframes"] == 1
+    assert st[3]["state"] == OK and st[3]["track"] == "reference_kf"
+    assert len(slam.rel_poses) == 2 and all(k.id < 2 for k in slam.keyframes)

@@ -15,11 +15,13 @@
 #   gloo2            bench.py --gpus 2 --dist-backend gloo (config 4 rehearsal on one device)
 #   prof             rocprofv3 --kernel-trace --stats of the default bench
 #   prof_MODE        the same for --mode MODE
+#   ktrace[_MODE]    rocprofv3 --kernel-trace of a short bench run + tools/trace_gaps.py
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the default bench -> traffic.json
 #   pmc_MODE         the same for --mode MODE
 #   native[_async]   tools/native_probe.py (sync / concurrent LocalMapping)
 #   nativeprof[_async] its rocprofv3 kernel stats
 #   lmprobe          tools/lm_chain_probe.py (per-call split of the LocalMapping chain)
+#   solvetrace[=VAR=1]  per-step split of the reduced-system solve (tools/ubench/solve_trace)
 #   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 TAG=${1:-run}
@@ -72,6 +74,12 @@ for step in "$@"; do
             find $OUT/prof_$m -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats_$m.csv \;
             cp $OUT/prof_$m.log $P/prof_stats_$m.log
             cut -d, -f1-5 $P/kernel_stats_$m.csv | head -25;;
+        ktrace|ktrace_*)
+            # kernel trace (start / end per dispatch) and the idle gaps between dependent launches
+            m=${step#ktrace}; m=${m#_}; m=${m:-track}
+            run ktrace_$m 500 rocprofv3 --kernel-trace -f csv -d $OUT/ktrace_$m -o kt -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
+            f=$(find $OUT/ktrace_$m -name "*kernel_trace.csv" | head -1)
+            python tools/trace_gaps.py $f > $P/trace_gaps_$m.txt; cp $f $P/kernel_trace_$m.csv; cat $P/trace_gaps_$m.txt;;
         pmc|pmc_*)
             m=${step#pmc}; m=${m#_}; m=${m:-track}
             run pmc_fetch_$m 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch_$m -o fetch -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
@@ -87,6 +95,20 @@ for step in "$@"; do
             cut -d, -f1-5 $P/native${a}_kernel_stats.csv | head -30;;
         lmprobe)
             run lmprobe 300 python tools/lm_chain_probe.py 20; tail -14 $OUT/lmprobe.log;;
+        solvetrace|solvetrace=*)
+            # per-step cycle split of the reduced-system solve (tools/ubench/solve_trace, built beforehand)
+            v=${step#solvetrace}; v=${v#=}
+            run solvetrace$v 60 env $v ./tools/ubench/solve_trace 20; cat $OUT/solvetrace$v.log;;
+        solvebin=*)
+            # a solve_trace build variant: solvebin=NAME runs tools/ubench/solve_trace_NAME
+            b=${step#solvebin=}
+            run solvebin_$b 60 ./tools/ubench/solve_trace_$b 20; cat $OUT/solvebin_$b.log;;
+        solvepmc|solvepmc=*)
+            # SQ counters of the reduced-system solve (tools/ubench/solve_trace), one pass
+            v=${step#solvepmc}; v=${v#=}
+            run solvepmc$v 90 env $v timeout -s KILL 60 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace -f csv -d $OUT/solvepmc$v -o sp -- ./tools/ubench/solve_trace 20
+            f=$(find $OUT/solvepmc$v -name "*counter_collection.csv" | head -1); cp $f $P/solve_pmc$v.csv
+            python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[(r['Kernel_Name'][:40],r['Counter_Name'])].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1]))]; [print(k, sum(v)/len(v)) for k,v in sorted(d.items())]" $f;;
         mfma_pmc)
             # MFMA A/B of the Schur products: MFMA issue / busy counters of each variant's kernel
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur

@@ -44,7 +44,9 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     auto launch = [&] {
-        if (np <= kBaSolveRowsMaxPoses && !getenv("TPT1") && !getenv("OLD"))
+        if (np <= kBaSolveRowsMaxPoses && getenv("PIPE"))
+            hipLaunchKernelGGL(k_ba_solve_pipe, dim3(1), dim3(kBaSolvePipeThreads), 0, 0, a);
+        else if (np <= kBaSolveRowsMaxPoses && !getenv("TPT1") && !getenv("OLD"))
             hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, 0, a);
         else if (np <= 21 && !getenv("TPT1"))  // the previous tile layout, TPT 2
             hipLaunchKernelGGL(k_ba_solve<2>, dim3(1), dim3(kBaSolveThreads), 0, 0, a);
