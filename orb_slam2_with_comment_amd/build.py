@@ -16,7 +16,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 # ORBMI_LIB / ORBMI_CFLAGS: an alternative library path and extra -D flags, for A/B builds of a
-# kernel variant (tools/gpu_iter.sh); the product build uses neither
+# kernel variant (tools/gpu.sh ab=A,B); the product build uses neither
 LIB = os.environ.get("ORBMI_LIB") or os.path.join(PKG, "liborbmi.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ORBMI_ARCH", "gfx950")

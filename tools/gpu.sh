@@ -15,6 +15,8 @@
 #   gloo2            bench.py --gpus 2 --dist-backend gloo (config 4 rehearsal on one device)
 #   prof             rocprofv3 --kernel-trace --stats of the default bench
 #   prof_MODE        the same for --mode MODE
+#   sqpmc[_MODE]     two SQ counter passes (waves, issue, LDS, VMEM) -> per-kernel means
+#   poselat[=LIB]    tools/pose_latency.py (PoseOptimization latency), optionally on another build
 #   ktrace[_MODE]    rocprofv3 --kernel-trace of a short bench run + tools/trace_gaps.py
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the default bench -> traffic.json
 #   pmc_MODE         the same for --mode MODE
@@ -44,6 +46,7 @@ modeargs() {  # MODE -> bench args
         lba) echo "--mode lba --steps 50 --warmup 10";;
         batch) echo "--mode batch --steps 50 --warmup 4";;
         extract) echo "--mode extract";;
+        extractq) echo "--mode extract --steps 20 --warmup 4";;
         system) echo "--mode system";;
     esac
 }
@@ -109,6 +112,19 @@ for step in "$@"; do
             run solvepmc$v 90 env $v timeout -s KILL 60 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace -f csv -d $OUT/solvepmc$v -o sp -- ./tools/ubench/solve_trace 20
             f=$(find $OUT/solvepmc$v -name "*counter_collection.csv" | head -1); cp $f $P/solve_pmc$v.csv
             python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[(r['Kernel_Name'][:40],r['Counter_Name'])].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1]))]; [print(k, sum(v)/len(v)) for k,v in sorted(d.items())]" $f;;
+        sqpmc|sqpmc_*)
+            # two passes of 8 SQ counters over a short bench run -> per-kernel means (tools/pmc_sq.py)
+            m=${step#sqpmc}; m=${m#_}; m=${m:-track}
+            P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
+            P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_LDS_IDX_ACTIVE"
+            run sqpmc1_$m 150 timeout -s KILL 120 rocprofv3 --pmc $P1 --kernel-trace -f csv -d $OUT/sqpmc_$m/p1 -o p1 -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
+            run sqpmc2_$m 150 timeout -s KILL 120 rocprofv3 --pmc $P2 --kernel-trace -f csv -d $OUT/sqpmc_$m/p2 -o p2 -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
+            python tools/pmc_sq.py $OUT/sqpmc_$m > $P/sq_counters_$m.txt; head -60 $P/sq_counters_$m.txt;;
+        poselat|poselat=*)
+            # PoseOptimization latency probe (tools/pose_latency.py); poselat=LIB runs it on another build
+            l=${step#poselat}; l=${l#=}
+            if [ -n "$l" ]; then ORBMI_LIB=$l run poselat_ab 120 python tools/pose_latency.py; cat $OUT/poselat_ab.log
+            else run poselat 120 python tools/pose_latency.py; cat $OUT/poselat.log; fi;;
         mfma_pmc)
             # MFMA A/B of the Schur products: MFMA issue / busy counters of each variant's kernel
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur
