@@ -1427,15 +1427,68 @@ __global__ __launch_bounds__(256) void k_triangulate(tri::Side K1, const tri::Si
     }
 }
 
+// The same outcome with every (keypoint, pair) geometry evaluated at once: G >= npairs lanes per
+// KF1 keypoint (lane j = pair j, G a power of two dividing 64), each running triangulate_one for
+// its match; the first pair (in the reference's order) whose geometry accepts owns the keypoint
+// -- a wave ballot -- and the later pairs' matches of it are dropped, exactly as the sequential
+// loop would (an accepted point makes pKF1's keypoint taken for the searches after it, and the
+// KF1 keypoints of SearchForTriangulation are independent of each other).
+template <int G>
+__global__ __launch_bounds__(256) void k_triangulate_par(tri::Side K1, const tri::Side* __restrict__ K2s, int npairs,
+                                                         int* __restrict__ match, int n1, uint8_t* __restrict__ ok,
+                                                         float* __restrict__ x3d) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / G, j = t % G, lane = threadIdx.x & 63;
+    const bool live = i < n1 && j < npairs;
+    const size_t r = (size_t)j * n1 + i;
+    const int i2 = live ? match[r] : -1;
+    bool acc = false;
+    float x[3];
+    if (i2 >= 0) {
+        const tri::Side& K2 = K2s[j];
+        const float cps1 = K1.ur[i] >= 0 ? K1.cos_stereo[i] : 0.f;
+        const float cps2 = K2.ur[i2] >= 0 ? K2.cos_stereo[i2] : 0.f;
+        acc = tri::triangulate_one(K1, K2, i, i2, cps1, cps2, x);
+    }
+    const unsigned long long bits = __ballot(acc);
+    const unsigned long long mine = G == 64 ? bits : (bits >> (lane & ~(G - 1))) & ((1ull << G) - 1);
+    const int first = mine ? __builtin_ctzll(mine) : G;  // the pair that owns keypoint i
+    if (!live) return;
+    if (i2 >= 0 && j > first) match[r] = -1;
+    ok[r] = j == first ? 1 : 0;
+    if (j == first) {
+        x3d[3 * r] = x[0];
+        x3d[3 * r + 1] = x[1];
+        x3d[3 * r + 2] = x[2];
+    }
+}
+
 int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, const DevFV& fv1, int npairs,
                          TriPair* pairs_host, TriPair* pairs_dev, const tri::Side& S1, const tri::Side* S2_dev,
                          int* match, uint8_t* ok, float* x3d) {
     if (npairs <= 0) return ORBMI_OK;
     int rc;
     if ((rc = launch_tri_search(m, KF1, has1, fv1, npairs, pairs_host, pairs_dev, 0, 0, match))) return rc;
-    if (KF1.n > 0)
+    auto par = [&](auto kern, int G) {
+        const long long nt = (long long)KF1.n * G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
+                           KF1.n, ok, x3d);
+    };
+    if (KF1.n <= 0) {
+    } else if (npairs <= 4) {
+        par(k_triangulate_par<4>, 4);
+    } else if (npairs <= 8) {
+        par(k_triangulate_par<8>, 8);
+    } else if (npairs <= 16) {
+        par(k_triangulate_par<16>, 16);
+    } else if (npairs <= 32) {
+        par(k_triangulate_par<32>, 32);
+    } else if (npairs <= 64) {
+        par(k_triangulate_par<64>, 64);
+    } else {
         hipLaunchKernelGGL(k_triangulate, dim3((KF1.n + 255) / 256), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
                            KF1.n, ok, x3d);
+    }
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 
