@@ -1768,6 +1768,9 @@ struct orbmi_ba {
     size_t cap = 0;
     uint8_t* h_stage = nullptr;  // pinned staging of the uploaded graph (one H2D copy)
     size_t cap_stage = 0;
+    hipEvent_t up_done = nullptr;  // the last upload from h_stage has been read
+    uint8_t* h_out = nullptr;      // pinned staging of the results (poses, positions, erase flags)
+    size_t cap_out = 0;
     orbmi::BaCtl* h_ctl = nullptr;  // pinned readback of the LM control block
     int* h_stop = nullptr;          // host-mapped mirror of the caller's stop flag
     int* d_stop = nullptr;          //   (its device address)
@@ -1880,6 +1883,7 @@ int orbmi_ba_create(int device, orbmi_ba** out) {
     b->device = device;
     if (hipSetDevice(device) != hipSuccess || orbmi::stream_create(&b->stream, "BA") != hipSuccess ||
         hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&b->up_done, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&b->h_ctl, sizeof(BaCtl)) != hipSuccess ||
         hipHostMalloc((void**)&b->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&b->d_stop, b->h_stop, 0) != hipSuccess) {
@@ -1900,6 +1904,8 @@ void orbmi_ba_destroy(orbmi_ba* b) {
     if (b->h_ctl) (void)hipHostFree(b->h_ctl);
     if (b->h_stop) (void)hipHostFree(b->h_stop);
     if (b->done) (void)hipEventDestroy(b->done);
+    if (b->up_done) (void)hipEventDestroy(b->up_done);
+    if (b->h_out) (void)hipHostFree(b->h_out);
     if (b->stream && b->own_stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
@@ -1969,8 +1975,10 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk);
     const size_t up_bytes = off;
     hipStream_t s = h.stream;
-    // the previous call's upload may still be reading the staging buffer
-    ORBMI_HIP(hipStreamSynchronize(s));
+    // the previous call's upload may still be reading the staging buffer (only that copy is
+    // waited for: the stream's other work, e.g. the searches enqueued before this call on a
+    // shared stream, keeps running while the graph is indexed)
+    ORBMI_HIP(hipEventSynchronize(h.up_done));
     if (up_bytes > h.cap_stage) {
         if (h.h_stage) (void)hipHostFree(h.h_stage);
         h.h_stage = nullptr;
@@ -2039,6 +2047,16 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     uint8_t* B = h.d_buf;
     tr.mark("host_index");
     ORBMI_HIP(hipMemcpyAsync(B, S, up_bytes, hipMemcpyHostToDevice, s));
+    ORBMI_HIP(hipEventRecord(h.up_done, s));
+    const size_t out_bytes = o_oerase + (size_t)std::max(ne, 1) - o_otcw;  // tcw, pos, erase (aligned)
+    if (out_bytes > h.cap_out) {
+        if (h.h_out) (void)hipHostFree(h.h_out);
+        h.h_out = nullptr;
+        h.cap_out = 0;
+        ORBMI_HIP(hipHostMalloc((void**)&h.h_out, out_bytes));
+        h.cap_out = out_bytes;
+    }
+    uint8_t* const Ho = h.h_out;
     ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
     ORBMI_HIP(hipMemsetAsync(B + o_ctl, 0, sizeof(BaCtl), s));
     BaDev a;
@@ -2106,9 +2124,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         hipLaunchKernelGGL(k_ba_finish, dim3(nb_all), dim3(kBaBlock), 0, s, a, (float*)(B + o_otcw), (float*)(B + o_opos),
                            out_erase);
         hipError_t e = hipSuccess;
-        if (nkf && e == hipSuccess) e = hipMemcpyAsync(R->tcw, B + o_otcw, 64 * nkf, hipMemcpyDeviceToHost, s);
-        if (npt && e == hipSuccess) e = hipMemcpyAsync(R->pos, B + o_opos, 12 * npt, hipMemcpyDeviceToHost, s);
-        if (ne && e == hipSuccess) e = hipMemcpyAsync(R->erase, out_erase, ne, hipMemcpyDeviceToHost, s);
+        // the outputs are contiguous in the arena (tcw, pos, erase): one copy into pinned memory
+        if (e == hipSuccess) e = hipMemcpyAsync(Ho, B + o_otcw, o_oerase + ne - o_otcw, hipMemcpyDeviceToHost, s);
         return e;
     };
     int rc, from = 0, more = 0;
@@ -2125,6 +2142,9 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         tr.mark(from == 1 ? "resume5" : "resume10");
     }
     tr.mark("optimize+finish");
+    if (nkf) std::memcpy(R->tcw, Ho, 64 * (size_t)nkf);
+    if (npt) std::memcpy(R->pos, Ho + (o_opos - o_otcw), 12 * (size_t)npt);
+    if (ne) std::memcpy(R->erase, Ho + (o_oerase - o_otcw), (size_t)ne);
     const BaCtl& c = *h.h_ctl;
     const bool second = c.do_more != 0;
     R->iterations[0] = c.it_out[0];
