@@ -300,7 +300,7 @@ def run_track(a, rank, world, local, dist):
     mapper.wait()
     lba_ms = (time.perf_counter() - t0) * 1e3
     lba_info = mapper.last
-    chain_info = mapper.last_chain if full_chain else None
+    chain_info = dict(mapper.last_chain.materialize()) if full_chain else None
     t0 = time.perf_counter()
     for _ in range(10):
         b = mapper.bow

@@ -359,6 +359,28 @@ class LocalMappingJob:
         self.c_F12 = np.ascontiguousarray(np.concatenate(self.F12) if nnb else np.zeros(9), np.float32)
 
 
+class ChainStats(dict):
+    """run_job's counts: the cheap ones at once, the search statistics (which need a device
+    reduction and a read-back) on first access or materialize()."""
+
+    _LAZY = ("triangulation_pairs", "new_points", "fuse_candidates")
+
+    def __init__(self, lazy, **kw):
+        super().__init__(**kw)
+        self._lazy = lazy
+
+    def materialize(self):
+        if self._lazy is not None:
+            f, self._lazy = self._lazy, None
+            self.update(f())
+        return self
+
+    def __missing__(self, k):
+        if k in self._LAZY and self._lazy is not None:
+            return self.materialize()[k]
+        raise KeyError(k)
+
+
 class LocalMapper:
     """LocalMapping thread (src/LocalMapping.cc:47-128), concurrent with tracking as in the
     reference.  For every queued keyframe, in the reference's order, on the mapper's own GPU
@@ -396,6 +418,13 @@ class LocalMapper:
                             counts=torch.zeros(2, dtype=torch.int32, device=dev))
         self._dev = dev
         self._bufs = {}
+        # pinned host words for the BowVector / FeatureVector sizes, written by a copy on the
+        # mapper's stream (the HIP runtime directly: a torch pinned tensor would record events on
+        # this external stream when freed, after the stream is gone)
+        self._hip = C.CDLL("libamdhip64.so.7")  # the runtime torch (and liborbmi.so) already use
+        self._counts_h = C.c_void_p()
+        if self._hip.hipHostMalloc(C.byref(self._counts_h), C.c_size_t(8), C.c_uint(0)) != 0:
+            raise RuntimeError("hipHostMalloc failed")
         ms = _vp()
         check("orbmi_matcher_get_stream", lib().orbmi_matcher_get_stream(self.matcher._h, C.byref(ms)))
         self._ms = torch.cuda.ExternalStream(ms.value, device=dev)  # the mapper's search stream
@@ -453,36 +482,45 @@ class LocalMapper:
             bow_done.synchronize()
 
     def run_job(self, job: LocalMappingJob):
-        """One LocalMapping::Run iteration (see the class doc) -> counts of what it found."""
+        """One LocalMapping::Run iteration (see the class doc) -> counts of what it found.  The
+        chain runs in order on the mapper's stream with one host synchronisation before
+        CreateNewMapPoints (the FeatureVector's node count sizes its search) and the one LocalBA
+        ends with; the statistics of the searches are read lazily (ChainStats)."""
         import torch
-        from .types import FeatureVector
+        from .types import FeatureVector, FeatureVectorView
         L = lib()
         m = self.matcher._h
         kf = job.kf
-        out = {}
-        # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors)
+        # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
+        # ComputeDistinctiveDescriptors of the keyframe's map points, enqueued back to back
         b = self.bow
         self.voc.transform_device(job.d_desc, kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
                                   b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
-        self.voc.synchronize()
-        counts = b["counts"].cpu().numpy()  # mBowVec / mFeatVec sizes; the vectors stay in HBM
-        nn = int(counts[1])
-        out["bow_words"] = int(counts[0])
-        # ... and ComputeDistinctiveDescriptors of the keyframe's map points
+        if not self._one_stream:  # the transform ran on the vocabulary's own stream
+            self.voc.synchronize()
+        if self._hip.hipMemcpyAsync(self._counts_h, _vp(b["counts"].data_ptr()), C.c_size_t(8), C.c_int(2),
+                                    _vp(self._ms.cuda_stream)) != 0:  # mBowVec / mFeatVec sizes, in order
+            raise RuntimeError("hipMemcpyAsync failed")
         d_obs, d_off, npts = job.obs
         best = self._buf("best", (max(npts, 1),), torch.int32)
         dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
-        # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
-        # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
-        from .types import FeatureVectorView
+        # the later stages' buffers, prepared while the GPU runs the two above
         nnb = len(job.neighbours)
         tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
         tri_ok = self._buf("tri_ok", (max(nnb, 1) * kf.n,), torch.uint8)
         x3d = self._buf("tri_x3d", (max(nnb, 1) * kf.n * 3,), torch.float32)
-        fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
+        d_kp, n_kp = job.kf_points
+        d_tp, n_tp = job.target_points
+        bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
+        bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
+        self.voc.synchronize()
+        nw, nn = (C.c_int * 2).from_address(self._counts_h.value)
+        # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
+        # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
+        fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
         if nnb:
             check("orbmi_create_new_map_points", L.orbmi_create_new_map_points(
                 m, C.addressof(kf.view), C.addressof(kf.tri_dev), _vp(kf.d_cos.data_ptr()), _vp(kf.d_has_mp),
@@ -490,10 +528,6 @@ class LocalMapper:
                 _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         nt = nnb * kf.n
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
-        d_kp, n_kp = job.kf_points
-        d_tp, n_tp = job.target_points
-        bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
-        bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         if nnb:
             check("orbmi_fuse_search_batch", L.orbmi_fuse_search_batch(
                 m, nnb, kf2, _vp(d_kp), None, int(n_kp), 3.0, _vp(bi.data_ptr()), _vp(bd.data_ptr()), None))
@@ -506,13 +540,14 @@ class LocalMapper:
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
         # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
-        out["local_ba_iterations"] = list(self.last["iterations"])
-        # counts of what the searches found: read after the chain (the BA call has synchronised
-        # the stream; no round trip between the stages for statistics only)
-        self._ms.synchronize()
-        counts = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64),
-                              (bi[:o + n_tp] >= 0).sum()]).cpu().numpy()
-        out["triangulation_pairs"], out["new_points"], out["fuse_candidates"] = (int(c) for c in counts)
+        ms = self._ms
+
+        def stats():  # what the searches found (statistics only: off the chain's path)
+            ms.synchronize()
+            c = torch.stack([(tri[:nt] >= 0).sum(), tri_ok[:nt].sum(dtype=torch.int64),
+                             (bi[:o + n_tp] >= 0).sum()]).cpu().numpy()
+            return {"triangulation_pairs": int(c[0]), "new_points": int(c[1]), "fuse_candidates": int(c[2])}
+        out = ChainStats(stats, bow_words=nw, local_ba_iterations=list(self.last["iterations"]))
         self._out = dict(tri=lambda: tri[:nt].cpu().numpy().reshape(nnb, kf.n),
                          tri_ok=lambda: tri_ok[:nt].cpu().numpy().reshape(nnb, kf.n),
                          x3d=lambda: x3d[:3 * nt].cpu().numpy().reshape(nnb, kf.n, 3),
@@ -551,6 +586,9 @@ class LocalMapper:
             check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(self.voc._h, None))
         self.ba.close()
         self.matcher.close()
+        if self._counts_h:
+            self._hip.hipHostFree(self._counts_h)
+            self._counts_h = C.c_void_p()
 
 
 def gather_stream_features(dist, desc, kps, count):
