@@ -67,12 +67,14 @@ struct BaCtl {
     int steps;        // trial steps executed (diagnostics)
     int lin;          // which of the two linear-system buffers holds the current system
     unsigned arrive;  // blocks of k_ba_update_errors finished (the last one runs the control)
+    unsigned arrive_e;  // blocks of k_ba_activate_edges / k_ba_errors finished (the last one
+                        // runs the one-wave tail: the LM state set-up / activeRobustChi2)
     double lambda, ni, currentChi, iniChi;
     double chi_out[2];  // activeRobustChi2 after optimize(5) / optimize(10)
     int it_out[2];      // iterations of optimize(5) / optimize(10); -1 with an empty mapping
     // The whole call is enqueued at once (Runner); these gate each kernel to its optimize():
     int gen;          // the optimize() the LM state belongs to (1: optimize(5), 2: optimize(10))
-    int phases_done;  // optimize() calls finished (k_ba_chi)
+    int phases_done;  // optimize() calls finished (k_ba_errors' tail)
     int do_more;      // optimize(10) runs: pbStopFlag was clear after optimize(5) (:689-692)
 };
 
@@ -335,7 +337,8 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_levels(BaDev a) {
 // and each block counts the points whose first active edge it holds (partials in part_lin,
 // which the next linearisation overwrites).  Bit 0 is never rewritten, so reading it from the
 // point's other edges while they are updated is safe.
-__global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int gen) {
+__device__ inline void activate_ctl_body(const BaDev& a, int max_it, int gen);
+__global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int max_it, int gen) {
     if (gen > 1 && !(a.ctl->phases_done >= gen - 1 && a.ctl->do_more)) return;
     __shared__ double red[kBaBlock / 64];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -353,14 +356,23 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int gen
         a.eflag[i] = f;
     }
     const double n = block_sum<kBaBlock>((double)first, red);
-    if (threadIdx.x == 0) a.part_lin[blockIdx.x] = n;
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        a.part_lin[blockIdx.x] = n;
+        __threadfence();
+        last = atomicAdd(&a.ctl->arrive_e, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // every block's eflag / kf_act / part_lin
+    if (threadIdx.x < 64) activate_ctl_body(a, max_it, gen);  // one wave: the LM state
+    if (threadIdx.x == 0) a.ctl->arrive_e = 0;
 }
 
 // One wave: the number of active points, pose indices in vertex-id order (poses first) by a
 // ballot scan over the id-ordered keyframes, and the LM state of levenberg.cpp:61-70.  The
 // edges' pose indices (e_pi) are written by the next k_ba_linearize.
-__global__ __launch_bounds__(64) void k_ba_activate_ctl(BaDev a, int max_it, int gen) {
-    if (gen > 1 && !(a.ctl->phases_done >= gen - 1 && a.ctl->do_more)) return;
+__device__ inline void activate_ctl_body(const BaDev& a, int max_it, int gen) {
     if (a.stop && *a.stop) max_it = 0;  // pbStopFlag raised meanwhile: optimize() returns at once
     const int lane = threadIdx.x;
     double c = 0;
@@ -489,7 +501,8 @@ __global__ __launch_bounds__(kPairThreads) void k_ba_pairs_fill(BaDev a) {
 // ---------------------------------------------------------------- errors
 // computeActiveErrors (recompute = 1) + activeRobustChi2; per-block partial sums
 // activeRobustChi2 on the stored (possibly stale) errors; per-block partial sums
-__global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a) {
+__device__ inline void chi_body(const BaDev& a, int phase);
+__global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a, int phase) {
     if (!(a.ctl->done && a.ctl->gen == a.run_gen)) return;  // its optimize() still running
     __shared__ double red[kBaBlock / 64];
     double* part = a.part_lin;
@@ -501,7 +514,17 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a) {
         s = r0;
     }
     s = block_sum<kBaBlock>(s, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s;
+        __threadfence();
+        last = atomicAdd(&a.ctl->arrive_e, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (threadIdx.x < 64) chi_body(a, phase);  // one wave: the partials in a fixed order
+    if (threadIdx.x == 0) a.ctl->arrive_e = 0;
 }
 
 // ---------------------------------------------------------------- linear system
@@ -1713,8 +1736,7 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
 }
 
 // activeRobustChi2 after optimize() (k_ba_errors partials) and the iteration count
-__global__ __launch_bounds__(64) void k_ba_chi(BaDev a, int phase) {
-    if (!(a.ctl->done && a.ctl->gen == a.run_gen)) return;
+__device__ inline void chi_body(const BaDev& a, int phase) {
     const double chi = wave_sum_fixed(a.part_lin, a.nb_e);
     if (threadIdx.x == 0) {
         BaCtl& c = *a.ctl;
@@ -1854,8 +1876,7 @@ struct Runner {
     void prologue(int iterations, int gen) {
         a.run_gen = gen;
         if (gen == 2) hipLaunchKernelGGL(k_ba_levels, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);  // :694-737
-        hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, gen);
-        hipLaunchKernelGGL(k_ba_activate_ctl, dim3(1), dim3(64), 0, h.stream, a, iterations, gen);
+        hipLaunchKernelGGL(k_ba_activate_edges, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, iterations, gen);
         // iteration 0's computeActiveErrors + buildSystem (later ones come with the trials)
         hipLaunchKernelGGL(k_ba_linearize, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
         hipLaunchKernelGGL(k_ba_reduce, dim3(a.nb_p + std::max(a.nf, 1)), dim3(kBaBlock), 0, h.stream, a);
@@ -1864,8 +1885,7 @@ struct Runner {
     // activeRobustChi2 after optimize() gen
     void epilogue(int gen) {
         a.run_gen = gen;
-        hipLaunchKernelGGL(k_ba_errors, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a);
-        hipLaunchKernelGGL(k_ba_chi, dim3(1), dim3(64), 0, h.stream, a, gen - 1);
+        hipLaunchKernelGGL(k_ba_errors, dim3(a.nb_e), dim3(kBaBlock), 0, h.stream, a, gen - 1);
     }
 };
 
