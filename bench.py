@@ -407,7 +407,7 @@ def run_track(a, rank, world, local, dist):
                             f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
                             + (f"+ LocalMapping::Run every {KF_EVERY}th frame on the concurrent LocalMapping thread "
                                "[ProcessNewKeyFrame: KeyFrame::ComputeBoW + ComputeDistinctiveDescriptors; "
-                               "CreateNewMapPoints: SearchForTriangulation x9 neighbours + host triangulation; "
+                               "CreateNewMapPoints: SearchForTriangulation x9 neighbours + triangulation geometry, all on the device; "
                                "SearchInNeighbors: Fuse x9 targets + Fuse(KF, targets' points) + "
                                "ComputeDistinctiveDescriptors; LocalBundleAdjustment(config 3)]" if full_chain else
                                "+ KeyFrame::ComputeBoW + LocalBundleAdjustment(config 3) "
