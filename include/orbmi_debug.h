@@ -30,12 +30,14 @@ int orbmi_debug_pose_trace(orbmi_pose* h, orbmi_pose_frame* frames, const orbmi_
 
 /* k_greedy (the order-dependent exclusion of SearchByProjection) since the last reset, summed
  * over every matcher of the process: out = {calls, rounds, largest round count, slow-path query
- * evaluations, calls that fell back to the sequential replay}; synchronises the device. */
+ * evaluations, calls that fell back to the sequential replay}; synchronises the device.  The
+ * kernels collect these (and orbmi_debug_greedy_cycles) only after the first call of either. */
 int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
 
 /* k_greedy's s_memtime cycles summed over calls since the last reset: out[0] prologue (queries'
  * prefixes and the keypoints' octave / occupancy loaded), [1] the rounds to the fixpoint,
- * [2] the outputs (rotation histogram, last assignment per keypoint). */
+ * [2] the outputs (rotation histogram, last assignment per keypoint); [3..6] reserved (0).
+ * out: 7 entries. */
 int orbmi_debug_greedy_cycles(unsigned long long* out, int reset);
 
 /* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame

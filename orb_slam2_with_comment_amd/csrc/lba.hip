@@ -944,13 +944,6 @@ __device__ inline double rcp_f64(double d) {
     return fma(r, e, r);
 }
 
-// lane `l`'s value of v, in every lane (l wave-uniform)
-__device__ inline double readlane_f64(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
 // LDL^T of a 6x6 tile (full row-major, upper triangle used): on return F[j][c] = U_jc (c > j),
 // F[j][j] = d_j, inv6 = 1 / d.  False on a zero or non-finite pivot.
 __device__ inline bool ldl6(double F[36], double inv6[6]) {
@@ -1223,7 +1216,7 @@ __global__ __launch_bounds__(kBaSolveRowsThreads) void k_ba_solve_rows(BaDev a) 
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_f64(A[r * CPT + c % 2], base + c / 2);
+            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_d(A[r * CPT + c % 2], base + c / 2);
         const bool ok = ldl6(F, inv6);
         if (dg && bi == k && h == 0 && !ok) fail = 1;
         if (!(own && bi == k && bj > k)) return;
@@ -1412,7 +1405,7 @@ __global__ __launch_bounds__(kBaSolvePipeThreads) void k_ba_solve_pipe(BaDev a) 
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_f64(A[r * CPT + c % 2], base + c / 2);
+            for (int c = r; c < 6; c++) F[r * 6 + c] = readlane_d(A[r * CPT + c % 2], base + c / 2);
         const bool ok = ldl6(F, inv6);
         if (lane == 0 && !ok) fail = 1;
         double R[6 * CPT];

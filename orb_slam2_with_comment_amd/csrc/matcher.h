@@ -140,7 +140,7 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
                       float th, int* best_idx, int* best_dist, int* ncand);
 int launch_patch_desc(Matcher& m, orbmi_mappoint* mps, const int* desc_from, const uint8_t* desc, int n);
 int greedy_stats(unsigned long long out[5], int reset);
-int greedy_cycles(unsigned long long out[3], int reset);
+int greedy_cycles(unsigned long long out[7], int reset);
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out);
 int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, const uint8_t* td, int nseg,
                   int seg_cap, const int* seg_counts, int skip_seg, int th, float ratio, int* match, int* nmatches);

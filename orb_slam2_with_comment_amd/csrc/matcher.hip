@@ -501,16 +501,21 @@ constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = ORBMI_GREEDY_
 // k_greedy statistics (orbmi_debug_greedy_stats): calls, rounds summed, largest round count,
 // slow-path query evaluations summed, calls that fell back to the sequential replay
 __device__ unsigned long long g_greedy_stats[5];
+__device__ int g_greedy_on;  // set by the first orbmi_debug_greedy_* call: statistics collected from then on
 // development aid: s_memtime cycles of k_greedy's phases summed over calls (prologue, rounds,
 // epilogue), read with the statistics (orbmi_debug_greedy_stats out[5..7] when asked for 8)
-__device__ unsigned long long g_greedy_cycles[3];
+__device__ unsigned long long g_greedy_cycles[7];
 
 // Each thread keeps its queries (q = tid + k * 1024) in registers: current result, candidate
 // count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
-// octave and the initial occupancy live in LDS.  A round then touches LDS only, except for
-// queries whose prefix runs out of unclaimed entries (full list / re-enumeration).
+// octave and the initial occupancy live in LDS.  A round then touches LDS only, except
+// for queries whose prefix runs out of unclaimed entries (full list / re-enumeration).
+// Claims carry the round: claim[i] = tag(r) | q with tag(r) = (64 - r) << 16 (an atomicMin keeps
+// the current round's smallest query, and an older round's claim reads as free), 0 for a keypoint
+// occupied on entry; so the array is set once, and a round is claims, a barrier, the evaluation,
+// a barrier (the convergence flag alternates between two slots).
 __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
-    __shared__ int claim[kGreedyMaxKp];   // min query index holding the keypoint (with obs);
+    __shared__ int claim[kGreedyMaxKp];   // round-tagged min query index holding the keypoint;
                                           // afterwards the max query index assigned to it
     __shared__ uint8_t occ0[kGreedyMaxKp], oct[kGreedyMaxKp];  // occ0: afterwards "rejected"
     __shared__ int slowres[kGreedyQPer * kGreedyThreads];
@@ -546,33 +551,40 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
 #pragma unroll
             for (int j = 0; j < kGreedyPre; j++) {
                 const unsigned long long e = t[j];
-                pre[k][j] = ((unsigned)(e >> 40) << 16) | (unsigned)(e & 0xFFFF);
+                pre[k][j] = ((unsigned)(e >> 40) << 16) | (unsigned)(e & 0xFFFF);  // dist <= 256: 9 bits
             }
         }
     }
     if (!regs)
         for (int q = tid; q < nq; q += blockDim.x) a.res[q] = -1;
+    // claims set once (round tags, 0 = occupied on entry), flags cleared
+    for (int i = tid; i < n; i += blockDim.x) claim[i] = occ0[i] ? 0 : 0x7FFFFFFF;
+    if (tid < 2) flag[tid] = 0;
     __syncthreads();
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     bool converged = false;
     int rounds = 0, nslow = 0;
+    static_assert(kGreedyRounds < 48 + 1 && kGreedyMaxKp <= 65536, "round tags and query indices share 32 bits");
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
         rounds++;
-        // the initial occupancy folded in (-1 < every query): one LDS read per candidate test
-        for (int i = tid; i < n; i += blockDim.x) claim[i] = occ0[i] ? -1 : 0x7FFFFFFF;
-        if (tid == 0) flag[0] = 0;
-        __syncthreads();
+        const int tag = (64 - round) << 16;
+        // keypoint idx is taken for query q: occupied on entry, or claimed this round by an earlier query
+        auto taken = [&](int idx, int q) {
+            const int v = claim[idx];
+            return v == 0 || ((v & ~0xFFFF) == tag && (v & 0xFFFF) < q);
+        };
         if (regs) {
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++)
-                if (res[k] >= 0 && obs[k]) atomicMin(&claim[res[k]], tid + k * kGreedyThreads);
+                if (res[k] >= 0 && obs[k]) atomicMin(&claim[res[k]], tag | (tid + k * kGreedyThreads));
         } else {
             for (int q = tid; q < nq; q += blockDim.x) {
                 const int r = a.res[q];
-                if (r >= 0 && query_has_obs(a, q)) atomicMin(&claim[r], q);
+                if (r >= 0 && query_has_obs(a, q)) atomicMin(&claim[r], tag | q);
             }
         }
         __syncthreads();
+        if (tid == 0) flag[(round + 1) & 1] = 0;  // the next round's slot (last read before this round's claims)
         int changed = 0;
         if (regs) {
             unsigned slow = 0;
@@ -581,50 +593,60 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             for (int k = 0; k < kGreedyQPer; k++) {
                 const int q = tid + k * kGreedyThreads;
                 fast[k] = res[k];
+                // the query's prefix claims read at once (independent LDS reads, one latency)
+                int cv[kGreedyPre];
+#pragma unroll
+                for (int j = 0; j < kGreedyPre; j++) cv[j] = claim[pre[k][j] & 0xFFFF];
                 if (q >= nq) continue;
                 int d1 = 0, i1 = -1, d2 = 0, i2 = -1;
                 const int kk = nc[k] <= a.cap ? min(nc[k], kGreedyPre) : 0;
 #pragma unroll
                 for (int j = 0; j < kGreedyPre; j++) {
                     if (j >= kk || i2 >= 0) continue;
-                    const int idx = (int)(pre[k][j] & 0xFFFF), d = (int)(pre[k][j] >> 16);
-                    if (claim[idx] < q) continue;
+                    const int v = cv[j];
+                    if (v == 0 || ((v & ~0xFFFF) == tag && (v & 0xFFFF) < q)) continue;
+                    const unsigned e = pre[k][j];
+                    const int idx = (int)(e & 0xFFFF), d = (int)((e >> 16) & 0x1FF);
                     if (i1 < 0) { d1 = d; i1 = idx; } else { d2 = d; i2 = idx; }
                 }
                 if (i2 < 0 && nc[k] > kGreedyPre) slow |= 1u << k;  // prefix exhausted
                 else fast[k] = greedy_decide(a, oct, d1, i1, d2, i2);
             }
             nslow += __builtin_popcount(slow);
-            for (int k = 0; k < kGreedyQPer; k++)  // not unrolled: one copy of the slow path
-                if (slow >> k & 1) {
-                    const int q = tid + k * kGreedyThreads;
-                    auto occ = [&](int idx) { return claim[idx] < q; };
-                    int r;
-                    if (nc[k] <= a.cap) {
-                        // the whole list, 16 loads in flight; octaves from LDS.  k_candidates
-                        // writes the list only past kTopK entries: below that the sorted prefix
-                        // holds all of them
-                        unsigned long long b1 = ~0ull, b2 = ~0ull;
+            // queries whose prefix ran out: the whole wave evaluates each one together, every
+            // lane loading entries of its candidate list (one global latency instead of a serial
+            // scan), the two smallest unclaimed entries by wave minima (entries are distinct)
+            const int lane = tid & 63;
+            unsigned long long pending = __ballot(slow != 0);
+            while (pending) {
+                const int src = __builtin_ctzll(pending);
+                pending &= pending - 1;
+                const unsigned sl = (unsigned)__shfl((int)slow, src, 64);
+                for (int k = 0; k < kGreedyQPer; k++) {
+                    if (!(sl >> k & 1)) continue;
+                    const int q = tid - lane + src + k * kGreedyThreads;
+                    const int ncq = __shfl(nc[k], src, 64);
+                    int r = -1;
+                    if (ncq <= a.cap) {
                         const unsigned long long* c =
-                            nc[k] <= kTopK ? a.top + (long long)q * kTopK : a.cand + (long long)q * a.cap;
-                        for (int k0 = 0; k0 < nc[k]; k0 += 16) {
-                            unsigned long long e[16];
-#pragma unroll
-                            for (int j = 0; j < 16; j++) e[j] = k0 + j < nc[k] ? c[k0 + j] : ~0ull;
-#pragma unroll
-                            for (int j = 0; j < 16; j++) {
-                                if (e[j] == ~0ull || occ((int)(e[j] & 0xFFFFF))) continue;
-                                if (e[j] < b1) { b2 = b1; b1 = e[j]; }
-                                else if (e[j] < b2) b2 = e[j];
-                            }
+                            ncq <= kTopK ? a.top + (long long)q * kTopK : a.cand + (long long)q * a.cap;
+                        unsigned long long b1 = ~0ull, b2 = ~0ull;
+                        for (int p = lane; p < ncq; p += 64) {
+                            const unsigned long long e = c[p];
+                            if (taken((int)(e & 0xFFFFF), q)) continue;
+                            if (e < b1) { b2 = b1; b1 = e; }
+                            else if (e < b2) b2 = e;
                         }
-                        r = greedy_decide(a, oct, (int)(b1 >> 40), b1 == ~0ull ? -1 : (int)(b1 & 0xFFFFF), (int)(b2 >> 40),
-                                          b2 == ~0ull ? -1 : (int)(b2 & 0xFFFFF));
-                    } else {  // overflowed list: enumerate again
-                        r = greedy_eval(a, q, Tc.m, fw, bw, occ);
+                        const unsigned long long m1 = wave_min_u64_dpp(b1);
+                        const unsigned long long m2 = wave_min_u64_dpp(b1 == m1 ? b2 : b1);
+                        r = greedy_decide(a, oct, (int)(m1 >> 40), m1 == ~0ull ? -1 : (int)(m1 & 0xFFFFF),
+                                          (int)(m2 >> 40), m2 == ~0ull ? -1 : (int)(m2 & 0xFFFFF));
+                    } else if (lane == src) {  // overflowed list: enumerate again
+                        r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return taken(idx, q); });
                     }
-                    slowres[k * kGreedyThreads + tid] = r;
+                    if (lane == src) slowres[k * kGreedyThreads + tid] = r;
                 }
+            }
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++) {
                 const int r = (slow >> k & 1) ? slowres[k * kGreedyThreads + tid] : fast[k];
@@ -632,14 +654,13 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             }
         } else {
             for (int q = tid; q < nq; q += blockDim.x) {
-                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return claim[idx] < q; });
+                const int r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return taken(idx, q); });
                 if (r != a.res[q]) { a.res[q] = r; changed = 1; }
             }
         }
-        if (changed) atomicOr(&flag[0], 1);
+        if (__ballot(changed) && (tid & 63) == 0) flag[round & 1] = 1;  // one LDS store per wave, no atomics
         __syncthreads();
-        converged = flag[0] == 0;
-        __syncthreads();
+        converged = flag[round & 1] == 0;
     }
     if (regs) {
 #pragma unroll
@@ -694,16 +715,24 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         }
     };
     const bool ori = a.mode == 1 && a.check_ori;
+    // match counts per thread, then one LDS atomic per wave (a shared counter hit by every
+    // thread serialises the wave's 64 atomics)
+    auto wave_count = [&](int c, int sign) {
+        c = (int)wave_sum((double)c);
+        if ((tid & 63) == 0 && c) atomicAdd(&flag[1], sign * c);
+    };
+    int nmine = 0;
     each_query([&](int k, int q, int r) {
         if (r < 0) return;
         atomicMax(&last[r], q);
-        atomicAdd(&flag[1], 1);
+        nmine++;
         if (ori) {
             const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
             atomicAdd(&hist[bin], 1);
             if (k >= 0) fbin[k] = bin;
         }
     });
+    wave_count(nmine, 1);
     __syncthreads();
     int ind1 = -1, ind2 = -1, ind3 = -1;
     if (a.mode == 1 && a.check_ori) {  // ComputeThreeMaxima (:1854-1895), same in every thread
@@ -716,6 +745,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         }
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int nrej = 0;
         each_query([&](int k, int q, int r) {
             if (r < 0) return;
             int bin = -1;
@@ -726,12 +756,14 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             } else {
                 bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
             }
-            if (bin != ind1 && bin != ind2 && bin != ind3) { rejected[r] = 1; atomicSub(&flag[1], 1); }
+            if (bin != ind1 && bin != ind2 && bin != ind3) { rejected[r] = 1; nrej++; }
         });
+        wave_count(nrej, -1);
         __syncthreads();
     }
     for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
     if (tid == 0) *a.nmatches = flag[1];
+    if (!g_greedy_on) return;  // statistics only once a probe asked for them
     if (nslow) atomicAdd(&g_greedy_stats[3], (unsigned long long)nslow);
     if (tid == 0) {
         const unsigned long long c3 = __builtin_amdgcn_s_memtime();
@@ -745,11 +777,13 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     }
 }
 
-int greedy_cycles(unsigned long long out[3], int reset) {
+int greedy_cycles(unsigned long long out[7], int reset) {
     ORBMI_HIP(hipDeviceSynchronize());
-    ORBMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_greedy_cycles), sizeof(unsigned long long) * 3));
+    const int on = 1;
+    ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_greedy_on), &on, sizeof(on)));
+    ORBMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_greedy_cycles), sizeof(unsigned long long) * 7));
     if (reset) {
-        const unsigned long long z[3] = {0, 0, 0};
+        const unsigned long long z[7] = {0, 0, 0, 0, 0, 0, 0};
         ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_greedy_cycles), z, sizeof(z)));
     }
     return ORBMI_OK;
@@ -757,6 +791,8 @@ int greedy_cycles(unsigned long long out[3], int reset) {
 
 int greedy_stats(unsigned long long out[5], int reset) {
     ORBMI_HIP(hipDeviceSynchronize());
+    const int on = 1;
+    ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_greedy_on), &on, sizeof(on)));
     ORBMI_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_greedy_stats), sizeof(unsigned long long) * 5));
     if (reset) {
         const unsigned long long z[5] = {0, 0, 0, 0, 0};

@@ -125,6 +125,8 @@ for step in "$@"; do
             l=${step#poselat}; l=${l#=}
             if [ -n "$l" ]; then ORBMI_LIB=$l run poselat_ab 120 python tools/pose_latency.py; cat $OUT/poselat_ab.log
             else run poselat 120 python tools/pose_latency.py; cat $OUT/poselat.log; fi;;
+        greedy)
+            run greedy 120 python tools/greedy_probe.py 64; cat $OUT/greedy.log;;
         mfma_pmc)
             # MFMA A/B of the Schur products: MFMA issue / busy counters of each variant's kernel
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur

@@ -27,7 +27,7 @@ def main():
                  S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
     tr.synchronize()
     L.orbmi_debug_greedy_stats(st, 1)
-    cyc = (C.c_ulonglong * 3)()
+    cyc = (C.c_ulonglong * 7)()
     L.orbmi_debug_greedy_cycles(cyc, 1)
     for i in range(nfr):
         f = 2 + i % 8
@@ -40,7 +40,7 @@ def main():
           f"{st[3] / calls:.1f}, sequential fallbacks {st[4]}")
     L.orbmi_debug_greedy_cycles(cyc, 0)
     print("k_greedy s_memtime cycles per call: prologue %.0f, rounds %.0f, "
-          "outputs %.0f" % tuple(c / calls for c in cyc))
+          "outputs %.0f" % tuple(c / calls for c in cyc[:3]))
     print("result:", tr.results()["search_matches"], tr.results()["inliers"])
     tr.close()
 
