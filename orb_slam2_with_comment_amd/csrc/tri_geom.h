@@ -71,28 +71,37 @@ ORBMI_HD inline void null_vector4(const float* A, double v[4]) {
     for (int p = 0; p < 4; p++) diag2 += M[p][p] * M[p][p];
     for (int sweep = 0; sweep < 30; sweep++) {
         double off = 0;
+#pragma unroll
         for (int p = 0; p < 4; p++)
+#pragma unroll
             for (int q = p + 1; q < 4; q++) off += M[p][q] * M[p][q];
         // converged to working precision: the off-diagonal mass is below (1e-17)^2 of the
         // diagonal's, so further rotations only move rounding (sweeping on to an exact zero
         // took ~4x the rotations)
         if (off <= 1e-34 * diag2) break;
+        // p, q, k unrolled: every index static, so the matrices stay in registers on the device
+        // (a rolled loop put them in scratch memory); the same operations in the same order
+#pragma unroll
         for (int p = 0; p < 4; p++)
+#pragma unroll
             for (int q = p + 1; q < 4; q++) {
                 if (M[p][q] == 0) continue;
                 const double theta = (M[q][q] - M[p][p]) / (2 * M[p][q]);
                 const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
                 const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+#pragma unroll
                 for (int k = 0; k < 4; k++) {  // M <- J^T M J
                     const double mkp = M[k][p], mkq = M[k][q];
                     M[k][p] = c * mkp - s * mkq;
                     M[k][q] = s * mkp + c * mkq;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const double mpk = M[p][k], mqk = M[q][k];
                     M[p][k] = c * mpk - s * mqk;
                     M[q][k] = s * mpk + c * mqk;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const double vkp = V[k][p], vkq = V[k][q];
                     V[k][p] = c * vkp - s * vkq;
@@ -101,9 +110,18 @@ ORBMI_HD inline void null_vector4(const float* A, double v[4]) {
             }
     }
     int m = 0;
+    double mm = M[0][0];
+#pragma unroll
     for (int i = 1; i < 4; i++)
-        if (M[i][i] < M[m][m]) m = i;
-    for (int k = 0; k < 4; k++) v[k] = V[k][m];
+        if (M[i][i] < mm) { m = i; mm = M[i][i]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        double x = V[k][0];
+#pragma unroll
+        for (int i = 1; i < 4; i++)
+            if (m == i) x = V[k][i];
+        v[k] = x;
+    }
 }
 
 // One keyframe of a triangulation pair: pose (rows 0-2 of Tcw) and what derives from it, the
