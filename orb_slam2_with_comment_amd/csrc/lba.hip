@@ -1609,7 +1609,10 @@ __device__ inline void k_ba_control_body(const BaDev& a) {
 // state (T_t from the solve) and the edge's linearisation at that state into the other
 // linear-system buffer; threads 0..31 then sum the points' Hll / b_l there.  Block partials:
 // robust chi2 and scale; the last block to finish runs the Levenberg decision.
-constexpr int kBaUpdPts = 32;                      // (16 per block, 188 blocks for config 3, measured slower)
+#ifndef ORBMI_UPD_PTS
+#define ORBMI_UPD_PTS 32
+#endif
+constexpr int kBaUpdPts = ORBMI_UPD_PTS;          // (16 per block, 188 blocks for config 3, measured slower)
 constexpr int kBaUpdLanes = 8;                     // threads per point
 constexpr int kBaUpdThreads = kBaUpdPts * kBaUpdLanes;
 constexpr int kBaUpdLdsEdges = 512;                // a block's edges whose Hll / b_l terms stay in LDS

@@ -139,6 +139,16 @@ for step in "$@"; do
                 ORBMI_LIB=$B run ab_B$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
                 echo "A $(tail -1 $OUT/ab_A$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')  B $(tail -1 $OUT/ab_B$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')" | tee -a $OUT/ab.txt
             done;;
+        ablba=*)
+            # LocalBA (config 3) A/B/... over library builds: ablba=LIB1,LIB2,... alternating, 3 rounds
+            libs=${step#ablba=}
+            for i in 1 2 3; do
+                for l in ${libs//,/ }; do
+                    n=$(basename $l .so)
+                    ORBMI_LIB=$l run ablba_${n}_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
+                    echo "$n $(tail -1 $OUT/ablba_${n}_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')" | tee -a $OUT/ablba.txt
+                done
+            done;;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
