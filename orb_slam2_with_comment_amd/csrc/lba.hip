@@ -1560,9 +1560,21 @@ __device__ inline double wave_sum_fixed(const double* p, int n) {
 // on a rejection keeps the estimate, hence the chi2 and the linear system).
 __device__ inline void k_ba_control_body(const BaDev& a) {
     BaCtl& c = *a.ctl;
-    const double lin = wave_sum_fixed(a.part_lin, a.nb_e);
-    const double tchi = wave_sum_fixed(a.part_tchi, a.nb_q);
-    const double tsc = wave_sum_fixed(a.part_tscale, a.nb_q);
+    // the three fixed-order sums of wave_sum_fixed with their loads issued together (one memory
+    // latency on the trial chain instead of three); the linearisation's chi2 only where it is read
+    const bool need_lin = c.trial == 0 && c.it == 0;
+    double l = 0, t = 0, sc = 0;
+    const int lane = threadIdx.x, nmax = max(need_lin ? a.nb_e : 0, a.nb_q);
+    for (int k = lane; k < nmax; k += 64) {
+        if (need_lin && k < a.nb_e) l += a.part_lin[k];
+        if (k < a.nb_q) { t += a.part_tchi[k]; sc += a.part_tscale[k]; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        l += __shfl_xor(l, o, 64);
+        t += __shfl_xor(t, o, 64);
+        sc += __shfl_xor(sc, o, 64);
+    }
+    const double lin = __shfl(l, 0, 64), tchi = __shfl(t, 0, 64), tsc = __shfl(sc, 0, 64);
     if (threadIdx.x != 0) return;
     if (c.trial == 0) {
         if (c.it == 0) c.currentChi = lin;
