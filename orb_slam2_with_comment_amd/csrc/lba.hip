@@ -605,14 +605,20 @@ struct EdgeIn {
     int pi, kpos;
     unsigned char fl;
 };
-__device__ inline void edge_in(const BaDev& a, int i, const double* T, EdgeIn& s) {
+__device__ inline void edge_in_static(const BaDev& a, int i, EdgeIn& s) {  // fixed within an optimize()
     s.e = a.edges[i];
     s.fl = a.eflag[i];
     s.pi = a.e_pi[i];
     s.kpos = a.kf_pos[i];
     s.cam = ba_cam(a.kfs[s.e.kf]);
+}
+__device__ inline void edge_in_pose(const double* T, EdgeIn& s) {
 #pragma unroll
     for (int q = 0; q < 8; q++) s.T[q] = T[8 * s.e.kf + q];
+}
+__device__ inline void edge_in(const BaDev& a, int i, const double* T, EdgeIn& s) {
+    edge_in_static(a, i, s);
+    edge_in_pose(T, s);
 }
 
 // computeActiveErrors + robust chi2 + the linearisation of one edge at the trial state from
@@ -781,6 +787,23 @@ __device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
 }
 
 __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
+    // the block's pair structure (static within an optimize()) is loaded before the LM state, so
+    // that its two dependent loads overlap the control block's instead of following it
+    const int b = blockIdx.x;
+    int pka = 0, pkb = 0, pi1 = -1, pi2 = -1, pjs = 0, pje = 0, ppt = 0;
+    int2 ppr = make_int2(0, 0);
+    if (b < a.nblk) {
+        pka = a.blk_kf[2 * b];
+        pkb = a.blk_kf[2 * b + 1];
+        pjs = a.blk_start[b];
+        pje = a.blk_start[b + 1];
+        pi1 = a.pose_idx[pka];
+        pi2 = a.pose_idx[pkb];
+        if (pjs + (int)threadIdx.x < pje) {
+            ppr = a.blk_pairs[pjs + threadIdx.x];
+            ppt = a.blk_pt[pjs + threadIdx.x];
+        }
+    }
     const BaCtl& ctl = *a.ctl;
     if (ctl.done || ctl.gen != a.run_gen) return;
     ba_use(a, ctl.lin);
@@ -836,19 +859,19 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
         }
         return;
     }
-    const int b = blockIdx.x;
-    const int ka = a.blk_kf[2 * b], kb = a.blk_kf[2 * b + 1];
-    const int i1 = a.pose_idx[ka], i2 = a.pose_idx[kb];
+    const int ka = pka, kb = pkb;
+    const int i1 = pi1, i2 = pi2;
     if (i1 < 0 || i2 < 0) return;
     const bool diag = ka == kb;
     if (diag) pose_rows_sum<21>(a, ka, 0, rows, ptot);  // Hpp of the keyframe (upper, row-major)
     double acc[36];
 #pragma unroll
     for (int q = 0; q < 36; q++) acc[q] = 0;
-    for (int j = a.blk_start[b] + threadIdx.x; j < a.blk_start[b + 1]; j += blockDim.x) {
-        const int2 pr = a.blk_pairs[j];  // inactive edges carry a zero Hpl block
+    for (int j = pjs + threadIdx.x; j < pje; j += blockDim.x) {
+        const bool first = j == pjs + (int)threadIdx.x;  // the prefetched pair
+        const int2 pr = first ? ppr : a.blk_pairs[j];  // inactive edges carry a zero Hpl block
         double Di[9];
-        point_dinv(a.Hll, a.blk_pt[j], lam, Di);
+        point_dinv(a.Hll, first ? ppt : a.blk_pt[j], lam, Di);
         const double* B1 = a.Hpl + 18 * (long long)pr.x;
         const double* B2 = a.Hpl + 18 * (long long)pr.y;
         double BD[18];
@@ -1639,6 +1662,17 @@ __device__ inline double sum8(double v) {
 }
 
 __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
+    // the graph's part of what the block reads (static within an optimize()) is requested before
+    // the LM state, so that its dependent loads overlap the control block's
+    const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
+    const int tid = threadIdx.x, ps = tid / kBaUpdLanes, j = tid % kBaUpdLanes;
+    const int p = p0 + ps;
+    const bool own = p < p1;
+    const int pe0 = own ? a.pt_start[p] : 0, pe1 = own ? a.pt_start[p + 1] : 0;
+    const int be0 = p0 < p1 ? a.pt_start[p0] : 0, be1 = p0 < p1 ? a.pt_start[p1] : 0;
+    const int e_pre = be0 + tid;
+    EdgeIn pre;
+    if (e_pre < be1) edge_in_static(a, e_pre, pre);
     BaCtl& ctl = *a.ctl;
     if (ctl.done || ctl.gen != a.run_gen) return;
     const int L = ctl.lin;
@@ -1655,17 +1689,9 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     __shared__ double sHe[kBaUpdLdsEdges * 9];
     __shared__ bool last;
     const bool ok = a.istat[3] != 0;
-    const int p0 = blockIdx.x * kBaUpdPts, p1 = min(p0 + kBaUpdPts, a.npt);
-    const int tid = threadIdx.x, ps = tid / kBaUpdLanes, j = tid % kBaUpdLanes;
-    const int p = p0 + ps;
-    const bool own = p < p1;
-    const int pe0 = own ? a.pt_start[p] : 0, pe1 = own ? a.pt_start[p + 1] : 0;
-    // the block's edges (thread per edge in the trial pass): the first one's record, camera and
-    // trial pose are loaded now, under the back substitution's loads
-    const int be0 = p0 < p1 ? a.pt_start[p0] : 0, be1 = p0 < p1 ? a.pt_start[p1] : 0;
-    const int e_pre = be0 + tid;
-    EdgeIn pre;
-    if (e_pre < be1) edge_in(a, e_pre, Tt, pre);
+    // the block's edges (thread per edge in the trial pass): the first one's trial pose is loaded
+    // now, under the back substitution's loads (its record and camera came before the LM state)
+    if (e_pre < be1) edge_in_pose(Tt, pre);
     double sc = 0, chi = 0;
     {  // back substitution x_l = D^-1 (b_l - sum_e Hpl_e^T x_p), 8 lanes per point
         double c0 = 0, c1 = 0, c2 = 0, act = 0;
