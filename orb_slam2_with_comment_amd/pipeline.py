@@ -421,7 +421,10 @@ class LocalMapper:
         # pinned host words for the BowVector / FeatureVector sizes, written by a copy on the
         # mapper's stream (the HIP runtime directly: a torch pinned tensor would record events on
         # this external stream when freed, after the stream is gone)
-        self._hip = C.CDLL("libamdhip64.so.7")  # the runtime torch (and liborbmi.so) already use
+        try:  # the runtime torch (and liborbmi.so) already use
+            self._hip = C.CDLL("libamdhip64.so.7")
+        except OSError:
+            self._hip = C.CDLL("libamdhip64.so")
         self._counts_h = C.c_void_p()
         if self._hip.hipHostMalloc(C.byref(self._counts_h), C.c_size_t(8), C.c_uint(0)) != 0:
             raise RuntimeError("hipHostMalloc failed")
