@@ -378,10 +378,18 @@ __global__ __launch_bounds__(256) void k_candidates(CandArgs a) {
             const unsigned long long e = buf[gl][p];
             if ((k == 0 || e > last) && e < m) m = e;
         }
+        if constexpr (G == 16) {  // group = one DPP row: four DPP moves, no LDS permute round trips
+            unsigned long long v;
+            v = dpp_mov_u64<kDppXor1>(m); m = v < m ? v : m;
+            v = dpp_mov_u64<kDppXor2>(m); m = v < m ? v : m;
+            v = dpp_mov_u64<kDppHalfMirror>(m); m = v < m ? v : m;
+            v = dpp_mov_u64<kDppRor8>(m); m = v < m ? v : m;
+        } else {
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) {
-            const unsigned long long v = __shfl_xor(m, o, G);
-            m = v < m ? v : m;
+            for (int o = G / 2; o > 0; o >>= 1) {
+                const unsigned long long v = __shfl_xor(m, o, G);
+                m = v < m ? v : m;
+            }
         }
         if (valid && lane == 0) a.top[(long long)q * kTopK + k] = m;
         last = m;
