@@ -44,23 +44,58 @@ __host__ __device__ inline int cv_floor_f(float v) { int i = (int)v; return i - 
 __host__ __device__ inline int cv_round_f(float v) { return (int)__builtin_rintf(v); }
 
 // ---- wave-level reductions (wave64) --------------------------------------------------
+// DPP moves inside each row of 16 lanes (quad perms, half-row mirror, row rotate by 8) and
+// v_permlane16/32_swap across rows: no LDS round trip (a __shfl_xor butterfly is one
+// ds_bpermute per step and dword); every lane ends with the result.  The reductions are
+// integer / min / max, so their order does not matter.
+namespace wave_detail {
+template <int CTRL>
+__device__ inline int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false); }
+template <int W>  // the value of lane ^ W (W = 16 or 32)
+__device__ inline int partner(int v) {
+    const auto r = W == 32 ? __builtin_amdgcn_permlane32_swap(v, v, false, false)
+                           : __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    // one of the pair is the own value, the other the partner's (equal values: either)
+    return (int)r[0] == v ? (int)r[1] : (int)r[0];
+}
+__device__ inline unsigned long long dpp64(unsigned long long u, int which) {
+    const int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
+    int l, h;
+    switch (which) {
+        case 0: l = dpp<0xB1>(lo); h = dpp<0xB1>(hi); break;    // quad_perm [1,0,3,2]: lane ^ 1
+        case 1: l = dpp<0x4E>(lo); h = dpp<0x4E>(hi); break;    // quad_perm [2,3,0,1]: lane ^ 2
+        case 2: l = dpp<0x141>(lo); h = dpp<0x141>(hi); break;  // row_half_mirror: 7 - i within 8
+        case 3: l = dpp<0x128>(lo); h = dpp<0x128>(hi); break;  // row_ror:8: lane ^ 8 within 16
+        case 4: l = partner<16>(lo); h = partner<16>(hi); break;
+        default: l = partner<32>(lo); h = partner<32>(hi); break;
+    }
+    return (unsigned long long)(unsigned)h << 32 | (unsigned)l;
+}
+}  // namespace wave_detail
+
 __device__ inline int wave_sum_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    using namespace wave_detail;
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x128>(v);
+    v += partner<16>(v);
+    return v + partner<32>(v);
 }
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long w = __shfl_xor(v, o, 64);
+    for (int k = 0; k < 6; k++) {
+        // the permlane swaps pair a lane with lane ^ 16 / ^ 32 only through the own value test
+        // above, which is exact for distinct keys and harmless for equal ones
+        const unsigned long long w = wave_detail::dpp64(v, k);
         v = w < v ? w : v;
     }
     return v;
 }
 __device__ inline unsigned long long wave_max_u64(unsigned long long v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long w = __shfl_xor(v, o, 64);
+    for (int k = 0; k < 6; k++) {
+        const unsigned long long w = wave_detail::dpp64(v, k);
         v = w > v ? w : v;
     }
     return v;
