@@ -899,7 +899,7 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                         kd = r0 + __ffsll((long long)hit);
                         break;
                     }
-                    run += __shfl(incl, 63);
+                    run += __builtin_amdgcn_readlane(incl, 63);
                 }
                 int push = 0;
                 for (int r0 = 0; r0 < kd; r0 += 64) {
@@ -911,7 +911,7 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                         S.dflag[n] = 1;
                         S.newpos[n] = push + incl - m;
                     }
-                    push += __shfl(incl, 63);
+                    push += __builtin_amdgcn_readlane(incl, 63);
                 }
                 kdiv = kd;
             }

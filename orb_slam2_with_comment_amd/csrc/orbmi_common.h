@@ -101,14 +101,18 @@ __device__ inline unsigned long long wave_max_u64(unsigned long long v) {
     return v;
 }
 // Inclusive prefix sum across the 64 lanes.
+// Inside each row of 16 lanes by DPP row shifts (a lane without a source adds 0), then the
+// totals of the rows before by readlane: no LDS round trip.
 __device__ inline int wave_incl_scan(int v) {
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int w = __shfl_up(v, o, 64);
-        if (lane >= o) v += w;
-    }
-    return v;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    const int t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
+    const int t2 = __builtin_amdgcn_readlane(v, 47);
+    const int row = lane >> 4;
+    return v + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
 }
 
 // Block-wide exclusive scan of one int per thread; `scratch` holds >= blockDim/64 + 1 ints.

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(1024) void k_stereo_filter(const int* __restrict__ 
         int c[4], s = 0;
         for (int j = 0; j < per; j++) { c[j] = h[tid * per + j]; s += c[j]; }
         const int incl = wave_incl_scan(s);
-        *total = __shfl(incl, 63);
+        *total = __builtin_amdgcn_readlane(incl, 63);
         const int rank = rank_in < 0 ? *total / 2 : rank_in;
         int before = incl - s;
         for (int j = 0; j < per; j++) {
