@@ -35,6 +35,7 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "extractor.h"
@@ -1855,6 +1856,10 @@ struct BaTrace {
     }
 };
 
+// the caller's stop flag (bool* pbStopFlag, src/Optimizer.cc:483), written by other threads:
+// read with an atomic load
+inline bool stop_set(const volatile int* stop) { return stop && __atomic_load_n(stop, __ATOMIC_ACQUIRE) != 0; }
+
 // Trial steps enqueued beyond the iterations still to run: a rejected trial consumes one step
 // without finishing an iteration, so the steps enqueued up front usually finish optimize().
 constexpr int kBaStepSlack = 1;
@@ -1871,9 +1876,10 @@ struct Runner {
     bool solve_pipe;  // k_ba_solve_pipe (a dedicated pivot wave) in place of k_ba_solve_rows
                       // (ORBMI_BA_SOLVE=rows selects the latter, for A/B runs)
 
-    bool stopped() const { return stop && *stop; }
+    bool stopped() const { return stop_set(stop); }
 
-    // wait for the stream; meanwhile mirror the caller's stop flag to the device
+    // wait for the stream; meanwhile mirror the caller's stop flag to the device, yielding the
+    // core between polls (the caller's other threads, e.g. tracking, run on the host meanwhile)
     int wait() {
         ORBMI_HIP(hipEventRecord(h.done, h.stream));
         if (!stop) {
@@ -1881,10 +1887,11 @@ struct Runner {
             return ORBMI_OK;
         }
         for (;;) {
-            *(volatile int*)h.h_stop = *stop ? 1 : 0;
+            *(volatile int*)h.h_stop = stop_set(stop) ? 1 : 0;
             const hipError_t e = hipEventQuery(h.done);
             if (e == hipSuccess) return ORBMI_OK;
             if (e != hipErrorNotReady) return ORBMI_E_HIP;
+            std::this_thread::yield();
         }
     }
 
@@ -1988,7 +1995,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     R->iterations[0] = R->iterations[1] = 0;
     R->chi2[0] = R->chi2[1] = 0;
     for (int i = 0; i < P->nedge; i++) R->erase[i] = 0;
-    if (stop && *stop) {  // src/Optimizer.cc:685-687
+    if (stop_set(stop)) {  // src/Optimizer.cc:685-687
         R->aborted = 1;
         return ORBMI_OK;
     }

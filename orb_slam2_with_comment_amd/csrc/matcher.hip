@@ -505,6 +505,8 @@ __device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int
 #define ORBMI_GREEDY_PRE 4
 #endif
 constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = ORBMI_GREEDY_PRE;
+constexpr int kGreedyQBits = 24, kGreedyQMask = (1 << kGreedyQBits) - 1;  // query index field of a claim
+constexpr int kGreedyMaxQueries = 1 << kGreedyQBits;
 
 // k_greedy statistics (orbmi_debug_greedy_stats): calls, rounds summed, largest round count,
 // slow-path query evaluations summed, calls that fell back to the sequential replay
@@ -518,10 +520,11 @@ __device__ unsigned long long g_greedy_cycles[7];
 // count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
 // octave and the initial occupancy live in LDS.  A round then touches LDS only, except
 // for queries whose prefix runs out of unclaimed entries (full list / re-enumeration).
-// Claims carry the round: claim[i] = tag(r) | q with tag(r) = (64 - r) << 16 (an atomicMin keeps
+// Claims carry the round: claim[i] = tag(r) | q with tag(r) = (64 - r) << 24 (an atomicMin keeps
 // the current round's smallest query, and an older round's claim reads as free), 0 for a keypoint
 // occupied on entry; so the array is set once, and a round is claims, a barrier, the evaluation,
-// a barrier (the convergence flag alternates between two slots).
+// a barrier (the convergence flag alternates between two slots).  Query indices take the low 24
+// bits (the launchers refuse nq >= 2^24), the round tag the 7 above them.
 __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     __shared__ int claim[kGreedyMaxKp];   // round-tagged min query index holding the keypoint;
                                           // afterwards the max query index assigned to it
@@ -572,14 +575,14 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     bool converged = false;
     int rounds = 0, nslow = 0;
-    static_assert(kGreedyRounds < 48 + 1 && kGreedyMaxKp <= 65536, "round tags and query indices share 32 bits");
+    static_assert(kGreedyRounds < 48 + 1 && kGreedyMaxKp <= 65536, "round tags (7 bits) above 24-bit query indices");
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
         rounds++;
-        const int tag = (64 - round) << 16;
+        const int tag = (64 - round) << kGreedyQBits;
         // keypoint idx is taken for query q: occupied on entry, or claimed this round by an earlier query
         auto taken = [&](int idx, int q) {
             const int v = claim[idx];
-            return v == 0 || ((v & ~0xFFFF) == tag && (v & 0xFFFF) < q);
+            return v == 0 || ((v & ~kGreedyQMask) == tag && (v & kGreedyQMask) < q);
         };
         if (regs) {
 #pragma unroll
@@ -612,7 +615,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                 for (int j = 0; j < kGreedyPre; j++) {
                     if (j >= kk || i2 >= 0) continue;
                     const int v = cv[j];
-                    if (v == 0 || ((v & ~0xFFFF) == tag && (v & 0xFFFF) < q)) continue;
+                    if (v == 0 || ((v & ~kGreedyQMask) == tag && (v & kGreedyQMask) < q)) continue;
                     const unsigned e = pre[k][j];
                     const int idx = (int)(e & 0xFFFF), d = (int)((e >> 16) & 0x1FF);
                     if (i1 < 0) { d1 = d; i1 = idx; } else { d2 = d; i2 = idx; }
@@ -1096,6 +1099,7 @@ int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int
 
 int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, const orbmi_mappoint* mps,
                         const orbmi_mappoint_track* tr, int n, float th, float nnratio, int* out, int* nmatches) {
+    if (n >= kGreedyMaxQueries) return ORBMI_E_UNSUPPORTED;  // k_greedy's claim field
     int rc;
     if ((rc = grid_for(m, F))) return rc;
     const int cap = Matcher::kCandCap;
@@ -1123,6 +1127,7 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
     int rc;
     if ((rc = grid_for(m, CF, gate, gate_min))) return rc;
     const int n = LF.n, cap = Matcher::kCandCap;
+    if (n >= kGreedyMaxQueries) return ORBMI_E_UNSUPPORTED;  // k_greedy's claim field
     if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)std::max(n, 1) * cap))) return rc;
     if ((rc = ensure_buf(&m.d_ncand, &m.cap_ncand, (size_t)std::max(n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_res, &m.cap_res, (size_t)std::max(n, 1)))) return rc;

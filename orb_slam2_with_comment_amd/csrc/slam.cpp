@@ -298,7 +298,11 @@ struct orbmi_slam {
     bool lm_busy = false;       // !mbAcceptKeyFrames
     bool lm_quit = false;
     int lm_rc = ORBMI_OK;       // the first error of the mapping thread
-    volatile int abort_ba = 0;  // mbAbortBA
+    // mbAbortBA: written by the tracking thread (InterruptBA, InsertKeyFrame) and the mapping
+    // thread, read by the mapping thread and by LocalBA's stop-flag mirror (orbmi_local_bundle_
+    // adjustment reads it with an atomic load): every access is an atomic operation on this word
+    int abort_ba = 0;
+    void set_abort_ba(int v) { __atomic_store_n(&abort_ba, v, __ATOMIC_RELEASE); }
     std::thread lm_thread;
     bool async_lm() const { return s.async_local_mapping != 0; }
 
@@ -754,7 +758,7 @@ struct orbmi_slam {
         st.need_kf = (c1a || c1b || c1c) && c2;
         if (!st.need_kf) return false;
         if (idle) return true;
-        abort_ba = 1;       // mpLocalMapper->InterruptBA()
+        set_abort_ba(1);    // mpLocalMapper->InterruptBA()
         return queued < 3;  // stereo: KeyframesInQueue() < 3
     }
 
@@ -793,7 +797,7 @@ struct orbmi_slam {
             std::lock_guard<std::mutex> g(q_mtx);
             if (lm_rc) return lm_rc;
             lm_queue.push_back(k);
-            abort_ba = 1;  // a new keyframe interrupts the running BA (src/LocalMapping.cc:148)
+            set_abort_ba(1);  // a new keyframe interrupts the running BA (src/LocalMapping.cc:148)
         }
         q_cv.notify_one();
         return ORBMI_OK;
@@ -882,7 +886,7 @@ struct orbmi_slam {
             next(PH_LM_FUSE);
             if (!new_keyframes_queued()) SLAM_CHECK(search_in_neighbors(k));
         }
-        abort_ba = 0;
+        set_abort_ba(0);
         if (!new_keyframes_queued()) {
             next(PH_LM_BA);
             if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));

@@ -34,6 +34,7 @@ import numpy as np
 
 from . import _capi
 from ._capi import check, lib
+from ._hip import PinnedWords
 from .types import FRAME_GRID_COLS, FRAME_GRID_ROWS, FrameView
 
 _vp = C.c_void_p
@@ -409,28 +410,27 @@ class LocalMapper:
         dev = torch.device("cuda", device)
         cap = max_features
         self.cap = cap
-        if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
-            self.bow = dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
-                            value=torch.zeros(cap, dtype=torch.float64, device=dev),
-                            node=torch.zeros(cap, dtype=torch.int32, device=dev),
-                            off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
-                            feat=torch.zeros(cap, dtype=torch.int32, device=dev),
-                            counts=torch.zeros(2, dtype=torch.int32, device=dev))
         self._dev = dev
         self._bufs = {}
-        # pinned host words for the BowVector / FeatureVector sizes, written by a copy on the
-        # mapper's stream (the HIP runtime directly: a torch pinned tensor would record events on
-        # this external stream when freed, after the stream is gone)
-        try:  # the runtime torch (and liborbmi.so) already use
-            self._hip = C.CDLL("libamdhip64.so.7")
-        except OSError:
-            self._hip = C.CDLL("libamdhip64.so")
-        self._counts_h = C.c_void_p()
-        if self._hip.hipHostMalloc(C.byref(self._counts_h), C.c_size_t(8), C.c_uint(0)) != 0:
-            raise RuntimeError("hipHostMalloc failed")
+        self._out = None
         ms = _vp()
         check("orbmi_matcher_get_stream", lib().orbmi_matcher_get_stream(self.matcher._h, C.byref(ms)))
         self._ms = torch.cuda.ExternalStream(ms.value, device=dev)  # the mapper's search stream
+        # device buffers the chain writes are allocated on the stream that uses them, so the
+        # caching allocator hands a freed block back only in that stream's order
+        with torch.cuda.stream(self._ms):
+            if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
+                self.bow = dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                value=torch.zeros(cap, dtype=torch.float64, device=dev),
+                                node=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
+                                feat=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                counts=torch.zeros(2, dtype=torch.int32, device=dev))
+        self._ms.synchronize()
+        # the BowVector / FeatureVector sizes, copied to pinned host words on the mapper's stream:
+        # hipHostMalloc memory, never a torch pinned tensor (_hip.py: torch would record events on
+        # this library-owned stream when such a tensor is freed, after close() destroyed it)
+        self._counts_h = PinnedWords(2)
         # the whole chain (ComputeBoW, searches, LocalBA) is in order: one stream, so that the
         # process's streams stay within the device's hardware queues (orbmi_ba_set_stream)
         self._one_stream = os.environ.get("ORBMI_LM_STREAMS", "one") == "one"
@@ -450,7 +450,8 @@ class LocalMapper:
         import torch
         b = self._bufs.get(name)
         if b is None or b.numel() < int(np.prod(shape)) or b.dtype != dtype:
-            b = torch.empty(int(np.prod(shape)), dtype=dtype, device=self._dev)
+            with torch.cuda.stream(self._ms):  # allocated on the stream that writes it
+                b = torch.empty(int(np.prod(shape)), dtype=dtype, device=self._dev)
             self._bufs[name] = b
         return b
 
@@ -501,9 +502,8 @@ class LocalMapper:
                                   b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
         if not self._one_stream:  # the transform ran on the vocabulary's own stream
             self.voc.synchronize()
-        if self._hip.hipMemcpyAsync(self._counts_h, _vp(b["counts"].data_ptr()), C.c_size_t(8), C.c_int(2),
-                                    _vp(self._ms.cuda_stream)) != 0:  # mBowVec / mFeatVec sizes, in order
-            raise RuntimeError("hipMemcpyAsync failed")
+        # mBowVec / mFeatVec sizes, behind the transform on the mapper's stream
+        self._counts_h.copy_async(b["counts"].data_ptr(), self._ms.cuda_stream)
         d_obs, d_off, npts = job.obs
         best = self._buf("best", (max(npts, 1),), torch.int32)
         dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
@@ -519,8 +519,7 @@ class LocalMapper:
         bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
-        self.voc.synchronize()
-        nw, nn = (C.c_int * 2).from_address(self._counts_h.value)
+        nw, nn = self._counts_h.read()  # waits for the size copy only (whatever the stream mode)
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
         fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
@@ -583,15 +582,21 @@ class LocalMapper:
             raise self.error
 
     def close(self):
+        """Stop the thread, drain the mapper's stream, settle everything that refers to it (the
+        lazy statistics, the result views, the buffers, the pinned words), then destroy the
+        handles that own the stream.  Nothing used on the stream outlives it."""
         self.q.put(None)
         self.t.join()
+        self._ms.synchronize()
+        if isinstance(self.last_chain, ChainStats):
+            self.last_chain.materialize()  # its closure synchronises self._ms
+        self._out = None
+        self._bufs = {}
+        self._counts_h.close()
         if self._one_stream and self.voc is not None and getattr(self.voc, "_h", None):  # it outlives the mapper
             check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(self.voc._h, None))
         self.ba.close()
         self.matcher.close()
-        if self._counts_h:
-            self._hip.hipHostFree(self._counts_h)
-            self._counts_h = C.c_void_p()
 
 
 def gather_stream_features(dist, desc, kps, count):

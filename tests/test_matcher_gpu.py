@@ -37,6 +37,22 @@ def test_local_search_parity(oracle, M, th, nnratio, dup):
     np.testing.assert_array_equal(m, m_ref)
 
 
+def test_local_search_many_queries(oracle, M):
+    """More than 65,536 map-point queries (k_greedy's non-register path, query indices above 16
+    bits in its round-tagged claims): the local map tiled 12 times, so later copies compete with
+    earlier ones for the same keypoints, index-exact against the sequential replay."""
+    F = make_frame(3)
+    base = local_map((0, 1, 2), seed=21)
+    mps = np.tile(base, 70_000 // len(base) + 1)
+    assert len(mps) > 65_536
+    tr = oracle.is_in_frustum(F, mps, 0.5)
+    occ = np.zeros(len(F.keys), np.uint8)
+    m_ref, n_ref = oracle.search_by_projection_local(F, occ, mps, tr, 1.0, 0.8)
+    m, n = M(0.8).SearchByProjection(F, occ, mps, tr, 1.0)
+    assert n == n_ref and n > 100
+    np.testing.assert_array_equal(m, m_ref)
+
+
 def test_search_local_points_fused(oracle, M):
     F = make_frame(4)
     mps = local_map((1, 2, 3), seed=9)

@@ -135,3 +135,30 @@ def test_native_reset_after_loss_matches_oracle(tmp_path):
     T, _, lost = gpu.frame_poses()
     assert len(T) == 2 and not lost.any()
     gpu.Shutdown()
+
+
+def test_native_reset_while_mapping_concurrently(tmp_path):
+    """Tracking::Reset with the concurrent LocalMapping (csrc/slam.cpp reset(): the queue is
+    cleared, the caller's map lock released while the mapping thread finishes the keyframe in
+    hand, its HBM blocks freed, the lock taken again): frames 0-3 track and queue keyframes, the
+    flat frame 4 is lost with <= 5 keyframes in the map and resets, frames 5-8 initialise again and
+    track; the counts start over and Shutdown joins the mapping thread cleanly."""
+    fr = render_sequence(8)
+    flat = np.full_like(fr[0][0], 128)
+    seq = [f[:2] for f in fr[:4]] + [(flat, flat)] + [f[:2] for f in fr[4:]]
+    s = sequence_settings(tmp_path)
+    slam = NativeStereoSLAM(s, device=0, vocabulary=small_vocabulary(), async_local_mapping=True)
+    for i, (L, R) in enumerate(seq):
+        slam.TrackStereo(L, R, 0.1 * i)
+    slam.WaitLocalMapping()
+    st = slam.stats
+    assert len(st) == len(seq)
+    assert all(x["state"] == OK for x in st[:4]), st[:4]
+    assert st[4]["reset"] == 1 and st[4]["n"] == 0, st[4]
+    assert st[5]["init"] and st[5]["frame"] == 0 and st[5]["keyframes"] == 1, st[5]
+    assert all(x["state"] == OK for x in st[5:]), st[5:]
+    c = slam.counts()
+    assert c["frames"] == 4 and 1 <= c["keyframes"] <= 4 and c["mappoints"] > 100, c
+    T, _, lost = slam.frame_poses()
+    assert len(T) == 4 and not lost.any()
+    slam.Shutdown()
