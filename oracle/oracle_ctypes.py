@@ -459,6 +459,41 @@ def search_for_triangulation(kf1, has_mp1, fv1, kf2, has_mp2, fv2, F12, only_ste
     return out[:len(kf1.keys)], n.value
 
 
+class TriKf(C.Structure):
+    """orc_tri_keyframe (oracle/orb_oracle.h)."""
+    _fields_ = [("tcw", C.c_void_p), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("depth", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("mb", C.c_float), ("level_sigma2", C.c_void_p), ("scale_factors", C.c_void_p)]
+
+
+def tri_keyframe(tcw, keys, u_right, depth, fx, fy, cx, cy, bf, mb, level_sigma2, scale_factors):
+    """An orc_tri_keyframe over numpy arrays (returned with the arrays it points into)."""
+    arrs = [np.ascontiguousarray(tcw, np.float32).reshape(4, 4), np.ascontiguousarray(keys),
+            np.ascontiguousarray(u_right, np.float32), np.ascontiguousarray(depth, np.float32),
+            np.ascontiguousarray(level_sigma2, np.float32), np.ascontiguousarray(scale_factors, np.float32)]
+    k = TriKf(arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data, arrs[3].ctypes.data, fx, fy, cx, cy,
+              bf, mb, arrs[4].ctypes.data, arrs[5].ctypes.data)
+    k._keep = arrs
+    return k
+
+
+def triangulate_matches(kf1, kf2, idx1, idx2):
+    """CreateNewMapPoints' per-match geometry (tri_oracle.cpp, an independent restatement of
+    src/LocalMapping.cc:385-575) -> (ok[n] u8, x3d[n,3] f32, margin[n] f32)."""
+    L = lib()
+    L.orc_triangulate_matches.argtypes = [C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 3
+    i1 = np.ascontiguousarray(idx1, np.int32)
+    i2 = np.ascontiguousarray(idx2, np.int32)
+    n = len(i1)
+    ok = np.zeros(max(n, 1), np.uint8)
+    x = np.zeros((max(n, 1), 3), np.float32)
+    mg = np.zeros(max(n, 1), np.float32)
+    rc = L.orc_triangulate_matches(C.addressof(kf1), C.addressof(kf2), i1.ctypes.data, i2.ctypes.data, n,
+                                   x.ctypes.data, ok.ctypes.data, mg.ctypes.data)
+    assert rc == 0
+    return ok[:n], x[:n], mg[:n]
+
+
 def fuse_search(kf, mps, in_kf=None, th=3.0):
     """ORBmatcher::Fuse search restatement -> (best_idx, best_dist, ncandidates)."""
     L = lib()

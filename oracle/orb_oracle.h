@@ -95,6 +95,24 @@ int orc_stereo(const orc_params* p, const uint8_t* imL, const uint8_t* imR, int 
 float orc_fast_atan2(float y, float x);
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
+/* The KeyFrame members CreateNewMapPoints reads (src/LocalMapping.cc:385-575): Tcw (4x4
+ * row-major), mvKeysUn, mvuRight, mvDepth, fx/fy/cx/cy, mbf, mb, mvLevelSigma2, mvScaleFactors. */
+typedef struct orc_tri_keyframe {
+    const float* tcw;
+    const orc_keypoint* keys_un;
+    const float* u_right;
+    const float* depth;
+    float fx, fy, cx, cy, bf, mb;
+    const float* level_sigma2;
+    const float* scale_factors;
+} orc_tri_keyframe;
+
+/* CreateNewMapPoints' geometry for n matches (idx1[k] of kf1, idx2[k] of kf2), tri_oracle.cpp:
+ * ok[k], x3d[3k..3k+2], and margin[k] (may be NULL) = the smallest relative distance of a
+ * deciding quantity from its threshold on the path taken. */
+int orc_triangulate_matches(const orc_tri_keyframe* kf1, const orc_tri_keyframe* kf2, const int32_t* idx1,
+                            const int32_t* idx2, int n, float* x3d, uint8_t* ok, float* margin);
+
 #ifdef __cplusplus
 }
 #endif

@@ -106,3 +106,76 @@ def test_create_new_map_points_matches_sequential_loop(oracle, host_cos):
         mt.close()
         voc.close()
         S["tr"].close()
+
+
+GEOM_MARGIN = 1e-4   # a decision closer than this (relative) to its threshold may go either way
+X3D_RTOL = 2e-5
+
+
+def test_create_new_map_points_vs_geometry_oracle(oracle):
+    """k_triangulate_par's decisions and new points against the independent C++ geometry oracle
+    (oracle/tri_oracle.cpp: its own restatement of src/LocalMapping.cc:385-575 with a one-sided
+    Jacobi SVD), not against the host compile of the product's tri_geom.h: for every pair's
+    device matches, the accept flags are identical except where the oracle's decision margin is
+    below GEOM_MARGIN, and the accepted points agree within X3D_RTOL of their distance."""
+    import bench
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd._capi import check, lib
+    from orb_slam2_with_comment_amd.matcher import ORBmatcher
+    from orb_slam2_with_comment_amd.types import FeatureVectorView, FrameView, TriKeyFrame
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary, Vocabulary
+    S = bench.setup_track(argparse.Namespace(frames=4, nfeatures=2000), 0, 0)
+    vocab = Vocabulary.synthetic(k=10, L=5, seed=7)
+    voc = ORBVocabulary(vocab, device=0)
+    problem, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
+    jobs, keep = bench.setup_local_mapping(S, voc, vocab, 0, problem)
+    mt = ORBmatcher()
+    names = [f[0] for f in oracle.TriKf._fields_]
+
+    def okf(t):  # the same keyframe data, as the oracle's own struct
+        return oracle.TriKf(*[getattr(t, nm) for nm in names])
+    try:
+        n_acc = n_cmp = n_diff = 0
+        for f in (3, 5):
+            job, h = jobs[f], jobs[f].host
+            kf, nbs = job.kf, job.neighbours
+            n1, npairs = kf.n, len(nbs)
+            kf2 = (FrameView * npairs)(*[nb.view for nb in nbs])
+            tri2 = (TriKeyFrame * npairs)(*[nb.tri for nb in nbs])
+            has2_arr = [np.ascontiguousarray(hn["has_mp"], np.uint8) for hn in h["neighbours"]]
+            has2 = (C.c_void_p * npairs)(*[a.ctypes.data for a in has2_arr])
+            fv2 = (FeatureVectorView * npairs)(*[nb.fv.view() for nb in nbs])
+            fv1 = h["kf"]["fv"].view()
+            has1_in = np.ascontiguousarray(h["kf"]["has_mp"], np.uint8)
+            F12 = np.ascontiguousarray(np.concatenate(job.F12), np.float32)
+            got_m = np.zeros((npairs, n1), np.int32)
+            got_ok = np.zeros((npairs, n1), np.uint8)
+            got_x = np.zeros((npairs, n1, 3), np.float32)
+            check("orbmi_create_new_map_points", lib().orbmi_create_new_map_points(
+                mt._h, C.addressof(kf.view), C.addressof(kf.tri), None, has1_in.ctypes.data, C.addressof(fv1), npairs,
+                kf2, tri2, None, has2, fv2, F12.ctypes.data, got_m.ctypes.data, got_ok.ctypes.data,
+                got_x.ctypes.data))
+            k1 = okf(kf.tri)
+            for j in range(npairs):
+                idx1 = np.nonzero(got_m[j] >= 0)[0].astype(np.int32)
+                if not len(idx1):
+                    continue
+                ok, x, mg = oracle.triangulate_matches(k1, okf(nbs[j].tri), idx1, got_m[j][idx1])
+                dev_ok = got_ok[j][idx1]
+                diff = np.nonzero(dev_ok != ok)[0]
+                assert (mg[diff] < GEOM_MARGIN).all(), \
+                    f"keyframe {f} pair {j}: " + str([(int(idx1[k]), int(dev_ok[k]), float(mg[k])) for k in diff])
+                both = (dev_ok == 1) & (ok == 1)
+                dx = got_x[j][idx1[both]].astype(np.float64) - x[both]
+                scale = np.maximum(1.0, np.linalg.norm(x[both].astype(np.float64), axis=1))
+                rel = np.abs(dx).max(axis=1) / scale if both.any() else np.zeros(0)
+                assert (rel <= X3D_RTOL).all(), f"keyframe {f} pair {j}: max rel {rel.max()}"
+                n_acc += int(both.sum())
+                n_cmp += len(idx1)
+                n_diff += len(diff)
+        print(f"geometry oracle: {n_cmp} matches, {n_acc} accepted by both, {n_diff} margin-level differences")
+        assert n_acc > 50 and n_diff <= 0.01 * n_cmp, (n_acc, n_diff, n_cmp)
+    finally:
+        mt.close()
+        voc.close()
+        S["tr"].close()
