@@ -124,7 +124,9 @@ struct BaDev {
     double* blb[2];
     double* Hpp;               // kBaMaxPoses x 36
     double* bp;                // kBaMaxPoses x 6 (k_ba_schur, read by the solve)
-    double* S;                 // packed upper reduced system (kBaPacked)
+    double* S;                 // reduced system: packed upper (kBaPacked), or in k_ba_solve_mfma's
+                               // tile layout when mfma_T > 0 (mfma_tile_pos)
+    int mfma_T;                // tiles per dimension of the MFMA solve (0: the VALU solves)
     double* bs;                // kBaMaxN
     double* xp;                // kBaMaxN
     double* scal;              // [1] poses' computeScale part, [2] solve ok, [3] lambda used
@@ -280,6 +282,16 @@ __device__ inline double block_max(double v, double* red) {
 }
 
 __device__ inline int packed(int r, int c, int N) { return r * N - r * (r - 1) / 2 + (c - r); }  // r <= c
+
+// position of element (R, C) of the reduced system in the MFMA solve's tile layout (k_ba_schur
+// writes it, k_ba_solve_mfma loads it with one coalesced read per tile register): tile
+// (R >> 4, C >> 4) of the upper triangle numbered row by row with the right-hand side as tile
+// column T (C = 16 T), MFMA C layout inside the tile.  Diagonal tiles hold both triangles.
+__host__ __device__ inline int mfma_tile_pos(int T, int R, int C) {
+    const int i = R >> 4, j = C >> 4, rr = R & 15;
+    return (i * (T + 1) - i * (i - 1) / 2 + (j - i)) * 256 + (rr >> 2) * 64 + 16 * (rr & 3) + (C & 15);
+}
+
 
 __device__ inline bool point_active(const BaDev& a, int p) {
     for (int i = a.pt_start[p]; i < a.pt_start[p + 1]; i++)
@@ -827,6 +839,22 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if ((int)blockIdx.x == a.nblk + a.nf) {  // the MFMA solve's padding: identity rows / columns
+        // beyond N, zero columns 1..15 of the right-hand-side tiles (static within an optimize())
+        const int T = a.mfma_T, NT = T * (T + 3) / 2;
+        for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
+            int t = e >> 8, i = 0;
+            while (t >= T + 1 - i) { t -= T + 1 - i; i++; }
+            const int j = i + t, rr = ((e >> 6) & 3) * 4 + ((e >> 4) & 3), cc = e & 15;
+            const int R = 16 * i + rr, C = 16 * j + cc;
+            if (j == T) {
+                if (cc != 0 || R >= N) a.S[e] = 0.0;
+            } else if (R >= N || C >= N) {
+                a.S[e] = R == C ? 1.0 : 0.0;
+            }
+        }
+        return;
+    }
     if ((int)blockIdx.x >= a.nblk) {  // blocks nblk + r: b_schur of the r-th free keyframe
         const int r = blockIdx.x - a.nblk;
         const int ka = a.blk_kf[2 * (r * a.nf - r * (r - 1) / 2)];
@@ -857,6 +885,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
             for (int w = 0; w < kSchurWaves; w++) t += red[w][threadIdx.x];
             a.bp[6 * i1 + threadIdx.x] = ptot[threadIdx.x];  // the solve's computeScale reads it
             a.bs[6 * i1 + threadIdx.x] = ptot[threadIdx.x] - t;
+            if (a.mfma_T) a.S[mfma_tile_pos(a.mfma_T, 6 * i1 + threadIdx.x, 16 * a.mfma_T)] = ptot[threadIdx.x] - t;
         }
         return;
     }
@@ -907,9 +936,18 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
         double t = 0;
         for (int w = 0; w < kSchurWaves; w++) t += red[w][q];
         const int r = q / 6, c = q % 6;
-        if (!diag) a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
-        else if (c >= r)
+        if (a.mfma_T) {  // the MFMA solve's tiles: diagonal tiles hold both triangles
+            const int R = 6 * i1 + r, Cc = 6 * i2 + c;
+            if (!diag || c >= r) {
+                const double v = diag ? (ptot[packed(r, c, 6)] + (r == c ? lam : 0.0)) - t : -t;
+                a.S[mfma_tile_pos(a.mfma_T, R, Cc)] = v;
+                if ((R >> 4) == (Cc >> 4) && R != Cc) a.S[mfma_tile_pos(a.mfma_T, Cc, R)] = v;
+            }
+        } else if (!diag) {
+            a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
+        } else if (c >= r) {
             a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (ptot[packed(r, c, 6)] + (r == c ? lam : 0.0)) - t;
+        }
     }
 }
 
@@ -1566,6 +1604,279 @@ __global__ __launch_bounds__(kBaSolvePipeThreads) void k_ba_solve_pipe(BaDev a) 
     SOLVE_STAMP_FLUSH();
 }
 
+// ---------------------------------------------------------------- MFMA reduced-system solve
+// The reduced camera system (g2o's BlockSolver::solve -> LinearSolverEigen, SimplicialLDLT:
+// Thirdparty/g2o/g2o/core/block_solver.hpp:354-486, solvers/linear_solver_eigen.h:94-124) as a
+// blocked right-looking LDL^T in 16 x 16 tiles, the tile products on v_mfma_f64_16x16x4f64.
+// N = 6 np unknowns are padded to 16 T (identity rows); the right-hand side rides as tile column
+// T (its column 0).  Every tile (i <= j, upper triangle, and (i, T)) lives in one wave's
+// registers in the MFMA C layout (lane l, register s: row (l >> 4) + 4 s, column l & 15) for the
+// whole solve.  Panel p:
+//   factor  every wave factors the diagonal tile A_pp (staged in LDS) redundantly, one row per
+//           lane (the four 16-lane rows alike): Gaussian elimination on [A_pp | I] with the
+//           pivot row broadcast by DPP row_newbcast gives D_p and E_p = L_pp^-1 (no sync);
+//   row     owners of (p, j > p): W^T_jp = E_p A_pj (4 MFMAs; a C-layout tile is exactly the
+//           B operand), L^T_jp = D_p^-1 W^T_jp, both to LDS;
+//   update  owners of (i, j), p < i <= j: A_ij -= (L^T_ip)^T W^T_jp (4 MFMAs; both operands are
+//           C-layout tiles read lane for lane), the next diagonal tile to LDS.
+// Three barriers per panel.  Then one wave back-substitutes L^T x = D^-1 E b with the stored
+// L^T_jp and E_p.  Same solution as the LDL^T of the reference up to the rounding order.
+using double4_t = __attribute__((ext_vector_type(4))) double;
+constexpr int kBaMfmaWaves = 4;
+constexpr int kBaMfmaThreads = 64 * kBaMfmaWaves;
+constexpr int kBaSolveMfmaMaxPoses = 21;  // 126 unknowns in 8 tiles
+
+template <int J>
+__device__ inline double bcast16(double v) {  // lane J of this lane's row of 16 (DPP64 row_newbcast)
+    const long long x = __double_as_longlong(v);
+    return __longlong_as_double(__builtin_amdgcn_update_dpp(0ll, x, 0x150 + J, 0xF, 0xF, false));
+}
+
+// fused broadcast multiply-add, v_fmac_f64 with a DPP64 row_newbcast source (one instruction):
+//   fmac_self<J>(acc, m)   acc += m * acc[lane J of the row]
+//   fmac_bc<J>(acc, s, m)  acc += s[lane J of the row] * m
+// Callers keep every lane active and issue `s_nop 1` between a VALU write of the broadcast
+// register and its first DPP read (the DPP read-after-write hazard; hipcc pads nothing in asm).
+template <int J> __device__ inline void fmac_self(double& acc, double m);
+template <int J> __device__ inline void fmac_bc(double& acc, double s, double m);
+#define ORBMI_FMAC_DPP(J)                                                                                        \
+    template <> __device__ inline void fmac_self<J>(double& acc, double m) {                                     \
+        asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(m)); \
+    }                                                                                                            \
+    template <> __device__ inline void fmac_bc<J>(double& acc, double s, double m) {                             \
+        asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                   \
+                     : "+v"(acc) : "v"(s), "v"(m));                                                              \
+    }
+ORBMI_FMAC_DPP(0) ORBMI_FMAC_DPP(1) ORBMI_FMAC_DPP(2) ORBMI_FMAC_DPP(3) ORBMI_FMAC_DPP(4) ORBMI_FMAC_DPP(5)
+ORBMI_FMAC_DPP(6) ORBMI_FMAC_DPP(7) ORBMI_FMAC_DPP(8) ORBMI_FMAC_DPP(9) ORBMI_FMAC_DPP(10) ORBMI_FMAC_DPP(11)
+ORBMI_FMAC_DPP(12) ORBMI_FMAC_DPP(13) ORBMI_FMAC_DPP(14) ORBMI_FMAC_DPP(15)
+#undef ORBMI_FMAC_DPP
+
+// elimination step J of [A | E] (row r of the tile per lane): rows r > J subtract l_rJ times
+// pivot row J (A[J + 1 ..] and E[.. J - 1] of lane J, by DPP broadcast inside the fused FMA);
+// E becomes L^-1 (unit lower); inv[J] = 1 / d_J (the same in every lane)
+template <int J>
+__device__ inline void ldl16_step(double (&A)[16], double (&E)[16], double (&inv)[16], int r) {
+    if constexpr (J < 16) {
+        const double d = bcast16<J>(A[J]);
+        inv[J] = rcp_f64(d);
+        const double nl = r > J ? -(A[J] * inv[J]) : 0.0;
+        asm volatile("s_nop 1");
+#pragma unroll
+        for (int k = J + 1; k < 16; k++) fmac_self<J>(A[k], nl);
+#pragma unroll
+        for (int k = 0; k < J; k++) fmac_self<J>(E[k], nl);
+        E[J] += nl;
+        ldl16_step<J + 1>(A, E, inv, r);
+    }
+}
+
+// x += sum_t M[t][c] v_t, c = this lane's column, v_t in lane t of the row (16 fused FMAs)
+template <int J>
+__device__ inline void gemv16_bc(double& x, double v, const double* __restrict__ Mcol) {
+    if constexpr (J < 16) {
+        fmac_bc<J>(x, v, Mcol[16 * J]);
+        gemv16_bc<J + 1>(x, v, Mcol);
+    }
+}
+
+// tiles of the T x T upper triangle plus the right-hand-side column, row-major: t -> (i, j)
+template <int T>
+__device__ inline void mfma_tile_ij(int t, int& i, int& j) {
+    i = 0;
+    while (t >= T + 1 - i) { t -= T + 1 - i; i++; }
+    j = i + t;
+}
+
+template <int T>
+__global__ __launch_bounds__(kBaMfmaThreads) void k_ba_solve_mfma(BaDev a) {
+    const BaCtl& ctl = *a.ctl;
+    if (ctl.done || ctl.gen != a.run_gen) return;
+    constexpr int NT = T * (T + 3) / 2;                       // upper tiles + right-hand side tiles
+    constexpr int K = (NT + kBaMfmaWaves - 1) / kBaMfmaWaves;  // tile slots per wave
+    constexpr int NL = T * (T - 1) / 2;                       // L^T_jp tiles, p < j < T
+    const int np = ctl.np, N = 6 * np;
+    const double lam = a.scal[3];
+    const double* __restrict__ Tc = a.Tb[ctl.cur];
+    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    __shared__ double dg[16 * 17];                 // the diagonal tile of the next panel (row-major)
+    __shared__ double Ew[kBaMfmaWaves][16 * 17];   // per wave: E_p rows (MFMA A operands from here)
+    __shared__ double dvw[kBaMfmaWaves][16];       // per wave: 1 / d of the panel's rows
+    __shared__ double Eall[T][256];                // E_p for the back substitution (row-major)
+    __shared__ double Wt[T + 1][4][64];            // -W^T_jp of the current panel (C layout)
+    __shared__ double Lt[NL > 0 ? NL : 1][4][64];  // L^T_jp (C layout: row t contiguous at [t >> 2][16 (t & 3)])
+    __shared__ double ys[16 * T], xs[16 * T];
+    __shared__ int fail;
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, n = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    SOLVE_STAMP_DECL;
+    SOLVE_STAMP(tid == 0, 250);
+    auto lt_index = [](int p, int j) { return p * (2 * T - p - 1) / 2 + (j - p - 1); };  // p < j < T
+    // ---- load the tiles (k_ba_schur's tile layout, padding included): consumed lazily, so the
+    // loads of the later tiles overlap the first panel's factorisation
+    double4_t C[K];
+    int ti[K], tj[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int t = w + kBaMfmaWaves * k;
+        ti[k] = tj[k] = -1;
+        if (t < NT) mfma_tile_ij<T>(t, ti[k], tj[k]);
+        const double* src = a.S + (size_t)(t < NT ? t : 0) * 256 + lane;  // padding written by k_ba_schur
+#pragma unroll
+        for (int s = 0; s < 4; s++) C[k][s] = src[64 * s];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        if (ti[k] == 0 && tj[k] == 0)
+#pragma unroll
+            for (int s = 0; s < 4; s++) dg[(q + 4 * s) * 17 + n] = C[k][s];
+    if (tid == 0) fail = 0;
+    SOLVE_STAMP(tid == 0, 251);
+    for (int p = 0; p < T; p++) {
+        __syncthreads();  // dg = A_pp after its last update
+        SOLVE_STAMP(tid == 0, 8 * p);
+        // ---- factor A_pp (every wave, one row per lane)
+        {
+            double A[16], E[16], inv[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                A[k] = dg[n * 17 + k];
+                E[k] = k == n ? 1.0 : 0.0;
+            }
+            ldl16_step<0>(A, E, inv, n);
+            if (lane < 16) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) Ew[w][n * 17 + k] = E[k];
+                if (w == 0) {
+#pragma unroll
+                    for (int k = 0; k < 16; k++) Eall[p][n * 16 + k] = E[k];
+                }
+            }
+            if (lane == 0) {
+                bool bad = false;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    dvw[w][k] = inv[k];
+                    bad |= !isfinite(inv[k]) || inv[k] == 0.0;  // d zero, inf or NaN
+                }
+                if (bad && w == 0) fail = 1;
+            }
+        }
+        SOLVE_STAMP(tid == 0, 8 * p + 1);
+        wave_sync_lds();
+        double e[4], dv[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            e[s] = Ew[w][n * 17 + 4 * s + q];  // A operand: E[n][4 s + q]
+            dv[s] = dvw[w][q + 4 * s];         // 1 / d of C-layout row q + 4 s
+        }
+        // ---- row panel: W^T_jp = E_p A_pj, L^T_jp = D^-1 W^T_jp
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (ti[k] == p && tj[k] > p) {
+                double4_t z = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s = 0; s < 4; s++) z = __builtin_amdgcn_mfma_f64_16x16x4f64(e[s], C[k][s], z, 0, 0, 0);
+                const int j = tj[k];
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    Wt[j][s][lane] = -z[s];
+                    const double lt = z[s] * dv[s];
+                    if (j < T) Lt[lt_index(p, j)][s][lane] = lt;
+                    else if (n == 0) ys[16 * p + q + 4 * s] = lt;  // y_p = D^-1 E b_p
+                }
+            }
+        }
+        SOLVE_STAMP(tid == 0, 8 * p + 2);
+        if (p == T - 1) break;
+        __syncthreads();
+        SOLVE_STAMP(tid == 0, 8 * p + 3);
+        // ---- trailing update A_ij -= (L^T_ip)^T W^T_jp, p < i <= j
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (ti[k] > p) {
+                const double* lp = &Lt[lt_index(p, ti[k])][0][lane];
+                const double* wp = &Wt[tj[k]][0][lane];
+                double lo[4], wo[4];
+#pragma unroll
+                for (int s = 0; s < 4; s++) { lo[s] = lp[64 * s]; wo[s] = wp[64 * s]; }
+#pragma unroll
+                for (int s = 0; s < 4; s++) C[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(lo[s], wo[s], C[k], 0, 0, 0);
+                if (ti[k] == p + 1 && tj[k] == p + 1)
+#pragma unroll
+                    for (int s = 0; s < 4; s++) dg[(q + 4 * s) * 17 + n] = C[k][s];
+            }
+        }
+        SOLVE_STAMP(tid == 0, 8 * p + 4);
+    }
+    __syncthreads();
+    SOLVE_STAMP(tid == 0, 252);
+    if (fail) {  // pop: trial poses = current ones, computeScale = 0
+        for (int k = tid; k < a.nkf; k += blockDim.x)
+            for (int qq = 0; qq < 8; qq++) Tt[8 * k + qq] = Tc[8 * k + qq];
+        if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
+        return;
+    }
+    if (w != 0) return;
+    // ---- back substitution (one wave, x in registers): x_p = E_p^T (y_p - sum_{j > p} L^T_jp x_j).
+    // Lane (g, t), g = lane >> 4: the copies xr[j] are rotated by 4 g (lane (g, c) holds
+    // x_j[(c + 4 g) & 15]), so group g covers columns 4 g .. 4 g + 3 of every tile with four fused
+    // DPP FMAs reading x from lanes 0..3 of its row; the four groups' partial sums meet by permlane
+    // swaps.  x_p itself comes out rotated: lane (g, c) forms column (c + 4 g) & 15 of E_p^T r.
+    {
+        const int g = q, t = n, rot = (n + 4 * g) & 15;
+        double xr[T];
+#pragma unroll
+        for (int p = T - 1; p >= 0; p--) {
+            double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+            for (int j = p + 1; j < T; j++) {
+                const double* row = &Lt[lt_index(p, j)][t >> 2][16 * (t & 3) + 4 * g];
+                double& acc = ((j - p) & 1) ? acc0 : acc1;
+                const double l0 = row[0], l1 = row[1], l2 = row[2], l3 = row[3];
+                fmac_bc<0>(acc, xr[j], l0);
+                fmac_bc<1>(acc, xr[j], l1);
+                fmac_bc<2>(acc, xr[j], l2);
+                fmac_bc<3>(acc, xr[j], l3);
+            }
+            double acc = acc0 + acc1;
+            acc = swap_combine<16>(acc, acc);
+            acc = swap_combine<32>(acc, acc);
+            const double r = ys[16 * p + t] - acc;
+            double x = 0.0;
+            asm volatile("s_nop 1");
+            gemv16_bc<0>(x, r, &Eall[p][rot]);  // column rot of E_p: sum_t E[t][rot] r_t
+            asm volatile("s_nop 1");
+            xr[p] = x;
+            if (lane < 16) xs[16 * p + t] = x;  // group 0: unrotated
+        }
+        wave_sync_lds();
+    }
+    SOLVE_STAMP(lane == 0, 254);
+    for (int qq = lane; qq < N; qq += 64) a.xp[qq] = xs[qq];
+    for (int k = lane; k < a.nkf; k += 64) {
+        const int pi = a.pose_idx[k];
+        if (pi >= 0) {
+            double u[6];
+#pragma unroll
+            for (int qq = 0; qq < 6; qq++) u[qq] = xs[6 * pi + qq];
+            se3_oplus(u, Tc + 8 * k, Tt + 8 * k);
+        } else {
+            for (int qq = 0; qq < 8; qq++) Tt[8 * k + qq] = Tc[8 * k + qq];
+        }
+    }
+    double sc = 0;
+    for (int qq = lane; qq < N; qq += 64) sc += xs[qq] * (lam * xs[qq] + a.bp[qq]);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+        a.scal[1] = sc;
+        a.scal[2] = 1;
+        a.istat[3] = 1;
+    }
+    SOLVE_STAMP(lane == 0, 253);
+    SOLVE_STAMP_FLUSH();
+}
+
 // ---------------------------------------------------------------- Levenberg control
 // fixed-order sum of n partials by one wave (lane l: l, l + 64, ...; then a fixed xor tree,
 // lane 0's value broadcast): deterministic run to run
@@ -1875,6 +2186,18 @@ struct Runner {
     bool solve_rows;  // nf <= kBaSolveRowsMaxPoses: k_ba_solve_rows, else k_ba_solve<1>
     bool solve_pipe;  // k_ba_solve_pipe (a dedicated pivot wave) in place of k_ba_solve_rows
                       // (ORBMI_BA_SOLVE=rows selects the latter, for A/B runs)
+    int mfma_tiles;   // > 0: k_ba_solve_mfma<mfma_tiles> (nf <= kBaSolveMfmaMaxPoses, ORBMI_BA_SOLVE=mfma)
+
+    void launch_mfma() {
+        switch (mfma_tiles) {
+#define ORBMI_MFMA_CASE(T_) \
+    case T_: hipLaunchKernelGGL(k_ba_solve_mfma<T_>, dim3(1), dim3(kBaMfmaThreads), 0, h.stream, a); break;
+            ORBMI_MFMA_CASE(1) ORBMI_MFMA_CASE(2) ORBMI_MFMA_CASE(3) ORBMI_MFMA_CASE(4)
+            ORBMI_MFMA_CASE(5) ORBMI_MFMA_CASE(6) ORBMI_MFMA_CASE(7) ORBMI_MFMA_CASE(8)
+#undef ORBMI_MFMA_CASE
+            default: break;
+        }
+    }
 
     bool stopped() const { return stop_set(stop); }
 
@@ -1905,8 +2228,11 @@ struct Runner {
     // when that optimize() is done or not the current one
     void step(int gen) {
         a.run_gen = gen;
-        if (a.nblk > 0) hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf), dim3(kSchurThreads), 0, h.stream, a);
-        if (solve_rows && solve_pipe)
+        if (a.nblk > 0)  // (+ the MFMA solve's padding block)
+            hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf + (a.mfma_T > 0)), dim3(kSchurThreads), 0, h.stream, a);
+        if (mfma_tiles > 0)
+            launch_mfma();
+        else if (solve_rows && solve_pipe)
             hipLaunchKernelGGL(k_ba_solve_pipe, dim3(1), dim3(kBaSolvePipeThreads), 0, h.stream, a);
         else if (solve_rows) hipLaunchKernelGGL(k_ba_solve_rows, dim3(1), dim3(kBaSolveRowsThreads), 0, h.stream, a);
         else hipLaunchKernelGGL(k_ba_solve<1>, dim3(1), dim3(kBaSolveThreads), 0, h.stream, a);
@@ -2159,7 +2485,9 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
     a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
     const char* sv = getenv("ORBMI_BA_SOLVE");
-    Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses, !(sv && !strcmp(sv, "rows"))};
+    const bool mfma_solve = sv && !strcmp(sv, "mfma");  // (A/B: the VALU pivot-wave solve is the default)
+    a.mfma_T = (mfma_solve && nf <= kBaSolveMfmaMaxPoses) ? std::max(1, (6 * nf + 15) / 16) : 0;
+    Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses, !(sv && !strcmp(sv, "rows")), a.mfma_T};
     unsigned char* out_erase = B + o_oerase;
     const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
     hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);

@@ -46,6 +46,16 @@ def test_lba_parity(oracle, BA, seed, free, fixed, npts):
     _compare(BA.run(prob), ref, prob)
 
 
+@pytest.mark.parametrize("seed,free,fixed,npts", [(3, 6, 2, 300), (42, 20, 4, 3000), (7, 10, 0, 800),
+                                                 (11, 21, 3, 1500), (13, 2, 1, 200), (17, 3, 0, 250)])
+def test_lba_parity_mfma_solve(oracle, BA, monkeypatch, seed, free, fixed, npts):
+    """The reduced system solved by the blocked LDL^T on MFMA (k_ba_solve_mfma<T>, tiles of
+    16: 1 to 8 tiles across these sizes, padded last tiles included), same bars."""
+    monkeypatch.setenv("ORBMI_BA_SOLVE", "mfma")
+    prob, _ = SM.local_ba_problem(seed=seed, n_free=free, n_fixed=fixed, n_points=npts)
+    _compare(BA.run(prob), oracle.local_ba(prob, edge_chi2=True), prob)
+
+
 def test_lba_resume_after_rejections(oracle, BA, monkeypatch):
     """The call is enqueued at once with a few spare trials per optimize(); with none
     (ORBMI_BA_SLACK=0) every rejected trial leaves an optimize() short of trials, the gated

@@ -149,6 +149,30 @@ for step in "$@"; do
                     echo "$n $(tail -1 $OUT/ablba_${n}_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')" | tee -a $OUT/ablba.txt
                 done
             done;;
+        mfmatrace|mfmatrace=*)
+            # per-panel split of the MFMA reduced-system solve (tools/ubench/mfma_solve_trace, built
+            # beforehand) and the VALU pivot-wave solve on the same system
+            np_=${step#mfmatrace}; np_=${np_#=}; np_=${np_:-20}
+            run mfmatrace$np_ 60 ./tools/ubench/mfma_solve_trace $np_; cat $OUT/mfmatrace$np_.log
+            PIPE=1 run mfmatrace_pipe$np_ 60 ./tools/ubench/mfma_solve_trace $np_; cat $OUT/mfmatrace_pipe$np_.log
+            cat $OUT/mfmatrace$np_.log $OUT/mfmatrace_pipe$np_.log > $P/mfma_solve_trace_np$np_.txt;;
+        ubench=*)
+            # a microbenchmark binary under tools/ubench (built beforehand)
+            b=${step#ubench=}
+            run ubench_$b 60 ./tools/ubench/$b; cat $OUT/ubench_$b.log; cp $OUT/ubench_$b.log $P/;;
+        lbasolve)
+            # config 3 with the MFMA reduced-system solve vs the VALU pivot-wave solve
+            for i in 1 2 3; do
+                ORBMI_BA_SOLVE=mfma run lbasolve_mfma_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
+                ORBMI_BA_SOLVE=pipe run lbasolve_pipe_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
+                echo "mfma $(tail -1 $OUT/lbasolve_mfma_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')  pipe $(tail -1 $OUT/lbasolve_pipe_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')" | tee -a $OUT/lbasolve.txt
+            done; cp $OUT/lbasolve.txt $P/;;
+        mfmapmc|mfmapmc_*)
+            # MFMA issue / busy counters per kernel over a short bench run (one pass)
+            m=${step#mfmapmc}; m=${m#_}; m=${m:-lba}
+            run mfmapmc_$m 150 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS --kernel-trace -f csv -d $OUT/mfmapmc_$m -o mp -- python3 bench.py $(modeargs $m) --steps 10 --warmup 2 --no-cpu-baseline
+            f=$(find $OUT/mfmapmc_$m -name "*counter_collection.csv" | head -1); cp $f $P/mfma_pmc_$m.csv
+            python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[(r['Kernel_Name'][:48],r['Counter_Name'])].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1]))]; [print(k, len(v), sum(v)/len(v)) for k,v in sorted(d.items()) if 'ba_' in k[0]]" $f | tee $P/mfma_pmc_$m.txt;;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
