@@ -68,6 +68,7 @@ struct BaCtl {
     int steps;        // trial steps executed (diagnostics)
     int lin;          // which of the two linear-system buffers holds the current system
     unsigned arrive;  // blocks of k_ba_update_errors finished (the last one runs the control)
+    unsigned arrive_s;  // blocks of k_ba_schur_solve finished (the last one solves)
     unsigned arrive_e;  // blocks of k_ba_activate_edges / k_ba_errors finished (the last one
                         // runs the one-wave tail: the LM state set-up / activeRobustChi2)
     double lambda, ni, currentChi, iniChi;
@@ -799,7 +800,7 @@ __device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
+__device__ inline void schur_body(BaDev a) {
     // the block's pair structure (static within an optimize()) is loaded before the LM state, so
     // that its two dependent loads overlap the control block's instead of following it
     const int b = blockIdx.x;
@@ -951,6 +952,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) {
     }
 }
 
+__global__ __launch_bounds__(kSchurThreads) void k_ba_schur(BaDev a) { schur_body(a); }
+
 // ---------------------------------------------------------------- reduced system solve
 // Block Gauss-Jordan on the LDL^T = U^T D U factorisation of the reduced camera system,
 // blocked by the 6x6 pose blocks and held in registers: TPT threads own tile (i, j), i <= j, of
@@ -978,10 +981,17 @@ __device__ unsigned long long g_solve_trace[256];
         if (threadIdx.x == 0)                                                                \
             for (int i_ = 0; i_ < 256; i_++) g_solve_trace[i_] = tstamp[i_];                 \
     } while (0)
+#define SOLVE_STAMP_TO(ts, cond, i)                                                          \
+    do {                                                                                     \
+        if (cond) (ts)[i] = __builtin_amdgcn_s_memtime();                                    \
+    } while (0)
+#define SOLVE_STAMP_PTR tstamp
 #else
 #define SOLVE_STAMP_DECL
 #define SOLVE_STAMP(cond, i) do {} while (0)
 #define SOLVE_STAMP_FLUSH() do {} while (0)
+#define SOLVE_STAMP_TO(ts, cond, i) do {} while (0)
+#define SOLVE_STAMP_PTR nullptr
 #endif
 
 __device__ inline void wave_sync_lds() {
@@ -1622,8 +1632,7 @@ __global__ __launch_bounds__(kBaSolvePipeThreads) void k_ba_solve_pipe(BaDev a) 
 // Three barriers per panel.  Then one wave back-substitutes L^T x = D^-1 E b with the stored
 // L^T_jp and E_p.  Same solution as the LDL^T of the reference up to the rounding order.
 using double4_t = __attribute__((ext_vector_type(4))) double;
-constexpr int kBaMfmaWaves = 4;
-constexpr int kBaMfmaThreads = 64 * kBaMfmaWaves;
+constexpr int kBaMfmaThreads = 256;  // one wave per SIMD: critical tiles, two bulk waves, factor
 constexpr int kBaSolveMfmaMaxPoses = 21;  // 126 unknowns in 8 tiles
 
 template <int J>
@@ -1652,221 +1661,362 @@ ORBMI_FMAC_DPP(6) ORBMI_FMAC_DPP(7) ORBMI_FMAC_DPP(8) ORBMI_FMAC_DPP(9) ORBMI_FM
 ORBMI_FMAC_DPP(12) ORBMI_FMAC_DPP(13) ORBMI_FMAC_DPP(14) ORBMI_FMAC_DPP(15)
 #undef ORBMI_FMAC_DPP
 
-// elimination step J of [A | E] (row r of the tile per lane): rows r > J subtract l_rJ times
-// pivot row J (A[J + 1 ..] and E[.. J - 1] of lane J, by DPP broadcast inside the fused FMA);
-// E becomes L^-1 (unit lower); inv[J] = 1 / d_J (the same in every lane)
+// 1 / d: v_rcp_f64 (2^-24.4 relative, tools/ubench/dpp64.hip) and one Newton step (2^-48)
+__device__ inline double rcp1_f64(double d) {
+    const double r = __builtin_amdgcn_rcp(d);
+    return fma(r, fma(-d, r, 1.0), r);
+}
+
+// item I of elimination step J's bulk FMAs: A[J + 2 ..] then E[.. J - 1] (14 items for J < 15)
+template <int J, int I0, int I1>
+__device__ inline void ldl_bulk(double (&A)[16], double (&E)[16], double nl) {
+    if constexpr (I0 < I1) {
+        constexpr int NA = 14 - J;
+        if constexpr (I0 < NA) fmac_self<J>(A[J + 2 + I0], nl);
+        else if constexpr (I0 - NA < J) fmac_self<J>(E[I0 - NA], nl);
+        ldl_bulk<J, I0 + 1, I1>(A, E, nl);
+    }
+}
+
+// elimination step J of [A | E] (row r of the tile per lane), software-pipelined: nl = -l_rJ
+// (0 for rows r <= J) comes from the previous step.  Rows r > J subtract l_rJ times pivot row J
+// (A[J + 1 ..] and E[.. J - 1] of lane J, broadcast inside the fused FMAs).  The next pivot
+// column A[J + 1] goes first; step J + 1's pivot broadcast, reciprocal and multiplier (a chain
+// of dependent instructions) are interleaved with this step's other FMAs in program order, so
+// the in-order issue hides their latencies.  E ends as L^-1 (unit lower); inv[J] = 1 / d_J.
 template <int J>
-__device__ inline void ldl16_step(double (&A)[16], double (&E)[16], double (&inv)[16], int r) {
-    if constexpr (J < 16) {
-        const double d = bcast16<J>(A[J]);
-        inv[J] = rcp_f64(d);
-        const double nl = r > J ? -(A[J] * inv[J]) : 0.0;
+__device__ inline void ldl16_step(double (&A)[16], double (&E)[16], double (&inv)[16], int r, double nl) {
+    if constexpr (J < 15) {
+        asm volatile("s_nop 1");
+        fmac_self<J>(A[J + 1], nl);
+        asm volatile("s_nop 1");  // the asm's VGPR write before the DPP read below
+        const double d = bcast16<J + 1>(A[J + 1]);
+        ldl_bulk<J, 0, 3>(A, E, nl);
+        const double r0 = __builtin_amdgcn_rcp(d);
+        ldl_bulk<J, 3, 7>(A, E, nl);
+        const double e1 = fma(-d, r0, 1.0);
+        ldl_bulk<J, 7, 9>(A, E, nl);
+        const double r1 = fma(r0, e1, r0);
+        inv[J + 1] = r1;
+        ldl_bulk<J, 9, 11>(A, E, nl);
+        const double m = A[J + 1] * r1;
+        ldl_bulk<J, 11, 13>(A, E, nl);
+        const double nl_next = r > J + 1 ? -m : 0.0;
+        ldl_bulk<J, 13, 14>(A, E, nl);
+        E[J] += nl;
+        ldl16_step<J + 1>(A, E, inv, r, nl_next);
+    } else {  // J == 15: only E[0 .. 14] and E[15]
         asm volatile("s_nop 1");
 #pragma unroll
-        for (int k = J + 1; k < 16; k++) fmac_self<J>(A[k], nl);
+        for (int k = 0; k < 15; k++) fmac_self<15>(E[k], nl);
+        E[15] += nl;
+    }
+}
+
+__device__ inline void ldl16(double (&A)[16], double (&E)[16], double (&inv)[16], int r) {
+    inv[0] = rcp1_f64(bcast16<0>(A[0]));
+    const double nl0 = r > 0 ? -(A[0] * inv[0]) : 0.0;
+    ldl16_step<0>(A, E, inv, r, nl0);
+}
+
+// LDS flag hand-offs between the waves of one workgroup (release after the data, acquire after
+// the flag)
+__device__ inline void lds_publish(int* f, int v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    *(volatile int*)f = v;
+}
+__device__ inline void lds_wait_ge(const int* f, int v) {
+    while (*(const volatile int*)f < v) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// tile (i, j) of the upper triangle plus the right-hand-side column (j == T), row-major numbering
+template <int T>
+__host__ __device__ constexpr int mfma_tile_index(int i, int j) { return i * (T + 1) - i * (i - 1) / 2 + (j - i); }
+// the m-th tile (i, j) with j >= i + 2 (the bulk waves' tiles), row-major
+template <int T>
+__host__ __device__ constexpr int mfma_bulk_i(int m) {
+    for (int i = 0; i < T; i++) {
+        if (m < T - i - 1) return i;
+        m -= T - i - 1;
+    }
+    return -1;
+}
+template <int T>
+__host__ __device__ constexpr int mfma_bulk_j(int m) {
+    for (int i = 0; i < T; i++) {
+        if (m < T - i - 1) return i + 2 + m;
+        m -= T - i - 1;
+    }
+    return -1;
+}
+
+template <int T>
+struct MfmaSolveLds {
+    static constexpr int NL = T * (T - 1) / 2;  // L^T_jp tiles, p < j < T
+    double dg[16 * 17];                  // the next panel's diagonal tile (row-major)
+    double Es[2][16 * 17];               // E_p rows, buffer p & 1 (the MFMA A operands are read here)
+    double dvs[2][16];                   // 1 / d of the panel's rows
+    double Eall[T][256];                 // E_p for the back substitution (row-major)
+    double Wt[2][T + 1][4][64];          // -W^T_jp, buffer p & 1 (C layout)
+    double Lt[NL > 0 ? NL : 1][4][64];   // L^T_jp (C layout: row t contiguous at [t >> 2][16 (t & 3)])
+    double ys[16 * T], xs[16 * T];
+    int flag_dg, flag_e, row_cnt[T], fail;
+    __device__ static int lt_index(int p, int j) { return p * (2 * T - p - 1) / 2 + (j - p - 1); }
+};
+
+constexpr int kMfmaBulkWaves = 2;  // waves 1, 2; wave 0 = critical tiles, wave 3 = factor
+
+// row panel product of one tile X = A_pj (C layout, registers) with E_p: z = W^T_jp = E_p X;
+// -W^T to LDS, L^T = D^-1 W^T to LDS (or y_p = D^-1 E_p b_p for the right-hand side); returns z
+template <int T>
+__device__ inline double4_t mfma_row_tile(MfmaSolveLds<T>& L, int p, int j, const double4_t& X, const double (&e)[4],
+                                          const double (&dv)[4], int lane) {
+    double4_t z = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < J; k++) fmac_self<J>(E[k], nl);
-        E[J] += nl;
-        ldl16_step<J + 1>(A, E, inv, r);
+    for (int s = 0; s < 4; s++) z = __builtin_amdgcn_mfma_f64_16x16x4f64(e[s], X[s], z, 0, 0, 0);
+    const int q = lane >> 4, n = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        L.Wt[p & 1][j][s][lane] = -z[s];
+        const double lt = z[s] * dv[s];
+        if (j < T) L.Lt[MfmaSolveLds<T>::lt_index(p, j)][s][lane] = lt;
+        else if (n == 0) L.ys[16 * p + q + 4 * s] = lt;
+    }
+    return z;
+}
+
+// trailing update of tile (i, j) by panel p: X -= (L^T_ip)^T W^T_jp, both operands from LDS
+template <int T>
+__device__ inline void mfma_update_tile(MfmaSolveLds<T>& L, int p, int i, int j, double4_t& X, int lane) {
+    const double* lp = &L.Lt[MfmaSolveLds<T>::lt_index(p, i)][0][lane];
+    const double* wp = &L.Wt[p & 1][j][0][lane];
+    double lo[4], wo[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) { lo[s] = lp[64 * s]; wo[s] = wp[64 * s]; }
+#pragma unroll
+    for (int s = 0; s < 4; s++) X = __builtin_amdgcn_mfma_f64_16x16x4f64(lo[s], wo[s], X, 0, 0, 0);
+}
+
+template <int T>
+__device__ inline void mfma_load_tile(const BaDev& a, int i, int j, double4_t& X, int lane) {
+    const double* src = a.S + (size_t)mfma_tile_index<T>(i, j) * 256 + lane;  // padding written by k_ba_schur
+#pragma unroll
+    for (int s = 0; s < 4; s++) X[s] = src[64 * s];
+}
+
+template <int T>
+__device__ inline void mfma_operands(const MfmaSolveLds<T>& L, int p, int lane, double (&e)[4], double (&dv)[4]) {
+    const int q = lane >> 4, n = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        e[s] = L.Es[p & 1][n * 17 + 4 * s + q];  // A operand: E[n][4 s + q]
+        dv[s] = L.dvs[p & 1][q + 4 * s];         // 1 / d of C-layout row q + 4 s
     }
 }
 
-// x += sum_t M[t][c] v_t, c = this lane's column, v_t in lane t of the row (16 fused FMAs)
-template <int J>
-__device__ inline void gemv16_bc(double& x, double v, const double* __restrict__ Mcol) {
-    if constexpr (J < 16) {
-        fmac_bc<J>(x, v, Mcol[16 * J]);
-        gemv16_bc<J + 1>(x, v, Mcol);
+template <int T>
+__device__ inline void mfma_put_dg(MfmaSolveLds<T>& L, const double4_t& X, int lane) {
+    const int q = lane >> 4, n = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 4; s++) L.dg[(q + 4 * s) * 17 + n] = X[s];
+}
+
+// wave 0: the critical tiles, diagonal (i, i) and first off-diagonal (i, i + 1) (the last one the
+// right-hand side's).  Per panel: as soon as E_p is published, row tile (p, p + 1), then the next
+// diagonal tile's update from registers and its hand-off to the factor wave; then the bulk of its
+// updates of this panel
+template <int T>
+__device__ inline void mfma_critical_wave(const BaDev& a, MfmaSolveLds<T>& L, int lane,
+                                          unsigned long long* ts) {
+    double4_t D[T], F1[T];
+#pragma unroll
+    for (int i = 0; i < T; i++) {
+        mfma_load_tile<T>(a, i, i, D[i], lane);
+        mfma_load_tile<T>(a, i, i + 1, F1[i], lane);
+    }
+    mfma_put_dg<T>(L, D[0], lane);
+    if (lane == 0) lds_publish(&L.flag_dg, 0);
+    SOLVE_STAMP_TO(ts, lane == 0, 251);
+#pragma unroll
+    for (int p = 0; p < T; p++) {
+        lds_wait_ge(&L.flag_e, p);
+        SOLVE_STAMP_TO(ts, lane == 0, 8 * p + 2);
+        double e[4], dv[4];
+        mfma_operands<T>(L, p, lane, e, dv);
+        const double4_t z = mfma_row_tile<T>(L, p, p + 1, F1[p], e, dv, lane);
+        if (p == T - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) atomicAdd(&L.row_cnt[p], 1);
+            break;
+        }
+        // A_{p+1,p+1} -= (L^T)^T W^T with this tile's L^T = D^-1 z and W^T = z, in registers
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            D[p + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(z[s] * dv[s], -z[s], D[p + 1], 0, 0, 0);
+        mfma_put_dg<T>(L, D[p + 1], lane);
+        if (lane == 0) lds_publish(&L.flag_dg, p + 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) atomicAdd(&L.row_cnt[p], 1);
+        SOLVE_STAMP_TO(ts, lane == 0, 8 * p + 3);
+        lds_wait_ge(&L.row_cnt[p], 1 + kMfmaBulkWaves);
+        SOLVE_STAMP_TO(ts, lane == 0, 8 * p + 4);
+#pragma unroll
+        for (int i = p + 1; i < T; i++) mfma_update_tile<T>(L, p, i, i + 1, F1[i], lane);
+#pragma unroll
+        for (int i = p + 2; i < T; i++) mfma_update_tile<T>(L, p, i, i, D[i], lane);
+        SOLVE_STAMP_TO(ts, lane == 0, 8 * p + 5);
     }
 }
 
-// tiles of the T x T upper triangle plus the right-hand-side column, row-major: t -> (i, j)
-template <int T>
-__device__ inline void mfma_tile_ij(int t, int& i, int& j) {
-    i = 0;
-    while (t >= T + 1 - i) { t -= T + 1 - i; i++; }
-    j = i + t;
+// waves 1, 2: the tiles (i, j >= i + 2), round-robin
+template <int T, int O>
+__device__ inline void mfma_bulk_wave(const BaDev& a, MfmaSolveLds<T>& L, int lane) {
+    constexpr int NB = T * (T - 1) / 2;
+    constexpr int KB = (NB + kMfmaBulkWaves - 1 - O) / kMfmaBulkWaves;
+    double4_t X[KB > 0 ? KB : 1];
+#pragma unroll
+    for (int k = 0; k < KB; k++)
+        mfma_load_tile<T>(a, mfma_bulk_i<T>(O + kMfmaBulkWaves * k), mfma_bulk_j<T>(O + kMfmaBulkWaves * k), X[k], lane);
+    for (int p = 0; p < T; p++) {
+        lds_wait_ge(&L.flag_e, p);
+        double e[4], dv[4];
+        mfma_operands<T>(L, p, lane, e, dv);
+#pragma unroll
+        for (int k = 0; k < KB; k++) {
+            const int i = mfma_bulk_i<T>(O + kMfmaBulkWaves * k), j = mfma_bulk_j<T>(O + kMfmaBulkWaves * k);
+            if (i == p) mfma_row_tile<T>(L, p, j, X[k], e, dv, lane);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) atomicAdd(&L.row_cnt[p], 1);
+        if (p == T - 1) break;
+        lds_wait_ge(&L.row_cnt[p], 1 + kMfmaBulkWaves);
+#pragma unroll
+        for (int k = 0; k < KB; k++) {
+            const int i = mfma_bulk_i<T>(O + kMfmaBulkWaves * k), j = mfma_bulk_j<T>(O + kMfmaBulkWaves * k);
+            if (i > p) mfma_update_tile<T>(L, p, i, j, X[k], lane);
+        }
+    }
 }
 
 template <int T>
-__global__ __launch_bounds__(kBaMfmaThreads) void k_ba_solve_mfma(BaDev a) {
+__device__ inline void solve_mfma_body(const BaDev& a) {
     const BaCtl& ctl = *a.ctl;
     if (ctl.done || ctl.gen != a.run_gen) return;
-    constexpr int NT = T * (T + 3) / 2;                       // upper tiles + right-hand side tiles
-    constexpr int K = (NT + kBaMfmaWaves - 1) / kBaMfmaWaves;  // tile slots per wave
-    constexpr int NL = T * (T - 1) / 2;                       // L^T_jp tiles, p < j < T
     const int np = ctl.np, N = 6 * np;
-    const double lam = a.scal[3];
-    const double* __restrict__ Tc = a.Tb[ctl.cur];
-    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
-    __shared__ double dg[16 * 17];                 // the diagonal tile of the next panel (row-major)
-    __shared__ double Ew[kBaMfmaWaves][16 * 17];   // per wave: E_p rows (MFMA A operands from here)
-    __shared__ double dvw[kBaMfmaWaves][16];       // per wave: 1 / d of the panel's rows
-    __shared__ double Eall[T][256];                // E_p for the back substitution (row-major)
-    __shared__ double Wt[T + 1][4][64];            // -W^T_jp of the current panel (C layout)
-    __shared__ double Lt[NL > 0 ? NL : 1][4][64];  // L^T_jp (C layout: row t contiguous at [t >> 2][16 (t & 3)])
-    __shared__ double ys[16 * T], xs[16 * T];
-    __shared__ int fail;
+    __shared__ MfmaSolveLds<T> L;
     const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, n = lane & 15;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     SOLVE_STAMP_DECL;
     SOLVE_STAMP(tid == 0, 250);
-    auto lt_index = [](int p, int j) { return p * (2 * T - p - 1) / 2 + (j - p - 1); };  // p < j < T
-    // ---- load the tiles (k_ba_schur's tile layout, padding included): consumed lazily, so the
-    // loads of the later tiles overlap the first panel's factorisation
-    double4_t C[K];
-    int ti[K], tj[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int t = w + kBaMfmaWaves * k;
-        ti[k] = tj[k] = -1;
-        if (t < NT) mfma_tile_ij<T>(t, ti[k], tj[k]);
-        const double* src = a.S + (size_t)(t < NT ? t : 0) * 256 + lane;  // padding written by k_ba_schur
-#pragma unroll
-        for (int s = 0; s < 4; s++) C[k][s] = src[64 * s];
+    if (tid == 0) {
+        L.flag_dg = L.flag_e = -1;
+        L.fail = 0;
     }
-#pragma unroll
-    for (int k = 0; k < K; k++)
-        if (ti[k] == 0 && tj[k] == 0)
-#pragma unroll
-            for (int s = 0; s < 4; s++) dg[(q + 4 * s) * 17 + n] = C[k][s];
-    if (tid == 0) fail = 0;
-    SOLVE_STAMP(tid == 0, 251);
+    if (tid < T) L.row_cnt[tid] = 0;
+    __syncthreads();
+    if (w == 0) { mfma_critical_wave<T>(a, L, lane, SOLVE_STAMP_PTR); return; }
+    if (w == 1) { mfma_bulk_wave<T, 0>(a, L, lane); return; }
+    if (w == 2) { mfma_bulk_wave<T, 1>(a, L, lane); return; }
+    // ---- wave 3: A_pp -> E_p = L_pp^-1, D_p^-1 as soon as A_pp is final
     for (int p = 0; p < T; p++) {
-        __syncthreads();  // dg = A_pp after its last update
-        SOLVE_STAMP(tid == 0, 8 * p);
-        // ---- factor A_pp (every wave, one row per lane)
-        {
-            double A[16], E[16], inv[16];
+        lds_wait_ge(&L.flag_dg, p);
+        SOLVE_STAMP(lane == 0, 8 * p);
+        double A[16], E[16], inv[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            A[k] = L.dg[n * 17 + k];
+            E[k] = k == n ? 1.0 : 0.0;
+        }
+        ldl16(A, E, inv, n);
+        if (lane < 16) {
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                A[k] = dg[n * 17 + k];
-                E[k] = k == n ? 1.0 : 0.0;
-            }
-            ldl16_step<0>(A, E, inv, n);
-            if (lane < 16) {
-#pragma unroll
-                for (int k = 0; k < 16; k++) Ew[w][n * 17 + k] = E[k];
-                if (w == 0) {
-#pragma unroll
-                    for (int k = 0; k < 16; k++) Eall[p][n * 16 + k] = E[k];
-                }
-            }
-            if (lane == 0) {
-                bool bad = false;
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    dvw[w][k] = inv[k];
-                    bad |= !isfinite(inv[k]) || inv[k] == 0.0;  // d zero, inf or NaN
-                }
-                if (bad && w == 0) fail = 1;
+                L.Es[p & 1][n * 17 + k] = E[k];
+                L.Eall[p][n * 16 + k] = E[k];
             }
         }
-        SOLVE_STAMP(tid == 0, 8 * p + 1);
-        wave_sync_lds();
-        double e[4], dv[4];
+        if (lane == 0) {
+            bool bad = false;
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            e[s] = Ew[w][n * 17 + 4 * s + q];  // A operand: E[n][4 s + q]
-            dv[s] = dvw[w][q + 4 * s];         // 1 / d of C-layout row q + 4 s
-        }
-        // ---- row panel: W^T_jp = E_p A_pj, L^T_jp = D^-1 W^T_jp
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            if (ti[k] == p && tj[k] > p) {
-                double4_t z = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s = 0; s < 4; s++) z = __builtin_amdgcn_mfma_f64_16x16x4f64(e[s], C[k][s], z, 0, 0, 0);
-                const int j = tj[k];
-#pragma unroll
-                for (int s = 0; s < 4; s++) {
-                    Wt[j][s][lane] = -z[s];
-                    const double lt = z[s] * dv[s];
-                    if (j < T) Lt[lt_index(p, j)][s][lane] = lt;
-                    else if (n == 0) ys[16 * p + q + 4 * s] = lt;  // y_p = D^-1 E b_p
-                }
+            for (int k = 0; k < 16; k++) {
+                L.dvs[p & 1][k] = inv[k];
+                bad |= !isfinite(inv[k]) || inv[k] == 0.0;  // d zero, inf or NaN
             }
+            if (bad) L.fail = 1;
         }
-        SOLVE_STAMP(tid == 0, 8 * p + 2);
-        if (p == T - 1) break;
-        __syncthreads();
-        SOLVE_STAMP(tid == 0, 8 * p + 3);
-        // ---- trailing update A_ij -= (L^T_ip)^T W^T_jp, p < i <= j
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            if (ti[k] > p) {
-                const double* lp = &Lt[lt_index(p, ti[k])][0][lane];
-                const double* wp = &Wt[tj[k]][0][lane];
-                double lo[4], wo[4];
-#pragma unroll
-                for (int s = 0; s < 4; s++) { lo[s] = lp[64 * s]; wo[s] = wp[64 * s]; }
-#pragma unroll
-                for (int s = 0; s < 4; s++) C[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(lo[s], wo[s], C[k], 0, 0, 0);
-                if (ti[k] == p + 1 && tj[k] == p + 1)
-#pragma unroll
-                    for (int s = 0; s < 4; s++) dg[(q + 4 * s) * 17 + n] = C[k][s];
-            }
-        }
-        SOLVE_STAMP(tid == 0, 8 * p + 4);
+        if (lane == 0) lds_publish(&L.flag_e, p);
+        SOLVE_STAMP(lane == 0, 8 * p + 1);
     }
-    __syncthreads();
-    SOLVE_STAMP(tid == 0, 252);
-    if (fail) {  // pop: trial poses = current ones, computeScale = 0
-        for (int k = tid; k < a.nkf; k += blockDim.x)
+    // ---- after every row panel: back substitution and the trial poses
+    lds_wait_ge(&L.row_cnt[T - 1], 1 + kMfmaBulkWaves);
+    SOLVE_STAMP(lane == 0, 252);
+    const double* __restrict__ Tc = a.Tb[ctl.cur];
+    double* __restrict__ Tt = a.Tb[ctl.cur ^ 1];
+    if (L.fail) {  // pop: trial poses = current ones, computeScale = 0
+        for (int k = lane; k < a.nkf; k += 64)
             for (int qq = 0; qq < 8; qq++) Tt[8 * k + qq] = Tc[8 * k + qq];
-        if (tid == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
+        if (lane == 0) { a.istat[3] = 0; a.scal[1] = 0; a.scal[2] = 0; }
         return;
     }
-    if (w != 0) return;
-    // ---- back substitution (one wave, x in registers): x_p = E_p^T (y_p - sum_{j > p} L^T_jp x_j).
-    // Lane (g, t), g = lane >> 4: the copies xr[j] are rotated by 4 g (lane (g, c) holds
-    // x_j[(c + 4 g) & 15]), so group g covers columns 4 g .. 4 g + 3 of every tile with four fused
-    // DPP FMAs reading x from lanes 0..3 of its row; the four groups' partial sums meet by permlane
-    // swaps.  x_p itself comes out rotated: lane (g, c) forms column (c + 4 g) & 15 of E_p^T r.
+    // x_p = E_p^T (y_p - sum_{j > p} L^T_jp x_j).  Lane (g, t), g = lane >> 4: the copies xr[j]
+    // are rotated by 4 g (lane (g, c) holds x_j[(c + 4 g) & 15]), so group g covers columns
+    // 4 g .. 4 g + 3 of every tile with four fused DPP FMAs reading x from lanes 0..3 of its row;
+    // the groups' partial sums meet by permlane swaps.  x_p comes out rotated: lane (g, c) forms
+    // column (c + 4 g) & 15 of E_p^T r (four partial sums over t).
     {
         const int g = q, t = n, rot = (n + 4 * g) & 15;
         double xr[T];
 #pragma unroll
         for (int p = T - 1; p >= 0; p--) {
-            double acc0 = 0.0, acc1 = 0.0;
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = p + 1; j < T; j++) {
-                const double* row = &Lt[lt_index(p, j)][t >> 2][16 * (t & 3) + 4 * g];
-                double& acc = ((j - p) & 1) ? acc0 : acc1;
+                const double* row = &L.Lt[MfmaSolveLds<T>::lt_index(p, j)][t >> 2][16 * (t & 3) + 4 * g];
                 const double l0 = row[0], l1 = row[1], l2 = row[2], l3 = row[3];
-                fmac_bc<0>(acc, xr[j], l0);
-                fmac_bc<1>(acc, xr[j], l1);
-                fmac_bc<2>(acc, xr[j], l2);
-                fmac_bc<3>(acc, xr[j], l3);
+                double& a0 = acc[(j - p) & 3];
+                fmac_bc<0>(a0, xr[j], l0);
+                fmac_bc<1>(a0, xr[j], l1);
+                fmac_bc<2>(a0, xr[j], l2);
+                fmac_bc<3>(a0, xr[j], l3);
             }
-            double acc = acc0 + acc1;
-            acc = swap_combine<16>(acc, acc);
-            acc = swap_combine<32>(acc, acc);
-            const double r = ys[16 * p + t] - acc;
-            double x = 0.0;
+            double s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            s = swap_combine<16>(s, s);
+            s = swap_combine<32>(s, s);
+            const double r = L.ys[16 * p + t] - s;
+            const double* Ec = &L.Eall[p][rot];
+            double e4[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) e4[u] = Ec[16 * u];
+            double x0 = 0.0, x1 = 0.0, x2 = 0.0, x3 = 0.0;
             asm volatile("s_nop 1");
-            gemv16_bc<0>(x, r, &Eall[p][rot]);  // column rot of E_p: sum_t E[t][rot] r_t
+            fmac_bc<0>(x0, r, e4[0]);   fmac_bc<1>(x1, r, e4[1]);   fmac_bc<2>(x2, r, e4[2]);   fmac_bc<3>(x3, r, e4[3]);
+            fmac_bc<4>(x0, r, e4[4]);   fmac_bc<5>(x1, r, e4[5]);   fmac_bc<6>(x2, r, e4[6]);   fmac_bc<7>(x3, r, e4[7]);
+            fmac_bc<8>(x0, r, e4[8]);   fmac_bc<9>(x1, r, e4[9]);   fmac_bc<10>(x2, r, e4[10]); fmac_bc<11>(x3, r, e4[11]);
+            fmac_bc<12>(x0, r, e4[12]); fmac_bc<13>(x1, r, e4[13]); fmac_bc<14>(x2, r, e4[14]); fmac_bc<15>(x3, r, e4[15]);
+            const double x = (x0 + x1) + (x2 + x3);
             asm volatile("s_nop 1");
             xr[p] = x;
-            if (lane < 16) xs[16 * p + t] = x;  // group 0: unrotated
+            if (lane < 16) L.xs[16 * p + t] = x;  // group 0: unrotated
         }
         wave_sync_lds();
     }
     SOLVE_STAMP(lane == 0, 254);
-    for (int qq = lane; qq < N; qq += 64) a.xp[qq] = xs[qq];
+    const double lam = a.scal[3];
+    for (int qq = lane; qq < N; qq += 64) a.xp[qq] = L.xs[qq];
     for (int k = lane; k < a.nkf; k += 64) {
         const int pi = a.pose_idx[k];
         if (pi >= 0) {
             double u[6];
 #pragma unroll
-            for (int qq = 0; qq < 6; qq++) u[qq] = xs[6 * pi + qq];
+            for (int qq = 0; qq < 6; qq++) u[qq] = L.xs[6 * pi + qq];
             se3_oplus(u, Tc + 8 * k, Tt + 8 * k);
         } else {
             for (int qq = 0; qq < 8; qq++) Tt[8 * k + qq] = Tc[8 * k + qq];
         }
     }
     double sc = 0;
-    for (int qq = lane; qq < N; qq += 64) sc += xs[qq] * (lam * xs[qq] + a.bp[qq]);
+    for (int qq = lane; qq < N; qq += 64) sc += L.xs[qq] * (lam * L.xs[qq] + a.bp[qq]);
     sc = wave_sum(sc);
     if (lane == 0) {
         a.scal[1] = sc;
@@ -1874,7 +2024,37 @@ __global__ __launch_bounds__(kBaMfmaThreads) void k_ba_solve_mfma(BaDev a) {
         a.istat[3] = 1;
     }
     SOLVE_STAMP(lane == 0, 253);
-    SOLVE_STAMP_FLUSH();
+#ifdef ORBMI_SOLVE_TRACE
+    if (lane == 0)
+        for (int i_ = 0; i_ < 256; i_++) g_solve_trace[i_] = tstamp[i_];
+#endif
+}
+
+template <int T>
+__global__ __launch_bounds__(kBaMfmaThreads) void k_ba_solve_mfma(BaDev a) { solve_mfma_body<T>(a); }
+
+// The Schur complement and the MFMA solve in one launch: the Schur blocks as k_ba_schur, then the
+// last block to finish (arrival counter; device-scope release / acquire, so every block's tiles
+// are visible to it) runs the solve with its first four waves.  One launch per trial fewer.
+template <int T>
+__global__ __launch_bounds__(kSchurThreads) void k_ba_schur_solve(BaDev a) {
+    {
+        const BaCtl& ctl = *a.ctl;
+        if (ctl.done || ctl.gen != a.run_gen) return;  // the same for every block
+    }
+    schur_body(a);
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&a.ctl->arrive_s, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (threadIdx.x == 0) a.ctl->arrive_s = 0;
+    if (threadIdx.x >= kBaMfmaThreads) return;
+    solve_mfma_body<T>(a);
 }
 
 // ---------------------------------------------------------------- Levenberg control
@@ -2186,12 +2366,17 @@ struct Runner {
     bool solve_rows;  // nf <= kBaSolveRowsMaxPoses: k_ba_solve_rows, else k_ba_solve<1>
     bool solve_pipe;  // k_ba_solve_pipe (a dedicated pivot wave) in place of k_ba_solve_rows
                       // (ORBMI_BA_SOLVE=rows selects the latter, for A/B runs)
-    int mfma_tiles;   // > 0: k_ba_solve_mfma<mfma_tiles> (nf <= kBaSolveMfmaMaxPoses, ORBMI_BA_SOLVE=mfma)
+    int mfma_tiles;   // > 0: k_ba_solve_mfma<mfma_tiles> (nf <= kBaSolveMfmaMaxPoses, the default)
 
+    bool fuse_schur = false;  // k_ba_schur_solve (ORBMI_BA_FUSE=1; measured slower than two launches)
     void launch_mfma() {
+        const dim3 gs(a.nblk + a.nf + 1);
         switch (mfma_tiles) {
-#define ORBMI_MFMA_CASE(T_) \
-    case T_: hipLaunchKernelGGL(k_ba_solve_mfma<T_>, dim3(1), dim3(kBaMfmaThreads), 0, h.stream, a); break;
+#define ORBMI_MFMA_CASE(T_)                                                                                      \
+    case T_:                                                                                                     \
+        if (fuse_schur) hipLaunchKernelGGL(k_ba_schur_solve<T_>, gs, dim3(kSchurThreads), 0, h.stream, a);       \
+        else hipLaunchKernelGGL(k_ba_solve_mfma<T_>, dim3(1), dim3(kBaMfmaThreads), 0, h.stream, a);             \
+        break;
             ORBMI_MFMA_CASE(1) ORBMI_MFMA_CASE(2) ORBMI_MFMA_CASE(3) ORBMI_MFMA_CASE(4)
             ORBMI_MFMA_CASE(5) ORBMI_MFMA_CASE(6) ORBMI_MFMA_CASE(7) ORBMI_MFMA_CASE(8)
 #undef ORBMI_MFMA_CASE
@@ -2228,7 +2413,7 @@ struct Runner {
     // when that optimize() is done or not the current one
     void step(int gen) {
         a.run_gen = gen;
-        if (a.nblk > 0)  // (+ the MFMA solve's padding block)
+        if (a.nblk > 0 && !(mfma_tiles > 0 && fuse_schur))  // (+ the MFMA solve's padding block)
             hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf + (a.mfma_T > 0)), dim3(kSchurThreads), 0, h.stream, a);
         if (mfma_tiles > 0)
             launch_mfma();
@@ -2485,9 +2670,14 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.S = (double*)(B + o_S); a.bs = (double*)(B + o_bs); a.xp = (double*)(B + o_xp);
     a.scal = (double*)(B + o_scal); a.istat = (int*)(B + o_istat);
     const char* sv = getenv("ORBMI_BA_SOLVE");
-    const bool mfma_solve = sv && !strcmp(sv, "mfma");  // (A/B: the VALU pivot-wave solve is the default)
-    a.mfma_T = (mfma_solve && nf <= kBaSolveMfmaMaxPoses) ? std::max(1, (6 * nf + 15) / 16) : 0;
+    // the MFMA solve for nf <= kBaSolveMfmaMaxPoses (ORBMI_BA_SOLVE=pipe / rows: the VALU solves)
+    const bool valu_solve = sv && (!strcmp(sv, "pipe") || !strcmp(sv, "rows"));
+    a.mfma_T = (!valu_solve && nf <= kBaSolveMfmaMaxPoses) ? std::max(1, (6 * nf + 15) / 16) : 0;
     Runner r{h, a, stop, nf <= kBaSolveRowsMaxPoses, !(sv && !strcmp(sv, "rows")), a.mfma_T};
+    {
+        const char* fz = getenv("ORBMI_BA_FUSE");
+        r.fuse_schur = fz && !strcmp(fz, "1");
+    }
     unsigned char* out_erase = B + o_oerase;
     const int nb_all = std::max(1, (std::max(std::max(nkf, npt), ne) + kBaBlock - 1) / kBaBlock);
     hipLaunchKernelGGL(k_ba_setup, dim3(nb_all), dim3(kBaBlock), 0, s, a, a.Tb[0], a.Xb[0], out_erase);

@@ -245,6 +245,7 @@ struct orbmi_slam {
         bool count(int m) const { return m < (int)mark.size() && mark[m] == gen; }
     } seen;
     SeenSet local_mark;           // UpdateLocalPoints' mnTrackReferenceForFrame
+    SeenSet local_kf_mark;        // UpdateLocalKeyFrames' mnTrackReferenceForFrame
     std::vector<int> kf_counter;  // UpdateLocalKeyFrames' keyframe counter (indexed by id)
     // mlRelativeFramePoses, mlpReferences, mlFrameTimes, mlbLost
     std::vector<M4> rel_poses;
@@ -282,6 +283,97 @@ struct orbmi_slam {
         float* h_dep = nullptr;
     } dev;
     hipStream_t xstream = nullptr;  // the left extractor's stream
+    // Device-resident tracking stages: TrackWithMotionModel (SearchByProjection(CF, LF) with the
+    // retry gated on the device count, PoseOptimization on the device-held matches) and
+    // TrackLocalMap (SearchLocalPoints, PoseOptimization over both match arrays) are each enqueued
+    // on the tracking stream (the matcher's, shared with PoseOptimization) behind one upload of
+    // the records the host builds, and read back with one synchronisation.  Host arrays are
+    // pinned, so the copies are plain DMA.
+    struct TrackBuf {
+        size_t cap_kp = 0, cap_lf = 0, cap_rec = 0;
+        // device
+        orbmi_lastframe_point* d_lfp = nullptr;  // TWMM: the last frame's points / TLM: the current frame's
+        orbmi_mappoint* d_rec = nullptr;         // TLM: the local map points
+        orbmi_mappoint_track* d_tr = nullptr;
+        int32_t* d_m = nullptr;                  // matches (TWMM: to LF keypoints; TLM: to local map points)
+        int32_t* d_mlf = nullptr;                // TLM: keypoint -> its own point record (or -1)
+        uint8_t* d_occ = nullptr;
+        uint8_t* d_out = nullptr;                // mvbOutlier
+        int* d_n = nullptr;                      // match count
+        orbmi_pose_frame* d_pose = nullptr;
+        // pinned host
+        orbmi_lastframe_point* h_lfp = nullptr;
+        orbmi_mappoint* h_rec = nullptr;
+        orbmi_mappoint_track* h_tr = nullptr;
+        int32_t* h_m = nullptr;
+        int32_t* h_mlf = nullptr;
+        uint8_t* h_occ = nullptr;
+        uint8_t* h_out = nullptr;
+        int* h_n = nullptr;
+        orbmi_pose_frame* h_pose = nullptr;
+    } tb;
+    hipStream_t tstream = nullptr;  // the tracking stream (the matcher's)
+
+    template <class T>
+    static int grow(T** d, T** h, size_t n) {  // device + pinned host arrays of n elements (contents dropped)
+        if (*d) (void)hipFree(*d);
+        if (*h) (void)hipHostFree(*h);
+        *d = nullptr;
+        *h = nullptr;
+        if (hipMalloc((void**)d, n * sizeof(T)) != hipSuccess) return ORBMI_E_HIP;
+        if (hipHostMalloc((void**)h, n * sizeof(T), hipHostMallocDefault) != hipSuccess) return ORBMI_E_HIP;
+        return ORBMI_OK;
+    }
+    int track_buffers(size_t nkp, size_t nlf, size_t nrec) {
+        nkp = std::max<size_t>(nkp, 1);
+        nlf = std::max<size_t>(nlf, 1);
+        nrec = std::max<size_t>(nrec, 1);
+        TrackBuf& t = tb;
+        if (nkp > t.cap_kp) {
+            const size_t c = nkp + nkp / 4;
+            SLAM_CHECK(grow(&t.d_m, &t.h_m, c));
+            SLAM_CHECK(grow(&t.d_mlf, &t.h_mlf, c));
+            SLAM_CHECK(grow(&t.d_occ, &t.h_occ, c));
+            SLAM_CHECK(grow(&t.d_out, &t.h_out, c));
+            t.cap_kp = c;
+        }
+        if (nlf > t.cap_lf) {
+            const size_t c = nlf + nlf / 4;
+            SLAM_CHECK(grow(&t.d_lfp, &t.h_lfp, c));
+            t.cap_lf = c;
+        }
+        if (nrec > t.cap_rec) {
+            const size_t c = nrec + nrec / 4;
+            SLAM_CHECK(grow(&t.d_rec, &t.h_rec, c));
+            SLAM_CHECK(grow(&t.d_tr, &t.h_tr, c));
+            t.cap_rec = c;
+        }
+        if (!t.d_n) {
+            SLAM_CHECK(grow(&t.d_n, &t.h_n, 2));
+            SLAM_CHECK(grow(&t.d_pose, &t.h_pose, 1));
+        }
+        return ORBMI_OK;
+    }
+    void free_track_buffers() {
+        TrackBuf& t = tb;
+        void* d[] = {t.d_lfp, t.d_rec, t.d_tr, t.d_m, t.d_mlf, t.d_occ, t.d_out, t.d_n, t.d_pose};
+        void* h[] = {t.h_lfp, t.h_rec, t.h_tr, t.h_m, t.h_mlf, t.h_occ, t.h_out, t.h_n, t.h_pose};
+        for (void* x : d)
+            if (x) (void)hipFree(x);
+        for (void* x : h)
+            if (x) (void)hipHostFree(x);
+        tb = TrackBuf{};
+    }
+    template <class T>
+    int up(T* d, const T* h, size_t n) {
+        if (!n) return ORBMI_OK;
+        return hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+    }
+    template <class T>
+    int down(T* h, const T* d, size_t n) {
+        if (!n) return ORBMI_OK;
+        return hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+    }
     double phase_ms[PH_COUNT] = {};
     long phase_frames = 0;
 
@@ -1498,6 +1590,10 @@ struct orbmi_slam {
     // ---- tracking stages ----------------------------------------------------------------------
     std::vector<orbmi_mappoint> mp_records(const std::vector<int>& pts) const {
         std::vector<orbmi_mappoint> rec(pts.size());
+        mp_records_into(pts, rec.data());
+        return rec;
+    }
+    void mp_records_into(const std::vector<int>& pts, orbmi_mappoint* rec) const {
         for (size_t j = 0; j < pts.size(); j++) {
             const MapPoint& mp = mps[pts[j]];
             orbmi_mappoint& r = rec[j];
@@ -1509,12 +1605,17 @@ struct orbmi_slam {
                       (mp.nobs > 0 ? ORBMI_MP_HAS_OBS : 0u);
             std::memcpy(r.desc, mp.desc, 32);
         }
-        return rec;
     }
 
     std::vector<orbmi_lastframe_point> lf_records(const std::vector<int>& lf_mps, const std::vector<uint8_t>* outlier) const {
         std::vector<orbmi_lastframe_point> rec(std::max<size_t>(lf_mps.size(), 1));
-        std::memset(rec.data(), 0, rec.size() * sizeof(orbmi_lastframe_point));
+        lf_records_into(lf_mps, outlier, rec.data());
+        rec.resize(lf_mps.size());
+        return rec;
+    }
+    void lf_records_into(const std::vector<int>& lf_mps, const std::vector<uint8_t>* outlier,
+                         orbmi_lastframe_point* rec) const {
+        std::memset(rec, 0, std::max<size_t>(lf_mps.size(), 1) * sizeof(orbmi_lastframe_point));
         for (size_t i = 0; i < lf_mps.size(); i++) {
             const int m = lf_mps[i];
             if (m < 0) continue;
@@ -1523,8 +1624,6 @@ struct orbmi_slam {
             rec[i].flags = ORBMI_LF_HAS_MP | (mps[m].nobs > 0 ? ORBMI_MP_HAS_OBS : 0u) |
                            (outlier && (*outlier)[i] ? ORBMI_LF_OUTLIER : 0u);
         }
-        rec.resize(lf_mps.size());
-        return rec;
     }
 
     int discard_outliers(TrackedFrame& cf, const std::vector<uint8_t>& outlier) {  // -> nmatchesMap
@@ -1579,7 +1678,7 @@ struct orbmi_slam {
         return ORBMI_OK;
     }
 
-    int track_motion_model(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:997-1063
+    int track_motion_model_staged(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:997-1063
         ok = false;
         TrackedFrame& lf = last_frame;
         lf.tcw = mul(rel_poses.back(), kfs[lf.ref_kf].tcw);  // UpdateLastFrame (pose only, SLAM mode)
@@ -1638,7 +1737,8 @@ struct orbmi_slam {
         std::sort(touched.begin(), touched.end());
         int best = 0, kfmax = -1;
         std::vector<int> local;
-        std::set<int> mark;
+        local_kf_mark.clear();  // mnTrackReferenceForFrame of the keyframes (generation stamps)
+        SeenSet& mark = local_kf_mark;
         for (int id : touched) {
             const int cnt = kf_counter[id];
             kf_counter[id] = 0;
@@ -1648,14 +1748,17 @@ struct orbmi_slam {
             mark.insert(id);
         }
         size_t i = 0;
+        std::vector<int> ch;
         while (i < local.size()) {
             if (local.size() > 80) break;
             const int k = local[i++];
-            const std::vector<int> cov(kfs[k].covisible.begin(),
-                                       kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
-            for (int nb : cov)
+            const std::vector<int>& cov = kfs[k].covisible;
+            const size_t ncov = std::min<size_t>(10, cov.size());
+            for (size_t c = 0; c < ncov; c++) {  // the first 10 (the list may grow below: by index)
+                const int nb = kfs[k].covisible[c];
                 if (!kfs[nb].bad && !mark.count(nb)) { local.push_back(nb); mark.insert(nb); break; }
-            std::vector<int> ch = kfs[k].children;
+            }
+            ch.assign(kfs[k].children.begin(), kfs[k].children.end());
             std::sort(ch.begin(), ch.end());
             for (int c : ch)
                 if (!kfs[c].bad && !mark.count(c)) { local.push_back(c); mark.insert(c); break; }
@@ -1685,7 +1788,7 @@ struct orbmi_slam {
         local_mps.swap(out);
     }
 
-    int track_local_map(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:1075-1104
+    int track_local_map_staged(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {  // src/Tracking.cc:1075-1104
         ok = false;
         {
             PhaseTimer pt(&phase_ms[PH_LOCAL_UPDATE]);
@@ -1741,6 +1844,157 @@ struct orbmi_slam {
         cf.outlier = out;
         int inliers = 0;
         for (int i = 0; i < cf.n(); i++) {  // (:1087-1101)
+            const int m = cf.mps[i];
+            if (m < 0) continue;
+            if (!cf.outlier[i]) {
+                mps[m].found++;  // IncreaseFound
+                if (mps[m].nobs > 0) inliers++;
+            } else if (cf.ur[i] >= 0) {
+                cf.mps[i] = -1;  // stereo outliers are dropped
+            }
+        }
+        matches_inliers = inliers;
+        st.inliers = inliers;
+        ok = inliers >= 30;
+        return ORBMI_OK;
+    }
+
+    // the per-call staged path (ORBMI_SLAM_STAGED=1): every operator call stages its host inputs
+    // and synchronises; the default enqueues a stage's operators behind one upload
+    const bool staged_track = getenv("ORBMI_SLAM_STAGED") != nullptr;
+    int track_motion_model(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {
+        return staged_track ? track_motion_model_staged(cf, st, ok) : track_motion_model_dev(cf, st, ok);
+    }
+    int track_local_map(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {
+        return staged_track ? track_local_map_staged(cf, st, ok) : track_local_map_dev(cf, st, ok);
+    }
+
+    // Tracking::TrackWithMotionModel (src/Tracking.cc:997-1063), device-resident: the last frame's
+    // point records go up once; SearchByProjection(CF, LF, 7) and the retry at 14 when fewer than
+    // 20 matched (the count stays on the device), PoseOptimization on those matches, then one
+    // read-back.  The pose optimisation is enqueued even when the search will have found fewer
+    // than 20 matches; the host then ignores it, as the reference never runs it.
+    int track_motion_model_dev(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {
+        ok = false;
+        TrackedFrame& lf = last_frame;
+        lf.tcw = mul(rel_poses.back(), kfs[lf.ref_kf].tcw);  // UpdateLastFrame (pose only, SLAM mode)
+        cf.tcw = mul(velocity, lf.tcw);
+        cf.has_tcw = true;
+        const int nc = cf.n(), nl = lf.n();
+        SLAM_CHECK(track_buffers(nc, nl, 0));
+        TrackBuf& t = tb;
+        lf_records_into(lf.mps, &lf.outlier, t.h_lfp);
+        SLAM_CHECK(up(t.d_lfp, t.h_lfp, nl));
+        if (hipMemsetAsync(t.d_occ, 0, std::max(nc, 1), tstream) != hipSuccess ||
+            hipMemsetAsync(t.d_n, 0, sizeof(int), tstream) != hipSuccess)
+            return ORBMI_E_HIP;
+        const orbmi_frame_view vc = view(cf, cf.tcw.data()), vl = view(lf, lf.tcw.data());
+        const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
+        orbmi_frame_mappoints fm{};
+        fm.match_lf = t.d_m;
+        fm.lf_points = t.d_lfp;
+        fm.n_lf_points = nl;
+        {
+            PhaseTimer pt(&phase_ms[PH_LF_SEARCH]);
+            SLAM_CHECK(unlocked([&] {
+                int rc = orbmi_search_by_projection_last_frame_if(matcher, &vc, t.d_occ, &vl, t.d_lfp, th, 0, 1, t.d_m,
+                                                                  t.d_n, 1);
+                if (!rc) rc = orbmi_search_by_projection_last_frame_if(matcher, &vc, t.d_occ, &vl, t.d_lfp, 2 * th, 0, 1,
+                                                                       t.d_m, t.d_n, 20);
+                if (!rc) rc = orbmi_pose_optimization_frame(pose, &vc, inv_level_sigma2.data(), &fm, t.d_pose, t.d_out);
+                if (!rc) rc = down(t.h_n, t.d_n, 1);
+                if (!rc) rc = down(t.h_m, t.d_m, nc);
+                if (!rc) rc = down(t.h_out, t.d_out, nc);
+                if (!rc) rc = down(t.h_pose, t.d_pose, 1);
+                if (!rc && hipStreamSynchronize(tstream) != hipSuccess) rc = ORBMI_E_HIP;
+                return rc;
+            }));
+        }
+        const int n = *t.h_n;
+        st.track = 1;
+        st.lf_matches = n;
+        if (n < 20) return ORBMI_OK;
+        for (int i = 0; i < nc; i++) cf.mps[i] = t.h_m[i] >= 0 ? lf.mps[t.h_m[i]] : -1;
+        std::memcpy(cf.tcw.data(), t.h_pose->tcw, sizeof(t.h_pose->tcw));
+        cf.outlier.assign(t.h_out, t.h_out + nc);
+        seen.clear();
+        const int nmap = discard_outliers(cf, cf.outlier);
+        st.nmatches_map = nmap;
+        ok = nmap >= 10;
+        return ORBMI_OK;
+    }
+
+    // Tracking::TrackLocalMap (src/Tracking.cc:1075-1104), device-resident: UpdateLocalMap on the
+    // host, then the local map points' records, the occupancy and the frame's own point records
+    // go up once; SearchLocalPoints (isInFrustum + SearchByProjection(F, MPs, 1)) and
+    // PoseOptimization over the frame's points and the new matches (keypoint i's edge uses the
+    // local map point when it matched one, else its own point), then one read-back.
+    int track_local_map_dev(TrackedFrame& cf, orbmi_slam_frame_stats& st, bool& ok) {
+        ok = false;
+        {
+            PhaseTimer pt(&phase_ms[PH_LOCAL_UPDATE]);
+            update_local_keyframes(cf);
+            update_local_points();
+        }
+        const int nc = cf.n(), nr = (int)local_mps.size();
+        SLAM_CHECK(track_buffers(nc, nc, nr));
+        TrackBuf& t = tb;
+        for (int i = 0; i < nc; i++) {  // SearchLocalPoints' first loop
+            const int m = cf.mps[i];
+            t.h_occ[i] = 0;
+            if (m < 0) continue;
+            if (mps[m].bad) cf.mps[i] = -1;
+            else {
+                mps[m].visible++;  // IncreaseVisible
+                seen.insert(m);
+                t.h_occ[i] = mps[m].nobs > 0 ? 1 : 0;
+            }
+        }
+        {
+            PhaseTimer pr(&phase_ms[PH_LOCAL_RECORDS]);
+            mp_records_into(local_mps, t.h_rec);
+            lf_records_into(cf.mps, nullptr, t.h_lfp);
+            for (int i = 0; i < nc; i++) t.h_mlf[i] = cf.mps[i] >= 0 ? i : -1;
+        }
+        SLAM_CHECK(up(t.d_occ, t.h_occ, nc));
+        SLAM_CHECK(up(t.d_rec, t.h_rec, nr));
+        SLAM_CHECK(up(t.d_lfp, t.h_lfp, nc));
+        SLAM_CHECK(up(t.d_mlf, t.h_mlf, nc));
+        const orbmi_frame_view vc = view(cf, cf.tcw.data());
+        orbmi_frame_mappoints fm{};
+        fm.match_lf = t.d_mlf;
+        fm.lf_points = t.d_lfp;
+        fm.n_lf_points = nc;
+        fm.match_mp = t.d_m;
+        fm.mps = t.d_rec;
+        fm.n_mps = nr;
+        {
+            PhaseTimer pt(&phase_ms[PH_LOCAL_SEARCH]);
+            SLAM_CHECK(unlocked([&] {
+                int rc = orbmi_search_local_points_track(matcher, &vc, t.d_occ, t.d_rec, nr, 1.f, t.d_m, nullptr, nullptr,
+                                                         t.d_tr);
+                if (!rc) rc = orbmi_pose_optimization_frame(pose, &vc, inv_level_sigma2.data(), &fm, t.d_pose, t.d_out);
+                if (!rc) rc = down(t.h_m, t.d_m, nc);
+                if (!rc) rc = down(t.h_tr, t.d_tr, nr);
+                if (!rc) rc = down(t.h_out, t.d_out, nc);
+                if (!rc) rc = down(t.h_pose, t.d_pose, 1);
+                if (!rc && hipStreamSynchronize(tstream) != hipSuccess) rc = ORBMI_E_HIP;
+                return rc;
+            }));
+        }
+        int nl = 0;
+        for (int j = 0; j < nr; j++)
+            if (t.h_tr[j].in_view) mps[local_mps[j]].visible++;
+        std::vector<int> cur = cf.mps;
+        for (int i = 0; i < nc; i++)
+            if (t.h_m[i] >= 0) { cur[i] = local_mps[t.h_m[i]]; nl++; }
+        st.local_map_points = nr;
+        st.local_matches = nl;
+        std::memcpy(cf.tcw.data(), t.h_pose->tcw, sizeof(t.h_pose->tcw));
+        cf.mps = cur;
+        cf.outlier.assign(t.h_out, t.h_out + nc);
+        int inliers = 0;
+        for (int i = 0; i < nc; i++) {  // (:1087-1101)
             const int m = cf.mps[i];
             if (m < 0) continue;
             if (!cf.outlier[i]) {
@@ -1941,6 +2195,11 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
     // LocalMapping: searches + LocalBA), so the streams stay within the hardware queues
     if (!rc) rc = orbmi_pose_share_matcher_stream(h->pose, h->matcher);
     if (!rc) {
+        void* ts = nullptr;
+        rc = orbmi_matcher_get_stream(h->matcher, &ts);
+        h->tstream = (hipStream_t)ts;
+    }
+    if (!rc) {
         void* st = nullptr;
         rc = orbmi_matcher_get_stream(h->lm_matcher ? h->lm_matcher : h->matcher, &st);
         if (!rc) rc = orbmi_ba_set_stream(h->ba, st);
@@ -1979,7 +2238,9 @@ void orbmi_slam_destroy(orbmi_slam* h) {
         h->lm_thread.join();
     }
     if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+    if (h->tstream) (void)hipStreamSynchronize(h->tstream);
     h->free_dev();
+    h->free_track_buffers();
     orbmi_ba_destroy(h->ba);
     orbmi_pose_destroy(h->pose);
     orbmi_matcher_destroy(h->matcher);

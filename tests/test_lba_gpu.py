@@ -46,6 +46,14 @@ def test_lba_parity(oracle, BA, seed, free, fixed, npts):
     _compare(BA.run(prob), ref, prob)
 
 
+@pytest.mark.parametrize("seed,free,fixed,npts", [(42, 20, 4, 3000), (11, 21, 3, 1500)])
+def test_lba_parity_valu_solve(oracle, BA, monkeypatch, seed, free, fixed, npts):
+    """The VALU pivot-wave solve (ORBMI_BA_SOLVE=pipe), kept for A/B runs, same bars."""
+    monkeypatch.setenv("ORBMI_BA_SOLVE", "pipe")
+    prob, _ = SM.local_ba_problem(seed=seed, n_free=free, n_fixed=fixed, n_points=npts)
+    _compare(BA.run(prob), oracle.local_ba(prob, edge_chi2=True), prob)
+
+
 @pytest.mark.parametrize("seed,free,fixed,npts", [(3, 6, 2, 300), (42, 20, 4, 3000), (7, 10, 0, 800),
                                                  (11, 21, 3, 1500), (13, 2, 1, 200), (17, 3, 0, 250)])
 def test_lba_parity_mfma_solve(oracle, BA, monkeypatch, seed, free, fixed, npts):
@@ -116,3 +124,17 @@ def test_lba_from_map_model(oracle, BA):
     problem, order, _ = gather_local_ba(free[-1])
     assert len(problem.edges) > 0 and problem.kfs["fixed"].sum() >= 1
     _compare(BA.run(problem), oracle.local_ba(problem, edge_chi2=True), problem)
+
+
+def test_lba_parity_mfma_solve_fused(oracle, BA, monkeypatch):
+    """The MFMA solve run by the last block of the Schur kernel (ORBMI_BA_FUSE=1) instead of its
+    own launch: the same results as the separate launch, bit for bit, and the oracle's bars."""
+    monkeypatch.setenv("ORBMI_BA_SOLVE", "mfma")
+    prob, _ = SM.local_ba_problem(seed=42, n_free=20, n_fixed=4, n_points=3000)
+    fused = BA.run(prob)
+    monkeypatch.setenv("ORBMI_BA_FUSE", "1")
+    r = BA.run(prob)
+    for k in ("tcw", "pos", "erase"):
+        np.testing.assert_array_equal(r[k], fused[k])
+    assert r["iterations"] == fused["iterations"]
+    _compare(r, oracle.local_ba(prob, edge_chi2=True), prob)

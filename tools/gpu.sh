@@ -160,12 +160,20 @@ for step in "$@"; do
             # a microbenchmark binary under tools/ubench (built beforehand)
             b=${step#ubench=}
             run ubench_$b 60 ./tools/ubench/$b; cat $OUT/ubench_$b.log; cp $OUT/ubench_$b.log $P/;;
+        fetchcal)
+            # FETCH_SIZE / WRITE_SIZE per load / store width (tools/ubench/fetch_calib, built beforehand)
+            run fetchcal_f 90 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/fetchcal_f -o f -- ./tools/ubench/fetch_calib
+            run fetchcal_w 90 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/fetchcal_w -o w -- ./tools/ubench/fetch_calib
+            python3 tools/fetch_calib_report.py $OUT/fetchcal_f $OUT/fetchcal_w | tee $P/fetch_calibration.txt;;
         lbasolve)
-            # config 3 with the MFMA reduced-system solve vs the VALU pivot-wave solve
+            # config 3: the MFMA solve fused with the Schur complement, the MFMA solve alone, the
+            # VALU pivot-wave solve
+            ms() { tail -1 $OUT/$1.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])'; }
             for i in 1 2 3; do
+                ORBMI_BA_SOLVE=mfma ORBMI_BA_FUSE=1 run lbasolve_fused_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
                 ORBMI_BA_SOLVE=mfma run lbasolve_mfma_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
                 ORBMI_BA_SOLVE=pipe run lbasolve_pipe_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
-                echo "mfma $(tail -1 $OUT/lbasolve_mfma_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')  pipe $(tail -1 $OUT/lbasolve_pipe_$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')" | tee -a $OUT/lbasolve.txt
+                echo "fused $(ms lbasolve_fused_$i)  mfma $(ms lbasolve_mfma_$i)  pipe $(ms lbasolve_pipe_$i)" | tee -a $OUT/lbasolve.txt
             done; cp $OUT/lbasolve.txt $P/;;
         mfmapmc|mfmapmc_*)
             # MFMA issue / busy counters per kernel over a short bench run (one pass)

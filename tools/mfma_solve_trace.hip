@@ -91,17 +91,21 @@ int main(int argc, char** argv) {
     printf("%s np=%d N=%d T=%d  avg kernel %.2f us  residual %.3e\n", pipe ? "pipe" : "mfma", np, N, T, ms * 1e3 / reps, res);
     if (pipe) return 0;
     auto cy = [&](int i, int j) { return (long long)(tr[j] - tr[i]); };
-    printf("load %lld cycles\n", cy(250, 251));
-    long long sf = 0, sc = 0, sb = 0, sd = 0, st = 0;
+    // factor wave: 8p (A_pp final, factor starts), 8p+1 (E_p published); tile wave 0: 8p+2 (E_p
+    // seen), 8p+3 (its row panel done), 8p+4 (every row panel done), 8p+5 (its updates done)
+    printf("load issue %lld cycles\n", cy(250, 251));
+    long long sf = 0, sw = 0;
     for (int p = 0; p < T; p++) {
-        const long long f = cy(8 * p, 8 * p + 1), c = cy(8 * p + 1, 8 * p + 2);
-        long long bb = 0, d = 0, t = 0;
-        if (p + 1 < T) { bb = cy(8 * p + 2, 8 * p + 3); d = cy(8 * p + 3, 8 * p + 4); t = cy(8 * p + 4, 8 * (p + 1)); }
-        printf("panel %d: factor %lld  row %lld  barrier %lld  update %lld  barrier %lld\n", p, f, c, bb, d, t);
-        sf += f; sc += c; sb += bb; sd += d; st += t;
+        const long long f = cy(8 * p, 8 * p + 1), handoff = cy(8 * p + 1, 8 * p + 2), row = cy(8 * p + 2, 8 * p + 3);
+        long long rs = 0, up = 0, next = 0;
+        if (p + 1 < T) { rs = cy(8 * p + 3, 8 * p + 4); up = cy(8 * p + 4, 8 * p + 5); next = cy(8 * p + 1, 8 * (p + 1)); }
+        printf("panel %d: factor %lld  E->tiles %lld  row %lld  row sync %lld  update(w0) %lld  | E_p -> A_p+1 final %lld\n",
+               p, f, handoff, row, rs, up, next);
+        sf += f;
+        sw += next;
     }
-    printf("sums: factor %lld  row %lld  barrier %lld  update %lld  barrier %lld\n", sf, sc, sb, sd, st);
-    printf("panels %lld  back substitution %lld  tail %lld  total %lld cycles\n", cy(0, 252), cy(252, 254), cy(254, 253),
-           cy(250, 253));
+    printf("factor sum %lld, waiting for the next diagonal tile %lld\n", sf, sw);
+    printf("start->first factor %lld  panels %lld  back substitution %lld  tail %lld  total %lld cycles\n", cy(250, 0),
+           cy(0, 252), cy(252, 254), cy(254, 253), cy(250, 253));
     return 0;
 }

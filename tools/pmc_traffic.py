@@ -5,8 +5,9 @@
 FETCH_DIR / WRITE_DIR hold the counter_collection CSVs of two separate passes
 (`rocprofv3 --pmc FETCH_SIZE --kernel-trace ...`, `--pmc WRITE_SIZE ...`).  Per
 MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the
-bytes of a wide coalesced read, so bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (the raw values
-are kept too: the x2 is calibrated for 16-B/lane streams only).
+bytes read, so bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024.  Calibrated on this pool for coalesced
+4-, 8- and 16-byte loads and stores per lane (tools/ubench/fetch_calib.hip,
+profiles/r04/fetch_calibration.txt: FETCH_SIZE x2.000 and WRITE_SIZE x1.000 at every width).
 """
 import csv
 import glob
@@ -53,7 +54,7 @@ def main(fetch_dir, write_dir, out):
         per[s] = round((2 * f + w) * 1024)
         raw[s] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w}
     json.dump({"per_launch_bytes": per, "raw_per_launch": raw,
-               "note": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)"},
+               "note": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half count, calibrated for 4/8/16-B loads: profiles/r04/fetch_calibration.txt)"},
               open(out, "w"), indent=1)
     print(json.dumps(per))
 
