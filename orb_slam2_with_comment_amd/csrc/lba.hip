@@ -1661,6 +1661,48 @@ ORBMI_FMAC_DPP(6) ORBMI_FMAC_DPP(7) ORBMI_FMAC_DPP(8) ORBMI_FMAC_DPP(9) ORBMI_FM
 ORBMI_FMAC_DPP(12) ORBMI_FMAC_DPP(13) ORBMI_FMAC_DPP(14) ORBMI_FMAC_DPP(15)
 #undef ORBMI_FMAC_DPP
 
+// The elimination step's dependent chain as single instructions in asm volatile statements:
+// volatile asm keeps its program order, so the chain stays interleaved with the step's bulk
+// FMAs (as plain builtins the scheduler sank the whole chain below them, exposing every latency).
+template <int J> __device__ inline double bcast16_asm(double v);
+#define ORBMI_BCAST_DPP(J)                                                                               \
+    template <> __device__ inline double bcast16_asm<J>(double v) {                                     \
+        double d;                                                                                        \
+        asm volatile("v_mov_b64_dpp %0, %1 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(v)); \
+        return d;                                                                                        \
+    }
+ORBMI_BCAST_DPP(1) ORBMI_BCAST_DPP(2) ORBMI_BCAST_DPP(3) ORBMI_BCAST_DPP(4) ORBMI_BCAST_DPP(5)
+ORBMI_BCAST_DPP(6) ORBMI_BCAST_DPP(7) ORBMI_BCAST_DPP(8) ORBMI_BCAST_DPP(9) ORBMI_BCAST_DPP(10)
+ORBMI_BCAST_DPP(11) ORBMI_BCAST_DPP(12) ORBMI_BCAST_DPP(13) ORBMI_BCAST_DPP(14) ORBMI_BCAST_DPP(15)
+#undef ORBMI_BCAST_DPP
+__device__ inline double rcp_asm(double d) {  // v_rcp_f64 (a transcendental: one wait state before a use)
+    double r;
+    asm volatile("v_rcp_f64 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+}
+__device__ inline double newton_err_asm(double d, double r) {  // 1 - d r
+    double e;
+    asm volatile("v_fma_f64 %0, -%1, %2, 1.0" : "=v"(e) : "v"(d), "v"(r));
+    return e;
+}
+__device__ inline double fma_asm(double a, double b, double c) {
+    double o;
+    asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(a), "v"(b), "v"(c));
+    return o;
+}
+__device__ inline double negmul_asm(double a, double b) {  // -(a b)
+    double o;
+    asm volatile("v_mul_f64 %0, -%1, %2" : "=v"(o) : "v"(a), "v"(b));
+    return o;
+}
+__device__ inline double select_asm(double v, unsigned long long lanes) {  // lanes set: v, else +0
+    const unsigned long long x = __double_as_longlong(v);
+    unsigned lo, hi;
+    asm volatile("v_cndmask_b32_e64 %0, 0, %2, %4\n\tv_cndmask_b32_e64 %1, 0, %3, %4"
+                 : "=&v"(lo), "=&v"(hi) : "v"((unsigned)x), "v"((unsigned)(x >> 32)), "s"(lanes));
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 // 1 / d: v_rcp_f64 (2^-24.4 relative, tools/ubench/dpp64.hip) and one Newton step (2^-48)
 __device__ inline double rcp1_f64(double d) {
     const double r = __builtin_amdgcn_rcp(d);
@@ -1689,20 +1731,21 @@ __device__ inline void ldl16_step(double (&A)[16], double (&E)[16], double (&inv
     if constexpr (J < 15) {
         asm volatile("s_nop 1");
         fmac_self<J>(A[J + 1], nl);
+        const unsigned long long below = __builtin_amdgcn_ballot_w64(r > J + 1);
         asm volatile("s_nop 1");  // the asm's VGPR write before the DPP read below
-        const double d = bcast16<J + 1>(A[J + 1]);
+        const double d = bcast16_asm<J + 1>(A[J + 1]);
         ldl_bulk<J, 0, 3>(A, E, nl);
-        const double r0 = __builtin_amdgcn_rcp(d);
-        ldl_bulk<J, 3, 7>(A, E, nl);
-        const double e1 = fma(-d, r0, 1.0);
-        ldl_bulk<J, 7, 9>(A, E, nl);
-        const double r1 = fma(r0, e1, r0);
+        const double r0 = rcp_asm(d);
+        ldl_bulk<J, 3, 6>(A, E, nl);
+        const double e1 = newton_err_asm(d, r0);
+        ldl_bulk<J, 6, 8>(A, E, nl);
+        const double r1 = fma_asm(r0, e1, r0);
         inv[J + 1] = r1;
-        ldl_bulk<J, 9, 11>(A, E, nl);
-        const double m = A[J + 1] * r1;
-        ldl_bulk<J, 11, 13>(A, E, nl);
-        const double nl_next = r > J + 1 ? -m : 0.0;
-        ldl_bulk<J, 13, 14>(A, E, nl);
+        ldl_bulk<J, 8, 10>(A, E, nl);
+        const double m = negmul_asm(A[J + 1], r1);
+        ldl_bulk<J, 10, 12>(A, E, nl);
+        const double nl_next = select_asm(m, below);
+        ldl_bulk<J, 12, 14>(A, E, nl);
         E[J] += nl;
         ldl16_step<J + 1>(A, E, inv, r, nl_next);
     } else {  // J == 15: only E[0 .. 14] and E[15]

@@ -384,6 +384,12 @@ struct orbmi_slam {
     // solve, which -- as the reference's mMutexMapUpdate does (src/Optimizer.cc:776) -- locks
     // only for the graph assembly and the write-back, so tracking proceeds while it runs.
     std::mutex map_mtx;
+    // mMutexMapUpdate (include/Map.h:66): Tracking holds it for the whole Track(), including the
+    // windows in which it releases map_mtx for its GPU work; LocalBundleAdjustment's write-back of
+    // poses and positions takes it first (src/Optimizer.cc:776), so no frame is tracked half
+    // against the map before a LocalBA and half against the map after it.  Lock order: update_mtx,
+    // then map_mtx.
+    std::mutex update_mtx;
     std::mutex q_mtx;
     std::condition_variable q_cv, idle_cv;
     std::deque<int> lm_queue;   // mlNewKeyFrames
@@ -1564,8 +1570,12 @@ struct orbmi_slam {
         res.pos = pos.data();
         res.erase = erase.data();
         int rc;
-        if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves (mMutexMapUpdate)
-            rc = unlocked([&] { return orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba); });
+        std::unique_lock<std::mutex> update_guard;  // held to the end of the write-back
+        if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves
+            held_lock->unlock();
+            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
+            update_guard = std::unique_lock<std::mutex>(update_mtx);  // (lock order: update, map)
+            held_lock->lock();
         } else {
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
         }
@@ -2267,6 +2277,8 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
         SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
     }
     PhaseTimer* lock_t = new PhaseTimer(&h->phase_ms[PH_LOCK]);
+    std::unique_lock<std::mutex> update_guard(h->update_mtx, std::defer_lock);
+    if (h->async_lm()) update_guard.lock();
     std::unique_lock<std::mutex> map_guard(h->map_mtx);
     delete lock_t;
     // with the mapping thread running, Tracking's GPU calls release the map lock (their inputs

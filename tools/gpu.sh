@@ -181,6 +181,18 @@ for step in "$@"; do
             run mfmapmc_$m 150 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS --kernel-trace -f csv -d $OUT/mfmapmc_$m -o mp -- python3 bench.py $(modeargs $m) --steps 10 --warmup 2 --no-cpu-baseline
             f=$(find $OUT/mfmapmc_$m -name "*counter_collection.csv" | head -1); cp $f $P/mfma_pmc_$m.csv
             python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[(r['Kernel_Name'][:48],r['Counter_Name'])].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1]))]; [print(k, len(v), sum(v)/len(v)) for k,v in sorted(d.items()) if 'ba_' in k[0]]" $f | tee $P/mfma_pmc_$m.txt;;
+        concur)
+            # the concurrent-LocalMapping test three times on the device-resident tracking path and
+            # three times on the staged one (ORBMI_SLAM_STAGED=1), ATE lines collected
+            for i in 1 2 3; do
+                run concur_dev_$i 200 python -u -m pytest -x -q -s -m gpu --timeout 150 --timeout-method thread tests/test_native_slam_gpu.py -k test_native_concurrent_local_mapping
+                ORBMI_SLAM_STAGED=1 run concur_staged_$i 200 python -u -m pytest -x -q -s -m gpu --timeout 150 --timeout-method thread tests/test_native_slam_gpu.py -k test_native_concurrent_local_mapping
+                echo "dev: $(grep -o 'ATE [0-9.]* m (synchronous [0-9.]* m)' $OUT/concur_dev_$i.log)  staged: $(grep -o 'ATE [0-9.]* m (synchronous [0-9.]* m)' $OUT/concur_staged_$i.log)" | tee -a $OUT/concur.txt
+            done;;
+        concurprobe|concurprobe=*)
+            # concurprobe=MS: frames paced MS apart (stereo_kitti.cc's timestamp wait)
+            ms=${step#concurprobe}; ms=${ms#=}; ms=${ms:-0}
+            run concurprobe$ms 300 python -u tools/concur_probe.py 2 $ms; grep -v "^   frame" $OUT/concurprobe$ms.log;;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
