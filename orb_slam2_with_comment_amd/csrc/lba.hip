@@ -1709,57 +1709,44 @@ __device__ inline double rcp1_f64(double d) {
     return fma(r, fma(-d, r, 1.0), r);
 }
 
-// item I of elimination step J's bulk FMAs: A[J + 2 ..] then E[.. J - 1] (14 items for J < 15)
+// Panel factorisation: Gaussian elimination on [A_pp | I] for D_p and E_p = L_pp^-1, one row r of
+// the tile per lane.  A is replicated in the four 16-lane groups; E is split by strided columns:
+// lane (g, r) holds E[r][g + 4 k], k = 0..3 (so a step's E update is J / 4 + 1 FMAs, not J + 1;
+// Eg[k] is also the MFMA A operand of k-chunk k).
+// Item I of elimination step J's bulk FMAs: A[J + 2 ..] (14 - J items), then the E columns.
 template <int J, int I0, int I1>
-__device__ inline void ldl_bulk(double (&A)[16], double (&E)[16], double nl) {
+__device__ inline void ldl_bulk(double (&A)[16], double (&Eg)[4], double nl) {
     if constexpr (I0 < I1) {
         constexpr int NA = 14 - J;
         if constexpr (I0 < NA) fmac_self<J>(A[J + 2 + I0], nl);
-        else if constexpr (I0 - NA < J) fmac_self<J>(E[I0 - NA], nl);
-        ldl_bulk<J, I0 + 1, I1>(A, E, nl);
+        else fmac_self<J>(Eg[I0 - NA], nl);
+        ldl_bulk<J, I0 + 1, I1>(A, Eg, nl);
     }
 }
+__device__ inline double mul_asm(double a, double b) {
+    double o;
+    asm volatile("v_mul_f64 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+    return o;
+}
 
-// elimination step J of [A | E] (row r of the tile per lane), software-pipelined: nl = -l_rJ
-// (0 for rows r <= J) comes from the previous step.  Rows r > J subtract l_rJ times pivot row J
-// (A[J + 1 ..] and E[.. J - 1] of lane J, broadcast inside the fused FMAs).  The next pivot
-// column A[J + 1] goes first; step J + 1's pivot broadcast, reciprocal and multiplier (a chain
-// of dependent instructions) are interleaved with this step's other FMAs in program order, so
-// the in-order issue hides their latencies.  E ends as L^-1 (unit lower); inv[J] = 1 / d_J.
+// Elimination step J, software-pipelined: nl = -l_rJ (0 for rows r <= J) comes from the previous
+// step.  Rows r > J subtract l_rJ times pivot row J (A[J + 1 ..] and the E columns <= J of lane J,
+// broadcast inside the fused FMAs).  The next pivot column A[J + 1] goes first; step J + 1's
+// multiplier is a short chain -- pivot broadcast, reciprocal, then the Newton-corrected quotient
+// nl' = a0 + a0 (1 - d r0) with a0 = -A[J + 1] r0 masked to the rows below the pivot (the mask
+// folded into a multiply, no select on the chain) -- interleaved with this step's bulk FMAs.
+// Step 15 has no row below its pivot: nothing to do.  inv[J] = 1 / d_J.  Each step is one asm
+// statement generated by tools/gen_ldl16.py (ldl16_steps.inc): the order and the DPP wait states
+// inside a step are fixed there, and the statement's leading s_nop 1 covers whatever the
+// compiler put in front of it (tools/check_dpp_hazards.py checks the built code).
 template <int J>
-__device__ inline void ldl16_step(double (&A)[16], double (&E)[16], double (&inv)[16], int r, double nl) {
-    if constexpr (J < 15) {
-        asm volatile("s_nop 1");
-        fmac_self<J>(A[J + 1], nl);
-        const unsigned long long below = __builtin_amdgcn_ballot_w64(r > J + 1);
-        asm volatile("s_nop 1");  // the asm's VGPR write before the DPP read below
-        const double d = bcast16_asm<J + 1>(A[J + 1]);
-        ldl_bulk<J, 0, 3>(A, E, nl);
-        const double r0 = rcp_asm(d);
-        ldl_bulk<J, 3, 6>(A, E, nl);
-        const double e1 = newton_err_asm(d, r0);
-        ldl_bulk<J, 6, 8>(A, E, nl);
-        const double r1 = fma_asm(r0, e1, r0);
-        inv[J + 1] = r1;
-        ldl_bulk<J, 8, 10>(A, E, nl);
-        const double m = negmul_asm(A[J + 1], r1);
-        ldl_bulk<J, 10, 12>(A, E, nl);
-        const double nl_next = select_asm(m, below);
-        ldl_bulk<J, 12, 14>(A, E, nl);
-        E[J] += nl;
-        ldl16_step<J + 1>(A, E, inv, r, nl_next);
-    } else {  // J == 15: only E[0 .. 14] and E[15]
-        asm volatile("s_nop 1");
-#pragma unroll
-        for (int k = 0; k < 15; k++) fmac_self<15>(E[k], nl);
-        E[15] += nl;
-    }
-}
+__device__ inline void ldl16_step(double (&A)[16], double (&Eg)[4], double (&inv)[16], int r, double nl);
+#include "ldl16_steps.inc"
 
-__device__ inline void ldl16(double (&A)[16], double (&E)[16], double (&inv)[16], int r) {
+__device__ inline void ldl16(double (&A)[16], double (&Eg)[4], double (&inv)[16], int r) {
     inv[0] = rcp1_f64(bcast16<0>(A[0]));
     const double nl0 = r > 0 ? -(A[0] * inv[0]) : 0.0;
-    ldl16_step<0>(A, E, inv, r, nl0);
+    ldl16_step<0>(A, Eg, inv, r, nl0);
 }
 
 // LDS flag hand-offs between the waves of one workgroup (release after the data, acquire after
@@ -1965,19 +1952,16 @@ __device__ inline void solve_mfma_body(const BaDev& a) {
     for (int p = 0; p < T; p++) {
         lds_wait_ge(&L.flag_dg, p);
         SOLVE_STAMP(lane == 0, 8 * p);
-        double A[16], E[16], inv[16];
+        double A[16], Eg[4], inv[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            A[k] = L.dg[n * 17 + k];
-            E[k] = k == n ? 1.0 : 0.0;
-        }
-        ldl16(A, E, inv, n);
-        if (lane < 16) {
+        for (int k = 0; k < 16; k++) A[k] = L.dg[n * 17 + k];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                L.Es[p & 1][n * 17 + k] = E[k];
-                L.Eall[p][n * 16 + k] = E[k];
-            }
+        for (int k = 0; k < 4; k++) Eg[k] = q + 4 * k == n ? 1.0 : 0.0;
+        ldl16(A, Eg, inv, n);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // lane (q, n): E[n][q + 4 k]
+            L.Es[p & 1][n * 17 + q + 4 * k] = Eg[k];
+            L.Eall[p][n * 16 + q + 4 * k] = Eg[k];
         }
         if (lane == 0) {
             bool bad = false;
@@ -2006,39 +1990,72 @@ __device__ inline void solve_mfma_body(const BaDev& a) {
     // are rotated by 4 g (lane (g, c) holds x_j[(c + 4 g) & 15]), so group g covers columns
     // 4 g .. 4 g + 3 of every tile with four fused DPP FMAs reading x from lanes 0..3 of its row;
     // the groups' partial sums meet by permlane swaps.  x_p comes out rotated: lane (g, c) forms
-    // column (c + 4 g) & 15 of E_p^T r (four partial sums over t).
+    // column (c + 4 g) & 15 of E_p^T r (four partial sums over t).  Software-pipelined: panel
+    // p - 1's LDS operands (L^T rows, y, E column) are loaded while panel p computes, so each
+    // panel waits on its dependent FMAs only, not on three LDS round trips.
     {
         const int g = q, t = n, rot = (n + 4 * g) & 15;
         double xr[T];
-#pragma unroll
-        for (int p = T - 1; p >= 0; p--) {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        double ltb[2][T][4], e4b[2][16], ysb[2];
+        auto load = [&](int p, int b) {
 #pragma unroll
             for (int j = p + 1; j < T; j++) {
                 const double* row = &L.Lt[MfmaSolveLds<T>::lt_index(p, j)][t >> 2][16 * (t & 3) + 4 * g];
-                const double l0 = row[0], l1 = row[1], l2 = row[2], l3 = row[3];
+#pragma unroll
+                for (int u = 0; u < 4; u++) ltb[b][j][u] = row[u];
+            }
+            ysb[b] = L.ys[16 * p + t];
+            const double* Ec = &L.Eall[p][rot];
+#pragma unroll
+            for (int u = 0; u < 16; u++) e4b[b][u] = Ec[16 * u];
+        };
+        load(T - 1, (T - 1) & 1);
+#pragma unroll
+        for (int p = T - 1; p >= 0; p--) {
+            const int b = p & 1;
+            if (p > 0) load(p - 1, b ^ 1);
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            // (each DPP group is one asm statement opening with s_nop 1: the broadcast sources
+            // xr[j] and r may have been written, or copied, right in front of it)
+#pragma unroll
+            for (int j = p + 1; j < T; j++) {
                 double& a0 = acc[(j - p) & 3];
-                fmac_bc<0>(a0, xr[j], l0);
-                fmac_bc<1>(a0, xr[j], l1);
-                fmac_bc<2>(a0, xr[j], l2);
-                fmac_bc<3>(a0, xr[j], l3);
+                asm volatile("s_nop 1\n\t"
+                             "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+                             "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+                             "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+                             "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf"
+                             : "+v"(a0)
+                             : "v"(xr[j]), "v"(ltb[b][j][0]), "v"(ltb[b][j][1]), "v"(ltb[b][j][2]), "v"(ltb[b][j][3]));
             }
             double s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
             s = swap_combine<16>(s, s);
             s = swap_combine<32>(s, s);
-            const double r = L.ys[16 * p + t] - s;
-            const double* Ec = &L.Eall[p][rot];
-            double e4[16];
-#pragma unroll
-            for (int u = 0; u < 16; u++) e4[u] = Ec[16 * u];
+            const double r = ysb[b] - s;
+            const double* e4 = e4b[b];
             double x0 = 0.0, x1 = 0.0, x2 = 0.0, x3 = 0.0;
-            asm volatile("s_nop 1");
-            fmac_bc<0>(x0, r, e4[0]);   fmac_bc<1>(x1, r, e4[1]);   fmac_bc<2>(x2, r, e4[2]);   fmac_bc<3>(x3, r, e4[3]);
-            fmac_bc<4>(x0, r, e4[4]);   fmac_bc<5>(x1, r, e4[5]);   fmac_bc<6>(x2, r, e4[6]);   fmac_bc<7>(x3, r, e4[7]);
-            fmac_bc<8>(x0, r, e4[8]);   fmac_bc<9>(x1, r, e4[9]);   fmac_bc<10>(x2, r, e4[10]); fmac_bc<11>(x3, r, e4[11]);
-            fmac_bc<12>(x0, r, e4[12]); fmac_bc<13>(x1, r, e4[13]); fmac_bc<14>(x2, r, e4[14]); fmac_bc<15>(x3, r, e4[15]);
+            asm volatile("s_nop 1\n\t"
+                         "v_fmac_f64_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %0, %4, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %1, %4, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %2, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %3, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %0, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %1, %4, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %2, %4, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %3, %4, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %0, %4, %17 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %1, %4, %18 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %2, %4, %19 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+                         "v_fmac_f64_dpp %3, %4, %20 row_newbcast:15 row_mask:0xf bank_mask:0xf"
+                         : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
+                         : "v"(r), "v"(e4[0]), "v"(e4[1]), "v"(e4[2]), "v"(e4[3]), "v"(e4[4]), "v"(e4[5]), "v"(e4[6]),
+                           "v"(e4[7]), "v"(e4[8]), "v"(e4[9]), "v"(e4[10]), "v"(e4[11]), "v"(e4[12]), "v"(e4[13]),
+                           "v"(e4[14]), "v"(e4[15]));
             const double x = (x0 + x1) + (x2 + x3);
-            asm volatile("s_nop 1");
             xr[p] = x;
             if (lane < 16) L.xs[16 * p + t] = x;  // group 0: unrotated
         }

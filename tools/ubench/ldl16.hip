@@ -10,29 +10,31 @@
 using namespace orbmi;
 
 template <int J>
-__device__ inline void bulk_only(double (&A)[16], double (&E)[16], double nl) {
+__device__ inline void bulk_only(double (&A)[16], double (&Eg)[4], double nl) {
     if constexpr (J < 15) {
+        constexpr int NB = (14 - J) + (J / 4 + 1);
         asm volatile("s_nop 1");
         fmac_self<J>(A[J + 1], nl);
-        ldl_bulk<J, 0, 14>(A, E, nl);
-        bulk_only<J + 1>(A, E, nl);
+        ldl_bulk<J, 0, NB>(A, Eg, nl);
+        bulk_only<J + 1>(A, Eg, nl);
     }
 }
 
 template <int J>
 __device__ inline void chain_only(double (&A)[16], double (&inv)[16], int r, double nl) {
     if constexpr (J < 15) {
-        const unsigned long long below = __builtin_amdgcn_ballot_w64(r > J + 1);
+        const double msk = select_asm(-1.0, __builtin_amdgcn_ballot_w64(r > J + 1));
         asm volatile("s_nop 1");
         fmac_self<J>(A[J + 1], nl);
+        const double am = mul_asm(A[J + 1], msk);
         asm volatile("s_nop 1");
         const double d = bcast16_asm<J + 1>(A[J + 1]);
         const double r0 = rcp_asm(d);
         const double e1 = newton_err_asm(d, r0);
-        const double r1 = fma_asm(r0, e1, r0);
-        inv[J + 1] = r1;
-        const double m = negmul_asm(A[J + 1], r1);
-        chain_only<J + 1>(A, inv, r, select_asm(m, below));
+        const double a0 = mul_asm(am, r0);
+        const double nl_next = fma_asm(a0, e1, a0);
+        inv[J + 1] = fma_asm(r0, e1, r0);
+        chain_only<J + 1>(A, inv, r, nl_next);
     }
 }
 
@@ -45,19 +47,20 @@ __global__ __launch_bounds__(256) void k(const double* Ain, double* out, unsigne
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; it++) {
-        double A[16], E[16], inv[16];
+        double A[16], E[4], inv[16];
 #pragma unroll
         for (int c = 0; c < 16; c++) {
             A[c] = A0[c];
-            E[c] = c == n ? 1.0 : 0.0;
             inv[c] = 0.0;
         }
+#pragma unroll
+        for (int c = 0; c < 4; c++) E[c] = (lane >> 4) + 4 * c == n ? 1.0 : 0.0;
         if constexpr (V == 0) ldl16(A, E, inv, n);
         if constexpr (V == 1) bulk_only<0>(A, E, 1e-3 * (1 + n));
         if constexpr (V == 2) chain_only<0>(A, inv, n, -0.5);
         double s = 0.0;
 #pragma unroll
-        for (int c = 0; c < 16; c++) s += A[c] + E[c] + inv[c];
+        for (int c = 0; c < 16; c++) s += A[c] + inv[c] + E[c & 3];
         acc += s;
         A0[it & 15] += 1e-300 * acc;  // a dependency: no iteration is hoisted
     }
