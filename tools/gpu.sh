@@ -193,6 +193,15 @@ for step in "$@"; do
             # concurprobe=MS: frames paced MS apart (stereo_kitti.cc's timestamp wait)
             ms=${step#concurprobe}; ms=${ms#=}; ms=${ms:-0}
             run concurprobe$ms 300 python -u tools/concur_probe.py 2 $ms; grep -v "^   frame" $OUT/concurprobe$ms.log;;
+        prio)
+            # native loop (bench --mode system): the default stream priorities (Tracking high,
+            # LocalMapping low) against all streams at the device default, 3 alternations
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["phase_ms_per_frame"]["local_search"], d["phase_ms_per_frame"]["frame_ctor"], d["ate_rmse_m"])'; }
+            for i in 1 2 3; do
+                run prio_hl_$i 300 python bench.py --mode system --no-cpu-baseline
+                ORBMI_PRIO_LM=default ORBMI_PRIO_MATCHER=default ORBMI_PRIO_POSE=default ORBMI_PRIO_EXTRACTOR=default run prio_flat_$i 300 python bench.py --mode system --no-cpu-baseline
+                echo "tracking high / LM low: $(v prio_hl_$i) | all default: $(v prio_flat_$i)" | tee -a $OUT/prio.txt
+            done;;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
