@@ -96,6 +96,7 @@ struct BaDev {
     const orbmi_ba_point* pts;
     const orbmi_ba_edge* edges;
     const int* kf_order;       // keyframe indices sorted by id (vertex order)
+    const int* free_kf;        // nf: the non-fixed keyframes in id order (the b_schur blocks')
     const int* pt_start;       // edges of point p: [pt_start[p], pt_start[p+1])
     const int* kf_start;       // CSR by keyframe over edge indices
     const int* kf_edges;
@@ -858,7 +859,7 @@ __device__ inline void schur_body(BaDev a) {
     }
     if ((int)blockIdx.x >= a.nblk) {  // blocks nblk + r: b_schur of the r-th free keyframe
         const int r = blockIdx.x - a.nblk;
-        const int ka = a.blk_kf[2 * (r * a.nf - r * (r - 1) / 2)];
+        const int ka = a.free_kf[r];
         const int i1 = a.pose_idx[ka];
         if (i1 < 0) return;
         pose_rows_sum<6>(a, ka, 21, rows, ptot);  // b_p of the keyframe (its edges in CSR order)
@@ -2593,7 +2594,44 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const long long nblk_ll = (long long)nf * (nf + 1) / 2;
     if (nblk_ll > (1 << 20)) return ORBMI_E_UNSUPPORTED;
     const int nblk = (int)nblk_ll;
-    auto blk_of = [nf](int ra, int rb) { return ra * nf - ra * (ra - 1) / 2 + (rb - ra); };
+    // pose-pair blocks placed by row: the blocks of row ra (pairs (ra, rb >= ra), which all read
+    // the Hpl blocks of keyframe ra's edges) go to block ids of one residue mod 8 -- one XCD under
+    // the round-robin dispatch, so their re-reads of those blocks hit one L2 (speed only).  Rows
+    // are dealt to the 8 residues largest first onto the least loaded; pairs beyond a residue's
+    // ids take the ids left over.
+    std::vector<int> blk_id(std::max(nblk, 1));
+    {
+        const int R = 8;
+        std::vector<int> rows(nf), load(R, 0), grp(std::max(nf, 1));
+        for (int r = 0; r < nf; r++) rows[r] = r;  // row r holds nf - r pairs: already largest first
+        for (int r : rows) {
+            const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            grp[r] = g;
+            load[g] += nf - r;
+        }
+        std::vector<int> next(R);
+        for (int g = 0; g < R; g++) next[g] = g;
+        std::vector<char> used(std::max(nblk, 1), 0);
+        std::vector<int> spill;
+        int l = 0;
+        for (int ra = 0; ra < nf; ra++)
+            for (int rb = ra; rb < nf; rb++, l++) {
+                const int g = grp[ra];
+                if (next[g] < nblk) { blk_id[l] = next[g]; used[next[g]] = 1; next[g] += R; }
+                else { blk_id[l] = -1; spill.push_back(l); }
+            }
+        if (getenv("ORBMI_BA_SCHUR_ROWMAJOR")) {  // (A/B: blocks in row-major pair order)
+            for (int x = 0; x < nblk; x++) blk_id[x] = x;
+            spill.clear();
+        }
+        int free_id = 0;
+        for (int x : spill) {
+            while (used[free_id]) free_id++;
+            blk_id[x] = free_id;
+            used[free_id] = 1;
+        }
+    }
+    auto blk_of = [nf, &blk_id](int ra, int rb) { return blk_id[ra * nf - ra * (ra - 1) / 2 + (rb - ra)]; };
     // ---- one device arena; the graph and its index arrays go up in one copy
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
     const int nb_q = std::max(1, (npt + kBaUpdPts - 1) / kBaUpdPts);
@@ -2604,7 +2642,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const size_t o_kfs = take(sizeof(orbmi_ba_keyframe) * nkf), o_pts = take(sizeof(orbmi_ba_point) * npt),
                  o_edges = take(sizeof(orbmi_ba_edge) * ne), o_order = take(4 * nkf), o_pts_start = take(4 * (npt + 1)),
                  o_kfs_start = take(4 * (nkf + 1)), o_kf_edges = take(4 * (size_t)ne), o_kf_pos = take(4 * (size_t)ne),
-                 o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk);
+                 o_kf_pt = take(4 * (size_t)ne), o_blk_kf = take(8 * (size_t)nblk), o_free = take(4 * (size_t)nf);
     const size_t up_bytes = off;
     hipStream_t s = h.stream;
     // the previous call's upload may still be reading the staging buffer (only that copy is
@@ -2649,6 +2687,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     if (npair_cap > (1LL << 28)) return ORBMI_E_UNSUPPORTED;
     const int npair = (int)npair_cap;
     if (nkf) std::memcpy(S + o_order, order.data(), 4 * (size_t)nkf);
+    if (nf) std::memcpy(S + o_free, free_kf.data(), 4 * (size_t)nf);
     {
         int* bk = (int*)(S + o_blk_kf);
         for (int ra = 0; ra < nf; ra++)
@@ -2705,6 +2744,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.pts = (const orbmi_ba_point*)(B + o_pts);
     a.edges = (const orbmi_ba_edge*)(B + o_edges);
     a.kf_order = (const int*)(B + o_order);
+    a.free_kf = (const int*)(B + o_free);
     a.pt_start = (const int*)(B + o_pts_start);
     a.kf_start = (const int*)(B + o_kfs_start);
     a.kf_edges = (const int*)(B + o_kf_edges);

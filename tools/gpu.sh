@@ -202,6 +202,22 @@ for step in "$@"; do
                 ORBMI_PRIO_LM=default ORBMI_PRIO_MATCHER=default ORBMI_PRIO_POSE=default ORBMI_PRIO_EXTRACTOR=default run prio_flat_$i 300 python bench.py --mode system --no-cpu-baseline
                 echo "tracking high / LM low: $(v prio_hl_$i) | all default: $(v prio_flat_$i)" | tee -a $OUT/prio.txt
             done;;
+        schurxcd)
+            # LocalBA (config 3): Schur blocks grouped by row onto one XCD (default) vs row-major,
+            # 3 alternations, plus FETCH_SIZE of each layout
+            ms() { tail -1 $OUT/$1.log | python -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])'; }
+            for i in 1 2 3; do
+                run sx_xcd_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
+                ORBMI_BA_SCHUR_ROWMAJOR=1 run sx_row_$i 200 python bench.py --mode lba --steps 50 --warmup 10 --no-cpu-baseline
+                echo "xcd rows $(ms sx_xcd_$i)  row-major $(ms sx_row_$i)" | tee -a $OUT/schurxcd.txt
+            done
+            run sx_fetch_xcd 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/sx_fetch_xcd -o f -- python3 bench.py --mode lba --steps 10 --warmup 2 --no-cpu-baseline
+            ORBMI_BA_SCHUR_ROWMAJOR=1 run sx_fetch_row 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/sx_fetch_row -o f -- python3 bench.py --mode lba --steps 10 --warmup 2 --no-cpu-baseline
+            for v in xcd row; do
+                f=$(find $OUT/sx_fetch_$v -name "*counter_collection.csv" | head -1)
+                python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[r['Kernel_Name'][:40]].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1])) if r['Counter_Name']=='FETCH_SIZE']; [print(sys.argv[2], k, len(v), round(2*sum(v)/len(v)/1024,3), 'MB (2 x FETCH_SIZE)') for k,v in sorted(d.items()) if 'ba_' in k]" $f $v | tee -a $OUT/schurxcd.txt
+            done
+            cp $OUT/schurxcd.txt $P/;;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
