@@ -774,7 +774,8 @@ constexpr int kSchurWaves = kSchurThreads / 64;
 // fixed order: thread = (value, lane) with kSchurThreads / nq lanes, then lanes in order;
 // tot[q] for q < nq in LDS after the call (LDS scratch red, >= kSchurThreads doubles)
 template <int NQ>
-__device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red, double* tot) {
+__device__ __attribute__((always_inline)) inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
+                                                                     double* tot) {
     constexpr int kLanes = kSchurThreads / NQ;
     const int q = threadIdx.x % NQ, el = threadIdx.x / NQ;
     const double* base = a.Hpe + 27 * (long long)a.kf_start[k] + q0 + q;
@@ -801,7 +802,10 @@ __device__ inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
     __syncthreads();
 }
 
-__device__ inline void schur_body(BaDev a) {
+// (always_inline here and on pose_rows_sum: called from two kernels, the compiler otherwise
+// outlines pose_rows_sum<21> into a function call with a 144-byte stack frame, and k_ba_schur
+// went 16.5 -> 23.3 us)
+__device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     // the block's pair structure (static within an optimize()) is loaded before the LM state, so
     // that its two dependent loads overlap the control block's instead of following it
     const int b = blockIdx.x;
@@ -842,7 +846,9 @@ __device__ inline void schur_body(BaDev a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if ((int)blockIdx.x == a.nblk + a.nf) {  // the MFMA solve's padding: identity rows / columns
-        // beyond N, zero columns 1..15 of the right-hand-side tiles (static within an optimize())
+        // beyond N, zero columns 1..15 of the right-hand-side tiles.  Static within an optimize()
+        // (N fixed, the solve only reads S): written on its first trial only
+        if (!(ctl.it == 0 && ctl.trial == 0)) return;
         const int T = a.mfma_T, NT = T * (T + 3) / 2;
         for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
             int t = e >> 8, i = 0;
@@ -1931,7 +1937,7 @@ __device__ inline void mfma_bulk_wave(const BaDev& a, MfmaSolveLds<T>& L, int la
 }
 
 template <int T>
-__device__ inline void solve_mfma_body(const BaDev& a) {
+__device__ __attribute__((always_inline)) inline void solve_mfma_body(const BaDev& a) {
     const BaCtl& ctl = *a.ctl;
     if (ctl.done || ctl.gen != a.run_gen) return;
     const int np = ctl.np, N = 6 * np;

@@ -218,6 +218,12 @@ for step in "$@"; do
                 python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[r['Kernel_Name'][:40]].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1])) if r['Counter_Name']=='FETCH_SIZE']; [print(sys.argv[2], k, len(v), round(2*sum(v)/len(v)/1024,3), 'MB (2 x FETCH_SIZE)') for k,v in sorted(d.items()) if 'ba_' in k]" $f $v | tee -a $OUT/schurxcd.txt
             done
             cp $OUT/schurxcd.txt $P/;;
+        profenv=*)
+            # rocprofv3 kernel stats of --mode lba under an environment setting: profenv=VAR=VALUE
+            kv=${step#profenv=}; tag=$(echo $kv | tr '=' '_')
+            env $kv timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/profenv_$tag -o stats -- python3 bench.py --mode lba --steps 20 --warmup 4 --no-cpu-baseline > $OUT/profenv_$tag.log 2>&1
+            echo "profenv_$tag exit $?" | tee -a $OUT/status.txt
+            f=$(find $OUT/profenv_$tag -name "*kernel_stats.csv" | head -1); echo "== $kv"; cut -d, -f1-4 $f | grep "k_ba_s\|k_ba_u";;
         *) echo "unknown step $step"; exit 2;;
     esac
 done
