@@ -2149,7 +2149,10 @@ __device__ inline void k_ba_control_body(const BaDev& a) {
     const int lane = threadIdx.x, nmax = max(need_lin ? a.nb_e : 0, a.nb_q);
     for (int k = lane; k < nmax; k += 64) {
         if (need_lin && k < a.nb_e) l += a.part_lin[k];
-        if (k < a.nb_q) { t += a.part_tchi[k]; sc += a.part_tscale[k]; }
+        if (k < a.nb_q) {  // (this launch's blocks wrote them: sc1 loads, see k_ba_update_errors)
+            t += __hip_atomic_load(&a.part_tchi[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sc += __hip_atomic_load(&a.part_tscale[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         l += __shfl_xor(l, o, 64);
@@ -2315,15 +2318,19 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     }
     chi = block_sum<kBaUpdThreads>(chi, red);
     sc = block_sum<kBaUpdThreads>(sc, red);
+    // the fan-in to the last block without __threadfence (an L2 write-back + L1 invalidate,
+    // ~3.5 us on gfx950, twice per trial): the two partials go out as agent-scope (sc1) stores,
+    // drained before the arrival add; the last block reads them with sc1 loads
+    // (MI355X_MICROARCH.md, inter-workgroup hand-offs, row 1).  What else the blocks wrote is
+    // read by the next launches only.
     if (tid == 0) {
-        part_chi[blockIdx.x] = chi;
-        part_scale[blockIdx.x] = sc;
-        __threadfence();
+        __hip_atomic_store(&part_chi[blockIdx.x], chi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&part_scale[blockIdx.x], sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = atomicAdd(&ctl.arrive, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
     if (tid < 64) k_ba_control_body(a);
     if (tid == 0) ctl.arrive = 0;
 }
