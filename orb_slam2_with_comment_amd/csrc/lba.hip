@@ -530,15 +530,14 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_errors(BaDev a, int phase) {
     }
     s = block_sum<kBaBlock>(s, red);
     __shared__ bool last;
-    if (threadIdx.x == 0) {
-        part[blockIdx.x] = s;
-        __threadfence();
+    if (threadIdx.x == 0) {  // the fan-in as k_ba_update_errors': sc1 store drained before the add
+        __hip_atomic_store(&part[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = atomicAdd(&a.ctl->arrive_e, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
-    if (threadIdx.x < 64) chi_body(a, phase);  // one wave: the partials in a fixed order
+    if (threadIdx.x < 64) chi_body(a, phase);  // one wave: the partials in a fixed order (sc1 loads)
     if (threadIdx.x == 0) a.ctl->arrive_e = 0;
 }
 
@@ -2127,6 +2126,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_ba_schur_solve(BaDev a) {
 // ---------------------------------------------------------------- Levenberg control
 // fixed-order sum of n partials by one wave (lane l: l, l + 64, ...; then a fixed xor tree,
 // lane 0's value broadcast): deterministic run to run
+// the same over partials other workgroups of this launch wrote with sc1 stores (sc1 loads)
+__device__ inline double wave_sum_fixed_sc1(const double* p, int n) {
+    double s = 0;
+    for (int k = threadIdx.x; k < n; k += 64) s += __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return __shfl(s, 0, 64);
+}
 __device__ inline double wave_sum_fixed(const double* p, int n) {
     double s = 0;
     for (int k = threadIdx.x; k < n; k += 64) s += p[k];
@@ -2337,7 +2343,7 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
 
 // activeRobustChi2 after optimize() (k_ba_errors partials) and the iteration count
 __device__ inline void chi_body(const BaDev& a, int phase) {
-    const double chi = wave_sum_fixed(a.part_lin, a.nb_e);
+    const double chi = wave_sum_fixed_sc1(a.part_lin, a.nb_e);
     if (threadIdx.x == 0) {
         BaCtl& c = *a.ctl;
         c.chi_out[phase] = chi;
