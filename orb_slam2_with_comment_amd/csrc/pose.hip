@@ -76,6 +76,45 @@ __device__ inline void pose_error(const double* T, const PoseCam& c, const orbmi
     }
 }
 
+// The pass's pose as a rotation matrix and translation, formed once per pass and held in SGPRs
+// (the pose is the same for every lane: readfirstlane), so each edge's camera-frame point is
+// 9 FMAs (p = R X + t) instead of the quaternion rotation's ~24 operations
+struct PoseRt { double r[9], t[3]; };
+__device__ inline double uniform_d(double v) {
+    const unsigned long long x = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+__device__ inline PoseRt pose_rt(const double* T) {
+    double R[3][3];
+    q_to_matrix(load_q(T), R);
+    PoseRt P;
+#pragma unroll
+    for (int k = 0; k < 9; k++) P.r[k] = R[k / 3][k % 3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) P.t[k] = T[4 + k];
+    return P;
+}
+__device__ inline void pose_error_rt(const PoseRt& P, const PoseCam& c, const orbmi_pose_obs& o, double p[3],
+                                     double& invz, double e[3]) {
+    const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
+#pragma unroll
+    for (int r = 0; r < 3; r++) p[r] = fma(P.r[3 * r], X[0], fma(P.r[3 * r + 1], X[1], fma(P.r[3 * r + 2], X[2], P.t[r])));
+    invz = fast_rcp(p[2]);
+    if (o.ur < 0) {
+        e[0] = (double)o.u - (p[0] * invz * c.fx + c.cx);
+        e[1] = (double)o.v - (p[1] * invz * c.fy + c.cy);
+        e[2] = 0;
+    } else {
+        const float fz = (float)invz;
+        const double r0 = p[0] * fz * c.fx + c.cx;
+        const double r1 = p[1] * fz * c.fy + c.cy;
+        e[0] = (double)o.u - r0;
+        e[1] = (double)o.v - r1;
+        e[2] = (double)o.ur - (r0 - c.bf * fz);
+    }
+}
+
 __device__ inline double pose_chi2(const orbmi_pose_obs& o, const double e[3]) {
     const double info = (double)o.inv_sigma2;
     return e[0] * (info * e[0]) + e[1] * (info * e[1]) + (o.ur < 0 ? 0.0 : e[2] * (info * e[2]));
@@ -227,11 +266,12 @@ __device__ inline void pose_pass(const double* T, const PoseCam& cam, const orbm
 #pragma unroll
     for (int q = 0; q < 28; q++) acc[q] = 0;
     const int k0 = threadIdx.x < kPoseFullThreads ? (int)threadIdx.x : n;  // the other waves: no edges
+    const PoseRt P = pose_rt(T);
     for (int k = k0; k < n; k += kPoseFullThreads) {
         if (outl[k]) continue;
         const orbmi_pose_obs o = sobs[k];
         double p[3], invz, e[3];
-        pose_error(T, cam, o, p, invz, e);
+        pose_error_rt(P, cam, o, p, invz, e);
         const double c2 = pose_chi2(o, e), info = (double)o.inv_sigma2;
         schi[k] = (float)c2;
         double rho0 = c2, rho1 = 1.0;
@@ -284,11 +324,12 @@ __device__ inline void pose_candidates(const double (&hb)[28], double lambda, do
 __device__ inline double pose_chi_pass(const double* T, const PoseCam& cam, const orbmi_pose_obs* sobs,
                                        const uint8_t* outl, float* schi, int n, bool robust) {
     double chi = 0;
+    const PoseRt P = pose_rt(T);
     for (int k = threadIdx.x; k < n; k += kPoseThreads) {
         if (outl[k]) continue;
         const orbmi_pose_obs o = sobs[k];
         double p[3], invz, e[3];
-        pose_error(T, cam, o, p, invz, e);
+        pose_error_rt(P, cam, o, p, invz, e);
         const double c2 = pose_chi2(o, e);
         schi[k] = (float)c2;
         double rho0 = c2;
