@@ -97,6 +97,8 @@ struct BaDev {
     const orbmi_ba_edge* edges;
     const int* kf_order;       // keyframe indices sorted by id (vertex order)
     const int* free_kf;        // nf: the non-fixed keyframes in id order (the b_schur blocks')
+    double* part_kf;           // kBaMaxPoses x kSchurKfSplit x 64: the keyframe blocks' half sums
+    unsigned* arrive_kf;       // kBaMaxPoses: halves of a keyframe's sums arrived (k_ba_setup zeroes)
     const int* pt_start;       // edges of point p: [pt_start[p], pt_start[p+1])
     const int* kf_start;       // CSR by keyframe over edge indices
     const int* kf_edges;
@@ -317,6 +319,7 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restri
         Ti[0] = q.x; Ti[1] = q.y; Ti[2] = q.z; Ti[3] = q.w; Ti[4] = t[3]; Ti[5] = t[7]; Ti[6] = t[11]; Ti[7] = 0;
         a.kf_act[i] = 0;
     }
+    if (i < a.nf) a.arrive_kf[i] = 0;
     if (i < a.npt) {
         for (int r = 0; r < 3; r++) X[4 * i + r] = a.pts[i].pos[r];
         X[4 * i + 3] = 0;
@@ -760,42 +763,54 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_reduce(BaDev a) {
 }
 
 // ---------------------------------------------------------------- Schur complement
-// one block per pose pair (i <= j): H_schur(i,j) = [Hpp_i + lambda I] - sum_points
-// B_i D^-1 B_j^T with D^-1 recomputed per observation pair; the diagonal block also writes
-// b_schur(i) = b_p - sum B D^-1 b_l.  lam < 0: lambda = 1e-5 max|diag H| (every block reduces
+// one block per pose pair (i < j): H_schur(i,j) = - sum_points B_i D^-1 B_j^T with D^-1
+// recomputed per observation pair; one block per free keyframe i for the diagonal block
+// [Hpp_i + lambda I] - sum_edges B D^-1 B^T and b_schur(i) = b_p - sum B D^-1 b_l (the (i, i)
+// pair blocks return at once).  lam < 0: lambda = 1e-5 max|diag H| (every block reduces
 // the same partials in the same order; block 0 publishes it in scal[3]).  512 threads (two
 // waves per SIMD hide the dependent loads of a pair); the 36 block sums are reduced per wave
 // by DPP / permlane reduce-scatter (wave_ops.h) and across waves in wave order.
 constexpr int kSchurThreads = 512;
 constexpr int kSchurWaves = kSchurThreads / 64;
+constexpr int kSchurKfSplit = 2;  // blocks per free keyframe for its diagonal block and b_schur
 
-// sum over keyframe k's edges (keyframe-CSR rows of Hpe) of values [q0, q0 + nq) of the 27,
-// fixed order: thread = (value, lane) with kSchurThreads / nq lanes, then lanes in order;
-// tot[q] for q < nq in LDS after the call (LDS scratch red, >= kSchurThreads doubles)
+// sum over keyframe k's edges (keyframe-CSR rows of Hpe) of values [q0, q0 + NQ) of the 27,
+// fixed order: thread t takes edges t, t + 512, ... (a config-3 keyframe has ~830: two per
+// thread, every load of both in flight at once), then a per-wave reduce-scatter (DPP /
+// permlane, wave_ops.h) and the waves' sums in wave order; tot[q] for q < NQ in LDS after the
+// call (LDS scratch red, >= kSchurWaves x 32 doubles).  The diagonal blocks' Hpp sum was the
+// Schur kernel's tail as value-per-lane loops (~35 dependent-batched loads per lane).
 template <int NQ>
 __device__ __attribute__((always_inline)) inline void pose_rows_sum(const BaDev& a, int k, int q0, double* red,
                                                                      double* tot) {
-    constexpr int kLanes = kSchurThreads / NQ;
-    const int q = threadIdx.x % NQ, el = threadIdx.x / NQ;
-    const double* base = a.Hpe + 27 * (long long)a.kf_start[k] + q0 + q;
-    const int n = a.kf_start[k + 1] - a.kf_start[k];
-    if (el < kLanes) {
-        double v[16];  // sixteen loads in flight per lane
+    static_assert(NQ <= 32, "one reduce-scatter");
+    const int js = a.kf_start[k], n = a.kf_start[k + 1] - js;
+    double v[32];
 #pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = 0;
-        int m = el;
-        for (; m + 15 * kLanes < n; m += 16 * kLanes)
+    for (int q = 0; q < 32; q++) v[q] = 0;
+    for (int m0 = threadIdx.x; m0 < n; m0 += 2 * kSchurThreads) {
+        double x[2][NQ];
 #pragma unroll
-            for (int u = 0; u < 16; u++) v[u] += base[27 * (long long)(m + u * kLanes)];
-        for (int u = 0; m < n; m += kLanes, u++) v[u] += base[27 * (long long)m];
+        for (int u = 0; u < 2; u++) {
+            const int m = min(m0 + u * kSchurThreads, n - 1);
+            const double* rec = a.Hpe + 27 * (long long)(js + m) + q0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] += v[u + 8];
-        red[el * NQ + q] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+            for (int q = 0; q < NQ; q++) x[u][q] = rec[q];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (m0 + u * kSchurThreads < n) {
+#pragma unroll
+                for (int q = 0; q < NQ; q++) v[q] += x[u][q];
+            }
     }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double r = wave_reduce_scatter32(v);  // lane l: value l >> 1 (even lanes)
+    if (!(lane & 1) && (lane >> 1) < NQ) red[wid * 32 + (lane >> 1)] = r;
     __syncthreads();
     if ((int)threadIdx.x < NQ) {
         double t = 0;
-        for (int w = 0; w < kLanes; w++) t += red[w * NQ + threadIdx.x];
+        for (int w = 0; w < kSchurWaves; w++) t += red[w * 32 + threadIdx.x];
         tot[threadIdx.x] = t;
     }
     __syncthreads();
@@ -826,7 +841,6 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     if (ctl.done || ctl.gen != a.run_gen) return;
     ba_use(a, ctl.lin);
     __shared__ double rows[kSchurThreads];
-    __shared__ double ptot[21];  // Hpp (upper) or b_p of the block's keyframe
     const int N = 6 * ctl.np, nmax = a.nb_p + ctl.np;
     const double* part_max = a.part_max;
     // lambda: computeLambdaInit on the first trial of iteration 0, the LM state otherwise
@@ -844,7 +858,7 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if ((int)blockIdx.x == a.nblk + a.nf) {  // the MFMA solve's padding: identity rows / columns
+    if ((int)blockIdx.x == a.nblk + kSchurKfSplit * a.nf) {  // the MFMA solve's padding: identity rows / columns
         // beyond N, zero columns 1..15 of the right-hand-side tiles.  Static within an optimize()
         // (N fixed, the solve only reads S): written on its first trial only
         if (!(ctl.it == 0 && ctl.trial == 0)) return;
@@ -862,37 +876,97 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
         }
         return;
     }
-    if ((int)blockIdx.x >= a.nblk) {  // blocks nblk + r: b_schur of the r-th free keyframe
-        const int r = blockIdx.x - a.nblk;
+    if ((int)blockIdx.x >= a.nblk) {
+        // blocks nblk + 2 r + h: half h of the r-th free keyframe's edges (CSR order) for its
+        // diagonal block and b_schur: Hpp and b_p (the edges' Hpe rows), and per edge e of point l
+        // with B = Hpl_e the diagonal pair product B D_l^-1 B^T and B D_l^-1 b_l -- the diagonal
+        // pose pair's observation pairs are exactly the keyframe's edges, so the (i, i) pair
+        // blocks return at once.  The two halves' 54 sums meet through sc1 partials and an
+        // arrival counter (the second to arrive combines them in half order and writes)
+        const int rb = blockIdx.x - a.nblk, r = rb / kSchurKfSplit, h = rb % kSchurKfSplit;
         const int ka = a.free_kf[r];
         const int i1 = a.pose_idx[ka];
         if (i1 < 0) return;
-        pose_rows_sum<6>(a, ka, 21, rows, ptot);  // b_p of the keyframe (its edges in CSR order)
-        double bacc[6] = {0, 0, 0, 0, 0, 0};
-        for (int j = a.kf_start[ka] + threadIdx.x; j < a.kf_start[ka + 1]; j += blockDim.x) {
+        double vh[32], vp[32];
+#pragma unroll
+        for (int q = 0; q < 32; q++) vh[q] = vp[q] = 0;
+        const int js = a.kf_start[ka], je = a.kf_start[ka + 1];
+        for (int j = js + h * kSchurThreads + threadIdx.x; j < je; j += kSchurKfSplit * kSchurThreads) {
             const int e = a.kf_edges[j];
             const int p = a.kf_pt[j];
+            const double* he = a.Hpe + 27 * (long long)j;  // keyframe-CSR rows
+            double hx[27];
+#pragma unroll
+            for (int q = 0; q < 27; q++) hx[q] = he[q];
             double Di[9];
             point_dinv(a.Hll, p, lam, Di);
             const double* blp = a.bl + 3 * p;
-            double db[3];
-            for (int rr = 0; rr < 3; rr++) db[rr] = Di[rr * 3] * blp[0] + Di[rr * 3 + 1] * blp[1] + Di[rr * 3 + 2] * blp[2];
             const double* B = a.Hpl + 18 * (long long)e;
+            double bb[18], BD[18];
 #pragma unroll
-            for (int rr = 0; rr < 6; rr++) bacc[rr] += B[rr * 3] * db[0] + B[rr * 3 + 1] * db[1] + B[rr * 3 + 2] * db[2];
+            for (int q = 0; q < 18; q++) bb[q] = B[q];
+#pragma unroll
+            for (int q = 0; q < 27; q++) vh[q] += hx[q];
+#pragma unroll
+            for (int rr = 0; rr < 6; rr++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) BD[rr * 3 + c] = bb[rr * 3] * Di[c] + bb[rr * 3 + 1] * Di[3 + c] + bb[rr * 3 + 2] * Di[6 + c];
+            int q = 0;
+#pragma unroll
+            for (int rr = 0; rr < 6; rr++)
+#pragma unroll
+                for (int c = rr; c < 6; c++, q++)
+                    vp[q] += BD[rr * 3] * bb[c * 3] + BD[rr * 3 + 1] * bb[c * 3 + 1] + BD[rr * 3 + 2] * bb[c * 3 + 2];
+#pragma unroll
+            for (int rr = 0; rr < 6; rr++) vp[21 + rr] += BD[rr * 3] * blp[0] + BD[rr * 3 + 1] * blp[1] + BD[rr * 3 + 2] * blp[2];
         }
-#pragma unroll
-        for (int q = 0; q < 6; q++) {
-            const double x = wave_sum(bacc[q]);
-            if (lane == 0) red[wid][q] = x;
+        {  // per wave: 27 + 27 sums by two reduce-scatters (lane l: value l >> 1), then across waves
+            const double x = wave_reduce_scatter32(vh), y = wave_reduce_scatter32(vp);
+            if (!(lane & 1) && (lane >> 1) < 27) {
+                rows[wid * 64 + (lane >> 1)] = x;
+                rows[wid * 64 + 32 + (lane >> 1)] = y;
+            }
         }
         __syncthreads();
-        if (threadIdx.x < 6) {
+        if (wid != 0) return;
+        double* part = a.part_kf + (size_t)(r * kSchurKfSplit + h) * 64;
+        {  // this half's sums out as sc1 stores, drained, then the arrival (wave 0 only)
             double t = 0;
-            for (int w = 0; w < kSchurWaves; w++) t += red[w][threadIdx.x];
-            a.bp[6 * i1 + threadIdx.x] = ptot[threadIdx.x];  // the solve's computeScale reads it
-            a.bs[6 * i1 + threadIdx.x] = ptot[threadIdx.x] - t;
-            if (a.mfma_T) a.S[mfma_tile_pos(a.mfma_T, 6 * i1 + threadIdx.x, 16 * a.mfma_T)] = ptot[threadIdx.x] - t;
+            for (int w = 0; w < kSchurWaves; w++) t += rows[w * 64 + lane];
+            if ((lane & 31) < 27) __hip_atomic_store(part + lane, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        int arrived = 0;
+        if (lane == 0) arrived = (int)atomicAdd(&a.arrive_kf[r], 1u);
+        arrived = __shfl(arrived, 0, 64);
+        if (arrived != kSchurKfSplit - 1) return;
+        if (lane == 0) a.arrive_kf[r] = 0;
+        const int q = lane;
+        if (q < 27) {
+            double th = 0, tp = 0;  // halves in order
+            for (int hh = 0; hh < kSchurKfSplit; hh++) {
+                const double* ph = a.part_kf + (size_t)(r * kSchurKfSplit + hh) * 64;
+                th += __hip_atomic_load(ph + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tp += __hip_atomic_load(ph + 32 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (q >= 21) {  // b_schur
+                const int k = q - 21;
+                a.bp[6 * i1 + k] = th;  // the solve's computeScale reads it
+                a.bs[6 * i1 + k] = th - tp;
+                if (a.mfma_T) a.S[mfma_tile_pos(a.mfma_T, 6 * i1 + k, 16 * a.mfma_T)] = th - tp;
+            } else {  // diagonal block entry (rr, c), c >= rr: Hpp + lambda I - sum
+                int rr = 0, c = q;
+                while (c >= 6 - rr) { c -= 6 - rr; rr++; }
+                c += rr;
+                const double val = (th + (rr == c ? lam : 0.0)) - tp;
+                const int R = 6 * i1 + rr, Cc = 6 * i1 + c;
+                if (a.mfma_T) {  // the MFMA solve's tiles: diagonal tiles hold both triangles
+                    a.S[mfma_tile_pos(a.mfma_T, R, Cc)] = val;
+                    if ((R >> 4) == (Cc >> 4) && R != Cc) a.S[mfma_tile_pos(a.mfma_T, Cc, R)] = val;
+                } else {
+                    a.S[packed(R, Cc, N)] = val;
+                }
+            }
         }
         return;
     }
@@ -900,7 +974,7 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     const int i1 = pi1, i2 = pi2;
     if (i1 < 0 || i2 < 0) return;
     const bool diag = ka == kb;
-    if (diag) pose_rows_sum<21>(a, ka, 0, rows, ptot);  // Hpp of the keyframe (upper, row-major)
+    if (diag) return;  // the keyframe's block nblk + r forms it (above)
     double acc[36];
 #pragma unroll
     for (int q = 0; q < 36; q++) acc[q] = 0;
@@ -942,18 +1016,13 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     if (q < 36) {
         double t = 0;
         for (int w = 0; w < kSchurWaves; w++) t += red[w][q];
-        const int r = q / 6, c = q % 6;
+        const int r = q / 6, c = q % 6;  // an off-diagonal pose pair: -sum
         if (a.mfma_T) {  // the MFMA solve's tiles: diagonal tiles hold both triangles
             const int R = 6 * i1 + r, Cc = 6 * i2 + c;
-            if (!diag || c >= r) {
-                const double v = diag ? (ptot[packed(r, c, 6)] + (r == c ? lam : 0.0)) - t : -t;
-                a.S[mfma_tile_pos(a.mfma_T, R, Cc)] = v;
-                if ((R >> 4) == (Cc >> 4) && R != Cc) a.S[mfma_tile_pos(a.mfma_T, Cc, R)] = v;
-            }
-        } else if (!diag) {
+            a.S[mfma_tile_pos(a.mfma_T, R, Cc)] = -t;
+            if ((R >> 4) == (Cc >> 4)) a.S[mfma_tile_pos(a.mfma_T, Cc, R)] = -t;
+        } else {
             a.S[packed(6 * i1 + r, 6 * i2 + c, N)] = -t;
-        } else if (c >= r) {
-            a.S[packed(6 * i1 + r, 6 * i1 + c, N)] = (ptot[packed(r, c, 6)] + (r == c ? lam : 0.0)) - t;
         }
     }
 }
@@ -2450,7 +2519,7 @@ struct Runner {
 
     bool fuse_schur = false;  // k_ba_schur_solve (ORBMI_BA_FUSE=1; measured slower than two launches)
     void launch_mfma() {
-        const dim3 gs(a.nblk + a.nf + 1);
+        const dim3 gs(a.nblk + kSchurKfSplit * a.nf + 1);
         switch (mfma_tiles) {
 #define ORBMI_MFMA_CASE(T_)                                                                                      \
     case T_:                                                                                                     \
@@ -2494,7 +2563,8 @@ struct Runner {
     void step(int gen) {
         a.run_gen = gen;
         if (a.nblk > 0 && !(mfma_tiles > 0 && fuse_schur))  // (+ the MFMA solve's padding block)
-            hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + a.nf + (a.mfma_T > 0)), dim3(kSchurThreads), 0, h.stream, a);
+            hipLaunchKernelGGL(k_ba_schur, dim3(a.nblk + kSchurKfSplit * a.nf + (a.mfma_T > 0)), dim3(kSchurThreads), 0,
+                               h.stream, a);
         if (mfma_tiles > 0)
             launch_mfma();
         else if (solve_rows && solve_pipe)
@@ -2726,7 +2796,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
                  o_bs = take(8 * kBaMaxN), o_xp = take(8 * kBaMaxN), o_scal = take(64), o_plin = take(8 * (size_t)nb_e),
                  o_ptchi = take(8 * (size_t)nb_q), o_ptsc = take(8 * (size_t)nb_q),
                  o_pmax = take(8 * ((size_t)nb_p + kBaMaxPoses)), o_istat = take(32), o_ctl = take(sizeof(BaCtl)),
-                 o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne);
+                 o_otcw = take(64 * nkf), o_opos = take(12 * npt), o_oerase = take(ne),
+                 o_pkfs = take(8 * 64 * kSchurKfSplit * (size_t)kBaMaxPoses), o_arrkf = take(4 * kBaMaxPoses);
     if (off > h.cap) {
         if (h.d_buf) (void)hipFree(h.d_buf);
         h.d_buf = nullptr;
@@ -2764,6 +2835,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.edges = (const orbmi_ba_edge*)(B + o_edges);
     a.kf_order = (const int*)(B + o_order);
     a.free_kf = (const int*)(B + o_free);
+    a.part_kf = (double*)(B + o_pkfs);
+    a.arrive_kf = (unsigned*)(B + o_arrkf);
     a.pt_start = (const int*)(B + o_pts_start);
     a.kf_start = (const int*)(B + o_kfs_start);
     a.kf_edges = (const int*)(B + o_kf_edges);
