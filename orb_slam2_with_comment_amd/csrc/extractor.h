@@ -77,6 +77,7 @@ struct Extractor {
     long long pimg = 0;      // bytes of one padded pyramid
     long long bimg = 0;      // bytes of one blurred pyramid
     int keys_cap = 0, out_cap = 0;
+    bool describe_wave = false;  // ORBMI_DESC=wave: the one-keypoint-per-wave describe kernel
 
     // device buffers (capacity for `bcap` images)
     int bcap = 0;

@@ -8,6 +8,7 @@
 // Results are bit-exact with the pinned CPU restatement (oracle/, DESIGN.md "Pinned semantics").
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/orbmi_pattern.h"
@@ -1284,6 +1285,177 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     }
 }
 
+// Four keypoints per wave, one DPP row (16 lanes) each: the per-keypoint scalar work -- the
+// moment sums' reduction, fastAtan2, the fp64 sincos, the output record -- runs once for four
+// keypoints, and the lane-parallel parts keep their instruction count per keypoint:
+//   * IC_Angle (:77-104) straight from the unblurred level: the 749 patch pixels as <= 213
+//     aligned dwords (c_ictab[ou], per 4-B phase ou of the patch's first byte), each dword
+//     weighted by three v_dot4_u32_u8: (u + 16), (v + 16) and 1 on the circle's bytes, 0 off it,
+//     so m_10 = S_u - 16 S_1 and m_01 = S_v - 16 S_1 (integers: exact);
+//   * the blurred 37 x 37 window staged in LDS with 8-B loads (rows of kBP bytes);
+//   * rBRIEF (:108-147, pinned P6): lane l takes the pairs 16 l + k, k = 15 .. 0; the rotation
+//     in packed fp32 (the same products and sums, rounded as the reference's float expression),
+//     cvRound by adding 1.5 * 2^23 (round-half-even to an integer in the low mantissa bits, which
+//     index LDS directly), and the bits shifted into one 16-bit word per lane: lane l holds bytes
+//     2l, 2l+1 of its keypoint's descriptor.
+// A workgroup takes kDescKpWG consecutive slots per step and strides over the image's slots.
+constexpr int kDescGroups = 4;                        // keypoints per wave
+constexpr int kDescWaves = 4;                         // waves per workgroup
+constexpr int kDescKpWG = kDescGroups * kDescWaves;  // slots per workgroup step
+constexpr int kDescTargetWG = 1536;                   // workgroups per launch (3 per CU, 2 rounds)
+constexpr int kBP = 48;                               // LDS pitch: 37 bytes from any 8-B phase need 44
+constexpr int kBQ = kBP / 8;                          // 8-B loads per window row
+constexpr int kIcItems = 224;                         // IC dwords per phase (<= 213 used): 14 per lane
+struct DescLevel { long long off, boff; int stride, bstride, out_base; float scale, size; };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__constant__ float4 c_pattern_f[256];     // (x0, x1, y0, y1) of pair t = 16 l + k at 16 k + l
+__constant__ uint4 c_ictab[4][kIcItems];  // {u + 16 weights, circle mask, window row, 4 * dword}
+
+__device__ inline unsigned row16_sum(unsigned v) {  // sum over the lane's DPP row, in every lane
+    using namespace wave_detail;
+    v += (unsigned)dpp<0xB1>((int)v);
+    v += (unsigned)dpp<0x4E>((int)v);
+    v += (unsigned)dpp<0x141>((int)v);
+    return v + (unsigned)dpp<0x128>((int)v);
+}
+
+__global__ __launch_bounds__(64 * kDescWaves) void k_describe4(const uint8_t* __restrict__ pyr,
+                                                               const uint8_t* __restrict__ blur, long long pimg,
+                                                               long long bimg, const LevelGeom* __restrict__ levels,
+                                                               int nlevels, const uint2* __restrict__ oct_out,
+                                                               int oct_cap, const int* __restrict__ oct_count,
+                                                               orbmi_keypoint* __restrict__ kps,
+                                                               uint8_t* __restrict__ desc, int* __restrict__ counts,
+                                                               int capacity, int out_cap) {
+    __shared__ float4 spat[256];
+    __shared__ uint4 sic[4][kIcItems];
+    __shared__ DescLevel slv[kMaxLevels];
+    __shared__ int spre[kMaxLevels], scnt[kMaxLevels];
+    __shared__ __attribute__((aligned(16))) uint8_t swin[kDescKpWG][kBW * kBP];
+    const int b = blockIdx.y, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, grp = lane >> 4, l = lane & 15;
+    spat[tid] = c_pattern_f[tid];
+    for (int i = tid; i < 4 * kIcItems; i += 64 * kDescWaves) (&sic[0][0])[i] = (&c_ictab[0][0])[i];
+    const int* lc = oct_count + b * nlevels;
+    if (tid < nlevels) {
+        const LevelGeom& g = levels[tid];
+        slv[tid] = DescLevel{g.off, g.boff, g.stride, g.bstride, g.out_base, g.scale, g.size};
+        int pre = 0;
+        for (int q = 0; q < tid; q++) pre += lc[q];
+        spre[tid] = pre;
+        scnt[tid] = lc[tid];
+        if (blockIdx.x == 0 && tid == nlevels - 1) counts[b] = pre + lc[tid];
+    }
+    __syncthreads();
+    uint8_t* W = swin[wid * kDescGroups + grp];
+    const int nchunks = (out_cap + kDescKpWG - 1) / kDescKpWG;
+    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const int j = ch * kDescKpWG + wid * kDescGroups + grp;
+        int level = -1;
+        for (int q = 0; q < nlevels; q++)
+            if (j >= levels[q].out_base && j < levels[q].out_base + levels[q].out_cap) level = q;
+        const int lv = level < 0 ? 0 : level;
+        const DescLevel G = slv[lv];
+        const int idx = j - G.out_base;
+        const bool valid = level >= 0 && idx < scnt[lv];
+        if (__ballot(valid) == 0) continue;  // wave-uniform
+        int x = 0, y = 0;
+        unsigned resp = 0;
+        if (valid) {
+            const uint2 o = oct_out[(long long)b * oct_cap + j];
+            x = o.x & 0xFFFF;
+            y = o.x >> 16;
+            resp = o.y;
+        }
+        // the blurred window, rows of kBP bytes from its 8-B aligned start: lanes 0..11 of the
+        // group load 8-B column q = l % 6 of rows 2k + l / 6 (byte offsets inside the image's planes)
+        const uint8_t* bimgp = blur + (long long)b * bimg;
+        const uint8_t* pimgp = pyr + (long long)b * pimg;
+        const unsigned sb = (unsigned)G.boff + (unsigned)((y - kBR) * G.bstride + x - kBR);
+        const int ob = (int)(sb & 7);
+        if (valid && l < 2 * kBQ) {
+            const int par = l >= kBQ ? 1 : 0, q = l - par * kBQ;
+            const unsigned go = sb - ob + 8 * q + par * G.bstride;
+            uint8_t* wd = W + 8 * q + kBP * par;
+            constexpr int kPairs = (kBW + 1) / 2;
+            uint2 v[kPairs];
+#pragma unroll
+            for (int k = 0; k < kPairs; k++)
+                v[k] = (2 * k + par < kBW) ? *reinterpret_cast<const uint2*>(bimgp + go + 2 * k * G.bstride)
+                                           : make_uint2(0u, 0u);
+#pragma unroll
+            for (int k = 0; k < kPairs; k++)
+                if (2 * k + par < kBW) *reinterpret_cast<uint2*>(wd + 2 * kBP * k) = v[k];
+        }
+        // IC_Angle: the patch's dwords from the padded level, weighted by c_ictab[ou]
+        unsigned s_u = 0, s_v = 0, s_1 = 0;
+        if (valid) {
+            const unsigned su = (unsigned)G.off + (unsigned)((kEdge + y - kUR) * G.stride + kEdge + x - kUR);
+            const int ou = (int)(su & 3);
+            const unsigned sua = su - ou;
+            unsigned val[kIcItems / 16];
+            uint4 it[kIcItems / 16];
+#pragma unroll
+            for (int k = 0; k < kIcItems / 16; k++) {
+                it[k] = sic[ou][l + 16 * k];
+                val[k] = *reinterpret_cast<const unsigned*>(pimgp + (sua + __umul24(it[k].z, G.stride) + it[k].w));
+            }
+#pragma unroll
+            for (int k = 0; k < kIcItems / 16; k++) {
+                s_u = __builtin_amdgcn_udot4(val[k], it[k].x, s_u, false);
+                s_1 = __builtin_amdgcn_udot4(val[k], it[k].y, s_1, false);
+                // (v + 16) on the circle bytes: a packed 16-bit multiply (__umul24 would drop the top byte)
+                const u16x2 wv = __builtin_bit_cast(u16x2, it[k].y) * (unsigned short)(it[k].z + 1);
+                s_v = __builtin_amdgcn_udot4(val[k], __builtin_bit_cast(unsigned, wv), s_v, false);
+            }
+        }
+        s_u = row16_sum(s_u);
+        s_v = row16_sum(s_v);
+        s_1 = row16_sum(s_1);
+        const int m10 = (int)s_u - 16 * (int)s_1, m01 = (int)s_v - 16 * (int)s_1;
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        const float ang = angle * (float)(3.14159265358979323846 / 180.0);
+        double sd, cd;
+        orbmi_sincos_f64((double)ang, &sd, &cd);
+        const float ca = valid ? (float)cd : 1.f, sa = valid ? (float)sd : 0.f;
+        // the window stores of this wave visible to its reads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // rBRIEF: window (kBR + r, kBR + c) at W[ob + (kBR + r) kBP + kBR + c]; with r, c as the low
+        // bits of (value + 1.5 * 2^23) the constant part folds into kadd (uint32 wrap-around)
+        const float kMagic = 12582912.0f;
+        const unsigned kadd = (unsigned)(ob + kBR * kBP + kBR) - 0x400000u * (unsigned)kBP - 0x4B400000u;
+        unsigned word = 0;
+#pragma unroll
+        for (int k = 15; k >= 0; k--) {
+            const float4 P = spat[16 * k + l];  // pair 16 l + k (k-major: one iteration reads 256 contiguous bytes)
+            const f32x2 px = {P.x, P.y}, py = {P.z, P.w};
+            const f32x2 cx = (px * ca - py * sa) + kMagic;
+            const f32x2 ry = (px * sa + py * ca) + kMagic;
+            const unsigned i0 = __umul24(__float_as_uint(ry.x), (unsigned)kBP) + __float_as_uint(cx.x) + kadd;
+            const unsigned i1 = __umul24(__float_as_uint(ry.y), (unsigned)kBP) + __float_as_uint(cx.y) + kadd;
+            word = 2 * word + (W[i0] < W[i1] ? 1u : 0u);
+        }
+        if (valid && spre[lv] + idx < capacity) {
+            const long long oi = (long long)b * capacity + spre[lv] + idx;
+            reinterpret_cast<unsigned short*>(desc + oi * 32)[l] = (unsigned short)word;
+            if (l == 0) {
+                orbmi_keypoint kp;
+                kp.x = level == 0 ? (float)x : (float)x * G.scale;
+                kp.y = level == 0 ? (float)y : (float)y * G.scale;
+                kp.size = G.size;
+                kp.angle = angle;
+                kp.response = (float)resp;
+                kp.octave = level;
+                kp.class_id = -1;
+                kps[oi] = kp;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ host
 static int cv_round_host(float v) { return (int)lrintf(v); }
 
@@ -1326,6 +1498,34 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
     ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBMI_PATTERN, sizeof(ORBMI_PATTERN)));
     ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_circle), circ, sizeof(circ)));
     ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ncircle), &nc, sizeof(int)));
+    {   // k_describe4's tables: the pattern as (x0, x1, y0, y1) floats, and per 4-B phase ou of
+        // the IC patch's first byte the dwords covering each circle row with their byte weights
+        float4 pf[256];
+        for (int t = 0; t < 256; t++)  // pair t = 16 l + k at 16 k + l
+            pf[16 * (t & 15) + (t >> 4)] =
+                make_float4(ORBMI_PATTERN[t][0], ORBMI_PATTERN[t][2], ORBMI_PATTERN[t][1], ORBMI_PATTERN[t][3]);
+        ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern_f), pf, sizeof(pf)));
+        static uint4 ic[4][kIcItems];
+        memset(ic, 0, sizeof(ic));
+        for (int ou = 0; ou < 4; ou++) {
+            int n = 0;
+            for (int v = -kHalfPatch; v <= kHalfPatch; v++) {
+                const int d = umax[v < 0 ? -v : v], r = v + kHalfPatch;
+                for (int dd = (ou + kHalfPatch - d) / 4; dd <= (ou + kHalfPatch + d) / 4; dd++) {
+                    if (n >= kIcItems) return ORBMI_E_ARG;
+                    unsigned wa = 0, wm = 0;
+                    for (int p = 0; p < 4; p++) {
+                        const int u = 4 * dd + p - ou - kHalfPatch;
+                        if (u >= -d && u <= d) { wa |= (unsigned)(u + 16) << (8 * p); wm |= 1u << (8 * p); }
+                    }
+                    ic[ou][n++] = make_uint4(wa, wm, (unsigned)r, (unsigned)(4 * dd));
+                }
+            }
+        }
+        ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ictab), ic, sizeof(ic)));
+        const char* e = getenv("ORBMI_DESC");
+        describe_wave = e && !strcmp(e, "wave");
+    }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
     ORBMI_HIP(hipMalloc((void**)&d_scale_tab, tab.size() * sizeof(float)));
@@ -1675,8 +1875,15 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         prof_end(ORBMI_STAGE_BLUR, ev);
     }
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
-    hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
-                       d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity);
+    if (describe_wave)  // ORBMI_DESC=wave: one keypoint per wave (A/B)
+        hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
+                           d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity);
+    else {
+        const int nch = (out_cap + kDescKpWG - 1) / kDescKpWG;
+        const int gx = std::max(1, std::min(nch, (kDescTargetWG + batch - 1) / batch));
+        hipLaunchKernelGGL(k_describe4, dim3(gx, batch), dim3(64 * kDescWaves), 0, stream, d_pyr, d_blur, pimg, bimg,
+                           d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity, out_cap);
+    }
     prof_end(ORBMI_STAGE_DESCRIBE, ev);
     ORBMI_HIP(hipGetLastError());
     last_batch = batch;

@@ -26,6 +26,7 @@
 #   solvetrace[=VAR=1]  per-step split of the reduced-system solve (tools/ubench/solve_trace)
 #   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
+#   descab           config 5: four keypoints per wave in k_describe vs one (ORBMI_DESC=wave)
 TAG=${1:-run}
 shift
 OUT=gpurun_out/$TAG
@@ -218,6 +219,15 @@ for step in "$@"; do
                 python3 -c "import csv,collections,sys; d=collections.defaultdict(list); [d[r['Kernel_Name'][:40]].append(float(r['Counter_Value'])) for r in csv.DictReader(open(sys.argv[1])) if r['Counter_Name']=='FETCH_SIZE']; [print(sys.argv[2], k, len(v), round(2*sum(v)/len(v)/1024,3), 'MB (2 x FETCH_SIZE)') for k,v in sorted(d.items()) if 'ba_' in k]" $f $v | tee -a $OUT/schurxcd.txt
             done
             cp $OUT/schurxcd.txt $P/;;
+        descab)
+            # config 5 batch: the four-keypoints-per-wave describe (default) vs one keypoint per
+            # wave (ORBMI_DESC=wave), 2 alternations
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["stage_ms_per_launch"])'; }
+            for i in 1 2; do
+                run descab_4_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                ORBMI_DESC=wave run descab_w_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                echo "4/wave: $(v descab_4_$i) | 1/wave: $(v descab_w_$i)" | tee -a $OUT/descab.txt
+            done; cp $OUT/descab.txt $P/;;
         profenv=*)
             # rocprofv3 kernel stats of --mode lba under an environment setting: profenv=VAR=VALUE
             kv=${step#profenv=}; tag=$(echo $kv | tr '=' '_')
