@@ -78,6 +78,7 @@ struct Extractor {
     long long bimg = 0;      // bytes of one blurred pyramid
     int keys_cap = 0, out_cap = 0;
     bool describe_wave = false;  // ORBMI_DESC=wave: the one-keypoint-per-wave describe kernel
+    bool fast_v1 = false;        // ORBMI_FAST=v1: the per-lane FAST kernel
 
     // device buffers (capacity for `bcap` images)
     int bcap = 0;

@@ -533,6 +533,209 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
     }
 }
 
+// k_fast2: k_fast with fewer VALU instructions per cell (k_fast issues ≈2,900 per cell and is
+// VALU-issue-bound).  The ROI tile and the score map have a compile-time pitch TS, so every
+// circle / compass / NMS neighbour read is one ds_read_u8 with an immediate offset from the
+// pixel's address, and the list holds tile offsets (y TS + x) rather than packed coordinates;
+// each circle comparison enters the lane's 16-bit mask with one compare and one add-with-carry;
+// the arc test is doubling on the mask (runs of 2, 4, 8, 9).  The compass pre-test combines its
+// eight compares as lane masks.  Measured alternatives (profiles/r04/fast_seg_ab.txt): the arc
+// test bit-sliced across the wave on the scalar unit (79 SALU ops per polarity for 64 pixels)
+// cut the VALU count by 40 % but made the kernel slower, 0.327 vs 0.307 ms per 64 frames: the
+// scalar unit issues at the same per-SIMD rate as the vector unit.  Stages, order and outputs
+// are k_fast's.
+// m * 2 + (a > b): the compare's lane mask is the add's carry-in (two VALU ops per bit; the
+// compiler's own form is compare, select, shift-or)
+__device__ inline unsigned shift_in_gt(unsigned m, int a, int b) {
+    unsigned r;
+    asm("v_cmp_gt_i32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc" : "=v"(r) : "v"(a), "v"(b), "v"(m) : "vcc");
+    return r;
+}
+
+// FAST's arc test on one lane's 16-bit circle mask (bit k = circle pixel k): runs of 2, 4, 8, 9
+// by doubling on m | m << 16 (a cyclic run starting at s < 16 is bits s .. s + 8).
+__device__ inline bool fast_arc9_word(unsigned m) {
+    unsigned x = m | (m << 16);
+    x &= x >> 1;
+    x &= x >> 2;
+    x &= x >> 4;
+    x &= x >> 1;
+    return (x & 0xFFFFu) != 0;
+}
+
+// The segment test of every lane's pixel: cm = the pixel at (X - 3, Y - 3) of the tile (pitch
+// TS), so all 17 reads take non-negative immediate offsets.  The caller masks inactive lanes.
+template <int TS>
+__device__ inline bool fast_segment_lane(const uint8_t* cm, int th) {
+    constexpr int o[16] = {6 * TS + 3, 6 * TS + 4, 5 * TS + 5, 4 * TS + 6, 3 * TS + 6, 2 * TS + 6, TS + 5, 4,
+                           3, 2, TS + 1, 2 * TS, 3 * TS, 4 * TS, 5 * TS + 1, 6 * TS + 2};
+    int p[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) p[k] = cm[o[k]];
+    const int v = cm[3 * TS + 3], hi = v + th, lo = v - th;
+    unsigned mb = 0, md = 0;
+#pragma unroll
+    for (int k = 15; k >= 0; k--) {
+        mb = shift_in_gt(mb, p[k], hi);
+        md = shift_in_gt(md, lo, p[k]);
+    }
+    return fast_arc9_word(mb) || fast_arc9_word(md);
+}
+
+constexpr int fast2_tile_bytes(int TS, int maxH) { return (TS * maxH + 15) & ~15; }
+__host__ __device__ inline int fast2_wave_bytes(int TS, int maxW, int maxH) {
+    return 2 * fast2_tile_bytes(TS, maxH) + ((2 * (maxW - 6) * (maxH - 6) + 15) & ~15);
+}
+
+template <int TS>
+__global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __restrict__ pyr, long long pimg,
+                                                           const CellGeom* __restrict__ cells, int ncells,
+                                                           uint2* __restrict__ cand, int keys_cap,
+                                                           int* __restrict__ level_count, int nlevels, int ini_th,
+                                                           int min_th, int maxW, int maxH) {
+    extern __shared__ uint4 fast_lds[];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * kFastCells + wid, b = blockIdx.y;
+    if (c >= ncells) return;
+    const CellGeom cg = cells[c];
+    if (cg.w == 0) return;
+    const long long a = b * pimg + cg.roi_off;
+    const int o = (int)(a & 3);  // stride is a multiple of 64: the same offset on every row
+    const unsigned* src = reinterpret_cast<const unsigned*>(pyr + (a - o));
+    const int w = cg.w, h = cg.h, nd = (w + o + 3) >> 2, s4 = cg.stride >> 2;
+    const int tbytes = fast2_tile_bytes(TS, maxH), lcap = (maxW - 6) * (maxH - 6);
+    uint8_t* wl = reinterpret_cast<uint8_t*>(fast_lds) + wid * fast2_wave_bytes(TS, maxW, maxH);
+    unsigned* t4 = reinterpret_cast<unsigned*>(wl);
+    uint8_t* sc = wl + tbytes;  // scores, sc[y * TS + x]
+    unsigned short* L = reinterpret_cast<unsigned short*>(wl + 2 * tbytes);
+    {   // lane = (row phase r0, dword d) of the tile, R rows per round: one division per lane
+        const int R = 64 / nd, r0 = lane / nd, d = lane - r0 * nd;
+        if (r0 < R) {
+            constexpr int kLd = 8;
+            for (int rb = r0; rb < h; rb += kLd * R) {
+                unsigned v[kLd];
+#pragma unroll
+                for (int k = 0; k < kLd; k++) {
+                    const int r = rb + k * R;
+                    v[k] = r < h ? src[(long long)r * s4 + d] : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < kLd; k++) {
+                    const int r = rb + k * R;
+                    if (r < h) t4[r * (TS / 4) + d] = v[k];
+                }
+            }
+        }
+    }
+    for (int k = lane; k < tbytes / 16; k += 64) reinterpret_cast<uint4*>(sc)[k] = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync_lds_ex();
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * TS + x]
+    const int dw = w - 6, dh = h - 6, npix = dw > 0 && dh > 0 ? dw * dh : 0;
+    const int ti = min(max(ini_th, 0), 255), tm = min(max(min_th, 0), 255), tl = min(ti, tm);
+    // A: compass pre-test over the ROI's scored pixels, row-major
+    int n = 0;
+    if (npix > 0) {
+        int y = lane / dw, x = lane - y * dw;
+        const int q = 64 / dw, r = 64 - q * dw;
+        for (int p0 = 0; p0 < npix; p0 += 64) {
+            // lanes past the last pixel read the ROI's last row (masked off below)
+            const int e0 = __umul24(min(y, dh - 1), TS) + x + 3;  // the pixel at (X, Y - 3)
+            const uint8_t* cp = tb + e0;
+            const int pc = cp[0], pd = cp[3 * TS - 3], v = cp[3 * TS], pb = cp[3 * TS + 3], pa = cp[6 * TS];
+            const int hi = v + tl, lo = v - tl;
+            const bool ba = pa > hi, bb = pb > hi, bc = pc > hi, bd = pd > hi;
+            const bool da = pa < lo, db = pb < lo, dc = pc < lo, dd = pd < lo;
+            const bool pass = (((ba | bc) & (bb | bd)) | ((da | dc) & (db | dd))) && p0 + lane < npix;
+            const unsigned long long m = __ballot(pass);
+            if (pass) L[n + lanes_below(m)] = (unsigned short)(e0 + 3 * TS);
+            n += __popcll(m);
+            x += r;
+            y += q;
+            if (x >= dw) { x -= dw; y++; }
+        }
+    }
+    wave_sync_lds_ex();
+    // B: full segment test at tl, compacted in place (a lane writes at or below the entry it read)
+    auto segment_pass = [&](const unsigned short* Ls, int ns, unsigned short* Ld, int th) {
+        int kept = 0;
+        for (int i0 = 0; i0 < ns; i0 += 64) {
+            const int i = i0 + lane;
+            const unsigned short e = Ls[min(i, ns - 1)];  // the last lanes repeat an entry, masked off
+            const bool pass = fast_segment_lane<TS>(tb + e - (3 * TS + 3), th) && i < ns;
+            const unsigned long long m = __ballot(pass);
+            if (pass) Ld[kept + lanes_below(m)] = e;
+            kept += __popcll(m);
+        }
+        wave_sync_lds_ex();
+        return kept;
+    };
+    const int nc = segment_pass(L, n, L, tl);
+    // B': the corners at ini_th among them, listed after them (see k_fast)
+    const bool split = ti > tl && nc > 64 && 2 * nc <= lcap;
+    unsigned short* LH = L;
+    int nh = nc;
+    if (split) {
+        LH = L + nc;
+        nh = segment_pass(L, nc, LH, ti);
+    }
+    auto score = [&](const unsigned short* Ls, int ns) {
+        for (int i = lane; i < ns; i += 64) {
+            const unsigned short e = Ls[i];
+            int p[16];
+            fast_circle(tb + e, TS, 0, 0, p);
+            sc[e] = (uint8_t)fast_corner_score(tb[e], p, tl);
+        }
+        wave_sync_lds_ex();
+    };
+    auto nms = [&](unsigned short* Ls, int ns, int t) {
+        int kept = 0;
+        for (int i0 = 0; i0 < ns; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            unsigned short e = 0;
+            if (i < ns) {
+                e = Ls[i];
+                const uint8_t* q = sc + e;
+                const int s = q[0];
+                if (s >= t && s != 0) {
+                    auto nb = [&](int off) {
+                        const int u = q[off];
+                        return u >= t ? u : 0;
+                    };
+                    keep = s > nb(-TS - 1) && s > nb(-TS) && s > nb(-TS + 1) && s > nb(-1) && s > nb(1) &&
+                           s > nb(TS - 1) && s > nb(TS) && s > nb(TS + 1);
+                }
+            }
+            const unsigned long long m = __ballot(keep);
+            if (keep) Ls[kept + lanes_below(m)] = e;
+            kept += __popcll(m);
+        }
+        return kept;
+    };
+    score(LH, nh);
+    int total = nms(LH, nh, ti);
+    const unsigned short* LO = LH;
+    if (total == 0 && tm != ti) {
+        if (split) score(L, nc);
+        total = nms(L, nc, tm);
+        LO = L;
+    }
+    if (total == 0) return;
+    wave_sync_lds_ex();
+    int base = 0;
+    if (lane == 0)
+        base = atomicAdd(&level_count[(b * nlevels + cg.level) * kFastRegions + cg.lcell % kFastRegions], total);
+    base = __shfl(base, 0);
+    uint2* dst = cand + (long long)b * keys_cap + cg.slot_base + base;
+    const unsigned tag = (unsigned)cg.lcell << 10;
+    for (int i = lane; i < total; i += 64) {
+        const unsigned short e = LO[i];
+        const int Y = e / TS, X = e - Y * TS;
+        dst[i] = make_uint2((uint32_t)(X + cg.sx) | ((uint32_t)(Y + cg.sy) << 12) | ((uint32_t)sc[e] << 24),
+                            tag | (unsigned)i);
+    }
+}
+
 // ------------------------------------------------------------------------------ octree
 // DistributeOctTree (src/ORBextractor.cc:539-763) as data-parallel passes inside one
 // workgroup per (image, level).  The std::list of nodes is kept as arrays in list order:
@@ -1525,6 +1728,8 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         ORBMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ictab), ic, sizeof(ic)));
         const char* e = getenv("ORBMI_DESC");
         describe_wave = e && !strcmp(e, "wave");
+        e = getenv("ORBMI_FAST");
+        fast_v1 = e && !strcmp(e, "v1");
     }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
@@ -1855,9 +2060,19 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
-    hipLaunchKernelGGL(k_fast, dim3((ncells + kFastCells - 1) / kFastCells, batch), dim3(64 * kFastCells),
-                       kFastCells * fast_wave_bytes, stream, d_pyr, pimg, d_levels, d_cells, ncells, d_cand, keys_cap,
-                       d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+    {
+        const dim3 grid((ncells + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
+        if (fast_v1)  // ORBMI_FAST=v1: per-lane bit assembly, runtime tile pitch (A/B)
+            hipLaunchKernelGGL(k_fast, grid, block, kFastCells * fast_wave_bytes, stream, d_pyr, pimg, d_levels, d_cells,
+                               ncells, d_cand, keys_cap, d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+        else {
+            const bool narrow = fast_maxw + 3 <= 48;
+            const size_t lds = kFastCells * fast2_wave_bytes(narrow ? 48 : 80, fast_maxw, fast_maxh);
+            auto* kf = narrow ? k_fast2<48> : k_fast2<80>;
+            hipLaunchKernelGGL(kf, grid, block, lds, stream, d_pyr, pimg, d_cells, ncells, d_cand, keys_cap,
+                               d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+        }
+    }
     prof_end(ORBMI_STAGE_FAST, ev);
     // small batches: the blur runs inside the octree launch on the CUs its nlevels x batch
     // workgroups leave idle; large batches fill the chip with octrees, so the blur gets its own

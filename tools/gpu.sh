@@ -27,6 +27,8 @@
 #   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 #   descab           config 5: four keypoints per wave in k_describe vs one (ORBMI_DESC=wave)
+#   fastab           config 5: bit-sliced k_fast2 vs the per-lane k_fast (ORBMI_FAST=v1)
+#   fastseg          config 5: k_fast2's arc-test splits (ORBMI_FAST_SEG=0/1/2) and k_fast
 TAG=${1:-run}
 shift
 OUT=gpurun_out/$TAG
@@ -228,6 +230,26 @@ for step in "$@"; do
                 ORBMI_DESC=wave run descab_w_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
                 echo "4/wave: $(v descab_4_$i) | 1/wave: $(v descab_w_$i)" | tee -a $OUT/descab.txt
             done; cp $OUT/descab.txt $P/;;
+        fastab)
+            # config 5 batch: bit-sliced FAST (default) vs the per-lane kernel (ORBMI_FAST=v1)
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["stage_ms_per_launch"]["fast"])'; }
+            for i in 1 2; do
+                run fastab_2_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                ORBMI_FAST=v1 run fastab_1_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                echo "sliced: $(v fastab_2_$i) | per-lane: $(v fastab_1_$i)" | tee -a $OUT/fastab.txt
+            done; cp $OUT/fastab.txt $P/;;
+        fastseg)
+            # config 5 batch: k_fast2's arc-test split (ORBMI_FAST_SEG=0 scalar, 1 per lane, 2 mixed)
+            # and the per-lane k_fast (ORBMI_FAST=v1), 2 alternations
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["stage_ms_per_launch"]["fast"])'; }
+            for i in 1 2; do
+                for sg in 0 1 2; do
+                    ORBMI_FAST_SEG=$sg run fastseg_${sg}_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                    echo "seg $sg: $(v fastseg_${sg}_$i)" | tee -a $OUT/fastseg.txt
+                done
+                ORBMI_FAST=v1 run fastseg_v1_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                echo "v1: $(v fastseg_v1_$i)" | tee -a $OUT/fastseg.txt
+            done; cp $OUT/fastseg.txt $P/;;
         profenv=*)
             # rocprofv3 kernel stats of --mode lba under an environment setting: profenv=VAR=VALUE
             kv=${step#profenv=}; tag=$(echo $kv | tr '=' '_')
