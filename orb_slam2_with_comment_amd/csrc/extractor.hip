@@ -1267,22 +1267,24 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
     const int cq = 4 * (tid & 31), rb = 4 * (tid >> 5);  // 4 columns x 4 output rows per thread
     if (y0 + rb >= g.H) return;
     const unsigned* in = reinterpret_cast<const unsigned*>(in4);
-    int rs[10][4];  // row sums of input rows rb .. rb + 9 (output row rb + rr reads rb + rr .. + 6)
+    // row pass: the 7 taps of column cq + c are bytes c .. c + 6 of (w0, w1, w2): two v_dot4
+    // over byte-aligned dwords (v_alignbyte), weights (18, 34, 49, 55) and (49, 34, 18, 0)
+    constexpr unsigned kW0 = 18u | 34u << 8 | 49u << 16 | 55u << 24, kW1 = 49u | 34u << 8 | 18u << 16;
+    unsigned rs[10][4];  // row sums of input rows rb .. rb + 9 (output row rb + rr reads rb + rr .. + 6)
 #pragma unroll
     for (int r = 0; r < 10; r++) {
         const unsigned* q = in + (rb + r) * (kBlurInS / 4) + cq / 4;  // bytes = input columns cq - 3 ..
         const unsigned w0 = q[0], w1 = q[1], w2 = q[2];
-        int v[12];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            v[k] = (w0 >> (8 * k)) & 255;
-            v[4 + k] = (w1 >> (8 * k)) & 255;
-            v[8 + k] = (w2 >> (8 * k)) & 255;
+        for (int c = 0; c < 4; c++) {
+            const unsigned a = c ? __builtin_amdgcn_alignbyte(w1, w0, c) : w0;
+            const unsigned h = c ? __builtin_amdgcn_alignbyte(w2, w1, c) : w1;
+            rs[r][c] = __builtin_amdgcn_udot4(h, kW1, __builtin_amdgcn_udot4(a, kW0, 0u, false), false);
         }
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-            rs[r][c] = 55 * v[c + 3] + 49 * (v[c + 2] + v[c + 4]) + 34 * (v[c + 1] + v[c + 5]) + 18 * (v[c] + v[c + 6]);
     }
+    // column pass: S = 55 c3 + 49 p1 + 34 p2 + 18 p3 < 2^24 unless the result saturates, so the
+    // reference's float path (SymmColumnVec_32s8u: S / 65536 in float, one rounding per operation,
+    // then rint) is exact: round-half-even of S / 65536; the scalar tail rounds half up
     uint8_t* dst = blur + b * bimg + g.boff;
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
@@ -1292,19 +1294,11 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
             const int x = x0 + cq + cc;
-            const int c3 = rs[rr + 3][cc], p1 = rs[rr + 2][cc] + rs[rr + 4][cc], p2 = rs[rr + 1][cc] + rs[rr + 5][cc],
-                      p3 = rs[rr][cc] + rs[rr + 6][cc];
-            int v;
-            if (x < g.blur_xv) {  // SymmColumnVec_32s8u float path
-                float sacc = (float)c3 * (55.f / 65536.f) + 0.0f;
-                sacc = sacc + (float)p1 * (49.f / 65536.f);
-                sacc = sacc + (float)p2 * (34.f / 65536.f);
-                sacc = sacc + (float)p3 * (18.f / 65536.f);
-                v = (int)__builtin_rintf(sacc);
-            } else {
-                v = (c3 * 55 + p1 * 49 + p2 * 34 + p3 * 18 + (1 << 15)) >> 16;
-            }
-            packedv |= (unsigned)(v < 0 ? 0 : (v > 255 ? 255 : v)) << (8 * cc);
+            const unsigned S = __umul24(rs[rr + 3][cc], 55u) + __umul24(rs[rr + 2][cc] + rs[rr + 4][cc], 49u) +
+                               __umul24(rs[rr + 1][cc] + rs[rr + 5][cc], 34u) + __umul24(rs[rr][cc] + rs[rr + 6][cc], 18u);
+            const unsigned up = x < g.blur_xv ? (S >> 16) & 1u : 1u;
+            const unsigned v = min((S + 0x7FFFu + up) >> 16, 255u);
+            packedv |= v << (8 * cc);
         }
         if (x0 + cq < g.bstride)
             *reinterpret_cast<unsigned*>(dst + (long long)y * g.bstride + x0 + cq) = packedv;
