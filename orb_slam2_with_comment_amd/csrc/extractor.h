@@ -79,6 +79,9 @@ struct Extractor {
     int keys_cap = 0, out_cap = 0;
     bool describe_wave = false;  // ORBMI_DESC=wave: the one-keypoint-per-wave describe kernel
     bool fast_v1 = false;        // ORBMI_FAST=v1: the per-lane FAST kernel
+    int blur_mode = 0;           // GaussianBlur: 0 side stream (default), 1 in the octree launch, 2 after it
+    hipStream_t bstream = nullptr;  // the blur's side stream
+    hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
 
     // device buffers (capacity for `bcap` images)
     int bcap = 0;
@@ -130,8 +133,8 @@ struct Extractor {
     std::vector<ProfPair> prof_pending;
     std::vector<hipEvent_t> prof_pool;
     hipEvent_t prof_event();
-    hipEvent_t prof_begin(int stage);
-    void prof_end(int stage, hipEvent_t a);
+    hipEvent_t prof_begin(int stage, hipStream_t s = nullptr);
+    void prof_end(int stage, hipEvent_t a, hipStream_t s = nullptr);
 
     int init(int dev, int nf, float sf, int nl, int ini, int mn);
     int set_geometry(int rows, int cols);

@@ -1305,12 +1305,12 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
     }
 }
 
-// DistributeOctTree and GaussianBlur in one launch: blocks [0, nlevels) run one pyramid level's
-// octree each (16 workgroups for a stereo pair), the remaining blocks blur four 128x32 tiles
-// each on the CUs the octree leaves idle.  Both only read the pyramid; the blur slices reuse
-// the octree's LDS.
+// DistributeOctTree and GaussianBlur in one launch, on a 1-D grid: blocks [0, nlevels x batch)
+// run one (image, level) octree each and are dispatched first; the blocks after them blur four
+// 128x32 tiles each on the CUs the octrees leave idle.  A level-0 octree is the launch's longest
+// workgroup (its candidates are the most), so the blur hides behind it instead of following it.
+// Both only read the pyramid; the blur slices reuse the octree's LDS.
 static_assert(sizeof(OctShared) >= 4 * sizeof(BlurShared), "blur slices overlay the octree LDS");
-constexpr int kFuseBlurMaxOctrees = 64;  // octree workgroups up to which the blur rides along
 __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restrict__ levels, int nlevels,
                                                          const uint2* __restrict__ cand,
                                                          const int* __restrict__ level_count,
@@ -1319,17 +1319,19 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
                                                          int keys_cap, uint2* __restrict__ oct_out, int out_cap,
                                                          int* __restrict__ oct_count, const uint8_t* __restrict__ pyr,
                                                          uint8_t* __restrict__ blur, long long pimg, long long bimg,
-                                                         const int2* __restrict__ btiles, int nbtiles) {
+                                                         const int2* __restrict__ btiles, int nbtiles, int batch) {
     __shared__ OctShared S;
-    if ((int)blockIdx.x < nlevels) {
-        octree_body(S, blockIdx.x, blockIdx.y, levels, nlevels, cand, level_count, regbase, node_of, keys_cap, oct_out,
-                    out_cap, oct_count);
+    const int noct = nlevels * batch;
+    if ((int)blockIdx.x < noct) {
+        octree_body(S, blockIdx.x % nlevels, blockIdx.x / nlevels, levels, nlevels, cand, level_count, regbase, node_of,
+                    keys_cap, oct_out, out_cap, oct_count);
         return;
     }
-    const int slice = threadIdx.x >> 8, ti = ((int)blockIdx.x - nlevels) * 4 + slice;
+    const int slice = threadIdx.x >> 8, ti = ((int)blockIdx.x - noct) * 4 + slice;  // over (image, tile)
+    const bool valid = ti < nbtiles * batch;
+    const int img = valid ? ti / nbtiles : 0, tile = valid ? ti - img * nbtiles : 0;
     BlurShared* B = reinterpret_cast<BlurShared*>(&S) + slice;
-    blur_tile(*B, pyr, blur, pimg, bimg, levels, ti < nbtiles ? btiles[ti] : make_int2(0, 0), blockIdx.y,
-              threadIdx.x & 255, ti < nbtiles);
+    blur_tile(*B, pyr, blur, pimg, bimg, levels, btiles[tile], img, threadIdx.x & 255, valid);
 }
 
 // GaussianBlur alone: one 128x32 tile per 256-thread workgroup.
@@ -1661,6 +1663,9 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
     device = dev; nfeatures = nf; scale_factor = sf; nlevels = nl; ini_th = ini; min_th = mn;
     ORBMI_HIP(hipSetDevice(device));
     ORBMI_HIP(orbmi::stream_create(&stream, "EXTRACTOR"));
+    ORBMI_HIP(orbmi::stream_create(&bstream, "EXTRACTOR"));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_pyr, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_blur, hipEventDisableTiming));
     // ORBextractor::ORBextractor  src/ORBextractor.cc:410-470 (same float/double steps)
     scale.assign(nl, 1.f); sigma2.assign(nl, 1.f); inv_scale.resize(nl); inv_sigma2.resize(nl);
     const double sfd = (double)sf;
@@ -1724,6 +1729,8 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         describe_wave = e && !strcmp(e, "wave");
         e = getenv("ORBMI_FAST");
         fast_v1 = e && !strcmp(e, "v1");
+        e = getenv("ORBMI_BLUR");
+        blur_mode = !e ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2 : 0;
     }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
@@ -2053,6 +2060,18 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                            pyr_hy, d_level_count, pyr_lds0, pyr_lds_half);
         prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
+    // GaussianBlur needs only the pyramid: by default it runs on a side stream (bstream) beside
+    // FAST and the octrees -- whose tail leaves most CUs idle -- and the describe waits for it.
+    // ORBMI_BLUR=fused: as extra workgroups of the octree launch; ORBMI_BLUR=serial: after it.
+    if (blur_mode == 0) {
+        ORBMI_HIP(hipEventRecord(ev_pyr, stream));
+        ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
+        hipEvent_t eb = prof_begin(ORBMI_STAGE_BLUR, bstream);
+        hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, bstream, d_pyr, d_blur, pimg, bimg, d_levels,
+                           d_btiles);
+        prof_end(ORBMI_STAGE_BLUR, eb, bstream);
+        ORBMI_HIP(hipEventRecord(ev_blur, bstream));
+    }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
     {
         const dim3 grid((ncells + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
@@ -2068,21 +2087,20 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         }
     }
     prof_end(ORBMI_STAGE_FAST, ev);
-    // small batches: the blur runs inside the octree launch on the CUs its nlevels x batch
-    // workgroups leave idle; large batches fill the chip with octrees, so the blur gets its own
-    // launch at full occupancy
-    const bool fuse_blur = batch * nlevels <= kFuseBlurMaxOctrees;
     ev = prof_begin(ORBMI_STAGE_OCTREE);
-    hipLaunchKernelGGL(k_octree, dim3(nlevels + (fuse_blur ? (nbtiles + 3) / 4 : 0), batch), dim3(kOctThreads), 0, stream,
-                       d_levels, nlevels, d_cand, d_level_count, d_regbase, d_node_of, keys_cap, d_oct, out_cap, d_oct_count, d_pyr,
-                       d_blur, pimg, bimg, d_btiles, nbtiles);
+    const bool fused = blur_mode == 1;
+    const int blur_blocks = fused ? (nbtiles * batch + 3) / 4 : 0;
+    hipLaunchKernelGGL(k_octree, dim3(nlevels * batch + blur_blocks), dim3(kOctThreads), 0, stream, d_levels, nlevels,
+                       d_cand, d_level_count, d_regbase, d_node_of, keys_cap, d_oct, out_cap, d_oct_count, d_pyr, d_blur,
+                       pimg, bimg, d_btiles, fused ? nbtiles : 0, batch);
     prof_end(ORBMI_STAGE_OCTREE, ev);
-    if (!fuse_blur) {
+    if (blur_mode == 2) {
         ev = prof_begin(ORBMI_STAGE_BLUR);
         hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg, d_levels,
                            d_btiles);
         prof_end(ORBMI_STAGE_BLUR, ev);
     }
+    if (blur_mode == 0) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
     if (describe_wave)  // ORBMI_DESC=wave: one keypoint per wave (A/B)
         hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
@@ -2107,18 +2125,18 @@ hipEvent_t Extractor::prof_event() {
     return e;
 }
 
-hipEvent_t Extractor::prof_begin(int stage) {
+hipEvent_t Extractor::prof_begin(int stage, hipStream_t s) {
     if (!(prof_mask >> stage & 1u)) return nullptr;
     hipEvent_t a = prof_event();
-    if (a) (void)hipEventRecord(a, stream);
+    if (a) (void)hipEventRecord(a, s ? s : stream);
     return a;
 }
 
-void Extractor::prof_end(int stage, hipEvent_t a) {
+void Extractor::prof_end(int stage, hipEvent_t a, hipStream_t s) {
     if (!a) return;
     hipEvent_t b = prof_event();
     if (!b) return;
-    (void)hipEventRecord(b, stream);
+    (void)hipEventRecord(b, s ? s : stream);
     prof_pending.push_back(ProfPair{stage, a, b});
 }
 
@@ -2135,6 +2153,11 @@ void Extractor::release() {
         if (p) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
+    if (bstream) (void)hipStreamDestroy(bstream);
+    bstream = nullptr;
+    if (ev_pyr) (void)hipEventDestroy(ev_pyr);
+    if (ev_blur) (void)hipEventDestroy(ev_blur);
+    ev_pyr = ev_blur = nullptr;
 }
 
 }  // namespace orbmi

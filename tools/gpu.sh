@@ -28,7 +28,7 @@
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 #   descab           config 5: four keypoints per wave in k_describe vs one (ORBMI_DESC=wave)
 #   fastab           config 5: bit-sliced k_fast2 vs the per-lane k_fast (ORBMI_FAST=v1)
-#   fastseg          config 5: k_fast2's arc-test splits (ORBMI_FAST_SEG=0/1/2) and k_fast
+#   blurab           config 5: GaussianBlur on a side stream / in the octree launch / after it
 TAG=${1:-run}
 shift
 OUT=gpurun_out/$TAG
@@ -250,6 +250,15 @@ for step in "$@"; do
                 ORBMI_FAST=v1 run fastseg_v1_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
                 echo "v1: $(v fastseg_v1_$i)" | tee -a $OUT/fastseg.txt
             done; cp $OUT/fastseg.txt $P/;;
+        blurab)
+            # config 5 batch: GaussianBlur on a side stream (default) / inside the octree launch / after it
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"])'; }
+            for i in 1 2; do
+                for m in side fused serial; do
+                    ORBMI_BLUR=$m run blurab_${m}_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                    echo "$m: $(v blurab_${m}_$i)" | tee -a $OUT/blurab.txt
+                done
+            done; cp $OUT/blurab.txt $P/;;
         profenv=*)
             # rocprofv3 kernel stats of --mode lba under an environment setting: profenv=VAR=VALUE
             kv=${step#profenv=}; tag=$(echo $kv | tr '=' '_')
