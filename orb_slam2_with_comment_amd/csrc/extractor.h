@@ -79,9 +79,10 @@ struct Extractor {
     int keys_cap = 0, out_cap = 0;
     bool describe_wave = false;  // ORBMI_DESC=wave: the one-keypoint-per-wave describe kernel
     bool fast_v1 = false;        // ORBMI_FAST=v1: the per-lane FAST kernel
-    int blur_mode = 0;           // GaussianBlur: 0 side stream (default), 1 in the octree launch, 2 after it
+    int blur_mode = -1;          // GaussianBlur (ORBMI_BLUR): -1 by batch, 0 side stream, 1 in the octree launch, 2 after it
     hipStream_t bstream = nullptr;  // the blur's side stream
-    hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
+    hipEvent_t ev_pyr = nullptr, ev_blur = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
+    bool fast_early = false;     // ORBMI_FAST_EARLY=1: level 0's FAST on the side stream beside the resize chain
 
     // device buffers (capacity for `bcap` images)
     int bcap = 0;

@@ -589,13 +589,13 @@ __host__ __device__ inline int fast2_wave_bytes(int TS, int maxW, int maxH) {
 
 template <int TS>
 __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __restrict__ pyr, long long pimg,
-                                                           const CellGeom* __restrict__ cells, int ncells,
+                                                           const CellGeom* __restrict__ cells, int c0, int ncells,
                                                            uint2* __restrict__ cand, int keys_cap,
                                                            int* __restrict__ level_count, int nlevels, int ini_th,
                                                            int min_th, int maxW, int maxH) {
     extern __shared__ uint4 fast_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = blockIdx.x * kFastCells + wid, b = blockIdx.y;
+    const int c = c0 + blockIdx.x * kFastCells + wid, b = blockIdx.y;  // cells [c0, ncells)
     if (c >= ncells) return;
     const CellGeom cg = cells[c];
     if (cg.w == 0) return;
@@ -1305,12 +1305,13 @@ __device__ __forceinline__ void blur_tile(BlurShared& B, const uint8_t* __restri
     }
 }
 
-// DistributeOctTree and GaussianBlur in one launch, on a 1-D grid: blocks [0, nlevels x batch)
-// run one (image, level) octree each and are dispatched first; the blocks after them blur four
+// DistributeOctTree and GaussianBlur in one launch, on a 1-D grid: the first blocks run one
+// (image, level) octree each and are dispatched first; the blocks after them blur four
 // 128x32 tiles each on the CUs the octrees leave idle.  A level-0 octree is the launch's longest
 // workgroup (its candidates are the most), so the blur hides behind it instead of following it.
 // Both only read the pyramid; the blur slices reuse the octree's LDS.
 static_assert(sizeof(OctShared) >= 4 * sizeof(BlurShared), "blur slices overlay the octree LDS");
+constexpr int kFuseBlurMaxOctrees = 64;  // octree workgroups up to which the blur rides along
 __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restrict__ levels, int nlevels,
                                                          const uint2* __restrict__ cand,
                                                          const int* __restrict__ level_count,
@@ -1321,10 +1322,19 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
                                                          uint8_t* __restrict__ blur, long long pimg, long long bimg,
                                                          const int2* __restrict__ btiles, int nbtiles, int batch) {
     __shared__ OctShared S;
-    const int noct = nlevels * batch;
+    // workgroup i goes to XCD i % 8: the octrees are numbered so that every XCD gets every level
+    // (level (i / 8) % nlevels, image 8 ((i / 8) / nlevels) + i % 8) -- with (image, level) in
+    // row order all the level-0 octrees, the launch's longest, would share one XCD
+    const int noct = nlevels * 8 * ((batch + 7) / 8);
     if ((int)blockIdx.x < noct) {
-        octree_body(S, blockIdx.x % nlevels, blockIdx.x / nlevels, levels, nlevels, cand, level_count, regbase, node_of,
-                    keys_cap, oct_out, out_cap, oct_count);
+        const int q = blockIdx.x >> 3, img = 8 * (q / nlevels) + (blockIdx.x & 7);
+#ifdef ORBMI_OCT_ONLY_LEVEL  // timing experiment (tools: A/B builds): run the octrees of one level only
+        if ((ORBMI_OCT_ONLY_LEVEL >= 0) != (q % nlevels == (ORBMI_OCT_ONLY_LEVEL < 0 ? -1 - ORBMI_OCT_ONLY_LEVEL : ORBMI_OCT_ONLY_LEVEL)))
+            return;
+#endif
+        if (img < batch)
+            octree_body(S, q % nlevels, img, levels, nlevels, cand, level_count, regbase, node_of, keys_cap, oct_out,
+                        out_cap, oct_count);
         return;
     }
     const int slice = threadIdx.x >> 8, ti = ((int)blockIdx.x - noct) * 4 + slice;  // over (image, tile)
@@ -1666,6 +1676,8 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
     ORBMI_HIP(orbmi::stream_create(&bstream, "EXTRACTOR"));
     ORBMI_HIP(hipEventCreateWithFlags(&ev_pyr, hipEventDisableTiming));
     ORBMI_HIP(hipEventCreateWithFlags(&ev_blur, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_l0, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_f0, hipEventDisableTiming));
     // ORBextractor::ORBextractor  src/ORBextractor.cc:410-470 (same float/double steps)
     scale.assign(nl, 1.f); sigma2.assign(nl, 1.f); inv_scale.resize(nl); inv_sigma2.resize(nl);
     const double sfd = (double)sf;
@@ -1729,8 +1741,10 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         describe_wave = e && !strcmp(e, "wave");
         e = getenv("ORBMI_FAST");
         fast_v1 = e && !strcmp(e, "v1");
+        e = getenv("ORBMI_FAST_EARLY");
+        fast_early = e && !strcmp(e, "1");
         e = getenv("ORBMI_BLUR");
-        blur_mode = !e ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2 : 0;
+        blur_mode = !e ? -1 : !strcmp(e, "side") ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2 : -1;
     }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
@@ -2036,6 +2050,31 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                    orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity) {
     ORBMI_HIP(hipSetDevice(device));
     const int ncells = (int)cells.size();
+    // GaussianBlur needs only the pyramid.  Small batches (<= kFuseBlurMaxOctrees octrees): it rides
+    // in the octree launch as extra workgroups on the CUs the octrees leave idle (a side stream's
+    // event round trip costs more there: 7.8k vs 6.9k stereo frames/s).  Large batches: it runs on
+    // a side stream (bstream) beside FAST and the octrees, and the describe waits for it (88.3k
+    // vs 84.9k frames/s at config 5).  ORBMI_BLUR=side|fused|serial overrides.
+    const int blur_mode = this->blur_mode >= 0 ? this->blur_mode : batch * nlevels <= kFuseBlurMaxOctrees ? 1 : 0;
+    // ORBMI_FAST_EARLY=1: with the level-wise pyramid and the side stream, level 0's FAST runs on
+    // the side stream as soon as level 0 is written, beside the resize chain of levels 1..7.  Off
+    // by default: every kernel here is issue-bound, so the overlap only slowed the resize chain
+    // (0.143 -> 0.222 ms) and config 5 stayed at 89k frames/s (profiles/r04/fast_early_ab.txt).
+    const bool early = batch > kPyrTiledMaxBatch && blur_mode == 0 && !fast_v1 && fast_early &&
+                       levels[0].cell_begin == 0 && nlevels > 1;
+    auto launch_fast = [&](int c0, int c1, hipStream_t s) {
+        const dim3 grid((c1 - c0 + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
+        if (fast_v1)  // ORBMI_FAST=v1: per-lane bit assembly, runtime tile pitch (A/B)
+            hipLaunchKernelGGL(k_fast, grid, block, kFastCells * fast_wave_bytes, s, d_pyr, pimg, d_levels, d_cells,
+                               ncells, d_cand, keys_cap, d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+        else {
+            const bool narrow = fast_maxw + 3 <= 48;
+            const size_t lds = kFastCells * fast2_wave_bytes(narrow ? 48 : 80, fast_maxw, fast_maxh);
+            auto* kf = narrow ? k_fast2<48> : k_fast2<80>;
+            hipLaunchKernelGGL(kf, grid, block, lds, s, d_pyr, pimg, d_cells, c0, c1, d_cand, keys_cap, d_level_count,
+                               nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+        }
+    };
     if (batch > kPyrTiledMaxBatch) {
         for (int l = 0; l < nlevels; l++) {
             const LevelGeom& g = levels[l];
@@ -2045,6 +2084,14 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                 const int lrow = (g.W + 3 + 3 + 15) & ~15;  // an image row from its aligned start
                 hipLaunchKernelGGL(k_pyr_level0, grid, dim3(kPyrBThreads), kPyrBRows * lrow, stream, d_images, step,
                                    image_stride, d_pyr, pimg, g, d_level_count, nlevels, lrow);
+                if (early) {  // level 0's FAST beside the resize chain (it reads level 0 only)
+                    ORBMI_HIP(hipEventRecord(ev_l0, stream));
+                    ORBMI_HIP(hipStreamWaitEvent(bstream, ev_l0, 0));
+                    hipEvent_t ef = prof_begin(ORBMI_STAGE_FAST, bstream);
+                    launch_fast(levels[0].cell_begin, levels[0].cell_end, bstream);
+                    prof_end(ORBMI_STAGE_FAST, ef, bstream);
+                    ORBMI_HIP(hipEventRecord(ev_f0, bstream));
+                }
             } else {
                 const int lrow = levels[l - 1].stride;  // a padded source row (64-B multiple)
                 hipLaunchKernelGGL(k_pyr_resize, grid, dim3(kPyrBThreads), 2 * kPyrBRows * lrow + 8 * g.W, stream, d_pyr, pimg,
@@ -2060,9 +2107,6 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                            pyr_hy, d_level_count, pyr_lds0, pyr_lds_half);
         prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
-    // GaussianBlur needs only the pyramid: by default it runs on a side stream (bstream) beside
-    // FAST and the octrees -- whose tail leaves most CUs idle -- and the describe waits for it.
-    // ORBMI_BLUR=fused: as extra workgroups of the octree launch; ORBMI_BLUR=serial: after it.
     if (blur_mode == 0) {
         ORBMI_HIP(hipEventRecord(ev_pyr, stream));
         ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
@@ -2073,24 +2117,14 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         ORBMI_HIP(hipEventRecord(ev_blur, bstream));
     }
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
-    {
-        const dim3 grid((ncells + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
-        if (fast_v1)  // ORBMI_FAST=v1: per-lane bit assembly, runtime tile pitch (A/B)
-            hipLaunchKernelGGL(k_fast, grid, block, kFastCells * fast_wave_bytes, stream, d_pyr, pimg, d_levels, d_cells,
-                               ncells, d_cand, keys_cap, d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
-        else {
-            const bool narrow = fast_maxw + 3 <= 48;
-            const size_t lds = kFastCells * fast2_wave_bytes(narrow ? 48 : 80, fast_maxw, fast_maxh);
-            auto* kf = narrow ? k_fast2<48> : k_fast2<80>;
-            hipLaunchKernelGGL(kf, grid, block, lds, stream, d_pyr, pimg, d_cells, ncells, d_cand, keys_cap,
-                               d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh);
-        }
-    }
+    launch_fast(early ? levels[1].cell_begin : 0, ncells, stream);
     prof_end(ORBMI_STAGE_FAST, ev);
+    if (early) ORBMI_HIP(hipStreamWaitEvent(stream, ev_f0, 0));
     ev = prof_begin(ORBMI_STAGE_OCTREE);
     const bool fused = blur_mode == 1;
     const int blur_blocks = fused ? (nbtiles * batch + 3) / 4 : 0;
-    hipLaunchKernelGGL(k_octree, dim3(nlevels * batch + blur_blocks), dim3(kOctThreads), 0, stream, d_levels, nlevels,
+    hipLaunchKernelGGL(k_octree, dim3(nlevels * 8 * ((batch + 7) / 8) + blur_blocks), dim3(kOctThreads), 0, stream,
+                       d_levels, nlevels,
                        d_cand, d_level_count, d_regbase, d_node_of, keys_cap, d_oct, out_cap, d_oct_count, d_pyr, d_blur,
                        pimg, bimg, d_btiles, fused ? nbtiles : 0, batch);
     prof_end(ORBMI_STAGE_OCTREE, ev);
@@ -2157,7 +2191,9 @@ void Extractor::release() {
     bstream = nullptr;
     if (ev_pyr) (void)hipEventDestroy(ev_pyr);
     if (ev_blur) (void)hipEventDestroy(ev_blur);
-    ev_pyr = ev_blur = nullptr;
+    if (ev_l0) (void)hipEventDestroy(ev_l0);
+    if (ev_f0) (void)hipEventDestroy(ev_f0);
+    ev_pyr = ev_blur = ev_l0 = ev_f0 = nullptr;
 }
 
 }  // namespace orbmi
