@@ -1536,13 +1536,29 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe4(const uint8_t* __
                                                                int oct_cap, const int* __restrict__ oct_count,
                                                                orbmi_keypoint* __restrict__ kps,
                                                                uint8_t* __restrict__ desc, int* __restrict__ counts,
-                                                               int capacity, int out_cap) {
+                                                               int capacity, int out_cap, int nimg) {
     __shared__ float4 spat[256];
     __shared__ uint4 sic[4][kIcItems];
     __shared__ DescLevel slv[kMaxLevels];
     __shared__ int spre[kMaxLevels], scnt[kMaxLevels];
     __shared__ __attribute__((aligned(16))) uint8_t swin[kDescKpWG][kBW * kBP];
-    const int b = blockIdx.y, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, grp = lane >> 4, l = lane & 15;
+    // workgroup i runs on XCD i % 8.  With >= 8 images the gx workgroups of image b are numbered
+    // to share XCD b % 8 (w-th of image b: i = 8 (w + gx (b / 8)) + b % 8), so an XCD's L2 holds
+    // the windows of the few images its workgroups walk together instead of slices of every
+    // image; fewer images are interleaved (i = w nimg + b) to spread over all XCDs.
+    int gx, w, b;
+    if (nimg >= 8) {
+        gx = (int)gridDim.x / (8 * ((nimg + 7) / 8));
+        const int q = blockIdx.x >> 3;
+        w = q % gx;
+        b = 8 * (q / gx) + (blockIdx.x & 7);
+        if (b >= nimg) return;
+    } else {
+        gx = (int)gridDim.x / nimg;
+        w = blockIdx.x / nimg;
+        b = blockIdx.x - w * nimg;
+    }
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, grp = lane >> 4, l = lane & 15;
     spat[tid] = c_pattern_f[tid];
     for (int i = tid; i < 4 * kIcItems; i += 64 * kDescWaves) (&sic[0][0])[i] = (&c_ictab[0][0])[i];
     const int* lc = oct_count + b * nlevels;
@@ -1553,12 +1569,12 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe4(const uint8_t* __
         for (int q = 0; q < tid; q++) pre += lc[q];
         spre[tid] = pre;
         scnt[tid] = lc[tid];
-        if (blockIdx.x == 0 && tid == nlevels - 1) counts[b] = pre + lc[tid];
+        if (w == 0 && tid == nlevels - 1) counts[b] = pre + lc[tid];
     }
     __syncthreads();
     uint8_t* W = swin[wid * kDescGroups + grp];
     const int nchunks = (out_cap + kDescKpWG - 1) / kDescKpWG;
-    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    for (int ch = w; ch < nchunks; ch += gx) {
         const int j = ch * kDescKpWG + wid * kDescGroups + grp;
         int level = -1;
         for (int q = 0; q < nlevels; q++)
@@ -2142,8 +2158,10 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     else {
         const int nch = (out_cap + kDescKpWG - 1) / kDescKpWG;
         const int gx = std::max(1, std::min(nch, (kDescTargetWG + batch - 1) / batch));
-        hipLaunchKernelGGL(k_describe4, dim3(gx, batch), dim3(64 * kDescWaves), 0, stream, d_pyr, d_blur, pimg, bimg,
-                           d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity, out_cap);
+        hipLaunchKernelGGL(k_describe4, dim3(batch >= 8 ? 8 * gx * ((batch + 7) / 8) : gx * batch), dim3(64 * kDescWaves),
+                           0, stream, d_pyr, d_blur,
+                           pimg, bimg, d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity,
+                           out_cap, batch);
     }
     prof_end(ORBMI_STAGE_DESCRIBE, ev);
     ORBMI_HIP(hipGetLastError());
