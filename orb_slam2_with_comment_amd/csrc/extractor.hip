@@ -242,6 +242,24 @@ __global__ __launch_bounds__(kPyrBThreads) void k_pyr_resize(uint8_t* __restrict
     }
 }
 
+// Workgroup i of a 1-D grid runs on XCD i % 8.  With >= 8 images, xcd_image_map numbers the
+// `per` workgroups of image b so that they share XCD b % 8 (unit w of image b: i = 8 (w + per
+// (b / 8)) + b % 8): an XCD's L2 then serves the few images its workgroups walk together, not
+// slices of every image.  Fewer images are interleaved over all XCDs (i = w nimg + b).
+__host__ inline int xcd_image_grid(int per, int nimg) { return nimg >= 8 ? 8 * per * ((nimg + 7) / 8) : per * nimg; }
+__device__ inline bool xcd_image_map(int nimg, int& unit, int& img) {
+    const int i = blockIdx.x;
+    if (nimg >= 8) {
+        const int per = (int)gridDim.x / (8 * ((nimg + 7) / 8)), q = i >> 3;
+        unit = q % per;
+        img = 8 * (q / per) + (i & 7);
+        return img < nimg;
+    }
+    unit = i / nimg;
+    img = i - unit * nimg;
+    return true;
+}
+
 // ------------------------------------------------------------------------------ FAST
 constexpr int kTile = 64;               // max cell ROI edge (wCell+6, hCell+6): list entries are y << 6 | x
 constexpr int kFastCells = 2;           // waves (cells) per workgroup
@@ -592,10 +610,12 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
                                                            const CellGeom* __restrict__ cells, int c0, int ncells,
                                                            uint2* __restrict__ cand, int keys_cap,
                                                            int* __restrict__ level_count, int nlevels, int ini_th,
-                                                           int min_th, int maxW, int maxH) {
+                                                           int min_th, int maxW, int maxH, int nimg) {
     extern __shared__ uint4 fast_lds[];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = c0 + blockIdx.x * kFastCells + wid, b = blockIdx.y;  // cells [c0, ncells)
+    int unit, b;
+    if (!xcd_image_map(nimg, unit, b)) return;
+    const int c = c0 + unit * kFastCells + wid;  // cells [c0, ncells)
     if (c >= ncells) return;
     const CellGeom cg = cells[c];
     if (cg.w == 0) return;
@@ -1347,9 +1367,11 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
 // GaussianBlur alone: one 128x32 tile per 256-thread workgroup.
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                               long long pimg, long long bimg, const LevelGeom* __restrict__ levels,
-                                              const int2* __restrict__ tiles) {
+                                              const int2* __restrict__ tiles, int nimg) {
     __shared__ BlurShared B;
-    blur_tile(B, pyr, blur, pimg, bimg, levels, tiles[blockIdx.x], blockIdx.y, threadIdx.x, true);
+    int tile, b;
+    if (!xcd_image_map(nimg, tile, b)) return;
+    blur_tile(B, pyr, blur, pimg, bimg, levels, tiles[tile], b, threadIdx.x, true);
 }
 
 // ------------------------------------------------------------------------------ describe
@@ -1542,22 +1564,10 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe4(const uint8_t* __
     __shared__ DescLevel slv[kMaxLevels];
     __shared__ int spre[kMaxLevels], scnt[kMaxLevels];
     __shared__ __attribute__((aligned(16))) uint8_t swin[kDescKpWG][kBW * kBP];
-    // workgroup i runs on XCD i % 8.  With >= 8 images the gx workgroups of image b are numbered
-    // to share XCD b % 8 (w-th of image b: i = 8 (w + gx (b / 8)) + b % 8), so an XCD's L2 holds
-    // the windows of the few images its workgroups walk together instead of slices of every
-    // image; fewer images are interleaved (i = w nimg + b) to spread over all XCDs.
-    int gx, w, b;
-    if (nimg >= 8) {
-        gx = (int)gridDim.x / (8 * ((nimg + 7) / 8));
-        const int q = blockIdx.x >> 3;
-        w = q % gx;
-        b = 8 * (q / gx) + (blockIdx.x & 7);
-        if (b >= nimg) return;
-    } else {
-        gx = (int)gridDim.x / nimg;
-        w = blockIdx.x / nimg;
-        b = blockIdx.x - w * nimg;
-    }
+    // the gx workgroups of an image share an XCD (xcd_image_map)
+    int w, b;
+    if (!xcd_image_map(nimg, w, b)) return;
+    const int gx = (int)gridDim.x / (nimg >= 8 ? 8 * ((nimg + 7) / 8) : nimg);
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, grp = lane >> 4, l = lane & 15;
     spat[tid] = c_pattern_f[tid];
     for (int i = tid; i < 4 * kIcItems; i += 64 * kDescWaves) (&sic[0][0])[i] = (&c_ictab[0][0])[i];
@@ -2087,8 +2097,8 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
             const bool narrow = fast_maxw + 3 <= 48;
             const size_t lds = kFastCells * fast2_wave_bytes(narrow ? 48 : 80, fast_maxw, fast_maxh);
             auto* kf = narrow ? k_fast2<48> : k_fast2<80>;
-            hipLaunchKernelGGL(kf, grid, block, lds, s, d_pyr, pimg, d_cells, c0, c1, d_cand, keys_cap, d_level_count,
-                               nlevels, ini_th, min_th, fast_maxw, fast_maxh);
+            hipLaunchKernelGGL(kf, dim3(xcd_image_grid(grid.x, batch)), block, lds, s, d_pyr, pimg, d_cells, c0, c1, d_cand,
+                               keys_cap, d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh, batch);
         }
     };
     if (batch > kPyrTiledMaxBatch) {
@@ -2127,8 +2137,8 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         ORBMI_HIP(hipEventRecord(ev_pyr, stream));
         ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
         hipEvent_t eb = prof_begin(ORBMI_STAGE_BLUR, bstream);
-        hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, bstream, d_pyr, d_blur, pimg, bimg, d_levels,
-                           d_btiles);
+        hipLaunchKernelGGL(k_blur, dim3(xcd_image_grid(nbtiles, batch)), dim3(256), 0, bstream, d_pyr, d_blur, pimg, bimg,
+                           d_levels, d_btiles, batch);
         prof_end(ORBMI_STAGE_BLUR, eb, bstream);
         ORBMI_HIP(hipEventRecord(ev_blur, bstream));
     }
@@ -2146,8 +2156,8 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     prof_end(ORBMI_STAGE_OCTREE, ev);
     if (blur_mode == 2) {
         ev = prof_begin(ORBMI_STAGE_BLUR);
-        hipLaunchKernelGGL(k_blur, dim3(nbtiles, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg, d_levels,
-                           d_btiles);
+        hipLaunchKernelGGL(k_blur, dim3(xcd_image_grid(nbtiles, batch)), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
+                           d_levels, d_btiles, batch);
         prof_end(ORBMI_STAGE_BLUR, ev);
     }
     if (blur_mode == 0) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
@@ -2158,7 +2168,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     else {
         const int nch = (out_cap + kDescKpWG - 1) / kDescKpWG;
         const int gx = std::max(1, std::min(nch, (kDescTargetWG + batch - 1) / batch));
-        hipLaunchKernelGGL(k_describe4, dim3(batch >= 8 ? 8 * gx * ((batch + 7) / 8) : gx * batch), dim3(64 * kDescWaves),
+        hipLaunchKernelGGL(k_describe4, dim3(xcd_image_grid(gx, batch)), dim3(64 * kDescWaves),
                            0, stream, d_pyr, d_blur,
                            pimg, bimg, d_levels, nlevels, d_oct, out_cap, d_oct_count, kps, desc, counts, capacity,
                            out_cap, batch);
