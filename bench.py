@@ -72,6 +72,8 @@ def parse():
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r04", "traffic_batch.json"),
+                    help="the same for --mode batch (tools/gpu.sh pmc_batch)")
     return ap.parse_args()
 
 
@@ -85,6 +87,19 @@ def level_geometry(rows, cols, nlevels=8, sf=1.2):
         H.append(int(np.rint(np.float32(rows) * inv)))
         s = np.float32(np.float64(s) * np.float64(np.float32(sf)))
     return W, H
+
+
+def batch_traffic(path, nlevels=8):
+    """HBM bytes of one config-5 launch sequence from a tools/pmc_traffic.py summary of the batch
+    mode (calibrated FETCH_SIZE / WRITE_SIZE per kernel launch): every stage once, the resize once
+    per level above 0; None without the file."""
+    if not os.path.exists(path):
+        return None
+    try:
+        per = json.load(open(path)).get("per_launch_bytes", {})
+        return int(sum(v * (nlevels - 1 if k == "pyr_resize" else 1) for k, v in per.items()))
+    except Exception:
+        return None
 
 
 def read_traffic(path, name):
@@ -993,7 +1008,9 @@ def run_batch(a, rank, world, local, dist):
             "kpts_desc_per_s": round(steps * nb * world * kp / dt, 1), "keypoints_per_frame": round(kp, 1),
             "stage_ms_per_launch": stage_ms,
             "roofline": {"kernel": "pipeline", "bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6),
+                         "traffic": batch_traffic(a.traffic_batch),
+                         "traffic_source": os.path.relpath(a.traffic_batch, ROOT),
                          "alg_bytes_per_launch": round(B)},
             "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp, "host": host_info(),
         }
