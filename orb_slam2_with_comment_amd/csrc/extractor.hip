@@ -1342,19 +1342,20 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(const LevelGeom* __restr
                                                          uint8_t* __restrict__ blur, long long pimg, long long bimg,
                                                          const int2* __restrict__ btiles, int nbtiles, int batch) {
     __shared__ OctShared S;
-    // workgroup i goes to XCD i % 8: the octrees are numbered so that every XCD gets every level
-    // (level (i / 8) % nlevels, image 8 ((i / 8) / nlevels) + i % 8) -- with (image, level) in
-    // row order all the level-0 octrees, the launch's longest, would share one XCD
-    const int noct = nlevels * 8 * ((batch + 7) / 8);
+    // workgroup i goes to XCD i % 8, and workgroups are dispatched in index order.  A large batch
+    // takes two rounds of one octree workgroup per CU, so the octrees are numbered longest first
+    // (level-major from the top level down: alone, every level takes 47-52 us and the top one
+    // 84 us at config 5), each level spread over all XCDs (image 8 s + i % 8 for slot s).
+    const int b8 = (batch + 7) / 8, noct = nlevels * 8 * b8;
     if ((int)blockIdx.x < noct) {
-        const int q = blockIdx.x >> 3, img = 8 * (q / nlevels) + (blockIdx.x & 7);
+        const int q = blockIdx.x >> 3, lv = nlevels - 1 - q / b8, img = 8 * (q % b8) + (blockIdx.x & 7);
 #ifdef ORBMI_OCT_ONLY_LEVEL  // timing experiment (tools: A/B builds): run the octrees of one level only
-        if ((ORBMI_OCT_ONLY_LEVEL >= 0) != (q % nlevels == (ORBMI_OCT_ONLY_LEVEL < 0 ? -1 - ORBMI_OCT_ONLY_LEVEL : ORBMI_OCT_ONLY_LEVEL)))
+        if ((ORBMI_OCT_ONLY_LEVEL >= 0) != (lv == (ORBMI_OCT_ONLY_LEVEL < 0 ? -1 - ORBMI_OCT_ONLY_LEVEL : ORBMI_OCT_ONLY_LEVEL)))
             return;
 #endif
         if (img < batch)
-            octree_body(S, q % nlevels, img, levels, nlevels, cand, level_count, regbase, node_of, keys_cap, oct_out,
-                        out_cap, oct_count);
+            octree_body(S, lv, img, levels, nlevels, cand, level_count, regbase, node_of, keys_cap, oct_out, out_cap,
+                        oct_count);
         return;
     }
     const int slice = threadIdx.x >> 8, ti = ((int)blockIdx.x - noct) * 4 + slice;  // over (image, tile)
