@@ -274,6 +274,27 @@ __device__ inline double block_sum(double v, double* red) {
     return t;
 }
 
+// two block sums in one pass, the results in thread 0 only: the same butterfly per wave and the
+// same wave order as block_sum (bit-identical sums), one barrier instead of four
+template <int NT>
+__device__ inline void block_sum2_t0(double& x, double& y, double* red /* 2 NT / 64 */) {
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = x;
+        red[NT / 64 + (threadIdx.x >> 6)] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = 0;
+        y = 0;
+        for (int w = 0; w < NT / 64; w++) x += red[w];
+        for (int w = 0; w < NT / 64; w++) y += red[NT / 64 + w];
+    }
+}
+
 template <int NT>
 __device__ inline double block_max(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -2321,7 +2342,7 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
     double* __restrict__ Xt = a.Xb[ctl.cur ^ 1];
     double* __restrict__ part_chi = a.part_tchi;
     double* __restrict__ part_scale = a.part_tscale;
-    __shared__ double red[kBaUpdThreads / 64];
+    __shared__ double red[2 * kBaUpdThreads / 64];
     __shared__ double xs[kBaUpdPts][4];
     __shared__ double sHe[kBaUpdLdsEdges * 9];
     __shared__ bool last;
@@ -2391,8 +2412,7 @@ __global__ __launch_bounds__(kBaUpdThreads) void k_ba_update_errors(BaDev a) {
             for (int k = 0; k < 3; k++) t.bl[3 * p + k] = h[6 + k];
         }
     }
-    chi = block_sum<kBaUpdThreads>(chi, red);
-    sc = block_sum<kBaUpdThreads>(sc, red);
+    block_sum2_t0<kBaUpdThreads>(chi, sc, red);  // thread 0 holds both
     // the fan-in to the last block without __threadfence (an L2 write-back + L1 invalidate,
     // ~3.5 us on gfx950, twice per trial): the two partials go out as agent-scope (sc1) stores,
     // drained before the arrival add; the last block reads them with sc1 loads
