@@ -74,7 +74,22 @@ def parse():
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r04", "traffic_batch.json"),
                     help="the same for --mode batch (tools/gpu.sh pmc_batch)")
+    ap.add_argument("--print-traffic-config", action="store_true",
+                    help="print the workload key tools/pmc_traffic.py stores with a traffic summary, and exit")
     return ap.parse_args()
+
+
+def traffic_config(a):
+    """The workload a PMC traffic summary was measured on (stored in it by tools/pmc_traffic.py):
+    a summary is reported as roofline.traffic only for the same workload, null otherwise."""
+    c = {"mode": a.mode, "nfeatures": a.nfeatures}
+    if a.mode == "batch":  # (run_batch: 5000 features whatever --nfeatures says)
+        c.update({"nfeatures": 5000, "rows": 480, "cols": 752, "batch": a.batch, "nlevels": 8})
+    else:
+        c.update({"rows": 376, "cols": 1241, "nlevels": 8})
+    if a.mode == "track":
+        c["lm_chain"] = a.lm_chain
+    return c
 
 
 def level_geometry(rows, cols, nlevels=8, sf=1.2):
@@ -89,26 +104,33 @@ def level_geometry(rows, cols, nlevels=8, sf=1.2):
     return W, H
 
 
-def batch_traffic(path, nlevels=8):
+def _traffic_summary(path, config):
+    """The per-kernel bytes of a tools/pmc_traffic.py summary when it was measured on `config`
+    (its stored "config"; a summary without one is not trusted either), else None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None
+    if config is not None and d.get("config") != config:
+        return None
+    return d.get("per_launch_bytes", {})
+
+
+def batch_traffic(path, config, nlevels=8):
     """HBM bytes of one config-5 launch sequence from a tools/pmc_traffic.py summary of the batch
     mode (calibrated FETCH_SIZE / WRITE_SIZE per kernel launch): every stage once, the resize once
-    per level above 0; None without the file."""
-    if not os.path.exists(path):
+    per level above 0; None without the file or when it was measured on another workload."""
+    per = _traffic_summary(path, config)
+    if per is None:
         return None
-    try:
-        per = json.load(open(path)).get("per_launch_bytes", {})
-        return int(sum(v * (nlevels - 1 if k == "pyr_resize" else 1) for k, v in per.items()))
-    except Exception:
-        return None
+    return int(sum(v * (nlevels - 1 if k == "pyr_resize" else 1) for k, v in per.items()))
 
 
-def read_traffic(path, name):
-    if not os.path.exists(path):
-        return None
-    try:
-        return json.load(open(path)).get("per_launch_bytes", {}).get(name)
-    except Exception:
-        return None
+def read_traffic(path, name, config=None):
+    per = _traffic_summary(path, config)
+    return None if per is None else per.get(name)
 
 
 # --------------------------------------------------------------------------------- track
@@ -398,8 +420,9 @@ def run_track(a, rank, world, local, dist):
         xch.synchronize()
         x_matches = int((xch.xmatch[:int(tr.counts[0])] >= 0).sum())
     value = a.steps * world / dt
-    ext_roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic)
-    roof = pose_roofline(pose_prof, outcome["recs"], a.traffic)
+    ext_roof = roofline_entry(dom, stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]], a.traffic,
+                              traffic_config(a))
+    roof = pose_roofline(pose_prof, outcome["recs"], a.traffic, traffic_config(a))
     out = None
     if rank == 0:
         cpu = None
@@ -530,12 +553,12 @@ def read_profile(handle):
     return ms, nl
 
 
-def roofline_entry(name, stage, ms_total, launches, traffic_path):
+def roofline_entry(name, stage, ms_total, launches, traffic_path, config):
     avg_s = ms_total / max(int(launches), 1) / 1e3
     alg = float(stage["alg"].get(name, 0.0))
     achieved = alg / avg_s / 1e9 if avg_s > 0 else 0.0
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": read_traffic(traffic_path, name),
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": read_traffic(traffic_path, name, config),
             "alg_bytes_per_launch": round(alg), "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches)}
 
 
@@ -554,7 +577,7 @@ POSE_FLOPS_PER_EDGE_PASS = 300
 POSE_FLOPS_PER_TRIAL = 600
 
 
-def pose_roofline(prof, recs, traffic_path):
+def pose_roofline(prof, recs, traffic_path, config):
     """k_pose_opt against the FP64 peak: edge passes counted as (iterations + 4 rounds) x edges
     of the frame's two PoseOptimizations (a lower bound: rejected trials add passes)."""
     ms_total, launches = prof
@@ -566,7 +589,7 @@ def pose_roofline(prof, recs, traffic_path):
     # §4 and the MFMA A/B in §4b); the peak is the fp64 vector peak, equal to the fp64 MFMA peak
     return {"kernel": "k_pose_opt", "bound": "fp64-valu", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFS, 8),
-            "traffic": read_traffic(traffic_path, "k_pose_opt"), "alg_flops_per_launch": round(float(flops)),
+            "traffic": read_traffic(traffic_path, "k_pose_opt", config), "alg_flops_per_launch": round(float(flops)),
             "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches),
             "note": "fp64 Levenberg on one workgroup per frame: serial-latency-bound (DESIGN.md)"}
 
@@ -711,7 +734,7 @@ def run_extract(a, rank, world, local, dist):
             "keypoints_per_frame": stage["kp_per_step"],
             "stage_ms_per_step": stage["stage_ms"],
             "roofline": roofline_entry(stage["dominant"], stage, ms[stage["dominant_id"]], nl[stage["dominant_id"]],
-                                       a.traffic),
+                                       a.traffic, traffic_config(a)),
             "pipeline_roofline": pipeline_roofline(stage, rows, cols),
             "cpu_baseline": cpu, "host": host_info(),
         }
@@ -1009,7 +1032,7 @@ def run_batch(a, rank, world, local, dist):
             "stage_ms_per_launch": stage_ms,
             "roofline": {"kernel": "pipeline", "bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6),
-                         "traffic": batch_traffic(a.traffic_batch),
+                         "traffic": batch_traffic(a.traffic_batch, traffic_config(a)),
                          "traffic_source": os.path.relpath(a.traffic_batch, ROOT),
                          "alg_bytes_per_launch": round(B)},
             "cpu_baseline": cpu, "cpu_baseline_throughput": cpu_tp, "host": host_info(),
@@ -1081,6 +1104,9 @@ def spawn_ranks(a):
 
 def main():
     a = parse()
+    if a.print_traffic_config:
+        print(json.dumps(traffic_config(a)))
+        return
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a))
     rank = int(os.environ.get("RANK", 0))

@@ -405,6 +405,9 @@ typedef struct orbmi_ba_result {
     int iterations[2];             /* optimize(5) / optimize(10) iterations run          */
     double chi2[2];                /* final activeRobustChi2 of both optimisations       */
     int aborted;                   /* stop flag seen before the first optimisation: no write-back */
+    int stop_check;                /* index of the first pbStopFlag check that found the flag
+                                    * raised (-1: none); numbering: orbmi_ba_set_stop_at_check */
+    int checks;                    /* pbStopFlag checks made by the call                 */
 } orbmi_ba_result;
 
 typedef struct orbmi_ba orbmi_ba;
@@ -413,12 +416,27 @@ void orbmi_ba_destroy(orbmi_ba* h);
 /* Run the handle on a caller's HIP stream, or its own new one when `stream` is NULL (as
  * orbmi_vocabulary_set_stream). */
 int orbmi_ba_set_stream(orbmi_ba* b, void* stream);
+/* Deterministic pbStopFlag (test and schedule-replay hook; no counterpart in the reference):
+ * in every later call on the handle the flag reads raised from its k-th check on (k < 0: off),
+ * whatever `stop` holds.  The checks are the reads of pbStopFlag in the order the reference
+ * evaluates them, numbered from 0:
+ *   #0  src/Optimizer.cc:685 (raised: return before optimising, `aborted`, no write-back);
+ *   SparseOptimizer::optimize's loop condition before each iteration while i < iterations
+ *       (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:376; none when the graph has no vertex);
+ *   the LM inner loop's condition after a rejected trial while qmax < 10
+ *       (optimization_algorithm_levenberg.cpp:149, evaluated only when rho < 0);
+ *   src/Optimizer.cc:689 (bDoMore) after optimize(5); then optimize(10)'s, as optimize(5)'s.
+ * A flag raised by another thread is first seen at one of these checks, so a call with
+ * k = result.stop_check of a concurrent run repeats that run exactly. */
+int orbmi_ba_set_stop_at_check(orbmi_ba* b, int k);
 
 /* Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (include/Optimizer.h:62,
  * src/Optimizer.cc:483-808) on the assembled graph: LM (g2o OptimizationAlgorithmLevenberg,
  * BlockSolver_6_3 Schur complement, Huber sqrt(5.991)/sqrt(7.815)) 5 iterations, outlier
  * levels, 10 iterations without kernels, erase list.  All arithmetic fp64 on the GPU.
- * `stop` (may be NULL) is polled like pbStopFlag / mbAbortBA. */
+ * `stop` (may be NULL) is read like pbStopFlag / mbAbortBA, at the checks listed under
+ * orbmi_ba_set_stop_at_check.  Edges must come grouped by point with at most one per (point,
+ * keyframe), as a map point's observations give them; otherwise ORBMI_E_ARG. */
 int orbmi_local_bundle_adjustment(orbmi_ba* h, const orbmi_ba_problem* problem, orbmi_ba_result* result,
                                   const volatile int* stop);
 

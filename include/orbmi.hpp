@@ -299,6 +299,7 @@ public:
         int iterations[2] = {0, 0};
         double chi2[2] = {0, 0};
         bool aborted = false;
+        int stop_check = -1;          // the first pbStopFlag check that found it raised (-1: none)
     };
 
     explicit LocalBundleAdjuster(int device = 0) { check(orbmi_ba_create(device, &h_), "orbmi_ba_create"); }
@@ -313,15 +314,19 @@ public:
         r.pos.assign(pts.size() * 3, 0.0f);
         r.erase.assign(edges.size(), 0);
         orbmi_ba_problem p{(int)kfs.size(), (int)pts.size(), (int)edges.size(), kfs.data(), pts.data(), edges.data()};
-        orbmi_ba_result out{r.tcw.data(), r.pos.data(), r.erase.data(), {0, 0}, {0, 0}, 0};
+        orbmi_ba_result out{r.tcw.data(), r.pos.data(), r.erase.data(), {0, 0}, {0, 0}, 0, -1, 0};
         check(orbmi_local_bundle_adjustment(h_, &p, &out, pbStopFlag), "orbmi_local_bundle_adjustment");
         r.iterations[0] = out.iterations[0];
         r.iterations[1] = out.iterations[1];
         r.chi2[0] = out.chi2[0];
         r.chi2[1] = out.chi2[1];
         r.aborted = out.aborted != 0;
+        r.stop_check = out.stop_check;
         return r;
     }
+
+    // the deterministic pbStopFlag of orbmi_ba_set_stop_at_check (k < 0: off)
+    void SetStopAtCheck(int k) { check(orbmi_ba_set_stop_at_check(h_, k), "orbmi_ba_set_stop_at_check"); }
 
 private:
     orbmi_ba* h_ = nullptr;

@@ -40,6 +40,15 @@ int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
  * out: 7 entries. */
 int orbmi_debug_greedy_cycles(unsigned long long* out, int reset);
 
+/* The k_ba_schur launch of a LocalBA with nf free keyframes (host computation, no GPU): for
+ * each of its *n_out = nf(nf+1)/2 + 2 nf + 1 blocks b, table[4b..4b+3] = {kind, x, y, z}:
+ * kind 0 pose-pair block (x, y = the pair's keyframe ranks ra <= rb, z = its row-major pair
+ * index); kind 1 keyframe
+ * block (x = rank, y = half); kind 2 the MFMA padding block (x = y = z = -1).  cap = entries of
+ * 4 ints; ORBMI_E_CAP with *n_out when short.  For the CPU test of the block table (every id a
+ * permutation, every index a block reads in range). */
+int orbmi_debug_ba_schur_blocks(int nf, int* table, int cap, int* n_out);
+
 /* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame
  * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
  * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,

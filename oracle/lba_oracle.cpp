@@ -135,8 +135,18 @@ struct Optimizer {
     int nBad = 0;
     std::vector<double> x;
 
-    Optimizer(Graph& gr, const volatile int* s) : g(gr), stop(s) {}
-    bool terminate() const { return stop && *stop; }
+    int stop_at = -1;      // orbmi_ba_set_stop_at_check's hook: raised from this check on
+    int checks = 0;        // pbStopFlag reads so far, numbered as orbmi_ba_set_stop_at_check's
+    int stop_seen = -1;    // the first read that found it raised
+    Optimizer(Graph& gr, const volatile int* s, int at) : g(gr), stop(s), stop_at(at) {}
+    // every read of pbStopFlag (src/Optimizer.cc:685, :689; SparseOptimizer::terminate()) in the
+    // order the reference's short-circuit conditions evaluate them
+    bool terminate() {
+        const int idx = checks++;
+        const bool s = (stop && *stop) || (stop_at >= 0 && idx >= stop_at);
+        if (s && stop_seen < 0) stop_seen = idx;
+        return s;
+    }
 
     bool initialize(int level) {  // initializeOptimization(level)
         active_edges.clear();
@@ -383,10 +393,11 @@ struct Optimizer {
 
 }  // namespace
 
-static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, double* edge_chi2);
+static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, int stop_at,
+                    double* edge_chi2);
 
 extern "C" int orc_local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop) {
-    return local_ba(P, R, stop, nullptr);
+    return local_ba(P, R, stop, -1, nullptr);
 }
 
 /* Same, and the chi2 every erase decision of src/Optimizer.cc:758-773 reads (per edge; -1 for
@@ -394,10 +405,18 @@ extern "C" int orc_local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const
  * GPU's sits on its threshold within the pose tolerance. */
 extern "C" int orc_local_ba_edge_chi2(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop,
                                       double* edge_chi2) {
-    return local_ba(P, R, stop, edge_chi2);
+    return local_ba(P, R, stop, -1, edge_chi2);
 }
 
-static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, double* edge_chi2) {
+/* Same with the deterministic pbStopFlag of orbmi_ba_set_stop_at_check (stop_at < 0: off);
+ * result.stop_check / checks report the reads as the device does. */
+extern "C" int orc_local_ba_ex(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, int stop_at,
+                               double* edge_chi2) {
+    return local_ba(P, R, stop, stop_at, edge_chi2);
+}
+
+static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatile int* stop, int stop_at,
+                    double* edge_chi2) {
     Graph g;
     for (int k = 0; k < P->nkf; k++) {
         g.T.push_back(se3_from_tcw(P->kfs[k].tcw));
@@ -426,15 +445,20 @@ static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatil
     R->iterations[0] = R->iterations[1] = 0;
     R->chi2[0] = R->chi2[1] = 0;
     for (int i = 0; i < P->nedge; i++) R->erase[i] = 0;
-    if (stop && *stop) {  // src/Optimizer.cc:685-687: return before optimising, no write-back
+    Optimizer opt(g, stop, stop_at);
+    auto report = [&] {
+        R->stop_check = opt.stop_seen;
+        R->checks = opt.checks;
+    };
+    if (opt.terminate()) {  // src/Optimizer.cc:685-687: return before optimising, no write-back
         R->aborted = 1;
+        report();
         return 0;
     }
-    Optimizer opt(g, stop);
     opt.initialize(0);
     R->iterations[0] = opt.optimize(5);
     R->chi2[0] = opt.active_robust_chi2();
-    bool bDoMore = !(stop && *stop);
+    bool bDoMore = !opt.terminate();  // :689-692
     if (bDoMore) {
         for (Edge& e : g.E) {
             if (P->pts[e.pt].bad) continue;
@@ -457,5 +481,6 @@ static int local_ba(const orbmi_ba_problem* P, orbmi_ba_result* R, const volatil
     for (int k = 0; k < P->nkf; k++) se3_to_tcw(g.T[k], R->tcw + 16 * k);
     for (int p = 0; p < P->npt; p++)
         for (int r = 0; r < 3; r++) R->pos[3 * p + r] = (float)g.X[p][r];
+    report();
     return 0;
 }

@@ -250,20 +250,23 @@ def search_by_bow(kf, kf_mp_ok, kf_fv, f, f_fv, nnratio=0.7, check_ori=True):
     return out[:len(f.keys)], n.value
 
 
-def local_ba(problem, stop=False, edge_chi2=False):
-    """Optimizer::LocalBundleAdjustment restatement -> dict(tcw, pos, erase, iterations, chi2, aborted)
-    (+ "edge_chi2": the chi2 each erase decision read, -1 bad point, -2 depth not positive)."""
+def local_ba(problem, stop=False, edge_chi2=False, stop_at_check=-1):
+    """Optimizer::LocalBundleAdjustment restatement -> dict(tcw, pos, erase, iterations, chi2, aborted,
+    stop_check, checks) (+ "edge_chi2": the chi2 each erase decision read, -1 bad point, -2 depth
+    not positive).  stop_at_check >= 0: pbStopFlag reads raised from that check on (the numbering
+    of orbmi_ba_set_stop_at_check)."""
     L = lib()
-    L.orc_local_ba_edge_chi2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.orc_local_ba_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     r, tcw, pos, erase = problem.result_buffers()
     v = problem.view()
     flag = C.c_int(1 if stop else 0)
     n = len(problem.kfs), len(problem.pts), len(problem.edges)
     ec = np.zeros(max(n[2], 1), np.float64)
-    rc = L.orc_local_ba_edge_chi2(C.addressof(v), C.addressof(r), C.addressof(flag), ec.ctypes.data)
+    rc = L.orc_local_ba_ex(C.addressof(v), C.addressof(r), C.addressof(flag), int(stop_at_check), ec.ctypes.data)
     assert rc == 0, rc
     out = {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
-           "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+           "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted,
+           "stop_check": r.stop_check, "checks": r.checks}
     if edge_chi2:
         out["edge_chi2"] = ec[:n[2]]
     return out

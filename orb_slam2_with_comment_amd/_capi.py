@@ -107,6 +107,8 @@ _PROTOS = {
     "orbmi_triangulate_matches": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_stereo_parallax_cos": (_i, [C.c_float, _vp, _i, _vp]),
     "orbmi_ba_set_stream": (_i, [_vp, _vp]),
+    "orbmi_ba_set_stop_at_check": (_i, [_vp, _i]),
+    "orbmi_debug_ba_schur_blocks": (_i, [_i, _vp, _i, _vp]),
     "orbmi_vocabulary_set_stream": (_i, [_vp, _vp]),
     "orbmi_fuse_search_refresh": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, C.c_float, _vp, _vp]),
     "orbmi_create_new_map_points": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -39,7 +39,9 @@ def _stale(out, deps):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    deps = sources() + glob.glob(os.path.join(PKG, "csrc", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+    # every file the sources include: headers, the generated csrc/*.inc asm, the C++ mirror
+    deps = sources() + glob.glob(os.path.join(PKG, "csrc", "*.h")) + glob.glob(os.path.join(PKG, "csrc", "*.inc"))
+    deps += glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.hpp"))
     if not force and not _stale(LIB, deps):
         return LIB
     tmp = LIB + ".tmp"

@@ -140,6 +140,7 @@ struct Extractor {
     int init(int dev, int nf, float sf, int nl, int ini, int mn);
     int set_geometry(int rows, int cols);
     int reserve(int batch, int capacity);
+    int ensure_side_stream();  // bstream + its events on first use (large batches only)
     int run(const uint8_t* d_images, int batch, size_t step, size_t image_stride,
             orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity);
     void release();

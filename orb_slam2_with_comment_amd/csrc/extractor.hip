@@ -1700,11 +1700,6 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
     device = dev; nfeatures = nf; scale_factor = sf; nlevels = nl; ini_th = ini; min_th = mn;
     ORBMI_HIP(hipSetDevice(device));
     ORBMI_HIP(orbmi::stream_create(&stream, "EXTRACTOR"));
-    ORBMI_HIP(orbmi::stream_create(&bstream, "EXTRACTOR"));
-    ORBMI_HIP(hipEventCreateWithFlags(&ev_pyr, hipEventDisableTiming));
-    ORBMI_HIP(hipEventCreateWithFlags(&ev_blur, hipEventDisableTiming));
-    ORBMI_HIP(hipEventCreateWithFlags(&ev_l0, hipEventDisableTiming));
-    ORBMI_HIP(hipEventCreateWithFlags(&ev_f0, hipEventDisableTiming));
     // ORBextractor::ORBextractor  src/ORBextractor.cc:410-470 (same float/double steps)
     scale.assign(nl, 1.f); sigma2.assign(nl, 1.f); inv_scale.resize(nl); inv_sigma2.resize(nl);
     const double sfd = (double)sf;
@@ -2073,6 +2068,19 @@ int Extractor::reserve(int batch, int capacity) {
     return ORBMI_OK;
 }
 
+// The side stream and its events, created on first use: only the large batches that put the
+// blur (or the early level-0 FAST) on a side stream need them, and an idle stream per extractor
+// would otherwise count against the process's hardware queues (GPU_MAX_HW_QUEUES) for nothing.
+int Extractor::ensure_side_stream() {
+    if (bstream) return ORBMI_OK;
+    ORBMI_HIP(orbmi::stream_create(&bstream, "EXTRACTOR"));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_pyr, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_blur, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_l0, hipEventDisableTiming));
+    ORBMI_HIP(hipEventCreateWithFlags(&ev_f0, hipEventDisableTiming));
+    return ORBMI_OK;
+}
+
 int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image_stride,
                    orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity) {
     ORBMI_HIP(hipSetDevice(device));
@@ -2089,6 +2097,10 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     // (0.143 -> 0.222 ms) and config 5 stayed at 89k frames/s (profiles/r04/fast_early_ab.txt).
     const bool early = batch > kPyrTiledMaxBatch && blur_mode == 0 && !fast_v1 && fast_early &&
                        levels[0].cell_begin == 0 && nlevels > 1;
+    if (blur_mode == 0 || early) {
+        const int rc = ensure_side_stream();
+        if (rc) return rc;
+    }
     auto launch_fast = [&](int c0, int c1, hipStream_t s) {
         const dim3 grid((c1 - c0 + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
         if (fast_v1)  // ORBMI_FAST=v1: per-lane bit assembly, runtime tile pitch (A/B)

@@ -42,6 +42,16 @@
 #include "se3_device.h"
 #include "wave_ops.h"
 
+// The fan-ins between workgroups (k_ba_update_errors, k_ba_errors, the keyframe halves of
+// k_ba_schur) hand partial sums over without __threadfence: agent-scope relaxed (sc1) stores
+// drained by s_waitcnt vmcnt(0) before a relaxed arrival atomicAdd, read back by sc1 loads.
+// That is ordered on gfx9's memory system (the store completes at L2 before the counter moves;
+// sc1 loads bypass the non-coherent L1), not by the HIP/LLVM memory model, so the file builds
+// only for the target it was validated on (MI355X_MICROARCH.md, inter-workgroup hand-offs).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "lba.hip's fence-free fan-ins are validated on gfx950 only"
+#endif
+
 // fp64 solver with a 1e-4 parity tolerance: multiply-add contraction allowed here (the
 // bit-exact extractor / matcher sources keep -ffp-contract=off)
 #pragma clang fp contract(fast)
@@ -78,6 +88,8 @@ struct BaCtl {
     int gen;          // the optimize() the LM state belongs to (1: optimize(5), 2: optimize(10))
     int phases_done;  // optimize() calls finished (k_ba_errors' tail)
     int do_more;      // optimize(10) runs: pbStopFlag was clear after optimize(5) (:689-692)
+    int checks;       // pbStopFlag checks made so far (#0 is the host's, src/Optimizer.cc:685)
+    int stop_seen;    // the first check that found the flag raised (-1: none)
 };
 
 struct BaDev {
@@ -86,6 +98,7 @@ struct BaDev {
     int nb_e, nb_p, nb_q;           // blocks: edges (256), points (256), points (kBaUpdPts per block)
     BaCtl* ctl;
     const volatile int* stop;  // host-mapped mirror of pbStopFlag (may be null)
+    int stop_at;               // orbmi_ba_set_stop_at_check: the flag reads raised from this check on (< 0: off)
     double* Tb[2];             // poses: SE3Quat (x, y, z, w, tx, ty, tz, -), current / trial
     double* Xb[2];             // points (x, y, z, -), current / trial
     double* part_lin;          // nb_e: robust chi2 at linearisation
@@ -326,9 +339,25 @@ __device__ inline bool point_active(const BaDev& a, int p) {
 
 // ---------------------------------------------------------------- setup / activation
 // vertices: SE3Quat from float Tcw (Converter::toSE3Quat), points to double
+// One read of pbStopFlag (the caller's flag through its host-mapped mirror, or the deterministic
+// stop_at hook), numbered in the order the reference evaluates them (orbmi_ba_set_stop_at_check);
+// one lane.  The reads are where g2o reads _forceStopFlag: SparseOptimizer::optimize's loop
+// condition (sparse_optimizer.cpp:376), the LM inner loop's (levenberg.cpp:149), and
+// src/Optimizer.cc:689.
+__device__ inline bool ba_check_stop(const BaDev& a, BaCtl& c) {
+    const int idx = c.checks++;
+    const bool s = (a.stop && *a.stop) || (a.stop_at >= 0 && idx >= a.stop_at);
+    if (s && c.stop_seen < 0) c.stop_seen = idx;
+    return s;
+}
+
 __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restrict__ T, double* __restrict__ X,
                                                        unsigned char* __restrict__ out_erase) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {  // check #0 (src/Optimizer.cc:685) was the host's, and found the flag clear
+        a.ctl->checks = 1;
+        a.ctl->stop_seen = -1;
+    }
     if (i < a.nkf) {
         const float* t = a.kfs[i].tcw;
         double R[3][3];
@@ -412,7 +441,6 @@ __global__ __launch_bounds__(kBaBlock) void k_ba_activate_edges(BaDev a, int max
 // ballot scan over the id-ordered keyframes, and the LM state of levenberg.cpp:61-70.  The
 // edges' pose indices (e_pi) are written by the next k_ba_linearize.
 __device__ inline void activate_ctl_body(const BaDev& a, int max_it, int gen) {
-    if (a.stop && *a.stop) max_it = 0;  // pbStopFlag raised meanwhile: optimize() returns at once
     const int lane = threadIdx.x;
     double c = 0;
     for (int b = lane; b < a.nb_e; b += 64) c += a.part_lin[b];
@@ -449,7 +477,11 @@ __device__ inline void activate_ctl_body(const BaDev& a, int max_it, int gen) {
         c2.nbad = 0;
         c2.lambda = 0;
         c2.ni = 2;
-        c2.done = (n + nl == 0) || c2.unsupported || max_it <= 0;
+        // SparseOptimizer::optimize: no vertex -> return -1 before the loop; else the loop
+        // condition `i < iterations && !terminate()` before iteration 0
+        const bool empty = n + nl == 0;
+        const bool stopped = !empty && max_it > 0 && ba_check_stop(a, c2);
+        c2.done = empty || c2.unsupported || max_it <= 0 || stopped;
         c2.gen = gen;
     }
 }
@@ -795,6 +827,21 @@ constexpr int kSchurThreads = 512;
 constexpr int kSchurWaves = kSchurThreads / 64;
 constexpr int kSchurKfSplit = 2;  // blocks per free keyframe for its diagonal block and b_schur
 
+// What block b of a k_ba_schur launch over nblk pose-pair blocks and nf free keyframes does
+// (host and device: the CPU test orbmi_debug_ba_schur_blocks checks every index it leads to):
+// b < nblk: pose-pair block b (blk_kf[2b], blk_kf[2b + 1], blk_start[b..b+1]); then kSchurKfSplit
+// blocks per free keyframe r (free_kf[r], part_kf / arrive_kf[r]); then the MFMA padding block.
+struct SchurRole {
+    int kind;  // 0 pair block, 1 keyframe block, 2 MFMA padding, 3 past the launch
+    int r, h;  // kind 1: free keyframe rank, half
+};
+__host__ __device__ inline SchurRole schur_role(int b, int nblk, int nf) {
+    if (b < nblk) return SchurRole{0, b, 0};
+    const int rb = b - nblk;
+    if (rb < kSchurKfSplit * nf) return SchurRole{1, rb / kSchurKfSplit, rb % kSchurKfSplit};
+    return SchurRole{rb == kSchurKfSplit * nf ? 2 : 3, 0, 0};
+}
+
 // sum over keyframe k's edges (keyframe-CSR rows of Hpe) of values [q0, q0 + NQ) of the 27,
 // fixed order: thread t takes edges t, t + 512, ... (a config-3 keyframe has ~830: two per
 // thread, every load of both in flight at once), then a per-wave reduce-scatter (DPP /
@@ -879,7 +926,8 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[3] = lam;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if ((int)blockIdx.x == a.nblk + kSchurKfSplit * a.nf) {  // the MFMA solve's padding: identity rows / columns
+    const SchurRole role = schur_role(blockIdx.x, a.nblk, a.nf);
+    if (role.kind == 2) {  // the MFMA solve's padding: identity rows / columns
         // beyond N, zero columns 1..15 of the right-hand-side tiles.  Static within an optimize()
         // (N fixed, the solve only reads S): written on its first trial only
         if (!(ctl.it == 0 && ctl.trial == 0)) return;
@@ -897,14 +945,14 @@ __device__ __attribute__((always_inline)) inline void schur_body(BaDev a) {
         }
         return;
     }
-    if ((int)blockIdx.x >= a.nblk) {
+    if (role.kind == 1) {
         // blocks nblk + 2 r + h: half h of the r-th free keyframe's edges (CSR order) for its
         // diagonal block and b_schur: Hpp and b_p (the edges' Hpe rows), and per edge e of point l
         // with B = Hpl_e the diagonal pair product B D_l^-1 B^T and B D_l^-1 b_l -- the diagonal
         // pose pair's observation pairs are exactly the keyframe's edges, so the (i, i) pair
         // blocks return at once.  The two halves' 54 sums meet through sc1 partials and an
         // arrival counter (the second to arrive combines them in half order and writes)
-        const int rb = blockIdx.x - a.nblk, r = rb / kSchurKfSplit, h = rb % kSchurKfSplit;
+        const int r = role.r, h = role.h;
         const int ka = a.free_kf[r];
         const int i1 = a.pose_idx[ka];
         if (i1 < 0) return;
@@ -2281,8 +2329,9 @@ __device__ inline void k_ba_control_body(const BaDev& a) {
     }
     c.trial++;
     c.steps++;
-    const bool stop = a.stop && *a.stop;
-    if (rho < 0 && c.trial < 10 && !stop) return;  // next trial of the same iteration
+    // the inner loop's `while (rho < 0 && qmax < 10 && !terminate())`: the flag is read only
+    // when the first two hold; raised, the iteration ends on the rejected trial
+    if (rho < 0 && c.trial < 10 && !ba_check_stop(a, c)) return;  // next trial of the same iteration
     c.it++;
     bool term;
     if (c.trial == 10 || rho == 0) {
@@ -2293,6 +2342,8 @@ __device__ inline void k_ba_control_body(const BaDev& a) {
         term = c.nbad >= 3;
     }
     c.trial = 0;
+    // the outer loop's `i < iterations && !terminate() && ok`: the flag is read while i < iterations
+    const bool stop = c.it < c.max_it && ba_check_stop(a, c);
     if (term || c.it >= c.max_it || stop) c.done = 1;
 }
 
@@ -2438,7 +2489,7 @@ __device__ inline void chi_body(const BaDev& a, int phase) {
         c.chi_out[phase] = chi;
         c.it_out[phase] = (c.np + c.nl == 0) ? -1 : c.it;
         c.phases_done = phase + 1;
-        if (phase == 0) c.do_more = !(a.stop && *a.stop);
+        if (phase == 0) c.do_more = !ba_check_stop(a, c);  // src/Optimizer.cc:689-692 (bDoMore)
     }
 }
 
@@ -2491,6 +2542,7 @@ struct orbmi_ba {
     orbmi::BaCtl* h_ctl = nullptr;  // pinned readback of the LM control block
     int* h_stop = nullptr;          // host-mapped mirror of the caller's stop flag
     int* d_stop = nullptr;          //   (its device address)
+    int stop_at = -1;               // orbmi_ba_set_stop_at_check
 };
 
 namespace {
@@ -2519,6 +2571,59 @@ struct BaTrace {
 // the caller's stop flag (bool* pbStopFlag, src/Optimizer.cc:483), written by other threads:
 // read with an atomic load
 inline bool stop_set(const volatile int* stop) { return stop && __atomic_load_n(stop, __ATOMIC_ACQUIRE) != 0; }
+
+// The pose-pair blocks' ids.  Pair l = (ra, rb >= ra) in row-major order (l = ra nf - ra (ra - 1)
+// / 2 + rb - ra) runs as block blk_id[l] of k_ba_schur.  Placed by row: the blocks of row ra
+// (which all read the Hpl blocks of keyframe ra's edges) go to ids of one residue mod 8 -- one XCD
+// under the round-robin dispatch, so their re-reads of those blocks hit one L2 (speed only).
+// Rows are dealt to the 8 residues largest first onto the least loaded; pairs beyond a residue's
+// ids take the ids left over, in increasing order.  rowmajor: blk_id[l] = l (A/B runs).
+// Every block id in [0, nblk) must name exactly one pair: an id no pair took would leave its
+// blk_kf entry to whatever the pinned staging buffer last held, and the pair kernels index
+// pose_idx / kf_start with it (the round-4 r04x illegal address, from a work-in-progress form of
+// this table, on the first call that reused a larger graph's staging buffer).  So the table is
+// checked before it is used: false = not a permutation (never, by construction; tested for
+// every nf by tests/test_capi_exports.py through orbmi_debug_ba_schur_blocks).
+bool ba_block_table(int nf, bool rowmajor, std::vector<int>& blk_id) {
+    const int nblk = nf * (nf + 1) / 2;
+    blk_id.assign(std::max(nblk, 1), -1);
+    if (rowmajor) {
+        for (int x = 0; x < nblk; x++) blk_id[x] = x;
+    } else {
+        const int R = 8;
+        std::vector<int> load(R, 0), grp(std::max(nf, 1));
+        for (int r = 0; r < nf; r++) {  // row r holds nf - r pairs: already largest first
+            const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            grp[r] = g;
+            load[g] += nf - r;
+        }
+        std::vector<int> next(R);
+        for (int g = 0; g < R; g++) next[g] = g;
+        std::vector<char> used(std::max(nblk, 1), 0);
+        std::vector<int> spill;
+        int l = 0;
+        for (int ra = 0; ra < nf; ra++)
+            for (int rb = ra; rb < nf; rb++, l++) {
+                const int g = grp[ra];
+                if (next[g] < nblk) { blk_id[l] = next[g]; used[next[g]] = 1; next[g] += R; }
+                else spill.push_back(l);
+            }
+        int free_id = 0;
+        for (int x : spill) {
+            while (free_id < nblk && used[free_id]) free_id++;
+            if (free_id >= nblk) return false;
+            blk_id[x] = free_id;
+            used[free_id] = 1;
+        }
+    }
+    std::vector<char> hit(std::max(nblk, 1), 0);
+    for (int x = 0; x < nblk; x++) {
+        const int id = blk_id[x];
+        if (id < 0 || id >= nblk || hit[id]) return false;
+        hit[id] = 1;
+    }
+    return true;
+}
 
 // Trial steps enqueued beyond the iterations still to run: a rejected trial consumes one step
 // without finishing an iteration, so the steps enqueued up front usually finish optimize().
@@ -2552,8 +2657,6 @@ struct Runner {
             default: break;
         }
     }
-
-    bool stopped() const { return stop_set(stop); }
 
     // wait for the stream; meanwhile mirror the caller's stop flag to the device, yielding the
     // core between polls (the caller's other threads, e.g. tracking, run on the host meanwhile)
@@ -2652,6 +2755,33 @@ void orbmi_ba_destroy(orbmi_ba* b) {
     delete b;
 }
 
+int orbmi_debug_ba_schur_blocks(int nf, int* table, int cap, int* n_out) {
+    if (nf < 0 || nf > kBaMaxPoses || !n_out) return ORBMI_E_ARG;
+    const int nblk = nf * (nf + 1) / 2, nb = nblk + kSchurKfSplit * nf + 1;
+    *n_out = nb;
+    if (cap < nb || !table) return ORBMI_E_CAP;
+    std::vector<int> blk_id;
+    if (!ba_block_table(nf, false, blk_id)) return ORBMI_E_UNSUPPORTED;
+    std::vector<int> ra_of(std::max(nblk, 1)), rb_of(std::max(nblk, 1)), l_of(std::max(nblk, 1));
+    for (int ra = 0, l = 0; ra < nf; ra++)
+        for (int rb = ra; rb < nf; rb++, l++) { ra_of[blk_id[l]] = ra; rb_of[blk_id[l]] = rb; l_of[blk_id[l]] = l; }
+    for (int b = 0; b < nb; b++) {
+        const SchurRole role = schur_role(b, nblk, nf);
+        int* t = table + 4 * b;
+        t[0] = role.kind;
+        t[1] = role.kind == 0 ? ra_of[role.r] : role.kind == 1 ? role.r : -1;
+        t[2] = role.kind == 0 ? rb_of[role.r] : role.kind == 1 ? role.h : -1;
+        t[3] = role.kind == 0 ? l_of[role.r] : -1;
+    }
+    return ORBMI_OK;
+}
+
+int orbmi_ba_set_stop_at_check(orbmi_ba* b, int k) {
+    if (!b) return ORBMI_E_ARG;
+    b->stop_at = k < 0 ? -1 : k;
+    return ORBMI_OK;
+}
+
 int orbmi_ba_set_stream(orbmi_ba* b, void* stream) {
     if (!b) return ORBMI_E_ARG;
     ORBMI_HIP(hipSetDevice(b->device));
@@ -2675,9 +2805,12 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     R->aborted = 0;
     R->iterations[0] = R->iterations[1] = 0;
     R->chi2[0] = R->chi2[1] = 0;
+    R->stop_check = -1;
+    R->checks = 1;
     for (int i = 0; i < P->nedge; i++) R->erase[i] = 0;
-    if (stop_set(stop)) {  // src/Optimizer.cc:685-687
+    if (stop_set(stop) || h.stop_at == 0) {  // check #0, src/Optimizer.cc:685-687
         R->aborted = 1;
+        R->stop_check = 0;
         return ORBMI_OK;
     }
     const int nkf = P->nkf, npt = P->npt, ne = P->nedge;
@@ -2685,10 +2818,18 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     // host-side graph indexing: edges grouped by point (the reference inserts them point by
     // point), CSR by keyframe, keyframes ordered by id (SparseOptimizer vertex order).  The index
     // arrays are written straight into the pinned staging buffer that goes up in one copy.
-    for (int i = 0; i < ne; i++) {
-        const orbmi_ba_edge& e = P->edges[i];
-        if (e.point < 0 || e.point >= npt || e.kf < 0 || e.kf >= nkf) return ORBMI_E_ARG;
-        if (i && e.point < P->edges[i - 1].point) return ORBMI_E_ARG;
+    {
+        // one edge per (point, keyframe), as the reference builds the graph from a map point's
+        // observations (a std::map per point): the per-keyframe Schur blocks sum each edge's
+        // B D^-1 B^T with itself only, so a second edge of one pair would lose its cross terms
+        std::vector<int> last_pt(std::max(nkf, 1), -1);
+        for (int i = 0; i < ne; i++) {
+            const orbmi_ba_edge& e = P->edges[i];
+            if (e.point < 0 || e.point >= npt || e.kf < 0 || e.kf >= nkf) return ORBMI_E_ARG;
+            if (i && e.point < P->edges[i - 1].point) return ORBMI_E_ARG;
+            if (last_pt[e.kf] == e.point) return ORBMI_E_ARG;  // (edges come grouped by point)
+            last_pt[e.kf] = e.point;
+        }
     }
     std::vector<int> order(std::max(nkf, 1));
     for (int k = 0; k < nkf; k++) order[k] = k;
@@ -2703,43 +2844,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const long long nblk_ll = (long long)nf * (nf + 1) / 2;
     if (nblk_ll > (1 << 20)) return ORBMI_E_UNSUPPORTED;
     const int nblk = (int)nblk_ll;
-    // pose-pair blocks placed by row: the blocks of row ra (pairs (ra, rb >= ra), which all read
-    // the Hpl blocks of keyframe ra's edges) go to block ids of one residue mod 8 -- one XCD under
-    // the round-robin dispatch, so their re-reads of those blocks hit one L2 (speed only).  Rows
-    // are dealt to the 8 residues largest first onto the least loaded; pairs beyond a residue's
-    // ids take the ids left over.
-    std::vector<int> blk_id(std::max(nblk, 1));
-    {
-        const int R = 8;
-        std::vector<int> rows(nf), load(R, 0), grp(std::max(nf, 1));
-        for (int r = 0; r < nf; r++) rows[r] = r;  // row r holds nf - r pairs: already largest first
-        for (int r : rows) {
-            const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-            grp[r] = g;
-            load[g] += nf - r;
-        }
-        std::vector<int> next(R);
-        for (int g = 0; g < R; g++) next[g] = g;
-        std::vector<char> used(std::max(nblk, 1), 0);
-        std::vector<int> spill;
-        int l = 0;
-        for (int ra = 0; ra < nf; ra++)
-            for (int rb = ra; rb < nf; rb++, l++) {
-                const int g = grp[ra];
-                if (next[g] < nblk) { blk_id[l] = next[g]; used[next[g]] = 1; next[g] += R; }
-                else { blk_id[l] = -1; spill.push_back(l); }
-            }
-        if (getenv("ORBMI_BA_SCHUR_ROWMAJOR")) {  // (A/B: blocks in row-major pair order)
-            for (int x = 0; x < nblk; x++) blk_id[x] = x;
-            spill.clear();
-        }
-        int free_id = 0;
-        for (int x : spill) {
-            while (used[free_id]) free_id++;
-            blk_id[x] = free_id;
-            used[free_id] = 1;
-        }
-    }
+    std::vector<int> blk_id;
+    if (!ba_block_table(nf, getenv("ORBMI_BA_SCHUR_ROWMAJOR") != nullptr, blk_id)) return ORBMI_E_UNSUPPORTED;
     auto blk_of = [nf, &blk_id](int ra, int rb) { return blk_id[ra * nf - ra * (ra - 1) / 2 + (rb - ra)]; };
     // ---- one device arena; the graph and its index arrays go up in one copy
     const int nb_e = std::max(1, (ne + kBaBlock - 1) / kBaBlock), nb_p = std::max(1, (npt + kBaBlock - 1) / kBaBlock);
@@ -2845,7 +2951,10 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     a.nb_e = nb_e; a.nb_p = nb_p; a.nb_q = nb_q;
     a.ctl = (BaCtl*)(B + o_ctl);
     a.stop = stop ? h.d_stop : nullptr;
-    *h.h_stop = 0;
+    a.stop_at = h.stop_at;
+    // the mirror starts with the flag's value now; Runner::wait keeps it current (the device reads
+    // it only at the checks)
+    *(volatile int*)h.h_stop = stop_set(stop) ? 1 : 0;
     a.Tb[0] = (double*)(B + o_T0); a.Tb[1] = (double*)(B + o_T1);
     a.Xb[0] = (double*)(B + o_X0); a.Xb[1] = (double*)(B + o_X1);
     a.part_lin = (double*)(B + o_plin); a.part_tchi = (double*)(B + o_ptchi); a.part_tscale = (double*)(B + o_ptsc);
@@ -2904,7 +3013,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     const char* slack_env = getenv("ORBMI_BA_SLACK");  // test hook: 0 forces the resume path
     const int slack = slack_env ? std::max(0, atoi(slack_env)) : kBaStepSlack;
     auto enqueue = [&](int from, int more) {
-        if (from == 0) r.prologue(r.stopped() ? 0 : 5, 1);
+        if (from == 0) r.prologue(5, 1);
         if (from <= 1) {
             for (int k = 0; k < (from == 0 ? 5 + slack : more); k++) r.step(1);
             r.epilogue(1);
@@ -2942,6 +3051,8 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     R->iterations[1] = second ? c.it_out[1] : 0;
     R->chi2[0] = c.chi_out[0];
     R->chi2[1] = second ? c.chi_out[1] : 0;
+    R->stop_check = c.stop_seen;
+    R->checks = c.checks;
     return ORBMI_OK;
 }
 

@@ -2073,9 +2073,17 @@ struct orbmi_slam {
                     if (cf.mps[i] >= 0 && cf.outlier[i]) cf.mps[i] = -1;
             }
             // Reset if the camera gets lost soon after initialisation (src/Tracking.cc:540-551):
-            // the map is cleared and the next frame initialises again; this frame is not recorded
+            // the map is cleared and the next frame initialises again; this frame is not recorded.
+            // With the mapping thread running, System::Reset only raises mbReset and
+            // Tracking::Reset runs at the start of the next TrackStereo (src/System.cc:139-146),
+            // outside mMutexMapUpdate: a LocalBA that finishes meanwhile needs that lock for its
+            // write-back, so waiting for the mapping thread here, inside Track(), would deadlock.
             if (state == LOST && keyframes_in_map() <= 5) {
-                SLAM_CHECK(reset());
+                if (async_lm()) {
+                    request_reset();
+                } else {
+                    SLAM_CHECK(reset());
+                }
                 resets++;
                 st.reset = 1;
                 st.state = state;
@@ -2106,22 +2114,34 @@ struct orbmi_slam {
         return ORBMI_OK;
     }
 
-    // Tracking::Reset (src/Tracking.cc:1780-1826): LocalMapping drops its queue and finishes the
-    // keyframe in hand (RequestReset; the tracking thread lets go of the map lock meanwhile), then
-    // the map, the tracking state, the frame / keyframe ids and the trajectory lists start over
-    int reset() {
-        if (async_lm()) {
-            {
-                std::lock_guard<std::mutex> g(q_mtx);
-                lm_queue.clear();
-            }
-            if (held_lock) held_lock->unlock();
-            {
-                std::unique_lock<std::mutex> g(q_mtx);
-                idle_cv.wait(g, [&] { return lm_queue.empty() && !lm_busy; });
-            }
-            if (held_lock) held_lock->lock();
+    // System::Reset with the mapping thread running: LocalMapping::RequestReset drops the queued
+    // keyframes (its ResetIfRequested, src/LocalMapping.cc:700-716; the keyframe in hand is
+    // finished first) and the rest of Tracking::Reset waits for the next TrackStereo
+    bool reset_pending = false;
+    void request_reset() {
+        std::lock_guard<std::mutex> g(q_mtx);
+        lm_queue.clear();
+        reset_pending = true;
+    }
+
+    // the deferred Tracking::Reset at the start of orbmi_slam_track_stereo (no lock held): the
+    // mapping thread finishes the keyframe in hand -- a LocalBA included, whose write-back takes
+    // update_mtx, free now -- then the map is cleared under both locks
+    int deferred_reset() {
+        {
+            std::unique_lock<std::mutex> g(q_mtx);
+            idle_cv.wait(g, [&] { return lm_queue.empty() && !lm_busy; });
+            reset_pending = false;
         }
+        std::lock_guard<std::mutex> u(update_mtx);
+        std::lock_guard<std::mutex> m(map_mtx);
+        return reset();
+    }
+
+    // Tracking::Reset (src/Tracking.cc:1780-1826): the map, the tracking state, the frame /
+    // keyframe ids and the trajectory lists start over (the mapping thread is idle: synchronous
+    // mode, or deferred_reset)
+    int reset() {
         for (auto& kf : kfs)
             if (kf.d_block) (void)hipFree(kf.d_block);
         kfs.clear();
@@ -2265,6 +2285,7 @@ void orbmi_slam_destroy(orbmi_slam* h) {
 int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
                             double timestamp, float* tcw_out, int* has_pose) {
     if (!h || !left || !right || rows <= 0 || cols <= 0 || step < (size_t)cols) return ORBMI_E_ARG;
+    if (h->reset_pending) SLAM_CHECK(h->deferred_reset());  // (src/System.cc:139-146)
     TrackedFrame cf;
     cf.id = h->frame_count;
     cf.ts = timestamp;

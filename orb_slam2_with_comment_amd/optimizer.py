@@ -31,7 +31,14 @@ class LocalBA:
         except Exception:
             pass
 
-    def run(self, problem: BAProblem, stop: C.c_int | None = None):
+    def set_stop_at_check(self, k: int):
+        """The deterministic pbStopFlag (orbmi_ba_set_stop_at_check): later calls read the flag
+        raised from their k-th check on; k < 0 turns it off."""
+        check("orbmi_ba_set_stop_at_check", lib().orbmi_ba_set_stop_at_check(self._h, int(k)))
+
+    def run(self, problem: BAProblem, stop: C.c_int | None = None, stop_at_check: int | None = None):
+        if stop_at_check is not None:
+            self.set_stop_at_check(stop_at_check)
         r, tcw, pos, erase = problem.result_buffers()
         v = problem.view()
         check("orbmi_local_bundle_adjustment",
@@ -39,7 +46,8 @@ class LocalBA:
                                                   C.addressof(stop) if stop is not None else None))
         n = len(problem.kfs), len(problem.pts), len(problem.edges)
         return {"tcw": tcw[:n[0]].reshape(-1, 4, 4), "pos": pos[:n[1]], "erase": erase[:n[2]].astype(bool),
-                "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted}
+                "iterations": tuple(r.iterations), "chi2": tuple(r.chi2), "aborted": r.aborted,
+                "stop_check": r.stop_check, "checks": r.checks}
 
 
 class PoseOptimizer:

@@ -154,7 +154,7 @@ class BAProblemView(C.Structure):
 
 class BAResultView(C.Structure):
     _fields_ = [("tcw", C.c_void_p), ("pos", C.c_void_p), ("erase", C.c_void_p), ("iterations", C.c_int * 2),
-                ("chi2", C.c_double * 2), ("aborted", C.c_int)]
+                ("chi2", C.c_double * 2), ("aborted", C.c_int), ("stop_check", C.c_int), ("checks", C.c_int)]
 
 
 class BAProblem:

@@ -49,3 +49,41 @@ def test_lba_deterministic(oracle, small):
     b = oracle.local_ba(prob)
     np.testing.assert_array_equal(a["tcw"], b["tcw"])
     np.testing.assert_array_equal(a["erase"], b["erase"])
+
+
+def test_lba_stop_check_numbering(oracle, small):
+    """The deterministic pbStopFlag (orbmi_ba_set_stop_at_check's numbering): a run stopped at
+    check k is the unstopped run up to that check, so it reports k as the first raised read; #0 is
+    src/Optimizer.cc:685 (abort, no write-back), the last read before optimize(10) is :689 (no
+    second optimisation), and k past the last read changes nothing."""
+    prob, _ = small
+    free = oracle.local_ba(prob, stop_at_check=-1)
+    n = free["checks"]
+    assert free["stop_check"] == -1 and n >= 4
+    # 1 (#0) + optimize(5)'s loop reads + inner-loop reads + :689 + optimize(10)'s
+    assert n >= 1 + free["iterations"][0] + 1 + free["iterations"][1]
+    seen_no_more = False
+    for k in range(n + 2):
+        r = oracle.local_ba(prob, stop_at_check=k)
+        if k < n:
+            assert r["stop_check"] == k, (k, r["stop_check"])
+        else:
+            assert r["stop_check"] == -1
+            for key in ("tcw", "pos", "erase"):
+                np.testing.assert_array_equal(r[key], free[key])
+        if k == 0:
+            assert r["aborted"] == 1 and r["iterations"] == (0, 0)
+        if k == 1:   # raised before optimize(5)'s first iteration: 0 iterations, no optimize(10)
+            assert r["iterations"] == (0, 0) and not r["aborted"]
+        if r["iterations"][0] == free["iterations"][0] and r["iterations"][1] == 0 and k < n:
+            seen_no_more = True  # the :689 read (or one of optimize(5)'s last) ends the call there
+        assert r["iterations"][0] <= free["iterations"][0]
+    assert seen_no_more
+
+
+def test_lba_stop_flag_equals_hook(oracle, small):
+    """A flag already raised reads raised at every check: the same as the hook at 0."""
+    prob, _ = small
+    a = oracle.local_ba(prob, stop=True)
+    b = oracle.local_ba(prob, stop_at_check=0)
+    assert a["aborted"] == b["aborted"] == 1 and a["stop_check"] == b["stop_check"] == 0

@@ -161,14 +161,17 @@ def test_native_reset_after_loss_matches_oracle(tmp_path):
 
 
 def test_native_reset_while_mapping_concurrently(tmp_path):
-    """Tracking::Reset with the concurrent LocalMapping (csrc/slam.cpp reset(): the queue is
-    cleared, the caller's map lock released while the mapping thread finishes the keyframe in
-    hand, its HBM blocks freed, the lock taken again): frames 0-3 track and queue keyframes, the
-    flat frame 4 is lost with <= 5 keyframes in the map and resets, frames 5-8 initialise again and
-    track; the counts start over and Shutdown joins the mapping thread cleanly."""
-    fr = render_sequence(8)
+    """Tracking::Reset with the concurrent LocalMapping: frames 0-5 track and queue keyframes (4
+    in the map after frame 5, whose keyframe starts a LocalMapping job with a LocalBA), the flat
+    frame 6 is lost with <= 5 keyframes and asks for the reset while that job -- LocalBA
+    included -- is typically still running; as System::Reset does (src/System.cc:139-146), the
+    reset itself runs at the start of the next TrackStereo, outside mMutexMapUpdate, after the
+    mapping thread has finished the keyframe in hand (a LocalBA write-back needs that lock, so
+    resetting inside Track() could deadlock).  Frames 7-10 initialise again and track; the
+    counts start over and Shutdown joins the mapping thread cleanly."""
+    fr = render_sequence(10)
     flat = np.full_like(fr[0][0], 128)
-    seq = [f[:2] for f in fr[:4]] + [(flat, flat)] + [f[:2] for f in fr[4:]]
+    seq = [f[:2] for f in fr[:6]] + [(flat, flat)] + [f[:2] for f in fr[6:]]
     s = sequence_settings(tmp_path)
     slam = NativeStereoSLAM(s, device=0, vocabulary=small_vocabulary(), async_local_mapping=True)
     for i, (L, R) in enumerate(seq):
@@ -176,10 +179,10 @@ def test_native_reset_while_mapping_concurrently(tmp_path):
     slam.WaitLocalMapping()
     st = slam.stats
     assert len(st) == len(seq)
-    assert all(x["state"] == OK for x in st[:4]), st[:4]
-    assert st[4]["reset"] == 1 and st[4]["n"] == 0, st[4]
-    assert st[5]["init"] and st[5]["frame"] == 0 and st[5]["keyframes"] == 1, st[5]
-    assert all(x["state"] == OK for x in st[5:]), st[5:]
+    assert all(x["state"] == OK for x in st[:6]), st[:6]
+    assert st[6]["reset"] == 1 and st[6]["n"] == 0, st[6]
+    assert st[7]["init"] and st[7]["frame"] == 0 and st[7]["keyframes"] == 1, st[7]
+    assert all(x["state"] == OK for x in st[7:]), st[7:]
     c = slam.counts()
     assert c["frames"] == 4 and 1 <= c["keyframes"] <= 4 and c["mappoints"] > 100, c
     T, _, lost = slam.frame_poses()

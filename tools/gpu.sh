@@ -90,7 +90,8 @@ for step in "$@"; do
             m=${step#pmc}; m=${m#_}; m=${m:-track}
             run pmc_fetch_$m 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/pmc_fetch_$m -o fetch -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
             run pmc_write_$m 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/pmc_write_$m -o write -- python3 bench.py $(modeargs $m) --steps 20 --warmup 4 --no-cpu-baseline
-            python tools/pmc_traffic.py $OUT/pmc_fetch_$m $OUT/pmc_write_$m $P/traffic_$m.json && head -40 $P/traffic_$m.json;;
+            cfg=$(python bench.py $(modeargs $m) --print-traffic-config)
+            python tools/pmc_traffic.py $OUT/pmc_fetch_$m $OUT/pmc_write_$m $P/traffic_$m.json "$cfg" && head -40 $P/traffic_$m.json;;
         native|native_async)
             a=${step#native}; a=${a#_}
             run native_probe$a 300 python tools/native_probe.py 200 $a; cat $OUT/native_probe$a.log;;

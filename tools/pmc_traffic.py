@@ -1,6 +1,9 @@
 """Summarise rocprofv3 PMC runs into per-kernel HBM bytes per launch.
 
-    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [CONFIG_JSON]
+
+CONFIG_JSON (`python bench.py --print-traffic-config <the run's args>`) is stored as "config":
+bench.py reports a summary as roofline.traffic only for a run of the same workload.
 
 FETCH_DIR / WRITE_DIR hold the counter_collection CSVs of two separate passes
 (`rocprofv3 --pmc FETCH_SIZE --kernel-trace ...`, `--pmc WRITE_SIZE ...`).  Per
@@ -43,7 +46,7 @@ def read(d, counter):
     return {k: sum(v) / len(v) for k, v in vals.items() if v}
 
 
-def main(fetch_dir, write_dir, out):
+def main(fetch_dir, write_dir, out, config=None):
     fetch = read(fetch_dir, "FETCH_SIZE")
     write = read(write_dir, "WRITE_SIZE")
     per = {}
@@ -53,11 +56,11 @@ def main(fetch_dir, write_dir, out):
         w = write.get(s, 0.0)
         per[s] = round((2 * f + w) * 1024)
         raw[s] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w}
-    json.dump({"per_launch_bytes": per, "raw_per_launch": raw,
+    json.dump({"per_launch_bytes": per, "raw_per_launch": raw, "config": json.loads(config) if config else None,
                "note": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half count, calibrated for 4/8/16-B loads: profiles/r04/fetch_calibration.txt)"},
               open(out, "w"), indent=1)
     print(json.dumps(per))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
