@@ -49,6 +49,43 @@ int orbmi_debug_greedy_cycles(unsigned long long* out, int reset);
  * permutation, every index a block reads in range). */
 int orbmi_debug_ba_schur_blocks(int nf, int* table, int cap, int* n_out);
 
+/* The schedule of a run with the concurrent LocalMapping (orbmi_slam_settings.async_local_mapping):
+ * one event per acquisition of the map lock, in acquisition order.  Tracking and LocalMapping
+ * touch shared state (the map, the keyframe queue, AcceptKeyFrames) only while they hold it, and
+ * their GPU calls run on copies with it released, so this order -- with each LocalBA's first
+ * raised pbStopFlag read (orbmi_slam_get_local_ba_log) -- determines the run: replayed through
+ * the same host logic (system.StereoSLAM.replay_schedule, tests/test_native_slam_gpu.py) it gives
+ * the same decisions and trajectory.  An event's label is where the thread resumes: */
+#define ORBMI_SCHED_T_FRAME 1          /* Track() of frame `arg` begins                          */
+#define ORBMI_SCHED_T_BOW 2            /* after TrackReferenceKeyFrame's SearchByBoW            */
+#define ORBMI_SCHED_T_POSE 3           /* after a PoseOptimization call (TrackReferenceKeyFrame) */
+#define ORBMI_SCHED_T_LF 4             /* after TrackWithMotionModel's searches + PoseOptimization */
+#define ORBMI_SCHED_T_LOCAL 5          /* after TrackLocalMap's SearchLocalPoints + PoseOptimization */
+#define ORBMI_SCHED_T_RESET 6          /* the deferred Tracking::Reset                           */
+#define ORBMI_SCHED_L_JOB 16           /* the mapping thread takes the next queued keyframe (`arg`, -1 none) */
+#define ORBMI_SCHED_L_DISTINCTIVE 17   /* after a ComputeDistinctiveDescriptors call             */
+#define ORBMI_SCHED_L_CREATE 18        /* after CreateNewMapPoints' searches + triangulation     */
+#define ORBMI_SCHED_L_CREATE_PAIR 19   /* after one pair's search (keyframes without HBM copies)  */
+#define ORBMI_SCHED_L_FUSE_BATCH 20    /* after SearchInNeighbors' batched Fuse searches         */
+#define ORBMI_SCHED_L_FUSE_REFRESH 21  /* after the refresh before target `arg`'s replay         */
+#define ORBMI_SCHED_L_FUSE 22          /* after one Fuse search                                  */
+#define ORBMI_SCHED_L_BA 23            /* after LocalBundleAdjustment's optimisation (keyframe `arg`) */
+typedef struct orbmi_slam_event {
+    int32_t thread;                /* 0 Tracking, 1 LocalMapping                             */
+    int32_t label, arg;
+} orbmi_slam_event;
+/* capacity < n -> ORBMI_E_CAP with *n set.  Empty in synchronous mode. */
+int orbmi_slam_get_schedule(orbmi_slam* h, orbmi_slam_event* out, int capacity, int* n);
+
+/* Per LocalBundleAdjustment call (either mode), in call order. */
+typedef struct orbmi_slam_ba_record {
+    int32_t keyframe;              /* the LocalMapping keyframe                              */
+    int32_t stop_check, aborted, checks;  /* orbmi_ba_result's                               */
+    int32_t iterations[2];
+    int32_t edges, erased;
+} orbmi_slam_ba_record;
+int orbmi_slam_get_local_ba_log(orbmi_slam* h, orbmi_slam_ba_record* out, int capacity, int* n);
+
 /* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame
  * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
  * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,

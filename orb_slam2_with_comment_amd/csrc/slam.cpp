@@ -40,6 +40,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/orbmi.h"
+#include "../../include/orbmi_debug.h"
 #include "tri_geom.h"
 
 namespace {
@@ -403,6 +404,13 @@ struct orbmi_slam {
     void set_abort_ba(int v) { __atomic_store_n(&abort_ba, v, __ATOMIC_RELEASE); }
     std::thread lm_thread;
     bool async_lm() const { return s.async_local_mapping != 0; }
+    // the schedule (orbmi_slam_get_schedule): every acquisition of map_mtx with the mapping thread
+    // running, logged by the thread that took it (so map_mtx guards the log too)
+    std::vector<orbmi_slam_event> sched;
+    void log_section(int label, int arg) {
+        if (async_lm()) sched.push_back(orbmi_slam_event{on_mapping_thread ? 1 : 0, label, arg});
+    }
+    std::vector<orbmi_slam_ba_record> ba_log;  // orbmi_slam_get_local_ba_log (under map_mtx)
 
     // ---- Frame views (include/Frame.h members the matchers read) --------------------------
     orbmi_frame_view view(const std::vector<orbmi_keypoint>& keys, const std::vector<uint8_t>& desc,
@@ -557,7 +565,9 @@ struct orbmi_slam {
         fm.n_lf_points = (int)lfp.size();
         orbmi_pose_frame rec{};
         out.assign(std::max(cf.n(), 1), 0);
-        SLAM_CHECK(unlocked([&] { return orbmi_pose_optimization_frame(pose, &v, inv_level_sigma2.data(), &fm, &rec, out.data()); }));
+        SLAM_CHECK(unlocked(ORBMI_SCHED_T_POSE, cf.id, [&] {
+            return orbmi_pose_optimization_frame(pose, &v, inv_level_sigma2.data(), &fm, &rec, out.data());
+        }));
         std::memcpy(tcw_out.data(), rec.tcw, sizeof(rec.tcw));
         out.resize(cf.n());
         return ORBMI_OK;
@@ -698,7 +708,7 @@ struct orbmi_slam {
         std::vector<int32_t> best(std::max(np, 1));
         std::vector<uint8_t> out((size_t)std::max(np, 1) * 32);
         orbmi_matcher* mt = lmm();
-        SLAM_CHECK(unlocked([&] {
+        SLAM_CHECK(unlocked(ORBMI_SCHED_L_DISTINCTIVE, -1, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_DISTINCTIVE_CALL]);
             return orbmi_compute_distinctive_descriptors(mt, rows.data(), off.data(), np, best.data(), out.data());
         }));
@@ -764,8 +774,9 @@ struct orbmi_slam {
     // map lock released (their inputs are the caller's copies or the keyframes' HBM copies)
     orbmi_matcher* lm_matcher = nullptr;
     orbmi_matcher* lmm() const { return on_mapping_thread ? lm_matcher : matcher; }
+    // `label`, `arg`: where the thread resumes, for the schedule (ORBMI_SCHED_*)
     template <class F>
-    int unlocked(F f) {
+    int unlocked(int label, int arg, F f) {
         if (!held_lock) return f();
         held_lock->unlock();
         const int rc = f();
@@ -775,6 +786,7 @@ struct orbmi_slam {
             PhaseTimer pt(&phase_ms[PH_LOCK]);
             held_lock->lock();
         }
+        log_section(label, arg);
         return rc;
     }
 
@@ -907,29 +919,39 @@ struct orbmi_slam {
         return !lm_queue.empty();
     }
 
-    // the mapping thread: one keyframe at a time, holding map_mtx except inside the BA solve
+    // the mapping thread: one keyframe at a time, holding map_mtx except inside its GPU calls.
+    // The keyframe is taken from the queue and AcceptKeyFrames changes only under map_mtx (as
+    // Tracking reads them), so the order of the map_mtx acquisitions (the schedule) decides every
+    // interaction of the two threads.
     void lm_run() {
         on_mapping_thread = true;
         for (;;) {
-            int k;
             {
                 std::unique_lock<std::mutex> g(q_mtx);
                 q_cv.wait(g, [&] { return lm_quit || !lm_queue.empty(); });
                 if (lm_queue.empty()) return;  // quit with nothing left
-                k = lm_queue.front();
-                lm_queue.pop_front();
-                lm_busy = true;
             }
-            int rc;
+            int rc = ORBMI_OK;
             {
                 std::unique_lock<std::mutex> m(map_mtx);
-                held_lock = &m;
-                rc = local_mapping(k);
-                held_lock = nullptr;
-            }
-            {
+                log_section(ORBMI_SCHED_L_JOB, -1);
+                int k = -1;
+                {
+                    std::lock_guard<std::mutex> g(q_mtx);
+                    if (!lm_queue.empty()) {  // (a reset may have dropped it meanwhile)
+                        k = lm_queue.front();
+                        lm_queue.pop_front();
+                        lm_busy = true;  // SetAcceptKeyFrames(false)
+                    }
+                }
+                sched.back().arg = k;
+                if (k >= 0) {
+                    held_lock = &m;
+                    rc = local_mapping(k);
+                    held_lock = nullptr;
+                }
                 std::lock_guard<std::mutex> g(q_mtx);
-                lm_busy = false;
+                lm_busy = false;  // SetAcceptKeyFrames(true), still under map_mtx
                 if (rc && !lm_rc) lm_rc = rc;
             }
             idle_cv.notify_all();
@@ -1083,7 +1105,7 @@ struct orbmi_slam {
         std::vector<uint8_t> ok(std::max<size_t>(n1 * np, 1));
         std::vector<float> x3d(std::max<size_t>(3 * n1 * np, 1));
         orbmi_matcher* mt = lmm();
-        SLAM_CHECK(unlocked([&] {
+        SLAM_CHECK(unlocked(ORBMI_SCHED_L_CREATE, k, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_CREATE_CALL]);
             return orbmi_create_new_map_points(mt, &f1, &t1, cos1, has1.data(), &fv1, np, f2.data(), t2.data(),
                                                cos2.data(), mp2.data(), fv2.data(), F12.data(), m12.data(), ok.data(),
@@ -1149,7 +1171,7 @@ struct orbmi_slam {
             std::vector<int32_t> m12(std::max<size_t>(n1, 1));
             int nm = 0;
             orbmi_matcher* mt = lmm();
-            SLAM_CHECK(unlocked([&] {
+            SLAM_CHECK(unlocked(ORBMI_SCHED_L_CREATE_PAIR, (int)i, [&] {
                 return orbmi_search_for_triangulation(mt, &f1, has1.data(), &fv1, &f2, has2.data(), &fv2, F12, 0, 0,
                                                       m12.data(), &nm);
             }));
@@ -1237,7 +1259,7 @@ struct orbmi_slam {
         std::vector<int32_t> dist(pts.size());
         int nc = 0;
         orbmi_matcher* mt = lmm();
-        return unlocked([&] {
+        return unlocked(ORBMI_SCHED_L_FUSE, k, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
             return orbmi_fuse_search(mt, &v, rec.data(), in_kf.data(), (int)pts.size(), 3.f, best.data(), dist.data(), &nc);
         });
@@ -1312,7 +1334,7 @@ struct orbmi_slam {
         }
         std::vector<int32_t> best((size_t)nt * np), dist((size_t)nt * np);
         orbmi_matcher* mt = lmm();
-        SLAM_CHECK(unlocked([&] {
+        SLAM_CHECK(unlocked(ORBMI_SCHED_L_FUSE_BATCH, -1, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
             return orbmi_fuse_search_batch(mt, nt, views.data(), rec0.data(), in0.data(), np, 3.f, best.data(),
                                            dist.data(), nullptr);
@@ -1357,7 +1379,7 @@ struct orbmi_slam {
                 std::vector<uint8_t> dout((size_t)nd * 32);
                 for (int d = 0; d < nd; d++) std::memcpy(&dout[32 * d], mps[due[d]].desc, 32);
                 orbmi_matcher* mt2 = lmm();
-                SLAM_CHECK(unlocked([&] {
+                SLAM_CHECK(unlocked(ORBMI_SCHED_L_FUSE_REFRESH, t, [&] {
                     PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
                     return orbmi_fuse_search_refresh(mt2, rows.empty() ? nullptr : rows.data(), off.data(), nd,
                                                      dbest.data(), dout.data(), ntr, rv.data(), rrec.data(),
@@ -1576,11 +1598,19 @@ struct orbmi_slam {
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
             update_guard = std::unique_lock<std::mutex>(update_mtx);  // (lock order: update, map)
             held_lock->lock();
+            log_section(ORBMI_SCHED_L_BA, k);
         } else {
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
         }
         SLAM_CHECK(rc);
         ba_calls++;
+        {
+            int erased = 0;
+            for (uint8_t x : erase) erased += x != 0;
+            ba_log.push_back(orbmi_slam_ba_record{k, res.stop_check, res.aborted, res.checks,
+                                                  {res.iterations[0], res.iterations[1]}, (int)E.size(), erased});
+        }
+        if (res.aborted) return ORBMI_OK;  // src/Optimizer.cc:685-687: no write-back
         for (size_t e = 0; e < E.size(); e++) {
             if (!erase[e]) continue;
             const int m = e_ref[e].first, kk = e_ref[e].second;
@@ -1667,7 +1697,9 @@ struct orbmi_slam {
         const std::vector<int> kf_mps = kf.mps;  // the keyframe's matches when the search ran
         std::vector<int32_t> m(std::max(cf.n(), 1));
         int n = 0;
-        SLAM_CHECK(unlocked([&] { return orbmi_search_by_bow(matcher, &vk, ok_mp.data(), &fk, &vf, &ff, 0.7f, 1, m.data(), &n); }));
+        SLAM_CHECK(unlocked(ORBMI_SCHED_T_BOW, cf.id, [&] {
+            return orbmi_search_by_bow(matcher, &vk, ok_mp.data(), &fk, &vf, &ff, 0.7f, 1, m.data(), &n);
+        }));
         st.bow_matches = n;
         st.track = 2;
         if (n < 15) return ORBMI_OK;
@@ -1702,7 +1734,7 @@ struct orbmi_slam {
         const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
         {
             PhaseTimer pt(&phase_ms[PH_LF_SEARCH]);
-            SLAM_CHECK(unlocked([&] {
+            SLAM_CHECK(unlocked(ORBMI_SCHED_T_LF, cf.id, [&] {
                 int rc = orbmi_search_by_projection_last_frame(matcher, &vc, occ.data(), &vl, lfp.data(), th, 0, 1,
                                                                m.data(), &n);
                 if (!rc && n < 20)
@@ -1827,7 +1859,7 @@ struct orbmi_slam {
         std::vector<orbmi_mappoint_track> tr(std::max<size_t>(rec.size(), 1));
         {
             PhaseTimer pt(&phase_ms[PH_LOCAL_SEARCH]);
-            SLAM_CHECK(unlocked([&] {
+            SLAM_CHECK(unlocked(ORBMI_SCHED_T_LOCAL, cf.id, [&] {
                 return orbmi_search_local_points_track(matcher, &vc, occ.data(), rec.data(), (int)rec.size(), 1.f,
                                                        m_mp.data(), &nl, nullptr, tr.data());
             }));
@@ -1906,7 +1938,7 @@ struct orbmi_slam {
         fm.n_lf_points = nl;
         {
             PhaseTimer pt(&phase_ms[PH_LF_SEARCH]);
-            SLAM_CHECK(unlocked([&] {
+            SLAM_CHECK(unlocked(ORBMI_SCHED_T_LF, cf.id, [&] {
                 int rc = orbmi_search_by_projection_last_frame_if(matcher, &vc, t.d_occ, &vl, t.d_lfp, th, 0, 1, t.d_m,
                                                                   t.d_n, 1);
                 if (!rc) rc = orbmi_search_by_projection_last_frame_if(matcher, &vc, t.d_occ, &vl, t.d_lfp, 2 * th, 0, 1,
@@ -1980,7 +2012,7 @@ struct orbmi_slam {
         fm.n_mps = nr;
         {
             PhaseTimer pt(&phase_ms[PH_LOCAL_SEARCH]);
-            SLAM_CHECK(unlocked([&] {
+            SLAM_CHECK(unlocked(ORBMI_SCHED_T_LOCAL, cf.id, [&] {
                 int rc = orbmi_search_local_points_track(matcher, &vc, t.d_occ, t.d_rec, nr, 1.f, t.d_m, nullptr, nullptr,
                                                          t.d_tr);
                 if (!rc) rc = orbmi_pose_optimization_frame(pose, &vc, inv_level_sigma2.data(), &fm, t.d_pose, t.d_out);
@@ -2135,6 +2167,7 @@ struct orbmi_slam {
         }
         std::lock_guard<std::mutex> u(update_mtx);
         std::lock_guard<std::mutex> m(map_mtx);
+        log_section(ORBMI_SCHED_T_RESET, -1);
         return reset();
     }
 
@@ -2302,6 +2335,7 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     if (h->async_lm()) update_guard.lock();
     std::unique_lock<std::mutex> map_guard(h->map_mtx);
     delete lock_t;
+    h->log_section(ORBMI_SCHED_T_FRAME, cf.id);
     // with the mapping thread running, Tracking's GPU calls release the map lock (their inputs
     // are this thread's copies); the reference's Tracking and LocalMapping likewise interleave
     struct Hold {
@@ -2320,6 +2354,24 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     const TrackedFrame& lf = h->last_frame;
     if (has_pose) *has_pose = lf.has_tcw ? 1 : 0;
     if (tcw_out && lf.has_tcw) std::memcpy(tcw_out, lf.tcw.data(), 16 * sizeof(float));
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_schedule(orbmi_slam* h, orbmi_slam_event* out, int capacity, int* n) {
+    if (!h || !n) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    *n = (int)h->sched.size();
+    if (capacity < *n) return ORBMI_E_CAP;
+    if (*n) std::memcpy(out, h->sched.data(), sizeof(orbmi_slam_event) * (size_t)*n);
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_local_ba_log(orbmi_slam* h, orbmi_slam_ba_record* out, int capacity, int* n) {
+    if (!h || !n) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    *n = (int)h->ba_log.size();
+    if (capacity < *n) return ORBMI_E_CAP;
+    if (*n) std::memcpy(out, h->ba_log.data(), sizeof(orbmi_slam_ba_record) * (size_t)*n);
     return ORBMI_OK;
 }
 

@@ -131,6 +131,26 @@ class NativeStereoSLAM:
         check("orbmi_slam_get_phase_ms", lib().orbmi_slam_get_phase_ms(self._h, ms.ctypes.data, len(ms), C.byref(n)))
         return {k: round(float(v) / max(n.value, 1), 4) for k, v in zip(self.PHASES, ms)}
 
+    def schedule(self) -> np.ndarray:
+        """The concurrent run's schedule (orbmi_slam_get_schedule): int32 [n, 3] rows of (thread,
+        label, arg), one per acquisition of the map lock, in order (empty when synchronous)."""
+        return self._records("orbmi_slam_get_schedule", 3)
+
+    def local_ba_log(self) -> np.ndarray:
+        """Per LocalBundleAdjustment call: int32 rows of (keyframe, stop_check, aborted, checks,
+        iterations0, iterations1, edges, erased) (orbmi_slam_get_local_ba_log)."""
+        return self._records("orbmi_slam_get_local_ba_log", 8)
+
+    def _records(self, fn, width):
+        n = C.c_int()
+        rc = getattr(lib(), fn)(self._h, None, 0, C.byref(n))
+        out = np.zeros((max(n.value, 1), width), np.int32)
+        if n.value:
+            check(fn, getattr(lib(), fn)(self._h, out.ctypes.data, n.value, C.byref(n)))
+        elif rc not in (0,):
+            check(fn, rc)
+        return out[:n.value]
+
     def WaitLocalMapping(self):
         """Block until the mapping thread has processed every queued keyframe (async mode)."""
         check("orbmi_slam_wait_local_mapping", lib().orbmi_slam_wait_local_mapping(self._h))

@@ -44,6 +44,16 @@ from .types import (LF_HAS_MP, LF_OUTLIER, LFPOINT_DTYPE, MAPPOINT_DTYPE, MP_BAD
 
 NO_IMAGES_YET, NOT_INITIALIZED, OK, LOST = 0, 1, 2, 3   # Tracking::eTrackingState (include/Tracking.h)
 
+# Where a thread resumes after releasing the map lock (include/orbmi_debug.h ORBMI_SCHED_*): the
+# generators below yield these at the points where the native loop (csrc/slam.cpp) releases
+# its map lock around a GPU call, so a recorded concurrent schedule can be replayed here
+T_FRAME, T_BOW, T_POSE, T_LF, T_LOCAL, T_RESET = 1, 2, 3, 4, 5, 6
+L_JOB, L_DISTINCTIVE, L_CREATE, L_CREATE_PAIR, L_FUSE_BATCH, L_FUSE_REFRESH, L_FUSE, L_BA = range(16, 24)
+
+
+class ScheduleMismatch(RuntimeError):
+    """A recorded concurrent schedule does not fit this host logic (replay_schedule)."""
+
 
 # ---- float32 pose algebra (cv::Mat CV_32F products accumulate in double, src/Converter.cc) --
 def _mul(*ms) -> np.ndarray:
@@ -452,8 +462,8 @@ class GpuBackend:
     def distinctive(self, obs_desc, obs_off):
         return self.m_util.ComputeDistinctiveDescriptors(obs_desc, obs_off)[1]
 
-    def local_ba(self, problem, stop=None):
-        return self.ba.run(problem, stop)
+    def local_ba(self, problem, stop=None, stop_at_check=-1):
+        return self.ba.run(problem, stop, stop_at_check=stop_at_check)
 
     def close(self):
         for h in (self.ba, self.pose, self.m_tri, self.m_util, self.m_bow, self.m_local, self.m_lf, self.right, self.left):
@@ -520,6 +530,13 @@ class StereoSLAM:
         self.rel_poses, self.references, self.frame_times, self.lost = [], [], [], []
         self.stats = []   # per frame: dict of the Tracking counters
         self.ba_log = []  # per LocalBundleAdjustment: graph size and erased observations
+        # the concurrent LocalMapping of a replayed schedule (replay_schedule): the keyframe queue
+        # (mlNewKeyFrames), !AcceptKeyFrames, mbAbortBA and the recorded LocalBA stop checks
+        self._concurrent = False
+        self._queue = []
+        self._busy = False
+        self._abort = False
+        self._ba_stop_at = None   # kf -> the pbStopFlag check a LocalBA stops at (-1: none)
 
     # ---- System::TrackStereo ----------------------------------------------------------------
     def TrackStereo(self, imLeft, imRight, timestamp: float):
@@ -531,12 +548,26 @@ class StereoSLAM:
         self._track(cf)
         return None if cf.tcw is None else cf.tcw.copy()
 
+    @staticmethod
+    def _drain(gen):
+        """Run a stage generator to its end (synchronous use: the yields are the native loop's
+        lock releases, nothing runs in between)."""
+        try:
+            while True:
+                next(gen)
+        except StopIteration as e:
+            return e.value
+
     def _frame(self, f: TrackedFrame, tcw=None) -> Frame:
         return Frame(f.keys, f.desc, f.u_right, f.tcw if tcw is None else tcw, self.cam, self.backend.scale_factors,
                      self.cam.width, self.cam.height)
 
     def _track(self, cf: TrackedFrame):
-        """Tracking::Track for a stereo sensor in SLAM mode (src/Tracking.cc:287-581)."""
+        return self._drain(self._track_gen(cf))
+
+    def _track_gen(self, cf: TrackedFrame):
+        """Tracking::Track for a stereo sensor in SLAM mode (src/Tracking.cc:287-581); a generator
+        that yields where the native loop releases the map lock (T_*)."""
         if self.state == NO_IMAGES_YET:
             self.state = NOT_INITIALIZED
         st = {"frame": cf.id, "n": cf.n}
@@ -551,16 +582,16 @@ class StereoSLAM:
             if self.state == OK:
                 self._check_replaced_in_last_frame()
                 if self.velocity is None or cf.id < self.last_reloc_frame_id + 2:
-                    ok = self._track_reference_kf(cf, st)
+                    ok = yield from self._track_reference_kf(cf, st)
                 else:
-                    ok = self._track_motion_model(cf, st)
+                    ok = yield from self._track_motion_model(cf, st)
                     if not ok:
-                        ok = self._track_reference_kf(cf, st)
+                        ok = yield from self._track_reference_kf(cf, st)
             else:
                 ok = False   # Relocalization is out of scope
             cf.ref_kf = self.ref_kf
             if ok:
-                ok = self._track_local_map(cf, st)
+                ok = yield from self._track_local_map(cf, st)
             self.state = OK if ok else LOST
             if ok:
                 if self.last_frame.tcw is not None:
@@ -578,6 +609,8 @@ class StereoSLAM:
                         cf.map_points[i] = None
             # Reset if the camera gets lost soon after initialisation (src/Tracking.cc:540-551)
             if self.state == LOST and sum(1 for k in self.keyframes if not k.bad) <= 5:
+                if self._concurrent:
+                    raise NotImplementedError("replay_schedule: a run with a Tracking::Reset")
                 self._reset()
                 st["reset"] = 1
                 st["state"] = self.state
@@ -660,7 +693,7 @@ class StereoSLAM:
         kf = self._new_keyframe(cf)
         self.keyframes.append(kf)
         self._create_points(kf, cf, [i for i in range(cf.n) if cf.depth[i] > 0])
-        self._local_mapping(kf)
+        self._insert_keyframe(kf)
         self.last_kf_frame_id = cf.id
         self.local_kfs = [kf]
         self.local_mps = [m for m in self.mappoints if not m.bad]
@@ -670,7 +703,8 @@ class StereoSLAM:
         self.state = OK
 
     def _need_new_keyframe(self, cf: TrackedFrame, st) -> bool:
-        """Tracking::NeedNewKeyFrame (src/Tracking.cc:1140-1249) with LocalMapping idle."""
+        """Tracking::NeedNewKeyFrame (src/Tracking.cc:1140-1249); LocalMapping is idle when it
+        runs synchronously, else AcceptKeyFrames / InterruptBA / KeyframesInQueue() < 3."""
         s = self.settings
         nkfs = self._keyframes_in_map()
         if cf.id < self.last_reloc_frame_id + s.max_frames and nkfs > s.max_frames:
@@ -683,12 +717,18 @@ class StereoSLAM:
         n_non_tracked_close = int(np.sum(close & ~tracked))
         need_close = n_tracked_close < 100 and n_non_tracked_close > 70
         th_ref = 0.4 if nkfs < 2 else 0.75
+        idle = not self._busy
         c1a = cf.id >= self.last_kf_frame_id + s.max_frames
-        c1b = cf.id >= self.last_kf_frame_id + s.min_frames   # LocalMapping idle (synchronous)
+        c1b = cf.id >= self.last_kf_frame_id + s.min_frames and idle
         c1c = self.matches_inliers < n_ref * 0.25 or need_close
         c2 = (self.matches_inliers < n_ref * np.float32(th_ref) or need_close) and self.matches_inliers > 15
         st["need_kf"] = bool((c1a or c1b or c1c) and c2)
-        return st["need_kf"]
+        if not st["need_kf"]:
+            return False
+        if idle:
+            return True
+        self._abort = True                # mpLocalMapper->InterruptBA()
+        return len(self._queue) < 3       # stereo: KeyframesInQueue() < 3
 
     def _create_new_keyframe(self, cf: TrackedFrame):
         """Tracking::CreateNewKeyFrame for stereo (src/Tracking.cc:1251-1330)."""
@@ -710,22 +750,44 @@ class StereoSLAM:
             if z > self.settings.th_depth and npts > 100:
                 break
         self._create_points(kf, cf, new)
-        self._local_mapping(kf)
+        self._insert_keyframe(kf)
         self.last_kf_frame_id = cf.id
 
-    # ---- LocalMapping (synchronous) ---------------------------------------------------------
+    def _insert_keyframe(self, kf: KeyFrame):
+        """LocalMapping::InsertKeyFrame: run it now (synchronous), or queue it for the mapping
+        thread and interrupt its BA (src/LocalMapping.cc:130-135)."""
+        if not self._concurrent:
+            self._drain(self._local_mapping_gen(kf))
+            return
+        self._queue.append(kf)
+        self._abort = True
+
+    # ---- LocalMapping -------------------------------------------------------------------------
+    # The stages are generators that yield where the native loop releases its map lock (L_*),
+    # with the same state changes between two yields as csrc/slam.cpp, so that a schedule
+    # recorded from the native concurrent run replays here (replay_schedule); synchronously they
+    # are drained and nothing runs in between.
     def _distinctive(self, mps: list):
-        """MapPoint::ComputeDistinctiveDescriptors for a batch of points (src/MapPoint.cc:247-316)
-        on the backend: descriptors of the non-bad observing keyframes, keyframe-id order."""
+        return self._drain(self._distinctive_gen(mps))
+
+    def _obs_rows(self, mps: list):
+        """The observation descriptors of the points (CSR, keyframe-id order, bad keyframes out)."""
         rows, off = [], [0]
         for mp in mps:
             for kf in sorted(mp.observations, key=lambda k: k.id):
                 if not kf.bad:
                     rows.append(kf.desc[mp.observations[kf]])
             off.append(len(rows))
+        return rows, off
+
+    def _distinctive_gen(self, mps: list):
+        """MapPoint::ComputeDistinctiveDescriptors for a batch of points (src/MapPoint.cc:247-316)
+        on the backend: descriptors of the non-bad observing keyframes, keyframe-id order."""
+        rows, off = self._obs_rows(mps)
         if not rows:
             return
         d = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32))
+        yield L_DISTINCTIVE, -1
         for j, mp in enumerate(mps):
             if off[j + 1] > off[j]:
                 mp.desc = np.asarray(d[j], np.uint8).copy()
@@ -733,10 +795,17 @@ class StereoSLAM:
     def _keyframes_in_map(self) -> int:
         return sum(1 for k in self.keyframes if not k.bad)   # Map::KeyFramesInMap
 
+    def _queued(self) -> bool:
+        """LocalMapping::CheckNewKeyFrames (always false when synchronous)."""
+        return self._concurrent and len(self._queue) > 0
+
     def _local_mapping(self, kf: KeyFrame):
-        """LocalMapping::Run for one keyframe (src/LocalMapping.cc:47-128), with no other keyframe
-        queued and no stop request: ProcessNewKeyFrame, MapPointCulling, CreateNewMapPoints,
-        SearchInNeighbors, LocalBundleAdjustment (more than 2 keyframes), KeyFrameCulling."""
+        return self._drain(self._local_mapping_gen(kf))
+
+    def _local_mapping_gen(self, kf: KeyFrame):
+        """LocalMapping::Run for one keyframe (src/LocalMapping.cc:47-128): ProcessNewKeyFrame,
+        MapPointCulling, CreateNewMapPoints, SearchInNeighbors unless a keyframe is queued,
+        LocalBundleAdjustment (more than 2 keyframes) and KeyFrameCulling unless one is queued."""
         # ProcessNewKeyFrame (:152-211)
         if self.backend_has_bow():
             kf.feat_vec = kf.feat_vec or self.backend.compute_bow(kf.desc)
@@ -750,16 +819,19 @@ class StereoSLAM:
             else:   # the new stereo points the Tracking inserted
                 self.recent_mps.append(mp)
         update_normals_and_depths(updated)
-        self._distinctive(updated)
+        yield from self._distinctive_gen(updated)
         kf.update_connections()
         self._map_point_culling(kf)
         if self.local_mapping_full:
-            self._create_new_map_points(kf)
-            self._search_in_neighbors(kf)
-        if self.use_local_ba and self._keyframes_in_map() > 2:
-            self._local_bundle_adjustment(kf)
-        if self.local_mapping_full:
-            self._keyframe_culling(kf)
+            yield from self._create_new_map_points_gen(kf)
+            if not self._queued():
+                yield from self._search_in_neighbors_gen(kf)
+        self._abort = False
+        if not self._queued():
+            if self.use_local_ba and self._keyframes_in_map() > 2:
+                yield from self._local_bundle_adjustment_gen(kf)
+            if self.local_mapping_full:
+                self._keyframe_culling(kf)
 
     def _map_point_culling(self, kf: KeyFrame):
         """LocalMapping::MapPointCulling (src/LocalMapping.cc:219-263), stereo: nThObs = 3."""
@@ -795,54 +867,69 @@ class StereoSLAM:
         return Frame(kf.keys_un, kf.desc, kf.u_right, kf.tcw, self.cam, self.backend.scale_factors,
                      self.cam.width, self.cam.height)
 
-    def _create_new_map_points(self, kf: KeyFrame):
+    def _create_new_map_points_gen(self, kf: KeyFrame):
         """LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:290-577), stereo: the 10 best
         covisible keyframes, baseline >= mb, SearchForTriangulation (0.6, no orientation check)
         on the backend, the triangulation / acceptance geometry on the host
-        (orbmi_triangulate_matches), new points with both observations."""
+        (orbmi_triangulate_matches), new points with both observations.  As the native loop does
+        it in one device call: every pair's search and triangulation first (a keypoint an earlier
+        pair triangulated is not searched again: the reference's `if (pMP1) continue`), then the
+        new points pair by pair with CheckNewKeyFrames between pairs (:331), then one
+        ComputeDistinctiveDescriptors of them all (per point: the same as pair by pair)."""
         import ctypes as C
         from ._capi import check, lib
+        if kf.feat_vec is None:
+            return   # (no vocabulary: no FeatureVector, no searches)
         ow1 = kf.Ow
         v1, keep1 = self._tri_view(kf)
         mb = np.float32(np.float32(self.cam.bf) / np.float32(self.cam.fx))
-        has1 = np.array([mp is not None for mp in kf.map_points], np.uint8)
-        for kf2 in kf.best_covisibility(10):
+        pairs = []
+        for i, kf2 in enumerate(kf.best_covisibility(10)):
             d = (kf2.Ow - ow1).astype(np.float32).astype(np.float64)
             baseline = np.float32(np.sqrt(np.sum(d * d)))
-            if baseline < mb:
+            if baseline < mb or kf2.feat_vec is None:
                 continue
             v2, keep2 = self._tri_view(kf2)
             F12 = np.zeros(9, np.float32)
             check("orbmi_compute_f12", lib().orbmi_compute_f12(C.addressof(v1), C.addressof(v2), F12.ctypes.data))
-            if kf.feat_vec is None or kf2.feat_vec is None:
-                continue
             has2 = np.array([mp is not None for mp in kf2.map_points], np.uint8)
+            pairs.append((i, kf2, v2, keep2, F12, has2))
+        if not pairs:
+            return
+        has1 = np.array([mp is not None for mp in kf.map_points], np.uint8)
+        results = []
+        for i, kf2, v2, keep2, F12, has2 in pairs:
             m12, _ = self.backend.search_for_triangulation(self._kf_frame(kf), has1, kf.feat_vec, self._kf_frame(kf2),
                                                            has2, kf2.feat_vec, F12.reshape(3, 3))
             idx1 = np.nonzero(np.asarray(m12) >= 0)[0].astype(np.int32)
-            if len(idx1) == 0:
-                continue
             idx2 = np.asarray(m12, np.int32)[idx1]
             x3d = np.zeros((len(idx1), 3), np.float32)
             ok = np.zeros(len(idx1), np.uint8)
-            check("orbmi_triangulate_matches", lib().orbmi_triangulate_matches(
-                C.addressof(v1), C.addressof(v2), idx1.ctypes.data, idx2.ctypes.data, len(idx1), x3d.ctypes.data,
-                ok.ctypes.data))
-            new = []
+            if len(idx1):
+                check("orbmi_triangulate_matches", lib().orbmi_triangulate_matches(
+                    C.addressof(v1), C.addressof(v2), idx1.ctypes.data, idx2.ctypes.data, len(idx1), x3d.ctypes.data,
+                    ok.ctypes.data))
+                has1[idx1[ok != 0]] = 1
+            results.append((i, kf2, idx1, idx2, ok, x3d))
+        yield L_CREATE, kf.id
+        fresh = []
+        for i, kf2, idx1, idx2, ok, x3d in results:
+            if i > 0 and self._queued():   # src/LocalMapping.cc:331
+                break
             for k in np.nonzero(ok)[0]:
                 i1, i2 = int(idx1[k]), int(idx2[k])
-                mp = MapPoint(len(self.mappoints), x3d[k].copy(), kf, first_kf_id=kf.id)
+                mp = MapPoint(len(self.mappoints), x3d[k].copy(), kf, first_kf_id=kf.id,
+                              desc=np.zeros(32, np.uint8), normal=np.zeros(3, np.float32))
                 mp.add_observation(kf, i1)
                 mp.add_observation(kf2, i2)
                 kf.map_points[i1] = mp
                 kf2.map_points[i2] = mp
-                has1[i1] = 1
                 self.mappoints.append(mp)
                 self.recent_mps.append(mp)
-                new.append(mp)
-            self._distinctive(new)
-            update_normals_and_depths(new)
-            del keep2
+                fresh.append(mp)
+        yield from self._distinctive_gen(fresh)
+        update_normals_and_depths(fresh)
+        del keep1
 
     def _mp_fuse_records(self, mps: list) -> np.ndarray:
         rec = np.zeros(len(mps), MAPPOINT_DTYPE)
@@ -857,18 +944,16 @@ class StereoSLAM:
                                 np.uint32)
         return rec
 
-    def _fuse(self, kf: KeyFrame, mps: list, dirty: set):
-        """ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for
-        every point on the backend, then the map updates in list order."""
-        if dirty:   # descriptors of points that took over observations (MapPoint::Replace)
-            pts = sorted((m for m in dirty if not m.bad), key=lambda m: m.id)
-            self._distinctive(pts)
-            dirty.clear()
-        pts = [mp for mp in mps if mp is not None]
-        if not pts:
-            return
+    def _fuse_search_gen(self, kf: KeyFrame, pts: list):
+        """The search of ORBmatcher::Fuse(pKF, points, 3.0) on the backend -> best keypoint per point."""
         in_kf = np.array([kf in mp.observations for mp in pts], np.uint8)
         best, _ = self.backend.fuse_search(self._kf_frame(kf), self._mp_fuse_records(pts), in_kf, 3.0)
+        yield L_FUSE, kf.id
+        return np.asarray(best, np.int32).copy()
+
+    @staticmethod
+    def _fuse_replay(kf: KeyFrame, pts: list, best, dirty: set):
+        """The map updates of ORBmatcher::Fuse (src/ORBmatcher.cc:1096-1124) in list order."""
         for mp, b in zip(pts, best):
             if mp.bad or kf in mp.observations or b < 0:
                 continue
@@ -885,7 +970,85 @@ class StereoSLAM:
                 mp.add_observation(kf, b)
                 kf.map_points[b] = mp
 
-    def _search_in_neighbors(self, kf: KeyFrame):
+    def _fuse_gen(self, kf: KeyFrame, mps: list, dirty: set):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for
+        every point on the backend, then the map updates in list order; first the descriptors
+        MapPoint::Replace still owes (src/MapPoint.cc:212)."""
+        if dirty:
+            pts = sorted((m for m in dirty if not m.bad), key=lambda m: m.id)
+            yield from self._distinctive_gen(pts)
+            dirty.clear()
+        pts = [mp for mp in mps if mp is not None]
+        if not pts:
+            return
+        best = yield from self._fuse_search_gen(kf, pts)
+        self._fuse_replay(kf, pts, best, dirty)
+
+    def _fuse_targets_gen(self, targets: list, lst: list, dirty: set):
+        """Fuse(target, the keyframe's points) for every target in order (src/LocalMapping.cc:
+        620-628), as csrc/slam.cpp fuse_targets runs it: every target searched on the records as
+        they are before the first one, then per target: the owed descriptors of listed points
+        (and those points searched again against this and the later targets), the points whose
+        record an earlier replay changed searched again, the replay.  Results are the
+        target-by-target loop's; the state between the steps is the native loop's."""
+        pts = [mp for mp in lst if mp is not None]
+        nt, npts = len(targets), len(pts)
+        if nt == 0 or npts == 0:
+            return
+        rec0 = self._mp_fuse_records(pts)
+        best = []
+        for t in targets:
+            in0 = np.array([t in mp.observations for mp in pts], np.uint8)
+            bi, _ = self.backend.fuse_search(self._kf_frame(t), rec0, in0, 3.0)
+            best.append(np.asarray(bi, np.int32).copy())
+        yield L_FUSE_BATCH, -1
+        listed = {}
+        for j in range(npts - 1, -1, -1):
+            listed[pts[j]] = j
+        for t in range(nt):
+            kt = targets[t]
+            due = []
+            for m in sorted(dirty, key=lambda m: m.id):
+                if m in listed:
+                    if not m.bad:
+                        due.append(m)
+                    dirty.discard(m)
+            if due:
+                rows, off = self._obs_rows(due)
+                rj, frm = [], []
+                for d, m in enumerate(due):
+                    for j in range(npts):
+                        if pts[j] is m:
+                            rj.append(j)
+                            frm.append(d if off[d + 1] > off[d] else -1)
+                newd = None
+                if rows:
+                    newd = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32))
+                rrec = self._mp_fuse_records([pts[j] for j in rj])
+                for q, f in enumerate(frm):
+                    if f >= 0:
+                        rrec["desc"][q] = np.asarray(newd[f], np.uint8)
+                for u in range(t, nt):
+                    rin = np.array([targets[u] in pts[j].observations for j in rj], np.uint8)
+                    bi, _ = self.backend.fuse_search(self._kf_frame(targets[u]), rrec, rin, 3.0)
+                    for q, j in enumerate(rj):
+                        best[u][j] = int(bi[q])
+                yield L_FUSE_REFRESH, t
+                for d, m in enumerate(due):
+                    if off[d + 1] > off[d]:
+                        m.desc = np.asarray(newd[d], np.uint8).copy()
+                for j in rj:
+                    rec0[j] = self._mp_fuse_records([pts[j]])[0]
+            row = best[t]
+            redo = [j for j, m in enumerate(pts) if not (m.bad or kt in m.observations)
+                    and self._mp_fuse_records([m])[0].tobytes() != rec0[j].tobytes()]
+            if redo:
+                b2 = yield from self._fuse_search_gen(kt, [pts[j] for j in redo])
+                for q, j in enumerate(redo):
+                    row[j] = b2[q]
+            self._fuse_replay(kt, pts, row, dirty)
+
+    def _search_in_neighbors_gen(self, kf: KeyFrame):
         """LocalMapping::SearchInNeighbors (src/LocalMapping.cc:589-674), stereo: nn = 10."""
         targets = []
         for k in kf.best_covisibility(10):
@@ -898,9 +1061,7 @@ class StereoSLAM:
                     continue
                 targets.append(k2)
         dirty = set()
-        matches = list(kf.map_points)
-        for k in targets:
-            self._fuse(k, matches, dirty)
+        yield from self._fuse_targets_gen(targets, list(kf.map_points), dirty)
         cands = []
         for k in targets:
             for mp in k.map_points:
@@ -908,7 +1069,7 @@ class StereoSLAM:
                     continue
                 mp.fuse_candidate_for_kf = kf.id
                 cands.append(mp)
-        self._fuse(kf, cands, dirty)
+        yield from self._fuse_gen(kf, cands, dirty)
         dirty.clear()
         pts = [mp for mp in kf.map_points if mp is not None and not mp.bad]
         seen, upd = set(), []
@@ -916,7 +1077,7 @@ class StereoSLAM:
             if id(mp) not in seen:
                 seen.add(id(mp))
                 upd.append(mp)
-        self._distinctive(upd)
+        yield from self._distinctive_gen(upd)
         update_normals_and_depths(upd)
         kf.update_connections()
 
@@ -953,17 +1114,25 @@ class StereoSLAM:
     def backend_has_bow(self) -> bool:
         return getattr(self.backend, "vocab", None) is not None
 
-    def _local_bundle_adjustment(self, kf: KeyFrame):
+    def _local_bundle_adjustment_gen(self, kf: KeyFrame):
         """Optimizer::LocalBundleAdjustment (src/Optimizer.cc:483-808): graph assembly on the host
-        (optimizer.gather_local_ba), optimisation on the backend, write-back under the map lock."""
+        (optimizer.gather_local_ba), optimisation on the backend, write-back under the map lock.
+        In a replayed schedule pbStopFlag (mbAbortBA) is the recorded run's: the backend stops at
+        the check where that run first saw it raised (orbmi_ba_set_stop_at_check)."""
         from .optimizer import gather_local_ba
         problem, kfs, mps = gather_local_ba(kf)
         if len(problem.edges) == 0:
             return
-        res = self.backend.local_ba(problem)
+        stop_at = -1 if self._ba_stop_at is None else self._ba_stop_at(kf)
+        res = self.backend.local_ba(problem, stop_at_check=stop_at)
+        yield L_BA, kf.id
         erase = np.asarray(res["erase"], bool)
         self.ba_log.append({"keyframe": kf.id, "keyframes": len(kfs), "points": len(mps),
-                            "edges": len(problem.edges), "erased": int(erase.sum())})
+                            "edges": len(problem.edges), "erased": int(erase.sum()),
+                            "iterations": tuple(res["iterations"]), "stop_check": res.get("stop_check", -1),
+                            "aborted": res["aborted"]})
+        if res["aborted"]:
+            return   # src/Optimizer.cc:685-687: stopped before optimising, nothing written back
         for e in np.nonzero(erase)[0]:
             ed = problem.edges[e]
             mp, k = mps[int(ed["point"])], kfs[int(ed["kf"])]
@@ -976,6 +1145,77 @@ class StereoSLAM:
         for j, mp in enumerate(mps):
             mp.pos = np.asarray(res["pos"][j], np.float32).copy()
         update_normals_and_depths(mps)
+
+    # ---- replay of a concurrent schedule ------------------------------------------------------
+    def _tracking_thread(self, frames):
+        """Tracking's side of a concurrent run: per frame the Frame constructor (no shared state),
+        then Track() under the map lock (T_FRAME) with its releases."""
+        for L, R, ts in frames:
+            keys, desc, u_right, depth = self.backend.extract_stereo(L, R)
+            n = len(keys)
+            cf = TrackedFrame(self.frame_count, float(ts), keys, desc.reshape(-1, 32), u_right, depth,
+                              map_points=[None] * n, outlier=np.zeros(n, bool))
+            yield T_FRAME, cf.id
+            self.frame_count += 1
+            yield from self._track_gen(cf)
+
+    def _mapping_thread(self):
+        """LocalMapping's thread: each time it takes the map lock it takes the next queued
+        keyframe (if any: a reset may have dropped it) and runs LocalMapping::Run for it."""
+        while True:
+            ev = yield L_JOB, None
+            kf = None
+            if self._queue:
+                kf = self._queue.pop(0)
+                self._busy = True   # SetAcceptKeyFrames(false)
+            got = -1 if kf is None else kf.id
+            if ev is not None and int(ev[2]) != got:
+                raise ScheduleMismatch(f"the mapping thread took keyframe {got}, the record {int(ev[2])}")
+            if kf is not None:
+                yield from self._local_mapping_gen(kf)
+            self._busy = False      # SetAcceptKeyFrames(true)
+
+    def replay_schedule(self, frames, schedule, ba_log):
+        """Replay a run of the native loop with the concurrent LocalMapping
+        (orbmi_slam_settings.async_local_mapping) on this host logic: `frames` = [(L, R, ts)] as
+        handed to TrackStereo, `schedule` = NativeStereoSLAM.schedule() (thread, label, arg per
+        acquisition of the map lock, in order), `ba_log` = NativeStereoSLAM.local_ba_log().  The
+        two threads' stretches between lock releases run in the recorded order and every
+        LocalBA stops at its recorded pbStopFlag check, so the run's decisions and trajectory
+        follow from the schedule.  Raises ScheduleMismatch where the record and this logic
+        disagree."""
+        self._concurrent = True
+        stops = iter([tuple(int(x) for x in r[:2]) for r in np.asarray(ba_log).reshape(-1, 8)])
+
+        def stop_at(kf):
+            rec = next(stops, None)
+            if rec is None or rec[0] != kf.id:
+                raise ScheduleMismatch(f"LocalBA of keyframe {kf.id}, the record has {rec}")
+            return rec[1]
+        self._ba_stop_at = stop_at
+        gens = {0: self._tracking_thread(frames), 1: self._mapping_thread()}
+        want = {t: next(g) for t, g in gens.items()}
+        for k, (thread, label, arg) in enumerate(np.asarray(schedule).reshape(-1, 3).tolist()):
+            w = want.get(thread)
+            if w is None or w[0] != label or (w[1] is not None and w[1] != arg):
+                raise ScheduleMismatch(f"event {k}: thread {thread} resumes at ({label}, {arg}), "
+                                       f"this logic at {w}")
+            try:
+                want[thread] = gens[thread].send((thread, label, arg))
+            except StopIteration:
+                want[thread] = None
+        if want[0] is not None:
+            raise ScheduleMismatch(f"the record ends with Tracking at {want[0]}")
+        if next(stops, None) is not None:
+            raise ScheduleMismatch("the record has more LocalBA calls")
+        self._concurrent = False
+        self._ba_stop_at = None
+
+    def ba_records(self) -> np.ndarray:
+        """ba_log in the layout of NativeStereoSLAM.local_ba_log (keyframe, stop_check, aborted,
+        checks, iterations0, iterations1, edges, erased; checks not kept: -1)."""
+        return np.array([[b["keyframe"], b["stop_check"], b["aborted"], -1, b["iterations"][0], b["iterations"][1],
+                          b["edges"], b["erased"]] for b in self.ba_log], np.int32).reshape(-1, 8)
 
     # ---- tracking stages --------------------------------------------------------------------
     def _mp_records(self, mps: list, seen: set) -> np.ndarray:
@@ -1034,24 +1274,27 @@ class StereoSLAM:
         lf = self.last_frame
         lf.tcw = _mul(self.rel_poses[-1], lf.ref_kf.tcw)
 
-    def _track_reference_kf(self, cf: TrackedFrame, st) -> bool:
-        """Tracking::TrackReferenceKeyFrame (src/Tracking.cc:871-917)."""
+    def _track_reference_kf(self, cf: TrackedFrame, st):
+        """Tracking::TrackReferenceKeyFrame (src/Tracking.cc:871-917); generator -> ok."""
         cf.feat_vec = self.backend.compute_bow(cf.desc)
         kf = self.ref_kf
         if kf.feat_vec is None:
             kf.feat_vec = self.backend.compute_bow(kf.desc)
         ok_mp = np.array([mp is not None and not mp.bad for mp in kf.map_points], np.uint8)
+        kf_mps = list(kf.map_points)   # the keyframe's matches when the search ran
         kfv = Frame(kf.keys_un, kf.desc, kf.u_right, kf.tcw, self.cam, self.backend.scale_factors,
                     self.cam.width, self.cam.height)
         m, n = self.backend.search_by_bow(kfv, ok_mp, kf.feat_vec, self._frame(cf, np.eye(4)), cf.feat_vec)
+        yield T_BOW, cf.id
         st["bow_matches"] = n
         st["track"] = "reference_kf"
         if n < 15:
             return False
-        cf.map_points = [kf.map_points[j] if j >= 0 else None for j in m]
+        cf.map_points = [kf_mps[j] if j >= 0 else None for j in m]
         cf.tcw = self.last_frame.tcw.copy()
-        lfp = self._lf_records(kf.map_points, None)
+        lfp = self._lf_records(kf_mps, None)
         tcw, out = self.backend.pose_optimization(self._frame(cf), np.asarray(m, np.int32), lfp)
+        yield T_POSE, cf.id
         cf.tcw = tcw
         cf.outlier = out.astype(bool)
         self._seen = set()
@@ -1059,8 +1302,10 @@ class StereoSLAM:
         st["nmatches_map"] = nmap
         return nmap >= 10
 
-    def _track_motion_model(self, cf: TrackedFrame, st) -> bool:
-        """Tracking::TrackWithMotionModel (src/Tracking.cc:997-1063)."""
+    def _track_motion_model(self, cf: TrackedFrame, st):
+        """Tracking::TrackWithMotionModel (src/Tracking.cc:997-1063); generator -> ok.  The
+        searches (the retry at 2 th when fewer than 20 matched) and PoseOptimization run on the
+        inputs as they are when the stage starts (the native loop's one device-resident window)."""
         self._update_last_frame()
         lf = self.last_frame
         cf.tcw = _mul(self.velocity, lf.tcw)
@@ -1071,12 +1316,14 @@ class StereoSLAM:
         m, n = self.backend.search_last_frame(self._frame(cf), occ, lfv, lfp, th)
         if n < 20:
             m, n = self.backend.search_last_frame(self._frame(cf), occ, lfv, lfp, 2 * th)
+        if n >= 20:
+            tcw, out = self.backend.pose_optimization(self._frame(cf), np.asarray(m, np.int32), lfp)
+        yield T_LF, cf.id
         st["track"] = "motion_model"
         st["lf_matches"] = n
         if n < 20:
             return False
         cf.map_points = [lf.map_points[j] if j >= 0 else None for j in m]
-        tcw, out = self.backend.pose_optimization(self._frame(cf), np.asarray(m, np.int32), lfp)
         cf.tcw = tcw
         cf.outlier = out.astype(bool)
         self._seen = set()
@@ -1144,9 +1391,10 @@ class StereoSLAM:
                 mark.add(id(mp))
         self.local_mps = out
 
-    def _track_local_map(self, cf: TrackedFrame, st) -> bool:
+    def _track_local_map(self, cf: TrackedFrame, st):
         """Tracking::TrackLocalMap (src/Tracking.cc:1075-1104) with UpdateLocalMap and
-        SearchLocalPoints (:1345-1420)."""
+        SearchLocalPoints (:1345-1420); generator -> ok.  SearchLocalPoints and PoseOptimization run
+        on the records as they are when the stage starts (the native loop's one window)."""
         self._update_local_keyframes(cf)
         self._update_local_points()
         seen = getattr(self, "_seen", set())
@@ -1163,10 +1411,6 @@ class StereoSLAM:
         mps = self.local_mps
         rec = self._mp_records(mps, seen)
         m_mp, nl, in_view = self.backend.search_local_points(self._frame(cf), occ, rec, 1.0)
-        for j in np.nonzero(np.asarray(in_view))[0]:   # isInFrustum -> IncreaseVisible
-            mps[int(j)].visible += 1
-        st["local_map_points"] = len(mps)
-        st["local_matches"] = nl
         m_lf = np.full(cf.n, -1, np.int32)
         cur = list(cf.map_points)
         for i, j in enumerate(m_mp):
@@ -1178,6 +1422,11 @@ class StereoSLAM:
             if mp is not None:
                 m_lf[i] = i
         tcw, out = self.backend.pose_optimization(self._frame(cf), m_lf, lfp)
+        yield T_LOCAL, cf.id
+        for j in np.nonzero(np.asarray(in_view))[0]:   # isInFrustum -> IncreaseVisible
+            mps[int(j)].visible += 1
+        st["local_map_points"] = len(mps)
+        st["local_matches"] = nl
         cf.tcw = tcw
         cf.map_points = cur
         cf.outlier = out.astype(bool)

@@ -76,9 +76,9 @@ class OracleBackend:
         self._count("distinctive")
         return self.O.compute_distinctive_descriptors(obs_desc, obs_off)[1]
 
-    def local_ba(self, problem, stop=None):
+    def local_ba(self, problem, stop=None, stop_at_check=-1):
         self._count("local_ba")
-        return self.O.local_ba(problem)
+        return self.O.local_ba(problem, stop_at_check=stop_at_check)
 
     def close(self):
         pass

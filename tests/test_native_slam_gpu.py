@@ -135,6 +135,56 @@ def test_native_concurrent_local_mapping(tmp_path):
         slam.Shutdown()
 
 
+def _concurrent_record(tmp_path, n, period):
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
+    _drive_paced(slam, frames, period)
+    slam.WaitLocalMapping()
+    rec = {"schedule": slam.schedule(), "ba_log": slam.local_ba_log(), "stats": slam.stats,
+           "traj": slam.trajectory_twc(), "counts": slam.counts()}
+    slam.Shutdown()
+    return frames, s, voc, rec
+
+
+@pytest.mark.parametrize("period", [0.0, 0.003])
+def test_concurrent_schedule_replays_on_oracle(tmp_path, period):
+    """The native loop with the concurrent LocalMapping (the reference's threading), frames handed
+    over back to back (the throughput regime: the mapping thread falls behind, keyframes are
+    refused while it is busy, LocalBAs are interrupted by InterruptBA / new keyframes) or paced.
+    The run is timing-dependent, but its schedule is recorded: the order in which the two threads
+    took the map lock, and where each LocalBA first saw mbAbortBA raised
+    (orbmi_ba_set_stop_at_check's numbering).  Replayed through the same host logic on the CPU
+    oracle (system.StereoSLAM.replay_schedule), it makes the same decisions on every frame, the
+    LocalBAs stop at the same checks with the same iteration counts, and the trajectory is the
+    same -- so the concurrent run's accuracy is what the reference's logic gives for that
+    interleaving, not a defect of the native loop."""
+    frames, s, voc, rec = _concurrent_record(tmp_path, 200, period)
+    sched, balog = rec["schedule"], rec["ba_log"]
+    assert len(sched) > 400 and (sched[:, 0] == 1).any()
+    ref = StereoSLAM(s, backend=OracleBackend(s, voc))
+    ref.replay_schedule([(L, R, 0.1 * f) for f, (L, R, _) in enumerate(frames)], sched, balog)
+    a_all, b_all = rec["stats"], ref.stats
+    assert len(a_all) == len(b_all) == 200
+    for a, b in zip(a_all, b_all):
+        assert {k: a.get(k) for k in _DECISIONS} == {k: b.get(k) for k in _DECISIONS}, (a, b)
+    assert len(ref.ba_log) == len(balog)
+    for r, b in zip(ref.ba_log, balog):
+        assert (r["keyframe"], r["stop_check"], r["aborted"], r["iterations"]) == \
+            (b[0], b[1], b[2], (b[4], b[5])), (r, b.tolist())
+    tg, tr = rec["traj"], ref.trajectory_twc()
+    np.testing.assert_allclose(tg[:, :3, 3], tr[:, :3, 3], atol=1e-3)
+    np.testing.assert_allclose(tg[:, :3, :3], tr[:, :3, :3], atol=1e-4)
+    gt = np.array([fr[2] for fr in frames])
+    ate_g, ate_r = ate_rmse(tg, gt), ate_rmse(tr, gt)
+    assert abs(ate_g - ate_r) < 1e-3, (ate_g, ate_r)
+    interrupted = int((balog[:, 1] > 0).sum())
+    print(f"period {period * 1e3:g} ms: {len(sched)} lock acquisitions, {len(balog)} LocalBAs "
+          f"({interrupted} interrupted, {int(balog[:, 2].sum())} aborted before starting), "
+          f"{rec['counts']['keyframes']} keyframes, ATE {ate_g:.4f} m (oracle replay {ate_r:.4f} m)")
+
+
 def test_native_reset_after_loss_matches_oracle(tmp_path):
     """A frame lost with <= 5 keyframes resets the system (src/Tracking.cc:540-551) in the native
     loop exactly as in the oracle-driven loop; the flat frame (no keypoints) goes through every

@@ -179,3 +179,65 @@ def test_tracking_loss_resets(tmp_path):
     assert st[2]["init"] and st[2]["frame"] == 0 and st[2]["keyframes"] == 1
     assert st[3]["state"] == OK and st[3]["track"] == "reference_kf"
     assert len(slam.rel_poses) == 2 and all(k.id < 2 for k in slam.keyframes)
+
+
+def _interleaved_run(s, voc, frames, seed, stop_prob=0.5):
+    """Tracking and LocalMapping interleaved at the native loop's lock releases in a random order
+    (each thread's stretches between releases run whole, the mapping thread only when it has a
+    keyframe or is mid-job) with random LocalBA stop checks: a concurrent run of the host logic
+    on the oracle, with its schedule recorded as the native loop records it."""
+    from orb_slam2_with_comment_amd.system import L_JOB
+    slam = StereoSLAM(s, backend=OracleBackend(s, voc))
+    rng = np.random.default_rng(seed)
+    slam._concurrent = True
+    slam._ba_stop_at = lambda kf: -1 if rng.random() >= stop_prob else int(rng.integers(0, 25))
+    gens = {0: slam._tracking_thread(frames), 1: slam._mapping_thread()}
+    want = {t: next(g) for t, g in gens.items()}
+    sched = []
+    while True:
+        elig = [0] if want[0] is not None else []
+        if want[1][0] != L_JOB or slam._queue:
+            elig.append(1)
+        if not elig:
+            break
+        t = elig[int(rng.integers(len(elig)))]
+        label, arg = want[t]
+        if t == 1 and label == L_JOB:
+            arg = slam._queue[0].id if slam._queue else -1
+        ev = (t, label, arg)
+        sched.append(ev)
+        try:
+            want[t] = gens[t].send(ev)
+        except StopIteration:
+            want[t] = None
+    slam._concurrent = False
+    return slam, np.array(sched, np.int32), slam.ba_records()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_replay_schedule_reproduces_interleaved_run(tmp_path, seed):
+    """StereoSLAM.replay_schedule (the replay of a native concurrent run) on a schedule recorded
+    from a randomly interleaved run of the same host logic: a fresh system replaying it takes the
+    same decisions on every frame, the LocalBAs stop where they stopped, and the trajectory is
+    bit-identical; the interleaving refuses or delays keyframes (AcceptKeyFrames) and interrupts
+    LocalBAs like the native loop's threads."""
+    from slam_backends import render_sequence, sequence_settings, small_vocabulary
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    fr = render_sequence(24)
+    frames = [(L, R, 0.1 * f) for f, (L, R, _) in enumerate(fr)]
+    run, sched, balog = _interleaved_run(s, voc, frames, seed)
+    assert len(run.stats) == 24 and len(balog) >= 2
+    rep = StereoSLAM(s, backend=OracleBackend(s, voc))
+    rep.replay_schedule(frames, sched, balog)
+    assert rep.stats == run.stats
+    np.testing.assert_array_equal(rep.ba_records(), balog)
+    np.testing.assert_array_equal(rep.trajectory_twc(), run.trajectory_twc())
+    # a record that does not fit is refused
+    from orb_slam2_with_comment_amd.system import ScheduleMismatch
+    bad = sched.copy()
+    k = int(np.nonzero(bad[:, 0] == 1)[0][3])
+    bad[[k, k - 1]] = bad[[k - 1, k]] if bad[k - 1, 0] == 0 else bad[[k, k - 1]]
+    bad[k, 1] = 99
+    with pytest.raises(ScheduleMismatch):
+        StereoSLAM(s, backend=OracleBackend(s, voc)).replay_schedule(frames, bad, balog)
