@@ -1,6 +1,7 @@
-"""The C++ host layer (include/orbmi.hpp): builds tests/cpp/dropin_extract.cpp against
-liborbmi.so (CPU: compile + link only), and on the GPU runs a Frame-shaped stereo extraction
-and compares it with the oracle bit for bit."""
+"""The C++ host layer (include/orbmi.hpp): builds tests/cpp/dropin_extract.cpp and
+tests/cpp/dropin_match_ba.cpp against liborbmi.so (CPU: compile + link only); on the GPU runs a
+Frame-shaped stereo extraction, and the matcher / LocalBA classes with the call shapes of
+Tracking and LocalMapping, and compares them with the oracle."""
 import os
 import subprocess
 
@@ -11,10 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "orb_slam2_with_comment_amd")
 
 
-def build_dropin(out_dir):
-    exe = os.path.join(out_dir, "dropin_extract")
-    cmd = ["g++", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "tests", "cpp", "dropin_extract.cpp"), "-L", LIBDIR, "-lorbmi",
+def build_dropin(out_dir, name="dropin_extract"):
+    exe = os.path.join(out_dir, name)
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", name + ".cpp"), "-L", LIBDIR, "-lorbmi",
            f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", exe]
     subprocess.run(cmd, check=True, capture_output=True)
     return exe
@@ -23,8 +24,8 @@ def build_dropin(out_dir):
 def test_cpp_layer_compiles_and_links(tmp_path):
     from orb_slam2_with_comment_amd import build
     build.build()
-    exe = build_dropin(str(tmp_path))
-    assert os.path.exists(exe)
+    for name in ("dropin_extract", "dropin_match_ba"):
+        assert os.path.exists(build_dropin(str(tmp_path), name))
 
 
 @pytest.mark.gpu
@@ -55,3 +56,90 @@ def test_cpp_dropin_matches_oracle(tmp_path, oracle):
     np.testing.assert_array_equal(desc, dl)
     np.testing.assert_array_equal(u, ru)
     np.testing.assert_array_equal(d, rd)
+
+
+def _write_frame(d, tag, F):
+    F.keys.tofile(d / f"in_{tag}_keys.bin")
+    F.desc.tofile(d / f"in_{tag}_desc.bin")
+    np.ascontiguousarray(F.u_right, np.float32).tofile(d / f"in_{tag}_ur.bin")
+    F.tcw.tofile(d / f"in_{tag}_tcw.bin")
+
+
+def _write_fv(d, tag, fv):
+    fv.node_id.tofile(d / f"in_{tag}_node.bin")
+    fv.off.tofile(d / f"in_{tag}_off.bin")
+    fv.feat.tofile(d / f"in_{tag}_feat.bin")
+
+
+@pytest.mark.gpu
+def test_cpp_dropin_matcher_and_local_ba(tmp_path, oracle):
+    """orbmi::ORBmatcher (include/ORBmatcher.h:44-66 drop-ins: IsInFrustum, both
+    SearchByProjection overloads, SearchLocalPoints, SearchByBoW) and orbmi::LocalBundleAdjuster
+    (include/Optimizer.h:62: without pbStopFlag, with it raised, with the deterministic stop at a
+    check inside optimize(5)) run from C++ against the oracle: match arrays index-exact, LocalBA
+    within the parity bars of tests/test_lba_gpu.py."""
+    from scenario import bow, lastframe, local_map, make_frame
+    from orb_slam2_with_comment_amd import synth_map as SM
+    exe = build_dropin(str(tmp_path), "dropin_match_ba")
+    d = tmp_path / "io"
+    d.mkdir()
+    F = make_frame(3)
+    v = F.view()
+    np.array([v.fx, v.fy, v.cx, v.cy, v.bf, v.mb, v.max_x, v.max_y, v.grid_w_inv, v.grid_h_inv, v.log_scale_factor],
+             np.float32).tofile(d / "in_cam.bin")
+    F.scale_factors.tofile(d / "in_scale_factors.bin")
+    # SearchLocalPoints
+    mps = local_map((0, 1, 2))
+    occ = (np.random.default_rng(5).random(len(F.keys)) < 0.1).astype(np.uint8)
+    _write_frame(d, "local", F)
+    mps.tofile(d / "in_local_mps.bin")
+    occ.tofile(d / "in_local_occ.bin")
+    # TrackWithMotionModel
+    cf = make_frame(3, pose_noise=0.01, seed=1)
+    lf, lfp = lastframe(2, seed=4)
+    occ_lf = (np.random.default_rng(11).random(len(cf.keys)) < 0.05).astype(np.uint8)
+    _write_frame(d, "cf", cf)
+    _write_frame(d, "lf", lf)
+    lfp.tofile(d / "in_lf_points.bin")
+    occ_lf.tofile(d / "in_lf_occ.bin")
+    # TrackReferenceKeyFrame
+    kf, ok, kfv, f, fv = bow(2, 3)
+    _write_frame(d, "bkf", kf)
+    _write_frame(d, "bf", f)
+    ok.tofile(d / "in_bkf_ok.bin")
+    _write_fv(d, "bkf_fv", kfv)
+    _write_fv(d, "bf_fv", fv)
+    # LocalBundleAdjustment, stopped at check 3 (inside optimize(5))
+    prob, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
+    prob.kfs.tofile(d / "in_ba_kfs.bin")
+    prob.pts.tofile(d / "in_ba_pts.bin")
+    prob.edges.tofile(d / "in_ba_edges.bin")
+    np.array([3], np.int32).tofile(d / "in_ba_stop_at.bin")
+    subprocess.run([exe, str(d)], check=True, timeout=120)
+
+    def out(name, dtype):
+        return np.fromfile(d / f"out_{name}.bin", dtype)
+    tr_ref = oracle.is_in_frustum(F, mps, 0.5)
+    np.testing.assert_array_equal(out("local_track", np.uint8), tr_ref.view(np.uint8).ravel())
+    m_ref, n_ref = oracle.search_by_projection_local(F, occ, mps, tr_ref, 1.0, 0.8)
+    n, n2, to_match = out("local_counts", np.int32)
+    assert n == n2 == n_ref and n_ref > 100 and to_match == int(tr_ref["in_view"].sum())
+    np.testing.assert_array_equal(out("local_match", np.int32), m_ref)
+    np.testing.assert_array_equal(out("local_fused_match", np.int32), m_ref)
+    m_ref, n_ref = oracle.search_by_projection_last_frame(cf, occ_lf, lf, lfp, 7.0, False, True)
+    assert out("lf_counts", np.int32)[0] == n_ref and n_ref > 50
+    np.testing.assert_array_equal(out("lf_match", np.int32), m_ref)
+    m_ref, n_ref = oracle.search_by_bow(kf, ok, kfv, f, fv, 0.7, True)
+    assert out("bow_counts", np.int32)[0] == n_ref and n_ref > 20
+    np.testing.assert_array_equal(out("bow_match", np.int32), m_ref)
+    for tag, kw in (("free", {}), ("raised", {"stop": True}), ("hook", {"stop_at_check": 3})):
+        ref = oracle.local_ba(prob, **kw)
+        it0, it1, aborted, stop_check = out(f"ba_{tag}_info", np.int32)
+        assert (it0, it1) == ref["iterations"] and aborted == ref["aborted"] and stop_check == ref["stop_check"], tag
+        if aborted:
+            continue
+        tcw = out(f"ba_{tag}_tcw", np.float32).reshape(-1, 4, 4)
+        assert np.abs(tcw - ref["tcw"]).max() <= 1e-4, tag
+        pos = out(f"ba_{tag}_pos", np.float32).reshape(-1, 3)
+        assert (np.abs(pos - ref["pos"]) / np.maximum(1.0, np.abs(ref["pos"]))).max() <= 1e-3, tag
+        np.testing.assert_array_equal(out(f"ba_{tag}_erase", np.uint8).astype(bool), ref["erase"])
