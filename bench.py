@@ -844,11 +844,16 @@ def run_system(a, rank, world, local, dist):
     s = load_settings(path)
     voc = Vocabulary.synthetic(k=10, L=5, seed=3)
 
-    def drive(slam):
+    def drive(slam, ahead=False):
+        """stereo_kitti's loop; ahead: the next pair handed over with each frame (its Frame
+        constructor runs on the GPU while the frame is tracked, orbmi_slam_track_stereo_ahead)."""
         times = []
         for f, (L, R, _) in enumerate(frames):
             t0 = time.perf_counter()
-            slam.TrackStereo(L, R, 0.1 * f)
+            if ahead:
+                slam.TrackStereo(L, R, 0.1 * f, next_pair=frames[f + 1][:2] if f + 1 < len(frames) else None)
+            else:
+                slam.TrackStereo(L, R, 0.1 * f)
             times.append(time.perf_counter() - t0)
         return np.array(times)
 
@@ -856,7 +861,7 @@ def run_system(a, rank, world, local, dist):
         slam = NativeStereoSLAM(s, device=local, vocabulary=voc, async_local_mapping=async_lm)
         if dist:
             dist.barrier()
-        times = drive(slam)
+        times = drive(slam, ahead=True)
         t0 = time.perf_counter()
         slam.WaitLocalMapping()  # the mapping thread's queue drains inside the measurement
         wait_s = time.perf_counter() - t0

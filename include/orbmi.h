@@ -641,6 +641,16 @@ void orbmi_slam_destroy(orbmi_slam* h);
 int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
                             double timestamp, float* tcw_out, int* has_pose);
 
+/* orbmi_slam_track_stereo for drivers that have the next pair at hand (a stereo_kitti loop over
+ * image files): as the plain call, and then the next pair's Frame constructor (upload, ORB
+ * extraction of both images, ComputeStereoMatches) is enqueued to run on the GPU while this frame
+ * is tracked.  The next call must pass that pair as left/right -- the same buffers, unmodified,
+ * same geometry -- to use it (any other pair is extracted as usual); next_left / next_right NULL:
+ * nothing ahead.  The extraction depends on the images only, so every result is the plain call's. */
+int orbmi_slam_track_stereo_ahead(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols,
+                                  size_t step, double timestamp, const uint8_t* next_left,
+                                  const uint8_t* next_right, float* tcw_out, int* has_pose);
+
 /* The counters of the `frame`-th TrackStereo call (0-based; the record stays across a reset,
  * while frame ids restart); ORBMI_E_ARG past the last call. */
 int orbmi_slam_get_stats(orbmi_slam* h, int frame, orbmi_slam_frame_stats* out);

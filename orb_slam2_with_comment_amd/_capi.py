@@ -118,6 +118,7 @@ _PROTOS = {
     "orbmi_slam_wait_local_mapping": (_i, [_vp]),
     "orbmi_slam_get_phase_ms": (_i, [_vp, _vp, _i, C.POINTER(C.c_long)]),
     "orbmi_slam_track_stereo": (_i, [_vp, _vp, _vp, _i, _i, _sz, C.c_double, _vp, C.POINTER(_i)]),
+    "orbmi_slam_track_stereo_ahead": (_i, [_vp, _vp, _vp, _i, _i, _sz, C.c_double, _vp, _vp, _vp, C.POINTER(_i)]),
     "orbmi_slam_get_stats": (_i, [_vp, _i, _vp]),
     "orbmi_slam_get_schedule": (_i, [_vp, _vp, _i, C.POINTER(_i)]),
     "orbmi_slam_get_local_ba_log": (_i, [_vp, _vp, _i, C.POINTER(_i)]),

@@ -263,19 +263,23 @@ struct orbmi_slam {
     std::vector<uint8_t> dbuf;
     // Device-resident frames: the image pair goes up once, both images are extracted as one
     // batch with the stereo match behind them on the extractor's stream, and the outputs stay
-    // in one of two slots (current frame, last frame), so the searches and the pose
-    // optimisations read the frames in place instead of staging them per call; the host gets its
-    // copy of the left outputs with one read-back.
+    // in one of three slots (current frame, last frame, the next frame's extraction running
+    // ahead), so the searches and the pose optimisations read the frames in place instead of
+    // staging them per call; the host gets its copy of the left outputs with one read-back.
+    static constexpr int kSlots = 3;
     struct Dev {
         uint8_t* img = nullptr;  // 2 x rows x cols
         size_t img_bytes = 0;
         uint8_t* h_img = nullptr;  // pinned staging of the pair
         int cap = 0;               // keypoints per item
-        orbmi_keypoint* kps[2] = {};
-        uint8_t* desc[2] = {};
-        int* cnt[2] = {};
-        float* ur[2] = {};
-        float* dep[2] = {};
+        orbmi_keypoint* kps[kSlots] = {};
+        uint8_t* desc[kSlots] = {};
+        int* cnt[kSlots] = {};
+        float* ur[kSlots] = {};
+        float* dep[kSlots] = {};
+        int seq = 0;               // extractions enqueued (slot = seq % kSlots)
+        // the extraction enqueued ahead (orbmi_slam_track_stereo_ahead) and not yet collected
+        struct Ahead { bool on = false; int slot = -1, rows = 0, cols = 0; size_t step = 0; const uint8_t *L = nullptr, *R = nullptr; } ahead;
         // pinned host mirror of a slot's left outputs
         orbmi_keypoint* h_kps = nullptr;
         uint8_t* h_desc = nullptr;
@@ -443,9 +447,9 @@ struct orbmi_slam {
     }
 
     // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images (one batch on the
-    // left handle) and ComputeStereoMatches, into device slot cf.id & 1; host copies of the left
-    // keypoints, descriptors, u_right and depth
-    int frame_stereo(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step) {
+    // left handle) and ComputeStereoMatches into the next device slot, enqueued on the extractor's
+    // stream with the read-back of the left outputs into pinned memory (frame_collect waits)
+    int frame_enqueue(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int* slot_out) {
         const size_t img = (size_t)rows * cols;
         if (2 * img > dev.img_bytes) {
             if (dev.img) (void)hipFree(dev.img);
@@ -459,7 +463,7 @@ struct orbmi_slam {
         if (!dev.kps[0]) {
             const int cap = s.n_features + 16 * s.n_levels + 64;
             dev.cap = cap;
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < kSlots; k++) {
                 if (hipMalloc((void**)&dev.kps[k], 2 * (size_t)cap * sizeof(orbmi_keypoint)) != hipSuccess ||
                     hipMalloc((void**)&dev.desc[k], 2 * (size_t)cap * 32) != hipSuccess ||
                     hipMalloc((void**)&dev.cnt[k], 2 * sizeof(int)) != hipSuccess ||
@@ -479,7 +483,7 @@ struct orbmi_slam {
             std::memcpy(dev.h_img + img + (size_t)r * cols, R + (size_t)r * step, cols);
         }
         if (hipMemcpyAsync(dev.img, dev.h_img, 2 * img, hipMemcpyHostToDevice, xstream) != hipSuccess) return ORBMI_E_HIP;
-        const int k = cf.id & 1, cap = dev.cap;
+        const int k = dev.seq++ % kSlots, cap = dev.cap;
         SLAM_CHECK(orbmi_extract_batch_device(left, dev.img, 2, rows, cols, cols, img, dev.kps[k], dev.desc[k], dev.cnt[k],
                                               cap));
         SLAM_CHECK(orbmi_compute_stereo_matches_batch_device(left, s.bf, s.fx, dev.ur[k], dev.dep[k]));
@@ -488,21 +492,61 @@ struct orbmi_slam {
                 hipSuccess ||
             hipMemcpyAsync(dev.h_desc, dev.desc[k], (size_t)cap * 32, hipMemcpyDeviceToHost, xstream) != hipSuccess ||
             hipMemcpyAsync(dev.h_ur, dev.ur[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
-            hipMemcpyAsync(dev.h_dep, dev.dep[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
-            hipStreamSynchronize(xstream) != hipSuccess)
+            hipMemcpyAsync(dev.h_dep, dev.dep[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess)
             return ORBMI_E_HIP;
-        const int n = std::min(dev.h_cnt[0], cap);
+        *slot_out = k;
+        return ORBMI_OK;
+    }
+
+    // the enqueued extraction's host copies into cf (waits for the extractor's stream)
+    int frame_collect(TrackedFrame& cf, int slot) {
+        if (hipStreamSynchronize(xstream) != hipSuccess) return ORBMI_E_HIP;
+        const int n = std::min(dev.h_cnt[0], dev.cap);
         cf.keys.assign(dev.h_kps, dev.h_kps + n);
         cf.desc.assign(dev.h_desc, dev.h_desc + (size_t)n * 32);
         cf.ur.assign(dev.h_ur, dev.h_ur + n);
         cf.depth.assign(dev.h_dep, dev.h_dep + n);
-        cf.dslot = k;
-        // new keypoints behind the slot's pointers: a grid pinned on the frame two back is stale
+        cf.dslot = slot;
+        // new keypoints behind a slot's pointers: a grid pinned on an older frame there is stale
         return orbmi_matcher_release_grid(matcher);
     }
 
+    int frame_stereo(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step) {
+        int slot = -1;
+        SLAM_CHECK(frame_enqueue(L, R, rows, cols, step, &slot));
+        return frame_collect(cf, slot);
+    }
+
+    // orbmi_slam_track_stereo_ahead: the Frame constructor of this pair from the extraction
+    // enqueued by the previous call when it was for the same pair (same buffers and geometry),
+    // else now; then the next pair's extraction is enqueued to run while this frame is tracked.
+    // Extraction depends on the images only, so the frame is the one the plain call builds.
+    int frame_stereo_ahead(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step,
+                           const uint8_t* nL, const uint8_t* nR) {
+        Dev::Ahead& a = dev.ahead;
+        if (a.on && a.L == L && a.R == R && a.rows == rows && a.cols == cols && a.step == step) {
+            a.on = false;
+            SLAM_CHECK(frame_collect(cf, a.slot));
+        } else {
+            if (a.on && hipStreamSynchronize(xstream) != hipSuccess) return ORBMI_E_HIP;  // a pair not asked for
+            a.on = false;
+            SLAM_CHECK(frame_stereo(cf, L, R, rows, cols, step));
+        }
+        if (nL && nR) {
+            SLAM_CHECK(frame_enqueue(nL, nR, rows, cols, step, &a.slot));
+            a.on = true;
+            a.L = nL;
+            a.R = nR;
+            a.rows = rows;
+            a.cols = cols;
+            a.step = step;
+        }
+        return ORBMI_OK;
+    }
+
     void free_dev() {
-        for (int k = 0; k < 2; k++) {
+        if (dev.ahead.on && xstream) (void)hipStreamSynchronize(xstream);
+        for (int k = 0; k < kSlots; k++) {
             (void)hipFree(dev.kps[k]);
             (void)hipFree(dev.desc[k]);
             (void)hipFree(dev.cnt[k]);
@@ -2315,8 +2359,9 @@ void orbmi_slam_destroy(orbmi_slam* h) {
     delete h;
 }
 
-int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
-                            double timestamp, float* tcw_out, int* has_pose) {
+static int track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+                        double timestamp, const uint8_t* next_left, const uint8_t* next_right, bool ahead, float* tcw_out,
+                        int* has_pose) {
     if (!h || !left || !right || rows <= 0 || cols <= 0 || step < (size_t)cols) return ORBMI_E_ARG;
     if (h->reset_pending) SLAM_CHECK(h->deferred_reset());  // (src/System.cc:139-146)
     TrackedFrame cf;
@@ -2328,7 +2373,8 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     h->phase_frames++;
     {
         PhaseTimer pt(&h->phase_ms[PH_FRAME]);
-        SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
+        if (ahead) SLAM_CHECK(h->frame_stereo_ahead(cf, left, right, rows, cols, step, next_left, next_right));
+        else SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
     }
     PhaseTimer* lock_t = new PhaseTimer(&h->phase_ms[PH_LOCK]);
     std::unique_lock<std::mutex> update_guard(h->update_mtx, std::defer_lock);
@@ -2355,6 +2401,17 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
     if (has_pose) *has_pose = lf.has_tcw ? 1 : 0;
     if (tcw_out && lf.has_tcw) std::memcpy(tcw_out, lf.tcw.data(), 16 * sizeof(float));
     return ORBMI_OK;
+}
+
+int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+                            double timestamp, float* tcw_out, int* has_pose) {
+    return track_stereo(h, left, right, rows, cols, step, timestamp, nullptr, nullptr, false, tcw_out, has_pose);
+}
+
+int orbmi_slam_track_stereo_ahead(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols,
+                                  size_t step, double timestamp, const uint8_t* next_left, const uint8_t* next_right,
+                                  float* tcw_out, int* has_pose) {
+    return track_stereo(h, left, right, rows, cols, step, timestamp, next_left, next_right, true, tcw_out, has_pose);
 }
 
 int orbmi_slam_get_schedule(orbmi_slam* h, orbmi_slam_event* out, int capacity, int* n) {

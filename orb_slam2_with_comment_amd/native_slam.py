@@ -56,15 +56,31 @@ class NativeStereoSLAM:
         self._h = h
         self._tcw = np.zeros(16, np.float32)
 
-    def TrackStereo(self, imLeft, imRight, timestamp: float):
+    def TrackStereo(self, imLeft, imRight, timestamp: float, next_pair=None):
+        """System::TrackStereo.  next_pair = (imLeft, imRight) of the next call: its Frame
+        constructor (extraction + stereo) then runs on the GPU while this frame is tracked
+        (orbmi_slam_track_stereo_ahead); the next call must pass those same arrays."""
         L = np.ascontiguousarray(imLeft, np.uint8)
         R = np.ascontiguousarray(imRight, np.uint8)
         if L.shape != R.shape or L.ndim != 2:
             raise ValueError("TrackStereo expects two gray images of the same size")
         has = C.c_int()
-        check("orbmi_slam_track_stereo", lib().orbmi_slam_track_stereo(
-            self._h, L.ctypes.data, R.ctypes.data, L.shape[0], L.shape[1], L.strides[0], float(timestamp),
-            self._tcw.ctypes.data, C.byref(has)))
+        if next_pair is None and not getattr(self, "_ahead", None):
+            check("orbmi_slam_track_stereo", lib().orbmi_slam_track_stereo(
+                self._h, L.ctypes.data, R.ctypes.data, L.shape[0], L.shape[1], L.strides[0], float(timestamp),
+                self._tcw.ctypes.data, C.byref(has)))
+        else:
+            nL = nR = None
+            if next_pair is not None:
+                nL = np.ascontiguousarray(next_pair[0], np.uint8)
+                nR = np.ascontiguousarray(next_pair[1], np.uint8)
+                if nL.shape != L.shape or nR.shape != L.shape:
+                    raise ValueError("next_pair must have the geometry of this pair")
+            check("orbmi_slam_track_stereo_ahead", lib().orbmi_slam_track_stereo_ahead(
+                self._h, L.ctypes.data, R.ctypes.data, L.shape[0], L.shape[1], L.strides[0], float(timestamp),
+                None if nL is None else nL.ctypes.data, None if nR is None else nR.ctypes.data,
+                self._tcw.ctypes.data, C.byref(has)))
+            self._ahead = (nL, nR) if nL is not None else None  # the buffers stay alive until used
         return self._tcw.reshape(4, 4).copy() if has.value else None
 
     def counts(self):

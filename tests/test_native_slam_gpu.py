@@ -17,18 +17,27 @@ _DECISIONS = ("n", "init", "track", "bow_matches", "lf_matches", "nmatches_map",
               "local_matches", "inliers", "need_kf", "state", "keyframes", "mappoints")
 
 
-def _drive(slam, frames):
+def _drive(slam, frames, ahead=False):
+    """TrackStereo per frame; ahead: with the next pair (its extraction runs while the frame is
+    tracked, orbmi_slam_track_stereo_ahead)."""
     for f, (L, R, _) in enumerate(frames):
-        slam.TrackStereo(L, R, 0.1 * f)
+        nxt = frames[f + 1][:2] if ahead and f + 1 < len(frames) else None
+        if ahead:
+            slam.TrackStereo(L, R, 0.1 * f, next_pair=nxt)
+        else:
+            slam.TrackStereo(L, R, 0.1 * f)
 
 
-def test_native_matches_oracle_200_frames(tmp_path):
+@pytest.mark.parametrize("ahead", [False, True])
+def test_native_matches_oracle_200_frames(tmp_path, ahead):
+    """ahead = True: the Frame constructor of frame k+1 runs on the GPU while frame k is tracked
+    (orbmi_slam_track_stereo_ahead, the bench's driver): the same decisions and trajectory."""
     n = 200  # config 1: the first 200 frames (stereo_kitti.cc), here of the synthetic sequence
     frames = render_sequence(n)
     s = sequence_settings(tmp_path)
     voc = small_vocabulary()
     gpu = NativeStereoSLAM(s, device=0, vocabulary=voc)
-    _drive(gpu, frames)
+    _drive(gpu, frames, ahead)
     ref = StereoSLAM(s, backend=OracleBackend(s, voc))
     _drive(ref, frames)
     a_all, b_all = gpu.stats, ref.stats
@@ -87,12 +96,13 @@ def test_native_needs_vocabulary_for_reference_tracking(tmp_path):
     slam.Shutdown()
 
 
-def _drive_paced(slam, frames, period):
+def _drive_paced(slam, frames, period, ahead=True):
     """Frames handed over `period` seconds apart, as stereo_kitti.cc:95-107 waits out each
-    frame's timestamp gap (there 0.1 s; scaled down here)."""
+    frame's timestamp gap (there 0.1 s; scaled down here); the next pair's extraction ahead."""
     t0 = time.perf_counter()
     for f, (L, R, _) in enumerate(frames):
-        slam.TrackStereo(L, R, 0.1 * f)
+        nxt = frames[f + 1][:2] if ahead and f + 1 < len(frames) else None
+        slam.TrackStereo(L, R, 0.1 * f, next_pair=nxt)
         wait = t0 + (f + 1) * period - time.perf_counter()
         if wait > 0:
             time.sleep(wait)
