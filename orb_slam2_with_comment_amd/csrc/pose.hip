@@ -42,14 +42,6 @@ constexpr int kPoseWaves = kPoseThreads / 64;
 constexpr int kPoseFullWaves = ORBMI_POSE_FULL_WAVES;
 constexpr int kPoseFullThreads = kPoseFullWaves * 64;
 static_assert(kPoseFullWaves >= 1 && kPoseFullWaves <= kPoseWaves, "buildSystem waves");
-// ORBMI_POSE_RCHAIN=1 (with ORBMI_POSE_THREADS=256: one wave per SIMD): every wave reduces the
-// system and solves the trial chain itself, its lanes holding the candidates in registers, so an
-// accepted trial needs no candidates barrier and no LDS round trip of the chain (A/B variant)
-#ifndef ORBMI_POSE_RCHAIN
-#define ORBMI_POSE_RCHAIN 0
-#endif
-constexpr bool kPoseRChain = ORBMI_POSE_RCHAIN != 0;
-static_assert(!kPoseRChain || kPoseWaves == kPoseFullWaves, "replicated chain: every wave runs buildSystem");
 constexpr int kPoseTraceWaves = 8;  // trace layout (orbmi_debug_pose_trace), whatever kPoseWaves
 constexpr int kPoseMaxObs = 4096;
 constexpr int kPoseTraceSeqs = 64;  // passes recorded by orbmi_debug_pose_trace
@@ -156,30 +148,6 @@ __device__ inline void pose_reduce28_w0(double (&acc)[28], double (*red)[32], do
 #pragma unroll
         for (int q = 0; q < 28; q++) acc[q] = stot[q];
     }
-}
-
-// the same sum into every wave (replicated-chain variant): each wave reads the waves' slots and
-// keeps its own copy of the totals (hb: LDS, per wave) for a later re-solve
-__device__ inline void pose_reduce28_all(double (&acc)[28], double (*red)[32], double* hb) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    {
-        double v[32];
-#pragma unroll
-        for (int q = 0; q < 28; q++) v[q] = acc[q];
-        v[28] = v[29] = v[30] = v[31] = 0;
-        const double s = wave_reduce_scatter32(v);
-        if (!(lane & 1)) red[wid][lane >> 1] = s;
-    }
-    __syncthreads();
-    double t = 0;
-#pragma unroll
-    for (int w = 0; w < kPoseFullWaves; w++) t += red[w][lane & 31];
-    if (lane < 28) hb[lane] = t;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < 28; q++) acc[q] = hb[q];
 }
 
 __device__ inline double pose_reduce1(double v, double* red1) {
@@ -351,30 +319,6 @@ __device__ inline void pose_candidates(const double (&hb)[28], double lambda, do
     }
 }
 
-// the same chain with lane j's candidate kept in its registers (replicated-chain variant)
-__device__ inline void pose_candidates_reg(const double (&hb)[28], double lambda, double ni, const double* T,
-                                           double (&ct)[8], double& cscale, double& cok) {
-    const int lane = threadIdx.x & 63;
-    double l = lambda, nn = ni;
-#pragma unroll
-    for (int m = 0; m < kPoseCands - 1; m++)
-        if (m < lane) { l *= nn; nn *= 2; }
-    double xv[6];
-    const bool ok = pose_solve6(hb, hb + 21, l, xv);
-    if (ok) se3_oplus(xv, T, ct);
-    else {
-#pragma unroll
-        for (int q = 0; q < 8; q++) ct[q] = T[q];
-#pragma unroll
-        for (int q = 0; q < 6; q++) xv[q] = 0;
-    }
-    double scale = 0;
-#pragma unroll
-    for (int j = 0; j < 6; j++) scale += xv[j] * (l * xv[j] + hb[21 + j]);
-    cscale = scale;
-    cok = ok ? 1.0 : 0.0;
-}
-
 // computeActiveErrors + activeRobustChi2 only (a trial's evaluation): this thread's robust chi2
 // sum; schi as pose_pass.  The Jacobians are formed only if the trial is accepted.
 __device__ inline double pose_chi_pass(const double* T, const PoseCam& cam, const orbmi_pose_obs* sobs,
@@ -451,8 +395,6 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     __shared__ double red1[2][kPoseWaves];
     __shared__ PoseCand scand[kPoseCands];  // wave 0's trial chain
     __shared__ double stot[32];              // wave 0's reduced system (H upper, b, chi2)
-    __shared__ double shb[kPoseRChain ? kPoseWaves : 1][32];  // each wave's system (replicated chain)
-    double ct[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cscale = 0, cok = 0;  // lane j's candidate (replicated chain)
     __shared__ double chiw[2][kPoseWaves];   // per-wave chi2 of a trial pass
     int cb = 0;                              // chiw buffer
     unsigned long long tstart = 0, rstart = 0;
@@ -578,19 +520,10 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
                 if (!first) {
                     // trial cj of the chain: the pose of oplus(x(lambda_cj)), evaluated by all waves
                     double Tt[8];
-                    bool ok2;
-                    double scale;
-                    if (kPoseRChain) {
 #pragma unroll
-                        for (int q = 0; q < 8; q++) Tt[q] = readlane_d(ct[q], cj);
-                        ok2 = readlane_d(cok, cj) != 0;
-                        scale = readlane_d(cscale, cj);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 8; q++) Tt[q] = scand[cj].T[q];
-                        ok2 = scand[cj].ok != 0;
-                        scale = scand[cj].scale;
-                    }
+                    for (int q = 0; q < 8; q++) Tt[q] = scand[cj].T[q];
+                    const bool ok2 = scand[cj].ok != 0;
+                    const double scale = scand[cj].scale;
                     seq++;
                     EV(0);
                     {
@@ -638,30 +571,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
                     if (done) break;
                     regen = !accept && cj == kPoseCands;  // chain exhausted: continue it
                 }
-                if (kPoseRChain && (accept || regen)) {
-                    // every wave: the reduced system (B2 inside) and the whole chain in its lanes
-                    if (accept) {
-                        pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
-                        EV(7);
-                        pose_reduce28_all(acc, red[rb], shb[wid]);
-                        rb ^= 1;
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 28; q++) acc[q] = shb[wid][q];
-                    }
-                    EV(4);
-                    if (first)  // computeLambdaInit, tau = 1e-5
-                        lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
-                                             fmax(fabs(acc[18]), fabs(acc[20])));
-                    pose_candidates_reg(acc, lambda, ni, T, ct, cscale, cok);
-                    EV(5);
-                    cj = 0;
-                    EV(6);
-                    if (first) {
-                        currentChi = iniChi = acc[27];
-                        first = false;
-                    }
-                } else if (accept || regen) {
+                if (accept || regen) {
                     if (accept) {  // buildSystem at the (new) estimate: the first iteration's, or
                                    // the next iteration's after an accepted trial
                         pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
