@@ -59,6 +59,11 @@ for step in "$@"; do
         tests)
             run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
             tail -4 $OUT/pytest_gpu.log; cp $OUT/pytest_gpu.log $P/;;
+        libtests=*)
+            # libtests=LIB:EXPR -- pytest -m gpu -k EXPR on another library build (A/B variants)
+            v=${step#libtests=}; l=${v%%:*}; e=${v#*:}; n=$(basename $l .so)
+            ORBMI_LIB=$l run libtests_$n 600 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "$e"
+            tail -5 $OUT/libtests_$n.log;;
         tests=*)
             run pytest_sel 600 python -u -m pytest tests -m gpu -v -rf -s --timeout 300 --timeout-method thread -k "${step#tests=}"
             tail -30 $OUT/pytest_sel.log;;
@@ -127,7 +132,7 @@ for step in "$@"; do
         poselat|poselat=*)
             # PoseOptimization latency probe (tools/pose_latency.py); poselat=LIB runs it on another build
             l=${step#poselat}; l=${l#=}
-            if [ -n "$l" ]; then ORBMI_LIB=$l run poselat_ab 120 python tools/pose_latency.py; cat $OUT/poselat_ab.log
+            if [ -n "$l" ]; then n=$(basename $l .so); ORBMI_LIB=$l run poselat_$n 120 python tools/pose_latency.py; cat $OUT/poselat_$n.log
             else run poselat 120 python tools/pose_latency.py; cat $OUT/poselat.log; fi;;
         greedy)
             run greedy 120 python tools/greedy_probe.py 64; cat $OUT/greedy.log;;
