@@ -70,7 +70,7 @@ def parse():
                     help="per-keyframe LocalMapping work: the whole LocalMapping::Run body, or ComputeBoW + LocalBA")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic_track.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r04", "traffic_batch.json"),
                     help="the same for --mode batch (tools/gpu.sh pmc_batch)")
