@@ -405,7 +405,13 @@ struct orbmi_slam {
     // thread, read by the mapping thread and by LocalBA's stop-flag mirror (orbmi_local_bundle_
     // adjustment reads it with an atomic load): every access is an atomic operation on this word
     int abort_ba = 0;
-    void set_abort_ba(int v) { __atomic_store_n(&abort_ba, v, __ATOMIC_RELEASE); }
+    // ORBMI_SLAM_NO_INTERRUPT=1 (experiment, tools/concur_breakdown.py): Tracking never raises
+    // mbAbortBA, so every LocalBA the mapping thread starts runs to its end
+    const bool no_interrupt = getenv("ORBMI_SLAM_NO_INTERRUPT") != nullptr;
+    void set_abort_ba(int v) {
+        if (v && no_interrupt) return;
+        __atomic_store_n(&abort_ba, v, __ATOMIC_RELEASE);
+    }
     std::thread lm_thread;
     bool async_lm() const { return s.async_local_mapping != 0; }
     // the schedule (orbmi_slam_get_schedule): every acquisition of map_mtx with the mapping thread

@@ -109,17 +109,14 @@ def _drive_paced(slam, frames, period, ahead=True):
 
 
 def test_native_concurrent_local_mapping(tmp_path):
-    """LocalMapping on its own thread (the reference's threading, src/System.cc:84-92): keyframe
-    decisions then depend on timing (AcceptKeyFrames, InterruptBA), so the check is the outcome:
-    every frame tracked, keyframes inserted and mapped, LocalBAs run (some possibly interrupted),
-    the trajectory as accurate as the synchronous loop's, and a clean shutdown.
-
-    Frames come paced as the reference's stereo_kitti.cc hands them over (a timestamp wait per
-    frame), at 3 ms -- short enough that the mapping thread still overlaps Tracking on most
-    keyframes.  Handed over back to back (no wait, the throughput bench's regime) the mapping
-    thread falls behind Tracking and the trajectory's accuracy then depends on how far
-    (tools/concur_probe.py: ATE 0.8-4.2 m on this sequence against 0.25-0.29 m paced at 3 ms and
-    the synchronous loop's 0.50 m); that run is checked for completion only."""
+    """LocalMapping on its own thread (the reference's threading, src/System.cc:84-92), frames
+    paced as the reference's stereo_kitti.cc hands them over (a timestamp wait per frame, 3 ms
+    here -- short enough that the mapping thread still overlaps Tracking on most keyframes):
+    every frame tracked, keyframes inserted and mapped, LocalBAs run, the trajectory as accurate
+    as the synchronous loop's, and a clean shutdown.  Handed over back to back the mapping thread
+    falls behind and the run depends on the interleaving; that regime is held to an exact bar by
+    test_concurrent_schedule_replays_on_oracle (its trajectory equals the oracle's replay of the
+    recorded schedule), and tools/concur_breakdown.py measures where its accuracy goes."""
     n = 200
     frames = render_sequence(n)
     s = sequence_settings(tmp_path)
@@ -129,20 +126,17 @@ def test_native_concurrent_local_mapping(tmp_path):
     _drive(sync, frames)
     ate_sync = ate_rmse(sync.trajectory_twc(), gt)
     sync.Shutdown()
-    for period in (0.003, 0.0):
-        slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
-        _drive_paced(slam, frames, period)
-        slam.WaitLocalMapping()
-        st = slam.stats
-        assert len(st) == n and all(x["state"] == OK for x in st)
-        c = slam.counts()
-        assert c["keyframes"] >= 10 and c["local_ba_calls"] >= 5 and c["mappoints"] > 1000, c
-        ate = ate_rmse(slam.trajectory_twc(), gt)
-        print(f"concurrent LocalMapping, frames {period * 1e3:g} ms apart: ATE {ate:.4f} m "
-              f"(synchronous {ate_sync:.4f} m), {c}")
-        if period > 0:
-            assert ate < max(2.0 * ate_sync, 0.6), (ate, ate_sync)
-        slam.Shutdown()
+    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
+    _drive_paced(slam, frames, 0.003)
+    slam.WaitLocalMapping()
+    st = slam.stats
+    assert len(st) == n and all(x["state"] == OK for x in st)
+    c = slam.counts()
+    assert c["keyframes"] >= 10 and c["local_ba_calls"] >= 5 and c["mappoints"] > 1000, c
+    ate = ate_rmse(slam.trajectory_twc(), gt)
+    print(f"concurrent LocalMapping, frames 3 ms apart: ATE {ate:.4f} m (synchronous {ate_sync:.4f} m), {c}")
+    assert ate < max(1.2 * ate_sync, 0.6), (ate, ate_sync)
+    slam.Shutdown()
 
 
 def _concurrent_record(tmp_path, n, period):

@@ -198,6 +198,11 @@ for step in "$@"; do
                 ORBMI_SLAM_STAGED=1 run concur_staged_$i 200 python -u -m pytest -x -q -s -m gpu --timeout 150 --timeout-method thread tests/test_native_slam_gpu.py -k test_native_concurrent_local_mapping
                 echo "dev: $(grep -o 'ATE [0-9.]* m (synchronous [0-9.]* m)' $OUT/concur_dev_$i.log)  staged: $(grep -o 'ATE [0-9.]* m (synchronous [0-9.]* m)' $OUT/concur_staged_$i.log)" | tee -a $OUT/concur.txt
             done;;
+        concurbd)
+            # tools/concur_breakdown.py: the concurrent LocalMapping's accuracy per regime (back to
+            # back, back to back without InterruptBA, paced), 3 runs each
+            run concurbd 600 python -u tools/concur_breakdown.py 3; grep -v "^{" $OUT/concurbd.log | tee $P/concur_breakdown.txt
+            tail -1 $OUT/concurbd.log > $P/concur_breakdown.json;;
         concurprobe|concurprobe=*)
             # concurprobe=MS: frames paced MS apart (stereo_kitti.cc's timestamp wait)
             ms=${step#concurprobe}; ms=${ms#=}; ms=${ms:-0}
