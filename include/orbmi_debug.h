@@ -36,7 +36,8 @@ int orbmi_debug_greedy_stats(unsigned long long* out, int reset);
 
 /* k_greedy's s_memtime cycles summed over calls since the last reset: out[0] prologue (queries'
  * prefixes and the keypoints' octave / occupancy loaded), [1] the rounds to the fixpoint,
- * [2] the outputs (rotation histogram, last assignment per keypoint); [3..6] reserved (0).
+ * [2] the outputs (rotation histogram, last assignment per keypoint); [3..5] thread 0's split of
+ * the rounds (claims + barrier, evaluation, convergence flag + barrier); [6] reserved (0).
  * out: 7 entries. */
 int orbmi_debug_greedy_cycles(unsigned long long* out, int reset);
 

@@ -501,89 +501,173 @@ __device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int
     return d1 <= TH_HIGH ? i1 : -1;
 }
 
-#ifndef ORBMI_GREEDY_PRE
-#define ORBMI_GREEDY_PRE 4
+#ifndef ORBMI_GREEDY_THREADS
+#define ORBMI_GREEDY_THREADS 1024
 #endif
-constexpr int kGreedyThreads = 1024, kGreedyQPer = 4, kGreedyPre = ORBMI_GREEDY_PRE;
+constexpr int kGreedyThreads = ORBMI_GREEDY_THREADS, kGreedyQPer = 4096 / kGreedyThreads, kGreedyPre = 4;
 constexpr int kGreedyQBits = 24, kGreedyQMask = (1 << kGreedyQBits) - 1;  // query index field of a claim
 constexpr int kGreedyMaxQueries = 1 << kGreedyQBits;
+
+// A prefix entry in a register: octave << 25 | dist << 16 | keypoint index (dist <= 256, index <
+// kGreedyMaxKp, octave < kMaxLevels); kNoEntry = none
+constexpr unsigned kNoEntry = ~0u;
+__device__ inline int pe_idx(unsigned e) { return (int)(e & 0xFFFF); }
+__device__ inline int pe_dist(unsigned e) { return (int)((e >> 16) & 0x1FF); }
+__device__ inline int pe_oct(unsigned e) { return (int)(e >> 25); }
+
+// greedy_decide on two prefix entries (the octaves travel with them: no LDS read)
+__device__ inline int greedy_decide_pe(const GreedyArgs& a, unsigned e1, unsigned e2) {
+    if (e1 == kNoEntry) return -1;
+    const int d1 = pe_dist(e1);
+    if (d1 > TH_HIGH) return -1;
+    if (a.mode == 0 && e2 != kNoEntry && pe_oct(e1) == pe_oct(e2) && d1 > a.nnratio * pe_dist(e2)) return -1;
+    return pe_idx(e1);
+}
 
 // k_greedy statistics (orbmi_debug_greedy_stats): calls, rounds summed, largest round count,
 // slow-path query evaluations summed, calls that fell back to the sequential replay
 __device__ unsigned long long g_greedy_stats[5];
 __device__ int g_greedy_on;  // set by the first orbmi_debug_greedy_* call: statistics collected from then on
 // development aid: s_memtime cycles of k_greedy's phases summed over calls (prologue, rounds,
-// epilogue), read with the statistics (orbmi_debug_greedy_stats out[5..7] when asked for 8)
+// epilogue; thread 0's split of the rounds: claims + barrier, evaluation, flag + barrier), read by
+// orbmi_debug_greedy_cycles
 __device__ unsigned long long g_greedy_cycles[7];
 
 // Each thread keeps its queries (q = tid + k * 1024) in registers: current result, candidate
-// count and the first kGreedyPre sorted entries packed as dist << 16 | idx; the keypoints'
-// octave and the initial occupancy live in LDS.  A round then touches LDS only, except
-// for queries whose prefix runs out of unclaimed entries (full list / re-enumeration).
+// count and the first kGreedyPre sorted entries (pe_* packing, the keypoint's octave included);
+// the initial occupancy lives in LDS.  A round then touches LDS only, except for queries whose
+// prefix runs out of unclaimed entries (full list / re-enumeration).
 // Claims carry the round: claim[i] = tag(r) | q with tag(r) = (64 - r) << 24 (an atomicMin keeps
 // the current round's smallest query, and an older round's claim reads as free), 0 for a keypoint
 // occupied on entry; so the array is set once, and a round is claims, a barrier, the evaluation,
 // a barrier (the convergence flag alternates between two slots).  Query indices take the low 24
 // bits (the launchers refuse nq >= 2^24), the round tag the 7 above them.
+// The evaluation is branch-free selects over the prefix's claim words; the prologue is two
+// dependent global round trips (gate, counts and poses; then every per-query and per-keypoint
+// load at once); the epilogue aggregates the rotation histogram per wave and takes its three
+// maxima with wave reductions.
 __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     __shared__ int claim[kGreedyMaxKp];   // round-tagged min query index holding the keypoint;
                                           // afterwards the max query index assigned to it
     __shared__ uint8_t occ0[kGreedyMaxKp], oct[kGreedyMaxKp];  // occ0: afterwards "rejected"
-    __shared__ int slowres[kGreedyQPer * kGreedyThreads];
+    __shared__ int ovfres[kGreedyQPer * kGreedyThreads];       // overflowed queries' results
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int flag[4];
-    if (a.gate && *a.gate >= a.gate_min) return;  // uniform: every thread reads before any write
     const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-    const int tid = threadIdx.x, n = frame_n(a.F);
-    const int nq = a.mode == 1 ? frame_n(a.LF) : a.nq;  // (the by-value argument stays unmodified)
+    const int tid = threadIdx.x, lane = tid & 63;
+    // round trip 1: the gate, the device-resident counts, the poses (mode 1).  The loads are
+    // unconditional, through a.ncand (at least one entry, always allocated) where a pointer is
+    // absent, so that they issue together (a branch per optional load serialises them).
+    const int gv = *(a.gate ? a.gate : a.ncand);
+    const int nFv = *(a.F.n_dev ? a.F.n_dev : a.ncand);
+    const int nLv = *(a.mode == 1 && a.LF.n_dev ? a.LF.n_dev : a.ncand);
     bool fw = false, bw = false;
     Pose34 Tc;
     if (a.mode == 1) {
         Tc = frame_pose(a.F);
         motion_direction(a.F, Tc.m, a.LF, a.mono, &fw, &bw);
     }
-    for (int i = tid; i < n; i += blockDim.x) { occ0[i] = a.occ0[i]; oct[i] = (uint8_t)a.F.keys[i].octave; }
+    if (a.gate && gv >= a.gate_min) return;  // uniform: every thread reads before any write
+    const int n = a.F.n_dev ? min(nFv, a.F.n) : a.F.n;
+    const int nq = a.mode == 1 ? (a.LF.n_dev ? min(nLv, a.LF.n) : a.LF.n) : a.nq;  // (a.nq stays unmodified)
     const bool regs = nq <= kGreedyThreads * kGreedyQPer;
+    const bool ori = a.mode == 1 && a.check_ori;
+    // round trip 2: the queries' counts, prefixes, observation flags (and LF angles), and the
+    // keypoints' occupancy and octave, all issued before the first use (query and keypoint
+    // indices clamped into range: straight-line loads, no branch between them)
     int res[kGreedyQPer], nc[kGreedyQPer];
     unsigned pre[kGreedyQPer][kGreedyPre];
     bool obs[kGreedyQPer];
+    float angL[kGreedyQPer];
 #pragma unroll
     for (int k = 0; k < kGreedyQPer; k++) {
-        const int q = tid + k * kGreedyThreads;
-        res[k] = -1;
-        nc[k] = 0;
-        obs[k] = false;
+        res[k] = -1; nc[k] = 0; obs[k] = false; angL[k] = 0.f;
 #pragma unroll
         for (int j = 0; j < kGreedyPre; j++) pre[k][j] = 0;
-        if (regs && q < nq) {
-            nc[k] = a.ncand[q];
-            obs[k] = query_has_obs(a, q);
-            const unsigned long long* t = a.top + (long long)q * kTopK;
+    }
+    // the first 4096 keypoints' occupancy and octave (the rest, if any, in a loop below)
+    int o0[4], v0[4];
 #pragma unroll
-            for (int j = 0; j < kGreedyPre; j++) {
-                const unsigned long long e = t[j];
-                pre[k][j] = ((unsigned)(e >> 40) << 16) | (unsigned)(e & 0xFFFF);  // dist <= 256: 9 bits
+    for (int u = 0; u < 4; u++) {
+        o0[u] = 0; v0[u] = 0;
+        if (u * kGreedyThreads < n) {  // uniform: slots past n issue nothing
+            const int ic = min(tid + u * kGreedyThreads, n - 1);
+            o0[u] = a.occ0[ic];
+            v0[u] = a.F.keys[ic].octave;
+        }
+    }
+    if (regs && nq > 0) {
+        int ncv[kGreedyQPer];
+        unsigned flv[kGreedyQPer];
+        float alv[kGreedyQPer];
+        unsigned long long ev[kGreedyQPer][kGreedyPre];
+#pragma unroll
+        for (int k = 0; k < kGreedyQPer; k++) {
+            if (k * kGreedyThreads >= nq) break;  // uniform: slots past nq issue nothing
+            const int qc = min(tid + k * kGreedyThreads, nq - 1);
+            ncv[k] = a.ncand[qc];
+            flv[k] = a.mode == 0 ? a.mps[qc].flags : a.lfp[qc].flags;
+            alv[k] = *(ori ? &a.LF.keys[qc].angle : (const float*)a.ncand);
+            const unsigned long long* t = a.top + (long long)qc * kTopK;
+#pragma unroll
+            for (int j = 0; j < kGreedyPre; j++) ev[k][j] = t[j];
+        }
+#pragma unroll
+        for (int k = 0; k < kGreedyQPer; k++) {
+            if (tid + k * kGreedyThreads >= nq) continue;
+            nc[k] = ncv[k];
+            obs[k] = (flv[k] & ORBMI_MP_HAS_OBS) != 0;
+            angL[k] = alv[k];
+#pragma unroll
+            for (int j = 0; j < kGreedyPre; j++)
+                pre[k][j] = ((unsigned)(ev[k][j] >> 40) << 16) | (unsigned)(ev[k][j] & 0xFFFF);
+        }
+    }
+    for (int base = 0; base < n; base += 4 * kGreedyThreads) {
+        int o[4], v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            o[u] = o0[u]; v[u] = v0[u];
+            if (base > 0) {
+                const int ic = min(base + tid + u * kGreedyThreads, n - 1);
+                o[u] = a.occ0[ic];
+                v[u] = a.F.keys[ic].octave;
             }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = base + tid + u * kGreedyThreads;
+            if (i < n) { occ0[i] = (uint8_t)o[u]; oct[i] = (uint8_t)v[u]; claim[i] = o[u] ? 0 : 0x7FFFFFFF; }
         }
     }
     if (!regs)
         for (int q = tid; q < nq; q += blockDim.x) a.res[q] = -1;
-    // claims set once (round tags, 0 = occupied on entry), flags cleared
-    for (int i = tid; i < n; i += blockDim.x) claim[i] = occ0[i] ? 0 : 0x7FFFFFFF;
     if (tid < 2) flag[tid] = 0;
     __syncthreads();
+    // usable prefix: past kCandCap the list is partial; entries past it point at keypoint 0
+    // (their claim words are read and ignored); mode 0 packs the octaves in
+    int kk[kGreedyQPer];
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) {
+        kk[k] = nc[k] <= a.cap ? min(nc[k], kGreedyPre) : 0;
+#pragma unroll
+        for (int j = 0; j < kGreedyPre; j++) {
+            if (j >= kk[k]) pre[k][j] = 0;
+            else if (a.mode == 0) pre[k][j] |= (unsigned)oct[pe_idx(pre[k][j])] << 25;
+        }
+    }
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     bool converged = false;
     int rounds = 0, nslow = 0;
+    unsigned long long tcl = 0, tev = 0, tfl = 0;  // thread 0's split of the rounds (development aid)
     static_assert(kGreedyRounds < 48 + 1 && kGreedyMaxKp <= 65536, "round tags (7 bits) above 24-bit query indices");
     for (int round = 0; round < kGreedyRounds && !converged; round++) {
         rounds++;
+        const unsigned long long r0 = __builtin_amdgcn_s_memtime();
         const int tag = (64 - round) << kGreedyQBits;
         // keypoint idx is taken for query q: occupied on entry, or claimed this round by an earlier query
-        auto taken = [&](int idx, int q) {
-            const int v = claim[idx];
-            return v == 0 || ((v & ~kGreedyQMask) == tag && (v & kGreedyQMask) < q);
-        };
+        // (one compare: claims of older rounds carry larger tags, 0 = occupied on entry)
+        auto taken = [&](int idx, int q) { return claim[idx] < (tag | q); };
         if (regs) {
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++)
@@ -595,72 +679,84 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             }
         }
         __syncthreads();
+        const unsigned long long r1 = __builtin_amdgcn_s_memtime();
         if (tid == 0) flag[(round + 1) & 1] = 0;  // the next round's slot (last read before this round's claims)
         int changed = 0;
         if (regs) {
-            unsigned slow = 0;
-            int fast[kGreedyQPer];
+            unsigned slow = 0, ovf = 0;
+            int nr[kGreedyQPer];
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++) {
                 const int q = tid + k * kGreedyThreads;
-                fast[k] = res[k];
-                // the query's prefix claims read at once (independent LDS reads, one latency)
+                nr[k] = res[k];
+                // A query is evaluated again only when a prefix keypoint changed claimers in the
+                // last round (or its last evaluation went past the prefix): otherwise every
+                // taken-bit it reads is the same, and so is its result.  Whole waves skip.
+                if (q >= nq) continue;
+                // the prefix's claim words read at once (independent LDS reads, one latency)
                 int cv[kGreedyPre];
 #pragma unroll
-                for (int j = 0; j < kGreedyPre; j++) cv[j] = claim[pre[k][j] & 0xFFFF];
-                if (q >= nq) continue;
-                int d1 = 0, i1 = -1, d2 = 0, i2 = -1;
-                const int kk = nc[k] <= a.cap ? min(nc[k], kGreedyPre) : 0;
+                for (int j = 0; j < kGreedyPre; j++) cv[j] = claim[pe_idx(pre[k][j])];
+                // the two smallest unclaimed prefix entries, by selects
+                unsigned e1 = kNoEntry, e2 = kNoEntry;
 #pragma unroll
                 for (int j = 0; j < kGreedyPre; j++) {
-                    if (j >= kk || i2 >= 0) continue;
-                    const int v = cv[j];
-                    if (v == 0 || ((v & ~kGreedyQMask) == tag && (v & kGreedyQMask) < q)) continue;
-                    const unsigned e = pre[k][j];
-                    const int idx = (int)(e & 0xFFFF), d = (int)((e >> 16) & 0x1FF);
-                    if (i1 < 0) { d1 = d; i1 = idx; } else { d2 = d; i2 = idx; }
+                    // taken <=> cv < tag | q: 0 (occupied on entry) and this round's earlier
+                    // claims are below it, later queries' and older rounds' claims (larger
+                    // tags) and 0x7FFFFFFF (never claimed) are not
+                    const bool fr = j < kk[k] && cv[j] >= (tag | q);
+                    const bool to1 = fr && e1 == kNoEntry;
+                    const bool to2 = fr && !to1 && e2 == kNoEntry;
+                    e2 = to2 ? pre[k][j] : e2;
+                    e1 = to1 ? pre[k][j] : e1;
                 }
-                if (i2 < 0 && nc[k] > kGreedyPre) slow |= 1u << k;  // prefix exhausted
-                else fast[k] = greedy_decide(a, oct, d1, i1, d2, i2);
+                // mode 1 decides on the best entry alone; mode 0 needs the second (ratio test)
+                const bool open = (a.mode == 0 ? e2 : e1) == kNoEntry && nc[k] > kGreedyPre;
+                if (!open) nr[k] = greedy_decide_pe(a, e1, e2);
+                else if (nc[k] <= a.cap) slow |= 1u << k;
+                else ovf |= 1u << k;
             }
-            nslow += __builtin_popcount(slow);
+            nslow += __builtin_popcount(slow | ovf);
             // queries whose prefix ran out: the whole wave evaluates each one together, every
             // lane loading entries of its candidate list (one global latency instead of a serial
             // scan), the two smallest unclaimed entries by wave minima (entries are distinct)
-            const int lane = tid & 63;
-            unsigned long long pending = __ballot(slow != 0);
-            while (pending) {
-                const int src = __builtin_ctzll(pending);
-                pending &= pending - 1;
-                const unsigned sl = (unsigned)__shfl((int)slow, src, 64);
-                for (int k = 0; k < kGreedyQPer; k++) {
-                    if (!(sl >> k & 1)) continue;
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++) {
+                unsigned long long pending = __ballot((slow >> k) & 1);
+                while (pending) {
+                    const int src = __builtin_ctzll(pending);
+                    pending &= pending - 1;
                     const int q = tid - lane + src + k * kGreedyThreads;
-                    const int ncq = __shfl(nc[k], src, 64);
-                    int r = -1;
-                    if (ncq <= a.cap) {
-                        const unsigned long long* c =
-                            ncq <= kTopK ? a.top + (long long)q * kTopK : a.cand + (long long)q * a.cap;
-                        unsigned long long b1 = ~0ull, b2 = ~0ull;
-                        for (int p = lane; p < ncq; p += 64) {
-                            const unsigned long long e = c[p];
-                            if (taken((int)(e & 0xFFFFF), q)) continue;
-                            if (e < b1) { b2 = b1; b1 = e; }
-                            else if (e < b2) b2 = e;
-                        }
-                        const unsigned long long m1 = wave_min_u64_dpp(b1);
-                        const unsigned long long m2 = wave_min_u64_dpp(b1 == m1 ? b2 : b1);
-                        r = greedy_decide(a, oct, (int)(m1 >> 40), m1 == ~0ull ? -1 : (int)(m1 & 0xFFFFF),
-                                          (int)(m2 >> 40), m2 == ~0ull ? -1 : (int)(m2 & 0xFFFFF));
-                    } else if (lane == src) {  // overflowed list: enumerate again
-                        r = greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return taken(idx, q); });
+                    const int ncq = __builtin_amdgcn_readlane(nc[k], src);
+                    const unsigned long long* c =
+                        ncq <= kTopK ? a.top + (long long)q * kTopK : a.cand + (long long)q * a.cap;
+                    unsigned long long b1 = ~0ull, b2 = ~0ull;
+                    for (int p = lane; p < ncq; p += 64) {
+                        const unsigned long long e = c[p];
+                        if (taken((int)(e & 0xFFFFF), q)) continue;
+                        if (e < b1) { b2 = b1; b1 = e; }
+                        else if (e < b2) b2 = e;
                     }
-                    if (lane == src) slowres[k * kGreedyThreads + tid] = r;
+                    const unsigned long long m1 = wave_min_u64_dpp(b1);
+                    const unsigned long long m2 = wave_min_u64_dpp(b1 == m1 ? b2 : b1);
+                    const int r = greedy_decide(a, oct, (int)(m1 >> 40), m1 == ~0ull ? -1 : (int)(m1 & 0xFFFFF),
+                                                (int)(m2 >> 40), m2 == ~0ull ? -1 : (int)(m2 & 0xFFFFF));
+                    if (lane == src) nr[k] = r;
+                }
+            }
+            // overflowed lists (more than kCandCap candidates): the owning lane enumerates again
+            if (ovf) {
+#pragma unroll 1
+                for (int k = 0; k < kGreedyQPer; k++) {
+                    if (!((ovf >> k) & 1)) continue;
+                    const int q = tid + k * kGreedyThreads;
+                    ovfres[k * kGreedyThreads + tid] =
+                        greedy_eval(a, q, Tc.m, fw, bw, [&](int idx) { return taken(idx, q); });
                 }
             }
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++) {
-                const int r = (slow >> k & 1) ? slowres[k * kGreedyThreads + tid] : fast[k];
+                const int r = (ovf >> k) & 1 ? ovfres[k * kGreedyThreads + tid] : nr[k];
                 if (r != res[k]) { res[k] = r; changed = 1; }
             }
         } else {
@@ -669,9 +765,12 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
                 if (r != a.res[q]) { a.res[q] = r; changed = 1; }
             }
         }
-        if (__ballot(changed) && (tid & 63) == 0) flag[round & 1] = 1;  // one LDS store per wave, no atomics
+        const unsigned long long r2 = __builtin_amdgcn_s_memtime();
+        if (__ballot(changed) && lane == 0) flag[round & 1] = 1;  // one LDS store per wave, no atomics
         __syncthreads();
         converged = flag[round & 1] == 0;
+        const unsigned long long r3 = __builtin_amdgcn_s_memtime();
+        tcl += r1 - r0; tev += r2 - r1; tfl += r3 - r2;
     }
     if (regs) {
 #pragma unroll
@@ -692,83 +791,94 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             }
         }
         __syncthreads();
+        if (regs) {  // the sequential replay's results
+#pragma unroll
+            for (int k = 0; k < kGreedyQPer; k++) {
+                const int q = tid + k * kGreedyThreads;
+                if (q < nq) res[k] = a.res[q];
+            }
+        }
     }
     const unsigned long long c2 = __builtin_amdgcn_s_memtime();
     // outputs: last assignment per keypoint (claim[] reused); rotation consistency (mode 1),
-    // rejected keypoints flagged in occ0[]
+    // rejected keypoints flagged in occ0[].  The matched keypoints' angles are loaded first and
+    // travel while the tables are cleared.
+    float angF[kGreedyQPer];
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) {
+        angF[k] = 0.f;
+        if (regs && ori && tid + k * kGreedyThreads < nq && res[k] >= 0) angF[k] = a.F.keys[res[k]].angle;
+    }
     int* last = claim;
     uint8_t* rejected = occ0;
     for (int i = tid; i < n; i += blockDim.x) { last[i] = -1; rejected[i] = 0; }
     if (tid < HISTO_LENGTH) hist[tid] = 0;
     if (tid == 0) flag[1] = 0;
     __syncthreads();
-    // the final assignments (registers when the queries fit them) and, for the rotation check,
-    // each query's bin, computed once
     int fbin[kGreedyQPer];
-#pragma unroll
-    for (int k = 0; k < kGreedyQPer; k++) fbin[k] = -1;
-    if (!converged && regs) {  // the sequential replay's results
+    int nmine = 0;
+    if (regs) {
 #pragma unroll
         for (int k = 0; k < kGreedyQPer; k++) {
             const int q = tid + k * kGreedyThreads;
-            if (q < nq) res[k] = a.res[q];
+            const bool m = q < nq && res[k] >= 0;
+            fbin[k] = -1;
+            if (m) {
+                atomicMax(&last[res[k]], q);
+                nmine++;
+                if (ori) fbin[k] = rot_bin(angL[k], angF[k]);
+            }
+            // the wave's bins: one LDS atomic per distinct bin (most matches share one or two)
+            unsigned long long act = __ballot(fbin[k] >= 0);
+            while (act) {
+                const int b = __builtin_amdgcn_readlane(fbin[k], __builtin_ctzll(act));
+                const unsigned long long same = __ballot(fbin[k] == b);
+                if (lane == __builtin_ctzll(act)) atomicAdd(&hist[b], (int)__builtin_popcountll(same));
+                act &= ~same;
+            }
+        }
+    } else {
+        for (int q = tid; q < nq; q += blockDim.x) {
+            const int r = a.res[q];
+            if (r < 0) continue;
+            atomicMax(&last[r], q);
+            nmine++;
+            if (ori) atomicAdd(&hist[rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle)], 1);
         }
     }
-    auto each_query = [&](auto&& f) {
-        if (regs) {
-#pragma unroll
-            for (int k = 0; k < kGreedyQPer; k++) {
-                const int q = tid + k * kGreedyThreads;
-                if (q < nq) f(k, q, res[k]);
-            }
-        } else {
-            for (int q = tid; q < nq; q += blockDim.x) f(-1, q, a.res[q]);
-        }
-    };
-    const bool ori = a.mode == 1 && a.check_ori;
     // match counts per thread, then one LDS atomic per wave (a shared counter hit by every
     // thread serialises the wave's 64 atomics)
     auto wave_count = [&](int c, int sign) {
         c = (int)wave_sum((double)c);
-        if ((tid & 63) == 0 && c) atomicAdd(&flag[1], sign * c);
+        if (lane == 0 && c) atomicAdd(&flag[1], sign * c);
     };
-    int nmine = 0;
-    each_query([&](int k, int q, int r) {
-        if (r < 0) return;
-        atomicMax(&last[r], q);
-        nmine++;
-        if (ori) {
-            const int bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
-            atomicAdd(&hist[bin], 1);
-            if (k >= 0) fbin[k] = bin;
-        }
-    });
     wave_count(nmine, 1);
     __syncthreads();
-    int ind1 = -1, ind2 = -1, ind3 = -1;
-    if (a.mode == 1 && a.check_ori) {  // ComputeThreeMaxima (:1854-1895), same in every thread
-        int max1 = 0, max2 = 0, max3 = 0;
-        for (int i = 0; i < HISTO_LENGTH; i++) {
-            const int s = hist[i];
-            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-            else if (s > max3) { max3 = s; ind3 = i; }
-        }
+    if (ori) {
+        // ComputeThreeMaxima (:1854-1895): the three largest non-empty bins, a tie going to the
+        // lower bin (the scan's strict comparisons), by three wave maxima of count << 8 | (255 - bin)
+        const int s = lane < HISTO_LENGTH ? hist[lane] : 0;
+        const unsigned key = s > 0 ? ((unsigned)s << 8) | (unsigned)(255 - lane) : 0u;
+        const unsigned k1 = wave_max_u32_dpp(key);
+        const unsigned k2 = wave_max_u32_dpp(key == k1 ? 0u : key);
+        const unsigned k3 = wave_max_u32_dpp(key == k1 || key == k2 ? 0u : key);
+        const int max1 = (int)(k1 >> 8), max2 = (int)(k2 >> 8), max3 = (int)(k3 >> 8);
+        int ind1 = k1 ? 255 - (int)(k1 & 255) : -1, ind2 = k2 ? 255 - (int)(k2 & 255) : -1;
+        int ind3 = k3 ? 255 - (int)(k3 & 255) : -1;
         if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        auto keep = [&](int bin) { return bin == ind1 || bin == ind2 || bin == ind3; };
         int nrej = 0;
-        each_query([&](int k, int q, int r) {
-            if (r < 0) return;
-            int bin = -1;
-            if (k >= 0) {
+        if (regs) {
 #pragma unroll
-                for (int kk = 0; kk < kGreedyQPer; kk++)
-                    if (kk == k) bin = fbin[kk];
-            } else {
-                bin = rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle);
+            for (int k = 0; k < kGreedyQPer; k++)
+                if (fbin[k] >= 0 && !keep(fbin[k])) { rejected[res[k]] = 1; nrej++; }
+        } else {
+            for (int q = tid; q < nq; q += blockDim.x) {
+                const int r = a.res[q];
+                if (r >= 0 && !keep(rot_bin(a.LF.keys[q].angle, a.F.keys[r].angle))) { rejected[r] = 1; nrej++; }
             }
-            if (bin != ind1 && bin != ind2 && bin != ind3) { rejected[r] = 1; nrej++; }
-        });
+        }
         wave_count(nrej, -1);
         __syncthreads();
     }
@@ -781,6 +891,9 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         atomicAdd(&g_greedy_cycles[0], c1 - c0);
         atomicAdd(&g_greedy_cycles[1], c2 - c1);
         atomicAdd(&g_greedy_cycles[2], c3 - c2);
+        atomicAdd(&g_greedy_cycles[3], tcl);
+        atomicAdd(&g_greedy_cycles[4], tev);
+        atomicAdd(&g_greedy_cycles[5], tfl);
         atomicAdd(&g_greedy_stats[0], 1ull);
         atomicAdd(&g_greedy_stats[1], (unsigned long long)rounds);
         atomicMax(&g_greedy_stats[2], (unsigned long long)rounds);
@@ -1117,7 +1230,7 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
     a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = F;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches;
-    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.stream, a);
     return ORBMI_OK;
 }
 
@@ -1144,7 +1257,7 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
     a.LF = LF;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches; a.gate = gate; a.gate_min = gate_min;
-    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(1024), 0, m.stream, a);
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.stream, a);
     return ORBMI_OK;
 }
 

@@ -102,6 +102,20 @@ __device__ inline unsigned long long wave_min_u64_dpp(unsigned long long v) {
     return v;
 }
 
+// wave maximum of a u32 key (every lane ends with it), the same exchange pattern
+__device__ inline unsigned wave_max_u32_dpp(unsigned v) {
+    unsigned w;
+    w = __builtin_amdgcn_update_dpp(0u, v, kDppXor1, 0xf, 0xf, false); v = w > v ? w : v;
+    w = __builtin_amdgcn_update_dpp(0u, v, kDppXor2, 0xf, 0xf, false); v = w > v ? w : v;
+    w = __builtin_amdgcn_update_dpp(0u, v, kDppHalfMirror, 0xf, 0xf, false); v = w > v ? w : v;
+    w = __builtin_amdgcn_update_dpp(0u, v, kDppRor8, 0xf, 0xf, false); v = w > v ? w : v;
+    auto s16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    w = s16[0] == v ? s16[1] : s16[0]; v = w > v ? w : v;
+    auto s32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    w = s32[0] == v ? s32[1] : s32[0]; v = w > v ? w : v;
+    return v;
+}
+
 // all-reduce of one value over the wave (every lane ends with the same sum: each step adds the
 // partner's value, and a + b == b + a)
 __device__ inline double wave_sum(double v) {

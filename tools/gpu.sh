@@ -15,8 +15,10 @@
 #   gloo2            bench.py --gpus 2 --dist-backend gloo (config 4 rehearsal on one device)
 #   prof             rocprofv3 --kernel-trace --stats of the default bench
 #   prof_MODE        the same for --mode MODE
+#   proflib=LIB      the default bench's kernel stats on another library build
 #   sqpmc[_MODE]     two SQ counter passes (waves, issue, LDS, VMEM) -> per-kernel means
 #   poselat[=LIB]    tools/pose_latency.py (PoseOptimization latency), optionally on another build
+#   greedy[=LIB]     tools/greedy_probe.py (k_greedy rounds and phase cycles), optionally on another build
 #   ktrace[_MODE]    rocprofv3 --kernel-trace of a short bench run + tools/trace_gaps.py
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the default bench -> traffic.json
 #   pmc_MODE         the same for --mode MODE
@@ -79,6 +81,12 @@ for step in "$@"; do
         gloo2)
             run gloo2 500 python bench.py --gpus 2 --dist-backend gloo --steps 40 --warmup 8 --no-cpu-baseline
             tail -1 $OUT/gloo2.log | tee $P/bench_config4_gloo2.json;;
+        proflib=*)
+            # kernel stats of the default bench on another library build (A/B of a kernel variant)
+            l=${step#proflib=}; n=$(basename $l .so)
+            ORBMI_LIB=$l run prof_$n 500 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$n -o stats -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline
+            find $OUT/prof_$n -name "*kernel_stats.csv" -exec cp {} $P/kernel_stats_$n.csv \;
+            cut -d, -f1-5 $P/kernel_stats_$n.csv | head -12;;
         prof|prof_*)
             m=${step#prof}; m=${m#_}; m=${m:-track}
             run prof_$m 500 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$m -o stats -- python3 bench.py $(modeargs $m) --steps 100 --warmup 10 --no-cpu-baseline
@@ -134,8 +142,11 @@ for step in "$@"; do
             l=${step#poselat}; l=${l#=}
             if [ -n "$l" ]; then n=$(basename $l .so); ORBMI_LIB=$l run poselat_$n 120 python tools/pose_latency.py; cat $OUT/poselat_$n.log
             else run poselat 120 python tools/pose_latency.py; cat $OUT/poselat.log; fi;;
-        greedy)
-            run greedy 120 python tools/greedy_probe.py 64; cat $OUT/greedy.log;;
+        greedy|greedy=*)
+            # k_greedy statistics and phase cycles (tools/greedy_probe.py); greedy=LIB on another build
+            l=${step#greedy}; l=${l#=}
+            if [ -n "$l" ]; then n=$(basename $l .so); ORBMI_LIB=$l run greedy_$n 120 python tools/greedy_probe.py 64; cat $OUT/greedy_$n.log
+            else run greedy 120 python tools/greedy_probe.py 64; cat $OUT/greedy.log; fi;;
         mfma_pmc)
             # MFMA A/B of the Schur products: MFMA issue / busy counters of each variant's kernel
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur

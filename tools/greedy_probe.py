@@ -41,6 +41,8 @@ def main():
     L.orbmi_debug_greedy_cycles(cyc, 0)
     print("k_greedy s_memtime cycles per call: prologue %.0f, rounds %.0f, "
           "outputs %.0f" % tuple(c / calls for c in cyc[:3]))
+    print("  rounds (thread 0): claims + barrier %.0f, evaluation %.0f, flag + barrier %.0f"
+          % tuple(c / calls for c in cyc[3:6]))
     print("result:", tr.results()["search_matches"], tr.results()["inliers"])
     tr.close()
 
