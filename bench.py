@@ -72,7 +72,9 @@ def parse():
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic_track.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
-    ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r04", "traffic_batch.json"),
+    ap.add_argument("--traffic-lba", default=os.path.join(ROOT, "profiles", "r05", "traffic_lba.json"),
+                    help="per-kernel PMC HBM bytes per launch of --mode lba (tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r05", "traffic_batch.json"),
                     help="the same for --mode batch (tools/gpu.sh pmc_batch)")
     ap.add_argument("--print-traffic-config", action="store_true",
                     help="print the workload key tools/pmc_traffic.py stores with a traffic summary, and exit")
@@ -126,6 +128,16 @@ def batch_traffic(path, config, nlevels=8):
     if per is None:
         return None
     return int(sum(v * (nlevels - 1 if k == "pyr_resize" else 1) for k, v in per.items()))
+
+
+def lba_trial_traffic(a):
+    """HBM bytes of one LocalBA LM trial (its three launches) from the --mode lba PMC summary,
+    None without it or when it was measured on another workload."""
+    per = _traffic_summary(a.traffic_lba, traffic_config(a))
+    if not per:
+        return None
+    ks = ("k_ba_schur", "k_ba_solve_mfma", "k_ba_update_errors")
+    return int(sum(per[k] for k in ks)) if all(k in per for k in ks) else None
 
 
 def read_traffic(path, name, config=None):
@@ -813,7 +825,9 @@ def run_lba(a, rank, world, local, dist):
             "iterations": list(it), "chi2": list(res["chi2"]),
             "roofline": {"kernel": "LocalBA kernel chain", "bound": "latency (3 dependent launches per LM trial: Schur, solve, update + device-side LM decision)",
                          "achieved": round(achieved, 6), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP64_PEAK_TFS, 8), "traffic": None},
+                         "frac": round(achieved / FP64_PEAK_TFS, 8), "traffic": lba_trial_traffic(a),
+                         "traffic_scope": "HBM bytes of one LM trial's launches (k_ba_schur + k_ba_solve_mfma + "
+                                          "k_ba_update_errors), " + os.path.relpath(a.traffic_lba, ROOT)},
             "cpu_baseline": cpu, "host": host_info(),
         }
     ba.close()

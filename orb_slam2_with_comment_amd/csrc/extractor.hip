@@ -1535,7 +1535,10 @@ constexpr int kDescGroups = 4;                        // keypoints per wave
 constexpr int kDescWaves = 4;                         // waves per workgroup
 constexpr int kDescKpWG = kDescGroups * kDescWaves;  // slots per workgroup step
 constexpr int kDescTargetWG = 1536;                   // workgroups per launch (3 per CU, 2 rounds)
-constexpr int kBP = 48;                               // LDS pitch: 37 bytes from any 8-B phase need 44
+#ifndef ORBMI_DESC_BP
+#define ORBMI_DESC_BP 48
+#endif
+constexpr int kBP = ORBMI_DESC_BP;                    // LDS pitch: 37 bytes from any 8-B phase need 44
 constexpr int kBQ = kBP / 8;                          // 8-B loads per window row
 constexpr int kIcItems = 224;                         // IC dwords per phase (<= 213 used): 14 per lane
 struct DescLevel { long long off, boff; int stride, bstride, out_base; float scale, size; };

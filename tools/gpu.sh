@@ -28,6 +28,7 @@
 #   solvetrace[=VAR=1]  per-step split of the reduced-system solve (tools/ubench/solve_trace)
 #   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
+#   abbatch=A,B      the same in --mode batch (config 5)
 #   descab           config 5: four keypoints per wave in k_describe vs one (ORBMI_DESC=wave)
 #   fastab           config 5: bit-sliced k_fast2 vs the per-lane k_fast (ORBMI_FAST=v1)
 #   blurab           config 5: GaussianBlur on a side stream / in the octree launch / after it
@@ -152,6 +153,14 @@ for step in "$@"; do
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur
             find $OUT/mfma_pmc -name "*counter_collection.csv" -exec cp {} $P/mfma_schur_pmc.csv \;
             cp $OUT/mfma_pmc.log $P/mfma_schur_pmc.log; tail -12 $OUT/mfma_pmc.log;;
+        abbatch=*)
+            # config-5 (batch mode) A/B of two library builds, 3 alternations, stage times kept
+            pair=${step#abbatch=}; A=${pair%,*}; B=${pair#*,}
+            for i in 1 2 3; do
+                ORBMI_LIB=$A run abb_A$i 300 python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
+                ORBMI_LIB=$B run abb_B$i 300 python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
+                echo "A $(tail -1 $OUT/abb_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_step"))')  B $(tail -1 $OUT/abb_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_step"))')" | tee -a $OUT/abbatch.txt
+            done;;
         ab=*)
             pair=${step#ab=}; A=${pair%,*}; B=${pair#*,}
             for i in 1 2 3; do
