@@ -76,6 +76,9 @@ def parse():
                     help="per-kernel PMC HBM bytes per launch of --mode lba (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r05", "traffic_batch.json"),
                     help="the same for --mode batch (tools/gpu.sh pmc_batch)")
+    ap.add_argument("--frame-events", action="store_true",
+                    help="track mode: HIP events around every timed frame's extraction and tracking (their "
+                         "overlap in the JSON line's 'overlap'; diagnostics, adds four events per frame)")
     ap.add_argument("--print-traffic-config", action="store_true",
                     help="print the workload key tools/pmc_traffic.py stores with a traffic summary, and exit")
     return ap.parse_args()
@@ -128,6 +131,26 @@ def batch_traffic(path, config, nlevels=8):
     if per is None:
         return None
     return int(sum(v * (nlevels - 1 if k == "pyr_resize" else 1) for k, v in per.items()))
+
+
+def frame_overlap(evs):
+    """Per-frame timeline from the tracker's events (--frame-events): the tracking stream's idle
+    gap before each frame, when the next frame's extraction started relative to this frame's
+    tracking start, the extraction span and the wait of tracking on it (µs, median / p90)."""
+    base = evs[0][0]
+    t = np.array([[base.elapsed_time(e) * 1e3 for e in ev] for ev in evs])  # µs from the first event
+    stats = {}
+
+    def put(name, v):
+        v = np.sort(np.asarray(v))
+        stats[name] = {"median": round(float(v[len(v) // 2]), 1), "p90": round(float(v[int(0.9 * (len(v) - 1))]), 1)}
+    put("track_span_us", t[:, 3] - t[:, 2])
+    put("track_idle_gap_us", t[1:, 2] - t[:-1, 3])
+    put("next_extract_start_after_track_start_us", t[1:, 0] - t[:-1, 2])
+    put("extract_span_us", t[:, 1] - t[:, 0])
+    put("track_start_after_extract_end_us", t[:, 2] - t[:, 1])
+    stats["frames"] = len(evs)
+    return stats
 
 
 def lba_trial_traffic(a):
@@ -405,12 +428,16 @@ def run_track(a, rank, world, local, dist):
     reset_profile(tr.extractor.handle)
     # the path's dominant kernel (rocprofv3, profiles/): PoseOptimization, bracketed with HIP
     # events on the tracking stream it is launched on
-    lib.orbmi_pose_set_profiling(tr.pose._h, 1)
+    # (every POSE_PROF_STRIDE-th launch: a timed event pair is two queue packets of ~6 µs each on
+    # the tracking stream; an odd stride alternates TrackWithMotionModel's and TrackLocalMap's)
+    lib.orbmi_pose_set_profiling(tr.pose._h, POSE_PROF_STRIDE)
     pose_prof = read_pose_profile(lib, tr.pose._h)
     sync()
     if dist:
         dist.barrier()
     sync()
+    if a.frame_events:
+        tr.frame_events = []
     t0 = time.perf_counter()
     host_s = 0.0  # time the host spends enqueueing (a host-bound step shows host ~ wall)
     for i in range(a.steps):
@@ -426,6 +453,8 @@ def run_track(a, rank, world, local, dist):
     pose_prof = read_pose_profile(lib, tr.pose._h)
     lib.orbmi_pose_set_profiling(tr.pose._h, 0)
     dt = max_over_ranks(dt, dist)
+    overlap = frame_overlap(tr.frame_events) if tr.frame_events else None
+    tr.frame_events = None
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
     x_matches = None
     if xch is not None:
@@ -469,6 +498,7 @@ def run_track(a, rank, world, local, dist):
             "kpts_desc_per_s": round(value * kp_per_frame, 1),
             "keypoints_per_frame": round(kp_per_frame, 1),
             "host_enqueue_ms_per_step_timed": round(host_s / a.steps * 1e3, 4),
+            **({"overlap": overlap} if overlap else {}),
             "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp, "inliers": outcome["inliers"],
                                   "tracking_ok": outcome["ok"]},
             "phase_ms_per_frame": {k: round(v, 4) for k, v in phases.items()},
@@ -585,6 +615,7 @@ def read_pose_profile(lib, handle):
 # algorithmic fp64 flops of PoseOptimization: per edge and edge pass
 # (computeActiveErrors + linearizeOplus + J^T W J + b) and per Levenberg trial (damped 6x6 LDL^T
 # + exponential map + step control)
+POSE_PROF_STRIDE = int(os.environ.get("ORBMI_POSE_PROF_STRIDE", "7"))  # (A/B: 1 = every launch)
 POSE_FLOPS_PER_EDGE_PASS = 300
 POSE_FLOPS_PER_TRIAL = 600
 

@@ -483,9 +483,12 @@ int orbmi_pose_share_stream(orbmi_pose* h, orbmi_extractor* ex);
 /* Run the handle on the matcher's stream instead: the tracking stages (searches, pose
  * optimisations) then form one stream that can run beside the next frame's extraction. */
 int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m);
-/* Bracket every PoseOptimization kernel launched by orbmi_pose_optimization_frame with HIP
- * events on the handle's stream (on != 0); orbmi_pose_read_profile synchronises and returns
- * the summed device time (ms) and launch count since the last read. */
+/* Bracket PoseOptimization kernels launched by orbmi_pose_optimization_frame[_track] with HIP
+ * events on the handle's stream: every launch for on == 1, every on-th launch for on > 1 (each
+ * timed event is a queue packet of a few microseconds on the stream: sampling keeps the
+ * measurement from slowing what it measures), none for on <= 0; orbmi_pose_read_profile
+ * synchronises and returns the summed device time (ms) and the number of timed launches since
+ * the last read. */
 int orbmi_pose_set_profiling(orbmi_pose* h, int on);
 int orbmi_pose_read_profile(orbmi_pose* h, double* ms, long long* launches);
 
@@ -538,6 +541,16 @@ int orbmi_search_by_projection_last_frame_if(orbmi_matcher* m, const orbmi_frame
  * counts: 2 ints, host or device (device -> asynchronous). */
 int orbmi_track_update_matches(orbmi_matcher* m, const orbmi_frame_view* F, int stage, const uint8_t* outlier,
                                const orbmi_frame_mappoints* mp, uint8_t* occupied_out, int* counts);
+
+/* orbmi_pose_optimization_frame followed by orbmi_track_update_matches(stage) on its outlier
+ * flags, in one launch on the pose handle's stream (Tracking::TrackWithMotionModel's
+ * PoseOptimization + "Discard outliers", src/Tracking.cc:1033-1058, with stage 0; TrackLocalMap's
+ * PoseOptimization + statistics, :1079-1104, with stage 1): the same results as the two calls.
+ * Every array (rec, outlier, counts, occupied_out, the match arrays and point records of mp)
+ * must be device memory: the call is asynchronous; ORBMI_E_ARG otherwise. */
+int orbmi_pose_optimization_frame_track(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
+                                        const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier,
+                                        int stage, uint8_t* occupied_out, int* counts);
 
 /* ---- LocalMapping host geometry (CreateNewMapPoints around SearchForTriangulation) ----- */
 

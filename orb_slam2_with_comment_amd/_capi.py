@@ -94,6 +94,7 @@ _PROTOS = {
     "orbmi_fuse_search_batch": (_i, [_vp, _i, _vp, _vp, _vp, _i, _f, _vp, _vp, _vp]),
     "orbmi_pose_read_profile": (_i, [_vp, _vp, _vp]),
     "orbmi_pose_optimization_frame": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbmi_pose_optimization_frame_track": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orbmi_search_by_projection_last_frame_if": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _i]),
     "orbmi_track_update_matches": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "orbmi_set_profiling": (_i, [_vp, C.c_uint]),
@@ -148,6 +149,8 @@ def lib() -> C.CDLL:
             pass
         L = C.CDLL(path)
         for name, (res, args) in _PROTOS.items():
+            if os.environ.get("ORBMI_LIB") and not hasattr(L, name):  # an A/B build may predate an entry point
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -24,6 +24,7 @@
 #include <cstring>
 
 #include "matcher.h"
+#include "track_update.h"
 #include "tri_geom.h"
 #include "wave_ops.h"
 
@@ -505,7 +506,7 @@ __device__ inline int greedy_decide(const GreedyArgs& a, const uint8_t* oct, int
 #define ORBMI_GREEDY_THREADS 1024
 #endif
 constexpr int kGreedyThreads = ORBMI_GREEDY_THREADS, kGreedyQPer = 4096 / kGreedyThreads, kGreedyPre = 4;
-constexpr int kGreedyQBits = 24, kGreedyQMask = (1 << kGreedyQBits) - 1;  // query index field of a claim
+constexpr int kGreedyQBits = 24;  // query index field of a claim
 constexpr int kGreedyMaxQueries = 1 << kGreedyQBits;
 
 // A prefix entry in a register: octave << 25 | dist << 16 | keypoint index (dist <= 256, index <
@@ -926,10 +927,8 @@ int greedy_stats(unsigned long long out[5], int reset) {
 }
 
 // -------------------------------------------------------------------------- Tracking
-// Tracking's pass over mvpMapPoints after a PoseOptimization (orbmi_track_update_matches):
-// stage 0 = TrackWithMotionModel "Discard outliers" (src/Tracking.cc:1036-1058), stage 1 =
-// TrackLocalMap statistics (src/Tracking.cc:1085-1104).  Keypoint i's point is the local map
-// point when match_mp[i] >= 0, else the last-frame point when match_lf[i] >= 0.
+// Tracking's pass over mvpMapPoints after a PoseOptimization (orbmi_track_update_matches;
+// track_update.h, which k_pose_opt also runs as its tail for orbmi_pose_optimization_frame_track)
 __global__ __launch_bounds__(1024) void k_track_update(DevFrame F, int stage, const uint8_t* __restrict__ outlier,
                                                        int* __restrict__ match_lf,
                                                        const orbmi_lastframe_point* __restrict__ lfp, int n_lf,
@@ -937,37 +936,8 @@ __global__ __launch_bounds__(1024) void k_track_update(DevFrame F, int stage, co
                                                        const orbmi_mappoint* __restrict__ mps, int n_mp,
                                                        uint8_t* __restrict__ occ_out, int* __restrict__ counts) {
     __shared__ int cnt[2];
-    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int n = frame_n(F);
-    int c0 = 0, c1 = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        int* slot = nullptr;
-        bool obs = false;
-        if (match_mp && match_mp[i] >= 0 && match_mp[i] < n_mp) {  // (out-of-range indices read as NULL)
-            slot = &match_mp[i];
-            obs = (mps[*slot].flags & ORBMI_MP_HAS_OBS) != 0;
-        } else if (match_lf && match_lf[i] >= 0 && match_lf[i] < n_lf) {
-            slot = &match_lf[i];
-            obs = (lfp[*slot].flags & ORBMI_MP_HAS_OBS) != 0;
-        }
-        bool occ = false;
-        if (slot) {
-            const bool out = outlier[i] != 0;
-            if (stage == 0) {          // :1042-1055
-                if (out) { *slot = -1; c0++; }
-                else if (obs) { c1++; occ = true; }
-            } else {                   // :1087-1101
-                if (!out) c0 += obs;
-                else { c1++; if (F.u_right) *slot = -1; }
-            }
-        }
-        if (occ_out) occ_out[i] = occ;
-    }
-    if (c0) atomicAdd(&cnt[0], c0);
-    if (c1) atomicAdd(&cnt[1], c1);
-    __syncthreads();
-    if (threadIdx.x < 2) counts[threadIdx.x] = cnt[threadIdx.x];
+    track_update_body(frame_n(F), F.u_right != nullptr, stage, outlier, match_lf, lfp, n_lf, match_mp, mps, n_mp,
+                      occ_out, counts, cnt);
 }
 
 // -------------------------------------------------------------------------- SearchByBoW

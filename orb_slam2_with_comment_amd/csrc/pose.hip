@@ -23,6 +23,7 @@
 
 #include "extractor.h"
 #include "se3_device.h"
+#include "track_update.h"
 #include "wave_ops.h"
 
 #pragma clang fp contract(fast)  // fp64 with a 1e-4 parity tolerance (as lba.hip)
@@ -43,7 +44,10 @@ constexpr int kPoseFullWaves = ORBMI_POSE_FULL_WAVES;
 constexpr int kPoseFullThreads = kPoseFullWaves * 64;
 static_assert(kPoseFullWaves >= 1 && kPoseFullWaves <= kPoseWaves, "buildSystem waves");
 constexpr int kPoseTraceWaves = 8;  // trace layout (orbmi_debug_pose_trace), whatever kPoseWaves
-constexpr int kPoseMaxObs = 4096;
+#ifndef ORBMI_POSE_MAX_OBS
+#define ORBMI_POSE_MAX_OBS 4096
+#endif
+constexpr int kPoseMaxObs = ORBMI_POSE_MAX_OBS;
 constexpr int kPoseTraceSeqs = 64;  // passes recorded by orbmi_debug_pose_trace
 constexpr int kPoseTraceWords = 16 + kPoseTraceSeqs * kPoseTraceWaves * 8;
 
@@ -365,6 +369,13 @@ struct PoseGatherArgs {
     orbmi_pose_frame* rec;
     orbmi_pose_obs* obs;
     uint8_t* outlier;       // per keypoint, zeroed here
+    // orbmi_pose_optimization_frame_track: Tracking's pass over mvpMapPoints (track_update.h)
+    // as the kernel's tail, on the keypoints' final outlier flags; upd_counts == NULL: none
+    int* upd_counts;
+    int upd_stage;
+    uint8_t* upd_occ;
+    int* upd_match_lf;      // match_lf / match_mp, which the update rewrites
+    int* upd_match_mp;
 };
 
 
@@ -391,6 +402,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     __shared__ orbmi_pose_obs sobs[kPoseMaxObs];
     __shared__ float schi[kPoseMaxObs];    // (float) chi2 of the last computeActiveErrors
     __shared__ uint8_t outl[kPoseMaxObs];  // mvbOutlier; the edge's level is the same flag
+    __shared__ uint8_t eflag[GATHER ? kPoseMaxObs : 1];  // gather: 1 = point from match_mp, 2 = Observations() > 0
     __shared__ double red[2][kPoseWaves][32];
     __shared__ double red1[2][kPoseWaves];
     __shared__ PoseCand scand[kPoseCands];  // wave 0's trial chain
@@ -407,46 +419,90 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
     if (TR && (threadIdx.x & 63) == 0 && seq < kPoseTraceSeqs) evp()[e] = __builtin_amdgcn_s_memtime();
     const int tid = threadIdx.x;
     orbmi_pose_frame& F = GATHER ? *g.rec : frames[blockIdx.x];
-    int n;
+    int n, nkp = 0;
     const orbmi_pose_obs* O = nullptr;
     float tcw0[12];
     PoseCam cam;
     if (GATHER) {  // Optimizer::PoseOptimization's edge loop (src/Optimizer.cc:296-375)
         __shared__ int gscan[kPoseWaves + 1];
-        const int nkp = g.n_dev ? min(*g.n_dev, g.n) : g.n;
+        nkp = g.n_dev ? min(*g.n_dev, g.n) : g.n;
         // each thread owns a contiguous run of keypoints: count, one block scan, then write in
         // keypoint order (2 barriers whatever the keypoint count)
         const int per = (nkp + kPoseThreads - 1) / kPoseThreads;
         const int i0 = min(tid * per, nkp), i1 = min(i0 + per, nkp);
-        auto point_of = [&](int i) -> const float* {
-            const int jm = g.match_mp ? g.match_mp[i] : -1;
-            const int jl = g.match_lf ? g.match_lf[i] : -1;
-            if (jm >= 0 && jm < g.n_mp) return g.mps[jm].pos;
-            if (jl >= 0 && jl < g.n_lf) return g.lfp[jl].pos;
-            return nullptr;
+        // the point of keypoint i: mps[match_mp[i]] if in range, else lfp[match_lf[i]] if in
+        // range (out-of-range indices read as NULL); its flags give Observations() > 0
+        struct PointRef { const float* X; uint8_t ef; };
+        auto point_ref = [&](int i, int jm, int jl) -> PointRef {
+            if (jm >= 0 && jm < g.n_mp) return {g.mps[jm].pos, (uint8_t)(1 | ((g.mps[jm].flags & ORBMI_MP_HAS_OBS) ? 2 : 0))};
+            if (jl >= 0 && jl < g.n_lf) return {g.lfp[jl].pos, (uint8_t)((g.lfp[jl].flags & ORBMI_MP_HAS_OBS) ? 2 : 0)};
+            return {nullptr, 0};
         };
-        int cnt = 0;
-        for (int i = i0; i < i1; i++) cnt += point_of(i) != nullptr;
+        auto put_edge = [&](int off, int i, const float* X, const orbmi_keypoint& kp, float ur, uint8_t ef) {
+            orbmi_pose_obs o;
+            o.Xw[0] = X[0]; o.Xw[1] = X[1]; o.Xw[2] = X[2];
+            o.u = kp.x;
+            o.v = kp.y;
+            o.ur = ur;
+            const int oct = min(max(kp.octave, 0), g.nlevels - 1);
+            o.inv_sigma2 = g.inv_sigma2[oct];
+            o.index = i;
+            sobs[off] = o;
+            outl[off] = 0;
+            eflag[off] = ef;
+        };
         int total;
-        int off = block_excl_scan(cnt, gscan, &total);
-        for (int i = i0; i < i1; i++) {
-            const float* X = point_of(i);
-            g.outlier[i] = 0;
-            if (!X) continue;
-            if (off < kPoseMaxObs) {
-                const orbmi_keypoint kp = g.keys[i];
-                orbmi_pose_obs o;
-                o.Xw[0] = X[0]; o.Xw[1] = X[1]; o.Xw[2] = X[2];
-                o.u = kp.x;
-                o.v = kp.y;
-                o.ur = g.u_right ? g.u_right[i] : -1.0f;
-                const int oct = min(max(kp.octave, 0), g.nlevels - 1);
-                o.inv_sigma2 = g.inv_sigma2[oct];
-                o.index = i;
-                sobs[off] = o;
-                outl[off] = 0;
+        constexpr int kGP = 8;  // keypoints per thread gathered with their loads in flight together
+        if (per <= kGP) {
+            // round trip 1: the match indices; round trip 2: the points, their flags and the
+            // keypoints (indices clamped into range: straight-line loads, a dependent chain per
+            // batch instead of per keypoint)
+            int jm[kGP], jl[kGP];
+#pragma unroll
+            for (int u = 0; u < kGP; u++) {
+                const int i = min(i0 + u, max(nkp - 1, 0));
+                jm[u] = (u < per && g.match_mp) ? g.match_mp[i] : -1;
+                jl[u] = (u < per && g.match_lf) ? g.match_lf[i] : -1;
             }
-            off++;
+            PointRef P[kGP];
+            float Xv[kGP][3], ur[kGP];
+            orbmi_keypoint kp[kGP];
+            int cnt = 0;
+#pragma unroll
+            for (int u = 0; u < kGP; u++) {
+                const int i = i0 + u;
+                P[u] = i < i1 ? point_ref(i, jm[u], jl[u]) : PointRef{nullptr, 0};
+                cnt += P[u].X != nullptr;
+                if (P[u].X) {
+                    Xv[u][0] = P[u].X[0]; Xv[u][1] = P[u].X[1]; Xv[u][2] = P[u].X[2];
+                    kp[u] = g.keys[i];
+                    ur[u] = g.u_right ? g.u_right[i] : -1.0f;
+                }
+            }
+            int off = block_excl_scan(cnt, gscan, &total);
+#pragma unroll
+            for (int u = 0; u < kGP; u++) {
+                const int i = i0 + u;
+                if (i >= i1) continue;
+                g.outlier[i] = 0;
+                if (!P[u].X) continue;
+                if (off < kPoseMaxObs) put_edge(off, i, Xv[u], kp[u], ur[u], P[u].ef);
+                off++;
+            }
+        } else {  // more keypoints than kGP per thread: one at a time
+            auto ref_of = [&](int i) {
+                return point_ref(i, g.match_mp ? g.match_mp[i] : -1, g.match_lf ? g.match_lf[i] : -1);
+            };
+            int cnt = 0;
+            for (int i = i0; i < i1; i++) cnt += ref_of(i).X != nullptr;
+            int off = block_excl_scan(cnt, gscan, &total);
+            for (int i = i0; i < i1; i++) {
+                const PointRef r = ref_of(i);
+                g.outlier[i] = 0;
+                if (!r.X) continue;
+                if (off < kPoseMaxObs) put_edge(off, i, r.X, g.keys[i], g.u_right ? g.u_right[i] : -1.0f, r.ef);
+                off++;
+            }
         }
         n = total;
         for (int q = 0; q < 12; q++) tcw0[q] = g.tcw_dev ? g.tcw_dev[q] : g.tcw[q];
@@ -468,177 +524,212 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(orbmi_pose_frame* __r
         if (by_index) outlier_out[GATHER ? sobs[k].index : O[k].index] = v;
         else outlier_out[F.obs_begin + k] = v;
     };
-    if (n > kPoseMaxObs) {  // sized for kPoseMaxObs edges per frame (the host path checks first)
-        if (tid == 0) { F.inliers = -1; F.iterations = 0; }
-        return;
-    }
-    if (n < 3) {  // src/Optimizer.cc:378-379: no optimisation, pose untouched
-        if (!GATHER)  // (the gather zeroed every keypoint's flag)
+    // sized for kPoseMaxObs edges per frame (the host path checks first); fewer than 3: no
+    // optimisation, pose untouched (src/Optimizer.cc:378-379; the gather zeroed every flag)
+    const bool run = n >= 3 && n <= kPoseMaxObs;
+    if (!run) {
+        if (!GATHER && n <= kPoseMaxObs)
             for (int k = tid; k < n; k += kPoseThreads) put_flag(k, 0);
-        if (tid == 0) { F.inliers = 0; F.iterations = 0; }
-        return;
+        if (tid == 0) { F.inliers = n > kPoseMaxObs ? -1 : 0; F.iterations = 0; }
     }
-    if (!GATHER)
-        for (int k = tid; k < n; k += kPoseThreads) { sobs[k] = O[k]; outl[k] = 0; }
-    double T0[8];  // Converter::toSE3Quat(pFrame->mTcw)
-    {
-        double R[3][3];
-        for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++) R[r][c] = tcw0[4 * r + c];
-        Q q = q_from_matrix(R);
-        q_normalize(q);
-        T0[0] = q.x; T0[1] = q.y; T0[2] = q.z; T0[3] = q.w;
-        T0[4] = tcw0[3]; T0[5] = tcw0[7]; T0[6] = tcw0[11]; T0[7] = 0;
-    }
-    double T[8];
-    int nBad = 0, iters = 0, rb = 0;  // rb: alternating reduction buffer
-    const int wid = tid >> 6;
-    __syncthreads();
-    for (int it = 0; it < 4; it++) {
-        const bool robust = it < 3;  // setRobustKernel(0) after the third round (:463-464)
+    if (run) {
+        if (!GATHER)
+            for (int k = tid; k < n; k += kPoseThreads) { sobs[k] = O[k]; outl[k] = 0; }
+        double T0[8];  // Converter::toSE3Quat(pFrame->mTcw)
+        {
+            double R[3][3];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) R[r][c] = tcw0[4 * r + c];
+            Q q = q_from_matrix(R);
+            q_normalize(q);
+            T0[0] = q.x; T0[1] = q.y; T0[2] = q.z; T0[3] = q.w;
+            T0[4] = tcw0[3]; T0[5] = tcw0[7]; T0[6] = tcw0[11]; T0[7] = 0;
+        }
+        double T[8];
+        int nBad = 0, iters = 0, rb = 0;  // rb: alternating reduction buffer
+        const int wid = tid >> 6;
+        __syncthreads();
+        for (int it = 0; it < 4; it++) {
+            const bool robust = it < 3;  // setRobustKernel(0) after the third round (:463-464)
 #pragma unroll
-        for (int q = 0; q < 8; q++) T[q] = T0[q];
-        double nact = 0;
-        for (int k = tid; k < n; k += kPoseThreads) nact += !outl[k];
-        nact = pose_reduce1(nact, red1[rb]);
-        rb ^= 1;
-        if (nact > 0) {
-            // ---- optimize(10) on the level-0 edges.  Every wave runs the edge passes and the
-            // Levenberg decisions (replicated: the same instructions on the same LDS values, so
-            // every wave takes the same branch).  Wave 0 holds the reduced system and publishes,
-            // in scand, the trial poses of the whole rejected-trial chain that follows it (lane j
-            // solves for the lambda after j rejections): a rejected trial needs only the chi2
-            // sum of its pass, and only an accepted trial pays for the 28-value reduction and a
-            // fresh solve.
-            double acc[28];
-            double lambda = 0, ni = 2;  // meaningful in wave 0 only
-            double currentChi = 0, iniChi = 0;
-            int cj = 0, qmax = 0, nbadIt = 0, i = 0;
-            bool first = true;  // the pass at T: computeActiveErrors + buildSystem of iteration 0
-            for (;;) {
-                bool accept = true, regen = false;
-                if (!first) {
-                    // trial cj of the chain: the pose of oplus(x(lambda_cj)), evaluated by all waves
-                    double Tt[8];
+            for (int q = 0; q < 8; q++) T[q] = T0[q];
+            double nact = 0;
+            for (int k = tid; k < n; k += kPoseThreads) nact += !outl[k];
+            nact = pose_reduce1(nact, red1[rb]);
+            rb ^= 1;
+            if (nact > 0) {
+                // ---- optimize(10) on the level-0 edges.  Every wave runs the edge passes and the
+                // Levenberg decisions (replicated: the same instructions on the same LDS values, so
+                // every wave takes the same branch).  Wave 0 holds the reduced system and publishes,
+                // in scand, the trial poses of the whole rejected-trial chain that follows it (lane j
+                // solves for the lambda after j rejections): a rejected trial needs only the chi2
+                // sum of its pass, and only an accepted trial pays for the 28-value reduction and a
+                // fresh solve.
+                double acc[28];
+                double lambda = 0, ni = 2;  // meaningful in wave 0 only
+                double currentChi = 0, iniChi = 0;
+                int cj = 0, qmax = 0, nbadIt = 0, i = 0;
+                bool first = true;  // the pass at T: computeActiveErrors + buildSystem of iteration 0
+                for (;;) {
+                    bool accept = true, regen = false;
+                    if (!first) {
+                        // trial cj of the chain: the pose of oplus(x(lambda_cj)), evaluated by all waves
+                        double Tt[8];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) Tt[q] = scand[cj].T[q];
-                    const bool ok2 = scand[cj].ok != 0;
-                    const double scale = scand[cj].scale;
-                    seq++;
-                    EV(0);
-                    {
-                        const double c = wave_sum(pose_chi_pass(Tt, cam, sobs, outl, schi, n, robust));
-                        EV(1);
-                        if ((tid & 63) == 0) chiw[cb][wid] = c;
-                    }
-                    __syncthreads();  // B1: the trial's chi2 partials
-                    EV(2);
-                    double tempChi = 0;
-#pragma unroll
-                    for (int w = 0; w < kPoseWaves; w++) tempChi += chiw[cb][w];
-                    cb ^= 1;
-                    if (!ok2) tempChi = DBL_MAX;
-                    const double rho = (currentChi - tempChi) * fast_rcp(scale + 1e-3);
-                    accept = rho > 0 && isfinite(tempChi);
-                    if (accept) {
-                        const double t = 2 * rho - 1;
-                        double alpha = 1. - t * t * t;
-                        alpha = fmin(alpha, 2. / 3.);
-                        lambda *= fmax(1. / 3., alpha);
-                        ni = 2;
-                        currentChi = tempChi;
-#pragma unroll
-                        for (int q = 0; q < 8; q++) T[q] = Tt[q];
-                    } else {
-                        lambda *= ni;
-                        ni *= 2;
-                        cj++;
-                    }
-                    qmax++;
-                    bool done = false;
-                    if (!(rho < 0 && qmax < 10)) {  // the do-while of iteration i ends
-                        iters++;
-                        if (qmax == 10 || rho == 0) done = true;
-                        else {
-                            if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
-                            else nbadIt = 0;
-                            if (nbadIt >= 3 || ++i >= 10) done = true;
-                            iniChi = currentChi;
-                            qmax = 0;
+                        for (int q = 0; q < 8; q++) Tt[q] = scand[cj].T[q];
+                        const bool ok2 = scand[cj].ok != 0;
+                        const double scale = scand[cj].scale;
+                        seq++;
+                        EV(0);
+                        {
+                            const double c = wave_sum(pose_chi_pass(Tt, cam, sobs, outl, schi, n, robust));
+                            EV(1);
+                            if ((tid & 63) == 0) chiw[cb][wid] = c;
                         }
+                        __syncthreads();  // B1: the trial's chi2 partials
+                        EV(2);
+                        double tempChi = 0;
+#pragma unroll
+                        for (int w = 0; w < kPoseWaves; w++) tempChi += chiw[cb][w];
+                        cb ^= 1;
+                        if (!ok2) tempChi = DBL_MAX;
+                        const double rho = (currentChi - tempChi) * fast_rcp(scale + 1e-3);
+                        accept = rho > 0 && isfinite(tempChi);
+                        if (accept) {
+                            const double t = 2 * rho - 1;
+                            double alpha = 1. - t * t * t;
+                            alpha = fmin(alpha, 2. / 3.);
+                            lambda *= fmax(1. / 3., alpha);
+                            ni = 2;
+                            currentChi = tempChi;
+#pragma unroll
+                            for (int q = 0; q < 8; q++) T[q] = Tt[q];
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                            cj++;
+                        }
+                        qmax++;
+                        bool done = false;
+                        if (!(rho < 0 && qmax < 10)) {  // the do-while of iteration i ends
+                            iters++;
+                            if (qmax == 10 || rho == 0) done = true;
+                            else {
+                                if ((iniChi - currentChi) * 1e3 < iniChi) nbadIt++;
+                                else nbadIt = 0;
+                                if (nbadIt >= 3 || ++i >= 10) done = true;
+                                iniChi = currentChi;
+                                qmax = 0;
+                            }
+                        }
+                        EV(3);
+                        if (done) break;
+                        regen = !accept && cj == kPoseCands;  // chain exhausted: continue it
                     }
-                    EV(3);
-                    if (done) break;
-                    regen = !accept && cj == kPoseCands;  // chain exhausted: continue it
-                }
-                if (accept || regen) {
-                    if (accept) {  // buildSystem at the (new) estimate: the first iteration's, or
-                                   // the next iteration's after an accepted trial
-                        pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
-                        EV(7);
-                        pose_reduce28_w0(acc, red[rb], stot);  // B2 inside
-                        rb ^= 1;
-                    } else {
-                        __syncthreads();  // every wave has read scand
+                    if (accept || regen) {
+                        if (accept) {  // buildSystem at the (new) estimate: the first iteration's, or
+                                       // the next iteration's after an accepted trial
+                            pose_pass(T, cam, sobs, outl, schi, n, robust, acc);
+                            EV(7);
+                            pose_reduce28_w0(acc, red[rb], stot);  // B2 inside
+                            rb ^= 1;
+                        } else {
+                            __syncthreads();  // every wave has read scand
+                            if (wid == 0) {
+#pragma unroll
+                                for (int q = 0; q < 28; q++) acc[q] = stot[q];
+                            }
+                        }
+                        EV(4);
                         if (wid == 0) {
-#pragma unroll
-                            for (int q = 0; q < 28; q++) acc[q] = stot[q];
+                            if (first)  // computeLambdaInit, tau = 1e-5
+                                lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
+                                                     fmax(fabs(acc[18]), fabs(acc[20])));
+                            pose_candidates(acc, lambda, ni, T, scand);
+                            EV(5);
                         }
-                    }
-                    EV(4);
-                    if (wid == 0) {
-                        if (first)  // computeLambdaInit, tau = 1e-5
-                            lambda = 1e-5 * fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
-                                                 fmax(fabs(acc[18]), fabs(acc[20])));
-                        pose_candidates(acc, lambda, ni, T, scand);
-                        EV(5);
-                    }
-                    cj = 0;
-                    __syncthreads();  // B3: the trial chain published
-                    EV(6);
-                    if (first) {
-                        currentChi = iniChi = stot[27];
-                        first = false;
+                        cj = 0;
+                        __syncthreads();  // B3: the trial chain published
+                        EV(6);
+                        if (first) {
+                            currentChi = iniChi = stot[27];
+                            first = false;
+                        }
                     }
                 }
             }
-        }
-        // ---- outlier classification (:418-466): stale errors of the inliers, fresh ones of the
-        // outliers, chi2 compared in float
-        double bad = 0;
-        for (int k = tid; k < n; k += kPoseThreads) {
-            const orbmi_pose_obs o = sobs[k];
-            float c2 = schi[k];
-            if (outl[k]) {
-                double p[3], invz, e[3];
-                pose_error(T, cam, o, p, invz, e);
-                c2 = (float)pose_chi2(o, e);
-                schi[k] = c2;
+            // ---- outlier classification (:418-466): stale errors of the inliers, fresh ones of the
+            // outliers, chi2 compared in float
+            double bad = 0;
+            for (int k = tid; k < n; k += kPoseThreads) {
+                const orbmi_pose_obs o = sobs[k];
+                float c2 = schi[k];
+                if (outl[k]) {
+                    double p[3], invz, e[3];
+                    pose_error(T, cam, o, p, invz, e);
+                    c2 = (float)pose_chi2(o, e);
+                    schi[k] = c2;
+                }
+                const bool out = c2 > (o.ur < 0 ? 5.991f : 7.815f);
+                outl[k] = out;
+                bad += out;
             }
-            const bool out = c2 > (o.ur < 0 ? 5.991f : 7.815f);
-            outl[k] = out;
-            bad += out;
+            nBad = (int)pose_reduce1(bad, red1[rb]);
+            rb ^= 1;
+            if (n < 10) break;  // optimizer.edges().size() < 10
         }
-        nBad = (int)pose_reduce1(bad, red1[rb]);
-        rb ^= 1;
-        if (n < 10) break;  // optimizer.edges().size() < 10
-    }
-    for (int k = tid; k < n; k += kPoseThreads) put_flag(k, outl[k]);
-    if (tid == 0) {  // Converter::toCvMat(SE3quat_recov)
-        double R[3][3];
-        q_to_matrix(load_q(T), R);
-        for (int r = 0; r < 3; r++) {
-            for (int c = 0; c < 3; c++) F.tcw[4 * r + c] = (float)R[r][c];
-            F.tcw[4 * r + 3] = (float)T[4 + r];
+        for (int k = tid; k < n; k += kPoseThreads) put_flag(k, outl[k]);
+        if (tid == 0) {  // Converter::toCvMat(SE3quat_recov)
+            double R[3][3];
+            q_to_matrix(load_q(T), R);
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) F.tcw[4 * r + c] = (float)R[r][c];
+                F.tcw[4 * r + 3] = (float)T[4 + r];
+            }
+            F.tcw[12] = 0; F.tcw[13] = 0; F.tcw[14] = 0; F.tcw[15] = 1;
+            F.inliers = n - nBad;
+            F.iterations = iters;
         }
-        F.tcw[12] = 0; F.tcw[13] = 0; F.tcw[14] = 0; F.tcw[15] = 1;
-        F.inliers = n - nBad;
-        F.iterations = iters;
-    }
-    if (TR && tid == 0) {
-        trace[0] = __builtin_amdgcn_s_memtime() - tstart;
-        trace[1] = __builtin_amdgcn_s_memrealtime() - rstart;
-        trace[2] = seq;
+        if (TR && tid == 0) {
+            trace[0] = __builtin_amdgcn_s_memtime() - tstart;
+            trace[1] = __builtin_amdgcn_s_memrealtime() - rstart;
+            trace[2] = seq;
+        }
+    }  // run
+    if (GATHER && g.upd_counts) {  // Tracking's pass over mvpMapPoints (track_update.h) on the final flags
+        __shared__ int ucnt[2];
+        if (n <= kPoseMaxObs) {
+            // from the edges in LDS: keypoint, final mvbOutlier, which match array holds the point
+            // and its Observations() > 0 (eflag), so no global load; keypoints without a point
+            // only get occupied_out = 0 (zeroed first, then the edges' values)
+            if (tid < 2) ucnt[tid] = 0;
+            if (g.upd_occ)
+                for (int i = tid; i < nkp; i += kPoseThreads) g.upd_occ[i] = 0;
+            __syncthreads();
+            const bool stereo = g.u_right != nullptr;
+            int c0 = 0, c1 = 0;
+            for (int k = tid; k < n; k += kPoseThreads) {
+                const int i = sobs[k].index;
+                const uint8_t ef = eflag[k];
+                const bool out = outl[k] != 0, obs = (ef & 2) != 0;
+                int* slot = (ef & 1) ? &g.upd_match_mp[i] : &g.upd_match_lf[i];
+                if (g.upd_stage == 0) {  // src/Tracking.cc:1042-1055
+                    if (out) { *slot = -1; c0++; }
+                    else if (obs) { c1++; if (g.upd_occ) g.upd_occ[i] = 1; }
+                } else {                 // :1087-1101
+                    if (!out) c0 += obs;
+                    else { c1++; if (stereo) *slot = -1; }
+                }
+            }
+            if (c0) atomicAdd(&ucnt[0], c0);
+            if (c1) atomicAdd(&ucnt[1], c1);
+            __syncthreads();
+            if (tid < 2) g.upd_counts[tid] = ucnt[tid];
+        } else {  // (more edges than LDS holds: the keypoint form)
+            __syncthreads();
+            track_update_body(nkp, g.u_right != nullptr, g.upd_stage, g.outlier, g.upd_match_lf, g.lfp, g.n_lf,
+                              g.upd_match_mp, g.mps, g.n_mp, g.upd_occ, g.upd_counts, ucnt);
+        }
     }
 #undef EV
 }
@@ -713,8 +804,9 @@ struct orbmi_pose {
     size_t cap_obs = 0;
     uint8_t* d_stage = nullptr;
     size_t cap_stage = 0, used_stage = 0;
-    // orbmi_pose_set_profiling: HIP event pairs around every k_pose_opt launch
-    bool profiling = false;
+    // orbmi_pose_set_profiling: HIP event pairs around every stride-th k_pose_opt launch
+    int prof_stride = 0;
+    long long prof_seq = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t used_events = 0;
 };
@@ -802,7 +894,8 @@ int orbmi_pose_share_matcher_stream(orbmi_pose* h, orbmi_matcher* m) {
 
 int orbmi_pose_set_profiling(orbmi_pose* h, int on) {
     if (!h) return ORBMI_E_ARG;
-    h->profiling = on != 0;
+    h->prof_stride = on > 0 ? on : 0;
+    h->prof_seq = 0;
     return ORBMI_OK;
 }
 
@@ -871,8 +964,15 @@ int orbmi_pose_optimization(orbmi_pose* h, orbmi_pose_frame* frames, int nframes
     return ORBMI_OK;
 }
 
-int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
-                                  const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier) {
+}  // extern "C"
+
+namespace {
+
+// Tracking's update pass fused into the launch (orbmi_pose_optimization_frame_track)
+struct TrackUpd { int stage; uint8_t* occ; int* counts; };
+
+int pose_frame(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2, const orbmi_frame_mappoints* mp,
+               orbmi_pose_frame* rec, uint8_t* outlier, const TrackUpd* upd) {
     using namespace orbmi;
     if (!h || !F || !inv_level_sigma2 || !mp || !rec || !outlier || F->n < 0 || !F->tcw) return ORBMI_E_ARG;
     if (F->nlevels < 1 || F->nlevels > kMaxLevels || (F->n > 0 && !F->keys_un)) return ORBMI_E_ARG;
@@ -939,8 +1039,15 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     a.rec = (orbmi_pose_frame*)dev_out(rec, sizeof(orbmi_pose_frame));
     a.obs = h->d_obs;
     a.outlier = (uint8_t*)dev_out(outlier, n);
+    if (upd) {  // device arrays only (checked by the caller): the update rewrites them in place
+        a.upd_counts = upd->counts;
+        a.upd_stage = upd->stage;
+        a.upd_occ = upd->occ;
+        a.upd_match_lf = const_cast<int*>(a.match_lf);
+        a.upd_match_mp = const_cast<int*>(a.match_mp);
+    }
     if (rc) return rc;
-    auto* ev = h->profiling ? next_events(h) : nullptr;
+    auto* ev = (h->prof_stride > 0 && h->prof_seq++ % h->prof_stride == 0) ? next_events(h) : nullptr;
     if (ev) ORBMI_HIP(hipEventRecord(ev->first, h->stream));
     // edge assembly fused into the optimiser's prologue (k_pose_gather is the standalone form)
     hipLaunchKernelGGL((k_pose_opt<false, true>), dim3(1), dim3(kPoseThreads), 0, h->stream, a.rec,
@@ -956,6 +1063,29 @@ int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, cons
     h->used_stage = 0;
     if (rec->inliers < 0) return ORBMI_E_UNSUPPORTED;  // more than kPoseMaxObs edges
     return ORBMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbmi_pose_optimization_frame(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
+                                  const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier) {
+    return pose_frame(h, F, inv_level_sigma2, mp, rec, outlier, nullptr);
+}
+
+int orbmi_pose_optimization_frame_track(orbmi_pose* h, const orbmi_frame_view* F, const float* inv_level_sigma2,
+                                        const orbmi_frame_mappoints* mp, orbmi_pose_frame* rec, uint8_t* outlier,
+                                        int stage, uint8_t* occupied_out, int* counts) {
+    if (!h || !mp || !counts || (stage != 0 && stage != 1)) return ORBMI_E_ARG;
+    // one asynchronous launch: every array it reads or writes lives on the device
+    auto dev = [](const void* p) { return !p || is_device_ptr(p); };
+    if (!is_device_ptr(rec) || !is_device_ptr(outlier) || !is_device_ptr(counts) || !dev(occupied_out) ||
+        !dev(mp->match_lf) || !dev(mp->match_mp) || (mp->match_lf && !dev(mp->lf_points)) ||
+        (mp->match_mp && !dev(mp->mps)))
+        return ORBMI_E_ARG;
+    const TrackUpd u{stage, occupied_out, counts};
+    return pose_frame(h, F, inv_level_sigma2, mp, rec, outlier, &u);
 }
 
 // debug: one traced launch of the pose kernel on device arrays (include/orbmi_debug.h)

@@ -106,6 +106,17 @@ class PoseOptimizer:
                                                   rp, op))
         return int(np.asarray(rec["inliers"]).reshape(-1)[0]) if host else None
 
+    def PoseOptimizationTrack(self, view, inv_level_sigma2: np.ndarray, mappoints, rec: int, outlier: int, stage: int,
+                              occupied_out, counts: int):
+        """PoseOptimization followed by Tracking's pass over mvpMapPoints (orbmi_track_update_matches
+        `stage`: 0 = TrackWithMotionModel's outlier discard, 1 = TrackLocalMap's statistics) in one
+        launch; every address is device memory, enqueued on the handle's stream."""
+        sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        check("orbmi_pose_optimization_frame_track",
+              lib().orbmi_pose_optimization_frame_track(self._h, C.addressof(view), sig.ctypes.data,
+                                                        C.addressof(mappoints), rec, outlier, int(stage),
+                                                        occupied_out, counts))
+
 
 # ---- minimal map model for the graph assembly (src/Optimizer.cc:486-534) ------------------
 @dataclasses.dataclass(eq=False)

@@ -80,6 +80,8 @@ class StereoTracker:
         from .orb import ORBextractor
         from .types import POSE_FRAME_DTYPE
         self.cam, self.device, self.pipelined = cam, device, pipelined
+        self.unfused = os.environ.get("ORBMI_TRACK_UNFUSED") == "1"  # A/B: pose and update as two launches
+        self.frame_events = None  # a list: per-frame [extract start, end, track start, end] events (pipelined)
         self.extractor = ORBextractor(nfeatures, scale_factor, nlevels, ini_th, min_th, device=device)
         self.matcher = ORBmatcher(device=device)
         self.pose = PoseOptimizer(device)
@@ -196,10 +198,7 @@ class StereoTracker:
             check("orbmi_search_by_projection_last_frame_if", L.orbmi_search_by_projection_last_frame_if(
                 self.matcher._h, C.addressof(cv), _vp(self.no_points.data_ptr()), C.addressof(last_view),
                 _vp(last_points), t, 0, 1, _vp(self.match_lf.data_ptr()), _vp(self.tcounts.data_ptr()), gate))
-        self.pose.PoseOptimization(cv, self.inv_sigma2, mp, self.rec_tcw(0), self.outlier.data_ptr())
-        check("orbmi_track_update_matches", L.orbmi_track_update_matches(
-            self.matcher._h, C.addressof(cv), 0, _vp(self.outlier.data_ptr()), C.addressof(mp),
-            _vp(self.occupied.data_ptr()), _vp(self.tcounts.data_ptr() + 4)))
+        self._pose_and_update(cv, mp, 0, 0, self.occupied.data_ptr(), self.tcounts.data_ptr() + 4)
 
     def track_local_map(self, last_view, last_points, local_mps, n_mp, th=1.0):
         """Tracking::TrackLocalMap (src/Tracking.cc:1065-1104) at pose record 0: SearchLocalPoints,
@@ -210,10 +209,20 @@ class StereoTracker:
             self.matcher._h, C.addressof(cv), _vp(self.occupied.data_ptr()), _vp(local_mps), int(n_mp), th,
             _vp(self.match_mp.data_ptr()), None, None))
         mp = self.frame_mappoints(last_view, last_points, local_mps, n_mp)
-        self.pose.PoseOptimization(cv, self.inv_sigma2, mp, self.rec_tcw(1), self.outlier.data_ptr())
-        check("orbmi_track_update_matches", L.orbmi_track_update_matches(
-            self.matcher._h, C.addressof(cv), 1, _vp(self.outlier.data_ptr()), C.addressof(mp), None,
-            _vp(self.tcounts.data_ptr() + 12)))
+        self._pose_and_update(cv, mp, 1, 1, None, self.tcounts.data_ptr() + 12)
+
+    def _pose_and_update(self, cv, mp, rec, stage, occupied, counts):
+        """PoseOptimization -> pose record `rec`, then Tracking's pass over mvpMapPoints (stage 0:
+        TrackWithMotionModel's outlier discard, 1: TrackLocalMap's statistics), as one launch
+        (orbmi_pose_optimization_frame_track); ORBMI_TRACK_UNFUSED=1 issues the two calls."""
+        if not self.unfused:
+            self.pose.PoseOptimizationTrack(cv, self.inv_sigma2, mp, self.rec_tcw(rec), self.outlier.data_ptr(), stage,
+                                            occupied, counts)
+            return
+        self.pose.PoseOptimization(cv, self.inv_sigma2, mp, self.rec_tcw(rec), self.outlier.data_ptr())
+        check("orbmi_track_update_matches", lib().orbmi_track_update_matches(
+            self.matcher._h, C.addressof(cv), stage, _vp(self.outlier.data_ptr()), C.addressof(mp), _vp(occupied),
+            _vp(counts)))
 
     def frame_mappoints(self, last_view, last_points, local_mps, n_mp):
         from .types import FrameMapPoints
@@ -239,13 +248,25 @@ class StereoTracker:
         for ev in self._holds[s]:  # ... and read by every other consumer (hold_slot)
             self._E.wait_event(ev)
         self._holds[s].clear()
+        fe = self.frame_events
+        if fe is not None:  # diagnostics: extraction / tracking start and end on their streams
+            import torch
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(self._E)
         self.extract_stereo(d_left_right, rows, cols, slot=s)
         self._ev_extracted[s].record(self._E)
+        if fe is not None:
+            ev[1].record(self._E)
         self._T.wait_event(self._ev_extracted[s])
+        if fe is not None:
+            ev[2].record(self._T)
         self.slot = s
         self.track_with_motion_model(tcw, last_view, last_points, th_lf)
         self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
         self._ev_tracked[s].record(self._T)
+        if fe is not None:
+            ev[3].record(self._T)
+            fe.append(ev)
         self._pending[s] = True
 
     def hold_slot(self, stream):

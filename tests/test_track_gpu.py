@@ -152,3 +152,26 @@ def test_track_chain_retry_and_lost(oracle):
         if ok:
             assert np.abs(res["tcw"] - ref["tcw"]).max() <= POSE_TOL
         tr.close()
+
+
+@pytest.mark.parametrize("f", [4, 7])
+def test_track_fused_update_equals_two_launches(f):
+    """orbmi_pose_optimization_frame_track (PoseOptimization with Tracking's update pass as its
+    tail, the tracker's default) against the two launches it replaces (ORBMI_TRACK_UNFUSED):
+    pose records, outlier flags, match arrays, occupancy and counts byte-identical."""
+    out = []
+    for unfused in (False, True):
+        tr, d, tcw, lf, lfp, mps, cf = _setup(f)
+        tr.unfused = unfused
+        cam = cf.cam
+        lv = lf.view()
+        tr.extract_stereo(d["imgs"].data_ptr(), cam.height, cam.width)
+        tr.track_with_motion_model(tcw, lv, d["lfp"].data_ptr())
+        tr.track_local_map(lv, d["lfp"].data_ptr(), d["mps"].data_ptr(), len(mps))
+        tr.synchronize()
+        n = len(cf.keys)
+        out.append({k: getattr(tr, k)[:n].cpu().numpy().copy() for k in ("match_lf", "match_mp", "outlier", "occupied")}
+                   | {"tcounts": tr.tcounts.cpu().numpy().copy(), "recs": tr.recs.cpu().numpy().copy()})
+        tr.close()
+    for k in out[0]:
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)

@@ -16,6 +16,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the default bench
 #   prof_MODE        the same for --mode MODE
 #   proflib=LIB      the default bench's kernel stats on another library build
+#   hiptrace         kernel + HIP API trace of a short default bench
 #   sqpmc[_MODE]     two SQ counter passes (waves, issue, LDS, VMEM) -> per-kernel means
 #   poselat[=LIB]    tools/pose_latency.py (PoseOptimization latency), optionally on another build
 #   greedy[=LIB]     tools/greedy_probe.py (k_greedy rounds and phase cycles), optionally on another build
@@ -29,6 +30,7 @@
 #   mfma_pmc         MFMA counters of tools/ubench/mfma_schur (build it first)
 #   ab=A,B           bench A/B of two library builds (ORBMI_LIB paths), 3 alternations
 #   abbatch=A,B      the same in --mode batch (config 5)
+#   envab=VAR=VALUE  the default bench without / with an environment knob, 3 alternations
 #   descab           config 5: four keypoints per wave in k_describe vs one (ORBMI_DESC=wave)
 #   fastab           config 5: bit-sliced k_fast2 vs the per-lane k_fast (ORBMI_FAST=v1)
 #   blurab           config 5: GaussianBlur on a side stream / in the octree launch / after it
@@ -82,6 +84,10 @@ for step in "$@"; do
         gloo2)
             run gloo2 500 python bench.py --gpus 2 --dist-backend gloo --steps 40 --warmup 8 --no-cpu-baseline
             tail -1 $OUT/gloo2.log | tee $P/bench_config4_gloo2.json;;
+        hiptrace)
+            # kernel trace + HIP API trace of a short default bench (host enqueue vs GPU timeline)
+            run hiptrace 300 rocprofv3 --kernel-trace --hip-trace -f csv -d $OUT/hiptrace -o ht -- python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline
+            find $OUT/hiptrace -name "*.csv" | head;;
         proflib=*)
             # kernel stats of the default bench on another library build (A/B of a kernel variant)
             l=${step#proflib=}; n=$(basename $l .so)
@@ -153,6 +159,14 @@ for step in "$@"; do
             run mfma_pmc 90 timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -f csv -d $OUT/mfma_pmc -o mfma -- ./tools/ubench/mfma_schur
             find $OUT/mfma_pmc -name "*counter_collection.csv" -exec cp {} $P/mfma_schur_pmc.csv \;
             cp $OUT/mfma_pmc.log $P/mfma_schur_pmc.log; tail -12 $OUT/mfma_pmc.log;;
+        envab=*)
+            # default bench with / without an environment knob (VAR=VALUE), 3 alternations
+            kv=${step#envab=}
+            for i in 1 2 3; do
+                run envab_A$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+                run envab_B$i 300 env $kv python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+                echo "default $(tail -1 $OUT/envab_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["phase_ms_per_frame"])')  $kv $(tail -1 $OUT/envab_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["phase_ms_per_frame"])')" | tee -a $OUT/envab.txt
+            done;;
         abbatch=*)
             # config-5 (batch mode) A/B of two library builds, 3 alternations, stage times kept
             pair=${step#abbatch=}; A=${pair%,*}; B=${pair#*,}
