@@ -296,6 +296,15 @@ struct orbmi_slam {
     // pinned, so the copies are plain DMA.
     struct TrackBuf {
         size_t cap_kp = 0, cap_lf = 0, cap_rec = 0;
+        // One device arena and its pinned host mirror, laid out so that each tracking stage moves
+        // its inputs in one upload and its results in one read-back (every copy is a queue
+        // packet of several microseconds on the stream):
+        //   rec | mlf | occ | lfp | n | pose | out | m | tr
+        // TrackWithMotionModel uploads occ .. n (n zeroed: the first search's gate) and reads
+        // n .. m; TrackLocalMap uploads rec .. lfp and reads n .. tr.
+        uint8_t* d_arena = nullptr;
+        uint8_t* h_arena = nullptr;
+        size_t arena_bytes = 0;
         // device
         orbmi_lastframe_point* d_lfp = nullptr;  // TWMM: the last frame's points / TLM: the current frame's
         orbmi_mappoint* d_rec = nullptr;         // TLM: the local map points
@@ -319,65 +328,71 @@ struct orbmi_slam {
     } tb;
     hipStream_t tstream = nullptr;  // the tracking stream (the matcher's)
 
-    template <class T>
-    static int grow(T** d, T** h, size_t n) {  // device + pinned host arrays of n elements (contents dropped)
-        if (*d) (void)hipFree(*d);
-        if (*h) (void)hipHostFree(*h);
-        *d = nullptr;
-        *h = nullptr;
-        if (hipMalloc((void**)d, n * sizeof(T)) != hipSuccess) return ORBMI_E_HIP;
-        if (hipHostMalloc((void**)h, n * sizeof(T), hipHostMallocDefault) != hipSuccess) return ORBMI_E_HIP;
-        return ORBMI_OK;
-    }
     int track_buffers(size_t nkp, size_t nlf, size_t nrec) {
         nkp = std::max<size_t>(nkp, 1);
         nlf = std::max<size_t>(nlf, 1);
         nrec = std::max<size_t>(nrec, 1);
         TrackBuf& t = tb;
-        if (nkp > t.cap_kp) {
-            const size_t c = nkp + nkp / 4;
-            SLAM_CHECK(grow(&t.d_m, &t.h_m, c));
-            SLAM_CHECK(grow(&t.d_mlf, &t.h_mlf, c));
-            SLAM_CHECK(grow(&t.d_occ, &t.h_occ, c));
-            SLAM_CHECK(grow(&t.d_out, &t.h_out, c));
-            t.cap_kp = c;
+        if (nkp <= t.cap_kp && nlf <= t.cap_lf && nrec <= t.cap_rec && t.d_arena) return ORBMI_OK;
+        if (nkp > t.cap_kp) t.cap_kp = nkp + nkp / 4;
+        if (nlf > t.cap_lf) t.cap_lf = nlf + nlf / 4;
+        if (nrec > t.cap_rec) t.cap_rec = nrec + nrec / 4;
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        size_t off = 0;
+        auto take = [&](size_t bytes) { const size_t o = off; off += al(bytes); return o; };
+        const size_t o_rec = take(t.cap_rec * sizeof(orbmi_mappoint)), o_mlf = take(t.cap_kp * 4), o_occ = take(t.cap_kp);
+        const size_t o_lfp = off;  // (no padding between lfp and n: TWMM's upload ends right after n)
+        off += t.cap_lf * sizeof(orbmi_lastframe_point);
+        off = (off + 15) & ~(size_t)15;
+        const size_t o_n = take(2 * sizeof(int)), o_pose = take(sizeof(orbmi_pose_frame)), o_out = take(t.cap_kp),
+                     o_m = take(t.cap_kp * 4), o_tr = take(t.cap_rec * sizeof(orbmi_mappoint_track));
+        if (off > t.arena_bytes) {
+            if (t.d_arena) (void)hipFree(t.d_arena);
+            if (t.h_arena) (void)hipHostFree(t.h_arena);
+            t.d_arena = t.h_arena = nullptr;
+            t.arena_bytes = 0;
+            if (hipMalloc((void**)&t.d_arena, off) != hipSuccess) return ORBMI_E_HIP;
+            if (hipHostMalloc((void**)&t.h_arena, off, hipHostMallocDefault) != hipSuccess) return ORBMI_E_HIP;
+            t.arena_bytes = off;
         }
-        if (nlf > t.cap_lf) {
-            const size_t c = nlf + nlf / 4;
-            SLAM_CHECK(grow(&t.d_lfp, &t.h_lfp, c));
-            t.cap_lf = c;
-        }
-        if (nrec > t.cap_rec) {
-            const size_t c = nrec + nrec / 4;
-            SLAM_CHECK(grow(&t.d_rec, &t.h_rec, c));
-            SLAM_CHECK(grow(&t.d_tr, &t.h_tr, c));
-            t.cap_rec = c;
-        }
-        if (!t.d_n) {
-            SLAM_CHECK(grow(&t.d_n, &t.h_n, 2));
-            SLAM_CHECK(grow(&t.d_pose, &t.h_pose, 1));
+        auto at = [&](uint8_t* base, size_t o) { return (void*)(base + o); };
+        for (int side = 0; side < 2; side++) {
+            uint8_t* B = side ? t.h_arena : t.d_arena;
+            auto& rec = side ? t.h_rec : t.d_rec;
+            auto& mlf = side ? t.h_mlf : t.d_mlf;
+            auto& occ = side ? t.h_occ : t.d_occ;
+            auto& lfp = side ? t.h_lfp : t.d_lfp;
+            auto& n = side ? t.h_n : t.d_n;
+            auto& pose = side ? t.h_pose : t.d_pose;
+            auto& out = side ? t.h_out : t.d_out;
+            auto& m = side ? t.h_m : t.d_m;
+            auto& tr = side ? t.h_tr : t.d_tr;
+            rec = (orbmi_mappoint*)at(B, o_rec);
+            mlf = (int32_t*)at(B, o_mlf);
+            occ = (uint8_t*)at(B, o_occ);
+            lfp = (orbmi_lastframe_point*)at(B, o_lfp);
+            n = (int*)at(B, o_n);
+            pose = (orbmi_pose_frame*)at(B, o_pose);
+            out = (uint8_t*)at(B, o_out);
+            m = (int32_t*)at(B, o_m);
+            tr = (orbmi_mappoint_track*)at(B, o_tr);
         }
         return ORBMI_OK;
     }
     void free_track_buffers() {
         TrackBuf& t = tb;
-        void* d[] = {t.d_lfp, t.d_rec, t.d_tr, t.d_m, t.d_mlf, t.d_occ, t.d_out, t.d_n, t.d_pose};
-        void* h[] = {t.h_lfp, t.h_rec, t.h_tr, t.h_m, t.h_mlf, t.h_occ, t.h_out, t.h_n, t.h_pose};
-        for (void* x : d)
-            if (x) (void)hipFree(x);
-        for (void* x : h)
-            if (x) (void)hipHostFree(x);
+        if (t.d_arena) (void)hipFree(t.d_arena);
+        if (t.h_arena) (void)hipHostFree(t.h_arena);
         tb = TrackBuf{};
     }
-    template <class T>
-    int up(T* d, const T* h, size_t n) {
-        if (!n) return ORBMI_OK;
-        return hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+    // one contiguous copy of the arena's host bytes [from, to) up, or device bytes down
+    int up_range(const void* from, const void* to) {
+        const size_t o = (const uint8_t*)from - tb.h_arena, n = (const uint8_t*)to - (const uint8_t*)from;
+        return hipMemcpyAsync(tb.d_arena + o, from, n, hipMemcpyHostToDevice, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
     }
-    template <class T>
-    int down(T* h, const T* d, size_t n) {
-        if (!n) return ORBMI_OK;
-        return hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
+    int down_range(void* from, const void* to) {
+        const size_t o = (uint8_t*)from - tb.h_arena, n = (const uint8_t*)to - (uint8_t*)from;
+        return hipMemcpyAsync(from, tb.d_arena + o, n, hipMemcpyDeviceToHost, tstream) == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
     }
     double phase_ms[PH_COUNT] = {};
     long phase_frames = 0;
@@ -1976,10 +1991,9 @@ struct orbmi_slam {
         SLAM_CHECK(track_buffers(nc, nl, 0));
         TrackBuf& t = tb;
         lf_records_into(lf.mps, &lf.outlier, t.h_lfp);
-        SLAM_CHECK(up(t.d_lfp, t.h_lfp, nl));
-        if (hipMemsetAsync(t.d_occ, 0, std::max(nc, 1), tstream) != hipSuccess ||
-            hipMemsetAsync(t.d_n, 0, sizeof(int), tstream) != hipSuccess)
-            return ORBMI_E_HIP;
+        std::memset(t.h_occ, 0, (size_t)std::max(nc, 1));
+        *t.h_n = 0;
+        SLAM_CHECK(up_range(t.h_occ, t.h_n + 1));  // occ, the last frame's points, n = 0
         const orbmi_frame_view vc = view(cf, cf.tcw.data()), vl = view(lf, lf.tcw.data());
         const float th = 7.f;  // stereo (src/Tracking.cc:1011-1014)
         orbmi_frame_mappoints fm{};
@@ -1994,10 +2008,7 @@ struct orbmi_slam {
                 if (!rc) rc = orbmi_search_by_projection_last_frame_if(matcher, &vc, t.d_occ, &vl, t.d_lfp, 2 * th, 0, 1,
                                                                        t.d_m, t.d_n, 20);
                 if (!rc) rc = orbmi_pose_optimization_frame(pose, &vc, inv_level_sigma2.data(), &fm, t.d_pose, t.d_out);
-                if (!rc) rc = down(t.h_n, t.d_n, 1);
-                if (!rc) rc = down(t.h_m, t.d_m, nc);
-                if (!rc) rc = down(t.h_out, t.d_out, nc);
-                if (!rc) rc = down(t.h_pose, t.d_pose, 1);
+                if (!rc) rc = down_range(t.h_n, t.h_m + nc);  // n, pose, outliers, matches
                 if (!rc && hipStreamSynchronize(tstream) != hipSuccess) rc = ORBMI_E_HIP;
                 return rc;
             }));
@@ -2048,10 +2059,7 @@ struct orbmi_slam {
             lf_records_into(cf.mps, nullptr, t.h_lfp);
             for (int i = 0; i < nc; i++) t.h_mlf[i] = cf.mps[i] >= 0 ? i : -1;
         }
-        SLAM_CHECK(up(t.d_occ, t.h_occ, nc));
-        SLAM_CHECK(up(t.d_rec, t.h_rec, nr));
-        SLAM_CHECK(up(t.d_lfp, t.h_lfp, nc));
-        SLAM_CHECK(up(t.d_mlf, t.h_mlf, nc));
+        SLAM_CHECK(up_range(t.h_rec, t.h_lfp + nc));  // local map records, own-point index, occ, own records
         const orbmi_frame_view vc = view(cf, cf.tcw.data());
         orbmi_frame_mappoints fm{};
         fm.match_lf = t.d_mlf;
@@ -2066,10 +2074,7 @@ struct orbmi_slam {
                 int rc = orbmi_search_local_points_track(matcher, &vc, t.d_occ, t.d_rec, nr, 1.f, t.d_m, nullptr, nullptr,
                                                          t.d_tr);
                 if (!rc) rc = orbmi_pose_optimization_frame(pose, &vc, inv_level_sigma2.data(), &fm, t.d_pose, t.d_out);
-                if (!rc) rc = down(t.h_m, t.d_m, nc);
-                if (!rc) rc = down(t.h_tr, t.d_tr, nr);
-                if (!rc) rc = down(t.h_out, t.d_out, nc);
-                if (!rc) rc = down(t.h_pose, t.d_pose, 1);
+                if (!rc) rc = down_range(t.h_n, t.h_tr + nr);  // pose, outliers, matches, frustum records
                 if (!rc && hipStreamSynchronize(tstream) != hipSuccess) rc = ORBMI_E_HIP;
                 return rc;
             }));
