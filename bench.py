@@ -444,6 +444,12 @@ def run_track(a, rank, world, local, dist):
         th = time.perf_counter()
         step(i)
         host_s += time.perf_counter() - th
+    t_enq = time.perf_counter()
+    if a.frame_events:  # which chain ends the timed region: tracking or the LocalMapping jobs
+        tr.synchronize()
+        t_trk = time.perf_counter()
+        mapper.wait()
+        t_map = time.perf_counter()
     sync()
     if dist:
         dist.barrier()
@@ -454,6 +460,9 @@ def run_track(a, rank, world, local, dist):
     lib.orbmi_pose_set_profiling(tr.pose._h, 0)
     dt = max_over_ranks(dt, dist)
     overlap = frame_overlap(tr.frame_events) if tr.frame_events else None
+    if overlap:
+        overlap.update({"host_enqueued_ms": round((t_enq - t0) * 1e3, 3), "tracking_done_ms": round((t_trk - t0) * 1e3, 3),
+                        "mapping_done_ms": round((t_map - t0) * 1e3, 3)})
     tr.frame_events = None
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
     x_matches = None

@@ -627,15 +627,24 @@ int orbmi_create_new_map_points(orbmi_matcher* h, const orbmi_frame_view* kf1, c
         for (int q = 0; q < 9; q++) P.F12.m[q] = Fh[9 * j + q];
         if ((rc = side(&tri2[j], &kf2[j], P.KF2, cos2 ? cos2[j] : nullptr, &S2[j]))) return rc;
     }
-    TriPair* d_pairs = (TriPair*)m.stage(sizeof(TriPair) * npairs);
-    const orbmi::tri::Side* d_S2 = dev_in(m, S2.data(), (size_t)npairs, &rc);
     std::vector<OutBuf> outs;
     int* d_match = dev_out(m, match12, (size_t)K1.n * npairs, outs);
     uint8_t* d_ok = dev_out(m, ok, (size_t)K1.n * npairs, outs);
     float* d_x3d = dev_out(m, x3d, (size_t)3 * K1.n * npairs, outs);
-    if (rc || !d_pairs || !d_match || !d_ok || !d_x3d) return rc ? rc : ORBMI_E_HIP;
-    if ((rc = orbmi::launch_create_points(m, K1, has1, f1, npairs, pairs.data(), d_pairs, S1, d_S2, d_match, d_ok,
-                                          d_x3d)))
+    if (!d_match || !d_ok || !d_x3d) return ORBMI_E_HIP;
+    if ((rc = orbmi::tri_pairs_prepare(m, K1, npairs, pairs.data(), d_match))) return rc;
+    // the pair table and the KF2 sides go up in one copy
+    const size_t o_s2 = (sizeof(TriPair) * npairs + 255) & ~(size_t)255;
+    const size_t tab_bytes = o_s2 + sizeof(orbmi::tri::Side) * npairs;
+    std::vector<uint8_t> tab(tab_bytes);
+    memcpy(tab.data(), pairs.data(), sizeof(TriPair) * npairs);
+    memcpy(tab.data() + o_s2, S2.data(), sizeof(orbmi::tri::Side) * npairs);
+    uint8_t* d_tab = (uint8_t*)m.stage(tab_bytes);
+    if (!d_tab) return ORBMI_E_HIP;
+    ORBMI_HIP(hipMemcpyAsync(d_tab, tab.data(), tab_bytes, hipMemcpyHostToDevice, m.stream));
+    TriPair* d_pairs = (TriPair*)d_tab;
+    const orbmi::tri::Side* d_S2 = (const orbmi::tri::Side*)(d_tab + o_s2);
+    if ((rc = orbmi::launch_create_points(m, K1, has1, f1, npairs, nullptr, d_pairs, S1, d_S2, d_match, d_ok, d_x3d)))
         return rc;
     return finish(m, outs, nullptr, nullptr);
 }
@@ -652,12 +661,13 @@ int orbmi_fuse_search(orbmi_matcher* h, const orbmi_frame_view* kf, const orbmi_
     const orbmi_mappoint* d_mps = dev_in(m, mps, (size_t)n_mp, &rc);
     const uint8_t* d_in = dev_in(m, in_kf, in_kf ? (size_t)std::max(n_mp, 1) : 0, &rc);
     if (rc) return rc;
-    if ((rc = scalars(m))) return rc;
+    if (ncandidates && (rc = scalars(m))) return rc;  // the count only when asked for
     std::vector<OutBuf> outs;
     int* d_bi = dev_out(m, best_idx, (size_t)n_mp, outs);
     int* d_bd = dev_out(m, best_dist, (size_t)n_mp, outs);
-    if ((rc = orbmi::launch_fuse(m, F, d_mps, d_in, n_mp, th, d_bi, d_bd, m.d_scalars))) return rc;
-    return finish(m, outs, m.d_scalars, ncandidates);
+    int* d_cnt = ncandidates ? m.d_scalars : nullptr;
+    if ((rc = orbmi::launch_fuse(m, F, d_mps, d_in, n_mp, th, d_bi, d_bd, d_cnt))) return rc;
+    return finish(m, outs, d_cnt, ncandidates);
 }
 
 int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* kfs, const orbmi_mappoint* mps,

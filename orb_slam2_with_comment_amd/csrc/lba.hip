@@ -354,9 +354,13 @@ __device__ inline bool ba_check_stop(const BaDev& a, BaCtl& c) {
 __global__ __launch_bounds__(kBaBlock) void k_ba_setup(BaDev a, double* __restrict__ T, double* __restrict__ X,
                                                        unsigned char* __restrict__ out_erase) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {  // check #0 (src/Optimizer.cc:685) was the host's, and found the flag clear
-        a.ctl->checks = 1;
-        a.ctl->stop_seen = -1;
+    if (i == 0) {  // the control block and the index statistics start cleared; check #0
+                   // (src/Optimizer.cc:685) was the host's, and found the flag clear
+        BaCtl c = {};
+        c.checks = 1;
+        c.stop_seen = -1;
+        *a.ctl = c;
+        for (int k = 0; k < 8; k++) a.istat[k] = 0;
     }
     if (i < a.nkf) {
         const float* t = a.kfs[i].tcw;
@@ -2944,8 +2948,6 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
         h.cap_out = out_bytes;
     }
     uint8_t* const Ho = h.h_out;
-    ORBMI_HIP(hipMemsetAsync(B + o_istat, 0, 32, s));
-    ORBMI_HIP(hipMemsetAsync(B + o_ctl, 0, sizeof(BaCtl), s));
     BaDev a;
     a.nkf = nkf; a.npt = npt; a.nedge = ne; a.nblk = nblk; a.nf = nf;
     a.nb_e = nb_e; a.nb_p = nb_p; a.nb_q = nb_q;

@@ -131,6 +131,8 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
 int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
                          TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match);
 namespace tri { struct Side; }
+int tri_pairs_prepare(Matcher& m, const DevFrame& KF1, int npairs, TriPair* pairs_host, int* match);
+// pairs_host == nullptr: the pair table is already prepared (tri_pairs_prepare) and uploaded
 int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, const DevFV& fv1, int npairs,
                          TriPair* pairs_host, TriPair* pairs_dev, const tri::Side& S1, const tri::Side* S2_dev,
                          int* match, uint8_t* ok, float* x3d);

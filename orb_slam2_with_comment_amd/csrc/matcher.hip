@@ -82,6 +82,7 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevFrame F, int* __restrict
 __global__ __launch_bounds__(1024) void k_grid_build_multi(const FuseKF* __restrict__ kfs, int* __restrict__ kp_cell,
                                                            int ncap) {
     const FuseKF& K = kfs[blockIdx.x];
+    if (threadIdx.x == 0) *K.ncand = 0;  // k_fuse_multi counts into it behind this launch
     grid_build_block(K.F, const_cast<int*>(K.cs), const_cast<int*>(K.cl), kp_cell + (size_t)blockIdx.x * ncap);
 }
 
@@ -1489,20 +1490,32 @@ static int tri_splits(const DevFrame& KF1, const DevFV& fv1, int npairs) {
     return std::max(1, std::min(std::min(by_chip, by_size), 64));
 }
 
-static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
-                             TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
+// per-pair scratch and outputs of the search: match rows are consecutive (pair j at
+// match + j * KF1.n)
+int tri_pairs_prepare(Matcher& m, const DevFrame& KF1, int npairs, TriPair* pairs_host, int* match) {
     const size_t n1 = (size_t)std::max(KF1.n, 1);
     int rc;
     if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, n1 * npairs))) return rc;
     if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH * npairs))) return rc;
-    // per-pair scratch and outputs: match rows are consecutive (pair j at match + j * KF1.n)
     for (int j = 0; j < npairs; j++) {
         pairs_host[j].match = match + (size_t)j * KF1.n;
         pairs_host[j].bin_of = m.d_bin_of + (size_t)j * n1;
         pairs_host[j].hist = m.d_hist + (size_t)j * HISTO_LENGTH;
     }
-    ORBMI_HIP(hipMemcpyAsync(pairs_dev, pairs_host, sizeof(TriPair) * npairs, hipMemcpyHostToDevice, m.stream));
-    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
+    return ORBMI_OK;
+}
+
+// pairs_host == nullptr: the caller prepared and uploaded the pair table (tri_pairs_prepare)
+static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1, const DevFV& fv1, int npairs,
+                             TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match,
+                             bool counts) {
+    int rc;
+    if (pairs_host) {
+        if ((rc = tri_pairs_prepare(m, KF1, npairs, pairs_host, match))) return rc;
+        ORBMI_HIP(hipMemcpyAsync(pairs_dev, pairs_host, sizeof(TriPair) * npairs, hipMemcpyHostToDevice, m.stream));
+    }
+    // the histogram is read only by the orientation check
+    if (check_ori) ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
     if (KF1.n > 0) ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)KF1.n * npairs * sizeof(int), m.stream));
     if (fv1.nnodes > 0) {
         const int splits = tri_splits(KF1, fv1, npairs);
@@ -1510,7 +1523,9 @@ static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has
         hipLaunchKernelGGL(k_tri_match, dim3((waves + 3) / 4, npairs), dim3(256), 0, m.stream, KF1, has_mp1, fv1,
                            pairs_dev, only_stereo, check_ori, splits);
     }
-    hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.stream, KF1.n, pairs_dev, check_ori);
+    // without the orientation check and counts the finalize pass has nothing to do
+    if (check_ori || counts)
+        hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.stream, KF1.n, pairs_dev, check_ori);
     return ORBMI_OK;
 }
 
@@ -1518,7 +1533,10 @@ int launch_triangulation(Matcher& m, const DevFrame& KF1, const uint8_t* has_mp1
                          TriPair* pairs_host, TriPair* pairs_dev, int only_stereo, int check_ori, int* match) {
     if (npairs <= 0) return ORBMI_OK;
     int rc;
-    if ((rc = launch_tri_search(m, KF1, has_mp1, fv1, npairs, pairs_host, pairs_dev, only_stereo, check_ori, match)))
+    bool counts = false;
+    for (int j = 0; j < npairs; j++) counts |= pairs_host[j].nmatches != nullptr;
+    if ((rc = launch_tri_search(m, KF1, has_mp1, fv1, npairs, pairs_host, pairs_dev, only_stereo, check_ori, match,
+                                counts)))
         return rc;
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
@@ -1600,7 +1618,7 @@ int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, c
                          int* match, uint8_t* ok, float* x3d) {
     if (npairs <= 0) return ORBMI_OK;
     int rc;
-    if ((rc = launch_tri_search(m, KF1, has1, fv1, npairs, pairs_host, pairs_dev, 0, 0, match))) return rc;
+    if ((rc = launch_tri_search(m, KF1, has1, fv1, npairs, pairs_host, pairs_dev, 0, 0, match, false))) return rc;
     auto par = [&](auto kern, int G) {
         const long long nt = (long long)KF1.n * G;
         hipLaunchKernelGGL(kern, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
@@ -1720,7 +1738,7 @@ __device__ inline void fuse_one(const DevFrame& F, const int* __restrict__ cs, c
     best_dist[i] = bi >= 0 ? bd : 256;
     // one atomic per wave: a counter shared by the whole grid serialises per-thread atomics
     const unsigned long long m = __ballot(fused);
-    if (fused && (threadIdx.x & 63) == __ffsll((long long)m) - 1) atomicAdd(ncand, (int)__popcll(m));
+    if (ncand && fused && (threadIdx.x & 63) == __ffsll((long long)m) - 1) atomicAdd(ncand, (int)__popcll(m));
 }
 
 constexpr int kFuseLanes = 8;  // lanes per candidate map point (a window spans a few grid cells)
@@ -1772,7 +1790,6 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
         K.ncand = ncand + k;
     }
     ORBMI_HIP(hipMemcpyAsync(kfs_dev, kfs_host, sizeof(FuseKF) * nkf, hipMemcpyHostToDevice, m.stream));
-    ORBMI_HIP(hipMemsetAsync(ncand, 0, sizeof(int) * nkf, m.stream));
     hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.stream, kfs_dev, m.d_mkp_cell, ncap);
     if (n > 0)
         hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n,
