@@ -157,6 +157,12 @@ void orbmi_matcher_destroy(orbmi_matcher* m);
 int orbmi_matcher_share_stream(orbmi_matcher* m, orbmi_extractor* ex);
 /* The handle's HIP stream (hipStream_t): its own, or the extractor's after share_stream. */
 int orbmi_matcher_get_stream(orbmi_matcher* m, void** stream);
+/* Keep the handle's own stream off `n` compute units (hipExtStreamCreateWithCUMask; the last n
+ * bits of the device's CU mask cleared), so that work on other streams -- Tracking's one-
+ * workgroup searches and PoseOptimization -- always finds free CUs beside a LocalMapping chain
+ * (LocalBA, Fuse) that fills the device.  Call before the stream is shared or queried; n = 0
+ * restores an unmasked stream.  ORBMI_E_STATE on a shared stream. */
+int orbmi_matcher_reserve_cus(orbmi_matcher* m, int n);
 /* Frame::AssignFeaturesToGrid (src/Frame.cc:232-247), run once per Frame as the Frame
  * constructor does (src/Frame.cc:98): builds the keypoint grid of F (device-resident keypoints
  * only, else ORBMI_E_ARG) on the handle's stream and pins it, so the searches on the same frame

@@ -225,6 +225,28 @@ int orbmi_matcher_share_stream(orbmi_matcher* h, orbmi_extractor* ex) {
     return ORBMI_OK;
 }
 
+int orbmi_matcher_reserve_cus(orbmi_matcher* h, int n) {
+    if (!h || n < 0) return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    if (!m.own_stream) return ORBMI_E_STATE;
+    ORBMI_HIP(hipSetDevice(m.device));
+    int ncu = 0;
+    ORBMI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m.device));
+    if (n >= ncu) return ORBMI_E_ARG;
+    hipStream_t s = nullptr;
+    if (n == 0) {
+        ORBMI_HIP(orbmi::stream_create(&s, "MATCHER"));
+    } else {
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu - n; c++) mask[c >> 5] |= 1u << (c & 31);
+        ORBMI_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    (void)hipStreamSynchronize(m.stream);
+    (void)hipStreamDestroy(m.stream);
+    m.stream = s;
+    return ORBMI_OK;
+}
+
 int orbmi_matcher_assign_features_to_grid(orbmi_matcher* h, const orbmi_frame_view* v) {
     if (!h || !v || (v->n > 0 && !on_device(v->keys_un))) return ORBMI_E_ARG;
     Matcher& m = h->m;

@@ -2285,6 +2285,9 @@ struct orbmi_slam {
     }
 };
 
+// CUs LocalMapping's stream leaves to Tracking (ORBMI_LM_RESERVE_CUS overrides)
+constexpr int kLmReserveCus = 0;
+
 extern "C" {
 
 int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary* vocabulary, orbmi_slam** out) {
@@ -2307,6 +2310,11 @@ int orbmi_slam_create(const orbmi_slam_settings* s, int device, orbmi_vocabulary
     }
     if (!rc) rc = orbmi_matcher_create(device, &h->matcher);
     if (!rc && s->async_local_mapping) rc = orbmi_matcher_create(device, &h->lm_matcher);
+    if (!rc && h->lm_matcher) {  // LocalMapping's stream kept off a few CUs (orbmi_matcher_reserve_cus)
+        const char* v = getenv("ORBMI_LM_RESERVE_CUS");
+        const int n = v ? atoi(v) : kLmReserveCus;
+        if (n > 0) rc = orbmi_matcher_reserve_cus(h->lm_matcher, n);
+    }
     if (!rc) rc = orbmi_pose_create(device, &h->pose);
     if (!rc) rc = orbmi_ba_create(device, &h->ba);
     // each thread's operators in order on one stream (Tracking: searches + PoseOptimization;

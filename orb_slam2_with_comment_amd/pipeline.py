@@ -403,6 +403,9 @@ class ChainStats(dict):
         raise KeyError(k)
 
 
+LM_RESERVE_CUS = 0  # CUs the LocalMapping chain's stream leaves free (ORBMI_LM_RESERVE_CUS overrides)
+
+
 class LocalMapper:
     """LocalMapping thread (src/LocalMapping.cc:47-128), concurrent with tracking as in the
     reference.  For every queued keyframe, in the reference's order, on the mapper's own GPU
@@ -427,6 +430,11 @@ class LocalMapper:
         self.device = device
         self.ba = LocalBA(device)
         self.matcher = ORBmatcher(device=device)
+        # LocalMapping's stream kept off a few CUs, so Tracking's one-workgroup kernels always find
+        # room beside a chain that fills the device (orbmi_matcher_reserve_cus)
+        reserve = int(os.environ.get("ORBMI_LM_RESERVE_CUS", str(LM_RESERVE_CUS)))
+        if reserve > 0:
+            check("orbmi_matcher_reserve_cus", lib().orbmi_matcher_reserve_cus(self.matcher._h, reserve))
         self.voc = vocabulary  # ORBVocabulary (device handle) or None
         dev = torch.device("cuda", device)
         cap = max_features
