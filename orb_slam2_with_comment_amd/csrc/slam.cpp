@@ -288,6 +288,63 @@ struct orbmi_slam {
         float* h_dep = nullptr;
     } dev;
     hipStream_t xstream = nullptr;  // the left extractor's stream
+    // The next pair's Frame-constructor work (image staging, the extraction and stereo launches,
+    // the read-back copies: frame_enqueue) runs on a helper thread while the tracking thread
+    // tracks the current frame; track_stereo joins it before returning, so the caller's next
+    // images are never read after the call.  ORBMI_SLAM_INLINE_FRAME=1: on the tracking thread.
+    struct FrameWorker {
+        std::thread th;
+        std::mutex mtx;
+        std::condition_variable cv;
+        bool job = false, busy = false, quit = false;
+        int rc = ORBMI_OK;
+        const uint8_t *L = nullptr, *R = nullptr;
+        int rows = 0, cols = 0;
+        size_t step = 0;
+        int* slot = nullptr;
+    } fw;
+    const bool inline_frame = getenv("ORBMI_SLAM_INLINE_FRAME") != nullptr;
+    void frame_worker_run() {
+        (void)hipSetDevice(device);  // the current device is per thread
+        std::unique_lock<std::mutex> g(fw.mtx);
+        for (;;) {
+            fw.cv.wait(g, [this] { return fw.job || fw.quit; });
+            if (fw.quit) return;
+            fw.job = false;
+            g.unlock();
+            const int rc = frame_enqueue(fw.L, fw.R, fw.rows, fw.cols, fw.step, fw.slot);
+            g.lock();
+            fw.rc = rc;
+            fw.busy = false;
+            fw.cv.notify_all();
+        }
+    }
+    void frame_post(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int* slot) {
+        std::lock_guard<std::mutex> g(fw.mtx);
+        if (!fw.th.joinable()) fw.th = std::thread([this] { frame_worker_run(); });
+        fw.L = L; fw.R = R; fw.rows = rows; fw.cols = cols; fw.step = step; fw.slot = slot;
+        fw.job = true;
+        fw.busy = true;
+        fw.rc = ORBMI_OK;
+        fw.cv.notify_all();
+    }
+    int frame_join() {  // the posted enqueue finished; its status
+        std::unique_lock<std::mutex> g(fw.mtx);
+        fw.cv.wait(g, [this] { return !fw.busy; });
+        const int rc = fw.rc;
+        fw.rc = ORBMI_OK;
+        return rc;
+    }
+    void frame_worker_stop() {
+        if (!fw.th.joinable()) return;
+        (void)frame_join();
+        {
+            std::lock_guard<std::mutex> g(fw.mtx);
+            fw.quit = true;
+            fw.cv.notify_all();
+        }
+        fw.th.join();
+    }
     // Device-resident tracking stages: TrackWithMotionModel (SearchByProjection(CF, LF) with the
     // retry gated on the device count, PoseOptimization on the device-held matches) and
     // TrackLocalMap (SearchLocalPoints, PoseOptimization over both match arrays) are each enqueued
@@ -528,8 +585,13 @@ struct orbmi_slam {
         cf.ur.assign(dev.h_ur, dev.h_ur + n);
         cf.depth.assign(dev.h_dep, dev.h_dep + n);
         cf.dslot = slot;
-        // new keypoints behind a slot's pointers: a grid pinned on an older frame there is stale
-        return orbmi_matcher_release_grid(matcher);
+        // new keypoints behind a slot's pointers: a grid pinned on an older frame there is stale.
+        // Frame::AssignFeaturesToGrid (src/Frame.cc:98) then runs once for the frame, on the
+        // tracking stream: its searches (the last-frame search, the retry, SearchLocalPoints)
+        // reuse that grid instead of building one each
+        SLAM_CHECK(orbmi_matcher_release_grid(matcher));
+        const orbmi_frame_view v = view(cf, nullptr);
+        return orbmi_matcher_assign_features_to_grid(matcher, &v);
     }
 
     int frame_stereo(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step) {
@@ -554,7 +616,8 @@ struct orbmi_slam {
             SLAM_CHECK(frame_stereo(cf, L, R, rows, cols, step));
         }
         if (nL && nR) {
-            SLAM_CHECK(frame_enqueue(nL, nR, rows, cols, step, &a.slot));
+            if (inline_frame) SLAM_CHECK(frame_enqueue(nL, nR, rows, cols, step, &a.slot));
+            else frame_post(nL, nR, rows, cols, step, &a.slot);  // joined before the call returns
             a.on = true;
             a.L = nL;
             a.R = nR;
@@ -566,6 +629,7 @@ struct orbmi_slam {
     }
 
     void free_dev() {
+        frame_worker_stop();
         if (dev.ahead.on && xstream) (void)hipStreamSynchronize(xstream);
         for (int k = 0; k < kSlots; k++) {
             (void)hipFree(dev.kps[k]);
@@ -2378,23 +2442,8 @@ void orbmi_slam_destroy(orbmi_slam* h) {
     delete h;
 }
 
-static int track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
-                        double timestamp, const uint8_t* next_left, const uint8_t* next_right, bool ahead, float* tcw_out,
-                        int* has_pose) {
-    if (!h || !left || !right || rows <= 0 || cols <= 0 || step < (size_t)cols) return ORBMI_E_ARG;
-    if (h->reset_pending) SLAM_CHECK(h->deferred_reset());  // (src/System.cc:139-146)
-    TrackedFrame cf;
-    cf.id = h->frame_count;
-    cf.ts = timestamp;
-    // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images, ComputeStereoMatches
-    // (touches no map state: outside the map lock)
-    PhaseTimer total(&h->phase_ms[PH_TOTAL]);
-    h->phase_frames++;
-    {
-        PhaseTimer pt(&h->phase_ms[PH_FRAME]);
-        if (ahead) SLAM_CHECK(h->frame_stereo_ahead(cf, left, right, rows, cols, step, next_left, next_right));
-        else SLAM_CHECK(h->frame_stereo(cf, left, right, rows, cols, step));
-    }
+// Tracking::Track on a constructed frame, under the map locks
+static int track_frame(orbmi_slam* h, TrackedFrame& cf, float* tcw_out, int* has_pose) {
     PhaseTimer* lock_t = new PhaseTimer(&h->phase_ms[PH_LOCK]);
     std::unique_lock<std::mutex> update_guard(h->update_mtx, std::defer_lock);
     if (h->async_lm()) update_guard.lock();
@@ -2420,6 +2469,34 @@ static int track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right
     if (has_pose) *has_pose = lf.has_tcw ? 1 : 0;
     if (tcw_out && lf.has_tcw) std::memcpy(tcw_out, lf.tcw.data(), 16 * sizeof(float));
     return ORBMI_OK;
+}
+
+static int track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+                        double timestamp, const uint8_t* next_left, const uint8_t* next_right, bool ahead, float* tcw_out,
+                        int* has_pose) {
+    if (!h || !left || !right || rows <= 0 || cols <= 0 || step < (size_t)cols) return ORBMI_E_ARG;
+    if (h->reset_pending) SLAM_CHECK(h->deferred_reset());  // (src/System.cc:139-146)
+    TrackedFrame cf;
+    cf.id = h->frame_count;
+    cf.ts = timestamp;
+    // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images, ComputeStereoMatches
+    // (touches no map state: outside the map lock)
+    PhaseTimer total(&h->phase_ms[PH_TOTAL]);
+    h->phase_frames++;
+    {
+        PhaseTimer pt(&h->phase_ms[PH_FRAME]);
+        int rc = ahead ? h->frame_stereo_ahead(cf, left, right, rows, cols, step, next_left, next_right)
+                       : h->frame_stereo(cf, left, right, rows, cols, step);
+        if (rc) {
+            (void)h->frame_join();
+            return rc;
+        }
+    }
+    const int rc = track_frame(h, cf, tcw_out, has_pose);
+    // the next pair's enqueue (frame_post) has finished before the call returns: the caller's
+    // images are not read afterwards
+    const int jrc = h->frame_join();
+    return rc ? rc : jrc;
 }
 
 int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
