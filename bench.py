@@ -153,6 +153,36 @@ def frame_overlap(evs):
     return stats
 
 
+def job_overlap(jobs):
+    """The LocalMapping jobs' timeline (--frame-events): each job's span on the mapper's stream
+    (the first packet to LocalBA's return), the stream's gap between two jobs, and the host's gap
+    from one job's LocalBA return to the next job's start (µs, median / p90)."""
+    base = jobs[0][0]
+    t = np.array([[base.elapsed_time(e0) * 1e3, base.elapsed_time(e1) * 1e3] for e0, e1, _, _, _ in jobs])
+    h = np.array([[h0, h1] for _, _, h0, h1, _ in jobs]) * 1e6
+    out = {}
+
+    def put(name, v):
+        v = np.sort(np.asarray(v))
+        if len(v):
+            out[name] = {"median": round(float(v[len(v) // 2]), 1), "p90": round(float(v[int(0.9 * (len(v) - 1))]), 1)}
+    put("lm_job_span_us", t[:, 1] - t[:, 0])
+    put("lm_stream_gap_between_jobs_us", t[1:, 0] - t[:-1, 1])
+    put("lm_host_gap_between_jobs_us", h[1:, 0] - h[:-1, 1])
+    # the job's stages on the stream: each from the previous boundary (LocalBA: to the job's end)
+    names = [n for n, _ in jobs[0][4]]
+    if names and all([n for n, _ in j[4]] == names for j in jobs):
+        for k, n in enumerate(names + ["local_ba"]):
+            v = []
+            for e0, e1, _, _, mk in jobs:
+                a = e0 if k == 0 else mk[k - 1][1]
+                b = e1 if k == len(names) else mk[k][1]
+                v.append(a.elapsed_time(b) * 1e3)
+            put(f"lm_stage_{n}_us", v)
+    out["lm_jobs"] = len(jobs)
+    return out
+
+
 def lba_trial_traffic(a):
     """HBM bytes of one LocalBA LM trial (its three launches) from the --mode lba PMC summary,
     None without it or when it was measured on another workload."""
@@ -438,6 +468,7 @@ def run_track(a, rank, world, local, dist):
     sync()
     if a.frame_events:
         tr.frame_events = []
+        mapper.job_events = []
     t0 = time.perf_counter()
     host_s = 0.0  # time the host spends enqueueing (a host-bound step shows host ~ wall)
     for i in range(a.steps):
@@ -463,7 +494,10 @@ def run_track(a, rank, world, local, dist):
     if overlap:
         overlap.update({"host_enqueued_ms": round((t_enq - t0) * 1e3, 3), "tracking_done_ms": round((t_trk - t0) * 1e3, 3),
                         "mapping_done_ms": round((t_map - t0) * 1e3, 3)})
+    if overlap and mapper.job_events:
+        overlap.update(job_overlap(mapper.job_events))
     tr.frame_events = None
+    mapper.job_events = None
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
     x_matches = None
     if xch is not None:

@@ -71,6 +71,7 @@ int orbmi_debug_ba_schur_blocks(int nf, int* table, int cap, int* n_out);
 #define ORBMI_SCHED_L_FUSE_REFRESH 21  /* after the refresh before target `arg`'s replay         */
 #define ORBMI_SCHED_L_FUSE 22          /* after one Fuse search                                  */
 #define ORBMI_SCHED_L_BA 23            /* after LocalBundleAdjustment's optimisation (keyframe `arg`) */
+#define ORBMI_SCHED_L_BOW 24           /* after ProcessNewKeyFrame's ComputeBoW (keyframe `arg`)   */
 typedef struct orbmi_slam_event {
     int32_t thread;                /* 0 Tracking, 1 LocalMapping                             */
     int32_t label, arg;

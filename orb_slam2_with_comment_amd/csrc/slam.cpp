@@ -491,6 +491,30 @@ struct orbmi_slam {
     std::vector<orbmi_slam_event> sched;
     void log_section(int label, int arg) {
         if (async_lm()) sched.push_back(orbmi_slam_event{on_mapping_thread ? 1 : 0, label, arg});
+        if (lock_profile && on_mapping_thread) { hold_label = label; hold_t0 = std::chrono::steady_clock::now(); }
+    }
+    // ORBMI_SLAM_LOCK_PROFILE=1 (development aid): how long the mapping thread holds the map lock
+    // after each kind of acquisition (by schedule label), printed to stderr at destroy
+    const bool lock_profile = getenv("ORBMI_SLAM_LOCK_PROFILE") != nullptr;
+    int hold_label = -1;
+    std::chrono::steady_clock::time_point hold_t0;
+    std::map<int, std::pair<double, double>> hold_ms;  // label -> (sum, max) ms (mapping thread only)
+    std::map<int, long> hold_n;
+    void hold_end() {  // the mapping thread releases the map lock
+        if (!lock_profile || !on_mapping_thread || hold_label < 0) return;
+        const double d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - hold_t0).count();
+        auto& e = hold_ms[hold_label];
+        e.first += d;
+        e.second = std::max(e.second, d);
+        hold_n[hold_label]++;
+        hold_label = -1;
+    }
+    void hold_report() const {
+        if (!lock_profile) return;
+        for (const auto& kv : hold_ms)
+            fprintf(stderr, "map-lock hold after label %d: n %ld  total %.3f ms  mean %.4f ms  max %.4f ms\n", kv.first,
+                    hold_n.at(kv.first), kv.second.first, kv.second.first / std::max(1L, hold_n.at(kv.first)),
+                    kv.second.second);
     }
     std::vector<orbmi_slam_ba_record> ba_log;  // orbmi_slam_get_local_ba_log (under map_mtx)
 
@@ -907,6 +931,7 @@ struct orbmi_slam {
     template <class F>
     int unlocked(int label, int arg, F f) {
         if (!held_lock) return f();
+        hold_end();
         held_lock->unlock();
         const int rc = f();
         if (on_mapping_thread) {
@@ -1079,6 +1104,7 @@ struct orbmi_slam {
                     rc = local_mapping(k);
                     held_lock = nullptr;
                 }
+                hold_end();
                 std::lock_guard<std::mutex> g(q_mtx);
                 lm_busy = false;  // SetAcceptKeyFrames(true), still under map_mtx
                 if (rc && !lm_rc) lm_rc = rc;
@@ -1112,7 +1138,13 @@ struct orbmi_slam {
 
     template <class Next>
     int local_mapping_steps(int k, Next&& next) {
-        if (voc && !kfs[k].fv.valid) SLAM_CHECK(compute_bow(kfs[k].desc, kfs[k].fv));
+        if (voc && !kfs[k].fv.valid) {  // ComputeBoW with the map lock released (the keyframe's
+                                        // descriptors copied first: Tracking may grow kfs meanwhile)
+            const std::vector<uint8_t> desc = kfs[k].desc;
+            FeatVec fv;
+            SLAM_CHECK(unlocked(ORBMI_SCHED_L_BOW, k, [&] { return compute_bow(desc, fv); }));
+            if (!kfs[k].fv.valid) kfs[k].fv = std::move(fv);  // (Tracking may have computed it: the same)
+        }
         std::vector<int> updated;
         for (int i = 0; i < (int)kfs[k].mps.size(); i++) {
             const int m = kfs[k].mps[i];
@@ -1723,6 +1755,7 @@ struct orbmi_slam {
         int rc;
         std::unique_lock<std::mutex> update_guard;  // held to the end of the write-back
         if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves
+            hold_end();
             held_lock->unlock();
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
             update_guard = std::unique_lock<std::mutex>(update_mtx);  // (lock order: update, map)
@@ -2429,6 +2462,7 @@ void orbmi_slam_destroy(orbmi_slam* h) {
     }
     if (h->xstream) (void)hipStreamSynchronize(h->xstream);
     if (h->tstream) (void)hipStreamSynchronize(h->tstream);
+    h->hold_report();
     h->free_dev();
     h->free_track_buffers();
     orbmi_ba_destroy(h->ba);

@@ -29,6 +29,7 @@ import ctypes as C
 import os
 import queue
 import threading
+import time
 
 import numpy as np
 
@@ -468,6 +469,7 @@ class LocalMapper:
             if vocabulary is not None:
                 check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(vocabulary._h, ms))
         self.q: queue.Queue = queue.Queue()
+        self.job_events = None  # a list: per job (start event, end event, host start, host end)
         self.done = 0
         self.last = None
         self.last_chain = None
@@ -524,6 +526,18 @@ class LocalMapper:
         L = lib()
         m = self.matcher._h
         kf = job.kf
+        je = self.job_events  # diagnostics (bench --frame-events): the job's span on the stream
+        if je is not None:
+            t_host0 = time.perf_counter()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(self._ms)
+            marks = []
+
+        def mark(name):  # a stage boundary on the mapper's stream (diagnostics only)
+            if je is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self._ms)
+                marks.append((name, ev))
         # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
         # ComputeDistinctiveDescriptors of the keyframe's map points, enqueued back to back
         b = self.bow
@@ -548,6 +562,7 @@ class LocalMapper:
         bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
+        mark("bow_distinctive")
         nw, nn = self._counts_h.read()  # waits for the size copy only (whatever the stream mode)
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
@@ -558,6 +573,7 @@ class LocalMapper:
                 C.addressof(fv1), nnb, kf2, job.c_tri2, job.c_cos2, job.c_mp2, job.c_fv2, job.c_F12.ctypes.data,
                 _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         nt = nnb * kf.n
+        mark("create_new_map_points")
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
         if nnb:
             check("orbmi_fuse_search_batch", L.orbmi_fuse_search_batch(
@@ -566,12 +582,18 @@ class LocalMapper:
         check("orbmi_fuse_search", L.orbmi_fuse_search(
             m, C.addressof(kf.view), _vp(d_tp), None, int(n_tp), 3.0, _vp(bi.data_ptr() + 4 * o),
             _vp(bd.data_ptr() + 4 * o), None))
+        mark("fuse")
         # ComputeDistinctiveDescriptors + UpdateNormalAndDepth of the keyframe's points after fusion
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
+        mark("distinctive")
         # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
         ms = self._ms
+        if je is not None:  # LocalBA returned: its work is complete
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(ms)
+            je.append((e0, e1, t_host0, time.perf_counter(), marks))
 
         def stats():  # what the searches found (statistics only: off the chain's path)
             ms.synchronize()

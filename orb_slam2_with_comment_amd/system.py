@@ -48,7 +48,7 @@ NO_IMAGES_YET, NOT_INITIALIZED, OK, LOST = 0, 1, 2, 3   # Tracking::eTrackingSta
 # generators below yield these at the points where the native loop (csrc/slam.cpp) releases
 # its map lock around a GPU call, so a recorded concurrent schedule can be replayed here
 T_FRAME, T_BOW, T_POSE, T_LF, T_LOCAL, T_RESET = 1, 2, 3, 4, 5, 6
-L_JOB, L_DISTINCTIVE, L_CREATE, L_CREATE_PAIR, L_FUSE_BATCH, L_FUSE_REFRESH, L_FUSE, L_BA = range(16, 24)
+L_JOB, L_DISTINCTIVE, L_CREATE, L_CREATE_PAIR, L_FUSE_BATCH, L_FUSE_REFRESH, L_FUSE, L_BA, L_BOW = range(16, 25)
 
 
 class ScheduleMismatch(RuntimeError):
@@ -807,8 +807,11 @@ class StereoSLAM:
         MapPointCulling, CreateNewMapPoints, SearchInNeighbors unless a keyframe is queued,
         LocalBundleAdjustment (more than 2 keyframes) and KeyFrameCulling unless one is queued."""
         # ProcessNewKeyFrame (:152-211)
-        if self.backend_has_bow():
-            kf.feat_vec = kf.feat_vec or self.backend.compute_bow(kf.desc)
+        if self.backend_has_bow() and kf.feat_vec is None:
+            fv = self.backend.compute_bow(kf.desc)  # the native loop releases the map lock around it
+            yield L_BOW, kf.id
+            if kf.feat_vec is None:  # (Tracking may have computed it meanwhile: the same)
+                kf.feat_vec = fv
         updated = []
         for i, mp in enumerate(kf.map_points):
             if mp is None or mp.bad:
