@@ -665,7 +665,10 @@ int orbmi_slam_track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* r
  * extraction of both images, ComputeStereoMatches) is enqueued to run on the GPU while this frame
  * is tracked.  The next call must pass that pair as left/right -- the same buffers, unmodified,
  * same geometry -- to use it (any other pair is extracted as usual); next_left / next_right NULL:
- * nothing ahead.  The extraction depends on the images only, so every result is the plain call's. */
+ * nothing ahead.  The extraction depends on the images only, so every result is the plain call's.
+ * The next pair is copied and enqueued by a helper thread of the handle while this frame is
+ * tracked, and that work has finished when the call returns: next_left / next_right are not
+ * read after it (ORBMI_SLAM_INLINE_FRAME=1: on the calling thread, before tracking). */
 int orbmi_slam_track_stereo_ahead(orbmi_slam* h, const uint8_t* left, const uint8_t* right, int rows, int cols,
                                   size_t step, double timestamp, const uint8_t* next_left,
                                   const uint8_t* next_right, float* tcw_out, int* has_pose);
