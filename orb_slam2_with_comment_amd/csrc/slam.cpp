@@ -34,6 +34,7 @@
 #include <map>
 #include <new>
 #include <set>
+#include <stdexcept>
 #include <utility>
 #include <vector>
 
@@ -146,6 +147,49 @@ struct KeyFrame {
     const float* d_cos = nullptr;  // orbmi_stereo_parallax_cos per keypoint (CreateNewMapPoints)
 };
 
+// MapPoint::mObservations (keyframe id -> keypoint index, keyframe-id order) as a sorted flat
+// vector: a map point has a handful of observations, and the tracking thread walks them for every
+// matched point each frame (UpdateLocalKeyFrames), which node-based std::map made pointer chases
+struct ObsMap {
+    using Entry = std::pair<int, int>;
+    std::vector<Entry> v;
+    using iterator = std::vector<Entry>::iterator;
+    using const_iterator = std::vector<Entry>::const_iterator;
+    iterator begin() { return v.begin(); }
+    iterator end() { return v.end(); }
+    const_iterator begin() const { return v.begin(); }
+    const_iterator end() const { return v.end(); }
+    size_t size() const { return v.size(); }
+    bool empty() const { return v.empty(); }
+    void clear() { v.clear(); }
+    iterator lower(int k) {
+        return std::lower_bound(v.begin(), v.end(), k, [](const Entry& e, int x) { return e.first < x; });
+    }
+    const_iterator lower(int k) const {
+        return std::lower_bound(v.begin(), v.end(), k, [](const Entry& e, int x) { return e.first < x; });
+    }
+    iterator find(int k) {
+        auto it = lower(k);
+        return it != v.end() && it->first == k ? it : v.end();
+    }
+    const_iterator find(int k) const {
+        auto it = lower(k);
+        return it != v.end() && it->first == k ? it : v.end();
+    }
+    size_t count(int k) const { return find(k) != v.end() ? 1 : 0; }
+    int& operator[](int k) {
+        auto it = lower(k);
+        if (it == v.end() || it->first != k) it = v.insert(it, Entry{k, 0});
+        return it->second;
+    }
+    const int& at(int k) const {
+        auto it = find(k);
+        if (it == v.end()) throw std::out_of_range("ObsMap::at");
+        return it->second;
+    }
+    iterator erase(iterator it) { return v.erase(it); }
+};
+
 struct MapPoint {
     int id = 0;
     float pos[3] = {0, 0, 0};
@@ -153,7 +197,7 @@ struct MapPoint {
     uint8_t desc[32] = {};
     float normal[3] = {0, 0, 0};
     float max_distance = 0, min_distance = 0;
-    std::map<int, int> obs;      // keyframe id -> keypoint index (keyframe id order)
+    ObsMap obs;                  // keyframe id -> keypoint index (keyframe id order)
     int nobs = 0;
     bool bad = false;
     int first_kf_id = 0;         // mnFirstKFid
@@ -1375,7 +1419,7 @@ struct orbmi_slam {
     // Returns true when other gained them (its descriptor is recomputed before the next search).
     bool replace(int m, int other) {
         if (m == other) return false;
-        const std::map<int, int> obs = mps[m].obs;
+        const ObsMap obs = mps[m].obs;
         mps[m].obs.clear();
         mps[m].bad = true;
         mps[m].replaced = other;

@@ -200,3 +200,21 @@ def test_pinned_grid(oracle, M):
     vh = FA.view()                            # host keypoints: refused
     assert lib().orbmi_matcher_assign_features_to_grid(m._h, C.addressof(vh)) == ORBMI_E_ARG
     m.close()
+
+
+def test_search_on_cu_masked_stream(oracle, M):
+    """orbmi_matcher_reserve_cus: the handle's stream kept off 8 CUs (hipExtStreamCreateWithCUMask)
+    gives the same matches; 0 restores an unmasked stream; a negative count is refused."""
+    from orb_slam2_with_comment_amd._capi import lib
+    F = make_frame(3)
+    mps = local_map((0, 1, 2), seed=30)
+    tr = oracle.is_in_frustum(F, mps, 0.5)
+    occ = np.zeros(len(F.keys), np.uint8)
+    m_ref, n_ref = oracle.search_by_projection_local(F, occ, mps, tr, 1.0, 0.8)
+    mt = M(0.8)
+    for n in (8, 0):
+        assert lib().orbmi_matcher_reserve_cus(mt._h, n) == 0
+        m, k = mt.SearchByProjection(F, occ, mps, tr, 1.0)
+        assert k == n_ref
+        np.testing.assert_array_equal(m, m_ref)
+    assert lib().orbmi_matcher_reserve_cus(mt._h, -1) != 0
