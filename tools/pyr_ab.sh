@@ -1,5 +1,7 @@
-# config 5 (bench --mode batch): the one-launch pyramid (k_pyr_chain, default) vs a launch per
-# level (ORBMI_PYR=levels), and band counts: bash tools/pyr_ab.sh [BANDS ...]
+# config 5 (bench --mode batch): the one-launch pyramid (k_pyr_chain) vs a launch per level
+# (ORBMI_PYR=levels), and band counts: bash tools/pyr_ab.sh [BANDS ...].  Kept for the record of
+# profiles/r05/pyr_chain_ab.txt: k_pyr_chain measured no faster and was removed, so today every
+# variant runs the per-level launches.
 mkdir -p gpurun_out/pyrab
 for i in 1 2 3; do
   for v in levels chain "$@"; do
