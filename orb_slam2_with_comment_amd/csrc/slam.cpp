@@ -663,6 +663,12 @@ struct orbmi_slam {
     }
 
     int frame_stereo(TrackedFrame& cf, const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step) {
+        // a pair enqueued ahead and not asked for (a plain call after an ahead one): it shares the
+        // pinned read-back buffers, so it is drained and dropped first
+        if (dev.ahead.on) {
+            dev.ahead.on = false;
+            if (hipStreamSynchronize(xstream) != hipSuccess) return ORBMI_E_HIP;
+        }
         int slot = -1;
         SLAM_CHECK(frame_enqueue(L, R, rows, cols, step, &slot));
         return frame_collect(cf, slot);
