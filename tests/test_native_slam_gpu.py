@@ -55,6 +55,40 @@ def test_native_matches_oracle_200_frames(tmp_path, ahead):
     gpu.Shutdown()
 
 
+def test_native_plain_calls_between_ahead_calls(tmp_path):
+    """Plain orbmi_slam_track_stereo calls while a pair enqueued ahead is pending (the pending pair
+    is dropped: it shares the pinned read-back buffers) give the all-plain run's decisions and
+    trajectory."""
+    import ctypes as C
+    from orb_slam2_with_comment_amd._capi import lib
+    n = 30
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    ref = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    _drive(ref, frames)
+    mix = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    keep = []
+    for f, (L, R, _) in enumerate(frames):
+        if f in (10, 11, 20):  # plain, with frame f's pair enqueued ahead by the previous call
+            Lc, Rc = np.ascontiguousarray(L, np.uint8), np.ascontiguousarray(R, np.uint8)
+            tcw, has = np.zeros(16, np.float32), C.c_int()
+            assert lib().orbmi_slam_track_stereo(mix._h, Lc.ctypes.data, Rc.ctypes.data, Lc.shape[0], Lc.shape[1],
+                                                 Lc.strides[0], 0.1 * f, tcw.ctypes.data, C.byref(has)) == 0
+            mix._ahead = None
+        else:
+            nxt = frames[f + 1][:2] if f + 1 < n else None
+            keep.append(nxt)
+            mix.TrackStereo(L, R, 0.1 * f, next_pair=nxt)
+    a_all, b_all = mix.stats, ref.stats
+    assert len(a_all) == len(b_all) == n
+    for a, b in zip(a_all, b_all):
+        assert {k: a.get(k) for k in _DECISIONS} == {k: b.get(k) for k in _DECISIONS}, (a, b)
+    np.testing.assert_array_equal(mix.trajectory_twc(), ref.trajectory_twc())
+    mix.Shutdown()
+    ref.Shutdown()
+
+
 def test_native_writers_and_counts(tmp_path):
     n = 16
     frames = render_sequence(n)
