@@ -26,11 +26,43 @@ void* Matcher::stage(size_t bytes) {
     std::vector<Block>& arena = gens[gen].blocks;
     for (Block& b : arena)
         if (b.size - b.used >= bytes) { void* p = b.p + b.used; b.used += bytes; return p; }
-    Block b{nullptr, std::max(bytes, (size_t)(4 << 20)), 0};
+    Block b{nullptr, std::max(bytes, (size_t)(4 << 20)), 0, nullptr};
     if (hipMalloc((void**)&b.p, b.size) != hipSuccess) return nullptr;
+    if (hipHostMalloc((void**)&b.h, b.size, hipHostMallocDefault) != hipSuccess) {
+        (void)hipFree(b.p);
+        return nullptr;
+    }
     b.used = bytes;
     arena.push_back(b);
     return b.p;
+}
+
+uint8_t* Matcher::mirror(const void* d) {
+    const uint8_t* q = (const uint8_t*)d;
+    for (Block& b : gens[gen].blocks)
+        if (q >= b.p && q < b.p + b.size) return b.h + (q - b.p);
+    return nullptr;
+}
+
+hipError_t Matcher::h2d(void* d, const void* src, size_t bytes) {
+    if (!bytes) return hipSuccess;
+    uint8_t* h = mirror(d);
+    if (!h) return hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, stream);
+    memcpy(h, src, bytes);
+    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+}
+
+hipError_t Matcher::d2h(void* user, const void* d, size_t bytes) {
+    if (!bytes) return hipSuccess;
+    uint8_t* h = mirror(d);
+    if (!h) return hipMemcpyAsync(user, d, bytes, hipMemcpyDeviceToHost, stream);
+    pend.push_back(Pend{user, h, bytes});
+    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
+}
+
+void Matcher::d2h_flush() {
+    for (const Pend& p : pend) memcpy(p.user, p.mirror, p.bytes);
+    pend.clear();
 }
 
 void Matcher::arena_reset() {
@@ -54,6 +86,7 @@ void Matcher::arena_reset() {
         g.pending = false;
     }
     for (Block& b : g.blocks) b.used = 0;
+    pend.clear();
 }
 
 void Matcher::release() {
@@ -65,7 +98,10 @@ void Matcher::release() {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (Gen& g : gens) {
-        for (Block& b : g.blocks) (void)hipFree(b.p);
+        for (Block& b : g.blocks) {
+            (void)hipFree(b.p);
+            if (b.h) (void)hipHostFree(b.h);
+        }
         g.blocks.clear();
         if (g.ev) (void)hipEventDestroy(g.ev);
         g.ev = nullptr;
@@ -95,7 +131,7 @@ const T* dev_in(Matcher& m, const T* p, size_t n, int* rc) {
     if (!p || n == 0) return p;
     if (on_device(p)) return p;
     T* d = (T*)m.stage(n * sizeof(T));
-    if (!d || hipMemcpyAsync(d, p, n * sizeof(T), hipMemcpyHostToDevice, m.stream) != hipSuccess) {
+    if (!d || m.h2d(d, p, n * sizeof(T)) != hipSuccess) {
         *rc = ORBMI_E_HIP;
         return nullptr;
     }
@@ -122,11 +158,12 @@ int finish(Matcher& m, std::vector<OutBuf>& outs, int* nmatches_dev, int* nmatch
            int* extra = nullptr) {
     bool wait = false;
     for (OutBuf& o : outs)
-        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
+        if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     int tmp[2] = {0, 0};
     if (nmatches && nmatches_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
     if (extra && extra_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
     if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    m.d2h_flush();
     if (nmatches) *nmatches = tmp[0];
     if (extra) *extra = tmp[1];
     return ORBMI_OK;
@@ -515,7 +552,7 @@ int orbmi_compute_distinctive_descriptors(orbmi_matcher* h, const uint8_t* obs_d
     std::vector<OutBuf> outs;
     int* d_best = dev_out(m, best, (size_t)np, outs);
     uint8_t* d_out = dev_out(m, desc_out, (size_t)np * 32, outs);
-    if (!on_device(desc_out)) ORBMI_HIP(hipMemcpyAsync(d_out, desc_out, (size_t)np * 32, hipMemcpyHostToDevice, m.stream));
+    if (!on_device(desc_out)) ORBMI_HIP(m.h2d(d_out, desc_out, (size_t)np * 32));
     if ((rc = orbmi::launch_distinctive(m, d_desc, d_off, np, d_best, d_out))) return rc;
     return finish(m, outs, nullptr, nullptr);
 }
@@ -576,12 +613,13 @@ int orbmi_search_for_triangulation_batch(orbmi_matcher* h, const orbmi_frame_vie
         return rc;
     bool wait = false;
     for (OutBuf& o : outs)
-        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
+        if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     if (nmatches) {
-        ORBMI_HIP(hipMemcpyAsync(nmatches, d_counts, (size_t)npairs * sizeof(int), hipMemcpyDeviceToHost, m.stream));
+        ORBMI_HIP(m.d2h(nmatches, d_counts, (size_t)npairs * sizeof(int)));
         wait = true;
     }
     if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    m.d2h_flush();
     return ORBMI_OK;
 }
 
@@ -663,7 +701,7 @@ int orbmi_create_new_map_points(orbmi_matcher* h, const orbmi_frame_view* kf1, c
     memcpy(tab.data() + o_s2, S2.data(), sizeof(orbmi::tri::Side) * npairs);
     uint8_t* d_tab = (uint8_t*)m.stage(tab_bytes);
     if (!d_tab) return ORBMI_E_HIP;
-    ORBMI_HIP(hipMemcpyAsync(d_tab, tab.data(), tab_bytes, hipMemcpyHostToDevice, m.stream));
+    ORBMI_HIP(m.h2d(d_tab, tab.data(), tab_bytes));
     TriPair* d_pairs = (TriPair*)d_tab;
     const orbmi::tri::Side* d_S2 = (const orbmi::tri::Side*)(d_tab + o_s2);
     if ((rc = orbmi::launch_create_points(m, K1, has1, f1, npairs, nullptr, d_pairs, S1, d_S2, d_match, d_ok, d_x3d)))
@@ -720,12 +758,13 @@ int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* k
     if ((rc = orbmi::launch_fuse_multi(m, nkf, K.data(), d_k, d_mps, n_mp, th, d_bi, d_bd, d_cnt))) return rc;
     bool wait = false;
     for (OutBuf& o : outs)
-        if (o.bytes) { ORBMI_HIP(hipMemcpyAsync(o.user, o.dev, o.bytes, hipMemcpyDeviceToHost, m.stream)); wait = true; }
+        if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     if (ncandidates) {
-        ORBMI_HIP(hipMemcpyAsync(ncandidates, d_cnt, sizeof(int) * nkf, hipMemcpyDeviceToHost, m.stream));
+        ORBMI_HIP(m.d2h(ncandidates, d_cnt, sizeof(int) * nkf));
         wait = true;
     }
     if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    m.d2h_flush();
     return ORBMI_OK;
 }
 
@@ -754,15 +793,17 @@ int orbmi_fuse_search_refresh(orbmi_matcher* h, const uint8_t* obs_desc, const i
         int* d_best = dev_out(m, best, (size_t)nd, outs);
         d_dout = dev_out(m, desc_out, (size_t)nd * 32, outs);
         if (!on_device(desc_out))
-            ORBMI_HIP(hipMemcpyAsync(d_dout, desc_out, (size_t)nd * 32, hipMemcpyHostToDevice, m.stream));
+            ORBMI_HIP(m.h2d(d_dout, desc_out, (size_t)nd * 32));
         if ((rc = orbmi::launch_distinctive(m, d_desc, d_off, nd, d_best, d_dout))) return rc;
     }
     // the Fuse searches on records patched with the new descriptors
     if (nkf > 0 && n_mp > 0) {
         orbmi_mappoint* d_mps = (orbmi_mappoint*)m.stage(sizeof(orbmi_mappoint) * n_mp);
         if (!d_mps) return ORBMI_E_HIP;
-        ORBMI_HIP(hipMemcpyAsync(d_mps, mps, sizeof(orbmi_mappoint) * n_mp,
-                                 on_device(mps) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, m.stream));
+        if (on_device(mps))
+            ORBMI_HIP(hipMemcpyAsync(d_mps, mps, sizeof(orbmi_mappoint) * n_mp, hipMemcpyDeviceToDevice, m.stream));
+        else
+            ORBMI_HIP(m.h2d(d_mps, mps, sizeof(orbmi_mappoint) * n_mp));
         if (desc_from && nd > 0) {
             const int* d_from = dev_in(m, desc_from, (size_t)n_mp, &rc);
             if (rc) return rc;

@@ -105,12 +105,22 @@ struct Matcher {
     // the next generation, and waits only when that generation's last use (an event recorded
     // when the call after it began) has not finished -- so back-to-back asynchronous calls with
     // host inputs do not serialise on the host
+    // Every block has a pinned host mirror of the same size: host inputs are copied into the
+    // mirror and DMA'd from there, host outputs DMA'd into it and copied out after the call's
+    // wait (pageable hipMemcpyAsync goes through the runtime's own staging, one blocking chunked
+    // copy per array).  The mirror is reused with its block, under the same generation events.
     static constexpr int kArenaGens = 4;
-    struct Block { uint8_t* p; size_t size, used; };
+    struct Block { uint8_t* p; size_t size, used; uint8_t* h; };
     struct Gen { std::vector<Block> blocks; hipEvent_t ev = nullptr; bool pending = false; };
     Gen gens[kArenaGens];
     int gen = 0;
+    struct Pend { void* user; const uint8_t* mirror; size_t bytes; };
+    std::vector<Pend> pend;  // device-to-host copies landing in mirrors, copied out by d2h_flush
     void* stage(size_t bytes);
+    uint8_t* mirror(const void* d);  // host mirror of a staged device address, else nullptr
+    hipError_t h2d(void* d, const void* src, size_t bytes);    // stream-ordered upload
+    hipError_t d2h(void* user, const void* d, size_t bytes);   // stream-ordered read-back
+    void d2h_flush();                                          // after the stream's wait
     void arena_reset();
     void release();
 };

@@ -1512,7 +1512,7 @@ static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has
     int rc;
     if (pairs_host) {
         if ((rc = tri_pairs_prepare(m, KF1, npairs, pairs_host, match))) return rc;
-        ORBMI_HIP(hipMemcpyAsync(pairs_dev, pairs_host, sizeof(TriPair) * npairs, hipMemcpyHostToDevice, m.stream));
+        ORBMI_HIP(m.h2d(pairs_dev, pairs_host, sizeof(TriPair) * npairs));
     }
     // the histogram is read only by the orientation check
     if (check_ori) ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
@@ -1789,7 +1789,7 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
         K.best_dist = best_dist + (size_t)k * n;
         K.ncand = ncand + k;
     }
-    ORBMI_HIP(hipMemcpyAsync(kfs_dev, kfs_host, sizeof(FuseKF) * nkf, hipMemcpyHostToDevice, m.stream));
+    ORBMI_HIP(m.h2d(kfs_dev, kfs_host, sizeof(FuseKF) * nkf));
     hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.stream, kfs_dev, m.d_mkp_cell, ncap);
     if (n > 0)
         hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n,

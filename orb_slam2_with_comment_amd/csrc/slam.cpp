@@ -947,9 +947,14 @@ struct orbmi_slam {
             const void* sk = dslot ? (const void*)dev.kps[cf.dslot] : (const void*)kf.keys.data();
             const void* sd = dslot ? (const void*)dev.desc[cf.dslot] : (const void*)kf.desc.data();
             const void* su = dslot ? (const void*)dev.ur[cf.dslot] : (const void*)kf.ur.data();
-            if (hipMemcpy(kf.d_block, sk, bk, kind) == hipSuccess && hipMemcpy(kf.d_block + bk, sd, bd, kind) == hipSuccess &&
-                hipMemcpy(kf.d_block + bk + bd, su, bu, kind) == hipSuccess &&
-                hipMemcpy(kf.d_block + bk + bd + bu, dc.data(), 2 * bu, hipMemcpyHostToDevice) == hipSuccess) {
+            // four copies in stream order on the tracking stream (idle here: the frame's stages
+            // were read back), one wait -- instead of four blocking copies
+            const hipStream_t cs = tstream;
+            if (hipMemcpyAsync(kf.d_block, sk, bk, kind, cs) == hipSuccess &&
+                hipMemcpyAsync(kf.d_block + bk, sd, bd, kind, cs) == hipSuccess &&
+                hipMemcpyAsync(kf.d_block + bk + bd, su, bu, kind, cs) == hipSuccess &&
+                hipMemcpyAsync(kf.d_block + bk + bd + bu, dc.data(), 2 * bu, hipMemcpyHostToDevice, cs) == hipSuccess &&
+                hipStreamSynchronize(cs) == hipSuccess) {
                 kf.d_keys = (const orbmi_keypoint*)kf.d_block;
                 kf.d_desc = kf.d_block + bk;
                 kf.d_ur = (const float*)(kf.d_block + bk + bd);

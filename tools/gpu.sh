@@ -182,6 +182,17 @@ for step in "$@"; do
                 ORBMI_LIB=$B run ab_B$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
                 echo "A $(tail -1 $OUT/ab_A$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')  B $(tail -1 $OUT/ab_B$i.log | python -c 'import json,sys; print(json.load(sys.stdin)["value"])')" | tee -a $OUT/ab.txt
             done;;
+        absys=*)
+            # native loop (bench --mode system) A/B/... over library builds (absys=LIB1,LIB2,...), 3 rounds:
+            # frames/s, ATE, per-frame phases and the LocalMapping job split per keyframe
+            libs=${step#absys=}
+            for i in 1 2 3; do
+                for l in ${libs//,/ }; do
+                    n=$(basename $l .so)
+                    ORBMI_LIB=$l run absys_${n}_$i 300 python bench.py --mode system --no-cpu-baseline
+                    echo "$n $(tail -1 $OUT/absys_${n}_$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ate_rmse_m"], d["phase_ms_per_frame"]["total"], d["local_mapping_ms_per_keyframe"], d["synchronous_local_mapping"]["frames_per_s"])')" | tee -a $OUT/absys.txt
+                done
+            done;;
         ablba=*)
             # LocalBA (config 3) A/B/... over library builds: ablba=LIB1,LIB2,... alternating, 3 rounds
             libs=${step#ablba=}
