@@ -343,6 +343,11 @@ struct orbmi_vocabulary {
     void* d_vocab = nullptr;          // one allocation for all vocabulary arrays
     uint8_t* d_work = nullptr;        // keys, weights and staging of one transform
     size_t cap_work = 0;
+    // pinned host mirror of d_work: host descriptors go up from it, host outputs come back into it
+    // in one copy; in_ev marks the last upload from it (an asynchronous call may still be reading)
+    uint8_t* h_work = nullptr;
+    hipEvent_t in_ev = nullptr;
+    bool in_pending = false;
 };
 
 namespace {
@@ -415,6 +420,8 @@ void orbmi_vocabulary_destroy(orbmi_vocabulary* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->d_vocab) (void)hipFree(h->d_vocab);
     if (h->d_work) (void)hipFree(h->d_work);
+    if (h->h_work) (void)hipHostFree(h->h_work);
+    if (h->in_ev) (void)hipEventDestroy(h->in_ev);
     if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -473,11 +480,17 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
     if (need > h->cap_work) {
         ORBMI_HIP(hipStreamSynchronize(h->stream));
         if (h->d_work) (void)hipFree(h->d_work);
+        if (h->h_work) (void)hipHostFree(h->h_work);
         h->d_work = nullptr;
+        h->h_work = nullptr;
         h->cap_work = 0;
+        h->in_pending = false;
         ORBMI_HIP(hipMalloc((void**)&h->d_work, need));
+        ORBMI_HIP(hipHostMalloc((void**)&h->h_work, need, hipHostMallocDefault));
         h->cap_work = need;
     }
+    if (!h->in_ev) ORBMI_HIP(hipEventCreateWithFlags(&h->in_ev, hipEventDisableTiming));
+    auto mirror = [&](const void* d) { return h->h_work + ((const uint8_t*)d - h->d_work); };
     uint8_t* w = h->d_work;
     unsigned long long* key_w = (unsigned long long*)w; w += b_key;
     unsigned long long* key_n = (unsigned long long*)w; w += b_key;
@@ -491,7 +504,11 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
     int* s_cnt = (int*)w;
     const uint8_t* d_in = desc;
     if (n > 0 && !on_device(desc)) {
-        ORBMI_HIP(hipMemcpyAsync(in_stage, desc, (size_t)n * 32, hipMemcpyHostToDevice, h->stream));
+        if (h->in_pending) ORBMI_HIP(hipEventSynchronize(h->in_ev));  // the mirror's last upload
+        memcpy(mirror(in_stage), desc, (size_t)n * 32);
+        ORBMI_HIP(hipMemcpyAsync(in_stage, mirror(in_stage), (size_t)n * 32, hipMemcpyHostToDevice, h->stream));
+        ORBMI_HIP(hipEventRecord(h->in_ev, h->stream));
+        h->in_pending = true;
         d_in = in_stage;
     }
     bool host_out = false;
@@ -521,6 +538,26 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
                        (int*)o_feat, o_cnt);
     ORBMI_HIP(hipGetLastError());
     if (!host_out) return ORBMI_OK;
+    if (o_word == s_word && o_value == s_value && o_node == s_node && o_off == s_off && o_feat == s_feat &&
+        o_cnt == s_cnt) {
+        // every output on the host: the staged outputs (contiguous, s_word .. s_cnt) come back in
+        // one copy into the mirror and one wait, then the used parts are copied out
+        const uint8_t* lo = (const uint8_t*)s_word;
+        const size_t span = (size_t)((const uint8_t*)(s_cnt + 2) - lo);
+        ORBMI_HIP(hipMemcpyAsync(mirror(lo), lo, span, hipMemcpyDeviceToHost, h->stream));
+        ORBMI_HIP(hipStreamSynchronize(h->stream));
+        h->in_pending = false;
+        const int* hc = (const int*)mirror(s_cnt);
+        const size_t nwd = (size_t)hc[0], nnd = (size_t)hc[1];
+        const size_t nfeat = nnd > 0 ? (size_t)((const int32_t*)mirror(s_off))[nnd] : 0;
+        memcpy(bow_word, mirror(s_word), nwd * 4);
+        memcpy(bow_value, mirror(s_value), nwd * 8);
+        memcpy(fv_node, mirror(s_node), nnd * 4);
+        memcpy(fv_off, mirror(s_off), (nnd + 1) * 4);
+        memcpy(fv_feat, mirror(s_feat), nfeat * 4);
+        memcpy(counts, hc, 2 * sizeof(int));
+        return ORBMI_OK;
+    }
     int hc[2] = {0, 0};
     ORBMI_HIP(hipMemcpyAsync(hc, o_cnt, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     ORBMI_HIP(hipStreamSynchronize(h->stream));
