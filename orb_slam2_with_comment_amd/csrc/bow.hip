@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -343,6 +344,10 @@ struct orbmi_vocabulary {
     void* d_vocab = nullptr;          // one allocation for all vocabulary arrays
     uint8_t* d_work = nullptr;        // keys, weights and staging of one transform
     size_t cap_work = 0;
+    // one transform at a time: d_work is the call's staging, and Tracking (TrackReferenceKeyFrame)
+    // and LocalMapping (ProcessNewKeyFrame, run with the map lock released) may both transform
+    // on one handle -- the reference's Vocabulary::transform is const, safe from both threads
+    std::mutex mtx;
     // pinned host mirror of d_work: host descriptors go up from it, host outputs come back into it
     // in one copy; in_ev marks the last upload from it (an asynchronous call may still be reading)
     uint8_t* h_work = nullptr;
@@ -471,6 +476,7 @@ int orbmi_transform(orbmi_vocabulary* h, const uint8_t* desc, int n, const int* 
         return ORBMI_E_ARG;
     if (n > kBowMaxFeatures) return ORBMI_E_UNSUPPORTED;
     if (n_device && !on_device(n_device)) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> lock(h->mtx);
     ORBMI_HIP(hipSetDevice(h->device));
     const size_t nn = (size_t)std::max(n, 1);
     // work: keys (2 x 8 n), weights (8 n), staged input (32 n), staged outputs
