@@ -352,7 +352,8 @@ int orbmi_vocabulary_get_stream(orbmi_vocabulary* v, void** stream);
  * the FeatureVector as CSR (orbmi_feature_vector: node ids at level L - levelsup ascending,
  * feature indices ascending), counts[0] = words, counts[1] = nodes.  n_device (optional)
  * overrides n with a device-resident count <= n.  Arrays host or device; asynchronous on the
- * handle's stream when every output (counts included) is device memory.  n <= 8192. */
+ * handle's stream when every output (counts included) is device memory.  n <= 8192.  Calls on
+ * one handle from several threads are serialised (the reference's transform is const). */
 int orbmi_transform(orbmi_vocabulary* v, const uint8_t* desc, int n, const int* n_device, int levelsup,
                     uint32_t* bow_word, double* bow_value, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat,
                     int* counts);
