@@ -377,10 +377,17 @@ def run_track(a, rank, world, local, dist):
     ext = torch.cuda.ExternalStream(tr.stream_handle, device=tr.kps.device)        # extraction (E)
     trk = torch.cuda.ExternalStream(tr.track_stream_handle, device=tr.kps.device)  # tracking (T)
 
-    def step(i):
+    # the same frames in pinned host memory: the PCIe-inclusive pass DMAs each step's stereo pair
+    # to HBM on the extraction stream (stereo_kitti.cc:81-97 times TrackStereo from a host image)
+    from orb_slam2_with_comment_amd import _hip
+    h_imgs = _hip.PinnedBytes(S["imgs"].numel())
+    h_imgs.array[:] = S["imgs"].cpu().numpy().reshape(-1)
+
+    def step(i, host=False):
         f = 2 + i % F
-        tr.track(S["imgs"].data_ptr() + f * 2 * img_bytes, rows, cols, S["tcws"][f], S["lf_views"][f - 1],
-                 S["lf_pts"][f - 1].data_ptr(), S["mps"][f].data_ptr(), S["n_mp"][f])
+        src = (h_imgs.ptr if host else S["imgs"].data_ptr()) + f * 2 * img_bytes
+        tr.track(src, rows, cols, S["tcws"][f], S["lf_views"][f - 1], S["lf_pts"][f - 1].data_ptr(),
+                 S["mps"][f].data_ptr(), S["n_mp"][f], host=host)
         if xch is not None:  # config 4: exchange left features, match against the other streams
             xch.exchange()
         if i % KF_EVERY == 0:
@@ -498,6 +505,32 @@ def run_track(a, rank, world, local, dist):
         overlap.update(job_overlap(mapper.job_events))
     tr.frame_events = None
     mapper.job_events = None
+    # the PCIe-inclusive pass (not `value`: the contract's value has the inputs resident in HBM):
+    # the same steps with each stereo pair DMA'd from pinned host memory, overlapped with the
+    # previous frame's tracking; and the DMA alone, synchronised, per pair
+    ext_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    sync()
+    ext_ev[0].record(ext)
+    for i in range(16):
+        tr.upload(h_imgs.ptr + (2 + i % F) * 2 * img_bytes, rows, cols)
+    ext_ev[1].record(ext)
+    sync()
+    upload_ms = ext_ev[0].elapsed_time(ext_ev[1]) / 16
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i, host=True)
+    sync()
+    if dist:
+        dist.barrier()
+    dt_up = max_over_ranks(time.perf_counter() - t0, dist)
+    pcie = {"value": round(a.steps * world / dt_up, 3), "unit": "frames/s", "ms_per_step": round(dt_up / a.steps * 1e3, 4),
+            "upload_bytes_per_frame": 2 * img_bytes, "upload_ms_per_frame_alone": round(upload_ms, 4),
+            "upload_GBps_alone": round(2 * img_bytes / (upload_ms * 1e-3) / 1e9, 2),
+            "how": "each step's stereo pair hipMemcpyAsync'd from pinned host memory to HBM on the extraction "
+                   "stream, ahead of its extraction and overlapped with the previous frame's tracking"}
     n_lba = (a.steps + KF_EVERY - 1) // KF_EVERY
     x_matches = None
     if xch is not None:
@@ -541,6 +574,7 @@ def run_track(a, rank, world, local, dist):
             "kpts_desc_per_s": round(value * kp_per_frame, 1),
             "keypoints_per_frame": round(kp_per_frame, 1),
             "host_enqueue_ms_per_step_timed": round(host_s / a.steps * 1e3, 4),
+            "pcie_inclusive": pcie,
             **({"overlap": overlap} if overlap else {}),
             "matches_per_frame": {"last_frame": nm_lf, "local_map": nm_mp, "inliers": outcome["inliers"],
                                   "tracking_ok": outcome["ok"]},
@@ -569,6 +603,7 @@ def run_track(a, rank, world, local, dist):
         xch.close()
     mapper.close()
     tr.close()
+    h_imgs.close()
     return out
 
 
@@ -959,6 +994,7 @@ def run_system(a, rank, world, local, dist):
         st = slam.stats
         ok = sum(1 for x in st if x.get("state") == 2)
         counts = slam.counts()
+        counts["local_mapping_outcomes"] = slam.local_mapping_counts()
         ph = slam.phase_ms()
         counts["phase_ms_per_frame"] = {k: v for k, v in ph.items() if not k.startswith("lm_")}
         per_kf = len(st) / max(counts["keyframes"] - 1, 1)  # the first keyframe is not mapped
@@ -1021,6 +1057,9 @@ def run_system(a, rank, world, local, dist):
                         "0.25-0.29 m (tests/test_native_slam_gpu.py), the synchronous loop's below is exact",
             "frames_tracked": ok, "keyframes": counts["keyframes"],
             "local_ba_calls": counts["local_ba_calls"], "mappoints": counts["mappoints"],
+            "ba_skipped": counts["local_mapping_outcomes"]["ba_skipped"],
+            "ba_interrupted": counts["local_mapping_outcomes"]["ba_interrupted"],
+            "local_mapping_outcomes": counts["local_mapping_outcomes"],
             "local_mapping": "own thread, concurrent with Tracking (the reference's threading)",
             "phase_ms_per_frame": counts["phase_ms_per_frame"],
             "local_mapping_ms_per_keyframe": counts["local_mapping_ms_per_keyframe"],
@@ -1032,6 +1071,7 @@ def run_system(a, rank, world, local, dist):
                              "p90": round(float(np.percentile(s_times[W:], 90)) * 1e3, 3)},
                 "ate_rmse_m": round(s_ate, 5), "frames_tracked": s_ok, "keyframes": s_counts["keyframes"],
                 "local_ba_calls": s_counts["local_ba_calls"], "phase_ms_per_frame": s_counts["phase_ms_per_frame"],
+                "local_mapping_outcomes": s_counts["local_mapping_outcomes"],
                 "local_mapping_ms_per_keyframe": s_counts["local_mapping_ms_per_keyframe"]},
             "python_host_loop_on_gpu": py, "cpu_baseline": cpu, "host": host_info(),
         }

@@ -88,6 +88,35 @@ typedef struct orbmi_slam_ba_record {
 } orbmi_slam_ba_record;
 int orbmi_slam_get_local_ba_log(orbmi_slam* h, orbmi_slam_ba_record* out, int capacity, int* n);
 
+/* LocalMapping::Run outcomes since creation (either mode): out[0] jobs (keyframes processed),
+ * [1] SearchInNeighbors skipped and [2] LocalBundleAdjustment skipped because another keyframe
+ * was queued (CheckNewKeyFrames, src/LocalMapping.cc:79-90), [3] LocalBAs interrupted by
+ * mbAbortBA while optimising, [4] LocalBAs that saw it raised before starting. */
+int orbmi_slam_get_local_mapping_counts(orbmi_slam* h, int* out, int n);
+
+/* Recording of the schedule, the LocalBA log and the per-keyframe state log: off by default (they
+ * are replay / test hooks and grow with the run).  Turn it on before the first frame. */
+int orbmi_slam_set_recording(orbmi_slam* h, int on);
+
+/* Per-keyframe state of the map after each stage of the keyframe's LocalMapping job, in the
+ * mapping thread's order (either mode; recording on).  A replay of the schedule computes the same
+ * record at the same point and names the first keyframe and stage where the maps part
+ * (system.StereoSLAM.replay_schedule), instead of a lock label many events later.  Hashes are
+ * FNV-1a style over 32-bit words: h = (h ^ w) * 16777619, h0 = 2166136261. */
+#define ORBMI_KF_STATE_PROCESS 0  /* after ProcessNewKeyFrame: a = BowVector words (-1 without a
+                                     FeatureVector), b = hash of the FeatureVector (node ids, CSR
+                                     offsets, feature indices), c = hash of the keyframe's slots */
+#define ORBMI_KF_STATE_CREATE 1   /* after CreateNewMapPoints: a = new points, b = map points ever
+                                     created, c = slot hash                                     */
+#define ORBMI_KF_STATE_FUSE 2     /* after SearchInNeighbors (when it ran): a = Fuse map updates
+                                     (Replace calls + AddMapPoint), b = filled slots, c = slot hash */
+typedef struct orbmi_slam_kf_state {
+    int32_t keyframe, stage;
+    int32_t sched_index;           /* the schedule event of the section it was taken in (-1 sync) */
+    int32_t a, b, c;
+} orbmi_slam_kf_state;
+int orbmi_slam_get_keyframe_state_log(orbmi_slam* h, orbmi_slam_kf_state* out, int capacity, int* n);
+
 /* Wall time (ms) accumulated per phase of orbmi_slam_track_stereo since creation, and the frame
  * count: ms[0] Frame constructor (image upload, L+R extraction, stereo, read-back), [1] waiting
  * for the map lock (concurrent LocalMapping), [2] SearchByProjection(CF, LF) incl. the retry,
@@ -98,7 +127,11 @@ int orbmi_slam_get_local_ba_log(orbmi_slam* h, orbmi_slam_ba_record* out, int ca
  * [12] MapPointCulling, [13] CreateNewMapPoints, [14] SearchInNeighbors, [15]
  * LocalBundleAdjustment, [16] KeyFrameCulling, [17] all of LocalMapping::Run; within those,
  * [18] the orbmi_create_new_map_points calls, [19] the Fuse search calls, [20] the
- * ComputeDistinctiveDescriptors calls. */
+ * ComputeDistinctiveDescriptors calls; [21] the mapping thread's waits to re-take the map lock
+ * after a device call, [22] SearchInNeighbors' set-up (targets, records, IsInKeyFrame masks),
+ * [23] its per-target check of changed records, [24] its Fuse replays, [25] UpdateNormalAndDepth
+ * loops, [26] UpdateConnections, [27] the observation rows of ComputeDistinctiveDescriptors,
+ * [28] LocalBA's graph assembly, [29] its device call, [30] its write-back. */
 int orbmi_slam_get_phase_ms(orbmi_slam* h, double* ms, int n, long* frames);
 
 #ifdef __cplusplus

@@ -124,6 +124,9 @@ _PROTOS = {
     "orbmi_slam_get_stats": (_i, [_vp, _i, _vp]),
     "orbmi_slam_get_schedule": (_i, [_vp, _vp, _i, C.POINTER(_i)]),
     "orbmi_slam_get_local_ba_log": (_i, [_vp, _vp, _i, C.POINTER(_i)]),
+    "orbmi_slam_get_keyframe_state_log": (_i, [_vp, _vp, _i, C.POINTER(_i)]),
+    "orbmi_slam_set_recording": (_i, [_vp, _i]),
+    "orbmi_slam_get_local_mapping_counts": (_i, [_vp, _vp, _i]),
     "orbmi_slam_get_counts": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
     "orbmi_slam_get_trajectory": (_i, [_vp, _vp, _vp, _vp, _i, C.POINTER(_i)]),
     "orbmi_slam_save_trajectory_kitti": (_i, [_vp, C.c_char_p]),

@@ -15,7 +15,8 @@ from __future__ import annotations
 import ctypes as C
 
 _vp, _i, _u, _sz = C.c_void_p, C.c_int, C.c_uint, C.c_size_t
-HIP_MEMCPY_DEVICE_TO_HOST = 2  # hipMemcpyKind
+HIP_MEMCPY_HOST_TO_DEVICE = 1  # hipMemcpyKind
+HIP_MEMCPY_DEVICE_TO_HOST = 2
 HIP_EVENT_DISABLE_TIMING = 0x2
 
 PROTOS = {
@@ -92,3 +93,30 @@ class PinnedWords:
         if self._h:
             self._rt.hipHostFree(self._h)
             self._h = _vp()
+
+
+class PinnedBytes:
+    """n bytes of pinned host memory (hipHostMalloc) with a numpy view: the source of
+    asynchronous host-to-device copies on library streams (a frame's image pair DMA'd to HBM,
+    pipeline.StereoTracker.track(host=True)).  The owner keeps it alive until every copy from it
+    has completed."""
+
+    def __init__(self, n: int):
+        import numpy as np
+        self._rt = runtime()
+        self._h = _vp()
+        _ok("hipHostMalloc", self._rt.hipHostMalloc(C.byref(self._h), max(int(n), 1), 0))
+        self.n = int(n)
+        self.ptr = self._h.value
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.n, 1)).from_address(self.ptr))[:self.n]
+
+    def close(self) -> None:
+        if self._h is not None and self._h.value:
+            self.array = None
+            _ok("hipHostFree", self._rt.hipHostFree(self._h))
+            self._h = None
+
+
+def memcpy_h2d_async(dst_device_ptr: int, src_host_ptr: int, nbytes: int, stream_handle: int) -> None:
+    _ok("hipMemcpyAsync", runtime().hipMemcpyAsync(_vp(dst_device_ptr), _vp(src_host_ptr), int(nbytes),
+                                                   HIP_MEMCPY_HOST_TO_DEVICE, _vp(stream_handle)))

@@ -691,9 +691,8 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
             for (int k = 0; k < kGreedyQPer; k++) {
                 const int q = tid + k * kGreedyThreads;
                 nr[k] = res[k];
-                // A query is evaluated again only when a prefix keypoint changed claimers in the
-                // last round (or its last evaluation went past the prefix): otherwise every
-                // taken-bit it reads is the same, and so is its result.  Whole waves skip.
+                // every query is evaluated in every round (a per-wave skip of unchanged queries
+                // measured no gain: after round 0 the re-evaluations are spread over all waves)
                 if (q >= nq) continue;
                 // the prefix's claim words read at once (independent LDS reads, one latency)
                 int cv[kGreedyPre];

@@ -114,6 +114,7 @@ void quaternion_xyzw(const float R[9], float q_out[4]) {
 // DBoW2::FeatureVector as CSR (orbmi_feature_vector)
 struct FeatVec {
     bool valid = false;
+    int words = 0;  // the BowVector's word count (kept for the per-keyframe state record)
     std::vector<uint32_t> node;
     std::vector<int32_t> off, feat;
     orbmi_feature_vector view() const {
@@ -232,7 +233,14 @@ enum Phase { PH_FRAME, PH_LOCK, PH_LF_SEARCH, PH_LF_POSE, PH_LOCAL_UPDATE, PH_LO
              PH_LM_PROCESS, PH_LM_CULL, PH_LM_CREATE, PH_LM_FUSE, PH_LM_BA, PH_LM_KFCULL, PH_LM_TOTAL,
              // inside them: the device calls of CreateNewMapPoints, of the Fuse searches, and of
              // ComputeDistinctiveDescriptors (each with its staging and read-back)
-             PH_LM_CREATE_CALL, PH_LM_FUSE_CALL, PH_LM_DISTINCTIVE_CALL, PH_COUNT };
+             PH_LM_CREATE_CALL, PH_LM_FUSE_CALL, PH_LM_DISTINCTIVE_CALL,
+             // the mapping thread's host work, finer: waits to re-take the map lock after a device
+             // call; SearchInNeighbors' set-up (targets, records), its per-target check of changed
+             // records, its Fuse replays; UpdateNormalAndDepth loops; UpdateConnections; the
+             // observation rows of ComputeDistinctiveDescriptors; LocalBA's graph assembly, its
+             // device call, its write-back
+             PH_LM_LOCK, PH_LM_SIN_PREP, PH_LM_SIN_REDO, PH_LM_SIN_REPLAY, PH_LM_NORMALS, PH_LM_CONNECTIONS,
+             PH_LM_OBSROWS, PH_LM_BA_GATHER, PH_LM_BA_CALL, PH_LM_BA_WRITEBACK, PH_COUNT };
 struct PhaseTimer {
     double* acc;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
@@ -299,6 +307,10 @@ struct orbmi_slam {
     std::vector<uint8_t> lost;
     std::vector<orbmi_slam_frame_stats> stats;
     int ba_calls = 0;
+    // LocalMapping::Run outcomes (orbmi_slam_get_local_mapping_counts): jobs, SearchInNeighbors
+    // and LocalBA skipped because a keyframe was queued (src/LocalMapping.cc:79-90), LocalBAs that
+    // saw mbAbortBA while optimising / before starting
+    int lm_jobs = 0, sin_skipped = 0, ba_skipped = 0, ba_interrupted = 0, ba_aborted = 0;
     int resets = 0;  // Tracking::Reset calls (lost with <= 5 keyframes in the map)
     std::vector<float> level_sigma2;  // mvLevelSigma2
     std::vector<int> recent_mps;      // mlpRecentAddedMapPoints
@@ -321,7 +333,8 @@ struct orbmi_slam {
         int* cnt[kSlots] = {};
         float* ur[kSlots] = {};
         float* dep[kSlots] = {};
-        int seq = 0;               // extractions enqueued (slot = seq % kSlots)
+        // A slot is chosen per extraction (free_slot): never the current frame's nor the last
+        // frame's, which tracking reads on its stream while the next pair is extracted
         // the extraction enqueued ahead (orbmi_slam_track_stereo_ahead) and not yet collected
         struct Ahead { bool on = false; int slot = -1, rows = 0, cols = 0; size_t step = 0; const uint8_t *L = nullptr, *R = nullptr; } ahead;
         // pinned host mirror of a slot's left outputs
@@ -345,7 +358,7 @@ struct orbmi_slam {
         const uint8_t *L = nullptr, *R = nullptr;
         int rows = 0, cols = 0;
         size_t step = 0;
-        int* slot = nullptr;
+        int slot = -1;
     } fw;
     const bool inline_frame = getenv("ORBMI_SLAM_INLINE_FRAME") != nullptr;
     void frame_worker_run() {
@@ -363,7 +376,7 @@ struct orbmi_slam {
             fw.cv.notify_all();
         }
     }
-    void frame_post(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int* slot) {
+    void frame_post(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int slot) {
         std::lock_guard<std::mutex> g(fw.mtx);
         if (!fw.th.joinable()) fw.th = std::thread([this] { frame_worker_run(); });
         fw.L = L; fw.R = R; fw.rows = rows; fw.cols = cols; fw.step = step; fw.slot = slot;
@@ -533,8 +546,12 @@ struct orbmi_slam {
     // the schedule (orbmi_slam_get_schedule): every acquisition of map_mtx with the mapping thread
     // running, logged by the thread that took it (so map_mtx guards the log too)
     std::vector<orbmi_slam_event> sched;
+    // the schedule, the LocalBA log and the per-keyframe state log are kept only when recording
+    // is on (orbmi_slam_set_recording, before the first frame): a replay / test hook, not part of
+    // the production path
+    bool recording = false;
     void log_section(int label, int arg) {
-        if (async_lm()) sched.push_back(orbmi_slam_event{on_mapping_thread ? 1 : 0, label, arg});
+        if (recording && async_lm()) sched.push_back(orbmi_slam_event{on_mapping_thread ? 1 : 0, label, arg});
         if (lock_profile && on_mapping_thread) { hold_label = label; hold_t0 = std::chrono::steady_clock::now(); }
     }
     // ORBMI_SLAM_LOCK_PROFILE=1 (development aid): how long the mapping thread holds the map lock
@@ -561,6 +578,22 @@ struct orbmi_slam {
                     kv.second.second);
     }
     std::vector<orbmi_slam_ba_record> ba_log;  // orbmi_slam_get_local_ba_log (under map_mtx)
+    // orbmi_slam_get_keyframe_state_log (under map_mtx): the map as LocalMapping left it after each
+    // stage of a keyframe's job, so a replay names the first keyframe and stage whose map differs
+    std::vector<orbmi_slam_kf_state> kf_state;
+    static uint32_t fnv_mix(uint32_t h, uint32_t v) { return (h ^ v) * 16777619u; }
+    static constexpr uint32_t kFnv0 = 2166136261u;
+    uint32_t slot_hash(int k) const {  // the keyframe's map-point slots (ids, -1 empty)
+        uint32_t h = kFnv0;
+        for (int m : kfs[k].mps) h = fnv_mix(h, (uint32_t)m);
+        return h;
+    }
+    void log_state(int k, int stage, int a, uint32_t b, uint32_t c) {
+        if (!recording) return;
+        const int at = async_lm() ? (int)sched.size() - 1 : -1;
+        kf_state.push_back(orbmi_slam_kf_state{k, stage, at, a, (int32_t)b, (int32_t)c});
+    }
+    int fuse_ops = 0;  // map updates made by Fuse replays (Replace that moved observations, AddMapPoint)
 
     // ---- Frame views (include/Frame.h members the matchers read) --------------------------
     orbmi_frame_view view(const std::vector<orbmi_keypoint>& keys, const std::vector<uint8_t>& desc,
@@ -595,7 +628,14 @@ struct orbmi_slam {
     // Frame::Frame (stereo, src/Frame.cc:58-100): ORBextractor on both images (one batch on the
     // left handle) and ComputeStereoMatches into the next device slot, enqueued on the extractor's
     // stream with the read-back of the left outputs into pinned memory (frame_collect waits)
-    int frame_enqueue(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int* slot_out) {
+    // the first device slot that is neither a nor b (kSlots = 3 leaves at least one)
+    static int free_slot(int a, int b) {
+        for (int k = 0; k < kSlots; k++)
+            if (k != a && k != b) return k;
+        return -1;
+    }
+    int frame_enqueue(const uint8_t* L, const uint8_t* R, int rows, int cols, size_t step, int k) {
+        if (k < 0 || k >= kSlots) return ORBMI_E_ARG;
         const size_t img = (size_t)rows * cols;
         if (2 * img > dev.img_bytes) {
             if (dev.img) (void)hipFree(dev.img);
@@ -629,7 +669,7 @@ struct orbmi_slam {
             std::memcpy(dev.h_img + img + (size_t)r * cols, R + (size_t)r * step, cols);
         }
         if (hipMemcpyAsync(dev.img, dev.h_img, 2 * img, hipMemcpyHostToDevice, xstream) != hipSuccess) return ORBMI_E_HIP;
-        const int k = dev.seq++ % kSlots, cap = dev.cap;
+        const int cap = dev.cap;
         SLAM_CHECK(orbmi_extract_batch_device(left, dev.img, 2, rows, cols, cols, img, dev.kps[k], dev.desc[k], dev.cnt[k],
                                               cap));
         SLAM_CHECK(orbmi_compute_stereo_matches_batch_device(left, s.bf, s.fx, dev.ur[k], dev.dep[k]));
@@ -640,7 +680,6 @@ struct orbmi_slam {
             hipMemcpyAsync(dev.h_ur, dev.ur[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess ||
             hipMemcpyAsync(dev.h_dep, dev.dep[k], (size_t)cap * sizeof(float), hipMemcpyDeviceToHost, xstream) != hipSuccess)
             return ORBMI_E_HIP;
-        *slot_out = k;
         return ORBMI_OK;
     }
 
@@ -669,8 +708,9 @@ struct orbmi_slam {
             dev.ahead.on = false;
             if (hipStreamSynchronize(xstream) != hipSuccess) return ORBMI_E_HIP;
         }
-        int slot = -1;
-        SLAM_CHECK(frame_enqueue(L, R, rows, cols, step, &slot));
+        // the last frame's slot is read by this frame's tracking: extract into another one
+        const int slot = free_slot(last_frame.dslot, -1);
+        SLAM_CHECK(frame_enqueue(L, R, rows, cols, step, slot));
         return frame_collect(cf, slot);
     }
 
@@ -690,8 +730,11 @@ struct orbmi_slam {
             SLAM_CHECK(frame_stereo(cf, L, R, rows, cols, step));
         }
         if (nL && nR) {
-            if (inline_frame) SLAM_CHECK(frame_enqueue(nL, nR, rows, cols, step, &a.slot));
-            else frame_post(nL, nR, rows, cols, step, &a.slot);  // joined before the call returns
+            // tracking this frame reads cf's slot and the last frame's while the next pair is
+            // extracted; the next call then tracks a.slot against cf's
+            a.slot = free_slot(cf.dslot, last_frame.dslot);
+            if (inline_frame) SLAM_CHECK(frame_enqueue(nL, nR, rows, cols, step, a.slot));
+            else frame_post(nL, nR, rows, cols, step, a.slot);  // joined before the call returns
             a.on = true;
             a.L = nL;
             a.R = nR;
@@ -700,6 +743,13 @@ struct orbmi_slam {
             a.step = step;
         }
         return ORBMI_OK;
+    }
+
+    // forget the pair enqueued ahead (its extraction drained first)
+    void drop_ahead() {
+        if (dev.ahead.on && xstream) (void)hipStreamSynchronize(xstream);
+        dev.ahead.on = false;
+        dev.ahead.slot = -1;
     }
 
     void free_dev() {
@@ -751,6 +801,7 @@ struct orbmi_slam {
         SLAM_CHECK(orbmi_transform(voc, desc.data(), n, nullptr, 4, word.data(), value.data(), node.data(), off.data(),
                                    feat.data(), counts));
         const int nn = counts[1];
+        fv.words = counts[0];
         fv.node.assign(node.begin(), node.begin() + nn);
         fv.off.assign(off.begin(), off.begin() + nn + 1);
         fv.feat.assign(feat.begin(), feat.begin() + off[nn]);
@@ -801,6 +852,14 @@ struct orbmi_slam {
         sort_covisible(kfs[k]);
     }
 
+    void normals(const std::vector<int>& pts) {  // UpdateNormalAndDepth of each (timed)
+        PhaseTimer pt(&phase_ms[PH_LM_NORMALS]);
+        for (int m : pts) update_normal_and_depth(m);
+    }
+    void connections(int k) {
+        PhaseTimer pt(&phase_ms[PH_LM_CONNECTIONS]);
+        update_connections(k);
+    }
     void update_connections(int k) {  // KeyFrame::UpdateConnections (src/KeyFrame.cc:285-371)
         std::map<int, int> counter;
         for (int m : kfs[k].mps) {
@@ -905,7 +964,10 @@ struct orbmi_slam {
     int distinctive(const std::vector<int>& pts) {
         std::vector<uint8_t> rows;
         std::vector<int32_t> off;
-        obs_rows(pts, rows, off);
+        {
+            PhaseTimer pt(&phase_ms[PH_LM_OBSROWS]);
+            obs_rows(pts, rows, off);
+        }
         if (rows.empty()) return ORBMI_OK;
         const int np = (int)pts.size();
         std::vector<int32_t> best(std::max(np, 1));
@@ -990,6 +1052,7 @@ struct orbmi_slam {
         held_lock->unlock();
         const int rc = f();
         if (on_mapping_thread) {
+            PhaseTimer pt(&phase_ms[PH_LM_LOCK]);
             held_lock->lock();
         } else {
             PhaseTimer pt(&phase_ms[PH_LOCK]);
@@ -1153,7 +1216,7 @@ struct orbmi_slam {
                         lm_busy = true;  // SetAcceptKeyFrames(false)
                     }
                 }
-                sched.back().arg = k;
+                if (recording) sched.back().arg = k;
                 if (k >= 0) {
                     held_lock = &m;
                     rc = local_mapping(k);
@@ -1211,19 +1274,38 @@ struct orbmi_slam {
                 recent_mps.push_back(m);  // the new stereo points the Tracking inserted
             }
         }
-        for (int m : updated) update_normal_and_depth(m);
+        normals(updated);
         SLAM_CHECK(distinctive(updated));
-        update_connections(k);
+        connections(k);
+        if (recording) {  // ProcessNewKeyFrame's outcome: BowVector words, FeatureVector, slots
+            const FeatVec& fv = kfs[k].fv;
+            uint32_t h = kFnv0;
+            for (uint32_t v : fv.node) h = fnv_mix(h, v);
+            for (int32_t v : fv.off) h = fnv_mix(h, (uint32_t)v);
+            for (int32_t v : fv.feat) h = fnv_mix(h, (uint32_t)v);
+            log_state(k, ORBMI_KF_STATE_PROCESS, fv.valid ? fv.words : -1, h, slot_hash(k));
+        }
         next(PH_LM_CULL);
         map_point_culling(k);
         if (s.local_mapping) {
             next(PH_LM_CREATE);
+            const size_t nmp0 = mps.size();
             SLAM_CHECK(create_new_map_points(k));
+            log_state(k, ORBMI_KF_STATE_CREATE, (int)(mps.size() - nmp0), (uint32_t)mps.size(), slot_hash(k));
             next(PH_LM_FUSE);
-            if (!new_keyframes_queued()) SLAM_CHECK(search_in_neighbors(k));
+            if (new_keyframes_queued()) sin_skipped++;
+            else {
+                fuse_ops = 0;
+                SLAM_CHECK(search_in_neighbors(k));
+                int filled = 0;
+                for (int m : kfs[k].mps) filled += m >= 0;
+                log_state(k, ORBMI_KF_STATE_FUSE, fuse_ops, (uint32_t)filled, slot_hash(k));
+            }
         }
         set_abort_ba(0);
-        if (!new_keyframes_queued()) {
+        lm_jobs++;
+        if (new_keyframes_queued()) ba_skipped++;
+        else {
             next(PH_LM_BA);
             if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
             next(PH_LM_KFCULL);
@@ -1351,7 +1433,7 @@ struct orbmi_slam {
         }
         // per point, so one batch for all pairs gives the reference's per-pair results
         SLAM_CHECK(distinctive(fresh));
-        for (int m : fresh) update_normal_and_depth(m);
+        normals(fresh);
         return ORBMI_OK;
     }
 
@@ -1490,14 +1572,16 @@ struct orbmi_slam {
             if (in >= 0) {
                 if (!mps[in].bad) {
                     if (mps[in].nobs > mps[m].nobs) {
-                        if (replace(m, in)) dirty.insert(in);
+                        if (replace(m, in)) { dirty.insert(in); fuse_ops++; }
                     } else if (replace(in, m)) {
                         dirty.insert(m);
+                        fuse_ops++;
                     }
                 }
             } else {
                 add_observation(m, k, b);
                 kfs[k].mps[b] = m;
+                fuse_ops++;
             }
         }
     }
@@ -1538,6 +1622,7 @@ struct orbmi_slam {
             if (m >= 0) pts.push_back(m);
         const int nt = (int)targets.size(), np = (int)pts.size();
         if (nt == 0 || np == 0) return ORBMI_OK;
+        auto* prep = new PhaseTimer(&phase_ms[PH_LM_SIN_PREP]);
         std::vector<orbmi_mappoint> rec0(np);
         for (int j = 0; j < np; j++) rec0[j] = fuse_record(pts[j]);
         std::vector<uint8_t> in0((size_t)nt * np);
@@ -1550,6 +1635,7 @@ struct orbmi_slam {
         }
         std::vector<int32_t> best((size_t)nt * np), dist((size_t)nt * np);
         orbmi_matcher* mt = lmm();
+        delete prep;
         SLAM_CHECK(unlocked(ORBMI_SCHED_L_FUSE_BATCH, -1, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
             return orbmi_fuse_search_batch(mt, nt, views.data(), rec0.data(), in0.data(), np, 3.f, best.data(),
@@ -1610,6 +1696,7 @@ struct orbmi_slam {
             }
             int32_t* row = best.data() + (size_t)t * np;
             std::vector<int> redo_pts, redo_j;
+            auto* rt = new PhaseTimer(&phase_ms[PH_LM_SIN_REDO]);
             for (int j = 0; j < np; j++) {
                 const int m = pts[j];
                 // the replay skips bad points and points already in the target (observations are
@@ -1621,11 +1708,13 @@ struct orbmi_slam {
                     redo_j.push_back(j);
                 }
             }
+            delete rt;
             if (!redo_pts.empty()) {
                 std::vector<int32_t> b2;
                 SLAM_CHECK(fuse_search(kt, redo_pts, b2));
                 for (size_t q = 0; q < redo_j.size(); q++) row[redo_j[q]] = b2[q];
             }
+            PhaseTimer rp(&phase_ms[PH_LM_SIN_REPLAY]);
             fuse_replay(kt, pts, row, dirty);
         }
         return ORBMI_OK;
@@ -1663,8 +1752,8 @@ struct orbmi_slam {
         for (int m : kfs[k].mps)
             if (m >= 0 && !mps[m].bad && seen_pt.insert(m).second) upd.push_back(m);
         SLAM_CHECK(distinctive(upd));
-        for (int m : upd) update_normal_and_depth(m);
-        update_connections(k);
+        normals(upd);
+        connections(k);
         return ORBMI_OK;
     }
 
@@ -1752,6 +1841,7 @@ struct orbmi_slam {
     // Optimizer::LocalBundleAdjustment: the graph as src/Optimizer.cc:486-683 assembles it
     // (system/optimizer.gather_local_ba), the optimisation on the GPU, the write-back (:776-805)
     int local_bundle_adjustment(int k) {
+        auto* gt = new PhaseTimer(&phase_ms[PH_LM_BA_GATHER]);
         std::vector<int> lkf{k};
         std::set<int> local_set{k};
         for (int c : kfs[k].covisible) {
@@ -1799,6 +1889,7 @@ struct orbmi_slam {
                 E.push_back(orbmi_ba_edge{j, it->second, kp.x, kp.y, kf.ur[o.second], inv_level_sigma2[kp.octave]});
                 e_ref.push_back({lmp[j], o.first});
             }
+        delete gt;
         if (E.empty()) return ORBMI_OK;
         orbmi_ba_problem prob{(int)K.size(), (int)P.size(), (int)E.size(), K.data(), P.data(), E.data()};
         std::vector<float> tcw(K.size() * 16), pos(P.size() * 3 + 3);
@@ -1812,19 +1903,28 @@ struct orbmi_slam {
         if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves
             hold_end();
             held_lock->unlock();
-            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
+            {
+                PhaseTimer ct(&phase_ms[PH_LM_BA_CALL]);
+                rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
+            }
+            PhaseTimer lt(&phase_ms[PH_LM_LOCK]);
             update_guard = std::unique_lock<std::mutex>(update_mtx);  // (lock order: update, map)
             held_lock->lock();
             log_section(ORBMI_SCHED_L_BA, k);
         } else {
+            PhaseTimer ct(&phase_ms[PH_LM_BA_CALL]);
             rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
         }
         SLAM_CHECK(rc);
+        PhaseTimer wb(&phase_ms[PH_LM_BA_WRITEBACK]);
         ba_calls++;
+        if (res.aborted) ba_aborted++;
+        else if (res.stop_check >= 0) ba_interrupted++;
         {
             int erased = 0;
             for (uint8_t x : erase) erased += x != 0;
-            ba_log.push_back(orbmi_slam_ba_record{k, res.stop_check, res.aborted, res.checks,
+            if (recording)
+                ba_log.push_back(orbmi_slam_ba_record{k, res.stop_check, res.aborted, res.checks,
                                                   {res.iterations[0], res.iterations[1]}, (int)E.size(), erased});
         }
         if (res.aborted) return ORBMI_OK;  // src/Optimizer.cc:685-687: no write-back
@@ -2577,14 +2677,16 @@ static int track_stereo(orbmi_slam* h, const uint8_t* left, const uint8_t* right
         int rc = ahead ? h->frame_stereo_ahead(cf, left, right, rows, cols, step, next_left, next_right)
                        : h->frame_stereo(cf, left, right, rows, cols, step);
         if (rc) {
-            (void)h->frame_join();
+            if (h->frame_join() != ORBMI_OK) h->drop_ahead();
             return rc;
         }
     }
     const int rc = track_frame(h, cf, tcw_out, has_pose);
     // the next pair's enqueue (frame_post) has finished before the call returns: the caller's
-    // images are not read afterwards
+    // images are not read afterwards.  A failed enqueue leaves its slot and the pinned read-back
+    // buffers partly written: the pair is dropped, so the next call extracts it again
     const int jrc = h->frame_join();
+    if (jrc != ORBMI_OK) h->drop_ahead();
     return rc ? rc : jrc;
 }
 
@@ -2605,6 +2707,30 @@ int orbmi_slam_get_schedule(orbmi_slam* h, orbmi_slam_event* out, int capacity, 
     *n = (int)h->sched.size();
     if (capacity < *n) return ORBMI_E_CAP;
     if (*n) std::memcpy(out, h->sched.data(), sizeof(orbmi_slam_event) * (size_t)*n);
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_local_mapping_counts(orbmi_slam* h, int* out, int n) {
+    if (!h || !out || n < 0) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    const int v[5] = {h->lm_jobs, h->sin_skipped, h->ba_skipped, h->ba_interrupted, h->ba_aborted};
+    for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+    return ORBMI_OK;
+}
+
+int orbmi_slam_set_recording(orbmi_slam* h, int on) {
+    if (!h) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    h->recording = on != 0;
+    return ORBMI_OK;
+}
+
+int orbmi_slam_get_keyframe_state_log(orbmi_slam* h, orbmi_slam_kf_state* out, int capacity, int* n) {
+    if (!h || !n) return ORBMI_E_ARG;
+    std::lock_guard<std::mutex> map_guard(h->map_mtx);
+    *n = (int)h->kf_state.size();
+    if (capacity < *n) return ORBMI_E_CAP;
+    if (*n) std::memcpy(out, h->kf_state.data(), sizeof(orbmi_slam_kf_state) * (size_t)*n);
     return ORBMI_OK;
 }
 

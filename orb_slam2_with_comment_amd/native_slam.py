@@ -36,7 +36,9 @@ class NativeStereoSLAM:
     one dict per frame with the counters the stage that ran produced."""
 
     def __init__(self, settings, device: int = 0, vocabulary=None, local_ba: bool = True, local_mapping: bool = True,
-                 async_local_mapping: bool = False):
+                 async_local_mapping: bool = False, record: bool = False):
+        """record: keep the schedule, the LocalBA log and the per-keyframe state log
+        (orbmi_slam_set_recording) for schedule(), local_ba_log() and keyframe_state_log()."""
         from .settings import Settings, load_settings
         s = settings if isinstance(settings, Settings) else load_settings(settings)
         if s.width <= 0 or s.height <= 0:
@@ -55,6 +57,8 @@ class NativeStereoSLAM:
                                                            self._voc._h if self._voc else None, C.byref(h)))
         self._h = h
         self._tcw = np.zeros(16, np.float32)
+        if record:
+            check("orbmi_slam_set_recording", lib().orbmi_slam_set_recording(h, 1))
 
     def TrackStereo(self, imLeft, imRight, timestamp: float, next_pair=None):
         """System::TrackStereo.  next_pair = (imLeft, imRight) of the next call: its Frame
@@ -138,7 +142,9 @@ class NativeStereoSLAM:
     PHASES = ("frame_ctor", "map_lock_wait", "lf_search", "lf_pose", "local_kf_points", "local_records",
               "frustum", "local_search", "local_pose", "keyframe", "total", "lm_process", "lm_point_culling",
               "lm_create_points", "lm_search_in_neighbors", "lm_local_ba", "lm_keyframe_culling", "lm_total",
-              "lm_create_points_call", "lm_fuse_search_calls", "lm_distinctive_calls")
+              "lm_create_points_call", "lm_fuse_search_calls", "lm_distinctive_calls",
+              "lm_lock_wait", "lm_sin_prep", "lm_sin_redo_check", "lm_sin_replay", "lm_normals", "lm_connections",
+              "lm_obs_rows", "lm_ba_gather", "lm_ba_call", "lm_ba_writeback")
 
     def phase_ms(self):
         """Mean wall ms per tracked frame of each phase of TrackStereo (orbmi_slam_get_phase_ms)."""
@@ -156,6 +162,19 @@ class NativeStereoSLAM:
         """Per LocalBundleAdjustment call: int32 rows of (keyframe, stop_check, aborted, checks,
         iterations0, iterations1, edges, erased) (orbmi_slam_get_local_ba_log)."""
         return self._records("orbmi_slam_get_local_ba_log", 8)
+
+    def local_mapping_counts(self) -> dict:
+        """LocalMapping::Run outcomes (orbmi_slam_get_local_mapping_counts)."""
+        v = np.zeros(5, np.int32)
+        check("orbmi_slam_get_local_mapping_counts",
+              lib().orbmi_slam_get_local_mapping_counts(self._h, v.ctypes.data, len(v)))
+        return dict(zip(("jobs", "search_in_neighbors_skipped", "ba_skipped", "ba_interrupted", "ba_aborted"),
+                        (int(x) for x in v)))
+
+    def keyframe_state_log(self) -> np.ndarray:
+        """Per keyframe and LocalMapping stage: int32 rows of (keyframe, stage, schedule event, a,
+        b, c) (orbmi_slam_get_keyframe_state_log; include/orbmi_debug.h ORBMI_KF_STATE_*)."""
+        return self._records("orbmi_slam_get_keyframe_state_log", 6)
 
     def _records(self, fn, width):
         n = C.c_int()

@@ -51,6 +51,26 @@ T_FRAME, T_BOW, T_POSE, T_LF, T_LOCAL, T_RESET = 1, 2, 3, 4, 5, 6
 L_JOB, L_DISTINCTIVE, L_CREATE, L_CREATE_PAIR, L_FUSE_BATCH, L_FUSE_REFRESH, L_FUSE, L_BA, L_BOW = range(16, 25)
 
 
+KF_STATE_PROCESS, KF_STATE_CREATE, KF_STATE_FUSE = 0, 1, 2   # ORBMI_KF_STATE_* (include/orbmi_debug.h)
+FNV0 = 2166136261
+
+
+def _fnv(h: int, words) -> int:
+    """h = (h ^ w) * 16777619 mod 2^32 over 32-bit words (the native state record's hash)."""
+    for w in np.asarray(words).astype(np.int64).tolist():
+        h = ((h ^ (w & 0xFFFFFFFF)) * 16777619) & 0xFFFFFFFF
+    return h
+
+
+def _slot_hash(kf) -> int:
+    return _fnv(FNV0, [-1 if mp is None else mp.id for mp in kf.map_points])
+
+
+def _i32(v: int) -> int:
+    v = int(v) & 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
 class ScheduleMismatch(RuntimeError):
     """A recorded concurrent schedule does not fit this host logic (replay_schedule)."""
 
@@ -423,7 +443,9 @@ class GpuBackend:
     def compute_bow(self, desc):
         if self.vocab is None:
             raise RuntimeError("TrackReferenceKeyFrame needs a vocabulary (StereoSLAM(vocabulary=...))")
-        return self.vocab.ComputeBoW(desc)[2]
+        words, _, fv = self.vocab.ComputeBoW(desc)
+        fv.n_words = len(words)   # (the BowVector's size, for the per-keyframe state record)
+        return fv
 
     def search_by_bow(self, kf, kf_mp_ok, kf_fv, f, f_fv):
         return self.m_bow.SearchByBoW(kf, kf_mp_ok, kf_fv, f, f_fv)
@@ -530,6 +552,12 @@ class StereoSLAM:
         self.rel_poses, self.references, self.frame_times, self.lost = [], [], [], []
         self.stats = []   # per frame: dict of the Tracking counters
         self.ba_log = []  # per LocalBundleAdjustment: graph size and erased observations
+        # per keyframe and LocalMapping stage: (keyframe, stage, schedule event, a, b, c) as the
+        # native loop's orbmi_slam_get_keyframe_state_log records it (include/orbmi_debug.h)
+        self.kf_state = []
+        self._state_expect = None  # replay: the recorded rows still to be matched
+        self._sched_k = -1         # replay: the schedule event being run
+        self._fuse_ops = 0
         # the concurrent LocalMapping of a replayed schedule (replay_schedule): the keyframe queue
         # (mlNewKeyFrames), !AcceptKeyFrames, mbAbortBA and the recorded LocalBA stop checks
         self._concurrent = False
@@ -824,17 +852,42 @@ class StereoSLAM:
         update_normals_and_depths(updated)
         yield from self._distinctive_gen(updated)
         kf.update_connections()
+        fv = kf.feat_vec
+        if fv is None:
+            self._log_state(kf, KF_STATE_PROCESS, -1, FNV0, _slot_hash(kf))
+        else:
+            h = _fnv(_fnv(_fnv(FNV0, fv.node_id), fv.off), fv.feat)
+            self._log_state(kf, KF_STATE_PROCESS, getattr(fv, "n_words", -1), h, _slot_hash(kf))
         self._map_point_culling(kf)
         if self.local_mapping_full:
+            n0 = len(self.mappoints)
             yield from self._create_new_map_points_gen(kf)
+            self._log_state(kf, KF_STATE_CREATE, len(self.mappoints) - n0, len(self.mappoints), _slot_hash(kf))
             if not self._queued():
+                self._fuse_ops = 0
                 yield from self._search_in_neighbors_gen(kf)
+                filled = sum(1 for mp in kf.map_points if mp is not None)
+                self._log_state(kf, KF_STATE_FUSE, self._fuse_ops, filled, _slot_hash(kf))
         self._abort = False
         if not self._queued():
             if self.use_local_ba and self._keyframes_in_map() > 2:
                 yield from self._local_bundle_adjustment_gen(kf)
             if self.local_mapping_full:
                 self._keyframe_culling(kf)
+
+    def _log_state(self, kf: KeyFrame, stage: int, a: int, b: int, c: int):
+        """The per-keyframe state record (orbmi_slam_kf_state); in a replay, checked against the
+        native run's record at the same point, so a divergence is named by its first keyframe and
+        stage instead of by a lock label many events later."""
+        row = (kf.id, stage, self._sched_k, int(a), _i32(b), _i32(c))
+        self.kf_state.append(row)
+        if self._state_expect is None:
+            return
+        want = next(self._state_expect, None)
+        if want is None or tuple(want) != row:
+            names = ("ProcessNewKeyFrame", "CreateNewMapPoints", "SearchInNeighbors")
+            raise ScheduleMismatch(f"keyframe {kf.id}, after {names[stage]}: the native run recorded {want} "
+                                   f"(keyframe, stage, event, a, b, c), this logic {row}")
 
     def _map_point_culling(self, kf: KeyFrame):
         """LocalMapping::MapPointCulling (src/LocalMapping.cc:219-263), stereo: nThObs = 3."""
@@ -954,9 +1007,9 @@ class StereoSLAM:
         yield L_FUSE, kf.id
         return np.asarray(best, np.int32).copy()
 
-    @staticmethod
-    def _fuse_replay(kf: KeyFrame, pts: list, best, dirty: set):
-        """The map updates of ORBmatcher::Fuse (src/ORBmatcher.cc:1096-1124) in list order."""
+    def _fuse_replay(self, kf: KeyFrame, pts: list, best, dirty: set):
+        """The map updates of ORBmatcher::Fuse (src/ORBmatcher.cc:1096-1124) in list order
+        (counted in _fuse_ops for the state record)."""
         for mp, b in zip(pts, best):
             if mp.bad or kf in mp.observations or b < 0:
                 continue
@@ -967,11 +1020,14 @@ class StereoSLAM:
                     if mp_in_kf.nobs > mp.nobs:
                         if mp.replace(mp_in_kf):
                             dirty.add(mp_in_kf)
+                            self._fuse_ops += 1
                     elif mp_in_kf.replace(mp):
                         dirty.add(mp)
+                        self._fuse_ops += 1
             else:
                 mp.add_observation(kf, b)
                 kf.map_points[b] = mp
+                self._fuse_ops += 1
 
     def _fuse_gen(self, kf: KeyFrame, mps: list, dirty: set):
         """ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for
@@ -1178,7 +1234,7 @@ class StereoSLAM:
                 yield from self._local_mapping_gen(kf)
             self._busy = False      # SetAcceptKeyFrames(true)
 
-    def replay_schedule(self, frames, schedule, ba_log):
+    def replay_schedule(self, frames, schedule, ba_log, kf_state=None):
         """Replay a run of the native loop with the concurrent LocalMapping
         (orbmi_slam_settings.async_local_mapping) on this host logic: `frames` = [(L, R, ts)] as
         handed to TrackStereo, `schedule` = NativeStereoSLAM.schedule() (thread, label, arg per
@@ -1186,8 +1242,12 @@ class StereoSLAM:
         two threads' stretches between lock releases run in the recorded order and every
         LocalBA stops at its recorded pbStopFlag check, so the run's decisions and trajectory
         follow from the schedule.  Raises ScheduleMismatch where the record and this logic
-        disagree."""
+        disagree; with `kf_state` (NativeStereoSLAM.keyframe_state_log()) every keyframe's state
+        after ProcessNewKeyFrame, CreateNewMapPoints and SearchInNeighbors is compared as it is
+        reached, so a mismatch names the first keyframe and stage where the maps part."""
         self._concurrent = True
+        if kf_state is not None:
+            self._state_expect = iter([tuple(int(x) for x in r) for r in np.asarray(kf_state).reshape(-1, 6)])
         stops = iter([tuple(int(x) for x in r[:2]) for r in np.asarray(ba_log).reshape(-1, 8)])
 
         def stop_at(kf):
@@ -1203,6 +1263,7 @@ class StereoSLAM:
             if w is None or w[0] != label or (w[1] is not None and w[1] != arg):
                 raise ScheduleMismatch(f"event {k}: thread {thread} resumes at ({label}, {arg}), "
                                        f"this logic at {w}")
+            self._sched_k = k
             try:
                 want[thread] = gens[thread].send((thread, label, arg))
             except StopIteration:
@@ -1211,8 +1272,12 @@ class StereoSLAM:
             raise ScheduleMismatch(f"the record ends with Tracking at {want[0]}")
         if next(stops, None) is not None:
             raise ScheduleMismatch("the record has more LocalBA calls")
+        if self._state_expect is not None and next(self._state_expect, None) is not None:
+            raise ScheduleMismatch("the record has more keyframe states")
         self._concurrent = False
         self._ba_stop_at = None
+        self._state_expect = None
+        self._sched_k = -1
 
     def ba_records(self) -> np.ndarray:
         """ba_log in the layout of NativeStereoSLAM.local_ba_log (keyframe, stop_check, aborted,

@@ -37,8 +37,10 @@ class OracleBackend:
 
     def compute_bow(self, desc):
         self._count("compute_bow")
-        _, _, node, off, feat = self.O.transform(self.vocab, desc, 4)
-        return FeatureVector.from_csr(node, off, feat)
+        words, _, node, off, feat = self.O.transform(self.vocab, desc, 4)
+        fv = FeatureVector.from_csr(node, off, feat)
+        fv.n_words = len(words)   # (the BowVector's size, for the per-keyframe state record)
+        return fv
 
     def search_by_bow(self, kf, kf_mp_ok, kf_fv, f, f_fv):
         self._count("search_by_bow")

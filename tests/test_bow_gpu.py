@@ -110,3 +110,75 @@ def test_search_by_bow_with_gpu_feature_vectors(oracle):
         assert ngot == nref and nref > 20
         m.close()
     gv.close()
+
+
+def test_transform_from_two_threads_on_one_handle(oracle):
+    """Tracking (TrackReferenceKeyFrame: host descriptors, host outputs, src/Tracking.cc:871-917)
+    and LocalMapping (ProcessNewKeyFrame's ComputeBoW with the map lock released: here with device
+    outputs, as pipeline.LocalMapper makes them; src/LocalMapping.cc:152-160) transform on one
+    vocabulary handle at once -- the reference's const TemplatedVocabulary::transform
+    (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1126-1194) is safe from both threads.  Each
+    round both threads are released together by a barrier; every result equals the oracle's
+    transform of its own descriptors (orbmi_transform serialises calls per handle: its staging
+    buffer d_work is shared)."""
+    import threading
+    import torch
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary
+    v = _vocab(10, 5, seed=21)
+    gv = ORBVocabulary(v, device=0)
+    descs = [frame_data(f)[1] for f in range(6)]
+    refs = [oracle.transform(v, d, 4) for d in descs]
+    rounds = 24
+    bar = threading.Barrier(2)
+    errors = []
+
+    def tracking():
+        try:
+            for r in range(rounds):
+                i = r % len(descs)
+                bar.wait()
+                _check(gv.transform(descs[i], 4), refs[i])
+        except Exception as e:  # reported by the main thread
+            errors.append(("tracking", r, e))
+            bar.abort()
+
+    def mapping():
+        try:
+            torch.cuda.set_device(0)
+            cap = max(len(d) for d in descs)
+            outs = dict(word=torch.zeros(cap, dtype=torch.int32, device="cuda"),
+                        value=torch.zeros(cap, dtype=torch.float64, device="cuda"),
+                        node=torch.zeros(cap, dtype=torch.int32, device="cuda"),
+                        off=torch.zeros(cap + 1, dtype=torch.int32, device="cuda"),
+                        feat=torch.zeros(cap, dtype=torch.int32, device="cuda"),
+                        counts=torch.zeros(2, dtype=torch.int32, device="cuda"))
+            torch.cuda.synchronize()
+            for r in range(rounds):
+                i = (r + 3) % len(descs)
+                d = np.ascontiguousarray(descs[i])
+                bar.wait()
+                gv.transform_device(d.ctypes.data, len(d), None, 4, *(outs[k].data_ptr() for k in
+                                    ("word", "value", "node", "off", "feat", "counts")))
+                gv.synchronize()
+                rw, rval, rnode, roff, rfeat = refs[i]
+                nw, nn = (int(x) for x in outs["counts"].cpu())
+                assert (nw, nn) == (len(rw), len(rnode))
+                np.testing.assert_array_equal(outs["word"][:nw].cpu().numpy().astype(np.uint32), rw)
+                np.testing.assert_array_equal(outs["value"][:nw].cpu().numpy(), rval)
+                np.testing.assert_array_equal(outs["node"][:nn].cpu().numpy().astype(np.uint32), rnode)
+                np.testing.assert_array_equal(outs["off"][:nn + 1].cpu().numpy(), roff)
+                np.testing.assert_array_equal(outs["feat"][:len(rfeat)].cpu().numpy(), rfeat)
+        except Exception as e:
+            errors.append(("mapping", r, e))
+            bar.abort()
+
+    ts = [threading.Thread(target=tracking), threading.Thread(target=mapping)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    gv.close()
+    assert not any(t.is_alive() for t in ts)
+    real = [e for e in errors if not isinstance(e[2], threading.BrokenBarrierError)]
+    assert not real, real
+    assert not errors, errors

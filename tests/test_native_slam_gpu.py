@@ -36,7 +36,7 @@ def test_native_matches_oracle_200_frames(tmp_path, ahead):
     frames = render_sequence(n)
     s = sequence_settings(tmp_path)
     voc = small_vocabulary()
-    gpu = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    gpu = NativeStereoSLAM(s, device=0, vocabulary=voc, record=True)
     _drive(gpu, frames, ahead)
     ref = StereoSLAM(s, backend=OracleBackend(s, voc))
     _drive(ref, frames)
@@ -52,6 +52,11 @@ def test_native_matches_oracle_200_frames(tmp_path, ahead):
     gt = np.array([fr[2] for fr in frames])
     assert abs(ate_rmse(tg, gt) - ate_rmse(tr, gt)) < 1e-3   # identical trajectory RMSE (north_star)
     assert gpu.counts()["local_ba_calls"] == sum(1 for _ in ref.ba_log)
+    # every keyframe's map after ProcessNewKeyFrame (BowVector words, FeatureVector hash, slots),
+    # CreateNewMapPoints (new points) and SearchInNeighbors (Fuse updates): the same record
+    st_native = gpu.keyframe_state_log()
+    assert len(st_native) >= 3 * 40
+    np.testing.assert_array_equal(st_native, np.array(ref.kf_state, np.int32).reshape(-1, 6))
     gpu.Shutdown()
 
 
@@ -80,6 +85,33 @@ def test_native_plain_calls_between_ahead_calls(tmp_path):
             nxt = frames[f + 1][:2] if f + 1 < n else None
             keep.append(nxt)
             mix.TrackStereo(L, R, 0.1 * f, next_pair=nxt)
+    a_all, b_all = mix.stats, ref.stats
+    assert len(a_all) == len(b_all) == n
+    for a, b in zip(a_all, b_all):
+        assert {k: a.get(k) for k in _DECISIONS} == {k: b.get(k) for k in _DECISIONS}, (a, b)
+    np.testing.assert_array_equal(mix.trajectory_twc(), ref.trajectory_twc())
+    mix.Shutdown()
+    ref.Shutdown()
+
+
+def test_native_ahead_with_fresh_buffers_every_call(tmp_path):
+    """Every call hands the current pair in a fresh copy of the buffers the previous call named as
+    next_pair (same content, other addresses: what np.ascontiguousarray of a strided view does) and
+    posts the next pair again.  The pair enqueued ahead is then never the one asked for: it is
+    dropped, the current pair extracted now, and the next pair enqueued behind it -- into a device
+    slot that is neither this frame's nor the last frame's, which this frame's tracking reads while
+    that extraction runs (seq % 3 put it on the last frame's slot).  The decisions and
+    the trajectory are the all-plain run's."""
+    n = 40
+    frames = render_sequence(n)
+    s = sequence_settings(tmp_path)
+    voc = small_vocabulary()
+    ref = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    _drive(ref, frames)
+    mix = NativeStereoSLAM(s, device=0, vocabulary=voc)
+    for f, (L, R, _) in enumerate(frames):
+        nxt = frames[f + 1][:2] if f + 1 < n else None
+        mix.TrackStereo(L.copy(), R.copy(), 0.1 * f, next_pair=nxt)
     a_all, b_all = mix.stats, ref.stats
     assert len(a_all) == len(b_all) == n
     for a, b in zip(a_all, b_all):
@@ -177,10 +209,11 @@ def _concurrent_record(tmp_path, n, period):
     frames = render_sequence(n)
     s = sequence_settings(tmp_path)
     voc = small_vocabulary()
-    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
+    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True, record=True)
     _drive_paced(slam, frames, period)
     slam.WaitLocalMapping()
-    rec = {"schedule": slam.schedule(), "ba_log": slam.local_ba_log(), "stats": slam.stats,
+    rec = {"schedule": slam.schedule(), "ba_log": slam.local_ba_log(), "kf_state": slam.keyframe_state_log(),
+           "stats": slam.stats,
            "traj": slam.trajectory_twc(), "counts": slam.counts()}
     slam.Shutdown()
     return frames, s, voc, rec
@@ -202,7 +235,8 @@ def test_concurrent_schedule_replays_on_oracle(tmp_path, period):
     sched, balog = rec["schedule"], rec["ba_log"]
     assert len(sched) > 400 and (sched[:, 0] == 1).any()
     ref = StereoSLAM(s, backend=OracleBackend(s, voc))
-    ref.replay_schedule([(L, R, 0.1 * f) for f, (L, R, _) in enumerate(frames)], sched, balog)
+    # with the per-keyframe state record: a divergence is reported as its first keyframe and stage
+    ref.replay_schedule([(L, R, 0.1 * f) for f, (L, R, _) in enumerate(frames)], sched, balog, rec["kf_state"])
     a_all, b_all = rec["stats"], ref.stats
     assert len(a_all) == len(b_all) == 200
     for a, b in zip(a_all, b_all):

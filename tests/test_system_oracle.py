@@ -206,11 +206,13 @@ def _interleaved_run(s, voc, frames, seed, stop_prob=0.5):
             arg = slam._queue[0].id if slam._queue else -1
         ev = (t, label, arg)
         sched.append(ev)
+        slam._sched_k = len(sched) - 1   # (the state record's schedule event, as the native loop)
         try:
             want[t] = gens[t].send(ev)
         except StopIteration:
             want[t] = None
     slam._concurrent = False
+    slam._sched_k = -1
     return slam, np.array(sched, np.int32), slam.ba_records()
 
 
@@ -229,8 +231,11 @@ def test_replay_schedule_reproduces_interleaved_run(tmp_path, seed):
     run, sched, balog = _interleaved_run(s, voc, frames, seed)
     assert len(run.stats) == 24 and len(balog) >= 2
     rep = StereoSLAM(s, backend=OracleBackend(s, voc))
-    rep.replay_schedule(frames, sched, balog)
+    states = np.array(run.kf_state, np.int32).reshape(-1, 6)
+    assert len(states) >= 3 and (states[:, 2] >= 0).all()
+    rep.replay_schedule(frames, sched, balog, states)
     assert rep.stats == run.stats
+    np.testing.assert_array_equal(np.array(rep.kf_state, np.int32).reshape(-1, 6), states)
     np.testing.assert_array_equal(rep.ba_records(), balog)
     np.testing.assert_array_equal(rep.trajectory_twc(), run.trajectory_twc())
     # a record that does not fit is refused
@@ -241,3 +246,9 @@ def test_replay_schedule_reproduces_interleaved_run(tmp_path, seed):
     bad[k, 1] = 99
     with pytest.raises(ScheduleMismatch):
         StereoSLAM(s, backend=OracleBackend(s, voc)).replay_schedule(frames, bad, balog)
+    # a map that parts from the record is named by its first keyframe and stage
+    j = len(states) // 2
+    bad_state = states.copy()
+    bad_state[j, 5] ^= 1
+    with pytest.raises(ScheduleMismatch, match=f"keyframe {int(states[j, 0])}, after "):
+        StereoSLAM(s, backend=OracleBackend(s, voc)).replay_schedule(frames, sched, balog, bad_state)

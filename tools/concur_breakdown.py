@@ -56,7 +56,7 @@ def run(frames, s, voc, period, no_interrupt):
         os.environ["ORBMI_SLAM_NO_INTERRUPT"] = "1"
     else:
         os.environ.pop("ORBMI_SLAM_NO_INTERRUPT", None)
-    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True)
+    slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True, record=True)
     t0 = time.perf_counter()
     for f, (L, R, _) in enumerate(frames):
         nxt = frames[f + 1][:2] if f + 1 < len(frames) else None

@@ -27,14 +27,17 @@ def main():
     slam = NativeStereoSLAM(load_settings(path), device=0, vocabulary=Vocabulary.synthetic(k=10, L=5, seed=3),
                             async_local_mapping=async_lm)
     t0 = time.perf_counter()
-    for f, (L, R, _) in enumerate(frames):
-        slam.TrackStereo(L, R, 0.1 * f)
+    for f, (L, R, _) in enumerate(frames):  # the next pair handed over ahead, as bench --mode system
+        slam.TrackStereo(L, R, 0.1 * f, next_pair=frames[f + 1][:2] if f + 1 < n else None)
     slam.WaitLocalMapping()
     dt = time.perf_counter() - t0
     c = slam.counts()
     ph = slam.phase_ms()
     per_kf = n / max(c["keyframes"] - 1, 1)
-    print(f"{n} frames in {dt * 1e3:.1f} ms ({n / dt:.1f} fps), {c}")
+    gt = np.array([fr[2] for fr in frames])
+    from orb_slam2_with_comment_amd.system import ate_rmse
+    print(f"{n} frames in {dt * 1e3:.1f} ms ({n / dt:.1f} fps), {c}, ATE {ate_rmse(slam.trajectory_twc(), gt):.4f} m")
+    print(f"  local mapping: {slam.local_mapping_counts()}")
     for k, v in ph.items():
         print(f"  {k:24s} {v:8.4f} ms/frame" + (f"  {v * per_kf:8.4f} ms/keyframe" if k.startswith("lm_") else ""))
     slam.Shutdown()
