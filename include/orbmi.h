@@ -61,6 +61,16 @@ int orbmi_extract(orbmi_extractor* h, const uint8_t* image, int rows, int cols, 
 int orbmi_extract_batch_device(orbmi_extractor* h, const uint8_t* d_images, int batch, int rows,
                                int cols, size_t step, size_t image_stride, orbmi_keypoint* d_kps,
                                uint8_t* d_desc, int* d_counts, int capacity);
+/* The same with the images in host memory (the reference's operator() takes a host cv::Mat;
+ * src/Tracking.cc:168-205 builds the Frame from it): image b at images + b*image_stride, rows
+ * contiguous (pitch = cols).  The bytes go to HBM by a copy kernel on the handle's stream that
+ * reads pinned memory (hipHostMalloc / hipHostRegister) in place -- asynchronous, the host does
+ * not wait; the caller keeps the images unchanged until the stream has passed the call
+ * (orbmi_extractor_synchronize, or an event on orbmi_extractor_get_stream).  Pageable memory is
+ * first copied into one of two pinned staging buffers of the handle (the host may then wait for
+ * the copy kernel two calls back). */
+int orbmi_extract_batch_host(orbmi_extractor* h, const uint8_t* images, int batch, int rows, int cols,
+                             size_t image_stride, orbmi_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int capacity);
 int orbmi_extractor_synchronize(orbmi_extractor* h);
 /* The handle's HIP stream (hipStream_t), for callers that order their own work after it. */
 int orbmi_extractor_get_stream(orbmi_extractor* h, void** stream);

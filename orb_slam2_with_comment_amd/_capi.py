@@ -46,6 +46,7 @@ _PROTOS = {
     "orbmi_extractor_destroy": (None, [_vp]),
     "orbmi_extract": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _i, C.POINTER(_i)]),
     "orbmi_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _sz, _sz, _vp, _vp, _vp, _i]),
+    "orbmi_extract_batch_host": (_i, [_vp, _vp, _i, _i, _i, _sz, _vp, _vp, _vp, _i]),
     "orbmi_extractor_synchronize": (_i, [_vp]),
     "orbmi_extractor_get_levels": (_i, [_vp]),
     "orbmi_extractor_get_scale_factor": (_f, [_vp]),

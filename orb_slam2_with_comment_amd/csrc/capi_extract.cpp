@@ -97,6 +97,21 @@ int orbmi_extract_batch_device(orbmi_extractor* h, const uint8_t* d_images, int 
     return e.run(d_images, batch, step, image_stride, d_kps, d_desc, d_counts, capacity);
 }
 
+int orbmi_extract_batch_host(orbmi_extractor* h, const uint8_t* images, int batch, int rows, int cols,
+                             size_t image_stride, orbmi_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int capacity) {
+    if (!h || !images || batch <= 0 || rows <= 0 || cols <= 0 || image_stride < (size_t)rows * cols || !d_kps ||
+        !d_desc || !d_counts || capacity <= 0)
+        return ORBMI_E_ARG;
+    Extractor& e = h->ex;
+    ORBMI_HIP(hipSetDevice(e.device));
+    int rc;
+    if ((rc = e.set_geometry(rows, cols))) return rc;
+    if ((rc = e.reserve(batch, 0))) return rc;
+    const uint8_t* d = nullptr;
+    if ((rc = e.upload_host(images, image_stride * (size_t)(batch - 1) + (size_t)rows * cols, &d))) return rc;
+    return e.run(d, batch, cols, image_stride, d_kps, d_desc, d_counts, capacity);
+}
+
 int orbmi_extractor_synchronize(orbmi_extractor* h) {
     if (!h) return ORBMI_E_ARG;
     ORBMI_HIP(hipSetDevice(h->ex.device));

@@ -113,6 +113,12 @@ struct Extractor {
     int* d_counts = nullptr;
     uint8_t* d_image = nullptr;    // staging for host images
     size_t image_bytes = 0;
+    // pageable host images of orbmi_extract_batch_host: pinned staging, two alternating buffers,
+    // each guarded by the event after the copy kernel that reads it
+    uint8_t* h_stage[2] = {nullptr, nullptr};
+    size_t stage_bytes[2] = {0, 0};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    int stage_next = 0;
     int last_batch = 0;
     // last batch output location (may be caller buffers for the device API)
     orbmi_keypoint* last_kps = nullptr;
@@ -141,6 +147,9 @@ struct Extractor {
     int set_geometry(int rows, int cols);
     int reserve(int batch, int capacity);
     int ensure_side_stream();  // bstream + its events on first use (large batches only)
+    // host images -> d_image by a copy kernel on `stream` (pinned memory read in place, pageable
+    // memory staged first); *d_out = d_image
+    int upload_host(const uint8_t* h_images, size_t bytes, const uint8_t** d_out);
     int run(const uint8_t* d_images, int batch, size_t step, size_t image_stride,
             orbmi_keypoint* kps, uint8_t* desc, int* counts, int capacity);
     void release();

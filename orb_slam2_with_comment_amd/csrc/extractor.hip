@@ -2218,7 +2218,83 @@ void Extractor::prof_end(int stage, hipEvent_t a, hipStream_t s) {
     prof_pending.push_back(ProfPair{stage, a, b});
 }
 
+// ---- host images into HBM (orbmi_extract_batch_host) -------------------------------------------
+// The image bytes are read straight from pinned host memory by a copy kernel on the handle's
+// stream: the host never waits (hipMemcpyAsync from host memory measured as waiting for the
+// stream's earlier work, which serialised the host with the extraction it had queued).  16-B
+// loads, 4 in flight per lane before the stores (PCIe read latency); bytewise when unaligned.
+__global__ __launch_bounds__(256) void k_copy_host(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   size_t n) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const uint4* s4 = (const uint4*)src;
+        uint4* d4 = (uint4*)dst;
+        const size_t n16 = n >> 4;
+        size_t i = tid;
+        for (; i + 3 * nth < n16; i += 4 * nth) {
+            const uint4 a = s4[i], b = s4[i + nth],
+                        c = s4[i + 2 * nth], d = s4[i + 3 * nth];
+            d4[i] = a;
+            d4[i + nth] = b;
+            d4[i + 2 * nth] = c;
+            d4[i + 3 * nth] = d;
+        }
+        for (; i < n16; i += nth) d4[i] = s4[i];
+        for (size_t j = (n16 << 4) + tid; j < n; j += nth) dst[j] = src[j];
+    } else {
+        for (size_t j = tid; j < n; j += nth) dst[j] = src[j];
+    }
+}
+
+int Extractor::upload_host(const uint8_t* h_images, size_t bytes, const uint8_t** d_out) {
+    if (bytes > image_bytes) {
+        if (d_image) (void)hipFree(d_image);
+        d_image = nullptr;
+        image_bytes = 0;
+        ORBMI_HIP(hipMalloc((void**)&d_image, bytes));
+        image_bytes = bytes;
+    }
+    hipPointerAttribute_t at;
+    bool pinned = false;
+    if (hipPointerGetAttributes(&at, h_images) == hipSuccess) pinned = at.type == hipMemoryTypeHost;
+    else (void)hipGetLastError();
+    const uint8_t* src = h_images;
+    if (!pinned) {  // pageable: one host copy into a pinned staging buffer of the handle (two, alternating)
+        const int k = stage_next;
+        stage_next ^= 1;
+        if (bytes > stage_bytes[k]) {
+            if (stage_ev[k]) ORBMI_HIP(hipEventSynchronize(stage_ev[k]));
+            if (h_stage[k]) (void)hipHostFree(h_stage[k]);
+            h_stage[k] = nullptr;
+            stage_bytes[k] = 0;
+            ORBMI_HIP(hipHostMalloc((void**)&h_stage[k], bytes, hipHostMallocDefault));
+            stage_bytes[k] = bytes;
+        }
+        if (!stage_ev[k]) ORBMI_HIP(hipEventCreateWithFlags(&stage_ev[k], hipEventDisableTiming));
+        else ORBMI_HIP(hipEventSynchronize(stage_ev[k]));  // its last copy kernel has read it
+        std::memcpy(h_stage[k], h_images, bytes);
+        src = h_stage[k];
+        const int blocks = (int)std::min<size_t>(1024, (bytes / 16 + 255) / 256 + 1);
+        hipLaunchKernelGGL(k_copy_host, dim3(blocks), dim3(256), 0, stream, src, d_image, bytes);
+        ORBMI_HIP(hipGetLastError());
+        ORBMI_HIP(hipEventRecord(stage_ev[k], stream));
+    } else {
+        const int blocks = (int)std::min<size_t>(1024, (bytes / 16 + 255) / 256 + 1);
+        hipLaunchKernelGGL(k_copy_host, dim3(blocks), dim3(256), 0, stream, src, d_image, bytes);
+        ORBMI_HIP(hipGetLastError());
+    }
+    *d_out = d_image;
+    return ORBMI_OK;
+}
+
 void Extractor::release() {
+    for (int k = 0; k < 2; k++) {
+        if (stage_ev[k]) { (void)hipEventSynchronize(stage_ev[k]); (void)hipEventDestroy(stage_ev[k]); }
+        if (h_stage[k]) (void)hipHostFree(h_stage[k]);
+        stage_ev[k] = nullptr;
+        h_stage[k] = nullptr;
+        stage_bytes[k] = 0;
+    }
     for (auto& p : prof_pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : prof_pool) (void)hipEventDestroy(e);
     prof_pending.clear();

@@ -299,6 +299,11 @@ struct orbmi_slam {
     } seen;
     SeenSet local_mark;           // UpdateLocalPoints' mnTrackReferenceForFrame
     SeenSet local_kf_mark;        // UpdateLocalKeyFrames' mnTrackReferenceForFrame
+    // LocalBundleAdjustment's mnBALocalForKF / mnBAFixedForKF and its points' marks (the mapping
+    // thread's; generation stamps instead of std::set)
+    SeenSet ba_local_mark, ba_fixed_mark, ba_mp_mark;
+    // the points whose Fuse search record a replay may have changed (fuse_targets' check)
+    SeenSet fuse_touched;
     std::vector<int> kf_counter;  // UpdateLocalKeyFrames' keyframe counter (indexed by id)
     // mlRelativeFramePoses, mlpReferences, mlFrameTimes, mlbLost
     std::vector<M4> rel_poses;
@@ -754,6 +759,7 @@ struct orbmi_slam {
 
     void free_dev() {
         frame_worker_stop();
+        free_bow_async();
         if (dev.ahead.on && xstream) (void)hipStreamSynchronize(xstream);
         for (int k = 0; k < kSlots; k++) {
             (void)hipFree(dev.kps[k]);
@@ -807,6 +813,74 @@ struct orbmi_slam {
         fv.feat.assign(feat.begin(), feat.begin() + off[nn]);
         fv.valid = true;
         return ORBMI_OK;
+    }
+
+    // KeyFrame::ComputeBoW for the mapping thread from the keyframe's HBM descriptors, in two
+    // halves so that ProcessNewKeyFrame's ComputeDistinctiveDescriptors call runs while the
+    // transform does: bow_begin enqueues the transform (device outputs) and the read-back of the
+    // FeatureVector into pinned memory on the vocabulary's stream; bow_end waits and parses.
+    struct BowAsync {
+        uint8_t* d = nullptr;   // value f64[cap] | word u32[cap] | node u32[cap] | off i32[cap+1] | feat i32[cap] | counts i32[2]
+        uint8_t* h = nullptr;   // pinned mirror of node .. counts
+        int cap = 0, n = 0;
+        hipStream_t stream = nullptr;
+        bool pending = false;
+    } bowa;
+    size_t bow_tail_bytes(int cap) const { return (size_t)(3 * cap + 3) * 4; }
+    int bow_begin(const uint8_t* d_desc, int n) {
+        BowAsync& b = bowa;
+        if (n > b.cap) {
+            if (b.d) (void)hipFree(b.d);
+            if (b.h) (void)hipHostFree(b.h);
+            b.d = b.h = nullptr;
+            b.cap = 0;
+            const int cap = std::max(n, 2048);
+            if (hipMalloc((void**)&b.d, (size_t)cap * 12 + bow_tail_bytes(cap)) != hipSuccess) return ORBMI_E_HIP;
+            if (hipHostMalloc((void**)&b.h, bow_tail_bytes(cap), hipHostMallocDefault) != hipSuccess) return ORBMI_E_HIP;
+            b.cap = cap;
+        }
+        void* vs = nullptr;
+        SLAM_CHECK(orbmi_vocabulary_get_stream(voc, &vs));
+        b.stream = (hipStream_t)vs;
+        b.n = n;
+        const int cap = b.cap;
+        double* value = (double*)b.d;
+        uint32_t* word = (uint32_t*)(b.d + (size_t)cap * 8);
+        uint8_t* tail = b.d + (size_t)cap * 12;
+        uint32_t* node = (uint32_t*)tail;
+        int32_t* off = (int32_t*)(node + cap);
+        int32_t* feat = off + cap + 1;
+        int* counts = (int*)(feat + cap);
+        SLAM_CHECK(orbmi_transform(voc, d_desc, n, nullptr, 4, word, value, node, off, feat, counts));
+        if (hipMemcpyAsync(b.h, tail, bow_tail_bytes(cap), hipMemcpyDeviceToHost, b.stream) != hipSuccess)
+            return ORBMI_E_HIP;
+        b.pending = true;
+        return ORBMI_OK;
+    }
+    int bow_end(FeatVec& fv) {
+        BowAsync& b = bowa;
+        if (!b.pending) return ORBMI_E_STATE;
+        b.pending = false;
+        if (hipStreamSynchronize(b.stream) != hipSuccess) return ORBMI_E_HIP;
+        const int cap = b.cap;
+        const uint32_t* node = (const uint32_t*)b.h;
+        const int32_t* off = (const int32_t*)(node + cap);
+        const int32_t* feat = off + cap + 1;
+        const int* counts = (const int*)(feat + cap);
+        const int nn = counts[1];
+        if (nn < 0 || nn > b.n || off[nn] > b.n) return ORBMI_E_STATE;
+        fv.words = counts[0];
+        fv.node.assign(node, node + nn);
+        fv.off.assign(off, off + nn + 1);
+        fv.feat.assign(feat, feat + off[nn]);
+        fv.valid = true;
+        return ORBMI_OK;
+    }
+    void free_bow_async() {
+        if (bowa.pending && bowa.stream) (void)hipStreamSynchronize(bowa.stream);
+        if (bowa.d) (void)hipFree(bowa.d);
+        if (bowa.h) (void)hipHostFree(bowa.h);
+        bowa = BowAsync{};
     }
 
     // Optimizer::PoseOptimization over keypoint i -> lfp[match[i]] (match[i] >= 0)
@@ -1256,13 +1330,13 @@ struct orbmi_slam {
 
     template <class Next>
     int local_mapping_steps(int k, Next&& next) {
-        if (voc && !kfs[k].fv.valid) {  // ComputeBoW with the map lock released (the keyframe's
-                                        // descriptors copied first: Tracking may grow kfs meanwhile)
-            const std::vector<uint8_t> desc = kfs[k].desc;
-            FeatVec fv;
-            SLAM_CHECK(unlocked(ORBMI_SCHED_L_BOW, k, [&] { return compute_bow(desc, fv); }));
-            if (!kfs[k].fv.valid) kfs[k].fv = std::move(fv);  // (Tracking may have computed it: the same)
-        }
+        // ProcessNewKeyFrame (src/LocalMapping.cc:152-211): ComputeBoW, the observations of the
+        // keyframe's points, UpdateNormalAndDepth, ComputeDistinctiveDescriptors, UpdateConnections.
+        // The transform reads only the keyframe's descriptors, so it runs in the same window with
+        // the map lock released as the descriptors of the updated points: one release, and the
+        // two device calls overlap (the keyframe's descriptors are copied first when it has no
+        // HBM copy: Tracking may grow kfs meanwhile).
+        const bool need_bow = voc && !kfs[k].fv.valid;
         std::vector<int> updated;
         for (int i = 0; i < (int)kfs[k].mps.size(); i++) {
             const int m = kfs[k].mps[i];
@@ -1275,7 +1349,41 @@ struct orbmi_slam {
             }
         }
         normals(updated);
-        SLAM_CHECK(distinctive(updated));
+        std::vector<uint8_t> rows;
+        std::vector<int32_t> off;
+        {
+            PhaseTimer pt(&phase_ms[PH_LM_OBSROWS]);
+            obs_rows(updated, rows, off);
+        }
+        if (need_bow || !rows.empty()) {
+            const int np = (int)updated.size();
+            std::vector<int32_t> best(std::max(np, 1));
+            std::vector<uint8_t> out((size_t)std::max(np, 1) * 32);
+            const uint8_t* d_desc = kfs[k].d_desc;
+            const int nk = (int)kfs[k].keys.size();
+            const std::vector<uint8_t> desc = need_bow && !d_desc ? kfs[k].desc : std::vector<uint8_t>();
+            FeatVec fv;
+            orbmi_matcher* mt = lmm();
+            SLAM_CHECK(unlocked(need_bow ? ORBMI_SCHED_L_BOW : ORBMI_SCHED_L_DISTINCTIVE, need_bow ? k : -1, [&] {
+                int rc = ORBMI_OK;
+                const bool async_bow = need_bow && d_desc && nk > 0;
+                if (async_bow) rc = bow_begin(d_desc, nk);
+                else if (need_bow) rc = compute_bow(desc, fv);
+                if (!rc && !rows.empty()) {
+                    PhaseTimer pt(&phase_ms[PH_LM_DISTINCTIVE_CALL]);
+                    rc = orbmi_compute_distinctive_descriptors(mt, rows.data(), off.data(), np, best.data(), out.data());
+                }
+                if (async_bow) {
+                    const int rc2 = bow_end(fv);
+                    if (!rc) rc = rc2;
+                }
+                return rc;
+            }));
+            if (need_bow && !kfs[k].fv.valid) kfs[k].fv = std::move(fv);  // (Tracking may have computed it: the same)
+            if (!rows.empty())
+                for (int j = 0; j < np; j++)
+                    if (off[j + 1] > off[j]) std::memcpy(mps[updated[j]].desc, &out[32 * j], 32);
+        }
         connections(k);
         if (recording) {  // ProcessNewKeyFrame's outcome: BowVector words, FeatureVector, slots
             const FeatVec& fv = kfs[k].fv;
@@ -1571,6 +1679,8 @@ struct orbmi_slam {
             const int in = kfs[k].mps[b];
             if (in >= 0) {
                 if (!mps[in].bad) {
+                    fuse_touched.insert(m);
+                    fuse_touched.insert(in);
                     if (mps[in].nobs > mps[m].nobs) {
                         if (replace(m, in)) { dirty.insert(in); fuse_ops++; }
                     } else if (replace(in, m)) {
@@ -1579,6 +1689,7 @@ struct orbmi_slam {
                     }
                 }
             } else {
+                fuse_touched.insert(m);
                 add_observation(m, k, b);
                 kfs[k].mps[b] = m;
                 fuse_ops++;
@@ -1589,20 +1700,55 @@ struct orbmi_slam {
     // ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for every
     // point on the GPU, then the map updates in list order.  `dirty`: the survivors of Replace
     // whose ComputeDistinctiveDescriptors (MapPoint::Replace, src/MapPoint.cc:212) is still due.
+    // The owed descriptors and the search go to the device as one orbmi_fuse_search_refresh call
+    // (one round trip): the search reads each due point's record with its new descriptor.
     int fuse(int k, const std::vector<int>& list, std::set<int>& dirty) {
-        if (!dirty.empty()) {
-            std::vector<int> pts;
-            for (int m : dirty)
-                if (!mps[m].bad) pts.push_back(m);
-            SLAM_CHECK(distinctive(pts));
-            dirty.clear();
-        }
+        std::vector<int> due;
+        for (int m : dirty)
+            if (!mps[m].bad) due.push_back(m);
+        dirty.clear();
         std::vector<int> pts;
         for (int m : list)
             if (m >= 0) pts.push_back(m);
-        if (pts.empty()) return ORBMI_OK;
-        std::vector<int32_t> best;
-        SLAM_CHECK(fuse_search(k, pts, best));
+        if (pts.empty()) return distinctive(due);
+        std::vector<uint8_t> rows;
+        std::vector<int32_t> off;
+        {
+            PhaseTimer pt(&phase_ms[PH_LM_OBSROWS]);
+            obs_rows(due, rows, off);
+        }
+        if (rows.empty()) {  // no descriptor changes: the plain search
+            std::vector<int32_t> best;
+            SLAM_CHECK(fuse_search(k, pts, best));
+            fuse_replay(k, pts, best.data(), dirty);
+            return ORBMI_OK;
+        }
+        const int nd = (int)due.size(), np = (int)pts.size();
+        std::vector<orbmi_mappoint> rec(np);
+        std::vector<uint8_t> in_kf(np);
+        std::vector<int32_t> from(np, -1);
+        for (int j = 0; j < np; j++) {
+            rec[j] = fuse_record(pts[j]);
+            in_kf[j] = mps[pts[j]].obs.count(k) ? 1 : 0;
+            auto it = std::lower_bound(due.begin(), due.end(), pts[j]);  // (due ascending: a std::set's order)
+            if (it != due.end() && *it == pts[j]) {
+                const int d = (int)(it - due.begin());
+                if (off[d + 1] > off[d]) from[j] = d;
+            }
+        }
+        std::vector<int32_t> dbest(nd), best(np, -1), bd(np);
+        std::vector<uint8_t> dout((size_t)nd * 32);
+        for (int d = 0; d < nd; d++) std::memcpy(&dout[32 * d], mps[due[d]].desc, 32);
+        const M4 tcw = kfs[k].tcw;
+        const orbmi_frame_view v = kf_view(kfs[k], tcw.data());
+        orbmi_matcher* mt = lmm();
+        SLAM_CHECK(unlocked(ORBMI_SCHED_L_FUSE, k, [&] {
+            PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
+            return orbmi_fuse_search_refresh(mt, rows.data(), off.data(), nd, dbest.data(), dout.data(), 1, &v,
+                                             rec.data(), from.data(), in_kf.data(), np, 3.f, best.data(), bd.data());
+        }));
+        for (int d = 0; d < nd; d++)
+            if (off[d + 1] > off[d]) std::memcpy(mps[due[d]].desc, &dout[32 * d], 32);
         fuse_replay(k, pts, best.data(), dirty);
         return ORBMI_OK;
     }
@@ -1623,6 +1769,7 @@ struct orbmi_slam {
         const int nt = (int)targets.size(), np = (int)pts.size();
         if (nt == 0 || np == 0) return ORBMI_OK;
         auto* prep = new PhaseTimer(&phase_ms[PH_LM_SIN_PREP]);
+        fuse_touched.clear();
         std::vector<orbmi_mappoint> rec0(np);
         for (int j = 0; j < np; j++) rec0[j] = fuse_record(pts[j]);
         std::vector<uint8_t> in0((size_t)nt * np);
@@ -1697,13 +1844,24 @@ struct orbmi_slam {
             int32_t* row = best.data() + (size_t)t * np;
             std::vector<int> redo_pts, redo_j;
             auto* rt = new PhaseTimer(&phase_ms[PH_LM_SIN_REDO]);
+            // A record can change here only through an earlier target's replay (Replace, a new
+            // observation: fuse_touched) -- Tracking creates points but changes no existing
+            // point's position, normal, distances, flags or descriptor, and the refreshed
+            // descriptors are in rec0 -- so only touched points are compared.  With recording on
+            // (the parity tests) every point is compared too and a difference fails the call.
             for (int j = 0; j < np; j++) {
                 const int m = pts[j];
                 // the replay skips bad points and points already in the target (observations are
                 // only gained here, so a point in the target now was in it or is skipped anyway)
+                if (!recording && !fuse_touched.count(m)) continue;
                 if (mps[m].bad || mps[m].obs.count(kt)) continue;
                 const orbmi_mappoint r = fuse_record(m);
                 if (std::memcmp(&r, &rec0[j], sizeof(r)) != 0) {
+                    if (!fuse_touched.count(m)) {
+                        delete rt;
+                        fprintf(stderr, "orbmi_slam: Fuse record of point %d changed untouched\n", m);
+                        return ORBMI_E_STATE;
+                    }
                     redo_pts.push_back(m);
                     redo_j.push_back(j);
                 }
@@ -1843,25 +2001,34 @@ struct orbmi_slam {
     int local_bundle_adjustment(int k) {
         auto* gt = new PhaseTimer(&phase_ms[PH_LM_BA_GATHER]);
         std::vector<int> lkf{k};
-        std::set<int> local_set{k};
+        SeenSet& local_set = ba_local_mark;
+        local_set.clear();
+        local_set.insert(k);
         for (int c : kfs[k].covisible) {
             local_set.insert(c);
             if (!kfs[c].bad) lkf.push_back(c);
         }
         std::vector<int> lmp;
-        std::set<int> seen_mp;
+        SeenSet& seen_mp = ba_mp_mark;
+        seen_mp.clear();
         for (int kk : lkf)
             for (int m : kfs[kk].mps)
-                if (m >= 0 && !mps[m].bad && seen_mp.insert(m).second) lmp.push_back(m);
+                if (m >= 0 && !mps[m].bad && !seen_mp.count(m)) {
+                    seen_mp.insert(m);
+                    lmp.push_back(m);
+                }
         std::vector<int> fixed;
-        std::set<int> fixed_set;
+        SeenSet& fixed_set = ba_fixed_mark;
+        fixed_set.clear();
         for (int m : lmp)
             for (auto& o : mps[m].obs)
-                if (!local_set.count(o.first) && fixed_set.insert(o.first).second && !kfs[o.first].bad)
-                    fixed.push_back(o.first);
+                if (!local_set.count(o.first) && !fixed_set.count(o.first)) {
+                    fixed_set.insert(o.first);
+                    if (!kfs[o.first].bad) fixed.push_back(o.first);
+                }
         std::vector<int> all = lkf;
         all.insert(all.end(), fixed.begin(), fixed.end());
-        std::map<int, int> kidx;
+        std::vector<int> kidx(kfs.size(), -1);  // keyframe id -> its vertex
         for (int i = 0; i < (int)all.size(); i++) kidx[all[i]] = i;
         std::vector<orbmi_ba_keyframe> K(all.size());
         for (int i = 0; i < (int)all.size(); i++) {
@@ -1882,11 +2049,11 @@ struct orbmi_slam {
         std::vector<std::pair<int, int>> e_ref;  // (map point id, keyframe id) per edge
         for (int j = 0; j < (int)lmp.size(); j++)
             for (auto& o : mps[lmp[j]].obs) {
-                auto it = kidx.find(o.first);
-                if (kfs[o.first].bad || it == kidx.end()) continue;
+                const int vi = kidx[o.first];
+                if (kfs[o.first].bad || vi < 0) continue;
                 const KeyFrame& kf = kfs[o.first];
                 const orbmi_keypoint& kp = kf.keys[o.second];
-                E.push_back(orbmi_ba_edge{j, it->second, kp.x, kp.y, kf.ur[o.second], inv_level_sigma2[kp.octave]});
+                E.push_back(orbmi_ba_edge{j, vi, kp.x, kp.y, kf.ur[o.second], inv_level_sigma2[kp.octave]});
                 e_ref.push_back({lmp[j], o.first});
             }
         delete gt;

@@ -154,15 +154,21 @@ class StereoTracker:
             self._views[key] = v
         return v
 
-    def extract_stereo(self, d_left_right: int, rows: int, cols: int, slot=None):
+    def extract_stereo(self, d_left_right: int, rows: int, cols: int, slot=None, host=False):
         """ORBextractor(left) + ORBextractor(right) as one batch + ComputeStereoMatches into
         `slot` (default: the current one) on the extraction stream; d_left_right = device address
-        of the 2 x rows x cols u8 image pair."""
+        of the 2 x rows x cols u8 image pair (host=True: host address, copied to HBM by the
+        extraction stream itself, orbmi_extract_batch_host)."""
         L = lib()
         sl = self.slots[self.slot if slot is None else slot]
-        check("orbmi_extract_batch_device", L.orbmi_extract_batch_device(
-            self.extractor.handle, _vp(d_left_right), 2, rows, cols, cols, rows * cols, _vp(sl["kps"].data_ptr()),
-            _vp(sl["desc"].data_ptr()), _vp(sl["counts"].data_ptr()), self.cap))
+        if host:
+            check("orbmi_extract_batch_host", L.orbmi_extract_batch_host(
+                self.extractor.handle, _vp(d_left_right), 2, rows, cols, rows * cols, _vp(sl["kps"].data_ptr()),
+                _vp(sl["desc"].data_ptr()), _vp(sl["counts"].data_ptr()), self.cap))
+        else:
+            check("orbmi_extract_batch_device", L.orbmi_extract_batch_device(
+                self.extractor.handle, _vp(d_left_right), 2, rows, cols, cols, rows * cols, _vp(sl["kps"].data_ptr()),
+                _vp(sl["desc"].data_ptr()), _vp(sl["counts"].data_ptr()), self.cap))
         check("orbmi_compute_stereo_matches_batch_device", L.orbmi_compute_stereo_matches_batch_device(
             self.extractor.handle, self.cam.bf, self.cam.fx, _vp(sl["u_right"].data_ptr()), _vp(sl["depth"].data_ptr())))
         # new keypoints behind the slot's pointers: a grid pinned on an earlier frame is stale
@@ -233,38 +239,21 @@ class StereoTracker:
             mp.match_mp, mp.mps, mp.n_mps = self.match_mp.data_ptr(), local_mps, int(n_mp)
         return mp
 
-    def upload(self, h_left_right: int, rows: int, cols: int) -> int:
-        """DMA a 2 x rows x cols u8 image pair from pinned host memory into the tracker's image
-        buffer on the extraction stream (stream order: after the previous frame's extraction has
-        read the buffer, before this frame's) -> its device address.  The caller keeps the host
-        bytes unchanged until the frame's extraction has run."""
-        import torch
-        from . import _hip
-        nb = 2 * rows * cols
-        if getattr(self, "_img", None) is None or self._img.numel() < nb:
-            self._img = torch.empty(nb, dtype=torch.uint8, device=self.slots[0]["kps"].device)
-            torch.cuda.synchronize(self._img.device)
-        _hip.memcpy_h2d_async(self._img.data_ptr(), h_left_right, nb, self.stream_handle)
-        return self._img.data_ptr()
-
     def track(self, d_left_right, rows, cols, tcw, last_view, last_points, local_mps, n_mp, th_lf=7.0, th_local=1.0,
               host=False):
         """Enqueue one tracked stereo frame (Frame ctor + TrackWithMotionModel + TrackLocalMap);
         results stay on the device: self.match_lf / match_mp (final mvpMapPoints), self.outlier,
         pose records self.recs, counts self.tcounts (see results()).  host=True: d_left_right is
-        a pinned host pair, DMA'd to HBM on the extraction stream first (upload), so the copy of
-        frame k+1 overlaps frame k's tracking as its extraction does."""
-        if host and not self.pipelined:
-            d_left_right = self.upload(d_left_right, rows, cols)
+        a host pair (pinned: read in place), copied to HBM by the extraction stream ahead of its
+        extraction (orbmi_extract_batch_host), so the copy of frame k+1 overlaps frame k's
+        tracking as its extraction does."""
         if not self.pipelined:
-            self.extract_stereo(d_left_right, rows, cols)
+            self.extract_stereo(d_left_right, rows, cols, host=host)
             self.track_with_motion_model(tcw, last_view, last_points, th_lf)
             self.track_local_map(last_view, last_points, local_mps, n_mp, th_local)
             return
         s = self._next
         self._next ^= 1
-        if host:  # the image buffer is E's alone: the copy need not wait for the slot below
-            d_left_right = self.upload(d_left_right, rows, cols)
         if self._pending[s]:  # the slot's previous frame must be tracked before it is overwritten
             self._E.wait_event(self._ev_tracked[s])
         for ev in self._holds[s]:  # ... and read by every other consumer (hold_slot)
@@ -275,7 +264,7 @@ class StereoTracker:
             import torch
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             ev[0].record(self._E)
-        self.extract_stereo(d_left_right, rows, cols, slot=s)
+        self.extract_stereo(d_left_right, rows, cols, slot=s, host=host)
         self._ev_extracted[s].record(self._E)
         if fe is not None:
             ev[1].record(self._E)

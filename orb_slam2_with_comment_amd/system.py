@@ -834,12 +834,10 @@ class StereoSLAM:
         """LocalMapping::Run for one keyframe (src/LocalMapping.cc:47-128): ProcessNewKeyFrame,
         MapPointCulling, CreateNewMapPoints, SearchInNeighbors unless a keyframe is queued,
         LocalBundleAdjustment (more than 2 keyframes) and KeyFrameCulling unless one is queued."""
-        # ProcessNewKeyFrame (:152-211)
-        if self.backend_has_bow() and kf.feat_vec is None:
-            fv = self.backend.compute_bow(kf.desc)  # the native loop releases the map lock around it
-            yield L_BOW, kf.id
-            if kf.feat_vec is None:  # (Tracking may have computed it meanwhile: the same)
-                kf.feat_vec = fv
+        # ProcessNewKeyFrame (:152-211); as the native loop: the observations first, then
+        # ComputeBoW and the updated points' ComputeDistinctiveDescriptors in one window with the
+        # map lock released (the transform reads only the keyframe's descriptors)
+        need_bow = self.backend_has_bow() and kf.feat_vec is None
         updated = []
         for i, mp in enumerate(kf.map_points):
             if mp is None or mp.bad:
@@ -850,7 +848,17 @@ class StereoSLAM:
             else:   # the new stereo points the Tracking inserted
                 self.recent_mps.append(mp)
         update_normals_and_depths(updated)
-        yield from self._distinctive_gen(updated)
+        rows, off = self._obs_rows(updated)
+        if need_bow or rows:
+            fv = self.backend.compute_bow(kf.desc) if need_bow else None
+            d = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32)) if rows else None
+            yield (L_BOW, kf.id) if need_bow else (L_DISTINCTIVE, -1)
+            if need_bow and kf.feat_vec is None:  # (Tracking may have computed it meanwhile: the same)
+                kf.feat_vec = fv
+            if rows:
+                for j, mp in enumerate(updated):
+                    if off[j + 1] > off[j]:
+                        mp.desc = np.asarray(d[j], np.uint8).copy()
         kf.update_connections()
         fv = kf.feat_vec
         if fv is None:
@@ -1033,14 +1041,32 @@ class StereoSLAM:
         """ORBmatcher::Fuse(pKF, vpMapPoints, 3.0) (src/ORBmatcher.cc:977-1127): the search for
         every point on the backend, then the map updates in list order; first the descriptors
         MapPoint::Replace still owes (src/MapPoint.cc:212)."""
-        if dirty:
-            pts = sorted((m for m in dirty if not m.bad), key=lambda m: m.id)
-            yield from self._distinctive_gen(pts)
-            dirty.clear()
+        due = sorted((m for m in dirty if not m.bad), key=lambda m: m.id)
+        dirty.clear()
         pts = [mp for mp in mps if mp is not None]
         if not pts:
+            yield from self._distinctive_gen(due)
             return
-        best = yield from self._fuse_search_gen(kf, pts)
+        rows, off = self._obs_rows(due)
+        if not rows:
+            best = yield from self._fuse_search_gen(kf, pts)
+            self._fuse_replay(kf, pts, best, dirty)
+            return
+        # the native loop's one device call (orbmi_fuse_search_refresh): the owed descriptors,
+        # then the search with each due point's new descriptor
+        newd = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32))
+        at = {m.id: d for d, m in enumerate(due) if off[d + 1] > off[d]}
+        rec = self._mp_fuse_records(pts)
+        for j, mp in enumerate(pts):
+            if mp.id in at:
+                rec["desc"][j] = np.asarray(newd[at[mp.id]], np.uint8)
+        in_kf = np.array([kf in mp.observations for mp in pts], np.uint8)
+        best, _ = self.backend.fuse_search(self._kf_frame(kf), rec, in_kf, 3.0)
+        best = np.asarray(best, np.int32).copy()
+        yield L_FUSE, kf.id
+        for d, m in enumerate(due):
+            if off[d + 1] > off[d]:
+                m.desc = np.asarray(newd[d], np.uint8).copy()
         self._fuse_replay(kf, pts, best, dirty)
 
     def _fuse_targets_gen(self, targets: list, lst: list, dirty: set):

@@ -188,6 +188,49 @@ def test_batch_device_matches_host_api(orb, oracle, images):
         np.testing.assert_array_equal(dd[i, :counts[i]], d_ref)
 
 
+@pytest.mark.parametrize("pinned", [True, False])
+def test_batch_host_images(orb, oracle, images, pinned):
+    """orbmi_extract_batch_host: the images in host memory -- pinned (read in place by the copy
+    kernel on the handle's stream) or pageable (staged through the handle's pinned buffers) --
+    give the oracle's keypoints and descriptors, call after call on one handle (a pageable
+    buffer is reusable as soon as the call returns), and at an odd image size whose bytes are not a
+    multiple of 16 (the copy's byte tail)."""
+    import ctypes as C
+    import torch
+    from orb_slam2_with_comment_amd import _capi, _hip
+    p = oracle.params(2000)
+    ex = _extractor(orb, p)
+    cap = 2100
+    for names, (r, c) in ((["kitti_L0", "kitti_R0"], (376, 1241)), (["kitti_L11", "kitti_R11"], (376, 1241)),
+                          (["kitti_L0", "kitti_R11"], (371, 1237))):
+        imgs = np.stack([np.ascontiguousarray(images[n][:r, :c]) for n in names])
+        if pinned:
+            buf = _hip.PinnedBytes(imgs.nbytes)
+            buf.array[:] = imgs.reshape(-1)
+            ptr = buf.ptr
+        else:
+            buf = imgs.copy()
+            ptr = buf.ctypes.data
+        d_k = torch.zeros((2, cap, 7), dtype=torch.int32, device="cuda")
+        d_d = torch.zeros((2, cap, 32), dtype=torch.uint8, device="cuda")
+        d_n = torch.zeros(2, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        _capi.check("batch_host", _capi.lib().orbmi_extract_batch_host(
+            ex.handle, C.c_void_p(ptr), 2, r, c, r * c, C.c_void_p(d_k.data_ptr()), C.c_void_p(d_d.data_ptr()),
+            C.c_void_p(d_n.data_ptr()), cap))
+        if not pinned:
+            buf[:] = 0  # pageable input: staged during the call, free to reuse at once
+        _capi.check("sync", _capi.lib().orbmi_extractor_synchronize(ex.handle))
+        counts, kk, dd = d_n.cpu().numpy(), d_k.cpu().numpy(), d_d.cpu().numpy()
+        for i in range(2):
+            k_ref, d_ref = oracle.extract(p, imgs[i])
+            assert counts[i] == len(k_ref)
+            np.testing.assert_array_equal(kk[i, :counts[i]].view(_capi.KP_DTYPE).reshape(-1), k_ref)
+            np.testing.assert_array_equal(dd[i, :counts[i]], d_ref)
+        if pinned:
+            buf.close()
+
+
 def test_batch_levelwise_pyramid_unaligned_rows(orb, oracle, images):
     """Batches > 8 build the pyramid level by level (k_pyr_level0 / k_pyr_resize): 10 frames of an
     odd width on an odd row pitch (rows start at every byte alignment), every padded level of

@@ -165,7 +165,7 @@ for step in "$@"; do
             for i in 1 2 3; do
                 run envab_A$i 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline
                 run envab_B$i 300 env $kv python bench.py --steps 100 --warmup 10 --no-cpu-baseline
-                echo "default $(tail -1 $OUT/envab_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["phase_ms_per_frame"])')  $kv $(tail -1 $OUT/envab_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["phase_ms_per_frame"])')" | tee -a $OUT/envab.txt
+                echo "default $(tail -1 $OUT/envab_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("pcie_inclusive", {}).get("value"), d["phase_ms_per_frame"])')  $kv $(tail -1 $OUT/envab_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("pcie_inclusive", {}).get("value"), d["phase_ms_per_frame"])')" | tee -a $OUT/envab.txt
             done;;
         abbatch=*)
             # config-5 (batch mode) A/B of two library builds, 3 alternations, stage times kept
