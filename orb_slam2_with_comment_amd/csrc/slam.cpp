@@ -1398,13 +1398,16 @@ struct orbmi_slam {
         if (s.local_mapping) {
             next(PH_LM_CREATE);
             const size_t nmp0 = mps.size();
-            SLAM_CHECK(create_new_map_points(k));
+            std::vector<int> owed;
+            SLAM_CHECK(create_new_map_points(k, owed));
             log_state(k, ORBMI_KF_STATE_CREATE, (int)(mps.size() - nmp0), (uint32_t)mps.size(), slot_hash(k));
             next(PH_LM_FUSE);
-            if (new_keyframes_queued()) sin_skipped++;
-            else {
+            if (new_keyframes_queued()) {
+                sin_skipped++;
+                SLAM_CHECK(distinctive(owed));
+            } else {
                 fuse_ops = 0;
-                SLAM_CHECK(search_in_neighbors(k));
+                SLAM_CHECK(search_in_neighbors(k, owed));
                 int filled = 0;
                 for (int m : kfs[k].mps) filled += m >= 0;
                 log_state(k, ORBMI_KF_STATE_FUSE, fuse_ops, (uint32_t)filled, slot_hash(k));
@@ -1445,7 +1448,10 @@ struct orbmi_slam {
     // triangulation pair by pair, the keypoints earlier pairs claimed excluded on the device), run
     // on the keyframes' HBM copies with the map lock released; the new points are then made here in
     // the reference's order.
-    int create_new_map_points(int k) {
+    // `owed`: the new points, whose ComputeDistinctiveDescriptors the caller does (with
+    // SearchInNeighbors' first device call when that runs: one round trip fewer)
+    int create_new_map_points(int k, std::vector<int>& owed) {
+        owed.clear();
         float ow1[3];
         kf_ow(k, ow1);
         const float mb = s.bf / s.fx;
@@ -1539,9 +1545,10 @@ struct orbmi_slam {
                 fresh.push_back(mp.id);
             }
         }
-        // per point, so one batch for all pairs gives the reference's per-pair results
-        SLAM_CHECK(distinctive(fresh));
+        // ComputeDistinctiveDescriptors per point, so one batch for all pairs gives the
+        // reference's per-pair results; UpdateNormalAndDepth does not read the descriptor
         normals(fresh);
+        owed = std::move(fresh);
         return ORBMI_OK;
     }
 
@@ -1762,12 +1769,15 @@ struct orbmi_slam {
     // of a survivor is done before the first read of its record (a survivor gains no observation
     // from AddObservation before then: only listed points do, and a listed dirty point is
     // recomputed before the target that could add one).
-    int fuse_targets(const std::vector<int>& targets, const std::vector<int>& list, std::set<int>& dirty) {
+    // `owed`: points whose descriptors CreateNewMapPoints left to compute -- computed in the same
+    // device call as the batched searches, which read them.
+    int fuse_targets(const std::vector<int>& targets, const std::vector<int>& list, std::set<int>& dirty,
+                     const std::vector<int>& owed) {
         std::vector<int> pts;
         for (int m : list)
             if (m >= 0) pts.push_back(m);
         const int nt = (int)targets.size(), np = (int)pts.size();
-        if (nt == 0 || np == 0) return ORBMI_OK;
+        if (nt == 0 || np == 0) return distinctive(owed);
         auto* prep = new PhaseTimer(&phase_ms[PH_LM_SIN_PREP]);
         fuse_touched.clear();
         std::vector<orbmi_mappoint> rec0(np);
@@ -1782,12 +1792,44 @@ struct orbmi_slam {
         }
         std::vector<int32_t> best((size_t)nt * np), dist((size_t)nt * np);
         orbmi_matcher* mt = lmm();
+        // the owed descriptors (ascending ids, as created) and the records that take them
+        std::vector<int> due;
+        for (int m : owed)
+            if (!mps[m].bad) due.push_back(m);
+        std::vector<uint8_t> orows;
+        std::vector<int32_t> ooff, ofrom;
+        obs_rows(due, orows, ooff);
+        const int nd = (int)due.size();
+        std::vector<uint8_t> odesc;
+        if (!orows.empty()) {
+            ofrom.assign(np, -1);
+            for (int j = 0; j < np; j++) {
+                auto it = std::lower_bound(due.begin(), due.end(), pts[j]);
+                if (it != due.end() && *it == pts[j]) {
+                    const int d = (int)(it - due.begin());
+                    if (ooff[d + 1] > ooff[d]) ofrom[j] = d;
+                }
+            }
+            odesc.resize((size_t)nd * 32);
+            for (int d = 0; d < nd; d++) std::memcpy(&odesc[32 * d], mps[due[d]].desc, 32);
+        }
         delete prep;
         SLAM_CHECK(unlocked(ORBMI_SCHED_L_FUSE_BATCH, -1, [&] {
             PhaseTimer pt(&phase_ms[PH_LM_FUSE_CALL]);
-            return orbmi_fuse_search_batch(mt, nt, views.data(), rec0.data(), in0.data(), np, 3.f, best.data(),
-                                           dist.data(), nullptr);
+            if (orows.empty())
+                return orbmi_fuse_search_batch(mt, nt, views.data(), rec0.data(), in0.data(), np, 3.f, best.data(),
+                                               dist.data(), nullptr);
+            std::vector<int32_t> dbest(nd);
+            return orbmi_fuse_search_refresh(mt, orows.data(), ooff.data(), nd, dbest.data(), odesc.data(), nt,
+                                             views.data(), rec0.data(), ofrom.data(), in0.data(), np, 3.f, best.data(),
+                                             dist.data());
         }));
+        if (!orows.empty()) {
+            for (int d = 0; d < nd; d++)
+                if (ooff[d + 1] > ooff[d]) std::memcpy(mps[due[d]].desc, &odesc[32 * d], 32);
+            for (int j = 0; j < np; j++)
+                if (ofrom[j] >= 0) std::memcpy(rec0[j].desc, &odesc[32 * ofrom[j]], 32);
+        }
         std::map<int, int> listed;  // point -> its (first) position in pts
         for (int j = np - 1; j >= 0; j--) listed[pts[j]] = j;
         for (int t = 0; t < nt; t++) {
@@ -1878,7 +1920,7 @@ struct orbmi_slam {
         return ORBMI_OK;
     }
 
-    int search_in_neighbors(int k) {  // src/LocalMapping.cc:589-674, stereo: nn = 10
+    int search_in_neighbors(int k, const std::vector<int>& owed) {  // src/LocalMapping.cc:589-674, stereo: nn = 10
         std::vector<int> targets;
         const std::vector<int> neigh(kfs[k].covisible.begin(),
                                      kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
@@ -1895,7 +1937,7 @@ struct orbmi_slam {
         }
         std::set<int> dirty;
         const std::vector<int> matches = kfs[k].mps;
-        SLAM_CHECK(fuse_targets(targets, matches, dirty));
+        SLAM_CHECK(fuse_targets(targets, matches, dirty, owed));
         std::vector<int> cands;
         for (int t : targets)
             for (int m : kfs[t].mps) {

@@ -869,11 +869,13 @@ class StereoSLAM:
         self._map_point_culling(kf)
         if self.local_mapping_full:
             n0 = len(self.mappoints)
-            yield from self._create_new_map_points_gen(kf)
+            owed = (yield from self._create_new_map_points_gen(kf)) or []
             self._log_state(kf, KF_STATE_CREATE, len(self.mappoints) - n0, len(self.mappoints), _slot_hash(kf))
-            if not self._queued():
+            if self._queued():
+                yield from self._distinctive_gen(owed)
+            else:
                 self._fuse_ops = 0
-                yield from self._search_in_neighbors_gen(kf)
+                yield from self._search_in_neighbors_gen(kf, owed)
                 filled = sum(1 for mp in kf.map_points if mp is not None)
                 self._log_state(kf, KF_STATE_FUSE, self._fuse_ops, filled, _slot_hash(kf))
         self._abort = False
@@ -938,8 +940,9 @@ class StereoSLAM:
         (orbmi_triangulate_matches), new points with both observations.  As the native loop does
         it in one device call: every pair's search and triangulation first (a keypoint an earlier
         pair triangulated is not searched again: the reference's `if (pMP1) continue`), then the
-        new points pair by pair with CheckNewKeyFrames between pairs (:331), then one
-        ComputeDistinctiveDescriptors of them all (per point: the same as pair by pair)."""
+        new points pair by pair with CheckNewKeyFrames between pairs (:331).  Their
+        ComputeDistinctiveDescriptors (per point: the same as pair by pair) is returned as owed, to
+        the caller, which does it with SearchInNeighbors' first device call."""
         import ctypes as C
         from ._capi import check, lib
         if kf.feat_vec is None:
@@ -991,9 +994,9 @@ class StereoSLAM:
                 self.mappoints.append(mp)
                 self.recent_mps.append(mp)
                 fresh.append(mp)
-        yield from self._distinctive_gen(fresh)
         update_normals_and_depths(fresh)
         del keep1
+        return fresh
 
     def _mp_fuse_records(self, mps: list) -> np.ndarray:
         rec = np.zeros(len(mps), MAPPOINT_DTYPE)
@@ -1069,7 +1072,7 @@ class StereoSLAM:
                 m.desc = np.asarray(newd[d], np.uint8).copy()
         self._fuse_replay(kf, pts, best, dirty)
 
-    def _fuse_targets_gen(self, targets: list, lst: list, dirty: set):
+    def _fuse_targets_gen(self, targets: list, lst: list, dirty: set, owed=()):
         """Fuse(target, the keyframe's points) for every target in order (src/LocalMapping.cc:
         620-628), as csrc/slam.cpp fuse_targets runs it: every target searched on the records as
         they are before the first one, then per target: the owed descriptors of listed points
@@ -1079,14 +1082,28 @@ class StereoSLAM:
         pts = [mp for mp in lst if mp is not None]
         nt, npts = len(targets), len(pts)
         if nt == 0 or npts == 0:
+            yield from self._distinctive_gen(list(owed))
             return
         rec0 = self._mp_fuse_records(pts)
+        # the descriptors CreateNewMapPoints owes, in the batch's device call (the searches read them)
+        due = [m for m in owed if not m.bad]
+        orows, ooff = self._obs_rows(due)
+        if orows:
+            odesc = self.backend.distinctive(np.asarray(orows, np.uint8), np.asarray(ooff, np.int32))
+            at = {m.id: d for d, m in enumerate(due) if ooff[d + 1] > ooff[d]}
+            for j, mp in enumerate(pts):
+                if mp.id in at:
+                    rec0["desc"][j] = np.asarray(odesc[at[mp.id]], np.uint8)
         best = []
         for t in targets:
             in0 = np.array([t in mp.observations for mp in pts], np.uint8)
             bi, _ = self.backend.fuse_search(self._kf_frame(t), rec0, in0, 3.0)
             best.append(np.asarray(bi, np.int32).copy())
         yield L_FUSE_BATCH, -1
+        if orows:
+            for d, m in enumerate(due):
+                if ooff[d + 1] > ooff[d]:
+                    m.desc = np.asarray(odesc[d], np.uint8).copy()
         listed = {}
         for j in range(npts - 1, -1, -1):
             listed[pts[j]] = j
@@ -1133,7 +1150,7 @@ class StereoSLAM:
                     row[j] = b2[q]
             self._fuse_replay(kt, pts, row, dirty)
 
-    def _search_in_neighbors_gen(self, kf: KeyFrame):
+    def _search_in_neighbors_gen(self, kf: KeyFrame, owed=()):
         """LocalMapping::SearchInNeighbors (src/LocalMapping.cc:589-674), stereo: nn = 10."""
         targets = []
         for k in kf.best_covisibility(10):
@@ -1146,7 +1163,7 @@ class StereoSLAM:
                     continue
                 targets.append(k2)
         dirty = set()
-        yield from self._fuse_targets_gen(targets, list(kf.map_points), dirty)
+        yield from self._fuse_targets_gen(targets, list(kf.map_points), dirty, owed)
         cands = []
         for k in targets:
             for mp in k.map_points:

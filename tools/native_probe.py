@@ -6,6 +6,10 @@ import sys
 import tempfile
 import time
 
+# as bench.py: 8 hardware queues (the process's streams then map onto queues of their own)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
