@@ -1939,9 +1939,7 @@ struct MfmaSolveLds {
     double Wt[2][T + 1][4][64];          // -W^T_jp, buffer p & 1 (C layout)
     double Lt[NL > 0 ? NL : 1][4][64];   // L^T_jp (C layout: row t contiguous at [t >> 2][16 (t & 3)])
     double ys[16 * T], xs[16 * T];
-    double Pv[16 * T];                   // back substitution: sum_{j >= p + 2} L^T_jp x_j (helper waves)
     int flag_dg, flag_e, row_cnt[T], fail;
-    int flag_x, flag_p[T];               // x_j published (count), Pv[p] published
     __device__ static int lt_index(int p, int j) { return p * (2 * T - p - 1) / 2 + (j - p - 1); }
 };
 
@@ -2079,48 +2077,6 @@ __device__ inline void mfma_bulk_wave(const BaDev& a, MfmaSolveLds<T>& L, int la
     }
 }
 
-// The back substitution's helpers: waves 0..2 once the factorisation is done.  Wave h keeps, for
-// each p = h (mod 3) <= T - 3, the partial sum P_p = sum_{j >= p + 2} L^T_jp x_j in registers,
-// adding x_j's term as soon as the factor wave publishes x_j, and publishes P_p (reduced over the
-// four column groups) once x_{p+2}'s term is in -- one step before the factor wave needs it.  So
-// the factor wave's chain per panel is only L^T_{p+1,p} x_{p+1}, the subtraction and E_p^T r.
-constexpr int kMfmaHelpers = 3;
-template <int T>
-__device__ inline void mfma_backsub_helper(MfmaSolveLds<T>& L, int lane, int h) {
-    constexpr int KH = (T + kMfmaHelpers - 1) / kMfmaHelpers;
-    if (h > T - 3) return;  // no p of this wave
-    lds_wait_ge(&L.row_cnt[T - 1], 1 + kMfmaBulkWaves);
-    if (L.fail) return;
-    const int g = lane >> 4, t = lane & 15, rot = (t + 4 * g) & 15;
-    double acc[KH];
-#pragma unroll
-    for (int k = 0; k < KH; k++) acc[k] = 0.0;
-    for (int j = T - 1; j >= h + 2; j--) {
-        lds_wait_ge(&L.flag_x, T - j);
-        const double xj = L.xs[16 * j + rot];
-#pragma unroll
-        for (int k = 0; k < KH; k++) {
-            const int p = h + kMfmaHelpers * k;
-            if (p > j - 2) continue;  // (uniform)
-            const double* row = &L.Lt[MfmaSolveLds<T>::lt_index(p, j)][t >> 2][16 * (t & 3) + 4 * g];
-            const double l0 = row[0], l1 = row[1], l2 = row[2], l3 = row[3];
-            asm volatile("s_nop 1\n\t"
-                         "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf"
-                         : "+v"(acc[k])
-                         : "v"(xj), "v"(l0), "v"(l1), "v"(l2), "v"(l3));
-            if (p == j - 2) {  // complete: reduce over the column groups and publish
-                double sp = swap_combine<16>(acc[k], acc[k]);
-                sp = swap_combine<32>(sp, sp);
-                if (lane < 16) L.Pv[16 * p + t] = sp;
-                if (lane == 0) lds_publish(&L.flag_p[p], 1);
-            }
-        }
-    }
-}
-
 template <int T>
 __device__ __attribute__((always_inline)) inline void solve_mfma_body(const BaDev& a) {
     const BaCtl& ctl = *a.ctl;
@@ -2134,20 +2090,12 @@ __device__ __attribute__((always_inline)) inline void solve_mfma_body(const BaDe
     if (tid == 0) {
         L.flag_dg = L.flag_e = -1;
         L.fail = 0;
-        L.flag_x = 0;
     }
     if (tid < T) L.row_cnt[tid] = 0;
-    if (tid < T) L.flag_p[tid] = 0;
     __syncthreads();
-#ifdef ORBMI_BA_BACKSUB_SERIAL  // A/B: the factor wave's serial back substitution alone
     if (w == 0) { mfma_critical_wave<T>(a, L, lane, SOLVE_STAMP_PTR); return; }
     if (w == 1) { mfma_bulk_wave<T, 0>(a, L, lane); return; }
     if (w == 2) { mfma_bulk_wave<T, 1>(a, L, lane); return; }
-#else
-    if (w == 0) { mfma_critical_wave<T>(a, L, lane, SOLVE_STAMP_PTR); mfma_backsub_helper<T>(L, lane, 0); return; }
-    if (w == 1) { mfma_bulk_wave<T, 0>(a, L, lane); mfma_backsub_helper<T>(L, lane, 1); return; }
-    if (w == 2) { mfma_bulk_wave<T, 1>(a, L, lane); mfma_backsub_helper<T>(L, lane, 2); return; }
-#endif
     // ---- wave 3: A_pp -> E_p = L_pp^-1, D_p^-1 as soon as A_pp is final
     for (int p = 0; p < T; p++) {
         lds_wait_ge(&L.flag_dg, p);
@@ -2193,79 +2141,6 @@ __device__ __attribute__((always_inline)) inline void solve_mfma_body(const BaDe
     // column (c + 4 g) & 15 of E_p^T r (four partial sums over t).  Software-pipelined: panel
     // p - 1's LDS operands (L^T rows, y, E column) are loaded while panel p computes, so each
     // panel waits on its dependent FMAs only, not on three LDS round trips.
-#ifndef ORBMI_BA_BACKSUB_SERIAL
-    // The chain: r = y_p - L^T_{p+1,p} x_{p+1} - P_p (P_p from the helper waves), x_p = E_p^T r.
-    // Lane (g, t) as below; x_{p+1} stays in a register (rotated), the next panel's operands (the
-    // L^T_{p,p-1} row, y, E column) are loaded while this one computes.
-    {
-        const int g = q, t = n, rot = (n + 4 * g) & 15;
-        double xn = 0.0;
-        double l4b[2][4], e4b[2][16], ysb[2];
-        auto load = [&](int p, int b) {
-            if (p + 1 < T) {
-                const double* row = &L.Lt[MfmaSolveLds<T>::lt_index(p, p + 1)][t >> 2][16 * (t & 3) + 4 * g];
-#pragma unroll
-                for (int u = 0; u < 4; u++) l4b[b][u] = row[u];
-            }
-            ysb[b] = L.ys[16 * p + t];
-            const double* Ec = &L.Eall[p][rot];
-#pragma unroll
-            for (int u = 0; u < 16; u++) e4b[b][u] = Ec[16 * u];
-        };
-        load(T - 1, (T - 1) & 1);
-#pragma unroll
-        for (int p = T - 1; p >= 0; p--) {
-            const int b = p & 1;
-            if (p > 0) load(p - 1, b ^ 1);
-            double r = ysb[b];
-            if (p + 1 < T) {
-                double a0 = 0.0;
-                asm volatile("s_nop 1\n\t"
-                             "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-                             "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-                             "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-                             "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf"
-                             : "+v"(a0)
-                             : "v"(xn), "v"(l4b[b][0]), "v"(l4b[b][1]), "v"(l4b[b][2]), "v"(l4b[b][3]));
-                double s = swap_combine<16>(a0, a0);
-                s = swap_combine<32>(s, s);
-                r -= s;
-            }
-            if (p + 2 < T) {
-                lds_wait_ge(&L.flag_p[p], 1);
-                r -= L.Pv[16 * p + t];
-            }
-            const double* e4 = e4b[b];
-            double x0 = 0.0, x1 = 0.0, x2 = 0.0, x3 = 0.0;
-            asm volatile("s_nop 1\n\t"
-                         "v_fmac_f64_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %4, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %1, %4, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %2, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %3, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %1, %4, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %2, %4, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %3, %4, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %0, %4, %17 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %1, %4, %18 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %2, %4, %19 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-                         "v_fmac_f64_dpp %3, %4, %20 row_newbcast:15 row_mask:0xf bank_mask:0xf"
-                         : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
-                         : "v"(r), "v"(e4[0]), "v"(e4[1]), "v"(e4[2]), "v"(e4[3]), "v"(e4[4]), "v"(e4[5]), "v"(e4[6]),
-                           "v"(e4[7]), "v"(e4[8]), "v"(e4[9]), "v"(e4[10]), "v"(e4[11]), "v"(e4[12]), "v"(e4[13]),
-                           "v"(e4[14]), "v"(e4[15]));
-            const double x = (x0 + x1) + (x2 + x3);
-            xn = x;
-            if (lane < 16) L.xs[16 * p + t] = x;  // group 0: unrotated
-            if (p >= 2 && lane == 0) lds_publish(&L.flag_x, T - p);  // (x_0, x_1 have no helper readers)
-        }
-        wave_sync_lds();
-    }
-#else
     {
         const int g = q, t = n, rot = (n + 4 * g) & 15;
         double xr[T];
@@ -2334,7 +2209,6 @@ __device__ __attribute__((always_inline)) inline void solve_mfma_body(const BaDe
         }
         wave_sync_lds();
     }
-#endif
     SOLVE_STAMP(lane == 0, 254);
     const double lam = a.scal[3];
     for (int qq = lane; qq < N; qq += 64) a.xp[qq] = L.xs[qq];
