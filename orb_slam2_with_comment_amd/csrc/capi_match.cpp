@@ -44,20 +44,37 @@ uint8_t* Matcher::mirror(const void* d) {
     return nullptr;
 }
 
+hipError_t Matcher::flush_up() {
+    if (!up.n) return hipSuccess;
+    const hipError_t e = hipMemcpyAsync(up.d, up.h, up.n, hipMemcpyHostToDevice, stream);
+    up.n = 0;
+    if (e != hipSuccess && up_err == hipSuccess) up_err = e;
+    return e;
+}
+
 hipError_t Matcher::h2d(void* d, const void* src, size_t bytes) {
     if (!bytes) return hipSuccess;
     uint8_t* h = mirror(d);
-    if (!h) return hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, stream);
+    if (!h) return hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ls());
     memcpy(h, src, bytes);
-    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+    // the allocation right after the pending range (stage() rounds to 256 B; the gap is the
+    // previous allocation's padding): extend the range, else send it and start a new one
+    const size_t end = (up.n + 255) & ~(size_t)255;
+    if (up.n && (uint8_t*)d == up.d + end && h == up.h + end) {
+        up.n = end + bytes;
+        return hipSuccess;
+    }
+    const hipError_t e = flush_up();
+    up = PendUp{(uint8_t*)d, h, bytes};
+    return e;
 }
 
 hipError_t Matcher::d2h(void* user, const void* d, size_t bytes) {
     if (!bytes) return hipSuccess;
     uint8_t* h = mirror(d);
-    if (!h) return hipMemcpyAsync(user, d, bytes, hipMemcpyDeviceToHost, stream);
+    if (!h) return hipMemcpyAsync(user, d, bytes, hipMemcpyDeviceToHost, ls());
     pend.push_back(Pend{user, h, bytes});
-    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
+    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ls());
 }
 
 void Matcher::d2h_flush() {
@@ -66,6 +83,8 @@ void Matcher::d2h_flush() {
 }
 
 void Matcher::arena_reset() {
+    (void)flush_up();  // (nothing is left pending by a finished call; kept for safety)
+    up_err = hipSuccess;
     // the generation just used may still be read by the work enqueued so far: mark it with an
     // event, move on, and wait only for the generation about to be reused
     bool used = false;
@@ -91,6 +110,7 @@ void Matcher::arena_reset() {
 
 void Matcher::release() {
     (void)hipSetDevice(device);
+    if (stream) (void)flush_up();
     if (own_stream && stream) (void)hipStreamSynchronize(stream);
     if (!own_stream && stream) (void)hipStreamSynchronize(stream);  // staged inputs may still be read
     void* ptrs[] = {d_cell_start, d_cell_list, d_kp_cell, d_mcell_start, d_mcell_list, d_mkp_cell, d_cand, d_ncand, d_top,
@@ -157,12 +177,14 @@ T* dev_out(Matcher& m, T* p, size_t n, std::vector<OutBuf>& outs) {
 int finish(Matcher& m, std::vector<OutBuf>& outs, int* nmatches_dev, int* nmatches, int* extra_dev = nullptr,
            int* extra = nullptr) {
     bool wait = false;
+    ORBMI_HIP(m.flush_up());
+    if (m.up_err != hipSuccess) return ORBMI_E_HIP;
     for (OutBuf& o : outs)
         if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     int tmp[2] = {0, 0};
-    if (nmatches && nmatches_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
-    if (extra && extra_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.stream)); wait = true; }
-    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (nmatches && nmatches_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[0], nmatches_dev, sizeof(int), hipMemcpyDeviceToHost, m.ls())); wait = true; }
+    if (extra && extra_dev) { ORBMI_HIP(hipMemcpyAsync(&tmp[1], extra_dev, sizeof(int), hipMemcpyDeviceToHost, m.ls())); wait = true; }
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.ls()));
     m.d2h_flush();
     if (nmatches) *nmatches = tmp[0];
     if (extra) *extra = tmp[1];
@@ -225,7 +247,7 @@ int make_fv(Matcher& m, const orbmi_feature_vector* v, DevFV* d) {
 int scalars(Matcher& m) {
     int rc = orbmi::ensure_buf(&m.d_scalars, &m.cap_scalars, 4);
     if (rc) return rc;
-    ORBMI_HIP(hipMemsetAsync(m.d_scalars, 0, 4 * sizeof(int), m.stream));
+    ORBMI_HIP(hipMemsetAsync(m.d_scalars, 0, 4 * sizeof(int), m.ls()));
     return ORBMI_OK;
 }
 
@@ -522,7 +544,7 @@ int orbmi_match_descriptors_segments(orbmi_matcher* h, const uint8_t* q_desc, in
     if ((rc = scalars(m))) return rc;
     std::vector<OutBuf> outs;
     int* d_out = dev_out(m, match, (size_t)nq, outs);
-    if (nseg * seg_capacity == 0 && nq > 0) ORBMI_HIP(hipMemsetAsync(d_out, 0xFF, (size_t)nq * sizeof(int), m.stream));
+    if (nseg * seg_capacity == 0 && nq > 0) ORBMI_HIP(hipMemsetAsync(d_out, 0xFF, (size_t)nq * sizeof(int), m.ls()));
     else if ((rc = orbmi::launch_xmatch(m, d_q, nq, nq_device, d_t, nseg, seg_capacity, d_cnt, skip_seg, th, ratio,
                                         d_out, m.d_scalars)))
         return rc;
@@ -612,13 +634,15 @@ int orbmi_search_for_triangulation_batch(orbmi_matcher* h, const orbmi_frame_vie
                                           d_out)))
         return rc;
     bool wait = false;
+    ORBMI_HIP(m.flush_up());
+    if (m.up_err != hipSuccess) return ORBMI_E_HIP;
     for (OutBuf& o : outs)
         if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     if (nmatches) {
         ORBMI_HIP(m.d2h(nmatches, d_counts, (size_t)npairs * sizeof(int)));
         wait = true;
     }
-    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.ls()));
     m.d2h_flush();
     return ORBMI_OK;
 }
@@ -757,13 +781,15 @@ int orbmi_fuse_search_batch(orbmi_matcher* h, int nkf, const orbmi_frame_view* k
     if (!d_k || !d_cnt) return ORBMI_E_HIP;
     if ((rc = orbmi::launch_fuse_multi(m, nkf, K.data(), d_k, d_mps, n_mp, th, d_bi, d_bd, d_cnt))) return rc;
     bool wait = false;
+    ORBMI_HIP(m.flush_up());
+    if (m.up_err != hipSuccess) return ORBMI_E_HIP;
     for (OutBuf& o : outs)
         if (o.bytes) { ORBMI_HIP(m.d2h(o.user, o.dev, o.bytes)); wait = true; }
     if (ncandidates) {
         ORBMI_HIP(m.d2h(ncandidates, d_cnt, sizeof(int) * nkf));
         wait = true;
     }
-    if (wait) ORBMI_HIP(hipStreamSynchronize(m.stream));
+    if (wait) ORBMI_HIP(hipStreamSynchronize(m.ls()));
     m.d2h_flush();
     return ORBMI_OK;
 }
@@ -801,7 +827,7 @@ int orbmi_fuse_search_refresh(orbmi_matcher* h, const uint8_t* obs_desc, const i
         orbmi_mappoint* d_mps = (orbmi_mappoint*)m.stage(sizeof(orbmi_mappoint) * n_mp);
         if (!d_mps) return ORBMI_E_HIP;
         if (on_device(mps))
-            ORBMI_HIP(hipMemcpyAsync(d_mps, mps, sizeof(orbmi_mappoint) * n_mp, hipMemcpyDeviceToDevice, m.stream));
+            ORBMI_HIP(hipMemcpyAsync(d_mps, mps, sizeof(orbmi_mappoint) * n_mp, hipMemcpyDeviceToDevice, m.ls()));
         else
             ORBMI_HIP(m.h2d(d_mps, mps, sizeof(orbmi_mappoint) * n_mp));
         if (desc_from && nd > 0) {

@@ -120,6 +120,17 @@ struct Matcher {
     uint8_t* mirror(const void* d);  // host mirror of a staged device address, else nullptr
     hipError_t h2d(void* d, const void* src, size_t bytes);    // stream-ordered upload
     hipError_t d2h(void* user, const void* d, size_t bytes);   // stream-ordered read-back
+    // Consecutive uploads into adjacent staging allocations go to the device as one copy: h2d
+    // fills the mirror and extends the pending range; ls() (the stream for any enqueue: launch,
+    // copy, wait) sends it first.  Each copy on the stream is a blit dispatch of several
+    // microseconds, and a call stages 2-6 inputs.
+    struct PendUp { uint8_t* d = nullptr; uint8_t* h = nullptr; size_t n = 0; } up;
+    hipError_t up_err = hipSuccess;
+    hipError_t flush_up();
+    hipStream_t ls() {
+        if (up.n) (void)flush_up();
+        return stream;
+    }
     void d2h_flush();                                          // after the stream's wait
     void arena_reset();
     void release();

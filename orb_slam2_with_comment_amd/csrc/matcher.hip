@@ -569,14 +569,11 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         Tc = frame_pose(a.F);
         motion_direction(a.F, Tc.m, a.LF, a.mono, &fw, &bw);
     }
-    if (a.gate && gv >= a.gate_min) return;  // uniform: every thread reads before any write
-    const int n = a.F.n_dev ? min(nFv, a.F.n) : a.F.n;
-    const int nq = a.mode == 1 ? (a.LF.n_dev ? min(nLv, a.LF.n) : a.LF.n) : a.nq;  // (a.nq stays unmodified)
-    const bool regs = nq <= kGreedyThreads * kGreedyQPer;
     const bool ori = a.mode == 1 && a.check_ori;
-    // round trip 2: the queries' counts, prefixes, observation flags (and LF angles), and the
-    // keypoints' occupancy and octave, all issued before the first use (query and keypoint
-    // indices clamped into range: straight-line loads, no branch between them)
+    // the same round trip: the queries' counts, prefixes, observation flags (and LF angles), and
+    // the keypoints' occupancy and octave, for every slot up to the arrays' capacities (the device
+    // counts above are not known yet; indices clamped into range, slots past the counts unused)
+    const int nCapF = a.F.n, nqCap = a.mode == 1 ? a.LF.n : a.nq;
     int res[kGreedyQPer], nc[kGreedyQPer];
     unsigned pre[kGreedyQPer][kGreedyPre];
     bool obs[kGreedyQPer];
@@ -592,28 +589,47 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         o0[u] = 0; v0[u] = 0;
-        if (u * kGreedyThreads < n) {  // uniform: slots past n issue nothing
-            const int ic = min(tid + u * kGreedyThreads, n - 1);
+        if (u * kGreedyThreads < nCapF) {  // uniform: slots past the capacity issue nothing
+            const int ic = min(tid + u * kGreedyThreads, nCapF - 1);
             o0[u] = a.occ0[ic];
             v0[u] = a.F.keys[ic].octave;
         }
     }
+    int ncv[kGreedyQPer];
+    unsigned flv[kGreedyQPer];
+    float alv[kGreedyQPer];
+    unsigned long long ev[kGreedyQPer][kGreedyPre];
+    unsigned sink = 0;
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) {
+        ncv[k] = 0; flv[k] = 0; alv[k] = 0.f;
+#pragma unroll
+        for (int j = 0; j < kGreedyPre; j++) ev[k][j] = 0;
+        if (k * kGreedyThreads >= nqCap) continue;  // uniform: slots past the capacity issue nothing
+        const int qc = min(tid + k * kGreedyThreads, nqCap - 1);
+        ncv[k] = a.ncand[qc];
+        flv[k] = a.mode == 0 ? a.mps[qc].flags : a.lfp[qc].flags;
+        alv[k] = *(ori ? &a.LF.keys[qc].angle : (const float*)a.ncand);
+        const unsigned long long* t = a.top + (long long)qc * kTopK;
+#pragma unroll
+        for (int j = 0; j < kGreedyPre; j++) ev[k][j] = t[j];
+    }
+    // every load above is issued before the gate's branch (one wait for all of them; a load the
+    // compiler sank past the branch would make a second round trip)
+#pragma unroll
+    for (int k = 0; k < kGreedyQPer; k++) {
+        sink ^= (unsigned)ncv[k] ^ flv[k] ^ __float_as_uint(alv[k]);
+#pragma unroll
+        for (int j = 0; j < kGreedyPre; j++) sink ^= (unsigned)ev[k][j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) sink ^= (unsigned)(o0[u] ^ v0[u]);
+    asm volatile("" ::"v"(sink));
+    if (a.gate && gv >= a.gate_min) return;  // uniform: every thread reads before any write
+    const int n = a.F.n_dev ? min(nFv, a.F.n) : a.F.n;
+    const int nq = a.mode == 1 ? (a.LF.n_dev ? min(nLv, a.LF.n) : a.LF.n) : a.nq;  // (a.nq stays unmodified)
+    const bool regs = nq <= kGreedyThreads * kGreedyQPer;
     if (regs && nq > 0) {
-        int ncv[kGreedyQPer];
-        unsigned flv[kGreedyQPer];
-        float alv[kGreedyQPer];
-        unsigned long long ev[kGreedyQPer][kGreedyPre];
-#pragma unroll
-        for (int k = 0; k < kGreedyQPer; k++) {
-            if (k * kGreedyThreads >= nq) break;  // uniform: slots past nq issue nothing
-            const int qc = min(tid + k * kGreedyThreads, nq - 1);
-            ncv[k] = a.ncand[qc];
-            flv[k] = a.mode == 0 ? a.mps[qc].flags : a.lfp[qc].flags;
-            alv[k] = *(ori ? &a.LF.keys[qc].angle : (const float*)a.ncand);
-            const unsigned long long* t = a.top + (long long)qc * kTopK;
-#pragma unroll
-            for (int j = 0; j < kGreedyPre; j++) ev[k][j] = t[j];
-        }
 #pragma unroll
         for (int k = 0; k < kGreedyQPer; k++) {
             if (tid + k * kGreedyThreads >= nq) continue;
@@ -670,6 +686,9 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         // keypoint idx is taken for query q: occupied on entry, or claimed this round by an earlier query
         // (one compare: claims of older rounds carry larger tags, 0 = occupied on entry)
         auto taken = [&](int idx, int q) { return claim[idx] < (tag | q); };
+        // (claims double-buffered by round parity, posted right after each evaluation, one barrier
+        // per round: no gain, the waves then wait at that barrier for the slowest one's atomics --
+        // profiles/r06/greedy_ab.txt)
         if (regs) {
 #pragma unroll
             for (int k = 0; k < kGreedyQPer; k++)
@@ -814,7 +833,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     uint8_t* rejected = occ0;
     for (int i = tid; i < n; i += blockDim.x) { last[i] = -1; rejected[i] = 0; }
     if (tid < HISTO_LENGTH) hist[tid] = 0;
-    if (tid == 0) flag[1] = 0;
+    if (tid == 0) flag[3] = 0;
     __syncthreads();
     int fbin[kGreedyQPer];
     int nmine = 0;
@@ -851,7 +870,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
     // thread serialises the wave's 64 atomics)
     auto wave_count = [&](int c, int sign) {
         c = (int)wave_sum((double)c);
-        if (lane == 0 && c) atomicAdd(&flag[1], sign * c);
+        if (lane == 0 && c) atomicAdd(&flag[3], sign * c);
     };
     wave_count(nmine, 1);
     __syncthreads();
@@ -884,7 +903,7 @@ __global__ __launch_bounds__(kGreedyThreads) void k_greedy(GreedyArgs a) {
         __syncthreads();
     }
     for (int i = tid; i < n; i += blockDim.x) a.out[i] = rejected[i] ? -2 : last[i];
-    if (tid == 0) *a.nmatches = flag[1];
+    if (tid == 0) *a.nmatches = flag[3];
     if (!g_greedy_on) return;  // statistics only once a probe asked for them
     if (nslow) atomicAdd(&g_greedy_stats[3], (unsigned long long)nslow);
     if (tid == 0) {
@@ -1131,9 +1150,9 @@ int launch_xmatch(Matcher& m, const uint8_t* qd, int nq_cap, const int* nq_dev, 
     nsplit = (int)std::max(1LL, (ntrain + chunk - 1) / chunk);
     int rc;
     if ((rc = ensure_buf(&m.d_cand, &m.cap_cand, (size_t)nsplit * nq_cap * 2))) return rc;
-    hipLaunchKernelGGL(k_xmatch_partial, dim3(qblocks, nsplit), dim3(256), 0, m.stream, qd, nq_cap, nq_dev, td, nseg,
+    hipLaunchKernelGGL(k_xmatch_partial, dim3(qblocks, nsplit), dim3(256), 0, m.ls(), qd, nq_cap, nq_dev, td, nseg,
                        seg_cap, seg_counts, skip_seg, chunk, m.d_cand);
-    hipLaunchKernelGGL(k_xmatch_final, dim3((nq_cap + 255) / 256), dim3(256), 0, m.stream, nq_cap, nq_dev, nsplit,
+    hipLaunchKernelGGL(k_xmatch_final, dim3((nq_cap + 255) / 256), dim3(256), 0, m.ls(), nq_cap, nq_dev, nsplit,
                        m.d_cand, th, ratio, match, nmatches);
     return ORBMI_OK;
 }
@@ -1155,7 +1174,7 @@ static int grid_for(Matcher& m, const DevFrame& F, const int* gate = nullptr, in
     if ((rc = ensure_buf(&m.d_cell_start, &m.cap_cell_start, (size_t)kGridCells + 1))) return rc;
     if ((rc = ensure_buf(&m.d_cell_list, &m.cap_cell_list, (size_t)std::max(F.n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_kp_cell, &m.cap_kp_cell, (size_t)std::max(F.n, 1)))) return rc;
-    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.stream, F, m.d_cell_start, m.d_cell_list, m.d_kp_cell,
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.ls(), F, m.d_cell_start, m.d_cell_list, m.d_kp_cell,
                        gate, gate_min);
     return ORBMI_OK;
 }
@@ -1176,7 +1195,7 @@ int pin_grid(Matcher& m, const DevFrame& F) {
 int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int n, float cosl,
                    orbmi_mappoint_track* tr, int* n_in_view) {
     if (n <= 0) return ORBMI_OK;
-    hipLaunchKernelGGL(k_frustum, dim3((n + 255) / 256), dim3(256), 0, m.stream, F, mps, n, cosl, tr, n_in_view);
+    hipLaunchKernelGGL(k_frustum, dim3((n + 255) / 256), dim3(256), 0, m.ls(), F, mps, n, cosl, tr, n_in_view);
     return ORBMI_OK;
 }
 
@@ -1194,13 +1213,13 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
         CandArgs ca{};
         ca.mode = 0; ca.nq = n; ca.F = F; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.mps = mps; ca.tr = tr;
         ca.th = th; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
-        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.stream, ca);
+        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.ls(), ca);
     }
     GreedyArgs a{};
     a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = F;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches;
-    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.stream, a);
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.ls(), a);
     return ORBMI_OK;
 }
 
@@ -1220,21 +1239,21 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
         ca.mode = 1; ca.nq = n; ca.F = CF; ca.LF = LF; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.lfp = lfp;
         ca.th = th; ca.mono = mono; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
         ca.gate = gate; ca.gate_min = gate_min;
-        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.stream, ca);
+        hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.ls(), ca);
     }
     GreedyArgs a{};
     a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = CF;
     a.LF = LF;
     a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches; a.gate = gate; a.gate_min = gate_min;
-    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.stream, a);
+    hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.ls(), a);
     return ORBMI_OK;
 }
 
 int launch_track_update(Matcher& m, const DevFrame& F, int stage, const uint8_t* outlier, int* match_lf,
                         const orbmi_lastframe_point* lfp, int n_lf, int* match_mp, const orbmi_mappoint* mps,
                         int n_mp, uint8_t* occ_out, int* counts) {
-    hipLaunchKernelGGL(k_track_update, dim3(1), dim3(1024), 0, m.stream, F, stage, outlier, match_lf, lfp, n_lf,
+    hipLaunchKernelGGL(k_track_update, dim3(1), dim3(1024), 0, m.ls(), F, stage, outlier, match_lf, lfp, n_lf,
                        match_mp, mps, n_mp, occ_out, counts);
     return ORBMI_OK;
 }
@@ -1244,12 +1263,12 @@ int launch_bow(Matcher& m, const DevFrame& KF, const uint8_t* kf_ok, const DevFV
     int rc;
     if ((rc = ensure_buf(&m.d_bin_of, &m.cap_bin_of, (size_t)std::max(F.n, 1)))) return rc;
     if ((rc = ensure_buf(&m.d_hist, &m.cap_hist, (size_t)HISTO_LENGTH))) return rc;
-    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, HISTO_LENGTH * sizeof(int), m.stream));
-    ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)std::max(F.n, 1) * sizeof(int), m.stream));
+    ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, HISTO_LENGTH * sizeof(int), m.ls()));
+    ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)std::max(F.n, 1) * sizeof(int), m.ls()));
     if (kfv.nnodes > 0)
-        hipLaunchKernelGGL(k_bow_match, dim3((kfv.nnodes + 3) / 4), dim3(256), 0, m.stream, KF, kf_ok, kfv, F, fv,
+        hipLaunchKernelGGL(k_bow_match, dim3((kfv.nnodes + 3) / 4), dim3(256), 0, m.ls(), KF, kf_ok, kfv, F, fv,
                            nnratio, check_ori, match, m.d_bin_of, m.d_hist);
-    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.stream, F, check_ori, m.d_hist, m.d_bin_of, match,
+    hipLaunchKernelGGL(k_bow_finalize, dim3(1), dim3(1024), 0, m.ls(), F, check_ori, m.d_hist, m.d_bin_of, match,
                        nmatches);
     return ORBMI_OK;
 }
@@ -1514,17 +1533,17 @@ static int launch_tri_search(Matcher& m, const DevFrame& KF1, const uint8_t* has
         ORBMI_HIP(m.h2d(pairs_dev, pairs_host, sizeof(TriPair) * npairs));
     }
     // the histogram is read only by the orientation check
-    if (check_ori) ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.stream));
-    if (KF1.n > 0) ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)KF1.n * npairs * sizeof(int), m.stream));
+    if (check_ori) ORBMI_HIP(hipMemsetAsync(m.d_hist, 0, (size_t)HISTO_LENGTH * npairs * sizeof(int), m.ls()));
+    if (KF1.n > 0) ORBMI_HIP(hipMemsetAsync(match, 0xFF, (size_t)KF1.n * npairs * sizeof(int), m.ls()));
     if (fv1.nnodes > 0) {
         const int splits = tri_splits(KF1, fv1, npairs);
         const int waves = fv1.nnodes * splits;
-        hipLaunchKernelGGL(k_tri_match, dim3((waves + 3) / 4, npairs), dim3(256), 0, m.stream, KF1, has_mp1, fv1,
+        hipLaunchKernelGGL(k_tri_match, dim3((waves + 3) / 4, npairs), dim3(256), 0, m.ls(), KF1, has_mp1, fv1,
                            pairs_dev, only_stereo, check_ori, splits);
     }
     // without the orientation check and counts the finalize pass has nothing to do
     if (check_ori || counts)
-        hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.stream, KF1.n, pairs_dev, check_ori);
+        hipLaunchKernelGGL(k_tri_finalize, dim3(npairs), dim3(1024), 0, m.ls(), KF1.n, pairs_dev, check_ori);
     return ORBMI_OK;
 }
 
@@ -1620,7 +1639,7 @@ int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, c
     if ((rc = launch_tri_search(m, KF1, has1, fv1, npairs, pairs_host, pairs_dev, 0, 0, match, false))) return rc;
     auto par = [&](auto kern, int G) {
         const long long nt = (long long)KF1.n * G;
-        hipLaunchKernelGGL(kern, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
+        hipLaunchKernelGGL(kern, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, m.ls(), S1, S2_dev, npairs, match,
                            KF1.n, ok, x3d);
     };
     if (KF1.n <= 0) {
@@ -1635,7 +1654,7 @@ int launch_create_points(Matcher& m, const DevFrame& KF1, const uint8_t* has1, c
     } else if (npairs <= 64) {
         par(k_triangulate_par<64>, 64);
     } else {
-        hipLaunchKernelGGL(k_triangulate, dim3((KF1.n + 255) / 256), dim3(256), 0, m.stream, S1, S2_dev, npairs, match,
+        hipLaunchKernelGGL(k_triangulate, dim3((KF1.n + 255) / 256), dim3(256), 0, m.ls(), S1, S2_dev, npairs, match,
                            KF1.n, ok, x3d);
     }
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
@@ -1763,7 +1782,7 @@ int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const 
     int rc;
     if ((rc = grid_for(m, F))) return rc;
     if (n > 0)
-        hipLaunchKernelGGL(k_fuse, dim3((n * kFuseLanes + 255) / 256), dim3(256), 0, m.stream, F, m.d_cell_start, m.d_cell_list,
+        hipLaunchKernelGGL(k_fuse, dim3((n * kFuseLanes + 255) / 256), dim3(256), 0, m.ls(), F, m.d_cell_start, m.d_cell_list,
                            mps, in_kf, n, th, best_idx, best_dist, ncand);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
@@ -1789,9 +1808,9 @@ int launch_fuse_multi(Matcher& m, int nkf, FuseKF* kfs_host, FuseKF* kfs_dev, co
         K.ncand = ncand + k;
     }
     ORBMI_HIP(m.h2d(kfs_dev, kfs_host, sizeof(FuseKF) * nkf));
-    hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.stream, kfs_dev, m.d_mkp_cell, ncap);
+    hipLaunchKernelGGL(k_grid_build_multi, dim3(nkf), dim3(1024), 0, m.ls(), kfs_dev, m.d_mkp_cell, ncap);
     if (n > 0)
-        hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.stream, kfs_dev, mps, n,
+        hipLaunchKernelGGL(k_fuse_multi, dim3((n * kFuseLanes + 255) / 256, nkf), dim3(256), 0, m.ls(), kfs_dev, mps, n,
                            th);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
@@ -1808,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_patch_desc(orbmi_mappoint* __restrict__
 }
 
 int launch_patch_desc(Matcher& m, orbmi_mappoint* mps, const int* desc_from, const uint8_t* desc, int n) {
-    if (n > 0) hipLaunchKernelGGL(k_patch_desc, dim3((8 * n + 255) / 256), dim3(256), 0, m.stream, mps, desc_from, desc, n);
+    if (n > 0) hipLaunchKernelGGL(k_patch_desc, dim3((8 * n + 255) / 256), dim3(256), 0, m.ls(), mps, desc_from, desc, n);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }
 
@@ -1855,7 +1874,7 @@ __global__ __launch_bounds__(256) void k_distinctive(const uint4* __restrict__ d
 
 int launch_distinctive(Matcher& m, const uint8_t* desc, const int* off, int np, int* best, uint8_t* out) {
     if (np <= 0) return ORBMI_OK;
-    hipLaunchKernelGGL(k_distinctive, dim3((np + 3) / 4), dim3(256), 0, m.stream, (const uint4*)desc, off, np, best,
+    hipLaunchKernelGGL(k_distinctive, dim3((np + 3) / 4), dim3(256), 0, m.ls(), (const uint4*)desc, off, np, best,
                        (uint4*)out);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }

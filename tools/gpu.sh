@@ -76,6 +76,10 @@ for step in "$@"; do
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; cat $OUT/smoke.log;;
         bench)
             run bench 500 python bench.py; tail -1 $OUT/bench.log | tee $P/bench.json;;
+        frame_events)
+            # which chain ends the headline's timed region (tracking_done_ms / mapping_done_ms)
+            run frame_events 500 python bench.py --frame-events --steps 200 --warmup 10 --no-cpu-baseline
+            tail -1 $OUT/frame_events.log | tee $P/bench_frame_events.json;;
         bench_quick)
             run bench_quick 300 python bench.py --steps 60 --warmup 8 --no-cpu-baseline; tail -1 $OUT/bench_quick.log;;
         bench_*)
