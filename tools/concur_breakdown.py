@@ -19,6 +19,10 @@ import os
 import sys
 import time
 
+# as bench.py: 8 hardware queues (the process's streams then map onto queues of their own)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -69,6 +73,9 @@ def run(frames, s, voc, period, no_interrupt):
     gt = np.array([fr[2] for fr in frames])
     ate = ate_rmse(slam.trajectory_twc(), gt)
     st, sched, ba, c = slam.stats, slam.schedule(), slam.local_ba_log(), slam.counts()
+    lmc = slam.local_mapping_counts()
+    ph = slam.phase_ms()
+    per_kf = len(frames) / max(c["keyframes"] - 1, 1)
     slam.Shutdown()
     refused = 0
     for a, b in zip(st, st[1:]):
@@ -79,7 +86,9 @@ def run(frames, s, voc, period, no_interrupt):
             "refused": refused, "jobs": len(jb), "sin_skipped": sum(not j["sin"] for j in jb),
             "ba_skipped": sum(not j["ba"] for j in jb), "local_ba": int(len(ba)),
             "ba_interrupted": int((ba[:, 1] > 0).sum()) if len(ba) else 0,
-            "ba_aborted_before_start": int((ba[:, 1] == 0).sum()) if len(ba) else 0}
+            "ba_aborted_before_start": int((ba[:, 1] == 0).sum()) if len(ba) else 0,
+            "lm_ms_per_keyframe": round(ph["lm_total"] * per_kf, 3), "lm_lock_wait_ms_per_keyframe":
+            round(ph["lm_lock_wait"] * per_kf, 3), "native_counts": lmc}
 
 
 def main():
@@ -96,7 +105,7 @@ def main():
         keys = list(rs[0])
         print(f"{name}:", flush=True)
         for k in keys:
-            print(f"  {k:24s} " + "  ".join(f"{r[k]:>8}" for r in rs), flush=True)
+            print(f"  {k:28s} " + "  ".join(f"{str(r[k]):>8}" for r in rs), flush=True)
     print(json.dumps(out))
 
 

@@ -124,6 +124,9 @@ for step in "$@"; do
             run native_prof$a 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/native_prof$a -o np -- python3 tools/native_probe.py 200 $a
             find $OUT/native_prof$a -name "*kernel_stats.csv" -exec cp {} $P/native${a}_kernel_stats.csv \;
             cut -d, -f1-5 $P/native${a}_kernel_stats.csv | head -30;;
+        concur)
+            # tools/concur_breakdown.py: the concurrent native loop's outcomes per regime, 3 runs each
+            run concur 300 python tools/concur_breakdown.py 3; grep -v "^{" $OUT/concur.log | tee $P/concur_breakdown.txt; tail -1 $OUT/concur.log > $P/concur_breakdown.json;;
         lmprobe)
             run lmprobe 300 python tools/lm_chain_probe.py 20; tail -14 $OUT/lmprobe.log;;
         solvetrace|solvetrace=*)
