@@ -1395,6 +1395,9 @@ struct orbmi_slam {
         }
         next(PH_LM_CULL);
         map_point_culling(k);
+        // SearchInNeighbors' last ComputeDistinctiveDescriptors (all the keyframe's points) rides in
+        // LocalBA's device window when LocalBA runs (one map-lock release fewer per keyframe)
+        std::vector<int> owed2;
         if (s.local_mapping) {
             next(PH_LM_CREATE);
             const size_t nmp0 = mps.size();
@@ -1407,7 +1410,7 @@ struct orbmi_slam {
                 SLAM_CHECK(distinctive(owed));
             } else {
                 fuse_ops = 0;
-                SLAM_CHECK(search_in_neighbors(k, owed));
+                SLAM_CHECK(search_in_neighbors(k, owed, owed2));
                 int filled = 0;
                 for (int m : kfs[k].mps) filled += m >= 0;
                 log_state(k, ORBMI_KF_STATE_FUSE, fuse_ops, (uint32_t)filled, slot_hash(k));
@@ -1415,10 +1418,13 @@ struct orbmi_slam {
         }
         set_abort_ba(0);
         lm_jobs++;
-        if (new_keyframes_queued()) ba_skipped++;
-        else {
+        if (new_keyframes_queued()) {
+            ba_skipped++;
+            SLAM_CHECK(distinctive(owed2));
+        } else {
             next(PH_LM_BA);
-            if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k));
+            if (s.local_ba && keyframes_in_map() > 2) SLAM_CHECK(local_bundle_adjustment(k, owed2));
+            else SLAM_CHECK(distinctive(owed2));
             next(PH_LM_KFCULL);
             if (s.local_mapping) keyframe_culling(k);
         }
@@ -1920,7 +1926,10 @@ struct orbmi_slam {
         return ORBMI_OK;
     }
 
-    int search_in_neighbors(int k, const std::vector<int>& owed) {  // src/LocalMapping.cc:589-674, stereo: nn = 10
+    // owed2 <- the keyframe's points, whose ComputeDistinctiveDescriptors (:656-667) the caller does
+    // -- in LocalBA's device window when that runs next.  UpdateNormalAndDepth and UpdateConnections
+    // do not read descriptors and are done here.
+    int search_in_neighbors(int k, const std::vector<int>& owed, std::vector<int>& owed2) {  // src/LocalMapping.cc:589-674, stereo: nn = 10
         std::vector<int> targets;
         const std::vector<int> neigh(kfs[k].covisible.begin(),
                                      kfs[k].covisible.begin() + std::min<size_t>(10, kfs[k].covisible.size()));
@@ -1951,9 +1960,9 @@ struct orbmi_slam {
         std::set<int> seen_pt;
         for (int m : kfs[k].mps)
             if (m >= 0 && !mps[m].bad && seen_pt.insert(m).second) upd.push_back(m);
-        SLAM_CHECK(distinctive(upd));
         normals(upd);
         connections(k);
+        owed2 = std::move(upd);
         return ORBMI_OK;
     }
 
@@ -2040,7 +2049,9 @@ struct orbmi_slam {
 
     // Optimizer::LocalBundleAdjustment: the graph as src/Optimizer.cc:486-683 assembles it
     // (system/optimizer.gather_local_ba), the optimisation on the GPU, the write-back (:776-805)
-    int local_bundle_adjustment(int k) {
+    // `owed`: points whose ComputeDistinctiveDescriptors runs in the same device window as the
+    // optimisation (the descriptors written back with the poses)
+    int local_bundle_adjustment(int k, const std::vector<int>& owed) {
         auto* gt = new PhaseTimer(&phase_ms[PH_LM_BA_GATHER]);
         std::vector<int> lkf{k};
         SeenSet& local_set = ba_local_mark;
@@ -2099,7 +2110,21 @@ struct orbmi_slam {
                 e_ref.push_back({lmp[j], o.first});
             }
         delete gt;
-        if (E.empty()) return ORBMI_OK;
+        if (E.empty()) return distinctive(owed);
+        std::vector<uint8_t> orows;
+        std::vector<int32_t> ooff;
+        {
+            PhaseTimer pt(&phase_ms[PH_LM_OBSROWS]);
+            obs_rows(owed, orows, ooff);
+        }
+        const int nod = (int)owed.size();
+        std::vector<int32_t> obest(std::max(nod, 1));
+        std::vector<uint8_t> oout((size_t)std::max(nod, 1) * 32);
+        auto owed_call = [&]() -> int {
+            if (orows.empty()) return ORBMI_OK;
+            PhaseTimer pt(&phase_ms[PH_LM_DISTINCTIVE_CALL]);
+            return orbmi_compute_distinctive_descriptors(lmm(), orows.data(), ooff.data(), nod, obest.data(), oout.data());
+        };
         orbmi_ba_problem prob{(int)K.size(), (int)P.size(), (int)E.size(), K.data(), P.data(), E.data()};
         std::vector<float> tcw(K.size() * 16), pos(P.size() * 3 + 3);
         std::vector<uint8_t> erase(E.size());
@@ -2112,7 +2137,8 @@ struct orbmi_slam {
         if (held_lock && on_mapping_thread) {  // tracking runs while the GPU solves
             hold_end();
             held_lock->unlock();
-            {
+            rc = owed_call();
+            if (!rc) {
                 PhaseTimer ct(&phase_ms[PH_LM_BA_CALL]);
                 rc = orbmi_local_bundle_adjustment(ba, &prob, &res, &abort_ba);
             }
@@ -2121,10 +2147,13 @@ struct orbmi_slam {
             held_lock->lock();
             log_section(ORBMI_SCHED_L_BA, k);
         } else {
+            rc = owed_call();
             PhaseTimer ct(&phase_ms[PH_LM_BA_CALL]);
-            rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
+            if (!rc) rc = orbmi_local_bundle_adjustment(ba, &prob, &res, nullptr);
         }
         SLAM_CHECK(rc);
+        for (int j = 0; j < nod; j++)  // the owed descriptors (under the map lock again)
+            if (ooff[j + 1] > ooff[j]) std::memcpy(mps[owed[j]].desc, &oout[32 * j], 32);
         PhaseTimer wb(&phase_ms[PH_LM_BA_WRITEBACK]);
         ba_calls++;
         if (res.aborted) ba_aborted++;

@@ -867,6 +867,7 @@ class StereoSLAM:
             h = _fnv(_fnv(_fnv(FNV0, fv.node_id), fv.off), fv.feat)
             self._log_state(kf, KF_STATE_PROCESS, getattr(fv, "n_words", -1), h, _slot_hash(kf))
         self._map_point_culling(kf)
+        owed2 = []   # SearchInNeighbors' last ComputeDistinctiveDescriptors, done in LocalBA's window
         if self.local_mapping_full:
             n0 = len(self.mappoints)
             owed = (yield from self._create_new_map_points_gen(kf)) or []
@@ -875,15 +876,19 @@ class StereoSLAM:
                 yield from self._distinctive_gen(owed)
             else:
                 self._fuse_ops = 0
-                yield from self._search_in_neighbors_gen(kf, owed)
+                owed2 = yield from self._search_in_neighbors_gen(kf, owed)
                 filled = sum(1 for mp in kf.map_points if mp is not None)
                 self._log_state(kf, KF_STATE_FUSE, self._fuse_ops, filled, _slot_hash(kf))
         self._abort = False
         if not self._queued():
             if self.use_local_ba and self._keyframes_in_map() > 2:
-                yield from self._local_bundle_adjustment_gen(kf)
+                yield from self._local_bundle_adjustment_gen(kf, owed2)
+            else:
+                yield from self._distinctive_gen(owed2)
             if self.local_mapping_full:
                 self._keyframe_culling(kf)
+        else:
+            yield from self._distinctive_gen(owed2)
 
     def _log_state(self, kf: KeyFrame, stage: int, a: int, b: int, c: int):
         """The per-keyframe state record (orbmi_slam_kf_state); in a replay, checked against the
@@ -1179,9 +1184,11 @@ class StereoSLAM:
             if id(mp) not in seen:
                 seen.add(id(mp))
                 upd.append(mp)
-        yield from self._distinctive_gen(upd)
+        # their ComputeDistinctiveDescriptors is returned to the caller (LocalBA's device window, as
+        # the native loop); UpdateNormalAndDepth and UpdateConnections do not read descriptors
         update_normals_and_depths(upd)
         kf.update_connections()
+        return upd
 
     def _keyframe_culling(self, kf: KeyFrame):
         """LocalMapping::KeyFrameCulling (src/LocalMapping.cc:775-841), stereo: close points only;
@@ -1216,18 +1223,27 @@ class StereoSLAM:
     def backend_has_bow(self) -> bool:
         return getattr(self.backend, "vocab", None) is not None
 
-    def _local_bundle_adjustment_gen(self, kf: KeyFrame):
+    def _local_bundle_adjustment_gen(self, kf: KeyFrame, owed=()):
         """Optimizer::LocalBundleAdjustment (src/Optimizer.cc:483-808): graph assembly on the host
         (optimizer.gather_local_ba), optimisation on the backend, write-back under the map lock.
         In a replayed schedule pbStopFlag (mbAbortBA) is the recorded run's: the backend stops at
         the check where that run first saw it raised (orbmi_ba_set_stop_at_check)."""
         from .optimizer import gather_local_ba
         problem, kfs, mps = gather_local_ba(kf)
+        owed = list(owed)
         if len(problem.edges) == 0:
+            yield from self._distinctive_gen(owed)
             return
+        # `owed`: ComputeDistinctiveDescriptors in the same device window (native: one lock release)
+        rows, off = self._obs_rows(owed)
+        d = self.backend.distinctive(np.asarray(rows, np.uint8), np.asarray(off, np.int32)) if rows else None
         stop_at = -1 if self._ba_stop_at is None else self._ba_stop_at(kf)
         res = self.backend.local_ba(problem, stop_at_check=stop_at)
         yield L_BA, kf.id
+        if rows:
+            for j, mp in enumerate(owed):
+                if off[j + 1] > off[j]:
+                    mp.desc = np.asarray(d[j], np.uint8).copy()
         erase = np.asarray(res["erase"], bool)
         self.ba_log.append({"keyframe": kf.id, "keyframes": len(kfs), "points": len(mps),
                             "edges": len(problem.edges), "erased": int(erase.sum()),
