@@ -70,7 +70,7 @@ def parse():
                     help="per-keyframe LocalMapping work: the whole LocalMapping::Run body, or ComputeBoW + LocalBA")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic_track.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06", "traffic_track.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--traffic-lba", default=os.path.join(ROOT, "profiles", "r05", "traffic_lba.json"),
                     help="per-kernel PMC HBM bytes per launch of --mode lba (tools/pmc_traffic.py)")

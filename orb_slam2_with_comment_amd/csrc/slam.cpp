@@ -1253,7 +1253,7 @@ struct orbmi_slam {
             std::lock_guard<std::mutex> g(q_mtx);
             if (lm_rc) return lm_rc;
             lm_queue.push_back(k);
-            set_abort_ba(1);  // a new keyframe interrupts the running BA (src/LocalMapping.cc:148)
+            set_abort_ba(1);  // a new keyframe interrupts the running BA (src/LocalMapping.cc:134)
         }
         q_cv.notify_one();
         return ORBMI_OK;
