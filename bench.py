@@ -72,9 +72,9 @@ def parse():
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06", "traffic_track.json"),
                     help="per-kernel PMC HBM bytes per launch (tools/pmc_traffic.py)")
-    ap.add_argument("--traffic-lba", default=os.path.join(ROOT, "profiles", "r05", "traffic_lba.json"),
+    ap.add_argument("--traffic-lba", default=os.path.join(ROOT, "profiles", "r06", "traffic_lba.json"),
                     help="per-kernel PMC HBM bytes per launch of --mode lba (tools/pmc_traffic.py)")
-    ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r05", "traffic_batch.json"),
+    ap.add_argument("--traffic-batch", default=os.path.join(ROOT, "profiles", "r06", "traffic_batch.json"),
                     help="the same for --mode batch (tools/gpu.sh pmc_batch)")
     ap.add_argument("--frame-events", action="store_true",
                     help="track mode: HIP events around every timed frame's extraction and tracking (their "
