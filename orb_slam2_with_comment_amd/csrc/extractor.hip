@@ -13,6 +13,7 @@
 
 #include "../../include/orbmi_pattern.h"
 #include "extractor.h"
+#include "fast_score.h"
 #include "trig_f64.h"
 
 namespace orbmi {
@@ -600,12 +601,23 @@ __device__ inline bool fast_segment_lane(const uint8_t* cm, int th) {
     return fast_arc9_word(mb) || fast_arc9_word(md);
 }
 
+// fast_arc_strength (fast_score.h) of every lane's pixel, cm as for fast_segment_lane
+template <int TS>
+__device__ inline int fast_strength_lane(const uint8_t* cm, int th) {
+    constexpr int o[16] = {6 * TS + 3, 6 * TS + 4, 5 * TS + 5, 4 * TS + 6, 3 * TS + 6, 2 * TS + 6, TS + 5, 4,
+                           3, 2, TS + 1, 2 * TS, 3 * TS, 4 * TS, 5 * TS + 1, 6 * TS + 2};
+    int p[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) p[k] = cm[o[k]];
+    return fast_arc_strength(cm[3 * TS + 3], p, th);
+}
+
 constexpr int fast2_tile_bytes(int TS, int maxH) { return (TS * maxH + 15) & ~15; }
 __host__ __device__ inline int fast2_wave_bytes(int TS, int maxW, int maxH) {
     return 2 * fast2_tile_bytes(TS, maxH) + ((2 * (maxW - 6) * (maxH - 6) + 15) & ~15);
 }
 
-template <int TS>
+template <int TS, bool kStrength>
 __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __restrict__ pyr, long long pimg,
                                                            const CellGeom* __restrict__ cells, int c0, int ncells,
                                                            uint2* __restrict__ cand, int keys_cap,
@@ -689,14 +701,37 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         wave_sync_lds_ex();
         return kept;
     };
-    const int nc = segment_pass(L, n, L, tl);
-    // B': the corners at ini_th among them, listed after them (see k_fast)
-    const bool split = ti > tl && nc > 64 && 2 * nc <= lcap;
+    int nc = 0;
+    bool split = false;
     unsigned short* LH = L;
-    int nh = nc;
-    if (split) {
-        LH = L + nc;
-        nh = segment_pass(L, nc, LH, ti);
+    int nh = 0;
+    if constexpr (kStrength) {
+        // B + C at once: S = fast_arc_strength at tl; a corner at t exactly when S > t, its score
+        // S - 1 (fast_score.h), so every corner is scored here and NMS reads the map at either
+        // threshold (scores below it count 0 there)
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const unsigned short e = L[min(i, n - 1)];
+            const int S = fast_strength_lane<TS>(tb + e - (3 * TS + 3), tl);
+            const bool pass = S > tl && i < n;
+            const unsigned long long m = __ballot(pass);
+            if (pass) {
+                L[nc + lanes_below(m)] = e;
+                sc[e] = (uint8_t)(S - 1);
+            }
+            nc += __popcll(m);
+        }
+        wave_sync_lds_ex();
+        nh = nc;
+    } else {
+        nc = segment_pass(L, n, L, tl);
+        // B': the corners at ini_th among them, listed after them (see k_fast)
+        split = ti > tl && nc > 64 && 2 * nc <= lcap;
+        nh = nc;
+        if (split) {
+            LH = L + nc;
+            nh = segment_pass(L, nc, LH, ti);
+        }
     }
     auto score = [&](const unsigned short* Ls, int ns) {
         for (int i = lane; i < ns; i += 64) {
@@ -732,7 +767,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         }
         return kept;
     };
-    score(LH, nh);
+    if (!kStrength) score(LH, nh);
     int total = nms(LH, nh, ti);
     const unsigned short* LO = LH;
     if (total == 0 && tm != ti) {
@@ -1766,6 +1801,7 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         describe_wave = e && !strcmp(e, "wave");
         e = getenv("ORBMI_FAST");
         fast_v1 = e && !strcmp(e, "v1");
+        fast_split = e && !strcmp(e, "split");
         e = getenv("ORBMI_FAST_EARLY");
         fast_early = e && !strcmp(e, "1");
         e = getenv("ORBMI_BLUR");
@@ -2112,7 +2148,8 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         else {
             const bool narrow = fast_maxw + 3 <= 48;
             const size_t lds = kFastCells * fast2_wave_bytes(narrow ? 48 : 80, fast_maxw, fast_maxh);
-            auto* kf = narrow ? k_fast2<48> : k_fast2<80>;
+            auto* kf = fast_split ? (narrow ? k_fast2<48, false> : k_fast2<80, false>)
+                                  : (narrow ? k_fast2<48, true> : k_fast2<80, true>);
             hipLaunchKernelGGL(kf, dim3(xcd_image_grid(grid.x, batch)), block, lds, s, d_pyr, pimg, d_cells, c0, c1, d_cand,
                                keys_cap, d_level_count, nlevels, ini_th, min_th, fast_maxw, fast_maxh, batch);
         }

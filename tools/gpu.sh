@@ -294,12 +294,13 @@ for step in "$@"; do
                 echo "4/wave: $(v descab_4_$i) | 1/wave: $(v descab_w_$i)" | tee -a $OUT/descab.txt
             done; cp $OUT/descab.txt $P/;;
         fastab)
-            # config 5 batch: bit-sliced FAST (default) vs the per-lane kernel (ORBMI_FAST=v1)
+            # config 5 batch: k_fast2 with the one-pass arc strength (default) vs its separate
+            # segment-test and score stages (ORBMI_FAST=split), 3 alternations
             v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["stage_ms_per_launch"]["fast"])'; }
-            for i in 1 2; do
-                run fastab_2_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
-                ORBMI_FAST=v1 run fastab_1_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
-                echo "sliced: $(v fastab_2_$i) | per-lane: $(v fastab_1_$i)" | tee -a $OUT/fastab.txt
+            for i in 1 2 3; do
+                run fastab_s_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                ORBMI_FAST=split run fastab_p_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
+                echo "one pass: $(v fastab_s_$i) | split: $(v fastab_p_$i)" | tee -a $OUT/fastab.txt
             done; cp $OUT/fastab.txt $P/;;
         fastseg)
             # config 5 batch: k_fast2's arc-test split (ORBMI_FAST_SEG=0 scalar, 1 per lane, 2 mixed)
