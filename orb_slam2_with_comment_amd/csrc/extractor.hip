@@ -612,6 +612,15 @@ __device__ inline int fast_strength_lane(const uint8_t* cm, int th) {
     return fast_arc_strength(cm[3 * TS + 3], p, th);
 }
 
+// e - back as an offset the compiler cannot fold into the reads that follow: they then take the
+// window's offsets as non-negative ds_read immediates (folded, the negative ones cost a VALU add
+// each)
+__device__ inline int lds_window(int e, int back) {
+    int b = e - back;
+    asm volatile("" : "+v"(b));
+    return b;
+}
+
 constexpr int fast2_tile_bytes(int TS, int maxH) { return (TS * maxH + 15) & ~15; }
 __host__ __device__ inline int fast2_wave_bytes(int TS, int maxW, int maxH) {
     return 2 * fast2_tile_bytes(TS, maxH) + ((2 * (maxW - 6) * (maxH - 6) + 15) & ~15);
@@ -693,7 +702,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         for (int i0 = 0; i0 < ns; i0 += 64) {
             const int i = i0 + lane;
             const unsigned short e = Ls[min(i, ns - 1)];  // the last lanes repeat an entry, masked off
-            const bool pass = fast_segment_lane<TS>(tb + e - (3 * TS + 3), th) && i < ns;
+            const bool pass = fast_segment_lane<TS>(tb + lds_window(e, 3 * TS + 3), th) && i < ns;
             const unsigned long long m = __ballot(pass);
             if (pass) Ld[kept + lanes_below(m)] = e;
             kept += __popcll(m);
@@ -712,7 +721,7 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         for (int i0 = 0; i0 < n; i0 += 64) {
             const int i = i0 + lane;
             const unsigned short e = L[min(i, n - 1)];
-            const int S = fast_strength_lane<TS>(tb + e - (3 * TS + 3), tl);
+            const int S = fast_strength_lane<TS>(tb + lds_window(e, 3 * TS + 3), tl);
             const bool pass = S > tl && i < n;
             const unsigned long long m = __ballot(pass);
             if (pass) {
@@ -750,16 +759,12 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
             unsigned short e = 0;
             if (i < ns) {
                 e = Ls[i];
-                const uint8_t* q = sc + e;
-                const int s = q[0];
-                if (s >= t && s != 0) {
-                    auto nb = [&](int off) {
-                        const int u = q[off];
-                        return u >= t ? u : 0;
-                    };
-                    keep = s > nb(-TS - 1) && s > nb(-TS) && s > nb(-TS + 1) && s > nb(-1) && s > nb(1) &&
-                           s > nb(TS - 1) && s > nb(TS) && s > nb(TS + 1);
-                }
+                const uint8_t* q = sc + lds_window(e, TS + 1);  // the 3x3 window's top-left
+                const int s = q[TS + 1];
+                const int u[8] = {q[0], q[1], q[2], q[TS], q[TS + 2], q[2 * TS], q[2 * TS + 1], q[2 * TS + 2]};
+                keep = s >= t && s != 0;  // a neighbour below t counts 0
+#pragma unroll
+                for (int k = 0; k < 8; k++) keep &= u[k] < t || s > u[k];
             }
             const unsigned long long m = __ballot(keep);
             if (keep) Ls[kept + lanes_below(m)] = e;
