@@ -673,83 +673,31 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
     const uint8_t* tb = reinterpret_cast<const uint8_t*>(t4) + o;  // tb[y * TS + x]
     const int dw = w - 6, dh = h - 6, npix = dw > 0 && dh > 0 ? dw * dh : 0;
     const int ti = min(max(ini_th, 0), 255), tm = min(max(min_th, 0), 255), tl = min(ti, tm);
-    // A: compass pre-test over the ROI's scored pixels, row-major
-    int n = 0;
-    if (npix > 0) {
-        int y = lane / dw, x = lane - y * dw;
-        const int q = 64 / dw, r = 64 - q * dw;
-        for (int p0 = 0; p0 < npix; p0 += 64) {
-            // lanes past the last pixel read the ROI's last row (masked off below)
-            const int e0 = __umul24(min(y, dh - 1), TS) + x + 3;  // the pixel at (X, Y - 3)
-            const uint8_t* cp = tb + e0;
-            const int pc = cp[0], pd = cp[3 * TS - 3], v = cp[3 * TS], pb = cp[3 * TS + 3], pa = cp[6 * TS];
-            const int hi = v + tl, lo = v - tl;
-            const bool ba = pa > hi, bb = pb > hi, bc = pc > hi, bd = pd > hi;
-            const bool da = pa < lo, db = pb < lo, dc = pc < lo, dd = pd < lo;
-            const bool pass = (((ba | bc) & (bb | bd)) | ((da | dc) & (db | dd))) && p0 + lane < npix;
-            const unsigned long long m = __ballot(pass);
-            if (pass) L[n + lanes_below(m)] = (unsigned short)(e0 + 3 * TS);
-            n += __popcll(m);
-            x += r;
-            y += q;
-            if (x >= dw) { x -= dw; y++; }
-        }
-    }
-    wave_sync_lds_ex();
-    // B: full segment test at tl, compacted in place (a lane writes at or below the entry it read)
-    auto segment_pass = [&](const unsigned short* Ls, int ns, unsigned short* Ld, int th) {
-        int kept = 0;
-        for (int i0 = 0; i0 < ns; i0 += 64) {
-            const int i = i0 + lane;
-            const unsigned short e = Ls[min(i, ns - 1)];  // the last lanes repeat an entry, masked off
-            const bool pass = fast_segment_lane<TS>(tb + lds_window(e, 3 * TS + 3), th) && i < ns;
-            const unsigned long long m = __ballot(pass);
-            if (pass) Ld[kept + lanes_below(m)] = e;
-            kept += __popcll(m);
-        }
-        wave_sync_lds_ex();
-        return kept;
-    };
-    int nc = 0;
-    bool split = false;
-    unsigned short* LH = L;
-    int nh = 0;
-    if constexpr (kStrength) {
-        // B + C at once: S = fast_arc_strength at tl; a corner at t exactly when S > t, its score
-        // S - 1 (fast_score.h), so every corner is scored here and NMS reads the map at either
-        // threshold (scores below it count 0 there)
-        for (int i0 = 0; i0 < n; i0 += 64) {
-            const int i = i0 + lane;
-            const unsigned short e = L[min(i, n - 1)];
-            const int S = fast_strength_lane<TS>(tb + lds_window(e, 3 * TS + 3), tl);
-            const bool pass = S > tl && i < n;
-            const unsigned long long m = __ballot(pass);
-            if (pass) {
-                L[nc + lanes_below(m)] = e;
-                sc[e] = (uint8_t)(S - 1);
+    // A: compass pre-test at t over the ROI's scored pixels, row-major, into L
+    auto compass = [&](int t) {
+        int n = 0;
+        if (npix > 0) {
+            int y = lane / dw, x = lane - y * dw;
+            const int q = 64 / dw, r = 64 - q * dw;
+            for (int p0 = 0; p0 < npix; p0 += 64) {
+                // lanes past the last pixel read the ROI's last row (masked off below)
+                const int e0 = __umul24(min(y, dh - 1), TS) + x + 3;  // the pixel at (X, Y - 3)
+                const uint8_t* cp = tb + e0;
+                const int pc = cp[0], pd = cp[3 * TS - 3], v = cp[3 * TS], pb = cp[3 * TS + 3], pa = cp[6 * TS];
+                const int hi = v + t, lo = v - t;
+                const bool ba = pa > hi, bb = pb > hi, bc = pc > hi, bd = pd > hi;
+                const bool da = pa < lo, db = pb < lo, dc = pc < lo, dd = pd < lo;
+                const bool pass = (((ba | bc) & (bb | bd)) | ((da | dc) & (db | dd))) && p0 + lane < npix;
+                const unsigned long long m = __ballot(pass);
+                if (pass) L[n + lanes_below(m)] = (unsigned short)(e0 + 3 * TS);
+                n += __popcll(m);
+                x += r;
+                y += q;
+                if (x >= dw) { x -= dw; y++; }
             }
-            nc += __popcll(m);
         }
         wave_sync_lds_ex();
-        nh = nc;
-    } else {
-        nc = segment_pass(L, n, L, tl);
-        // B': the corners at ini_th among them, listed after them (see k_fast)
-        split = ti > tl && nc > 64 && 2 * nc <= lcap;
-        nh = nc;
-        if (split) {
-            LH = L + nc;
-            nh = segment_pass(L, nc, LH, ti);
-        }
-    }
-    auto score = [&](const unsigned short* Ls, int ns) {
-        for (int i = lane; i < ns; i += 64) {
-            const unsigned short e = Ls[i];
-            int p[16];
-            fast_circle(tb + e, TS, 0, 0, p);
-            sc[e] = (uint8_t)fast_corner_score(tb[e], p, tl);
-        }
-        wave_sync_lds_ex();
+        return n;
     };
     auto nms = [&](unsigned short* Ls, int ns, int t) {
         int kept = 0;
@@ -772,13 +720,84 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         }
         return kept;
     };
-    if (!kStrength) score(LH, nh);
-    int total = nms(LH, nh, ti);
-    const unsigned short* LO = LH;
-    if (total == 0 && tm != ti) {
-        if (split) score(L, nc);
-        total = nms(L, nc, tm);
-        LO = L;
+    int total = 0;
+    const unsigned short* LO = L;
+    if constexpr (kStrength) {
+        // B + C at once: S = fast_arc_strength at t; a corner at t' >= t exactly when S > t', its
+        // score S - 1 whatever t (fast_score.h), so the pass both finds and scores the corners and
+        // NMS reads the map at either threshold (scores below it count 0 there)
+        auto strength = [&](int n, int t) {
+            int nc = 0;
+            for (int i0 = 0; i0 < n; i0 += 64) {
+                const int i = i0 + lane;
+                const unsigned short e = L[min(i, n - 1)];
+                const int S = fast_strength_lane<TS>(tb + lds_window(e, 3 * TS + 3), t);
+                const bool pass = S > t && i < n;
+                const unsigned long long m = __ballot(pass);
+                if (pass) {
+                    L[nc + lanes_below(m)] = e;
+                    sc[e] = (uint8_t)(S - 1);
+                }
+                nc += __popcll(m);
+            }
+            wave_sync_lds_ex();
+            return nc;
+        };
+        // FAST at ini_th first, from its own compass survivors (a corner at ini_th, and so every
+        // neighbour NMS at ini_th counts, passes the compass at ini_th): about half the candidates
+        // of the compass at min_th.  Only a cell without a survivor runs the min_th pass (the
+        // scores it rewrites are the same values).  With min_th >= ini_th one pass at ini_th
+        // holds the corners of both.
+        const bool two = tm < ti;
+        int nc = strength(compass(two ? ti : tl), two ? ti : tl);
+        total = nms(L, nc, ti);
+        if (total == 0 && tm != ti) {
+            if (two) nc = strength(compass(tm), tm);
+            total = nms(L, nc, tm);
+        }
+    } else {
+        const int n = compass(tl);
+        // B: full segment test at tl, compacted in place (a lane writes at or below the entry it read)
+        auto segment_pass = [&](const unsigned short* Ls, int ns, unsigned short* Ld, int th) {
+            int kept = 0;
+            for (int i0 = 0; i0 < ns; i0 += 64) {
+                const int i = i0 + lane;
+                const unsigned short e = Ls[min(i, ns - 1)];  // the last lanes repeat an entry, masked off
+                const bool pass = fast_segment_lane<TS>(tb + lds_window(e, 3 * TS + 3), th) && i < ns;
+                const unsigned long long m = __ballot(pass);
+                if (pass) Ld[kept + lanes_below(m)] = e;
+                kept += __popcll(m);
+            }
+            wave_sync_lds_ex();
+            return kept;
+        };
+        const int nc = segment_pass(L, n, L, tl);
+        // B': the corners at ini_th among them, listed after them (see k_fast)
+        const bool split = ti > tl && nc > 64 && 2 * nc <= lcap;
+        unsigned short* LH = L;
+        int nh = nc;
+        if (split) {
+            LH = L + nc;
+            nh = segment_pass(L, nc, LH, ti);
+        }
+        // C: cornerScore of the corners
+        auto score = [&](const unsigned short* Ls, int ns) {
+            for (int i = lane; i < ns; i += 64) {
+                const unsigned short e = Ls[i];
+                int p[16];
+                fast_circle(tb + e, TS, 0, 0, p);
+                sc[e] = (uint8_t)fast_corner_score(tb[e], p, tl);
+            }
+            wave_sync_lds_ex();
+        };
+        score(LH, nh);
+        total = nms(LH, nh, ti);
+        LO = LH;
+        if (total == 0 && tm != ti) {
+            if (split) score(L, nc);
+            total = nms(L, nc, tm);
+            LO = L;
+        }
     }
     if (total == 0) return;
     wave_sync_lds_ex();
