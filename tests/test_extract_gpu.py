@@ -79,6 +79,30 @@ def test_extract_parity(orb, oracle, images, name):
     _assert_same(oracle, p, ex, img, k, d)
 
 
+def _low_contrast():
+    """A 480x640 texture of +-12 grey levels (FAST corners at 7, rarely at 20: most cells fall back
+    to min_th) with a few high-contrast blocks (cells that keep ini_th's corners)."""
+    rng = np.random.default_rng(11)
+    img = (116 + rng.integers(0, 25, (480, 640))).astype(np.uint8)
+    for y, x in [(60, 80), (200, 330), (350, 500), (400, 90)]:
+        img[y:y + 24, x:x + 40] = rng.integers(0, 256, (24, 40))
+    return img
+
+
+# FAST at ini_th first and at min_th only for a cell without a survivor (k_fast2): both orders of
+# the thresholds, equal ones, and an image where most cells take the fallback
+@pytest.mark.parametrize("ini,mn", [(20, 7), (7, 20), (12, 12), (45, 5)])
+@pytest.mark.parametrize("name", ["low_contrast", "kitti_L0"])
+def test_extract_parity_thresholds(orb, oracle, images, name, ini, mn):
+    img = _low_contrast() if name == "low_contrast" else images[name]
+    p = oracle.params(2000, 1.2, 8, ini, mn)
+    ex = _extractor(orb, p)
+    k, d = ex(img)
+    if d is None:
+        d = np.zeros((0, 32), np.uint8)
+    _assert_same(oracle, p, ex, img, k, d)
+
+
 def test_extract_parity_5000_euroc(orb, oracle, images):
     p = oracle.params(5000)
     ex = _extractor(orb, p)
