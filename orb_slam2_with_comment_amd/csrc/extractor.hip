@@ -561,8 +561,13 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast(const uint8_t* __restr
 // eight compares as lane masks.  Measured alternatives (profiles/r04/fast_seg_ab.txt): the arc
 // test bit-sliced across the wave on the scalar unit (79 SALU ops per polarity for 64 pixels)
 // cut the VALU count by 40 % but made the kernel slower, 0.327 vs 0.307 ms per 64 frames: the
-// scalar unit issues at the same per-SIMD rate as the vector unit.  Stages, order and outputs
-// are k_fast's.
+// scalar unit issues at the same per-SIMD rate as the vector unit.  Outputs and their order are
+// k_fast's.  Round 6 (kStrength, the default; ORBMI_FAST=split keeps the stages above for A/B):
+// stages B and C are one pass of fast_arc_strength (fast_score.h: packed 16-bit min/max, S > t is
+// the segment test at t and S - 1 the score), run first at ini_th on the compass survivors at
+// ini_th and at min_th only for a cell with no survivor; the window bases are kept out of the
+// reads' address folding (lds_window), and NMS reads its eight neighbours unconditionally.
+// Config 5: FAST 0.289 -> 0.164 ms per 64 frames (profiles/r06/fastab.txt).
 // m * 2 + (a > b): the compare's lane mask is the add's carry-in (two VALU ops per bit; the
 // compiler's own form is compare, select, shift-or)
 __device__ inline unsigned shift_in_gt(unsigned m, int a, int b) {
