@@ -571,7 +571,8 @@ def run_track(a, rank, world, local, dist):
                             "PoseOptimization] + TrackLocalMap [SearchLocalPoints(th=1, "
                             f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
                             + (f"+ LocalMapping::Run every {KF_EVERY}th frame on the concurrent LocalMapping thread "
-                               "[ProcessNewKeyFrame: KeyFrame::ComputeBoW + ComputeDistinctiveDescriptors; "
+                               "[ProcessNewKeyFrame: KeyFrame::ComputeBoW (a queued keyframe's issued beside the "
+                               "previous LocalBA, on the vocabulary's stream) + ComputeDistinctiveDescriptors; "
                                "CreateNewMapPoints: SearchForTriangulation x9 neighbours + triangulation geometry, all on the device; "
                                "SearchInNeighbors: Fuse x9 targets + Fuse(KF, targets' points) + "
                                "ComputeDistinctiveDescriptors; LocalBundleAdjustment(config 3)]" if full_chain else
@@ -596,7 +597,8 @@ def run_track(a, rank, world, local, dist):
             "compute_bow": {"us_per_keyframe_synced": round(bow_us, 1), "words": bow_words,
                             "vocabulary": "synthetic k=10 L=6 (1,111,111 nodes), L1 / TF-IDF, levelsup 4"},
             "local_mapping": {"ms_per_keyframe_idle_gpu": round(lba_ms, 3), "chain": a.lm_chain,
-                              "keyframes_in_timed_region": n_lba, "last_keyframe": chain_info},
+                              "keyframes_in_timed_region": n_lba, "last_keyframe": chain_info,
+                              "compute_bow_issued_ahead": getattr(mapper, "bow_ahead", 0)},
             "local_ba": {"calls_in_timed_region": n_lba,
                          "iterations": list(lba_info["iterations"]) if lba_info else None,
                          "edges": int(len(problem.edges)), "points": int(len(problem.pts)),

@@ -458,26 +458,44 @@ class LocalMapper:
         self._ms = torch.cuda.ExternalStream(ms.value, device=dev)  # the mapper's search stream
         # device buffers the chain writes are allocated on the stream that uses them, so the
         # caching allocator hands a freed block back only in that stream's order
+        # ComputeBoW ahead (ORBMI_LM_PREBOW, default on): the next queued keyframe's transform runs
+        # on the vocabulary's own stream while this keyframe's LocalBA runs on the mapper's.  It is
+        # a pure function of the keyframe's descriptors (KeyFrame::ComputeBoW computes only an empty
+        # mBowVec, src/KeyFrame.cc:63-72, as the KeyFrame copies a Frame's computed one), so only
+        # the time it runs changes; two BowVector / FeatureVector sets alternate between the
+        # keyframe in flight and the next
+        self._prebow = vocabulary is not None and os.environ.get("ORBMI_LM_PREBOW", "1") == "1"
         with torch.cuda.stream(self._ms):
-            if vocabulary is not None:  # mBowVec / mFeatVec of the last keyframe, device-resident
-                self.bow = dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
-                                value=torch.zeros(cap, dtype=torch.float64, device=dev),
-                                node=torch.zeros(cap, dtype=torch.int32, device=dev),
-                                off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
-                                feat=torch.zeros(cap, dtype=torch.int32, device=dev),
-                                counts=torch.zeros(2, dtype=torch.int32, device=dev))
+            if vocabulary is not None:  # mBowVec / mFeatVec of the keyframe, device-resident
+                self.bows = [dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                  value=torch.zeros(cap, dtype=torch.float64, device=dev),
+                                  node=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                  off=torch.zeros(cap + 1, dtype=torch.int32, device=dev),
+                                  feat=torch.zeros(cap, dtype=torch.int32, device=dev),
+                                  counts=torch.zeros(2, dtype=torch.int32, device=dev))
+                             for _ in range(2 if self._prebow else 1)]
+                self.bow = self.bows[0]
         self._ms.synchronize()
-        # the BowVector / FeatureVector sizes, copied to pinned host words on the mapper's stream:
+        # the BowVector / FeatureVector sizes, copied to pinned host words behind the transform:
         # hipHostMalloc memory, never a torch pinned tensor (_hip.py: torch would record events on
         # this library-owned stream when such a tensor is freed, after close() destroyed it)
-        self._counts_h = PinnedWords(2)
-        # the whole chain (ComputeBoW, searches, LocalBA) is in order: one stream, so that the
-        # process's streams stay within the device's hardware queues (orbmi_ba_set_stream)
+        self._counts_hs = [PinnedWords(2) for _ in range(2 if self._prebow else 1)]
+        self._counts_h = self._counts_hs[0]
+        self._slot = 0
+        self.bow_ahead = 0  # transforms issued beside the previous keyframe's LocalBA
+        # the chain's searches and LocalBA are in order on one stream, so that the process's
+        # streams stay within the device's hardware queues (orbmi_ba_set_stream); without the
+        # transform ahead, ComputeBoW joins them there
         self._one_stream = os.environ.get("ORBMI_LM_STREAMS", "one") == "one"
         if self._one_stream:
             check("orbmi_ba_set_stream", lib().orbmi_ba_set_stream(self.ba._h, ms))
-            if vocabulary is not None:
+            if vocabulary is not None and not self._prebow:
                 check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(vocabulary._h, ms))
+        self._vs = None
+        if self._prebow:
+            vs = _vp()
+            check("orbmi_vocabulary_get_stream", lib().orbmi_vocabulary_get_stream(vocabulary._h, C.byref(vs)))
+            self._vs = torch.cuda.ExternalStream(vs.value, device=dev)
         self.q: queue.Queue = queue.Queue()
         self.job_events = None  # a list: per job (start event, end event, host start, host end)
         self.done = 0
@@ -520,8 +538,8 @@ class LocalMapper:
                                       b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
                                       b["counts"].data_ptr())
             bow_done = self._bow_event()
-        # LocalBundleAdjustment reads poses, points and observations, never the BowVector (both
-        # run in order on the mapper's stream)
+        # LocalBundleAdjustment reads poses, points and observations, never the BowVector (they run
+        # in order on the mapper's stream, or side by side with the transform ahead)
         self.last = self.ba.run(problem)
         if self.voc is not None and kf_desc is not None:
             bow_done.synchronize()
@@ -549,14 +567,22 @@ class LocalMapper:
                 ev.record(self._ms)
                 marks.append((name, ev))
         # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
-        # ComputeDistinctiveDescriptors of the keyframe's map points, enqueued back to back
-        b = self.bow
-        self.voc.transform_device(job.d_desc, kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
-                                  b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
-        if not self._one_stream:  # the transform ran on the vocabulary's own stream
-            self.voc.synchronize()
-        # mBowVec / mFeatVec sizes, behind the transform on the mapper's stream
-        self._counts_h.copy_async(b["counts"].data_ptr(), self._ms.cuda_stream)
+        # ComputeDistinctiveDescriptors of the keyframe's map points
+        bow_ev = None
+        if self._prebow:  # issued ahead while the previous keyframe's LocalBA ran, or now
+            slot, bow_ev = job._bow if getattr(job, "_bow", None) is not None else self._issue_bow(job)
+            job._bow = None
+            b, counts_h = self.bows[slot], self._counts_hs[slot]
+            self.bow = b
+        else:  # enqueued back to back with ComputeDistinctiveDescriptors
+            b, counts_h = self.bow, self._counts_h
+            self.voc.transform_device(job.d_desc, kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                                      b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(),
+                                      b["counts"].data_ptr())
+            if not self._one_stream:  # the transform ran on the vocabulary's own stream
+                self.voc.synchronize()
+            # mBowVec / mFeatVec sizes, behind the transform on the mapper's stream
+            counts_h.copy_async(b["counts"].data_ptr(), self._ms.cuda_stream)
         d_obs, d_off, npts = job.obs
         best = self._buf("best", (max(npts, 1),), torch.int32)
         dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
@@ -572,8 +598,10 @@ class LocalMapper:
         bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
+        if bow_ev is not None:  # CreateNewMapPoints reads the FeatureVector
+            self._ms.wait_event(bow_ev)
         mark("bow_distinctive")
-        nw, nn = self._counts_h.read()  # waits for the size copy only (whatever the stream mode)
+        nw, nn = counts_h.read()  # waits for the size copy only (whatever the stream mode)
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
         fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
@@ -597,6 +625,13 @@ class LocalMapper:
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
         mark("distinctive")
+        # the next queued keyframe's ComputeBoW, beside this LocalBA
+        if self._prebow:
+            with self.q.mutex:
+                nxt = self.q.queue[0] if self.q.queue else None
+            if isinstance(nxt, LocalMappingJob) and getattr(nxt, "_bow", None) is None:
+                self._issue_bow(nxt)
+                self.bow_ahead += 1
         # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
         ms = self._ms
@@ -619,6 +654,22 @@ class LocalMapper:
                                                            b["off"][:nn + 1].cpu().numpy(),
                                                            b["feat"][:kf.n].cpu().numpy()))
         return out
+
+    def _issue_bow(self, job):
+        """ComputeBoW of job's keyframe on the vocabulary's stream into the next BowVector /
+        FeatureVector set (the other one belongs to the keyframe in flight, whose searches have
+        been enqueued before this call), its sizes to that set's pinned words; -> (set, event)."""
+        import torch
+        slot = self._slot
+        self._slot = (slot + 1) % len(self.bows)
+        b = self.bows[slot]
+        self.voc.transform_device(job.d_desc, job.kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
+                                  b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
+        self._counts_hs[slot].copy_async(b["counts"].data_ptr(), self._vs.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(self._vs)
+        job._bow = (slot, ev)
+        return job._bow
 
     def _bow_event(self):
         """Event recorded on the vocabulary's stream after the transform just enqueued."""
@@ -653,7 +704,10 @@ class LocalMapper:
             self.last_chain.materialize()  # its closure synchronises self._ms
         self._out = None
         self._bufs = {}
-        self._counts_h.close()
+        if self._vs is not None:
+            self._vs.synchronize()
+        for c in self._counts_hs:
+            c.close()
         if self._one_stream and self.voc is not None and getattr(self.voc, "_h", None):  # it outlives the mapper
             check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(self.voc._h, None))
         self.ba.close()

@@ -86,3 +86,37 @@ def test_local_mapping_chain_matches_oracle(oracle):
         mapper.close()
         voc.close()
         S["tr"].close()
+
+
+def test_compute_bow_ahead_on_the_queue(oracle):
+    """Two keyframes queued on the LocalMapping thread: the second one's ComputeBoW is issued on the
+    vocabulary's stream beside the first one's LocalBA (pipeline.LocalMapper._issue_bow), into the
+    other BowVector / FeatureVector set; both FeatureVectors equal the oracle's transform."""
+    import bench
+    from orb_slam2_with_comment_amd import synth_map as SM
+    from orb_slam2_with_comment_amd.pipeline import LocalMapper
+    from orb_slam2_with_comment_amd.vocabulary import ORBVocabulary, Vocabulary
+    S = bench.setup_track(argparse.Namespace(frames=6, nfeatures=2000), 0, 0)
+    vocab = Vocabulary.synthetic(k=10, L=5, seed=7)
+    voc = ORBVocabulary(vocab, device=0)
+    problem, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
+    jobs, keep = bench.setup_local_mapping(S, voc, vocab, 0, problem)
+    mapper = LocalMapper(0, vocabulary=voc)
+    try:
+        if not mapper._prebow:
+            pytest.skip("ORBMI_LM_PREBOW=0")
+        for f in (3, 5, 3):
+            mapper.insert_keyframe(jobs[f])
+        mapper.wait()
+        assert mapper.done == 3 and mapper.bow_ahead >= 1
+        for slot, f in ((1, 5), (0, 3)):  # keyframes 2 and 3 took sets 1 and 0
+            b = mapper.bows[slot]
+            nn = int(b["counts"][1].item())
+            _, _, node, off, feat = oracle.transform(vocab, jobs[f].host["desc"], 4)
+            np.testing.assert_array_equal(b["node"][:nn].cpu().numpy().view(np.uint32), node)
+            np.testing.assert_array_equal(b["off"][:nn + 1].cpu().numpy(), off)
+            np.testing.assert_array_equal(b["feat"][:jobs[f].kf.n].cpu().numpy(), feat)
+    finally:
+        mapper.close()
+        voc.close()
+        S["tr"].close()

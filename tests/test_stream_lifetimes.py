@@ -68,7 +68,8 @@ def test_local_mapper_close_order(monkeypatch):
     m.t = threading.Thread(target=lambda: (m.q.get(), log.append("thread.exit")))
     m.t.start()
     m._ms = _Rec(log, "stream")
-    m._counts_h = _Rec(log, "pinned")
+    m._counts_hs = [_Rec(log, "pinned")]
+    m._vs = None
     m.ba = _Rec(log, "ba")
     m.matcher = _Rec(log, "matcher")
     m.voc = None
