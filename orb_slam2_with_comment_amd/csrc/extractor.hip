@@ -829,11 +829,12 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
 // after every pass through the parent's (node, quadrant) -> child table.
 constexpr int kOctThreads = 1024;
 constexpr int kOctRegKeys = 12;  // candidates per thread held in registers (12,288 per level; 13 spills)
-#ifdef ORBMI_OCT_TRACE  // tools/octree_trace.hip: s_memtime stamps of (level 0, image 0)
+#ifdef ORBMI_OCT_TRACE  // tools/octree_trace.hip: s_memtime stamps of workgroup g_oct_trace_block
 __device__ unsigned long long g_oct_trace[256];
-#define OCT_STAMP(i, v)                                                                      \
-    do {                                                                                     \
-        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_oct_trace[i] = (v);    \
+__device__ int g_oct_trace_block;
+#define OCT_STAMP(i, v)                                                                                   \
+    do {                                                                                                  \
+        if (threadIdx.x == 0 && (int)blockIdx.x == g_oct_trace_block && blockIdx.y == 0) g_oct_trace[i] = (v); \
     } while (0)
 #define OCT_SUB(it, j) do { if ((it) < 15) OCT_STAMP(100 + 10 * (it) + (j), __builtin_amdgcn_s_memtime()); } while (0)
 #else

@@ -293,6 +293,12 @@ for step in "$@"; do
                 ORBMI_DESC=wave run descab_w_$i 300 python bench.py --mode batch --steps 20 --warmup 4 --no-cpu-baseline
                 echo "4/wave: $(v descab_4_$i) | 1/wave: $(v descab_w_$i)" | tee -a $OUT/descab.txt
             done; cp $OUT/descab.txt $P/;;
+        octtrace)
+            # k_octree phase trace of every level (tools/octree_trace, built in-tree on the CPU) on a
+            # config-5 frame (synthetic EuRoC-shaped 752x480, 5000 features)
+            python -c "import numpy as np; from orb_slam2_with_comment_amd import synth; np.ascontiguousarray(synth.mono(synth.EUROC, 0, seed_base=5000), np.uint8).tofile('$OUT/euroc0.u8')"
+            run octtrace 120 ./tools/octree_trace $OUT/euroc0.u8 480 752 5000; cp $OUT/octtrace.log $P/octree_trace_levels.txt
+            grep -E "== level|total" $OUT/octtrace.log;;
         fastab)
             # config 5 batch: k_fast2 with the one-pass arc strength (default) vs its separate
             # segment-test and score stages (ORBMI_FAST=split), 3 alternations
