@@ -1138,38 +1138,45 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         // which nodes divide, and in which push order
         int ncand = 0, kdiv = 0;
         if (careful) {
-            // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733)
-            int np2 = 2;
-            while (np2 < L) np2 <<= 1;
-            if (np2 <= kOctThreads) {
-                const bool c2 = tid < L && S.cnt[cur][tid] >= 2;
-                const unsigned long long key =
-                    c2 ? ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][tid]) << 32) | (unsigned)tid : ~0ull;
-                const int nw = __popcll(__ballot(c2));
-                if (tid == 0) S.misc[0] = 0;
+            // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733).
+            // The nodes with >= 2 keys (the only ones that can divide) are compacted first, as
+            // (~size, node) keys in any order, and only they are sorted: in one wave by lane
+            // shuffles when they fit in 64, else by the block's bitonic sort on the next power of two
+            if (tid == 0) S.misc[0] = 0;
+            __syncthreads();
+            for (int i0 = 0; i0 < L; i0 += kOctThreads) {
+                const int i = i0 + tid;
+                const int c = i < L ? S.cnt[cur][i] : 0;
+                const unsigned long long m = __ballot(c >= 2);
+                int base = 0;
+                if ((tid & 63) == 0 && m) base = atomicAdd(&S.misc[0], __popcll(m));
+                base = __shfl(base, 0);
+                if (c >= 2)
+                    S.skey[base + lanes_below(m)] = ((unsigned long long)(0xFFFFFFFFu - (unsigned)c) << 32) | (unsigned)i;
+            }
+            for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
+            __syncthreads();
+            ncand = S.misc[0];
+            int np2 = 1;
+            while (np2 < ncand) np2 <<= 1;
+            if (np2 <= 64) {
+                if (tid < 64) {  // wave 0 only (it also walks them below): no barrier
+                    const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
+                    const unsigned long long sorted = bitonic_sort_block(v, 64, S.skey);  // shuffles only
+                    if (tid < ncand) S.skey[tid] = sorted;
+                    wave_sync_lds_ex();  // the walk below reads other lanes' entries
+                }
+            } else if (np2 <= kOctThreads) {
+                const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
+                __syncthreads();  // every key read before the sort reuses S.skey
+                const unsigned long long sorted = bitonic_sort_block(v, np2, S.skey);
                 __syncthreads();
-                if ((tid & 63) == 0 && nw) atomicAdd(&S.misc[0], nw);
-                const unsigned long long sorted = bitonic_sort_block(key, np2, S.skey);
-                __syncthreads();
-                if (tid < np2) S.skey[tid] = sorted;
-                for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
-                ncand = S.misc[0];
+                if (tid < ncand) S.skey[tid] = sorted;
                 __syncthreads();
             } else {
-                for (int i = tid; i < np2; i += blockDim.x) {
-                    unsigned long long key = ~0ull;
-                    if (i < L && S.cnt[cur][i] >= 2)
-                        key = ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
-                    S.skey[i] = key;
-                }
-                if (tid == 0) S.misc[0] = 0;
+                for (int i = ncand + tid; i < np2; i += blockDim.x) S.skey[i] = ~0ull;
                 __syncthreads();
-                for (int i = tid; i < L; i += blockDim.x) {
-                    if (S.cnt[cur][i] >= 2) atomicAdd(&S.misc[0], 1);
-                    S.dflag[i] = 0;
-                }
                 bitonic_sort(S.skey, np2);
-                ncand = S.misc[0];
             }
             // wave 0 walks the sorted candidates in chunks of 64 with wave scans: kdiv = 1 + the
             // first r whose division brings the list to N (L + sum_{r' <= r} (m_r' - 1) >= N),
