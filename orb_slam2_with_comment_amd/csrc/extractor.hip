@@ -1178,36 +1178,33 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                 __syncthreads();
                 bitonic_sort(S.skey, np2);
             }
-            // wave 0 walks the sorted candidates in chunks of 64 with wave scans: kdiv = 1 + the
-            // first r whose division brings the list to N (L + sum_{r' <= r} (m_r' - 1) >= N),
-            // then the divided nodes' push bases (prefix of m in sorted order)
-            if (tid < 64) {
+            // kdiv = 1 + the first r whose division brings the list to N (L + sum_{r' <= r}
+            // (m_r' - 1) >= N, m the node's non-empty children), then the divided nodes' push bases
+            // (prefix of m in sorted order): one block scan of m - 1 over the sorted candidates,
+            // two per thread (the prefix of m is that of m - 1 plus r); the first r to reach N is
+            // the only one whose exclusive prefix is still short of it, so one thread writes kdiv
+            {
                 auto m_of = [&](int n) {
                     return (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
                 };
-                int run = 0, kd = ncand;
-                for (int r0 = 0; r0 < ncand; r0 += 64) {
-                    const int r = r0 + tid;
-                    const int m = r < ncand ? m_of((int)(S.skey[r] & 0xFFFFFFFFu)) : 1;
-                    const int incl = wave_incl_scan(m - 1);
-                    const unsigned long long hit = __ballot(r < ncand && L + run + incl >= N);
-                    if (hit) {
-                        kd = r0 + __ffsll((long long)hit);
-                        break;
-                    }
-                    run += __builtin_amdgcn_readlane(incl, 63);
+                if (tid == 0) S.misc[5] = ncand;  // no r reaches N: every candidate divides
+                const int r0 = 2 * tid, r1 = r0 + 1;
+                const int n0 = r0 < ncand ? (int)(S.skey[r0] & 0xFFFFFFFFu) : 0;
+                const int n1 = r1 < ncand ? (int)(S.skey[r1] & 0xFFFFFFFFu) : 0;
+                const int d0 = r0 < ncand ? m_of(n0) - 1 : 0, d1 = r1 < ncand ? m_of(n1) - 1 : 0;
+                int tot;
+                const int e0 = block_excl_scan(d0 + d1, S.scratch, &tot);  // its barriers publish misc[5]
+                if (r0 < ncand && (r0 == 0 || L + e0 < N) && L + e0 + d0 >= N) S.misc[5] = r0 + 1;
+                if (r1 < ncand && L + e0 + d0 < N && L + e0 + d0 + d1 >= N) S.misc[5] = r1 + 1;
+                __syncthreads();
+                const int kd = S.misc[5];
+                if (r0 < kd) {
+                    S.dflag[n0] = 1;
+                    S.newpos[n0] = e0 + r0;
                 }
-                int push = 0;
-                for (int r0 = 0; r0 < kd; r0 += 64) {
-                    const int r = r0 + tid;
-                    const int n = r < kd ? (int)(S.skey[r] & 0xFFFFFFFFu) : 0;
-                    const int m = r < kd ? m_of(n) : 0;
-                    const int incl = wave_incl_scan(m);
-                    if (r < kd) {
-                        S.dflag[n] = 1;
-                        S.newpos[n] = push + incl - m;
-                    }
-                    push += __builtin_amdgcn_readlane(incl, 63);
+                if (r1 < kd) {
+                    S.dflag[n1] = 1;
+                    S.newpos[n1] = e0 + d0 + r1;
                 }
                 kdiv = kd;
             }
