@@ -1139,44 +1139,98 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         int ncand = 0, kdiv = 0;
         if (careful) {
             // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733).
-            // The nodes with >= 2 keys (the only ones that can divide) are compacted first, as
-            // (~size, node) keys in any order, and only they are sorted: in one wave by lane
-            // shuffles when they fit in 64, else by the block's bitonic sort on the next power of two
-            if (tid == 0) S.misc[0] = 0;
+            // Only the nodes with >= 2 keys can divide, and their sizes are small integers: a
+            // counting sort gives every such node its rank directly -- the nodes with a larger
+            // size, plus the earlier nodes of its own size (per chunk of 64 nodes from ballots over
+            // the chunk's distinct sizes, then a prefix over the chunks).  Sizes of 64 or more
+            // (rare) take the bitonic sort of the compacted candidates instead.
+            static_assert(2 * kOctThreads >= kOctNodeCap, "two nodes per thread");
+            int* Wh = S.tmp;      // [32 chunks][64 sizes]: counts, then their prefix over chunks
+            int* Sgt = S.newpos;  // [64]: candidates of a larger size (newpos is written after the sort)
+            for (int i = tid; i < 32 * 64; i += blockDim.x) Wh[i] = 0;
+            if (tid == 0) {
+                S.misc[0] = 0;
+                S.misc[6] = 0;
+            }
             __syncthreads();
-            for (int i0 = 0; i0 < L; i0 += kOctThreads) {
-                const int i = i0 + tid;
+            int val[2], rnk[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int i = tid + h * kOctThreads, q = i >> 6;
                 const int c = i < L ? S.cnt[cur][i] : 0;
-                const unsigned long long m = __ballot(c >= 2);
-                int base = 0;
-                if ((tid & 63) == 0 && m) base = atomicAdd(&S.misc[0], __popcll(m));
-                base = __shfl(base, 0);
-                if (c >= 2)
-                    S.skey[base + lanes_below(m)] = ((unsigned long long)(0xFFFFFFFFu - (unsigned)c) << 32) | (unsigned)i;
+                const int v = c >= 2 ? min(c, 63) : -1;
+                const unsigned long long mc = __ballot(v >= 0);
+                if (__ballot(c >= 64) && (tid & 63) == 0) S.misc[6] = 1;
+                if (mc && (tid & 63) == 0) atomicAdd(&S.misc[0], __popcll(mc));
+                unsigned long long rem = mc;
+                int rw = 0;
+                while (rem) {  // one round per distinct size in the chunk
+                    const int vv = __builtin_amdgcn_readlane(v, __ffsll((long long)rem) - 1);
+                    const unsigned long long mk = __ballot(v == vv);
+                    if (v == vv) rw = lanes_below(mk);
+                    if ((tid & 63) == 0) Wh[q * 64 + vv] = __popcll(mk);
+                    rem &= ~mk;
+                }
+                val[h] = v;
+                rnk[h] = rw;
             }
             for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
             __syncthreads();
             ncand = S.misc[0];
-            int np2 = 1;
-            while (np2 < ncand) np2 <<= 1;
-            if (np2 <= 64) {
-                if (tid < 64) {  // wave 0 only (it also walks them below): no barrier
-                    const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
-                    const unsigned long long sorted = bitonic_sort_block(v, 64, S.skey);  // shuffles only
-                    if (tid < ncand) S.skey[tid] = sorted;
-                    wave_sync_lds_ex();  // the walk below reads other lanes' entries
+            if (!S.misc[6]) {
+                if (tid < 64) {  // lane = size: prefix over the chunks, then the larger sizes' total
+                    int run = 0;
+                    for (int q0 = 0; q0 < 32; q0 += 8) {  // 8 loads in flight (the VGPR budget)
+                        int t[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) t[q] = Wh[(q0 + q) * 64 + tid];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            Wh[(q0 + q) * 64 + tid] = run;
+                            run += t[q];
+                        }
+                    }
+                    const int rv = __shfl(run, 63 - tid);  // total of size 63 - lane
+                    const int incl = wave_incl_scan(rv);
+                    Sgt[63 - tid] = incl - rv;
                 }
-            } else if (np2 <= kOctThreads) {
-                const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
-                __syncthreads();  // every key read before the sort reuses S.skey
-                const unsigned long long sorted = bitonic_sort_block(v, np2, S.skey);
                 __syncthreads();
-                if (tid < ncand) S.skey[tid] = sorted;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int i = tid + h * kOctThreads, v = val[h];
+                    if (v >= 0)
+                        S.skey[Sgt[v] + Wh[(i >> 6) * 64 + v] + rnk[h]] =
+                            ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
+                }
                 __syncthreads();
             } else {
-                for (int i = ncand + tid; i < np2; i += blockDim.x) S.skey[i] = ~0ull;
+                if (tid == 0) S.misc[0] = 0;
                 __syncthreads();
-                bitonic_sort(S.skey, np2);
+                for (int i0 = 0; i0 < L; i0 += kOctThreads) {
+                    const int i = i0 + tid;
+                    const int c = i < L ? S.cnt[cur][i] : 0;
+                    const unsigned long long m = __ballot(c >= 2);
+                    int base = 0;
+                    if ((tid & 63) == 0 && m) base = atomicAdd(&S.misc[0], __popcll(m));
+                    base = __shfl(base, 0);
+                    if (c >= 2)
+                        S.skey[base + lanes_below(m)] = ((unsigned long long)(0xFFFFFFFFu - (unsigned)c) << 32) | (unsigned)i;
+                }
+                __syncthreads();
+                int np2 = 1;
+                while (np2 < ncand) np2 <<= 1;
+                if (np2 <= kOctThreads) {
+                    const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
+                    __syncthreads();  // every key read before the sort reuses S.skey
+                    const unsigned long long sorted = bitonic_sort_block(v, max(np2, 2), S.skey);
+                    __syncthreads();
+                    if (tid < ncand) S.skey[tid] = sorted;
+                    __syncthreads();
+                } else {
+                    for (int i = ncand + tid; i < np2; i += blockDim.x) S.skey[i] = ~0ull;
+                    __syncthreads();
+                    bitonic_sort(S.skey, np2);
+                }
             }
             // kdiv = 1 + the first r whose division brings the list to N (L + sum_{r' <= r}
             // (m_r' - 1) >= N, m the node's non-empty children), then the divided nodes' push bases
