@@ -852,6 +852,7 @@ struct OctShared {
     unsigned char dflag[kOctNodeCap];
     int scratch[kOctThreads / 64 + 2];
     int misc[8];
+    int dummy[64];                       // per-lane sink of the key pass's branch-free adds
     int rpre[kFastRegions + 1];          // candidate regions: prefix of counts, first slots
     int rbase[kFastRegions];
     unsigned tagl[kOctThreads * kOctRegKeys];  // order tags of the register-resident keys
@@ -1109,17 +1110,16 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                 nreg[r] = v ? node | dep << 16 : 0;
                 tgt[r] = v ? 4 * node + oct_quad(preg[r], dep) : -1;
             }
-            int run = -1, rc = 0;
+            // one add per run of equal targets, branch-free: every key issues one ds_add, the
+            // ones inside a run (or absent) add 0 to the lane's own dummy word
+            int start = 0;
 #pragma unroll
             for (int r = 0; r < kOctRegKeys; r++) {
-                if (tgt[r] != run) {
-                    if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
-                    run = tgt[r];
-                    rc = 0;
-                }
-                rc++;
+                const bool flush = r == kOctRegKeys - 1 || tgt[r] != tgt[r + (r < kOctRegKeys - 1)];
+                const bool real = flush && tgt[r] >= 0;
+                atomicAdd(real ? &S.ccnt[0][0] + tgt[r] : &S.dummy[tid & 63], real ? r + 1 - start : 0);
+                start = flush ? r + 1 : start;
             }
-            if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
             OCT_SUB(iter, 7);
             // spilled keys
             for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
