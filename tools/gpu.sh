@@ -299,6 +299,12 @@ for step in "$@"; do
             python -c "import numpy as np; from orb_slam2_with_comment_amd import synth; np.ascontiguousarray(synth.mono(synth.EUROC, 0, seed_base=5000), np.uint8).tofile('$OUT/euroc0.u8')"
             run octtrace 120 ./tools/octree_trace $OUT/euroc0.u8 480 752 5000; cp $OUT/octtrace.log $P/octree_trace_levels.txt
             grep -E "== level|total" $OUT/octtrace.log;;
+        octab)
+            # the octree phase trace of every level on a KITTI-shaped left image (2000 features), this
+            # tree's kernel against tools/octree_trace_old (another build of the trace tool)
+            python -c "import numpy as np; from orb_slam2_with_comment_amd import synth; np.ascontiguousarray(synth.stereo_pair(synth.KITTI, 0)[0], np.uint8).tofile('$OUT/kitti0.u8')"
+            run octab_new 120 ./tools/octree_trace $OUT/kitti0.u8 376 1241 2000 && run octab_old 120 ./tools/octree_trace_old $OUT/kitti0.u8 376 1241 2000
+            for v in new old; do echo "== $v"; grep -E "== level|total" $OUT/octab_$v.log; done | tee $P/octree_ab_kitti.txt;;
         fastab)
             # config 5 batch: k_fast2 with the one-pass arc strength (default) vs its separate
             # segment-test and score stages (ORBMI_FAST=split), 3 alternations
