@@ -1141,36 +1141,45 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
             // vSizeAndPointerToNode sorted by (size, creation); divided largest first (:681-733).
             // Only the nodes with >= 2 keys can divide, and their sizes are small integers: a
             // counting sort gives every such node its rank directly -- the nodes with a larger
-            // size, plus the earlier nodes of its own size (per chunk of 64 nodes from ballots over
-            // the chunk's distinct sizes, then a prefix over the chunks).  Sizes of 64 or more
-            // (rare) take the bitonic sort of the compacted candidates instead.
+            // size, plus the earlier nodes of its own size (per chunk of 64 nodes from the ballots
+            // of the size's six bit planes, then a prefix over the chunks).  A size of 64 or more
+            // takes the bitonic sort of the compacted candidates instead.
             static_assert(2 * kOctThreads >= kOctNodeCap, "two nodes per thread");
             int* Wh = S.tmp;      // [32 chunks][64 sizes]: counts, then their prefix over chunks
             int* Sgt = S.newpos;  // [64]: candidates of a larger size (newpos is written after the sort)
-            for (int i = tid; i < 32 * 64; i += blockDim.x) Wh[i] = 0;
+            // a size of 64 or more anywhere takes the bitonic path: flagged with the zeroing
             if (tid == 0) {
                 S.misc[0] = 0;
                 S.misc[6] = 0;
             }
             __syncthreads();
+            {
+                bool big = false;
+                for (int i = tid; i < 32 * 64; i += blockDim.x) {
+                    Wh[i] = 0;
+                    big |= i < L && S.cnt[cur][i] >= 64;
+                }
+                if (__ballot(big) && (tid & 63) == 0) S.misc[6] = 1;
+            }
+            __syncthreads();
+            const bool counting = !S.misc[6];
             int val[2], rnk[2];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int i = tid + h * kOctThreads, q = i >> 6;
                 const int c = i < L ? S.cnt[cur][i] : 0;
-                const int v = c >= 2 ? min(c, 63) : -1;
-                const unsigned long long mc = __ballot(v >= 0);
-                if (__ballot(c >= 64) && (tid & 63) == 0) S.misc[6] = 1;
+                const int v = c >= 2 && counting ? c : -1;
+                const unsigned long long mc = __ballot(c >= 2);
                 if (mc && (tid & 63) == 0) atomicAdd(&S.misc[0], __popcll(mc));
-                unsigned long long rem = mc;
-                int rw = 0;
-                while (rem) {  // one round per distinct size in the chunk
-                    const int vv = __builtin_amdgcn_readlane(v, __ffsll((long long)rem) - 1);
-                    const unsigned long long mk = __ballot(v == vv);
-                    if (v == vv) rw = lanes_below(mk);
-                    if ((tid & 63) == 0) Wh[q * 64 + vv] = __popcll(mk);
-                    rem &= ~mk;
+                // the chunk's lanes of the same size: the six bit planes of the size, combined
+                unsigned long long same = __ballot(v >= 0);
+#pragma unroll
+                for (int bit = 0; bit < 6; bit++) {
+                    const unsigned long long pl = __ballot((v >> bit) & 1);
+                    same &= ((v >> bit) & 1) ? pl : ~pl;
                 }
+                const int rw = lanes_below(same);
+                if (v >= 0 && rw == 0) Wh[q * 64 + v] = __popcll(same);  // the size's first lane
                 val[h] = v;
                 rnk[h] = rw;
             }
