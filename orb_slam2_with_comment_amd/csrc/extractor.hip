@@ -852,7 +852,6 @@ struct OctShared {
     unsigned char dflag[kOctNodeCap];
     int scratch[kOctThreads / 64 + 2];
     int misc[8];
-    int dummy[64];                       // per-lane sink of the key pass's branch-free adds
     int rpre[kFastRegions + 1];          // candidate regions: prefix of counts, first slots
     int rbase[kFastRegions];
     unsigned tagl[kOctThreads * kOctRegKeys];  // order tags of the register-resident keys
@@ -1092,7 +1091,11 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
         for (int i = tid; i < L; i += blockDim.x) {
             S.ccnt[i][0] = S.ccnt[i][1] = S.ccnt[i][2] = S.ccnt[i][3] = 0;
         }
-        if (tid == 0) S.misc[2 + (iter & 1)] = 0;  // read at the end of pass iter - 2
+        if (tid == 0) {
+            S.misc[2 + (iter & 1)] = 0;  // read at the end of pass iter - 2
+            S.misc[0] = 0;               // careful mode: candidate count, size >= 64 flag
+            S.misc[6] = 0;
+        }
         __syncthreads();
         OCT_SUB(iter, 0);
         // keys: apply the previous pass's remap (an entry with bit 14 set means the node was
@@ -1110,16 +1113,17 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                 nreg[r] = v ? node | dep << 16 : 0;
                 tgt[r] = v ? 4 * node + oct_quad(preg[r], dep) : -1;
             }
-            // one add per run of equal targets, branch-free: every key issues one ds_add, the
-            // ones inside a run (or absent) add 0 to the lane's own dummy word
-            int start = 0;
+            int run = -1, rc = 0;
 #pragma unroll
             for (int r = 0; r < kOctRegKeys; r++) {
-                const bool flush = r == kOctRegKeys - 1 || tgt[r] != tgt[r + (r < kOctRegKeys - 1)];
-                const bool real = flush && tgt[r] >= 0;
-                atomicAdd(real ? &S.ccnt[0][0] + tgt[r] : &S.dummy[tid & 63], real ? r + 1 - start : 0);
-                start = flush ? r + 1 : start;
+                if (tgt[r] != run) {
+                    if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
+                    run = tgt[r];
+                    rc = 0;
+                }
+                rc++;
             }
+            if (rc && run >= 0) atomicAdd(&S.ccnt[0][0] + run, rc);
             OCT_SUB(iter, 7);
             // spilled keys
             for (int k = tid + kOctThreads * kOctRegKeys; k < nkeys; k += kOctThreads) {
@@ -1143,16 +1147,12 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
             // counting sort gives every such node its rank directly -- the nodes with a larger
             // size, plus the earlier nodes of its own size (per chunk of 64 nodes from the ballots
             // of the size's six bit planes, then a prefix over the chunks).  A size of 64 or more
-            // takes the bitonic sort of the compacted candidates instead.
+            // takes round 5's path: a bitonic sort of the whole list, wave 0 walking the result.
             static_assert(2 * kOctThreads >= kOctNodeCap, "two nodes per thread");
             int* Wh = S.tmp;      // [32 chunks][64 sizes]: counts, then their prefix over chunks
             int* Sgt = S.newpos;  // [64]: candidates of a larger size (newpos is written after the sort)
-            // a size of 64 or more anywhere takes the bitonic path: flagged with the zeroing
-            if (tid == 0) {
-                S.misc[0] = 0;
-                S.misc[6] = 0;
-            }
-            __syncthreads();
+            // a size of 64 or more anywhere takes round 5's bitonic path (misc[0], misc[6] were
+            // reset at the top of the pass)
             {
                 bool big = false;
                 for (int i = tid; i < 32 * 64; i += blockDim.x) {
@@ -1162,31 +1162,29 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                 if (__ballot(big) && (tid & 63) == 0) S.misc[6] = 1;
             }
             __syncthreads();
-            const bool counting = !S.misc[6];
-            int val[2], rnk[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int i = tid + h * kOctThreads, q = i >> 6;
-                const int c = i < L ? S.cnt[cur][i] : 0;
-                const int v = c >= 2 && counting ? c : -1;
-                const unsigned long long mc = __ballot(c >= 2);
-                if (mc && (tid & 63) == 0) atomicAdd(&S.misc[0], __popcll(mc));
-                // the chunk's lanes of the same size: the six bit planes of the size, combined
-                unsigned long long same = __ballot(v >= 0);
-#pragma unroll
-                for (int bit = 0; bit < 6; bit++) {
-                    const unsigned long long pl = __ballot((v >> bit) & 1);
-                    same &= ((v >> bit) & 1) ? pl : ~pl;
-                }
-                const int rw = lanes_below(same);
-                if (v >= 0 && rw == 0) Wh[q * 64 + v] = __popcll(same);  // the size's first lane
-                val[h] = v;
-                rnk[h] = rw;
-            }
-            for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
-            __syncthreads();
-            ncand = S.misc[0];
             if (!S.misc[6]) {
+                int val[2], rnk[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int i = tid + h * kOctThreads, q = i >> 6;
+                    const int c = i < L ? S.cnt[cur][i] : 0;
+                    const int v = c >= 2 ? c : -1;
+                    // the chunk's lanes of the same size: the six bit planes of the size, combined
+                    unsigned long long same = __ballot(v >= 0);
+                    if (same && (tid & 63) == 0) atomicAdd(&S.misc[0], __popcll(same));
+#pragma unroll
+                    for (int bit = 0; bit < 6; bit++) {
+                        const unsigned long long pl = __ballot((v >> bit) & 1);
+                        same &= ((v >> bit) & 1) ? pl : ~pl;
+                    }
+                    const int rw = lanes_below(same);
+                    if (v >= 0 && rw == 0) Wh[q * 64 + v] = __popcll(same);  // the size's first lane
+                    val[h] = v;
+                    rnk[h] = rw;
+                }
+                for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
+                __syncthreads();
+                ncand = S.misc[0];
                 if (tid < 64) {  // lane = size: prefix over the chunks, then the larger sizes' total
                     int run = 0;
                     for (int q0 = 0; q0 < 32; q0 += 8) {  // 8 loads in flight (the VGPR budget)
@@ -1212,64 +1210,98 @@ __device__ __forceinline__ void octree_body(OctShared& S, int level, int b, cons
                             ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
                 }
                 __syncthreads();
-            } else {
-                if (tid == 0) S.misc[0] = 0;
-                __syncthreads();
-                for (int i0 = 0; i0 < L; i0 += kOctThreads) {
-                    const int i = i0 + tid;
-                    const int c = i < L ? S.cnt[cur][i] : 0;
-                    const unsigned long long m = __ballot(c >= 2);
-                    int base = 0;
-                    if ((tid & 63) == 0 && m) base = atomicAdd(&S.misc[0], __popcll(m));
-                    base = __shfl(base, 0);
-                    if (c >= 2)
-                        S.skey[base + lanes_below(m)] = ((unsigned long long)(0xFFFFFFFFu - (unsigned)c) << 32) | (unsigned)i;
-                }
-                __syncthreads();
-                int np2 = 1;
-                while (np2 < ncand) np2 <<= 1;
-                if (np2 <= kOctThreads) {
-                    const unsigned long long v = tid < ncand ? S.skey[tid] : ~0ull;
-                    __syncthreads();  // every key read before the sort reuses S.skey
-                    const unsigned long long sorted = bitonic_sort_block(v, max(np2, 2), S.skey);
+                // kdiv = 1 + the first r whose division brings the list to N (L + sum_{r' <= r}
+                // (m_r' - 1) >= N, m the node's non-empty children), then the divided nodes' push bases
+                // (prefix of m in sorted order): one block scan of m - 1 over the sorted candidates,
+                // two per thread (the prefix of m is that of m - 1 plus r); the first r to reach N is
+                // the only one whose exclusive prefix is still short of it, so one thread writes kdiv
+                {
+                    auto m_of = [&](int n) {
+                        return (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
+                    };
+                    if (tid == 0) S.misc[5] = ncand;  // no r reaches N: every candidate divides
+                    const int r0 = 2 * tid, r1 = r0 + 1;
+                    const int n0 = r0 < ncand ? (int)(S.skey[r0] & 0xFFFFFFFFu) : 0;
+                    const int n1 = r1 < ncand ? (int)(S.skey[r1] & 0xFFFFFFFFu) : 0;
+                    const int d0 = r0 < ncand ? m_of(n0) - 1 : 0, d1 = r1 < ncand ? m_of(n1) - 1 : 0;
+                    int tot;
+                    const int e0 = block_excl_scan(d0 + d1, S.scratch, &tot);  // its barriers publish misc[5]
+                    if (r0 < ncand && (r0 == 0 || L + e0 < N) && L + e0 + d0 >= N) S.misc[5] = r0 + 1;
+                    if (r1 < ncand && L + e0 + d0 < N && L + e0 + d0 + d1 >= N) S.misc[5] = r1 + 1;
                     __syncthreads();
-                    if (tid < ncand) S.skey[tid] = sorted;
+                    const int kd = S.misc[5];
+                    if (r0 < kd) {
+                        S.dflag[n0] = 1;
+                        S.newpos[n0] = e0 + r0;
+                    }
+                    if (r1 < kd) {
+                        S.dflag[n1] = 1;
+                        S.newpos[n1] = e0 + d0 + r1;
+                    }
+                    kdiv = kd;
+                }
+            } else {
+                int np2 = 2;
+                while (np2 < L) np2 <<= 1;
+                if (np2 <= kOctThreads) {
+                    const bool c2 = tid < L && S.cnt[cur][tid] >= 2;
+                    const unsigned long long key =
+                        c2 ? ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][tid]) << 32) | (unsigned)tid : ~0ull;
+                    const int nw = __popcll(__ballot(c2));
+                    if ((tid & 63) == 0 && nw) atomicAdd(&S.misc[0], nw);
+                    const unsigned long long sorted = bitonic_sort_block(key, np2, S.skey);
+                    __syncthreads();
+                    if (tid < np2) S.skey[tid] = sorted;
+                    for (int i = tid; i < L; i += blockDim.x) S.dflag[i] = 0;
+                    ncand = S.misc[0];
                     __syncthreads();
                 } else {
-                    for (int i = ncand + tid; i < np2; i += blockDim.x) S.skey[i] = ~0ull;
-                    __syncthreads();
+                    for (int i = tid; i < np2; i += blockDim.x) {
+                        unsigned long long key = ~0ull;
+                        if (i < L && S.cnt[cur][i] >= 2)
+                            key = ((unsigned long long)(0xFFFFFFFFu - (unsigned)S.cnt[cur][i]) << 32) | (unsigned)i;
+                        S.skey[i] = key;
+                    }
+                    for (int i = tid; i < L; i += blockDim.x) {
+                        if (S.cnt[cur][i] >= 2) atomicAdd(&S.misc[0], 1);
+                        S.dflag[i] = 0;
+                    }
                     bitonic_sort(S.skey, np2);
+                    ncand = S.misc[0];
                 }
-            }
-            // kdiv = 1 + the first r whose division brings the list to N (L + sum_{r' <= r}
-            // (m_r' - 1) >= N, m the node's non-empty children), then the divided nodes' push bases
-            // (prefix of m in sorted order): one block scan of m - 1 over the sorted candidates,
-            // two per thread (the prefix of m is that of m - 1 plus r); the first r to reach N is
-            // the only one whose exclusive prefix is still short of it, so one thread writes kdiv
-            {
-                auto m_of = [&](int n) {
-                    return (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
-                };
-                if (tid == 0) S.misc[5] = ncand;  // no r reaches N: every candidate divides
-                const int r0 = 2 * tid, r1 = r0 + 1;
-                const int n0 = r0 < ncand ? (int)(S.skey[r0] & 0xFFFFFFFFu) : 0;
-                const int n1 = r1 < ncand ? (int)(S.skey[r1] & 0xFFFFFFFFu) : 0;
-                const int d0 = r0 < ncand ? m_of(n0) - 1 : 0, d1 = r1 < ncand ? m_of(n1) - 1 : 0;
-                int tot;
-                const int e0 = block_excl_scan(d0 + d1, S.scratch, &tot);  // its barriers publish misc[5]
-                if (r0 < ncand && (r0 == 0 || L + e0 < N) && L + e0 + d0 >= N) S.misc[5] = r0 + 1;
-                if (r1 < ncand && L + e0 + d0 < N && L + e0 + d0 + d1 >= N) S.misc[5] = r1 + 1;
-                __syncthreads();
-                const int kd = S.misc[5];
-                if (r0 < kd) {
-                    S.dflag[n0] = 1;
-                    S.newpos[n0] = e0 + r0;
+                // wave 0 walks the sorted candidates in chunks of 64 with wave scans: kdiv = 1 + the
+                // first r whose division brings the list to N (L + sum_{r' <= r} (m_r' - 1) >= N),
+                // then the divided nodes' push bases (prefix of m in sorted order)
+                if (tid < 64) {
+                    auto m_of = [&](int n) {
+                        return (S.ccnt[n][0] > 0) + (S.ccnt[n][1] > 0) + (S.ccnt[n][2] > 0) + (S.ccnt[n][3] > 0);
+                    };
+                    int run = 0, kd = ncand;
+                    for (int r0 = 0; r0 < ncand; r0 += 64) {
+                        const int r = r0 + tid;
+                        const int m = r < ncand ? m_of((int)(S.skey[r] & 0xFFFFFFFFu)) : 1;
+                        const int incl = wave_incl_scan(m - 1);
+                        const unsigned long long hit = __ballot(r < ncand && L + run + incl >= N);
+                        if (hit) {
+                            kd = r0 + __ffsll((long long)hit);
+                            break;
+                        }
+                        run += __builtin_amdgcn_readlane(incl, 63);
+                    }
+                    int push = 0;
+                    for (int r0 = 0; r0 < kd; r0 += 64) {
+                        const int r = r0 + tid;
+                        const int n = r < kd ? (int)(S.skey[r] & 0xFFFFFFFFu) : 0;
+                        const int m = r < kd ? m_of(n) : 0;
+                        const int incl = wave_incl_scan(m);
+                        if (r < kd) {
+                            S.dflag[n] = 1;
+                            S.newpos[n] = push + incl - m;
+                        }
+                        push += __builtin_amdgcn_readlane(incl, 63);
+                    }
+                    kdiv = kd;
                 }
-                if (r1 < kd) {
-                    S.dflag[n1] = 1;
-                    S.newpos[n1] = e0 + d0 + r1;
-                }
-                kdiv = kd;
             }
             __syncthreads();
         }
