@@ -461,7 +461,7 @@ class LocalMapper:
         # ComputeBoW ahead (ORBMI_LM_PREBOW, default on): the next queued keyframe's transform runs
         # on the vocabulary's own stream while this keyframe's LocalBA runs on the mapper's.  It is
         # a pure function of the keyframe's descriptors (KeyFrame::ComputeBoW computes only an empty
-        # mBowVec, src/KeyFrame.cc:63-72, as the KeyFrame copies a Frame's computed one), so only
+        # mBowVec, src/KeyFrame.cc:59-70, as the KeyFrame copies a Frame's computed one), so only
         # the time it runs changes; two BowVector / FeatureVector sets alternate between the
         # keyframe in flight and the next
         self._prebow = vocabulary is not None and os.environ.get("ORBMI_LM_PREBOW", "1") == "1"
