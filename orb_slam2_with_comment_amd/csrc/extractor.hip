@@ -158,7 +158,10 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(const uint8_t* __restri
 // then every thread forms 8 consecutive output bytes from LDS byte reads and stores them as one
 // 8-B word (byte stores only at the row's end).  Global byte loads would bind on the texture
 // addresser (one 64-lane address batch per byte).
-constexpr int kPyrBRows = 4;
+#ifndef ORBMI_PYR_ROWS
+#define ORBMI_PYR_ROWS 4
+#endif
+constexpr int kPyrBRows = ORBMI_PYR_ROWS;  // padded rows per workgroup (A/B builds: -DORBMI_PYR_ROWS)
 constexpr int kPyrBThreads = 256;
 
 // Level 0: copyMakeBorder(image, 19, BORDER_REFLECT_101) (src/ORBextractor.cc:1128-1129); it

@@ -180,7 +180,7 @@ for step in "$@"; do
             for i in 1 2 3; do
                 ORBMI_LIB=$A run abb_A$i 300 python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
                 ORBMI_LIB=$B run abb_B$i 300 python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
-                echo "A $(tail -1 $OUT/abb_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_step"))')  B $(tail -1 $OUT/abb_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_step"))')" | tee -a $OUT/abbatch.txt
+                echo "A $(tail -1 $OUT/abb_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_launch") or d.get("stage_ms_per_step"))')  B $(tail -1 $OUT/abb_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_launch") or d.get("stage_ms_per_step"))')" | tee -a $OUT/abbatch.txt
             done;;
         ab=*)
             pair=${step#ab=}; A=${pair%,*}; B=${pair#*,}
