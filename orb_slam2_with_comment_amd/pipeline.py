@@ -663,6 +663,11 @@ class LocalMapper:
         slot = self._slot
         self._slot = (slot + 1) % len(self.bows)
         b = self.bows[slot]
+        # behind everything enqueued on the mapper's stream so far: the set's previous keyframe
+        # read its FeatureVector there
+        ms_ev = torch.cuda.Event()
+        ms_ev.record(self._ms)
+        self._vs.wait_event(ms_ev)
         self.voc.transform_device(job.d_desc, job.kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
                                   b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
         self._counts_hs[slot].copy_async(b["counts"].data_ptr(), self._vs.cuda_stream)
