@@ -364,7 +364,11 @@ def run_track(a, rank, world, local, dist):
     # (ComputeBoW on the extraction stream, orbmi_vocabulary_share_stream, was measured slower:
     # 1,489 vs 2,517 frames/s -- the transform then queues behind the frames the host enqueued
     # ahead, and the LocalMapping thread waits for it)
-    mapper = LocalMapper(local, vocabulary=voc)
+    # ComputeBoW ahead takes one more stream (the vocabulary's); with N > 1 the exchange stream and
+    # RCCL's add theirs, so there it stays off unless ORBMI_LM_PREBOW says otherwise (the streams
+    # then stay within the 4 hardware queues the gloo rehearsal ran with)
+    prebow = os.environ.get("ORBMI_LM_PREBOW", "1" if world == 1 else "0") == "1"
+    mapper = LocalMapper(local, vocabulary=voc, prebow=prebow)
     kf_desc = lambda f: (S["keep"][1][f].data_ptr(), S["n_lf"][f])  # noqa: E731  (the keyframe's descriptors)
     # the whole LocalMapping::Run body per keyframe (ProcessNewKeyFrame, CreateNewMapPoints,
     # SearchInNeighbors, LocalBundleAdjustment); --lm-chain bow-ba keeps round 2's ComputeBoW + LocalBA
@@ -571,8 +575,10 @@ def run_track(a, rank, world, local, dist):
                             "PoseOptimization] + TrackLocalMap [SearchLocalPoints(th=1, "
                             f"~{int(np.mean([n for n in S['n_mp'] if n]))} MPs), PoseOptimization] "
                             + (f"+ LocalMapping::Run every {KF_EVERY}th frame on the concurrent LocalMapping thread "
-                               "[ProcessNewKeyFrame: KeyFrame::ComputeBoW (a queued keyframe's issued beside the "
-                               "previous LocalBA, on the vocabulary's stream) + ComputeDistinctiveDescriptors; "
+                               "[ProcessNewKeyFrame: KeyFrame::ComputeBoW"
+                               + (" (a queued keyframe's issued beside the previous LocalBA, on the vocabulary's stream)"
+                                  if getattr(mapper, "_prebow", False) else "")
+                               + " + ComputeDistinctiveDescriptors; "
                                "CreateNewMapPoints: SearchForTriangulation x9 neighbours + triangulation geometry, all on the device; "
                                "SearchInNeighbors: Fuse x9 targets + Fuse(KF, targets' points) + "
                                "ComputeDistinctiveDescriptors; LocalBundleAdjustment(config 3)]" if full_chain else

@@ -434,7 +434,7 @@ class LocalMapper:
     self-contained, like the LocalBA problem it carries.  A job given as (problem, kf_desc) runs
     only ComputeBoW + LocalBA (the round-2 chain)."""
 
-    def __init__(self, device=0, vocabulary=None, max_features=8192):
+    def __init__(self, device=0, vocabulary=None, max_features=8192, prebow=None):
         import torch
         from .matcher import ORBmatcher
         from .optimizer import LocalBA
@@ -464,7 +464,9 @@ class LocalMapper:
         # mBowVec, src/KeyFrame.cc:59-70, as the KeyFrame copies a Frame's computed one), so only
         # the time it runs changes; two BowVector / FeatureVector sets alternate between the
         # keyframe in flight and the next
-        self._prebow = vocabulary is not None and os.environ.get("ORBMI_LM_PREBOW", "1") == "1"
+        if prebow is None:
+            prebow = os.environ.get("ORBMI_LM_PREBOW", "1") == "1"
+        self._prebow = vocabulary is not None and bool(prebow)
         with torch.cuda.stream(self._ms):
             if vocabulary is not None:  # mBowVec / mFeatVec of the keyframe, device-resident
                 self.bows = [dict(word=torch.zeros(cap, dtype=torch.int32, device=dev),
