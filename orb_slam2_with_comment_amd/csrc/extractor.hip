@@ -1937,7 +1937,8 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         e = getenv("ORBMI_FAST_EARLY");
         fast_early = e && !strcmp(e, "1");
         e = getenv("ORBMI_BLUR");
-        blur_mode = !e ? -1 : !strcmp(e, "side") ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2 : -1;
+        blur_mode = !e ? -1 : !strcmp(e, "side") ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2
+                  : !strcmp(e, "afterfast") ? 3 : -1;
     }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
@@ -2268,7 +2269,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     // (0.143 -> 0.222 ms) and config 5 stayed at 89k frames/s (profiles/r04/fast_early_ab.txt).
     const bool early = batch > kPyrTiledMaxBatch && blur_mode == 0 && !fast_v1 && fast_early &&
                        levels[0].cell_begin == 0 && nlevels > 1;
-    if (blur_mode == 0 || early) {
+    if (blur_mode == 0 || blur_mode == 3 || early) {
         const int rc = ensure_side_stream();
         if (rc) return rc;
     }
@@ -2318,6 +2319,16 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                            pyr_hy, d_level_count, pyr_lds0, pyr_lds_half);
         prof_end(ORBMI_STAGE_PYR_LEVEL0, ev);
     }
+    auto side_blur = [&]() -> int {  // the blur on the side stream from this point of the stream
+        ORBMI_HIP(hipEventRecord(ev_pyr, stream));
+        ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
+        hipEvent_t eb = prof_begin(ORBMI_STAGE_BLUR, bstream);
+        hipLaunchKernelGGL(k_blur, dim3(xcd_image_grid(nbtiles, batch)), dim3(256), 0, bstream, d_pyr, d_blur, pimg, bimg,
+                           d_levels, d_btiles, batch);
+        prof_end(ORBMI_STAGE_BLUR, eb, bstream);
+        ORBMI_HIP(hipEventRecord(ev_blur, bstream));
+        return ORBMI_OK;
+    };
     if (blur_mode == 0) {
         ORBMI_HIP(hipEventRecord(ev_pyr, stream));
         ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
@@ -2330,6 +2341,10 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     hipEvent_t ev = prof_begin(ORBMI_STAGE_FAST);
     launch_fast(early ? levels[1].cell_begin : 0, ncells, stream);
     prof_end(ORBMI_STAGE_FAST, ev);
+    if (blur_mode == 3) {  // ORBMI_BLUR=afterfast: beside the octrees only (A/B)
+        const int rc = side_blur();
+        if (rc) return rc;
+    }
     if (early) ORBMI_HIP(hipStreamWaitEvent(stream, ev_f0, 0));
     ev = prof_begin(ORBMI_STAGE_OCTREE);
     const bool fused = blur_mode == 1;
@@ -2345,7 +2360,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                            d_levels, d_btiles, batch);
         prof_end(ORBMI_STAGE_BLUR, ev);
     }
-    if (blur_mode == 0) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
+    if (blur_mode == 0 || blur_mode == 3) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
     if (describe_wave)  // ORBMI_DESC=wave: one keypoint per wave (A/B)
         hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,

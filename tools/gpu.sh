@@ -174,6 +174,15 @@ for step in "$@"; do
                 run envab_B$i 300 env $kv python bench.py --steps 100 --warmup 10 --no-cpu-baseline
                 echo "default $(tail -1 $OUT/envab_A$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("pcie_inclusive", {}).get("value"), d["phase_ms_per_frame"])')  $kv $(tail -1 $OUT/envab_B$i.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("pcie_inclusive", {}).get("value"), d["phase_ms_per_frame"])')" | tee -a $OUT/envab.txt
             done;;
+        envbatch=*)
+            # config 5 (batch mode): default against an environment knob (VAR=VALUE), 3 alternations
+            kv=${step#envbatch=}
+            v() { tail -1 $OUT/$1.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d.get("stage_ms_per_launch"))'; }
+            for i in 1 2 3; do
+                run envb_A$i 300 python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
+                run envb_B$i 300 env $kv python bench.py --mode batch --steps 50 --warmup 4 --no-cpu-baseline
+                echo "default $(v envb_A$i) | $kv $(v envb_B$i)" | tee -a $OUT/envbatch.txt
+            done;;
         abbatch=*)
             # config-5 (batch mode) A/B of two library builds, 3 alternations, stage times kept
             pair=${step#abbatch=}; A=${pair%,*}; B=${pair#*,}
