@@ -80,9 +80,12 @@ struct Extractor {
     bool describe_wave = false;  // ORBMI_DESC=wave: the one-keypoint-per-wave describe kernel
     bool fast_v1 = false;        // ORBMI_FAST=v1: the per-lane FAST kernel
     bool fast_split = false;     // ORBMI_FAST=split: k_fast2 with the segment tests and scores as separate stages
-    int blur_mode = -1;          // GaussianBlur (ORBMI_BLUR): -1 by batch, 0 side stream, 1 in the octree launch, 2 after it, 3 side stream after FAST
+    int blur_mode = -1;          // GaussianBlur (ORBMI_BLUR): -1 by batch, 0 side stream, 1 in the octree launch, 2 after it,
+                                 // 3 side stream after FAST, 4 side stream level by level behind the pyramid
     hipStream_t bstream = nullptr;  // the blur's side stream
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
+    std::vector<hipEvent_t> ev_lv;   // ORBMI_BLUR=perlevel: level l of the pyramid written
+    std::vector<int> btile_off;      // first blur tile of each level (btiles are level-major), and the end
     bool fast_early = false;     // ORBMI_FAST_EARLY=1: level 0's FAST on the side stream beside the resize chain
 
     // device buffers (capacity for `bcap` images)

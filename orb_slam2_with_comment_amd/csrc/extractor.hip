@@ -1938,7 +1938,7 @@ int Extractor::init(int dev, int nf, float sf, int nl, int ini, int mn) {
         fast_early = e && !strcmp(e, "1");
         e = getenv("ORBMI_BLUR");
         blur_mode = !e ? -1 : !strcmp(e, "side") ? 0 : !strcmp(e, "fused") ? 1 : !strcmp(e, "serial") ? 2
-                  : !strcmp(e, "afterfast") ? 3 : -1;
+                  : !strcmp(e, "afterfast") ? 3 : !strcmp(e, "perlevel") ? 4 : -1;
     }
     std::vector<float> tab(scale);
     tab.insert(tab.end(), inv_scale.begin(), inv_scale.end());
@@ -2195,6 +2195,9 @@ int Extractor::set_geometry(int r, int c) {
         for (int y0 = 0; y0 < levels[l].H; y0 += kBlurTH)
             for (int x0 = 0; x0 < levels[l].W; x0 += kBlurTW) btiles.push_back(make_int2(l, x0 | (y0 << 16)));
     nbtiles = (int)btiles.size();
+    btile_off.assign(nlevels + 1, 0);
+    for (const int2& t : btiles) btile_off[t.x + 1]++;
+    for (int l = 0; l < nlevels; l++) btile_off[l + 1] += btile_off[l];
     (void)slot;
     keys_cap = key;
     out_cap = outb;
@@ -2269,9 +2272,17 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
     // (0.143 -> 0.222 ms) and config 5 stayed at 89k frames/s (profiles/r04/fast_early_ab.txt).
     const bool early = batch > kPyrTiledMaxBatch && blur_mode == 0 && !fast_v1 && fast_early &&
                        levels[0].cell_begin == 0 && nlevels > 1;
-    if (blur_mode == 0 || blur_mode == 3 || early) {
+    if (blur_mode == 0 || blur_mode >= 3 || early) {
         const int rc = ensure_side_stream();
         if (rc) return rc;
+    }
+    const bool per_level = blur_mode == 4 && batch > kPyrTiledMaxBatch;
+    if (per_level && (int)ev_lv.size() < nlevels) {
+        for (int l = (int)ev_lv.size(); l < nlevels; l++) {
+            hipEvent_t e = nullptr;
+            ORBMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ev_lv.push_back(e);
+        }
     }
     auto launch_fast = [&](int c0, int c1, hipStream_t s) {
         const dim3 grid((c1 - c0 + kFastCells - 1) / kFastCells, batch), block(64 * kFastCells);
@@ -2310,6 +2321,15 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                                    levels[l - 1], g, d_xtab + g.xtab_off, d_ytab + g.ytab_off, lrow);
             }
             prof_end(l == 0 ? ORBMI_STAGE_PYR_LEVEL0 : ORBMI_STAGE_PYR_RESIZE, ev);
+            if (per_level) {  // ORBMI_BLUR=perlevel: level l's blur as soon as level l is written (A/B)
+                const int n_l = btile_off[l + 1] - btile_off[l];
+                ORBMI_HIP(hipEventRecord(ev_lv[l], stream));
+                ORBMI_HIP(hipStreamWaitEvent(bstream, ev_lv[l], 0));
+                if (n_l > 0)
+                    hipLaunchKernelGGL(k_blur, dim3(xcd_image_grid(n_l, batch)), dim3(256), 0, bstream, d_pyr, d_blur, pimg,
+                                       bimg, d_levels, d_btiles + btile_off[l], batch);
+                if (l == nlevels - 1) ORBMI_HIP(hipEventRecord(ev_blur, bstream));
+            }
         }
     } else {
         hipEvent_t ev = prof_begin(ORBMI_STAGE_PYR_LEVEL0);  // the whole pyramid
@@ -2329,7 +2349,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
         ORBMI_HIP(hipEventRecord(ev_blur, bstream));
         return ORBMI_OK;
     };
-    if (blur_mode == 0) {
+    if (blur_mode == 0 || (blur_mode == 4 && !per_level)) {
         ORBMI_HIP(hipEventRecord(ev_pyr, stream));
         ORBMI_HIP(hipStreamWaitEvent(bstream, ev_pyr, 0));
         hipEvent_t eb = prof_begin(ORBMI_STAGE_BLUR, bstream);
@@ -2360,7 +2380,7 @@ int Extractor::run(const uint8_t* d_images, int batch, size_t step, size_t image
                            d_levels, d_btiles, batch);
         prof_end(ORBMI_STAGE_BLUR, ev);
     }
-    if (blur_mode == 0 || blur_mode == 3) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
+    if (blur_mode == 0 || blur_mode >= 3) ORBMI_HIP(hipStreamWaitEvent(stream, ev_blur, 0));
     ev = prof_begin(ORBMI_STAGE_DESCRIBE);
     if (describe_wave)  // ORBMI_DESC=wave: one keypoint per wave (A/B)
         hipLaunchKernelGGL(k_describe, dim3((out_cap + 3) / 4, batch), dim3(256), 0, stream, d_pyr, d_blur, pimg, bimg,
@@ -2493,6 +2513,8 @@ void Extractor::release() {
     stream = nullptr;
     if (bstream) (void)hipStreamDestroy(bstream);
     bstream = nullptr;
+    for (hipEvent_t e : ev_lv) (void)hipEventDestroy(e);
+    ev_lv.clear();
     if (ev_pyr) (void)hipEventDestroy(ev_pyr);
     if (ev_blur) (void)hipEventDestroy(ev_blur);
     if (ev_l0) (void)hipEventDestroy(ev_l0);
