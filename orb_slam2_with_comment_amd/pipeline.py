@@ -588,9 +588,18 @@ class LocalMapper:
         d_obs, d_off, npts = job.obs
         best = self._buf("best", (max(npts, 1),), torch.int32)
         dsc = self._buf("dsc", (max(npts, 1) * 32,), torch.uint8)
-        check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
-            m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
-        # the later stages' buffers, prepared while the GPU runs the two above
+
+        def distinctive():
+            check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
+                m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
+        # With the transform ahead its sizes are on the host already, so CreateNewMapPoints goes
+        # first and ProcessNewKeyFrame's ComputeDistinctiveDescriptors is enqueued while its kernels
+        # run (the searches read keypoint descriptors, not the map points' distinctive ones, and the
+        # replayed job applies no map update): the host's call setup then leaves no gap on the
+        # stream.  Without it, the two ProcessNewKeyFrame calls go first, as before.
+        if not self._prebow:
+            distinctive()
+        # the later stages' buffers, prepared while the GPU runs the calls above
         nnb = len(job.neighbours)
         tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
         tri_ok = self._buf("tri_ok", (max(nnb, 1) * kf.n,), torch.uint8)
@@ -602,7 +611,8 @@ class LocalMapper:
         kf2 = job.c_kf2
         if bow_ev is not None:  # CreateNewMapPoints reads the FeatureVector
             self._ms.wait_event(bow_ev)
-        mark("bow_distinctive")
+        else:
+            mark("bow_distinctive")
         nw, nn = counts_h.read()  # waits for the size copy only (whatever the stream mode)
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
@@ -614,6 +624,9 @@ class LocalMapper:
                 _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         nt = nnb * kf.n
         mark("create_new_map_points")
+        if self._prebow:
+            distinctive()
+            mark("bow_distinctive")
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
         if nnb:
             check("orbmi_fuse_search_batch", L.orbmi_fuse_search_batch(
