@@ -609,11 +609,13 @@ class LocalMapper:
         bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
-        if bow_ev is not None:  # CreateNewMapPoints reads the FeatureVector
-            self._ms.wait_event(bow_ev)
-        else:
+        if bow_ev is None:
             mark("bow_distinctive")
-        nw, nn = counts_h.read()  # waits for the size copy only (whatever the stream mode)
+        # waits for the size copy only (whatever the stream mode).  With the transform ahead the
+        # copy follows the transform on the vocabulary's stream, so once the host has read the
+        # sizes the FeatureVector is complete too and the mapper's stream needs no cross-stream
+        # wait (a wait packet costs the stream ~10 us)
+        nw, nn = counts_h.read()
         # ---- CreateNewMapPoints: every neighbour's SearchForTriangulation and the triangulation /
         # acceptance geometry on the device, in the reference's pair order (orbmi_create_new_map_points)
         fv1 = FeatureVectorView(nn, b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr())
