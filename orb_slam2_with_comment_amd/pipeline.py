@@ -570,9 +570,8 @@ class LocalMapper:
                 marks.append((name, ev))
         # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
         # ComputeDistinctiveDescriptors of the keyframe's map points
-        bow_ev = None
         if self._prebow:  # issued ahead while the previous keyframe's LocalBA ran, or now
-            slot, bow_ev = job._bow if getattr(job, "_bow", None) is not None else self._issue_bow(job)
+            slot, _ = job._bow if getattr(job, "_bow", None) is not None else self._issue_bow(job)
             job._bow = None
             b, counts_h = self.bows[slot], self._counts_hs[slot]
             self.bow = b
@@ -592,13 +591,10 @@ class LocalMapper:
         def distinctive():
             check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
                 m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
-        # With the transform ahead its sizes are on the host already, so CreateNewMapPoints goes
-        # first and ProcessNewKeyFrame's ComputeDistinctiveDescriptors is enqueued while its kernels
-        # run (the searches read keypoint descriptors, not the map points' distinctive ones, and the
-        # replayed job applies no map update): the host's call setup then leaves no gap on the
-        # stream.  Without it, the two ProcessNewKeyFrame calls go first, as before.
-        if not self._prebow:
-            distinctive()
+        # enqueued first, so the stream is busy while the host prepares CreateNewMapPoints (putting
+        # CreateNewMapPoints first left the stream idle for that setup: 2,836-2,881 against
+        # 2,914-2,949 frames/s, profiles/r06/lm_prebow_ab.txt)
+        distinctive()
         # the later stages' buffers, prepared while the GPU runs the calls above
         nnb = len(job.neighbours)
         tri = self._buf("tri", (max(nnb, 1) * kf.n,), torch.int32)
@@ -609,8 +605,7 @@ class LocalMapper:
         bi = self._buf("fuse_bi", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         bd = self._buf("fuse_bd", (max(nnb * n_kp + n_tp, 1),), torch.int32)
         kf2 = job.c_kf2
-        if bow_ev is None:
-            mark("bow_distinctive")
+        mark("bow_distinctive")
         # waits for the size copy only (whatever the stream mode).  With the transform ahead the
         # copy follows the transform on the vocabulary's stream, so once the host has read the
         # sizes the FeatureVector is complete too and the mapper's stream needs no cross-stream
@@ -626,9 +621,6 @@ class LocalMapper:
                 _vp(tri.data_ptr()), _vp(tri_ok.data_ptr()), _vp(x3d.data_ptr())))
         nt = nnb * kf.n
         mark("create_new_map_points")
-        if self._prebow:
-            distinctive()
-            mark("bow_distinctive")
         # ---- SearchInNeighbors: Fuse(target, keyframe's points) per target, Fuse(keyframe, targets' points)
         if nnb:
             check("orbmi_fuse_search_batch", L.orbmi_fuse_search_batch(
