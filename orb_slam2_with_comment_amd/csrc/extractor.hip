@@ -707,53 +707,6 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         wave_sync_lds_ex();
         return n;
     };
-    // A on pixel pairs (kStrength): lane = (x, x + 1) of one row, the five compass reads of both
-    // as 16-bit halves, the tests as packed u16 min / max / saturating differences (bright:
-    // min(max(a, c), max(b, d)) > v + t; dark: max(min(a, c), min(b, d)) < v - t, the same
-    // predicates as compass()); survivors in row-major order, x before x + 1
-    typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-    auto compass2 = [&](int t) {
-        int n = 0;
-        const int P = (dw + 1) >> 1, units = dh * P;
-        if (units > 0) {
-            int y = lane / P, j = lane - y * P;
-            const int q = 64 / P, r = 64 - q * P;
-            const u16x2_t t2 = {(unsigned short)t, (unsigned short)t};
-            for (int u0 = 0; u0 < units; u0 += 64) {
-                const int x = 2 * j;
-                const int e0 = __umul24(min(y, dh - 1), TS) + x + 3;  // pixel x at (X, Y - 3)
-                const uint8_t* cp = tb + e0;
-                // two bytes per read (ds_read_u16: gfx950's LDS takes unaligned addresses), spread
-                // into the 16-bit halves by one v_perm
-                auto pair = [&](int off) {
-                    unsigned short w;
-                    __builtin_memcpy(&w, cp + off, 2);
-                    return __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(0u, (unsigned)w, 0x0c010c00u));
-                };
-                const u16x2_t c2 = pair(0), d2 = pair(3 * TS - 3), v2 = pair(3 * TS), b2 = pair(3 * TS + 3),
-                              a2 = pair(6 * TS);
-                const u16x2_t hi = v2 + t2, lo = __builtin_elementwise_sub_sat(v2, t2);
-                const u16x2_t br = __builtin_elementwise_min(__builtin_elementwise_max(a2, c2),
-                                                             __builtin_elementwise_max(b2, d2));
-                const u16x2_t dk = __builtin_elementwise_max(__builtin_elementwise_min(a2, c2),
-                                                             __builtin_elementwise_min(b2, d2));
-                const u16x2_t pb = __builtin_elementwise_sub_sat(br, hi), pd = __builtin_elementwise_sub_sat(lo, dk);
-                const unsigned rr = __builtin_bit_cast(unsigned, pb) | __builtin_bit_cast(unsigned, pd);
-                const bool ok = u0 + lane < units;
-                const bool p0 = (rr & 0xFFFFu) != 0 && ok, p1 = (rr >> 16) != 0 && ok && x + 1 < dw;
-                const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1);
-                const int pos = n + lanes_below(m0) + lanes_below(m1);
-                if (p0) L[pos] = (unsigned short)(e0 + 3 * TS);
-                if (p1) L[pos + p0] = (unsigned short)(e0 + 3 * TS + 1);
-                n += __popcll(m0) + __popcll(m1);
-                j += r;
-                y += q;
-                if (j >= P) { j -= P; y++; }
-            }
-        }
-        wave_sync_lds_ex();
-        return n;
-    };
     auto nms = [&](unsigned short* Ls, int ns, int t) {
         int kept = 0;
         for (int i0 = 0; i0 < ns; i0 += 64) {
@@ -804,10 +757,10 @@ __global__ __launch_bounds__(64 * kFastCells) void k_fast2(const uint8_t* __rest
         // scores it rewrites are the same values).  With min_th >= ini_th one pass at ini_th
         // holds the corners of both.
         const bool two = tm < ti;
-        int nc = strength(compass2(two ? ti : tl), two ? ti : tl);
+        int nc = strength(compass(two ? ti : tl), two ? ti : tl);
         total = nms(L, nc, ti);
         if (total == 0 && tm != ti) {
-            if (two) nc = strength(compass2(tm), tm);
+            if (two) nc = strength(compass(tm), tm);
             total = nms(L, nc, tm);
         }
     } else {
