@@ -14,7 +14,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_local_mapping_chain_matches_oracle(oracle):
+@pytest.mark.parametrize("prebow", [True, False])  # ComputeBoW ahead on the vocabulary's stream, or in the chain
+def test_local_mapping_chain_matches_oracle(oracle, prebow):
     import bench
     from orb_slam2_with_comment_amd import synth_map as SM
     from orb_slam2_with_comment_amd._capi import check, lib
@@ -25,7 +26,7 @@ def test_local_mapping_chain_matches_oracle(oracle):
     voc = ORBVocabulary(vocab, device=0)
     problem, _ = SM.local_ba_problem(seed=3, n_free=6, n_fixed=2, n_points=300)
     jobs, keep = bench.setup_local_mapping(S, voc, vocab, 0, problem)
-    mapper = LocalMapper(0, vocabulary=voc)
+    mapper = LocalMapper(0, vocabulary=voc, prebow=prebow)
     try:
         for f in (3, 5):
             job = jobs[f]
