@@ -570,20 +570,11 @@ class LocalMapper:
                 marks.append((name, ev))
         # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
         # ComputeDistinctiveDescriptors of the keyframe's map points
-        if self._prebow:  # issued ahead while the previous keyframe ran, or now
+        if self._prebow:  # issued ahead while the previous keyframe's LocalBA ran, or now
             slot, _ = job._bow if getattr(job, "_bow", None) is not None else self._issue_bow(job)
             job._bow = None
             b, counts_h = self.bows[slot], self._counts_hs[slot]
             self.bow = b
-            # the next queued keyframe's ComputeBoW, into the other set (its previous keyframe is
-            # complete: the LocalBA that ended it was waited for), beside this keyframe's chain --
-            # issued now, so that the host's work just before LocalBA (its graph indexing, which
-            # overlaps the searches still running) stays short
-            with self.q.mutex:
-                nxt = self.q.queue[0] if self.q.queue else None
-            if isinstance(nxt, LocalMappingJob) and nxt is not job and getattr(nxt, "_bow", None) is None:
-                self._issue_bow(nxt)
-                self.bow_ahead += 1
         else:  # enqueued back to back with ComputeDistinctiveDescriptors
             b, counts_h = self.bow, self._counts_h
             self.voc.transform_device(job.d_desc, kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
@@ -643,6 +634,13 @@ class LocalMapper:
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
         mark("distinctive")
+        # the next queued keyframe's ComputeBoW, beside this LocalBA
+        if self._prebow:
+            with self.q.mutex:
+                nxt = self.q.queue[0] if self.q.queue else None
+            if isinstance(nxt, LocalMappingJob) and getattr(nxt, "_bow", None) is None:
+                self._issue_bow(nxt)
+                self.bow_ahead += 1
         # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
         ms = self._ms
