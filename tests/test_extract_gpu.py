@@ -334,3 +334,32 @@ def test_batch_ab_knobs_equal_default(orb, knob, monkeypatch):
     for i in range(len(imgs)):
         np.testing.assert_array_equal(k1[i, :n0[i]], k0[i, :n0[i]])
         np.testing.assert_array_equal(d1[i, :n0[i]], d0[i, :n0[i]])
+
+
+def test_batch_host_images_levelwise(orb, oracle, images):
+    """orbmi_extract_batch_host at a batch of 10 (the level-by-level pyramid of large batches) from
+    pageable host memory: every frame equals the oracle."""
+    import ctypes as C
+    import torch
+    from orb_slam2_with_comment_amd import _capi
+    p = oracle.params(2000)
+    ex = _extractor(orb, p)
+    names = ["kitti_L0", "kitti_R0", "kitti_L11", "kitti_R11"]
+    imgs = np.stack([images[names[i % 4]] for i in range(10)])
+    B, r, c = imgs.shape
+    cap = 2100
+    d_k = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    d_d = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    _capi.check("batch_host", _capi.lib().orbmi_extract_batch_host(
+        ex.handle, C.c_void_p(imgs.ctypes.data), B, r, c, r * c, C.c_void_p(d_k.data_ptr()),
+        C.c_void_p(d_d.data_ptr()), C.c_void_p(d_n.data_ptr()), cap))
+    _capi.check("sync", _capi.lib().orbmi_extractor_synchronize(ex.handle))
+    counts, kk, dd = d_n.cpu().numpy(), d_k.cpu().numpy(), d_d.cpu().numpy()
+    for i in range(4):  # the four distinct images (the rest repeat them)
+        k_ref, d_ref = oracle.extract(p, imgs[i])
+        for j in range(i, B, 4):
+            assert counts[j] == len(k_ref)
+            np.testing.assert_array_equal(kk[j, :counts[j]].view(_capi.KP_DTYPE).reshape(-1), k_ref)
+            np.testing.assert_array_equal(dd[j, :counts[j]], d_ref)
