@@ -446,6 +446,12 @@ int orbmi_ba_set_stream(orbmi_ba* b, void* stream);
  * A flag raised by another thread is first seen at one of these checks, so a call with
  * k = result.stop_check of a concurrent run repeats that run exactly. */
 int orbmi_ba_set_stop_at_check(orbmi_ba* b, int k);
+/* Host hook (no counterpart in the reference): in every later call on the handle, fn(arg) runs
+ * on the calling thread once the LocalBA's work has been enqueued and before the call waits for
+ * it, so a caller can enqueue independent work of its own (e.g. the next keyframe's
+ * ComputeBoW on another stream) beside the solve.  fn must not call back into this handle.
+ * fn = NULL removes it. */
+int orbmi_ba_set_enqueued_hook(orbmi_ba* b, void (*fn)(void*), void* arg);
 
 /* Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (include/Optimizer.h:62,
  * src/Optimizer.cc:483-808) on the assembled graph: LM (g2o OptimizationAlgorithmLevenberg,

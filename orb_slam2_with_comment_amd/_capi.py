@@ -111,6 +111,7 @@ _PROTOS = {
     "orbmi_stereo_parallax_cos": (_i, [C.c_float, _vp, _i, _vp]),
     "orbmi_ba_set_stream": (_i, [_vp, _vp]),
     "orbmi_ba_set_stop_at_check": (_i, [_vp, _i]),
+    "orbmi_ba_set_enqueued_hook": (_i, [_vp, _vp, _vp]),
     "orbmi_debug_ba_schur_blocks": (_i, [_i, _vp, _i, _vp]),
     "orbmi_vocabulary_set_stream": (_i, [_vp, _vp]),
     "orbmi_fuse_search_refresh": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, C.c_float, _vp, _vp]),

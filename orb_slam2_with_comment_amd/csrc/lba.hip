@@ -2547,6 +2547,8 @@ struct orbmi_ba {
     int* h_stop = nullptr;          // host-mapped mirror of the caller's stop flag
     int* d_stop = nullptr;          //   (its device address)
     int stop_at = -1;               // orbmi_ba_set_stop_at_check
+    void (*enqueued)(void*) = nullptr;  // orbmi_ba_set_enqueued_hook
+    void* enqueued_arg = nullptr;
 };
 
 namespace {
@@ -2783,6 +2785,13 @@ int orbmi_debug_ba_schur_blocks(int nf, int* table, int cap, int* n_out) {
 int orbmi_ba_set_stop_at_check(orbmi_ba* b, int k) {
     if (!b) return ORBMI_E_ARG;
     b->stop_at = k < 0 ? -1 : k;
+    return ORBMI_OK;
+}
+
+int orbmi_ba_set_enqueued_hook(orbmi_ba* b, void (*fn)(void*), void* arg) {
+    if (!b) return ORBMI_E_ARG;
+    b->enqueued = fn;
+    b->enqueued_arg = arg;
     return ORBMI_OK;
 }
 
@@ -3034,6 +3043,7 @@ int orbmi_local_bundle_adjustment(orbmi_ba* b, const orbmi_ba_problem* P, orbmi_
     for (;;) {
         ORBMI_HIP(enqueue(from, more));
         ORBMI_HIP(hipGetLastError());
+        if (from == 0 && h.enqueued) h.enqueued(h.enqueued_arg);  // the caller's work beside the solve
         if ((rc = r.read_ctl())) return rc;
         const BaCtl& c = *h.h_ctl;
         if (c.unsupported) return ORBMI_E_UNSUPPORTED;

@@ -494,10 +494,19 @@ class LocalMapper:
             if vocabulary is not None and not self._prebow:
                 check("orbmi_vocabulary_set_stream", lib().orbmi_vocabulary_set_stream(vocabulary._h, ms))
         self._vs = None
+        self._hook_cb = None
+        self._job_start_ev = None
+        self._cur_job = None
         if self._prebow:
             vs = _vp()
             check("orbmi_vocabulary_get_stream", lib().orbmi_vocabulary_get_stream(vocabulary._h, C.byref(vs)))
             self._vs = torch.cuda.ExternalStream(vs.value, device=dev)
+            # the next keyframe's transform is issued from LocalBA's enqueued hook: after the solve's
+            # work is on the stream and before the host waits for it, so the host's issue time is
+            # off the chain and the transform runs beside the one-workgroup solve
+            self._hook_cb = C.CFUNCTYPE(None, C.c_void_p)(self._on_ba_enqueued)
+            check("orbmi_ba_set_enqueued_hook", lib().orbmi_ba_set_enqueued_hook(
+                self.ba._h, C.cast(self._hook_cb, C.c_void_p), None))
         self.q: queue.Queue = queue.Queue()
         self.job_events = None  # a list: per job (start event, end event, host start, host end)
         self.done = 0
@@ -571,6 +580,9 @@ class LocalMapper:
         # ---- ProcessNewKeyFrame: ComputeBoW (transform of the keyframe's descriptors) and the
         # ComputeDistinctiveDescriptors of the keyframe's map points
         if self._prebow:  # issued ahead while the previous keyframe's LocalBA ran, or now
+            self._job_start_ev = torch.cuda.Event()
+            self._job_start_ev.record(self._ms)  # the previous keyframes' work: a free set's last reader
+            self._cur_job = job
             slot, _ = job._bow if getattr(job, "_bow", None) is not None else self._issue_bow(job)
             job._bow = None
             b, counts_h = self.bows[slot], self._counts_hs[slot]
@@ -634,13 +646,7 @@ class LocalMapper:
         check("orbmi_compute_distinctive_descriptors", L.orbmi_compute_distinctive_descriptors(
             m, _vp(d_obs), _vp(d_off), int(npts), _vp(best.data_ptr()), _vp(dsc.data_ptr())))
         mark("distinctive")
-        # the next queued keyframe's ComputeBoW, beside this LocalBA
-        if self._prebow:
-            with self.q.mutex:
-                nxt = self.q.queue[0] if self.q.queue else None
-            if isinstance(nxt, LocalMappingJob) and getattr(nxt, "_bow", None) is None:
-                self._issue_bow(nxt)
-                self.bow_ahead += 1
+        # (the next queued keyframe's ComputeBoW: _on_ba_enqueued, from inside this call)
         # ---- LocalBundleAdjustment (same stream, so it runs behind the searches above)
         self.last = self.ba.run(job.problem)
         ms = self._ms
@@ -664,19 +670,31 @@ class LocalMapper:
                                                            b["feat"][:kf.n].cpu().numpy()))
         return out
 
-    def _issue_bow(self, job):
+    def _on_ba_enqueued(self, _arg):
+        """LocalBA's enqueued hook (orbmi_ba_set_enqueued_hook): the next queued keyframe's
+        ComputeBoW, beside the solve.  Never raises into the C caller (errors surface in wait())."""
+        try:
+            with self.q.mutex:
+                nxt = self.q.queue[0] if self.q.queue else None
+            if isinstance(nxt, LocalMappingJob) and nxt is not self._cur_job and getattr(nxt, "_bow", None) is None:
+                self._issue_bow(nxt, after=self._job_start_ev)
+                self.bow_ahead += 1
+        except Exception as e:  # pragma: no cover
+            self.error = e
+
+    def _issue_bow(self, job, after=None):
         """ComputeBoW of job's keyframe on the vocabulary's stream into the next BowVector /
-        FeatureVector set (the other one belongs to the keyframe in flight, whose searches have
-        been enqueued before this call), its sizes to that set's pinned words; -> (set, event)."""
+        FeatureVector set (the other one belongs to the keyframe in flight), its sizes to that
+        set's pinned words; -> (set, event).  The transform waits for `after` (an event on the
+        mapper's stream behind the set's previous reader), else for everything enqueued there."""
         import torch
         slot = self._slot
         self._slot = (slot + 1) % len(self.bows)
         b = self.bows[slot]
-        # behind everything enqueued on the mapper's stream so far: the set's previous keyframe
-        # read its FeatureVector there
-        ms_ev = torch.cuda.Event()
-        ms_ev.record(self._ms)
-        self._vs.wait_event(ms_ev)
+        if after is None:  # behind everything enqueued on the mapper's stream so far
+            after = torch.cuda.Event()
+            after.record(self._ms)
+        self._vs.wait_event(after)
         self.voc.transform_device(job.d_desc, job.kf.n, None, 4, b["word"].data_ptr(), b["value"].data_ptr(),
                                   b["node"].data_ptr(), b["off"].data_ptr(), b["feat"].data_ptr(), b["counts"].data_ptr())
         self._counts_hs[slot].copy_async(b["counts"].data_ptr(), self._vs.cuda_stream)
@@ -718,6 +736,8 @@ class LocalMapper:
             self.last_chain.materialize()  # its closure synchronises self._ms
         self._out = None
         self._bufs = {}
+        if getattr(self, "_hook_cb", None) is not None and getattr(self.ba, "_h", None):
+            check("orbmi_ba_set_enqueued_hook", lib().orbmi_ba_set_enqueued_hook(self.ba._h, None, None))
         if self._vs is not None:
             self._vs.synchronize()
         for c in self._counts_hs:
