@@ -29,6 +29,7 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -206,6 +207,11 @@ struct MapPoint {
     int replaced = -1;           // mpReplaced
     int fuse_candidate_for_kf = -1;
 };
+// The mapping thread's device calls read keyframes' FeatureVectors through host pointers with the
+// map lock released, while Tracking may append to `kfs`: a reallocation must move the elements
+// (their heap arrays stay put), never copy and free them.
+static_assert(std::is_nothrow_move_constructible<KeyFrame>::value, "kfs growth would copy keyframes");
+static_assert(std::is_nothrow_move_constructible<FeatVec>::value, "FeatVec growth would copy");
 
 struct TrackedFrame {
     int id = 0;

@@ -1,9 +1,10 @@
 """Hunt for a concurrent-schedule replay mismatch (tests/test_native_slam_gpu.py::
 test_concurrent_schedule_replays_on_oracle) and localise it.
 
-    python tools/replay_hunt.py [runs] [period]
+    python tools/replay_hunt.py [runs] [period[,period...]]
 
-Records up to `runs` concurrent native runs (200 frames, frames `period` s apart) and replays
+Records up to `runs` concurrent native runs (200 frames, frames `period` s apart, the periods
+taken in turn when several are given) and replays
 each on the CPU oracle (system.StereoSLAM.replay_schedule with the per-keyframe state record).
 At the first mismatch it replays the same record with the GPU operators behind the same Python
 host logic (GpuBackend: the GPU searches, the host triangulation): if that replay agrees with the
@@ -38,13 +39,14 @@ def drive(slam, frames, period):
 
 def main():
     runs = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    period = float(sys.argv[2]) if len(sys.argv) > 2 else 0.003
+    periods = [float(p) for p in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0.003]
     frames = render_sequence(200)
     voc = small_vocabulary()
     tmp = tempfile.mkdtemp()
     s = sequence_settings(__import__("pathlib").Path(tmp))
     replay_frames = [(L, R, 0.1 * f) for f, (L, R, _) in enumerate(frames)]
     for run in range(runs):
+        period = periods[run % len(periods)]
         slam = NativeStereoSLAM(s, device=0, vocabulary=voc, async_local_mapping=True, record=True)
         drive(slam, frames, period)
         slam.WaitLocalMapping()
@@ -54,10 +56,10 @@ def main():
         ref = StereoSLAM(s, backend=OracleBackend(s, voc))
         try:
             ref.replay_schedule(replay_frames, rec["schedule"], rec["ba_log"], rec["kf_state"])
-            print(f"run {run}: replay exact ({len(rec['schedule'])} events, {counts})", flush=True)
+            print(f"run {run} (period {period}): replay exact ({len(rec['schedule'])} events, {counts})", flush=True)
             continue
         except ScheduleMismatch as e:
-            print(f"run {run}: ORACLE replay mismatch: {e}", flush=True)
+            print(f"run {run} (period {period}): ORACLE replay mismatch: {e}", flush=True)
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         np.savez(os.path.join(ROOT, "gpurun_out", "replay_hunt.npz"), schedule=rec["schedule"], ba_log=rec["ba_log"],
                  kf_state=rec["kf_state"], period=period)
