@@ -1,7 +1,7 @@
 """Hunt for a concurrent-schedule replay mismatch (tests/test_native_slam_gpu.py::
 test_concurrent_schedule_replays_on_oracle) and localise it.
 
-    python tools/replay_hunt.py [runs] [period[,period...]]
+    python tools/replay_hunt.py [runs] [period[,period...]] [both]
 
 Records up to `runs` concurrent native runs (200 frames, frames `period` s apart, the periods
 taken in turn when several are given) and replays
@@ -10,7 +10,8 @@ At the first mismatch it replays the same record with the GPU operators behind t
 host logic (GpuBackend: the GPU searches, the host triangulation): if that replay agrees with the
 native record where the oracle's did not, the oracle and the GPU operators disagree on that input;
 if it stops at the same place with the oracle's values, the native run's device call (or its
-inputs) differs.  The record goes to gpurun_out/replay_hunt.npz."""
+inputs) differs.  The record goes to gpurun_out/replay_hunt.npz.  `both`: every run is also replayed with the GPU
+operators (which must then be exact too), to exercise that path without waiting for a mismatch."""
 import os
 import sys
 import tempfile
@@ -40,6 +41,7 @@ def drive(slam, frames, period):
 def main():
     runs = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     periods = [float(p) for p in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0.003]
+    both = len(sys.argv) > 3 and sys.argv[3] == "both"
     frames = render_sequence(200)
     voc = small_vocabulary()
     tmp = tempfile.mkdtemp()
@@ -57,6 +59,18 @@ def main():
         try:
             ref.replay_schedule(replay_frames, rec["schedule"], rec["ba_log"], rec["kf_state"])
             print(f"run {run} (period {period}): replay exact ({len(rec['schedule'])} events, {counts})", flush=True)
+            if both:
+                gpu = StereoSLAM(s, device=0, vocabulary=voc)
+                try:
+                    gpu.replay_schedule(replay_frames, rec["schedule"], rec["ba_log"], rec["kf_state"])
+                    d = float(np.abs(gpu.trajectory_twc() - ref.trajectory_twc()).max())
+                    print(f"  GPU-operator replay: exact; its trajectory vs the oracle replay's: max |d| {d:.3g}",
+                          flush=True)
+                except ScheduleMismatch as e:
+                    print(f"  GPU-operator replay mismatch: {e}", flush=True)
+                    return 1
+                finally:
+                    gpu.backend.close()
             continue
         except ScheduleMismatch as e:
             print(f"run {run} (period {period}): ORACLE replay mismatch: {e}", flush=True)
