@@ -181,6 +181,15 @@ int orbmi_matcher_reserve_cus(orbmi_matcher* m, int n);
  * re-pins whenever the keypoints behind the pointers change (a new frame in the same buffers). */
 int orbmi_matcher_assign_features_to_grid(orbmi_matcher* m, const orbmi_frame_view* F);
 int orbmi_matcher_release_grid(orbmi_matcher* m);
+/* The same grid built ahead, on another stream: Frame::AssignFeaturesToGrid of F (device arrays
+ * only) into the handle's slot grid `slot` (0..3) on `stream` (hipStream_t; NULL = the handle's),
+ * e.g. the extraction stream right after the Frame's keypoints, so the build leaves the tracking
+ * chain.  The caller orders the searches that read the slot behind `stream` (an event), and the
+ * next build of the slot behind those searches.  orbmi_matcher_pin_grid_slot then makes the
+ * searches on F read that grid, pinned as above; ORBMI_E_STATE if the slot was built for another
+ * frame (keys / n / n_device / image bounds). */
+int orbmi_matcher_build_grid_slot(orbmi_matcher* m, const orbmi_frame_view* F, int slot, void* stream);
+int orbmi_matcher_pin_grid_slot(orbmi_matcher* m, const orbmi_frame_view* F, int slot);
 
 /* Frame::isInFrustum(pMP, viewingCosLimit) for n_mp points (src/Frame.cc:274-342) with
  * MapPoint::PredictScale (src/MapPoint.cc:421-436).  Points flagged BAD or SEEN are skipped

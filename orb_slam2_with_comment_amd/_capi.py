@@ -65,6 +65,8 @@ _PROTOS = {
     "orbmi_matcher_reserve_cus": (_i, [_vp, _i]),
     "orbmi_matcher_assign_features_to_grid": (_i, [_vp, _vp]),
     "orbmi_matcher_release_grid": (_i, [_vp]),
+    "orbmi_matcher_build_grid_slot": (_i, [_vp, _vp, _i, _vp]),
+    "orbmi_matcher_pin_grid_slot": (_i, [_vp, _vp, _i]),
     "orbmi_match_descriptors_segments": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _i, _i, _f, _vp, _vp]),
     "orbmi_extractor_get_stream": (_i, [_vp, C.POINTER(_vp)]),
     "orbmi_is_in_frustum": (_i, [_vp, _vp, _vp, _i, _f, _vp]),

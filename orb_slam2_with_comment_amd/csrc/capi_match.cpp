@@ -117,6 +117,12 @@ void Matcher::release() {
                     d_res, d_bin_of, d_hist, d_scalars, d_track};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (GridSlot& g : gslot) {
+        if (g.cs) (void)hipFree(g.cs);
+        if (g.cl) (void)hipFree(g.cl);
+        if (g.kc) (void)hipFree(g.kc);
+        g = GridSlot{};
+    }
     for (Gen& g : gens) {
         for (Block& b : g.blocks) {
             (void)hipFree(b.p);
@@ -317,6 +323,32 @@ int orbmi_matcher_assign_features_to_grid(orbmi_matcher* h, const orbmi_frame_vi
     if ((rc = orbmi::pin_grid(m, F))) return rc;
     ORBMI_HIP(hipGetLastError());
     return ORBMI_OK;
+}
+
+int orbmi_matcher_build_grid_slot(orbmi_matcher* h, const orbmi_frame_view* v, int slot, void* stream) {
+    if (!h || !v || slot < 0 || slot >= orbmi::Matcher::kGridSlots || (v->n > 0 && !on_device(v->keys_un)) ||
+        (v->n > 0 && !on_device(v->desc)) || (v->u_right && !on_device(v->u_right)))
+        return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, false))) return rc;  // device arrays: nothing staged
+    hipStream_t s = stream ? (hipStream_t)stream : m.ls();
+    if ((rc = orbmi::build_grid_slot(m, F, slot, s))) return rc;
+    ORBMI_HIP(hipGetLastError());
+    return ORBMI_OK;
+}
+
+int orbmi_matcher_pin_grid_slot(orbmi_matcher* h, const orbmi_frame_view* v, int slot) {
+    if (!h || !v || slot < 0 || slot >= orbmi::Matcher::kGridSlots || (v->n > 0 && !on_device(v->keys_un)))
+        return ORBMI_E_ARG;
+    Matcher& m = h->m;
+    ORBMI_HIP(hipSetDevice(m.device));
+    DevFrame F;
+    int rc;
+    if ((rc = make_frame(m, v, &F, false))) return rc;
+    return orbmi::pin_grid_slot(m, F, slot);
 }
 
 int orbmi_matcher_release_grid(orbmi_matcher* h) {

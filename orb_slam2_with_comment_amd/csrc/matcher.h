@@ -92,6 +92,24 @@ struct Matcher {
     const int* pin_ndev = nullptr;
     int pin_n = 0;
     float pin_geom[6] = {};
+    // the grid the searches read: the one built above, or a slot grid pinned by
+    // orbmi_matcher_pin_grid_slot
+    const int* cur_cs = nullptr;
+    const int* cur_cl = nullptr;
+    // slot grids (orbmi_matcher_build_grid_slot): built on another stream (the extraction's)
+    // ahead of the searches; each remembers the frame it was built for
+    static constexpr int kGridSlots = 4;
+    struct GridSlot {
+        int* cs = nullptr;
+        int* cl = nullptr;
+        int* kc = nullptr;
+        size_t cap = 0;
+        bool built = false;
+        const orbmi_keypoint* keys = nullptr;
+        const int* ndev = nullptr;
+        int n = 0;
+        float geom[6] = {};
+    } gslot[kGridSlots];
     // candidates / greedy
     unsigned long long* d_cand = nullptr; size_t cap_cand = 0;
     int* d_ncand = nullptr; size_t cap_ncand = 0;
@@ -137,6 +155,8 @@ struct Matcher {
 };
 
 int pin_grid(Matcher& m, const DevFrame& F);
+int build_grid_slot(Matcher& m, const DevFrame& F, int k, hipStream_t s);
+int pin_grid_slot(Matcher& m, const DevFrame& F, int k);
 int launch_frustum(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, int n, float cosl,
                    orbmi_mappoint_track* tr, int* n_in_view);
 int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, const orbmi_mappoint* mps,

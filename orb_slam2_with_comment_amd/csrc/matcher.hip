@@ -1176,19 +1176,63 @@ static int grid_for(Matcher& m, const DevFrame& F, const int* gate = nullptr, in
     if ((rc = ensure_buf(&m.d_kp_cell, &m.cap_kp_cell, (size_t)std::max(F.n, 1)))) return rc;
     hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, m.ls(), F, m.d_cell_start, m.d_cell_list, m.d_kp_cell,
                        gate, gate_min);
+    m.cur_cs = m.d_cell_start;
+    m.cur_cl = m.d_cell_list;
     return ORBMI_OK;
 }
 
-int pin_grid(Matcher& m, const DevFrame& F) {
-    m.grid_pinned = false;
-    int rc;
-    if ((rc = grid_for(m, F))) return rc;
+static void pin_key(Matcher& m, const DevFrame& F) {
     m.grid_pinned = true;
     m.pin_keys = F.keys;
     m.pin_ndev = F.n_dev;
     m.pin_n = F.n;
     const float g[6] = {F.min_x, F.max_x, F.min_y, F.max_y, F.grid_w_inv, F.grid_h_inv};
     memcpy(m.pin_geom, g, sizeof(g));
+}
+
+int pin_grid(Matcher& m, const DevFrame& F) {
+    m.grid_pinned = false;
+    int rc;
+    if ((rc = grid_for(m, F))) return rc;
+    pin_key(m, F);
+    return ORBMI_OK;
+}
+
+// Frame::AssignFeaturesToGrid into slot grid k on stream s (the caller orders the searches that
+// read it behind s, and the next build of slot k behind those searches)
+int build_grid_slot(Matcher& m, const DevFrame& F, int k, hipStream_t s) {
+    if (F.n > kGreedyMaxKp) return ORBMI_E_UNSUPPORTED;
+    Matcher::GridSlot& g = m.gslot[k];
+    const size_t need = (size_t)std::max(F.n, 1);
+    if (!g.cs) ORBMI_HIP(hipMalloc((void**)&g.cs, ((size_t)kGridCells + 1) * sizeof(int)));
+    if (need > g.cap) {
+        if (g.cl) (void)hipFree(g.cl);
+        if (g.kc) (void)hipFree(g.kc);
+        g.cl = g.kc = nullptr;
+        g.cap = 0;
+        ORBMI_HIP(hipMalloc((void**)&g.cl, need * sizeof(int)));
+        ORBMI_HIP(hipMalloc((void**)&g.kc, need * sizeof(int)));
+        g.cap = need;
+    }
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, s, F, g.cs, g.cl, g.kc, (const int*)nullptr, 0);
+    g.built = true;
+    g.keys = F.keys;
+    g.ndev = F.n_dev;
+    g.n = F.n;
+    const float geom[6] = {F.min_x, F.max_x, F.min_y, F.max_y, F.grid_w_inv, F.grid_h_inv};
+    memcpy(g.geom, geom, sizeof(geom));
+    return ORBMI_OK;
+}
+
+// the searches on frame F read slot grid k from now on (it must have been built for F)
+int pin_grid_slot(Matcher& m, const DevFrame& F, int k) {
+    const Matcher::GridSlot& g = m.gslot[k];
+    const float geom[6] = {F.min_x, F.max_x, F.min_y, F.max_y, F.grid_w_inv, F.grid_h_inv};
+    if (!g.built || g.keys != F.keys || g.ndev != F.n_dev || g.n != F.n || memcmp(g.geom, geom, sizeof(geom)) != 0)
+        return ORBMI_E_STATE;
+    pin_key(m, F);
+    m.cur_cs = g.cs;
+    m.cur_cl = g.cl;
     return ORBMI_OK;
 }
 
@@ -1211,13 +1255,13 @@ int launch_local_search(Matcher& m, const DevFrame& F, const uint8_t* occ0, cons
     if ((rc = ensure_buf(&m.d_top, &m.cap_top, (size_t)std::max(n, 1) * kTopK))) return rc;
     if (n > 0) {
         CandArgs ca{};
-        ca.mode = 0; ca.nq = n; ca.F = F; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.mps = mps; ca.tr = tr;
+        ca.mode = 0; ca.nq = n; ca.F = F; ca.cs = m.cur_cs; ca.cl = m.cur_cl; ca.mps = mps; ca.tr = tr;
         ca.th = th; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
         hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.ls(), ca);
     }
     GreedyArgs a{};
     a.mode = 0; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = F;
-    a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
+    a.cs = m.cur_cs; a.cl = m.cur_cl; a.mps = mps; a.tr = tr; a.th = th; a.nnratio = nnratio;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches;
     hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.ls(), a);
     return ORBMI_OK;
@@ -1236,7 +1280,7 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
     if ((rc = ensure_buf(&m.d_top, &m.cap_top, (size_t)std::max(n, 1) * kTopK))) return rc;
     if (n > 0) {
         CandArgs ca{};
-        ca.mode = 1; ca.nq = n; ca.F = CF; ca.LF = LF; ca.cs = m.d_cell_start; ca.cl = m.d_cell_list; ca.lfp = lfp;
+        ca.mode = 1; ca.nq = n; ca.F = CF; ca.LF = LF; ca.cs = m.cur_cs; ca.cl = m.cur_cl; ca.lfp = lfp;
         ca.th = th; ca.mono = mono; ca.cand = m.d_cand; ca.ncand = m.d_ncand; ca.top = m.d_top;
         ca.gate = gate; ca.gate_min = gate_min;
         hipLaunchKernelGGL(k_candidates<16>, dim3((n + 15) / 16), dim3(256), 0, m.ls(), ca);
@@ -1244,7 +1288,7 @@ int launch_lastframe_search(Matcher& m, const DevFrame& CF, const uint8_t* occ0,
     GreedyArgs a{};
     a.mode = 1; a.nq = n; a.cand = m.d_cand; a.ncand = m.d_ncand; a.top = m.d_top; a.cap = cap; a.occ0 = occ0; a.F = CF;
     a.LF = LF;
-    a.cs = m.d_cell_start; a.cl = m.d_cell_list; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
+    a.cs = m.cur_cs; a.cl = m.cur_cl; a.lfp = lfp; a.th = th; a.mono = mono; a.check_ori = check_ori;
     a.res = m.d_res; a.out = out; a.nmatches = nmatches; a.gate = gate; a.gate_min = gate_min;
     hipLaunchKernelGGL(k_greedy, dim3(1), dim3(kGreedyThreads), 0, m.ls(), a);
     return ORBMI_OK;
@@ -1782,7 +1826,7 @@ int launch_fuse(Matcher& m, const DevFrame& F, const orbmi_mappoint* mps, const 
     int rc;
     if ((rc = grid_for(m, F))) return rc;
     if (n > 0)
-        hipLaunchKernelGGL(k_fuse, dim3((n * kFuseLanes + 255) / 256), dim3(256), 0, m.ls(), F, m.d_cell_start, m.d_cell_list,
+        hipLaunchKernelGGL(k_fuse, dim3((n * kFuseLanes + 255) / 256), dim3(256), 0, m.ls(), F, m.cur_cs, m.cur_cl,
                            mps, in_kf, n, th, best_idx, best_dist, ncand);
     return hipGetLastError() == hipSuccess ? ORBMI_OK : ORBMI_E_HIP;
 }

@@ -82,6 +82,13 @@ class StereoTracker:
         from .types import POSE_FRAME_DTYPE
         self.cam, self.device, self.pipelined = cam, device, pipelined
         self.unfused = os.environ.get("ORBMI_TRACK_UNFUSED") == "1"  # A/B: pose and update as two launches
+        # ORBMI_GRID_AHEAD=1 (pipelined): Frame::AssignFeaturesToGrid on the extraction stream
+        # right after the frame's keypoints (a slot grid per frame slot), off the tracking chain.
+        # Tracking alone gains 3.5 % (0.319 -> 0.308 ms per frame back to back), but the headline
+        # with the concurrent LocalMapping chain loses 2.7 % (profiles/r06/grid_ahead_ab.txt), so
+        # the default builds the grid on the tracking stream at the first search
+        self.grid_ahead = pipelined and os.environ.get("ORBMI_GRID_AHEAD", "0") == "1"
+        self._tcw0 = np.eye(4, dtype=np.float32)  # (the grid reads no pose)
         self.frame_events = None  # a list: per-frame [extract start, end, track start, end] events (pipelined)
         self.extractor = ORBextractor(nfeatures, scale_factor, nlevels, ini_th, min_th, device=device)
         self.matcher = ORBmatcher(device=device)
@@ -173,6 +180,14 @@ class StereoTracker:
             self.extractor.handle, self.cam.bf, self.cam.fx, _vp(sl["u_right"].data_ptr()), _vp(sl["depth"].data_ptr())))
         # new keypoints behind the slot's pointers: a grid pinned on an earlier frame is stale
         check("orbmi_matcher_release_grid", L.orbmi_matcher_release_grid(self.matcher._h))
+        if self.grid_ahead and slot is not None:
+            # the slot's grid, in stream order behind its keypoints; the searches read it behind the
+            # extraction event, and the slot's next extraction waits for them (_ev_tracked)
+            v = frame_view(self.cap, sl["kps"].data_ptr(), sl["u_right"].data_ptr(), sl["desc"].data_ptr(), self._tcw0,
+                           self.cam, self.scale_factors, self.cam.width, self.cam.height,
+                           n_device=sl["counts"].data_ptr())
+            check("orbmi_matcher_build_grid_slot", L.orbmi_matcher_build_grid_slot(
+                self.matcher._h, C.addressof(v), int(slot), _vp(self.stream_handle)))
 
     def search_last_frame(self, tcw, last_view, last_points, th=7.0):
         """ORBmatcher(0.9, true).SearchByProjection(mCurrentFrame, mLastFrame, th, !stereo)
@@ -197,9 +212,13 @@ class StereoTracker:
         L = lib()
         cv = self.current_view(tcw)
         # Frame::AssignFeaturesToGrid once per frame: both last-frame searches and the
-        # local-map search reuse this grid
-        check("orbmi_matcher_assign_features_to_grid",
-              L.orbmi_matcher_assign_features_to_grid(self.matcher._h, C.addressof(cv)))
+        # local-map search reuse this grid (built ahead on the extraction stream when grid_ahead)
+        if self.grid_ahead:
+            check("orbmi_matcher_pin_grid_slot",
+                  L.orbmi_matcher_pin_grid_slot(self.matcher._h, C.addressof(cv), int(self.slot)))
+        else:
+            check("orbmi_matcher_assign_features_to_grid",
+                  L.orbmi_matcher_assign_features_to_grid(self.matcher._h, C.addressof(cv)))
         mp = self.frame_mappoints(last_view, last_points, None, 0)
         for t, gate in ((th, 0x7FFFFFFF), (2 * th, 20)):  # the first search always runs
             check("orbmi_search_by_projection_last_frame_if", L.orbmi_search_by_projection_last_frame_if(

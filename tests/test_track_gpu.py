@@ -175,3 +175,42 @@ def test_track_fused_update_equals_two_launches(f):
         tr.close()
     for k in out[0]:
         np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("f", [4, 7])
+def test_pipelined_grid_ahead_equals_tracking_stream_grid(oracle, f, monkeypatch):
+    """The pipelined tracker builds each frame's keypoint grid (Frame::AssignFeaturesToGrid) on
+    the extraction stream into the frame slot's grid (orbmi_matcher_build_grid_slot, the default)
+    and pins it for the frame's searches; ORBMI_GRID_AHEAD=0 builds it on the tracking stream at
+    the first search.  Frame after frame (the slots alternate, each grid reused behind its slot's
+    next extraction) the matches, outliers, counts and pose records are byte-identical, and the
+    end-to-end results meet the oracle as test_track_chain_end_to_end's."""
+    from orb_slam2_with_comment_amd import synth
+    from orb_slam2_with_comment_amd.pipeline import StereoTracker
+    out = {}
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("ORBMI_GRID_AHEAD", ahead)
+        tr0, d, tcw, lf, lfp, mps, cf = _setup(f)
+        tr0.close()
+        cam = synth.KITTI
+        tr = StereoTracker(cam, 2000, device=0, pipelined=True)
+        assert tr.grid_ahead == (ahead == "1")
+        lv = lf.view()
+        n = len(cf.keys)
+        runs = []
+        for _ in range(3):
+            tr.track(d["imgs"].data_ptr(), cam.height, cam.width, tcw, lv, d["lfp"].data_ptr(), d["mps"].data_ptr(),
+                     len(mps))
+            res = tr.results()
+            runs.append({k: getattr(tr, k)[:n].cpu().numpy().copy() for k in ("match_lf", "match_mp", "outlier")}
+                        | {"tcounts": tr.tcounts.cpu().numpy().copy(), "recs": tr.recs.cpu().numpy().copy(),
+                           "ok": res["ok"]})
+        tr.close()
+        out[ahead] = runs
+    ref = oracle.track_frame(cf, lf, lfp, mps, _inv_sigma2(oracle))
+    for a, b in zip(out["1"], out["0"]):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        assert a["ok"] == ref["ok"]
+        np.testing.assert_array_equal(a["match_mp"], ref["match_mp"])
+        np.testing.assert_array_equal(a["match_lf"], ref["match_lf"])
